@@ -1,0 +1,466 @@
+// Multi-head attention forward, head_dim = 32, for gfx950 (flash-style).
+//
+// One workgroup = 4 waves = 128 query rows of one (batch, head) and one slice
+// of the key range ("kv split").  Each wave owns 32 queries.  Keys are
+// consumed in 64-key tiles staged through a double-buffered LDS image (K and
+// V, 4 KB each); the next tile's global loads are in flight while the current
+// tile is computed.
+//
+// Per 64-key tile and wave (swapped-QK^T form, MI355X guide T12 / 'An
+// accumulator tile as the next MFMA's operand'):
+//   S^T[key][q] = K . Q^T      4 x v_mfma_f32_32x32x16   (K rows by ds_read_b128,
+//                                                         XOR-swizzled LDS image)
+//   online softmax per query   lane = query, 32 of the 64 scores per lane,
+//                              partner lane (l ^ 32) holds the other 32
+//   O^T[d][q] += V^T . P^T     4 x v_mfma_f32_32x32x16   (P^T straight from the
+//                              S^T accumulators, V^T by ds_read_b64_tr_b16)
+// With kv_splits > 1 each split writes unnormalised partial O with its running
+// max / row-sum and a combine kernel merges them (flash-decoding style), so a
+// 900-query problem still fills 256 CUs.
+#include "cmt_common.h"
+
+namespace {
+
+constexpr int KT = 64;     // keys per tile
+constexpr int QW = 32;     // queries per wave
+constexpr int NW = 4;      // waves per workgroup
+constexpr int QB = QW * NW;
+constexpr int D = 32;
+
+struct AttnKParams {
+    int B, H, Nq, Nk;
+    const void* Q; int64_t q_bs, q_hs, q_rs;
+    const void* K; int64_t k_bs, k_hs, k_rs;
+    const void* V; int64_t v_bs, v_hs, v_rs;
+    float* O; int64_t o_bs, o_rs;   // splits == 1: final output
+    float* Op; float* Mp; float* Lp; // splits > 1: partials [split][b][h][q]
+    float c;                        // scale * log2(e)
+    int splits;
+    int tiles_per_split;
+    int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) T Ks[2][KT * D];
+    __shared__ __attribute__((aligned(16))) T Vs[2][KT * D];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    const int bh = blockIdx.y;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+    const int split = blockIdx.z;
+
+    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+
+    const int q0 = blockIdx.x * QB + wave * QW;
+    const int q = q0 + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+
+    // Q^T fragments (B operand): B[k = 8*lh + j][col = q] = Q[q][16*ks + 8*lh + j]
+    frag qf[2];
+    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+
+    const int ntiles = (p.Nk + KT - 1) / KT;
+    const int t_begin = split * p.tiles_per_split;
+    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+
+    // staging: thread -> (key row, 16-byte chunk) of the K and V tiles
+    const int srow = tid >> 2;
+    const int schunk = tid & 3;
+    frag kreg, vreg;
+    auto load_tile = [&](int t) {
+        const int key = t * KT + srow;
+        if (key < p.Nk) {
+            kreg = *(const frag*)(Kb + (int64_t)key * p.k_rs + schunk * 8);
+            vreg = *(const frag*)(Vb + (int64_t)key * p.v_rs + schunk * 8);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { kreg[j] = (T)0.f; vreg[j] = (T)0.f; }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        *(frag*)(&Ks[buf][srow * D + 8 * (schunk ^ ((srow >> 2) & 3))]) = kreg;
+        *(frag*)(&Vs[buf][srow * D + 8 * schunk]) = vreg;
+    };
+
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    float m_run = -__builtin_inff();
+    float l_run = 0.f;
+    const float c = p.c;
+
+    if (t_begin < t_end) {
+        load_tile(t_begin);
+        store_tile(0);
+    }
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+        const int cur = (t - t_begin) & 1;
+        if (t + 1 < t_end) load_tile(t + 1);
+
+        // ---- S^T = K Q^T for the two 32-key blocks --------------------------
+        f32x16 s[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+            const int row = kb * 32 + lr;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                frag kf = *(const frag*)(&Ks[cur][row * D + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
+                s[kb] = mfma_traits<T>::mma(kf, qf[ks], s[kb]);
+            }
+        }
+        // ---- mask the ragged tail -------------------------------------------
+        if ((t + 1) * KT > p.Nk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    int key = t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (key >= p.Nk) s[kb][r] = -__builtin_inff();
+                }
+        }
+        // ---- online softmax ---------------------------------------------------
+        float mt = s[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mt = fmaxf(mt, s[0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[1][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = exp2f((m_run - m_new) * c);
+        const float mc = m_new * c;
+        float ls = 0.f;
+        frag pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float e = exp2f(fmaf(s[kb][r], c, -mc));
+                ls += e;
+                pf[kb][r >> 3][r & 7] = (T)e;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+
+        // ---- O^T += V^T P^T ----------------------------------------------------
+        const int dgrp = 16 * ((lane >> 4) & 1);
+        const int tq = (lane & 15) >> 2;
+        const int tp = lane & 3;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                const int r0 = kb * 32 + 16 * ss + 4 * lh + tq;
+                const T* base0 = &Vs[cur][r0 * D + dgrp + 4 * tp];
+                const T* base1 = base0 + 8 * D;
+                s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base0);
+                s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base1);
+                s16x8 vv;
+                vv[0] = lo[0]; vv[1] = lo[1]; vv[2] = lo[2]; vv[3] = lo[3];
+                vv[4] = hi[0]; vv[5] = hi[1]; vv[6] = hi[2]; vv[7] = hi[3];
+                frag vf = __builtin_bit_cast(frag, vv);
+                o = mfma_traits<T>::mma(vf, pf[kb][ss], o);
+            }
+
+        if (t + 1 < t_end) store_tile(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- write ---------------------------------------------------------------
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    if (q >= p.Nq) return;
+    if (p.splits == 1) {
+        const float inv = 1.f / l_tot;
+        float* dst = p.O + (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+            if (p.round_out) {   // flash-attn returns the input dtype (attention.py:46 out_fp32 cast after)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+            }
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+    } else {
+        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
+        float* dst = p.Op + row * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+        if (lh == 0) {
+            p.Mp[row] = m_run;
+            p.Lp[row] = l_tot;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Exact-f32 variant (v_mfma_f32_32x32x2_f32): same tiling and online softmax;
+// used where the reference computes attention in fp32 (nn.MultiheadAttention
+// self-attention).  K image rows padded to 36 floats (conflict-free
+// ds_read_b128); QK^T k index permuted as d = 16*(lane>>5) + t; P stays f32 in
+// the S^T accumulators and feeds the PV MFMAs directly, V^T elements by
+// ds_read_b32 (one row of 32 floats per half-wave: conflict-free).
+// ---------------------------------------------------------------------------
+constexpr int KP = 36;
+
+__global__ __launch_bounds__(256) void attn_fwd_f32_kernel(AttnKParams p) {
+    __shared__ __attribute__((aligned(16))) float Ks[2][KT * KP];
+    __shared__ __attribute__((aligned(16))) float Vs[2][KT * D];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    const int bh = blockIdx.y;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+    const int split = blockIdx.z;
+
+    const float* Qb = (const float*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const float* Kb = (const float*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const float* Vb = (const float*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+
+    const int q = blockIdx.x * QB + wave * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    f32x4 qf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qf[i] = *(const f32x4*)(Qb + (int64_t)qc * p.q_rs + 16 * lh + 4 * i);
+
+    const int ntiles = (p.Nk + KT - 1) / KT;
+    const int t_begin = split * p.tiles_per_split;
+    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+
+    f32x4 kreg[2], vreg[2];
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + 256 * i;
+            const int row = idx >> 3, c4 = idx & 7;
+            const int key = t * KT + row;
+            if (key < p.Nk) {
+                kreg[i] = *(const f32x4*)(Kb + (int64_t)key * p.k_rs + 4 * c4);
+                vreg[i] = *(const f32x4*)(Vb + (int64_t)key * p.v_rs + 4 * c4);
+            } else {
+                kreg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                vreg[i] = kreg[i];
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + 256 * i;
+            const int row = idx >> 3, c4 = idx & 7;
+            *(f32x4*)(&Ks[buf][row * KP + 4 * c4]) = kreg[i];
+            *(f32x4*)(&Vs[buf][row * D + 4 * c4]) = vreg[i];
+        }
+    };
+
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    float m_run = -__builtin_inff();
+    float l_run = 0.f;
+    const float c = p.c;
+
+    if (t_begin < t_end) {
+        load_tile(t_begin);
+        store_tile(0);
+    }
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+        const int cur = (t - t_begin) & 1;
+        if (t + 1 < t_end) load_tile(t + 1);
+        f32x16 s[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+            const float* krow = &Ks[cur][(kb * 32 + lr) * KP + 16 * lh];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f32x4 kv = *(const f32x4*)(krow + 4 * i);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[j], qf[i][j], s[kb], 0, 0, 0);
+            }
+        }
+        if ((t + 1) * KT > p.Nk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    int key = t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (key >= p.Nk) s[kb][r] = -__builtin_inff();
+                }
+        }
+        float mt = s[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mt = fmaxf(mt, s[0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[1][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = exp2f((m_run - m_new) * c);
+        const float mc = m_new * c;
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = exp2f(fmaf(s[kb][r], c, -mc));
+                ls += e;
+                s[kb][r] = e;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const float v = Vs[cur][key * D + lr];
+                o = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s[kb][r], o, 0, 0, 0);
+            }
+        if (t + 1 < t_end) store_tile(cur ^ 1);
+        __syncthreads();
+    }
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    if (q >= p.Nq) return;
+    if (p.splits == 1) {
+        const float inv = 1.f / l_tot;
+        float* dst = p.O + (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+    } else {
+        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
+        float* dst = p.Op + row * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+        if (lh == 0) {
+            p.Mp[row] = m_run;
+            p.Lp[row] = l_tot;
+        }
+    }
+}
+
+// One thread per (b, h, q, d): merge the kv-split partials.
+__global__ void attn_combine_kernel(AttnKParams p) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.B * p.H * p.Nq * D;
+    if (idx >= total) return;
+    const int d = idx & (D - 1);
+    const int64_t bhq = idx >> 5;
+    const int q = bhq % p.Nq;
+    const int64_t bh = bhq / p.Nq;
+    const int h = bh % p.H;
+    const int b = bh / p.H;
+    const int64_t stride = (int64_t)p.B * p.H * p.Nq;
+    float M = -__builtin_inff();
+    for (int s = 0; s < p.splits; ++s) M = fmaxf(M, p.Mp[s * stride + bhq]);
+    float num = 0.f, den = 0.f;
+    for (int s = 0; s < p.splits; ++s) {
+        const float ms = p.Mp[s * stride + bhq];
+        if (ms == -__builtin_inff()) continue;
+        const float w = exp2f((ms - M) * p.c);
+        num += w * p.Op[(s * stride + bhq) * D + d];
+        den += w * p.Lp[s * stride + bhq];
+    }
+    float r = num / den;
+    if (p.round_out == CMT_F16) r = (float)(f16_t)r;
+    else if (p.round_out == CMT_BF16) r = (float)(bf16_t)r;
+    p.O[(int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D + d] = r;
+}
+
+int choose_splits(const cmt_attn_args& a) {
+    if (a.kv_splits > 0) return a.kv_splits;
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int base = cdiv(a.Nq, QB) * a.B * a.H;
+    int s = 1;
+    // aim for >= 1024 workgroups (4 per CU) while keeping >= 8 tiles per split
+    while (base * s < 1024 && ntiles / (2 * s) >= 8) s *= 2;
+    return s;
+}
+
+}  // namespace
+
+extern "C" int64_t cmt_attn_workspace_bytes(const cmt_attn_args* a) {
+    if (!a) return 0;
+    const int s = choose_splits(*a);
+    if (s <= 1) return 0;
+    const int64_t rows = (int64_t)s * a->B * a->H * a->Nq;
+    return rows * (D + 2) * (int64_t)sizeof(float);
+}
+
+extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_attn_fwd: null args");
+    const cmt_attn_args& a = *ap;
+    CMT_REQUIRE(a.B > 0 && a.H > 0 && a.Nq > 0 && a.Nk > 0, "cmt_attn_fwd: empty problem");
+    CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16 || a.dtype == CMT_F32,
+                "cmt_attn_fwd: dtype must be f32, f16 or bf16");
+    CMT_REQUIRE(a.Q && a.K && a.V && a.O, "cmt_attn_fwd: null pointer");
+    CMT_REQUIRE(a.dtype != CMT_F32 || ((a.q_rstride | a.k_rstride | a.v_rstride) % 4 == 0),
+                "cmt_attn_fwd: f32 rows must be 16-byte aligned");
+    CMT_REQUIRE(a.o_rstride % 4 == 0 && a.o_bstride % 4 == 0, "cmt_attn_fwd: O strides must be multiples of 4");
+    CMT_REQUIRE(a.q_rstride % 8 == 0 && a.k_rstride % 8 == 0 && a.v_rstride % 8 == 0 && a.q_hstride % 8 == 0 &&
+                a.k_hstride % 8 == 0 && a.v_hstride % 8 == 0 && a.q_bstride % 8 == 0 && a.k_bstride % 8 == 0 &&
+                a.v_bstride % 8 == 0, "cmt_attn_fwd: Q/K/V strides must be multiples of 8 elements");
+    const int splits = choose_splits(a);
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    AttnKParams p;
+    p.B = a.B; p.H = a.H; p.Nq = a.Nq; p.Nk = a.Nk;
+    p.Q = a.Q; p.q_bs = a.q_bstride; p.q_hs = a.q_hstride; p.q_rs = a.q_rstride;
+    p.K = a.K; p.k_bs = a.k_bstride; p.k_hs = a.k_hstride; p.k_rs = a.k_rstride;
+    p.V = a.V; p.v_bs = a.v_bstride; p.v_hs = a.v_hstride; p.v_rs = a.v_rstride;
+    p.O = a.O; p.o_bs = a.o_bstride; p.o_rs = a.o_rstride;
+    p.c = a.scale * 1.4426950408889634f;
+    p.splits = splits;
+    p.tiles_per_split = cdiv(ntiles, splits);
+    p.round_out = (a.flags & CMT_ATTN_ROUND_OUTPUT) && a.dtype != CMT_F32 ? a.dtype : 0;
+    p.Op = p.Mp = p.Lp = nullptr;
+    if (splits > 1) {
+        const int64_t need = cmt_attn_workspace_bytes(&a);
+        if (a.workspace == nullptr || a.workspace_bytes < need)
+            return cmt_fail(CMT_EWORKSPACE, "cmt_attn_fwd: workspace too small");
+        const int64_t rows = (int64_t)splits * a.B * a.H * a.Nq;
+        p.Op = (float*)a.workspace;
+        p.Mp = p.Op + rows * D;
+        p.Lp = p.Mp + rows;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid(cdiv(a.Nq, QB), a.B * a.H, splits);
+    if (a.dtype == CMT_F16) attn_fwd_kernel<f16_t><<<grid, 256, 0, s>>>(p);
+    else if (a.dtype == CMT_BF16) attn_fwd_kernel<bf16_t><<<grid, 256, 0, s>>>(p);
+    else attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
+    int rc = cmt_check_launch("cmt_attn_fwd");
+    if (rc || splits == 1) return rc;
+    const int64_t total = (int64_t)a.B * a.H * a.Nq * D;
+    attn_combine_kernel<<<(unsigned)cdiv64(total, 256), 256, 0, s>>>(p);
+    return cmt_check_launch("cmt_attn_combine");
+}

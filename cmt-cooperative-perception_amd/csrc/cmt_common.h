@@ -1,0 +1,64 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of libcmt_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/cmt_hip.h"
+
+typedef __bf16 bf16_t;
+typedef _Float16 f16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short __attribute__((__vector_size__(4 * sizeof(short)))) s16v4_lds;
+
+#define CMT_LDS __attribute__((address_space(3)))
+
+// ---- error plumbing (host) -------------------------------------------------
+void cmt_set_error(const std::string& msg);
+int cmt_fail(int code, const std::string& msg);
+int cmt_check_launch(const char* what);
+
+#define CMT_REQUIRE(cond, msg)                                   \
+    do {                                                         \
+        if (!(cond)) return cmt_fail(CMT_EINVAL, std::string(msg)); \
+    } while (0)
+
+// ---- element conversion ----------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float to_f32(T x) { return (float)x; }
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float x) { return (T)x; }
+
+// MFMA wrappers: 32x32x16 (f16 / bf16 inputs, 8 elements per lane).
+template <typename T> struct mfma_traits;
+template <> struct mfma_traits<bf16_t> {
+    typedef bf16x8 frag;
+    static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct mfma_traits<f16_t> {
+    typedef f16x8 frag;
+    static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Non-finite sanitiser with torch.nan_to_num defaults.
+__device__ __forceinline__ float nan_to_num(float x) {
+    if (x != x) return 0.f;
+    if (x == __builtin_inff()) return 3.4028234663852886e38f;
+    if (x == -__builtin_inff()) return -3.4028234663852886e38f;
+    return x;
+}
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }

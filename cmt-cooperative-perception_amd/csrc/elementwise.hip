@@ -1,0 +1,457 @@
+// Wavefront-reduction / elementwise kernels of the decoder head (gfx950):
+// LayerNorm (+post-norm, nan_to_num, coop max), positional encodings,
+// camera-frustum geometry, layout transposes, task-head tail.
+// All are HBM- or latency-bound; one wave64 per row where a row reduction is
+// needed, 16-byte vector accesses where the layout allows.
+#include "cmt_common.h"
+
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm: one wave per row, VPT = C / 64 values per lane (lane-strided so
+// the loads are 256-byte coalesced per instruction).
+// ---------------------------------------------------------------------------
+template <int VPT>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ X, int64_t ldx, int rows,
+                                                        const float* __restrict__ W, const float* __restrict__ B,
+                                                        float eps, float* Y, int64_t ldy, int flags,
+                                                        const float* __restrict__ W2, const float* __restrict__ B2,
+                                                        float* Y2, int64_t ldy2, int flags2) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    constexpr int C = VPT * 64;
+    float v[VPT];
+    const float* x = X + (int64_t)row * ldx;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) v[i] = x[lane + 64 * i];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) s += v[i];
+    const float mean = wave_sum(s) / (float)C;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) { float d = v[i] - mean; ss += d * d; }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)C + eps);
+    float* y = Y + (int64_t)row * ldy;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = lane + 64 * i;
+        float o = (v[i] - mean) * rstd * W[c] + B[c];
+        v[i] = o;   // the second LN consumes the first LN's output
+        if (flags & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
+        if (flags & CMT_LN_MAX_INTO) o = fmaxf(o, y[c]);
+        y[c] = o;
+    }
+    if (Y2 == nullptr) return;
+    s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) s += v[i];
+    const float mean2 = wave_sum(s) / (float)C;
+    ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) { float d = v[i] - mean2; ss += d * d; }
+    const float rstd2 = rsqrtf(wave_sum(ss) / (float)C + eps);
+    float* y2 = Y2 + (int64_t)row * ldy2;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = lane + 64 * i;
+        float o = (v[i] - mean2) * rstd2 * W2[c] + B2[c];
+        if (flags2 & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
+        if (flags2 & CMT_LN_MAX_INTO) o = fmaxf(o, y2[c]);
+        y2[c] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// pos2embed (cmt_head.py:40-50), optionally fused with coords_bev (324-337) or
+// with sigmoid(inverse_sigmoid(.)) of the query reference points (470).
+// One thread per output element.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float inv_sigmoid_dev(float x) {
+    x = fminf(fmaxf(x, 0.f), 1.f);
+    const float x1 = fmaxf(x, 1e-5f);
+    const float x2 = fmaxf(1.f - x, 1e-5f);
+    return logf(x1 / x2);
+}
+__device__ __forceinline__ float sigmoid_dev(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ void pos2embed_kernel(const float* __restrict__ pos, int64_t pos_stride, int n, int F, int mode,
+                                 int x_size, int y_size, float* out, int64_t ldo) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)n * 2 * F;
+    if (idx >= total) return;
+    const int i = (int)(idx / (2 * F));
+    const int f = (int)(idx - (int64_t)i * 2 * F);
+    float px, py;
+    if (pos == nullptr) {
+        // coords_bev: token t = r * y_size + c  ->  x = (c+0.5)/x_size, y = (r+0.5)/y_size
+        const int r = i / y_size;
+        const int c = i - r * y_size;
+        px = ((float)c + 0.5f) / (float)x_size;
+        py = ((float)r + 0.5f) / (float)y_size;
+    } else {
+        px = pos[(int64_t)i * pos_stride];
+        py = pos[(int64_t)i * pos_stride + 1];
+        if (mode == 1) {
+            px = sigmoid_dev(inv_sigmoid_dev(px));
+            py = sigmoid_dev(inv_sigmoid_dev(py));
+        }
+    }
+    const float scale = 6.283185307179586f;
+    const int j = f < F ? f : f - F;          // first F outputs embed y, the next F embed x
+    const float p = (f < F ? py : px) * scale;
+    const float dim_t = 2.f * (float)(j >> 1) / (float)F + 1.f;
+    const float v = p / dim_t;
+    out[(int64_t)i * ldo + f] = (j & 1) ? cosf(v) : sinf(v);
+}
+
+// ---------------------------------------------------------------------------
+// _rv_pe geometry (cmt_head.py:417-432): one thread per (bv, h, w, depth).
+// ---------------------------------------------------------------------------
+struct PcRange { float v[6]; };
+
+__global__ void rv_pe_coords_kernel(int BV, int H, int W, int D, float pad_h, float pad_w, float dstep,
+                                    const float* __restrict__ i2l, PcRange pc, float* out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)BV * H * W * D;
+    if (idx >= total) return;
+    const int k = (int)(idx % D);
+    const int64_t tok = idx / D;
+    const int w = (int)(tok % W);
+    const int h = (int)((tok / W) % H);
+    const int bv = (int)(tok / ((int64_t)W * H));
+    const float u = (float)w * pad_w / (float)W;
+    const float v = (float)h * pad_h / (float)H;
+    const float d = 1.f + (float)k * dstep / (float)D;
+    const float c[4] = {u * d, v * d, d, 1.f};
+    const float* M = i2l + (int64_t)bv * 16;
+    float* o = out + tok * (3 * D) + 3 * k;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        float a = M[r * 4 + 0] * c[0];
+        a = fmaf(M[r * 4 + 1], c[1], a);
+        a = fmaf(M[r * 4 + 2], c[2], a);
+        a = fmaf(M[r * 4 + 3], c[3], a);
+        o[r] = (a - pc.v[r]) / (pc.v[3 + r] - pc.v[r]);
+    }
+}
+
+// _rv_query_embed geometry (cmt_head.py:446-463): one thread per (b, v, q, depth).
+__global__ void rv_query_coords_kernel(const float* __restrict__ ref, int B, int V, int Nq, int D,
+                                       float pad_h, float pad_w, float dstep,
+                                       const float* __restrict__ l2i, const float* __restrict__ i2l,
+                                       PcRange pc, float* out, float* mask) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)B * V * Nq * D;
+    if (idx >= total) return;
+    const int k = (int)(idx % D);
+    const int64_t bvq = idx / D;
+    const int q = (int)(bvq % Nq);
+    const int64_t bv = bvq / Nq;
+    const int b = (int)(bv / V);
+    float r[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float x = sigmoid_dev(inv_sigmoid_dev(ref[((int64_t)b * Nq + q) * 3 + c]));
+        r[c] = x * (pc.v[3 + c] - pc.v[c]) + pc.v[c];
+    }
+    const float* L = l2i + bv * 16;
+    float pr[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float a = L[c * 4 + 0] * r[0];
+        a = fmaf(L[c * 4 + 1], r[1], a);
+        a = fmaf(L[c * 4 + 2], r[2], a);
+        pr[c] = a + L[c * 4 + 3];
+    }
+    const bool zpos = pr[2] > 0.f;
+    const float den = pr[2] + (zpos ? 1e-6f : -1e-6f);
+    const float px = pr[0] / den, py = pr[1] / den, pz = pr[2] / den;
+    if (k == 0) {
+        const bool m = (px < pad_w) && (px >= 0.f) && (py < pad_h) && (py >= 0.f) && zpos;
+        mask[bvq] = m ? 1.f : 0.f;
+    }
+    const float d = 1.f + (float)k * dstep / (float)D;
+    const float c4[4] = {px * d, py * d, pz * d, 1.f};
+    const float* M = i2l + bv * 16;
+    float* o = out + bvq * (3 * D) + 3 * k;
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+        float a = M[rr * 4 + 0] * c4[0];
+        a = fmaf(M[rr * 4 + 1], c4[1], a);
+        a = fmaf(M[rr * 4 + 2], c4[2], a);
+        a = fmaf(M[rr * 4 + 3], c4[3], a);
+        o[rr] = (a - pc.v[rr]) / (pc.v[3 + rr] - pc.v[rr]);
+    }
+}
+
+__global__ void masked_view_sum_kernel(const float* __restrict__ X, const float* __restrict__ mask, int B, int V,
+                                       int Nq, int C, float* Y) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)B * Nq * C;
+    if (idx >= total) return;
+    const int c = (int)(idx % C);
+    const int64_t bq = idx / C;
+    const int q = (int)(bq % Nq);
+    const int b = (int)(bq / Nq);
+    float s = 0.f;
+    for (int v = 0; v < V; ++v) {
+        const int64_t bvq = ((int64_t)b * V + v) * Nq + q;
+        s += X[bvq * C + c] * mask[bvq];
+    }
+    Y[idx] += s;
+}
+
+// ---------------------------------------------------------------------------
+// NCHW -> token rows (64x64 tile transpose through LDS).
+// ---------------------------------------------------------------------------
+template <typename TO>
+__global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restrict__ X, int nv, int C, int HW,
+                                                           TO* Y, int64_t ldy, int64_t rows_per_batch,
+                                                           int64_t row_offset) {
+    __shared__ float tile[64][65];
+    const int img = blockIdx.z;
+    const int c0 = blockIdx.y * 64;
+    const int p0 = blockIdx.x * 64;
+    const float* xs = X + (int64_t)img * C * HW;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const int c = c0 + i, p = p0 + tx;
+        tile[i][tx] = (c < C && p < HW) ? xs[(int64_t)c * HW + p] : 0.f;
+    }
+    __syncthreads();
+    const int bo = img / nv, v = img - bo * nv;
+    for (int i = ty; i < 64; i += 4) {
+        const int p = p0 + i, c = c0 + tx;
+        if (p < HW && c < C) {
+            const int64_t row = (int64_t)bo * rows_per_batch + row_offset + (int64_t)v * HW + p;
+            Y[row * ldy + c] = (TO)tile[tx][i];
+        }
+    }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ X, TO* Y, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) Y[i] = (TO)(float)X[i];
+}
+
+// ---------------------------------------------------------------------------
+// Task-head tail (cmt_head.py:136-203, 501-513).
+// (1) GroupLayerNorm1d (per head, hc channels, biased var, eps 1e-6) + ReLU,
+//     in place on H1 [L][B*Nq][nheads*hc]; one wave per (l, row), hc == 64.
+// (2) grouped Conv1d #2 (+bias) with kernel k along the query axis and the
+//     center/height box epilogue; one thread per output element.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void group_ln_relu_kernel(float* H1, int rows, int nheads,
+                                                            const float* __restrict__ gw,
+                                                            const float* __restrict__ gb) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const int li = blockIdx.y;  // decoder layer = conv group
+    const int width = nheads * 64;
+    float* x = H1 + ((int64_t)li * rows + row) * width;
+    const float* w = gw + (int64_t)li * width;
+    const float* b = gb + (int64_t)li * width;
+    for (int hd = 0; hd < nheads; ++hd) {
+        const int c = hd * 64 + lane;
+        const float v = x[c];
+        const float mu = wave_sum(v) / 64.f;
+        const float d = v - mu;
+        const float var = wave_sum(d * d) / 64.f;
+        float y = d / sqrtf(var + 1e-6f);
+        y = w[c] * y + b[c];
+        x[c] = fmaxf(y, 0.f);
+    }
+}
+
+struct TailParams {
+    const float* G; int L, B, Nq, nheads, hc;
+    const float* W2; const float* B2;
+    int head_start[16]; int head_of[64];
+    int out_total, k;
+    const float* ref; int center_col, height_col;
+    float pc[6];
+    float* OUT;
+};
+
+__global__ void task_head_conv2_kernel(TailParams p) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.L * p.B * p.Nq * p.out_total;
+    if (idx >= total) return;
+    const int o = (int)(idx % p.out_total);
+    const int64_t lbq = idx / p.out_total;
+    const int q = (int)(lbq % p.Nq);
+    const int64_t lb = lbq / p.Nq;
+    const int b = (int)(lb % p.B);
+    const int l = (int)(lb / p.B);
+    const int hd = p.head_of[o];
+    const int width = p.nheads * p.hc;
+    const float* w = p.W2 + (((int64_t)l * p.out_total + o) * p.k) * p.hc;
+    float acc = p.B2[(int64_t)l * p.out_total + o];
+    const int half = p.k >> 1;
+    for (int t = 0; t < p.k; ++t) {
+        const int qq = q + t - half;
+        if (qq < 0 || qq >= p.Nq) continue;
+        const float* g = p.G + (((int64_t)l * p.B + b) * p.Nq + qq) * width + hd * p.hc;
+        const float* wt = w + t * p.hc;
+        float s = 0.f;
+        for (int c = 0; c < p.hc; ++c) s = fmaf(wt[c], g[c], s);
+        acc += s;
+    }
+    const int rel_c = o - p.center_col;
+    const int rel_h = o - p.height_col;
+    if (p.center_col >= 0 && rel_c >= 0 && rel_c < 2) {
+        const float rf = inv_sigmoid_dev(p.ref[((int64_t)b * p.Nq + q) * 3 + rel_c]);
+        acc = sigmoid_dev(acc + rf) * (p.pc[3 + rel_c] - p.pc[rel_c]) + p.pc[rel_c];
+    } else if (p.height_col >= 0 && rel_h == 0) {
+        const float rf = inv_sigmoid_dev(p.ref[((int64_t)b * p.Nq + q) * 3 + 2]);
+        acc = sigmoid_dev(acc + rf) * (p.pc[5] - p.pc[2]) + p.pc[2];
+    }
+    p.OUT[idx] = acc;
+}
+
+inline unsigned nblocks(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const float* W, const float* Bv,
+                             float eps, float* Y, int64_t ldy, int flags, const float* W2, const float* B2,
+                             float* Y2, int64_t ldy2, int flags2, void* stream) {
+    CMT_REQUIRE(X && W && Bv && Y && rows >= 0, "cmt_layernorm: null pointer");
+    CMT_REQUIRE(C % 64 == 0 && C >= 64 && C <= 1024, "cmt_layernorm: C must be a multiple of 64 in [64, 1024]");
+    CMT_REQUIRE(Y2 == nullptr || (W2 && B2), "cmt_layernorm: second LN needs W2/B2");
+    if (rows == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid(cdiv(rows, 4));
+#define LN_CASE(V)                                                                                   \
+    case V:                                                                                          \
+        layernorm_kernel<V><<<grid, 256, 0, s>>>(X, ldx, rows, W, Bv, eps, Y, ldy, flags, W2, B2, Y2, \
+                                                 ldy2, flags2);                                       \
+        break;
+    switch (C / 64) {
+        LN_CASE(1) LN_CASE(2) LN_CASE(3) LN_CASE(4) LN_CASE(5) LN_CASE(6) LN_CASE(7) LN_CASE(8)
+        LN_CASE(9) LN_CASE(10) LN_CASE(11) LN_CASE(12) LN_CASE(13) LN_CASE(14) LN_CASE(15) LN_CASE(16)
+    }
+#undef LN_CASE
+    return cmt_check_launch("cmt_layernorm");
+}
+
+extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F, int mode, int grid_h,
+                             int grid_w, float* out, int64_t ldo, void* stream) {
+    CMT_REQUIRE(out && n >= 0 && F > 0 && F % 2 == 0, "cmt_pos2embed: bad arguments");
+    CMT_REQUIRE(pos != nullptr || (grid_h > 0 && grid_w > 0 && n == grid_h * grid_w),
+                "cmt_pos2embed: grid mode needs n == grid_h*grid_w");
+    if (n == 0) return 0;
+    const int64_t total = (int64_t)n * 2 * F;
+    pos2embed_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(pos, pos_stride, n, F, mode, grid_h,
+                                                                            grid_w, out, ldo);
+    return cmt_check_launch("cmt_pos2embed");
+}
+
+extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float pad_w, float depth_max,
+                                const float* i2l, const float* pc_range6, float* out, void* stream) {
+    CMT_REQUIRE(i2l && pc_range6 && out && BV > 0 && h > 0 && w > 0 && D > 0, "cmt_rv_pe_coords: bad arguments");
+    PcRange pc;
+    for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
+    const int64_t total = (int64_t)BV * h * w * D;
+    rv_pe_coords_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(BV, h, w, D, pad_h, pad_w,
+                                                                               depth_max - 1.f, i2l, pc, out);
+    return cmt_check_launch("cmt_rv_pe_coords");
+}
+
+extern "C" int cmt_rv_query_coords(const float* ref, int B, int V, int Nq, int D, float pad_h, float pad_w,
+                                   const float* l2i, const float* i2l, const float* pc_range6, float* out,
+                                   float* mask, void* stream) {
+    CMT_REQUIRE(ref && l2i && i2l && pc_range6 && out && mask && B > 0 && V > 0 && Nq > 0 && D > 0,
+                "cmt_rv_query_coords: bad arguments");
+    PcRange pc;
+    for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
+    const int64_t total = (int64_t)B * V * Nq * D;
+    rv_query_coords_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(
+        ref, B, V, Nq, D, pad_h, pad_w, pc.v[3] - 1.f, l2i, i2l, pc, out, mask);
+    return cmt_check_launch("cmt_rv_query_coords");
+}
+
+extern "C" int cmt_masked_view_sum(const float* X, const float* mask, int B, int V, int Nq, int C, float* Y,
+                                   void* stream) {
+    CMT_REQUIRE(X && mask && Y && B > 0 && V > 0 && Nq > 0 && C > 0, "cmt_masked_view_sum: bad arguments");
+    const int64_t total = (int64_t)B * Nq * C;
+    masked_view_sum_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(X, mask, B, V, Nq, C, Y);
+    return cmt_check_launch("cmt_masked_view_sum");
+}
+
+extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype, int64_t ldy,
+                                int64_t rows_per_batch, int64_t row_offset, void* stream) {
+    CMT_REQUIRE(X && Y && nb > 0 && nv > 0 && C > 0 && HW > 0, "cmt_nchw_to_rows: bad arguments");
+    dim3 grid(cdiv(HW, 64), cdiv(C, 64), nb * nv);
+    hipStream_t s = (hipStream_t)stream;
+    if (ydtype == CMT_F32)
+        nchw_to_rows_kernel<float><<<grid, 256, 0, s>>>(X, nv, C, HW, (float*)Y, ldy, rows_per_batch, row_offset);
+    else if (ydtype == CMT_F16)
+        nchw_to_rows_kernel<f16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (f16_t*)Y, ldy, rows_per_batch, row_offset);
+    else if (ydtype == CMT_BF16)
+        nchw_to_rows_kernel<bf16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch, row_offset);
+    else
+        return cmt_fail(CMT_EINVAL, "cmt_nchw_to_rows: bad ydtype");
+    return cmt_check_launch("cmt_nchw_to_rows");
+}
+
+extern "C" int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* stream) {
+    CMT_REQUIRE(X && Y && n >= 0, "cmt_cast: bad arguments");
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned g = nblocks(n, 256);
+#define CAST(TI, TO) cast_kernel<TI, TO><<<g, 256, 0, s>>>((const TI*)X, (TO*)Y, n)
+    if (xdtype == CMT_F32 && ydtype == CMT_BF16) CAST(float, bf16_t);
+    else if (xdtype == CMT_F32 && ydtype == CMT_F16) CAST(float, f16_t);
+    else if (xdtype == CMT_F32 && ydtype == CMT_F32) CAST(float, float);
+    else if (xdtype == CMT_BF16 && ydtype == CMT_F32) CAST(bf16_t, float);
+    else if (xdtype == CMT_F16 && ydtype == CMT_F32) CAST(f16_t, float);
+    else return cmt_fail(CMT_EINVAL, "cmt_cast: unsupported dtype pair");
+#undef CAST
+    return cmt_check_launch("cmt_cast");
+}
+
+extern "C" int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nheads, int hc, const float* gln_w,
+                                  const float* gln_b, const float* W2, const float* B2, const int* head_out,
+                                  int out_total, int k, const float* ref, int center_col, int height_col,
+                                  const float* pc_range6, float* OUT, void* stream) {
+    CMT_REQUIRE(H1 && gln_w && gln_b && W2 && B2 && head_out && ref && pc_range6 && OUT,
+                "cmt_task_head_tail: null pointer");
+    CMT_REQUIRE(hc == 64, "cmt_task_head_tail: head_conv must be 64");
+    CMT_REQUIRE(nheads > 0 && nheads <= 16 && out_total > 0 && out_total <= 64 && (k == 1 || k == 3),
+                "cmt_task_head_tail: unsupported head geometry");
+    hipStream_t s = (hipStream_t)stream;
+    const int rows = B * Nq;
+    dim3 g1(cdiv(rows, 4), L);
+    group_ln_relu_kernel<<<g1, 256, 0, s>>>(const_cast<float*>(H1), rows, nheads, gln_w, gln_b);
+    int rc = cmt_check_launch("cmt_task_head_tail/gln");
+    if (rc) return rc;
+    TailParams p;
+    p.G = H1; p.L = L; p.B = B; p.Nq = Nq; p.nheads = nheads; p.hc = hc;
+    p.W2 = W2; p.B2 = B2; p.out_total = out_total; p.k = k;
+    p.ref = ref; p.center_col = center_col; p.height_col = height_col;
+    for (int i = 0; i < 6; ++i) p.pc[i] = pc_range6[i];
+    p.OUT = OUT;
+    int o = 0;
+    for (int hd = 0; hd < nheads; ++hd) {
+        p.head_start[hd] = o;
+        for (int j = 0; j < head_out[hd]; ++j) {
+            if (o >= 64) return cmt_fail(CMT_EINVAL, "cmt_task_head_tail: too many outputs");
+            p.head_of[o++] = hd;
+        }
+    }
+    CMT_REQUIRE(o == out_total, "cmt_task_head_tail: head_out does not sum to out_total");
+    const int64_t total = (int64_t)L * B * Nq * out_total;
+    task_head_conv2_kernel<<<nblocks(total, 256), 256, 0, s>>>(p);
+    return cmt_check_launch("cmt_task_head_tail/conv2");
+}

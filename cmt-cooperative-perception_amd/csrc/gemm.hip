@@ -1,0 +1,398 @@
+// MFMA GEMM with fused prologue (pos-add, implicit conv gathers) and epilogue
+// (bias, ReLU, residual, dtype cast, head-split scatter) for gfx950.
+//
+// C[m,n] = act(sum_k Aeff[m,k] * W[n,k] + bias[n]) + R[m,n]
+//
+// Block = 256 threads = 4 waves in a 2x2 grid; each wave owns a
+// (BM/2)x(BN/2) sub-tile built from 32x32 MFMA tiles.  K is consumed in
+// 32-deep steps staged through a double-buffered LDS image; the next step's
+// global loads are issued before the current step's MFMAs (register staging,
+// write-after-compute, one barrier per step).
+//
+// Low-precision path (f16/bf16): v_mfma_f32_32x32x16_{f16,bf16}; LDS image
+// [row][32] with 16-byte chunks XOR-swizzled by (row>>2)&3 so the 16-lane
+// groups of ds_read_b128 hit 16 distinct bank slots.
+// Exact-f32 path: v_mfma_f32_32x32x2_f32 with the k index permuted as
+// k = 16*(lane>>5) + t so each lane reads 16 contiguous floats; LDS rows are
+// padded to 36 floats (conflict-free ds_read_b128).
+#include "cmt_common.h"
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int NT = 256;
+
+struct RowInfo {         // per staged row: where the A row comes from
+    int valid;           // row < M
+    int img, y, x;       // CONV3X3
+    int q;               // CONV1D3 position inside its segment
+};
+
+template <int AMODE>
+__device__ __forceinline__ RowInfo make_row_info(const cmt_gemm_args& a, int row) {
+    RowInfo ri;
+    ri.valid = row < a.M;
+    ri.img = ri.y = ri.x = ri.q = 0;
+    if (AMODE == CMT_A_CONV3X3) {
+        int hw = a.conv_h * a.conv_w;
+        ri.img = row / hw;
+        int p = row - ri.img * hw;
+        ri.y = p / a.conv_w;
+        ri.x = p - ri.y * a.conv_w;
+    } else if (AMODE == CMT_A_CONV1D3) {
+        ri.q = row % a.seg_len;
+    }
+    return ri;
+}
+
+// Returns the element offset of A[row][k0 .. k0+len) or -1 if the gathered row is padding.
+template <int AMODE>
+__device__ __forceinline__ int64_t a_offset(const cmt_gemm_args& a, const RowInfo& ri, int row, int k0) {
+    if (!ri.valid) return -1;
+    if (AMODE == CMT_A_ROWS) {
+        return (int64_t)row * a.lda + k0;
+    } else if (AMODE == CMT_A_CONV3X3) {
+        int C = a.conv_c;
+        int tap = k0 / C;
+        int cin = k0 - tap * C;
+        int yy = ri.y + tap / 3 - 1;
+        int xx = ri.x + tap % 3 - 1;
+        if (yy < 0 || yy >= a.conv_h || xx < 0 || xx >= a.conv_w) return -1;
+        return (((int64_t)ri.img * a.conv_h + yy) * a.conv_w + xx) * a.lda + cin;
+    } else {  // CONV1D3
+        int C = a.K / 3;
+        int tap = k0 / C;
+        int c = k0 - tap * C;
+        int qq = ri.q + tap - 1;
+        if (qq < 0 || qq >= a.seg_len) return -1;
+        return (int64_t)(row + tap - 1) * a.lda + c;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_out(void* C, int64_t idx, int dt, float v) {
+    (void)sizeof(T);
+    if (dt == CMT_F32) ((float*)C)[idx] = v;
+    else if (dt == CMT_F16) ((f16_t*)C)[idx] = (f16_t)v;
+    else ((bf16_t*)C)[idx] = (bf16_t)v;
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[BM / 64][BN / 64],
+                                         int m0, int n0, int wm, int wn, int lane) {
+    const int h = lane >> 5;
+    const int col_l = lane & 31;
+    const int z = blockIdx.z;
+    const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
+    void* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
+    const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
+    const float* Rz = a.R ? a.R + (int64_t)z * a.r_bstride : nullptr;
+    for (int tn = 0; tn < BN / 64; ++tn) {
+        const int col = n0 + wn * (BN / 2) + tn * 32 + col_l;
+        const float bias = biasz ? biasz[col] : 0.f;
+        for (int tm = 0; tm < BM / 64; ++tm) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= a.M) continue;
+                float v = acc[tm][tn][r] + bias;
+                if (a.relu) v = fmaxf(v, 0.f);
+                if (Rz) v += Rz[(int64_t)row * a.ldr + col];
+                int64_t idx;
+                if (a.c_mode == CMT_C_ROWS) {
+                    idx = (int64_t)row * a.ldc + col;
+                } else {
+                    const int rpb = a.rows_per_batch;
+                    const int b = row / rpb;
+                    const int rr = row - b * rpb;
+                    idx = (((int64_t)b * (a.N >> 5) + (col >> 5)) * rpb + rr) * 32 + (col & 31);
+                }
+                store_out<float>(Cz, idx, a.c_dtype, v);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// f16 / bf16 compute
+// ---------------------------------------------------------------------------
+template <typename CT, int BM, int BN, int AMODE, bool A_F32>
+__global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
+    typedef typename mfma_traits<CT>::frag frag;
+    constexpr int ACH = BM / 64;  // 16-byte chunks of A per thread per k-step
+    constexpr int BCH = BN / 64;
+    __shared__ __attribute__((aligned(16))) CT As[2][BM * BK];
+    __shared__ __attribute__((aligned(16))) CT Bs[2][BN * BK];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int n0 = blockIdx.x * BN;
+    const int m0 = blockIdx.y * BM;
+    const int z = blockIdx.z;
+
+    const char* Ab = (const char*)a.A + (int64_t)z * a.a_bstride * (A_F32 ? 4 : 2);
+    const CT* Wb = (const CT*)a.W + (int64_t)z * a.w_bstride;
+    const bool use_a2 = (AMODE == CMT_A_ROWS) && a.A2 != nullptr && n0 < a.a2_cols;
+
+    RowInfo ri[ACH];
+    int arow[ACH], achunk[ACH];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+        int idx = tid + NT * i;
+        arow[i] = idx >> 2;
+        achunk[i] = idx & 3;
+        ri[i] = make_row_info<AMODE>(a, m0 + arow[i]);
+    }
+
+    frag areg[ACH];
+    frag breg[BCH];
+
+    auto load_tiles = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+            const int kk = k0 + achunk[i] * 8;
+            int64_t off = a_offset<AMODE>(a, ri[i], m0 + arow[i], kk);
+            if (off < 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) areg[i][j] = (CT)0.f;
+            } else if (A_F32) {
+                const float* p = (const float*)Ab + off;
+                f32x4 v0 = *(const f32x4*)p;
+                f32x4 v1 = *(const f32x4*)(p + 4);
+                if (use_a2) {
+                    const float* p2 = a.A2 + (int64_t)(m0 + arow[i]) * a.lda2 + kk;
+                    v0 += *(const f32x4*)p2;
+                    v1 += *(const f32x4*)(p2 + 4);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    areg[i][j] = (CT)v0[j];
+                    areg[i][j + 4] = (CT)v1[j];
+                }
+            } else {
+                areg[i] = *(const frag*)((const CT*)Ab + off);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            int idx = tid + NT * i;
+            int row = idx >> 2, c = idx & 3;
+            breg[i] = *(const frag*)(Wb + (int64_t)(n0 + row) * a.ldw + k0 + c * 8);
+        }
+    };
+    auto store_tiles = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+            int row = arow[i];
+            *(frag*)(&As[buf][row * BK + 8 * (achunk[i] ^ ((row >> 2) & 3))]) = areg[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            int idx = tid + NT * i;
+            int row = idx >> 2, c = idx & 3;
+            *(frag*)(&Bs[buf][row * BK + 8 * (c ^ ((row >> 2) & 3))]) = breg[i];
+        }
+    };
+
+    f32x16 acc[BM / 64][BN / 64];
+#pragma unroll
+    for (int i = 0; i < BM / 64; ++i)
+#pragma unroll
+        for (int j = 0; j < BN / 64; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = a.K / BK;
+    load_tiles(0);
+    store_tiles(0);
+    __syncthreads();
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            frag af[BM / 64], bfr[BN / 64];
+#pragma unroll
+            for (int tm = 0; tm < BM / 64; ++tm) {
+                int row = wm * (BM / 2) + tm * 32 + lr;
+                af[tm] = *(const frag*)(&As[cur][row * BK + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
+            }
+#pragma unroll
+            for (int tn = 0; tn < BN / 64; ++tn) {
+                int row = wn * (BN / 2) + tn * 32 + lr;
+                bfr[tn] = *(const frag*)(&Bs[cur][row * BK + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
+            }
+#pragma unroll
+            for (int tm = 0; tm < BM / 64; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < BN / 64; ++tn)
+                    acc[tm][tn] = mfma_traits<CT>::mma(af[tm], bfr[tn], acc[tm][tn]);
+        }
+        if (kt + 1 < nk) store_tiles(cur ^ 1);
+        __syncthreads();
+    }
+    epilogue<BM, BN>(a, acc, m0, n0, wm, wn, lane);
+}
+
+// ---------------------------------------------------------------------------
+// exact f32 compute (v_mfma_f32_32x32x2_f32)
+// ---------------------------------------------------------------------------
+constexpr int LDF = 36;  // padded LDS row (floats)
+
+template <int BM, int BN, int AMODE>
+__global__ __launch_bounds__(NT) void gemm_f32_kernel(cmt_gemm_args a) {
+    constexpr int ACH = BM / 32;  // float4 chunks per thread
+    constexpr int BCH = BN / 32;
+    __shared__ __attribute__((aligned(16))) float As[2][BM * LDF];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDF];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int n0 = blockIdx.x * BN;
+    const int m0 = blockIdx.y * BM;
+    const int z = blockIdx.z;
+
+    const float* Ab = (const float*)a.A + (int64_t)z * a.a_bstride;
+    const float* Wb = (const float*)a.W + (int64_t)z * a.w_bstride;
+    const bool use_a2 = (AMODE == CMT_A_ROWS) && a.A2 != nullptr && n0 < a.a2_cols;
+
+    RowInfo ri[ACH];
+    int arow[ACH], achunk[ACH];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+        int idx = tid + NT * i;
+        arow[i] = idx >> 3;
+        achunk[i] = idx & 7;
+        ri[i] = make_row_info<AMODE>(a, m0 + arow[i]);
+    }
+    f32x4 areg[ACH], breg[BCH];
+
+    auto load_tiles = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+            const int kk = k0 + achunk[i] * 4;
+            int64_t off = a_offset<AMODE>(a, ri[i], m0 + arow[i], kk);
+            if (off < 0) {
+                areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+                areg[i] = *(const f32x4*)(Ab + off);
+                if (use_a2) areg[i] += *(const f32x4*)(a.A2 + (int64_t)(m0 + arow[i]) * a.lda2 + kk);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            int idx = tid + NT * i;
+            int row = idx >> 3, c = idx & 7;
+            breg[i] = *(const f32x4*)(Wb + (int64_t)(n0 + row) * a.ldw + k0 + c * 4);
+        }
+    };
+    auto store_tiles = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) *(f32x4*)(&As[buf][arow[i] * LDF + achunk[i] * 4]) = areg[i];
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            int idx = tid + NT * i;
+            *(f32x4*)(&Bs[buf][(idx >> 3) * LDF + (idx & 7) * 4]) = breg[i];
+        }
+    };
+
+    f32x16 acc[BM / 64][BN / 64];
+#pragma unroll
+    for (int i = 0; i < BM / 64; ++i)
+#pragma unroll
+        for (int j = 0; j < BN / 64; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = a.K / BK;
+    load_tiles(0);
+    store_tiles(0);
+    __syncthreads();
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            f32x4 af[BM / 64], bfr[BN / 64];
+#pragma unroll
+            for (int tm = 0; tm < BM / 64; ++tm)
+                af[tm] = *(const f32x4*)(&As[cur][(wm * (BM / 2) + tm * 32 + lr) * LDF + 16 * lh + 4 * kc]);
+#pragma unroll
+            for (int tn = 0; tn < BN / 64; ++tn)
+                bfr[tn] = *(const f32x4*)(&Bs[cur][(wn * (BN / 2) + tn * 32 + lr) * LDF + 16 * lh + 4 * kc]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int tm = 0; tm < BM / 64; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < BN / 64; ++tn)
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm][t], bfr[tn][t], acc[tm][tn], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_tiles(cur ^ 1);
+        __syncthreads();
+    }
+    epilogue<BM, BN>(a, acc, m0, n0, wm, wn, lane);
+}
+
+template <int BM, int BN, int AMODE>
+int launch_mode(const cmt_gemm_args& a, hipStream_t s) {
+    dim3 grid(a.N / BN, cdiv(a.M, BM), a.batch);
+    if (a.w_dtype == CMT_F32) {
+        gemm_f32_kernel<BM, BN, AMODE><<<grid, NT, 0, s>>>(a);
+    } else if (a.w_dtype == CMT_BF16) {
+        if (a.a_dtype == CMT_F32) gemm_lowp_kernel<bf16_t, BM, BN, AMODE, true><<<grid, NT, 0, s>>>(a);
+        else gemm_lowp_kernel<bf16_t, BM, BN, AMODE, false><<<grid, NT, 0, s>>>(a);
+    } else {
+        if (a.a_dtype == CMT_F32) gemm_lowp_kernel<f16_t, BM, BN, AMODE, true><<<grid, NT, 0, s>>>(a);
+        else gemm_lowp_kernel<f16_t, BM, BN, AMODE, false><<<grid, NT, 0, s>>>(a);
+    }
+    return cmt_check_launch("cmt_gemm");
+}
+
+template <int BM, int BN>
+int launch_tiles(const cmt_gemm_args& a, hipStream_t s) {
+    switch (a.a_mode) {
+        case CMT_A_ROWS: return launch_mode<BM, BN, CMT_A_ROWS>(a, s);
+        case CMT_A_CONV3X3: return launch_mode<BM, BN, CMT_A_CONV3X3>(a, s);
+        default: return launch_mode<BM, BN, CMT_A_CONV1D3>(a, s);
+    }
+}
+
+}  // namespace
+
+extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_gemm: null args");
+    const cmt_gemm_args& a = *ap;
+    CMT_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.batch > 0, "cmt_gemm: empty problem");
+    CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
+    CMT_REQUIRE(a.K % BK == 0, "cmt_gemm: K must be a multiple of 32");
+    CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
+    CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16, "cmt_gemm: bad w_dtype");
+    CMT_REQUIRE(a.a_dtype == CMT_F32 || a.a_dtype == a.w_dtype, "cmt_gemm: A must be f32 or the compute dtype");
+    CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16, "cmt_gemm: bad c_dtype");
+    CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0, "cmt_gemm: lda/ldw must be multiples of 8 elements");
+    CMT_REQUIRE(a.A2 == nullptr || (a.a_mode == CMT_A_ROWS && a.a_dtype == CMT_F32 && a.lda2 % 4 == 0 &&
+                                    a.a2_cols % 128 == 0),
+                "cmt_gemm: A2 needs row mode, f32 A, 128-aligned a2_cols");
+    if (a.a_mode == CMT_A_CONV3X3)
+        CMT_REQUIRE(a.conv_c % BK == 0 && a.K == 9 * a.conv_c && a.conv_h > 0 && a.conv_w > 0 &&
+                    a.M % (a.conv_h * a.conv_w) == 0, "cmt_gemm: bad conv3x3 geometry");
+    if (a.a_mode == CMT_A_CONV1D3)
+        CMT_REQUIRE(a.K % 3 == 0 && (a.K / 3) % BK == 0 && a.seg_len > 0 && a.M % a.seg_len == 0,
+                    "cmt_gemm: bad conv1d3 geometry");
+    if (a.c_mode == CMT_C_HEADSPLIT)
+        CMT_REQUIRE(a.rows_per_batch > 0 && a.M % a.rows_per_batch == 0, "cmt_gemm: bad head-split rows");
+    hipStream_t s = (hipStream_t)stream;
+    // Tile choice: 128x128 when the grid still fills the chip, else 64x64.
+    const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
+    if (a.N % 128 == 0 && big_tiles >= 512) return launch_tiles<128, 128>(a, s);
+    return launch_tiles<64, 64>(a, s);
+}

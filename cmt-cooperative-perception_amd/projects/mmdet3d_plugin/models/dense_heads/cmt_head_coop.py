@@ -1,0 +1,95 @@
+"""Cooperative (vehicle + infrastructure) CMT heads on the gfx950 kernels.
+
+Reference: projects/mmdet3d_plugin/models/dense_heads/cmt_head_coop.py
+  filter_img_metas 41-57, CmtHeadCoop 72-809 (get_outs_dec 341-360,
+  forward_single 362-437, max-fusion 383-389), CmtImageHeadCoop 812-911,
+  CmtLidarHeadCoop 914-1017.
+One decoder pass per agent with the shared head weights; the element-wise
+max over agents is fused into the post_norm kernel of the second agent
+(LN_MAX_INTO), then the task heads run once.  ``forward_agents`` generalises
+the two-agent max to any number of agents (the 4-agent stress config).
+"""
+import torch
+
+from ...registry import HEADS
+from .cmt_head import CmtHead, multi_apply
+
+__all__ = ["filter_img_metas", "get_vehicle_image_metas", "get_infrastructure_image_metas", "CmtHeadCoop",
+           "CmtLidarHeadCoop", "CmtImageHeadCoop"]
+
+
+def filter_img_metas(img_meta, prefix="", ignore=""):
+    """cmt_head_coop.py:41-57."""
+    out = dict()
+    for k, v in img_meta.items():
+        if k.startswith(prefix):
+            out[k[len(prefix):]] = v
+        elif not k.startswith(ignore):
+            out[k] = v
+    out["node"] = prefix
+    return out
+
+
+def get_infrastructure_image_metas(img_metas):
+    return [filter_img_metas(m, prefix="infrastructure_", ignore="vehicle_") for m in img_metas]
+
+
+def get_vehicle_image_metas(img_metas):
+    return [filter_img_metas(m, prefix="vehicle_", ignore="infrastructure_") for m in img_metas]
+
+
+@HEADS.register_module()
+class CmtHeadCoop(CmtHead):
+    """cmt_head_coop.py:72-809 (fusion: LiDAR BEV + camera per agent)."""
+    variant = "fusion"
+
+    def forward_single(self, x_vehicle, x_infrastructure, x_img_vehicle, x_img_infrastructure, img_metas):
+        B = len(img_metas)
+        agents = []
+        if x_vehicle is not None or x_img_vehicle is not None:
+            agents.append((x_vehicle, x_img_vehicle, self._agent_metas(img_metas, "vehicle_")))
+        if x_infrastructure is not None or x_img_infrastructure is not None:
+            agents.append((x_infrastructure, x_img_infrastructure, self._agent_metas(img_metas, "infrastructure_")))
+        if not agents:
+            raise ValueError("CmtHeadCoop needs at least one agent's features")
+        return self._forward_agents(agents, img_metas, B)
+
+    def _agent_metas(self, img_metas, prefix):
+        if self.variant == "lidar":
+            return img_metas
+        return get_vehicle_image_metas(img_metas) if prefix == "vehicle_" else get_infrastructure_image_metas(img_metas)
+
+    def forward(self, vehicle_pts_feats, infrastructure_pts_feats, vehicle_img_feats=None,
+                infrastructure_img_feats=None, img_metas=None):
+        """cmt_head_coop.py:439-444."""
+        n = len(vehicle_pts_feats) if vehicle_pts_feats is not None else len(vehicle_img_feats)
+        none = [None] * n
+        img_metas = [img_metas for _ in range(n)]
+        return multi_apply(self.forward_single, vehicle_pts_feats or none, infrastructure_pts_feats or none,
+                           vehicle_img_feats or none, infrastructure_img_feats or none, img_metas)
+
+    def forward_agents(self, agents, img_metas):
+        """Any number of agents: ``agents`` = list of (prefix, pts_feat, img_feat);
+        outputs max-fused over agents (the reference fuses exactly two)."""
+        B = len(img_metas)
+        return self._forward_agents([(x, xi, self._agent_metas(img_metas, p)) for p, x, xi in agents], img_metas, B)
+
+
+@HEADS.register_module()
+class CmtImageHeadCoop(CmtHeadCoop):
+    """cmt_head_coop.py:812-911."""
+    variant = "image"
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.shared_conv = None
+
+
+@HEADS.register_module()
+class CmtLidarHeadCoop(CmtHeadCoop):
+    """cmt_head_coop.py:914-1017."""
+    variant = "lidar"
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.rv_embedding = None

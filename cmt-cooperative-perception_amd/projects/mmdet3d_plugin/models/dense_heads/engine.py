@@ -1,0 +1,216 @@
+"""Native execution of one CMT head forward (per agent and for the task heads).
+
+This is the hot path of SURVEY.md section 8(a), rows a1-a16, executed as a
+fixed sequence of gfx950 kernels over HBM-resident buffers:
+
+  shared_conv     NCHW->NHWC layout kernel + implicit-GEMM 3x3 conv (BN folded, ReLU)
+                  written straight into the memory rows (cmt_head.py:280-287, 481)
+  bev pos         pos2embed(coords_bev) fused kernel -> 2 GEMMs (bias/ReLU fused)
+                  written straight into the pos rows (cmt_head.py:324-337, 489)
+  image memory    layout kernel "(bs v) c h w -> bs (v h w) c" into the memory rows
+  rv pos          frustum geometry kernel (fp64 host inverse) -> 2 GEMMs into pos rows
+                  (cmt_head.py:417-433)
+  query embed     pos2embed(sigmoid(inverse_sigmoid(ref))) -> 2 GEMMs, plus the
+                  projected-view geometry kernel -> 2 GEMMs -> masked view sum
+                  (cmt_head.py:435-473)
+  decoder         PETRTransformerDecoder.run_rows (K/V of all layers in one GEMM,
+                  per layer 7 GEMMs + 2 attention + 3 LayerNorm launches)
+  coop max        fused into the post_norm kernel (cmt_head_coop.py:383-389)
+  task heads      grouped Conv1d as one batched (implicit conv1d) GEMM over the
+                  decoder layers, then GroupLayerNorm1d+ReLU, conv #2 and the
+                  box epilogue (cmt_head.py:136-203, 501-513)
+
+The reference computes the BEV positional encoding, the coordinate encodings
+and every layer's K/V projection again on each forward; so does this engine
+(no output caching across frames).
+"""
+import numpy as np
+import torch
+
+from ... import native
+from ...runtime import get_precision
+from ..utils.packing import to_dtype
+
+__all__ = ["HeadEngineMixin"]
+
+
+def _inv_lidar2img(metas):
+    """np.linalg.inv of every lidar2img in fp64 (cmt_head.py:428, 441-444)."""
+    l2i = np.stack([np.asarray(m["lidar2img"], dtype=np.float64) for m in metas])   # [B, V, 4, 4]
+    i2l = np.linalg.inv(l2i)
+    return l2i, i2l
+
+
+class HeadEngineMixin:
+    """Mixed into CmtHead / CmtHeadCoop and their LiDAR / image variants."""
+
+    # ------------------------------------------------------------------ packing
+    def _engine_pack(self, prec):
+        params = [p for p in self.parameters()] + [b for b in self.buffers()]
+
+        def build():
+            g = prec.gemm
+            pk = {}
+            if getattr(self, "shared_conv", None) is not None:
+                conv, bn = self.shared_conv.conv, self.shared_conv.bn
+                s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+                w = conv.weight * s[:, None, None, None]                   # [Cout, Cin, 3, 3]
+                pk["conv_w"] = to_dtype(w.permute(0, 2, 3, 1).reshape(w.shape[0], -1), g)   # [Cout, 9*Cin]
+                b = bn.bias - bn.running_mean * s
+                if conv.bias is not None:
+                    b = b + conv.bias * s
+                pk["conv_b"] = b.detach().float().contiguous()
+            be = self.bev_embedding
+            pk["bev"] = (to_dtype(be[0].weight, g), be[0].bias.detach().contiguous(),
+                         to_dtype(be[2].weight, g), be[2].bias.detach().contiguous())
+            if getattr(self, "rv_embedding", None) is not None:
+                re = self.rv_embedding
+                pk["rv"] = (to_dtype(re[0].weight, g), re[0].bias.detach().contiguous(),
+                            to_dtype(re[2].weight, g), re[2].bias.detach().contiguous())
+            return pk
+        return self._pack.get("engine", params, prec.name, build)
+
+    # ------------------------------------------------------------------ pieces
+    def _mlp(self, x, w, out=None, *, batch=1, a_bstride=0, c_bstride=0, c_offset=0, M=None):
+        """Linear-ReLU-Linear with the second GEMM optionally scattering rows
+        into a larger buffer (batched)."""
+        w0, b0, w2, b2 = w
+        h = native.linear(x, w0, b0, relu=True)
+        if out is None:
+            return native.linear(h, w2, b2)
+        M = M if M is not None else h.shape[0]
+        native.gemm(h, w2, out, M=M, N=w2.shape[0], K=w2.shape[1], lda=h.shape[1], ldw=w2.shape[1],
+                    ldc=out.shape[-1], bias=b2, batch=batch, a_bstride=a_bstride * h.shape[1] if batch > 1 else 0,
+                    c_bstride=c_bstride, c_offset=c_offset)
+        return out
+
+    def _shared_conv_into(self, x, mem, Nk, pk, prec):
+        B, Cin, H, W = x.shape
+        Cout = pk["conv_w"].shape[0]
+        in_dt = prec.gemm if prec.gemm != torch.float32 else torch.float32
+        xin = torch.empty((B * H * W, Cin), dtype=in_dt, device=x.device)
+        native.nchw_to_rows(x.contiguous().float(), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+        native.gemm(xin, pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,
+                    bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B,
+                    a_bstride=H * W * Cin, c_bstride=Nk * Cout)
+
+    def _bev_pos_into(self, pos, B, Nk, H, W, pk):
+        C = self.hidden_dim
+        cfg = self.train_cfg if self.train_cfg else self.test_cfg
+        x_size = cfg["grid_size"][1] // self.downsample_scale
+        y_size = cfg["grid_size"][0] // self.downsample_scale
+        if x_size * y_size != H * W:
+            raise ValueError(f"BEV map {H}x{W} does not match grid_size/downsample ({x_size}x{y_size})")
+        pe = torch.empty((H * W, 2 * C), dtype=torch.float32, device=pos.device)
+        native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
+        self._mlp(pe, pk["bev"], pos, batch=B, a_bstride=0, c_bstride=Nk * C, M=H * W)
+
+    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk):
+        C = self.hidden_dim
+        BV, _, h, w = x_img.shape
+        V = BV // B
+        pad_h, pad_w, _ = metas[0]["pad_shape"][0]
+        i2l = np.concatenate([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64)) for m in metas])
+        i2l = torch.from_numpy(i2l).float().to(pos.device)
+        D = self.depth_num
+        coords = torch.empty((BV * h * w, 3 * D), dtype=torch.float32, device=pos.device)
+        native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w, D=D, pad_h=float(pad_h), pad_w=float(pad_w),
+                            depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
+        w0, b0, w2, b2 = pk["rv"]
+        hid = native.linear(coords, w0, b0, relu=True)                       # [BV*h*w, 4C]
+        native.gemm(hid, w2, pos, M=V * h * w, N=C, K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
+                    bias=b2, batch=B, a_bstride=V * h * w * hid.shape[1], c_bstride=Nk * C, c_offset=offset * C)
+
+    def _query_pos(self, B, metas, with_rv, pk):
+        C = self.hidden_dim
+        ref = self.reference_points.weight.detach().contiguous()
+        Nq = ref.shape[0]
+        dev = ref.device
+        pe = torch.empty((Nq, 2 * C), dtype=torch.float32, device=dev)
+        native.pos2embed(ref, pe, n=Nq, F=C, mode=1, pos_stride=3)
+        qpos = torch.empty((B * Nq, C), dtype=torch.float32, device=dev)
+        self._mlp(pe, pk["bev"], qpos, batch=B, a_bstride=0, c_bstride=Nq * C, M=Nq)
+        if with_rv:
+            V = len(metas[0]["lidar2img"])
+            pad_h, pad_w, _ = metas[0]["pad_shape"][0]
+            l2i, i2l = _inv_lidar2img(metas)
+            l2i = torch.from_numpy(l2i).float().to(dev)
+            i2l = torch.from_numpy(i2l).float().to(dev)
+            refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
+            D = self.depth_num
+            coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)
+            mask = torch.empty((B * V * Nq,), dtype=torch.float32, device=dev)
+            native.rv_query_coords(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
+                                   pad_w=float(pad_w), pc_range=self.pc_range)
+            r = self._mlp(coords, pk["rv"])
+            native.masked_view_sum(r, mask, qpos, B=B, V=V, Nq=Nq, C=C)
+        return qpos
+
+    # ------------------------------------------------------------------ per agent
+    def _decode_agent(self, x, x_img, metas, B, out, post_flags, variant, prec):
+        """One get_outs_dec (cmt_head_coop.py:341-360) / the decoder part of
+        forward_single (cmt_head.py:481-499); writes post-normed, nan_to_num'ed
+        decoder outputs [L, B*Nq, C] into ``out`` (max-merged when post_flags
+        has LN_MAX_INTO)."""
+        pk = self._engine_pack(prec)
+        C = self.hidden_dim
+        dev = self.reference_points.weight.device
+        use_bev = variant != "image"
+        use_img = variant != "lidar"
+        HW = V = hw = 0
+        if use_bev:
+            _, _, H, W = x.shape
+            HW = H * W
+        if use_img:
+            BV, _, hi, wi = x_img.shape
+            V, hw = BV // B, hi * wi
+        Nk = HW + V * hw
+        mem = torch.empty((B * Nk, C), dtype=torch.float32, device=dev)
+        pos = torch.empty((B * Nk, C), dtype=torch.float32, device=dev)
+        if use_bev:
+            self._shared_conv_into(x, mem, Nk, pk, prec)
+            self._bev_pos_into(pos, B, Nk, H, W, pk)
+        if use_img:
+            native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C, rows_per_batch=Nk,
+                                row_offset=HW)
+            self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk)
+        qpos = self._query_pos(B, metas, use_img, pk)
+        Nq = self.num_query
+        self.transformer.decoder.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
+                                          prec=prec)
+        return out
+
+    # ------------------------------------------------------------------ task heads
+    def _task_outputs(self, outs_dec, B, prec):
+        """SeparateTaskHead for every task + box epilogue.  outs_dec [L, B*Nq, C]."""
+        L = outs_dec.shape[0]
+        Nq = self.num_query
+        C = self.hidden_dim
+        ref = self.reference_points.weight.detach()
+        refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
+        ret = []
+        for task in self.task_heads:
+            tp = task.packed(prec)
+            nh, k = len(tp["names"]), tp["k"]
+            width = nh * 64
+            H1 = torch.empty((L, B * Nq, width), dtype=torch.float32, device=outs_dec.device)
+            native.gemm(outs_dec, tp["w1"], H1, M=B * Nq, N=width, K=k * C, lda=C, ldw=k * C, ldc=width, batch=L,
+                        a_bstride=B * Nq * C, w_bstride=width * k * C, c_bstride=B * Nq * width,
+                        a_mode=native.A_CONV1D3 if k == 3 else native.A_ROWS, seg_len=Nq)
+            OUT = torch.empty((L, B, Nq, tp["out_total"]), dtype=torch.float32, device=outs_dec.device)
+            native.task_head_tail(H1, tp["gw"], tp["gb"], tp["w2"], tp["b2"], refB, OUT, L=L, B=B, Nq=Nq,
+                                  nheads=nh, hc=64, head_out=tp["head_out"], k=k, center_col=tp["center_col"],
+                                  height_col=tp["height_col"], pc_range=self.pc_range)
+            outs = {}
+            start = 0
+            for name, n in zip(tp["names"], tp["head_out"]):
+                outs[name] = OUT[..., start:start + n]
+                start += n
+            ret.append(outs)
+        return ret
+
+    def _check_eval(self):
+        if self.training:
+            raise NotImplementedError(
+                "training-mode forward (DN query groups, losses, Hungarian assignment) is not implemented on the "
+                "native path yet (SURVEY.md 8(f) next #2); call .eval()")

@@ -1,0 +1,34 @@
+"""Weight packing cache: converts module parameters once into the layouts and
+dtypes the gfx950 kernels read (e.g. bf16 [N, K] rows, BN folded into the
+conv, all decoder layers' K/V projections concatenated), and re-packs only when
+a parameter changes (tracked through ``Tensor._version`` and storage
+pointers, so optimizer steps and ``load_state_dict`` invalidate it)."""
+import torch
+
+__all__ = ["PackCache", "to_dtype"]
+
+
+def _key(tensors, extra):
+    return tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in tensors) + (extra,)
+
+
+class PackCache:
+    def __init__(self):
+        self._store = {}
+
+    def get(self, name, tensors, extra, builder):
+        k = _key(tensors, extra)
+        hit = self._store.get(name)
+        if hit is not None and hit[0] == k:
+            return hit[1]
+        with torch.no_grad():
+            val = builder()
+        self._store[name] = (k, val)
+        return val
+
+    def clear(self):
+        self._store.clear()
+
+
+def to_dtype(t, dtype):
+    return t.detach().to(dtype).contiguous()

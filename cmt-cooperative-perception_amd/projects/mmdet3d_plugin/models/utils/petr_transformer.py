@@ -1,0 +1,439 @@
+"""PETR decoder building blocks with the reference's registry names, kwargs
+and state_dict layout, executed by the gfx950 kernels.
+
+Reference: projects/mmdet3d_plugin/models/utils/petr_transformer.py
+  PETRMultiheadFlashAttention 182-321, PETRTransformerDecoder 324-371,
+  PETRTransformerDecoderLayer 374-487,
+and the mmcv 1.6.2 classes the configs instantiate through it
+(MultiheadAttention, FFN, BaseTransformerLayer, TransformerLayerSequence;
+not vendored -- restated from the pinned version).
+
+Two execution paths:
+  * module-level ``forward`` methods: the reference's per-module API on
+    sequence-first [N, B, C] tensors (each op one or more native launches);
+  * ``PETRTransformerDecoder.run_rows``: the fused decoder used by the heads --
+    the K/V projections of all layers are hoisted into ONE GEMM over the
+    memory (memory and key_pos are layer-invariant, cmt_transformer.py:84-127),
+    positional adds are fused into GEMM prologues, residual adds into GEMM
+    epilogues, and each layer's norms.2 LayerNorm is fused with the shared
+    post_norm (+ nan_to_num / coop max) in one wavefront-reduction kernel.
+"""
+import copy
+import math
+import warnings
+
+import torch
+import torch.nn as nn
+
+from ... import native
+from ...registry import (ATTENTION, FEEDFORWARD_NETWORK, TRANSFORMER_LAYER, TRANSFORMER_LAYER_SEQUENCE,
+                         build_from_cfg)
+from ...profiling import timed
+from ...runtime import get_precision
+from .attention import FlashMHA, project_attend_project
+from .packing import PackCache, to_dtype
+
+__all__ = ["FFN", "MultiheadAttention", "PETRMultiheadFlashAttention", "PETRMultiheadAttention",
+           "PETRTransformerDecoderLayer", "PETRTransformerDecoder"]
+
+
+def _rows(x):
+    """[N, B, C] -> contiguous fp32 [N*B, C]."""
+    return x.reshape(-1, x.shape[-1]).contiguous().float()
+
+
+@FEEDFORWARD_NETWORK.register_module()
+class FFN(nn.Module):
+    """mmcv 1.6.2 FFN: layers = Sequential(Sequential(Linear, act, Dropout) x (num_fcs-1),
+    Linear, Dropout); out = identity + layers(x) when add_identity."""
+
+    def __init__(self, embed_dims=256, feedforward_channels=1024, num_fcs=2, act_cfg=dict(type="ReLU", inplace=True),
+                 ffn_drop=0.0, dropout_layer=None, add_identity=True, init_cfg=None, **kwargs):
+        super().__init__()
+        assert num_fcs >= 2
+        if act_cfg.get("type", "ReLU") != "ReLU":
+            raise NotImplementedError("only ReLU FFNs are used by CMT configs")
+        self.embed_dims = embed_dims
+        self.feedforward_channels = feedforward_channels
+        self.num_fcs = num_fcs
+        layers = []
+        c_in = embed_dims
+        for _ in range(num_fcs - 1):
+            layers.append(nn.Sequential(nn.Linear(c_in, feedforward_channels), nn.ReLU(inplace=True),
+                                        nn.Dropout(ffn_drop)))
+            c_in = feedforward_channels
+        layers.append(nn.Linear(feedforward_channels, embed_dims))
+        layers.append(nn.Dropout(ffn_drop))
+        self.layers = nn.Sequential(*layers)
+        self.dropout_layer = nn.Identity()
+        self.add_identity = add_identity
+        self._pack = PackCache()
+
+    def packed(self, prec):
+        lins = [m[0] for m in self.layers[:-2]] + [self.layers[-2]]
+        return self._pack.get("w", [l.weight for l in lins], prec.name,
+                              lambda: [to_dtype(l.weight, prec.gemm) for l in lins])
+
+    def forward(self, x, identity=None):
+        prec = get_precision()
+        ws = self.packed(prec)
+        shape = x.shape
+        h = _rows(x)
+        lins = [m[0] for m in self.layers[:-2]] + [self.layers[-2]]
+        for i, (lin, w) in enumerate(zip(lins, ws)):
+            last = i == len(lins) - 1
+            R = None
+            if last and self.add_identity:
+                R = _rows(identity if identity is not None else x)
+            h = native.linear(h, w, lin.bias, relu=not last, R=R)
+        return h.view(*shape[:-1], self.embed_dims)
+
+
+class _MHABase(nn.Module):
+    """Shared forward of mmcv MultiheadAttention / PETRMultiheadFlashAttention
+    (sequence-first tensors, identity connection, positional encodings added
+    to query and key: petr_transformer.py:282-321)."""
+    fp16_core = False   # True for the flash-attn based wrapper
+
+    def _weights(self):
+        raise NotImplementedError
+
+    def forward(self, query, key=None, value=None, identity=None, query_pos=None, key_pos=None, attn_mask=None,
+                key_padding_mask=None, **kwargs):
+        if attn_mask is not None:
+            raise NotImplementedError("attention masks (training-time DN queries) are not implemented natively yet")
+        if key_padding_mask is not None and bool(key_padding_mask.any()):
+            raise NotImplementedError("non-trivial key_padding_mask is not used by CMT configs")
+        if key is None:
+            key = query
+        if value is None:
+            value = key
+        if identity is None:
+            identity = query
+        if key_pos is None and query_pos is not None:
+            if query_pos.shape == key.shape:
+                key_pos = query_pos
+            else:
+                warnings.warn(f"position encoding of key is missing in {self.__class__.__name__}.")
+        if self.batch_first:   # [B, N, C] -> sequence-first rows
+            query, key, value, identity = (t.transpose(0, 1) for t in (query, key, value, identity))
+            query_pos = query_pos.transpose(0, 1) if query_pos is not None else None
+            key_pos = key_pos.transpose(0, 1) if key_pos is not None else None
+        Nq, B, C = query.shape
+        Nk = key.shape[0]
+        prec = get_precision()
+        w_in, b_in, w_out, b_out = self._weights(prec)
+        adt, rnd = (prec.attn, prec.round_cross_out) if self.fp16_core else (prec.self_attn, False)
+        out = project_attend_project(_rows(query), _rows(key), _rows(value),
+                                     _rows(query_pos) if query_pos is not None else None,
+                                     _rows(key_pos) if key_pos is not None else None,
+                                     w_in, b_in, w_out, b_out, _rows(identity), adt, rnd, B=B, Nq=Nq, Nk=Nk,
+                                     H=self.num_heads, layout="seq_first")
+        out = out.view(Nq, B, C)
+        return out.transpose(0, 1) if self.batch_first else out
+
+
+@ATTENTION.register_module()
+class MultiheadAttention(_MHABase):
+    """mmcv 1.6.2 MultiheadAttention wrapper around ``nn.MultiheadAttention``
+    (self-attention, attn_cfgs[0] of every config).  ``self.attn`` keeps the
+    torch module only as the parameter container (state_dict keys
+    ``attn.in_proj_weight`` etc.); the math runs natively.  The reference core
+    runs in fp32; here it runs in the policy's attention dtype."""
+
+    def __init__(self, embed_dims, num_heads, attn_drop=0.0, proj_drop=0.0,
+                 dropout_layer=dict(type="Dropout", drop_prob=0.0), init_cfg=None, batch_first=False, **kwargs):
+        super().__init__()
+        if "dropout" in kwargs:
+            attn_drop = kwargs.pop("dropout")
+        self.embed_dims = embed_dims
+        self.num_heads = num_heads
+        self.batch_first = batch_first
+        self.attn = nn.MultiheadAttention(embed_dims, num_heads, attn_drop, **kwargs)
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.dropout_layer = nn.Identity()
+        self._pack = PackCache()
+
+    def _weights(self, prec):
+        a = self.attn
+        pk = self._pack.get("w", [a.in_proj_weight, a.out_proj.weight], prec.name, lambda: dict(
+            w_in=to_dtype(a.in_proj_weight, prec.gemm), w_out=to_dtype(a.out_proj.weight, prec.gemm)))
+        return pk["w_in"], a.in_proj_bias, pk["w_out"], a.out_proj.bias
+
+
+@ATTENTION.register_module()
+class PETRMultiheadFlashAttention(_MHABase):
+    """petr_transformer.py:182-321 (FlashMHA inside, batch_first forced True
+    at 224 -- the wrapper transposes; here the sequence-first rows are fed to
+    the kernel directly through its stride arguments)."""
+    fp16_core = True
+
+    def __init__(self, embed_dims, num_heads, attn_drop=0.0, proj_drop=0.0,
+                 dropout_layer=dict(type="Dropout", drop_prob=0.0), init_cfg=None, batch_first=True, **kwargs):
+        super().__init__()
+        if "dropout" in kwargs:
+            attn_drop = kwargs["dropout"]
+            kwargs.pop("dropout")
+        self.embed_dims = embed_dims
+        self.num_heads = num_heads
+        self.batch_first = False   # forward() receives sequence-first tensors (mmcv layer convention)
+        self.attn = FlashMHA(embed_dims, num_heads, attn_drop, **kwargs)
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.dropout_layer = nn.Identity()
+
+    def _weights(self, prec):
+        pk = self.attn.packed(prec)
+        return pk["w_in"], self.attn.in_proj_bias, pk["w_out"], self.attn.out_proj.bias
+
+
+@ATTENTION.register_module()
+class PETRMultiheadAttention(MultiheadAttention):
+    """petr_transformer.py:37-177 (registered, unused by the configs): the
+    mmcv MultiheadAttention contract with ``batch_first`` honoured."""
+
+
+@TRANSFORMER_LAYER.register_module()
+class PETRTransformerDecoderLayer(nn.Module):
+    """petr_transformer.py:374-487 over mmcv 1.6.2 BaseTransformerLayer
+    (post-norm op walk; deprecated ``feedforward_channels``/``ffn_dropout``/
+    ``ffn_num_fcs`` kwargs override ``ffn_cfgs`` as in mmcv)."""
+
+    SUPPORTED_ORDER = ("self_attn", "norm", "cross_attn", "norm", "ffn", "norm")
+
+    def __init__(self, attn_cfgs, feedforward_channels=None, ffn_dropout=0.0, operation_order=None,
+                 act_cfg=dict(type="ReLU", inplace=True), norm_cfg=dict(type="LN"), ffn_num_fcs=2, with_cp=True,
+                 ffn_cfgs=None, batch_first=False, init_cfg=None, **kwargs):
+        super().__init__()
+        assert len(operation_order) == 6
+        assert set(operation_order) == {"self_attn", "norm", "cross_attn", "ffn"}
+        self.operation_order = tuple(operation_order)
+        self.pre_norm = operation_order[0] == "norm"
+        self.use_checkpoint = with_cp
+        self.batch_first = batch_first
+        num_attn = sum(op in ("self_attn", "cross_attn") for op in operation_order)
+        if isinstance(attn_cfgs, dict):
+            attn_cfgs = [copy.deepcopy(attn_cfgs) for _ in range(num_attn)]
+        assert len(attn_cfgs) == num_attn
+        self.attentions = nn.ModuleList(build_from_cfg(c, ATTENTION) for c in attn_cfgs)
+        self.embed_dims = self.attentions[0].embed_dims
+        ffn_cfgs = copy.deepcopy(ffn_cfgs) if ffn_cfgs is not None else dict(
+            type="FFN", embed_dims=self.embed_dims, feedforward_channels=1024, num_fcs=2, ffn_drop=0.0,
+            act_cfg=dict(type="ReLU", inplace=True))
+        if feedforward_channels is not None:
+            ffn_cfgs["feedforward_channels"] = feedforward_channels
+        ffn_cfgs["ffn_drop"] = ffn_dropout
+        ffn_cfgs["num_fcs"] = ffn_num_fcs
+        ffn_cfgs.setdefault("embed_dims", self.embed_dims)
+        num_ffns = operation_order.count("ffn")
+        self.ffns = nn.ModuleList(build_from_cfg(copy.deepcopy(ffn_cfgs), FEEDFORWARD_NETWORK)
+                                  for _ in range(num_ffns))
+        if norm_cfg.get("type", "LN") != "LN":
+            raise NotImplementedError("only LN norms are used by CMT configs")
+        self.norms = nn.ModuleList(nn.LayerNorm(self.embed_dims) for _ in range(operation_order.count("norm")))
+
+    def _norm(self, i, x):
+        n = self.norms[i]
+        rows = _rows(x)
+        y = torch.empty_like(rows)
+        native.layernorm(rows, n.weight, n.bias, y, rows=rows.shape[0], C=rows.shape[1], ldx=rows.shape[1],
+                         ldy=rows.shape[1], eps=n.eps)
+        return y.view(x.shape)
+
+    def forward(self, query, key=None, value=None, query_pos=None, key_pos=None, attn_masks=None,
+                query_key_padding_mask=None, key_padding_mask=None, **kwargs):
+        """mmcv BaseTransformerLayer.forward op walk (post-norm)."""
+        if self.training and self.use_checkpoint:
+            raise NotImplementedError("training (with_cp) is not implemented on the native path yet")
+        num_attn = 2
+        if attn_masks is None or isinstance(attn_masks, torch.Tensor):
+            attn_masks = [attn_masks for _ in range(num_attn)]
+        attn_i = norm_i = ffn_i = 0
+        identity = query
+        for op in self.operation_order:
+            if op == "self_attn":
+                query = self.attentions[attn_i](query, query, query, identity if self.pre_norm else None,
+                                                query_pos=query_pos, key_pos=query_pos,
+                                                attn_mask=attn_masks[attn_i], key_padding_mask=query_key_padding_mask)
+                attn_i += 1
+                identity = query
+            elif op == "norm":
+                query = self._norm(norm_i, query)
+                norm_i += 1
+            elif op == "cross_attn":
+                query = self.attentions[attn_i](query, key, value, identity if self.pre_norm else None,
+                                                query_pos=query_pos, key_pos=key_pos,
+                                                attn_mask=attn_masks[attn_i], key_padding_mask=None)
+                attn_i += 1
+                identity = query
+            elif op == "ffn":
+                query = self.ffns[ffn_i](query, identity if self.pre_norm else None)
+                ffn_i += 1
+        return query
+
+
+@TRANSFORMER_LAYER_SEQUENCE.register_module()
+class PETRTransformerDecoder(nn.Module):
+    """petr_transformer.py:324-371 over mmcv TransformerLayerSequence."""
+
+    def __init__(self, transformerlayers=None, num_layers=None, post_norm_cfg=dict(type="LN"),
+                 return_intermediate=False, init_cfg=None, **kwargs):
+        super().__init__()
+        if isinstance(transformerlayers, dict):
+            transformerlayers = [copy.deepcopy(transformerlayers) for _ in range(num_layers)]
+        assert len(transformerlayers) == num_layers
+        self.num_layers = num_layers
+        self.layers = nn.ModuleList(build_from_cfg(c, TRANSFORMER_LAYER) for c in transformerlayers)
+        self.embed_dims = self.layers[0].embed_dims
+        self.pre_norm = self.layers[0].pre_norm
+        self.return_intermediate = return_intermediate
+        self.post_norm = nn.LayerNorm(self.embed_dims) if post_norm_cfg is not None else None
+        self._pack = PackCache()
+
+    # ------------------------------------------------------------------
+    def forward(self, query, key=None, value=None, query_pos=None, key_pos=None, attn_masks=None,
+                query_key_padding_mask=None, key_padding_mask=None, reg_branch=None, **kwargs):
+        """Sequence-first API (query [Nq,B,C], key [Nk,B,C]) ->
+        [L, Nq, B, C] (return_intermediate) or [1, Nq, B, C]."""
+        if attn_masks is not None and any(m is not None for m in (attn_masks if isinstance(attn_masks, list)
+                                                                 else [attn_masks])):
+            raise NotImplementedError("attention masks (training-time DN queries) are not implemented natively yet")
+        if value is not None and value is not key and not torch.equal(value, key):
+            # the fused path assumes value == key (true for every CMT transformer)
+            return self._forward_layers(query, key, value, query_pos, key_pos)
+        Nq, B, C = query.shape
+        Nk = key.shape[0]
+        if not self.fused_supported() or key_pos is None or query_pos is None:
+            return self._forward_layers(query, key, value, query_pos, key_pos)
+        mem = key.transpose(0, 1).reshape(B * Nk, C).contiguous().float()
+        pos = key_pos.transpose(0, 1).reshape(B * Nk, C).contiguous().float()
+        qpos = query_pos.transpose(0, 1).reshape(B * Nq, C).contiguous().float()
+        tgt0 = query.transpose(0, 1).reshape(B * Nq, C).contiguous().float()
+        out = self.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, post_flags=0, tgt0=tgt0)
+        out = out.view(self.num_layers, B, Nq, C).transpose(1, 2)
+        return out if self.return_intermediate else out[-1:]
+
+    def _forward_layers(self, query, key, value, query_pos, key_pos):
+        inter = []
+        for layer in self.layers:
+            query = layer(query, key, value, query_pos=query_pos, key_pos=key_pos)
+            if self.return_intermediate:
+                inter.append(self._post(query) if self.post_norm is not None else query)
+        if not self.return_intermediate:
+            return (self._post(query) if self.post_norm is not None else query)[None]
+        return torch.stack(inter)
+
+    def _post(self, x):
+        rows = _rows(x)
+        y = torch.empty_like(rows)
+        n = self.post_norm
+        native.layernorm(rows, n.weight, n.bias, y, rows=rows.shape[0], C=rows.shape[1], ldx=rows.shape[1],
+                         ldy=rows.shape[1], eps=n.eps)
+        return y.view(x.shape)
+
+    def fused_supported(self):
+        l0 = self.layers[0]
+        return (l0.operation_order == PETRTransformerDecoderLayer.SUPPORTED_ORDER and self.post_norm is not None
+                and self.embed_dims == 256 and all(len(l.ffns) == 1 and l.ffns[0].num_fcs == 2 for l in self.layers)
+                and all(a.num_heads * 32 == self.embed_dims for l in self.layers for a in l.attentions))
+
+    # ------------------------------------------------------------------
+    def packed(self, prec):
+        params = [p for p in self.parameters()]
+
+        def build():
+            L, C = self.num_layers, self.embed_dims
+            g = prec.gemm
+            layers = []
+            kw, kb, vw, vb = [], [], [], []
+            for lay in self.layers:
+                sa = lay.attentions[0].attn
+                ca = lay.attentions[1].attn
+                ffn = lay.ffns[0]
+                layers.append(dict(
+                    sa_w=to_dtype(sa.in_proj_weight, g), sa_b=sa.in_proj_bias.detach().contiguous(),
+                    sa_ow=to_dtype(sa.out_proj.weight, g), sa_ob=sa.out_proj.bias.detach().contiguous(),
+                    ca_wq=to_dtype(ca.in_proj_weight[:C], g),
+                    ca_bq=ca.in_proj_bias[:C].detach().contiguous() if ca.in_proj_bias is not None else None,
+                    ca_ow=to_dtype(ca.out_proj.weight, g),
+                    ca_ob=ca.out_proj.bias.detach().contiguous() if ca.out_proj.bias is not None else None,
+                    f1_w=to_dtype(ffn.layers[0][0].weight, g), f1_b=ffn.layers[0][0].bias.detach().contiguous(),
+                    f2_w=to_dtype(ffn.layers[1].weight, g), f2_b=ffn.layers[1].bias.detach().contiguous(),
+                    norms=[(n.weight.detach().contiguous(), n.bias.detach().contiguous(), n.eps)
+                           for n in lay.norms]))
+                kw.append(ca.in_proj_weight[C:2 * C])
+                vw.append(ca.in_proj_weight[2 * C:])
+                if ca.in_proj_bias is not None:
+                    kb.append(ca.in_proj_bias[C:2 * C])
+                    vb.append(ca.in_proj_bias[2 * C:])
+            kv_w = to_dtype(torch.cat(kw + vw, 0), g)
+            kv_b = torch.cat(kb + vb, 0).detach().contiguous() if kb else None
+            return dict(layers=layers, kv_w=kv_w, kv_b=kv_b,
+                        post=(self.post_norm.weight.detach().contiguous(),
+                              self.post_norm.bias.detach().contiguous(), self.post_norm.eps))
+        return self._pack.get("decoder", params, prec.name, build)
+
+    def run_rows(self, mem, pos, qpos, *, B, Nk, Nq, out=None, post_flags=native.LN_NAN_TO_NUM, prec=None,
+                 tgt0=None):
+        """Fused decoder.  mem/pos: [B*Nk, C] fp32 batch-major rows, qpos:
+        [B*Nq, C] fp32.  Writes the post-normed layer outputs to
+        out [L, B*Nq, C] (fp32) with ``post_flags`` (nan_to_num / max-into)."""
+        if not self.fused_supported():
+            raise NotImplementedError("fused decoder supports the CMT post-norm layout (C=256, 8x32 heads)")
+        prec = get_precision(prec)
+        pk = self.packed(prec)
+        L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
+        dev = mem.device
+        adt = prec.attn
+        f32 = torch.float32
+        rows = B * Nq
+        if out is None:
+            out = torch.empty((L, rows, C), dtype=f32, device=dev)
+        scale = 1.0 / math.sqrt(32.0)
+        # K/V of every layer in one GEMM: head-split [B][2L*H][Nk][32]
+        kv = torch.empty((B * 2 * L * C * Nk,), dtype=adt, device=dev)
+        native.gemm(mem, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
+                    A2=pos, lda2=C, a2_cols=L * C, headsplit_rows=Nk)
+        # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114)
+        tgt = tgt0.clone() if tgt0 is not None else torch.zeros((rows, C), dtype=f32, device=dev)
+        qkv = torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=dev)
+        qc = torch.empty((B * C * Nq,), dtype=adt, device=dev)
+        o = torch.empty((rows, C), dtype=f32, device=dev)
+        t1 = torch.empty_like(o)
+        t1n = torch.empty_like(o)
+        hf = torch.empty((rows, pk["layers"][0]["f1_w"].shape[0]), dtype=f32, device=dev)
+        ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
+                       native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
+        ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
+        FF = hf.shape[1]
+        for l, lw in enumerate(pk["layers"]):
+            # --- self attention (mmcv MultiheadAttention): q=k=tgt+qpos, v=tgt
+            native.gemm(tgt, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
+                        A2=qpos, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
+            native.attention(qkv, qkv, qkv, o, B=B, H=H, Nq=Nq, Nk=Nq,
+                             q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
+                             v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
+                             o_strides=(Nq * C, C), scale=scale, workspace=ws)
+            native.gemm(o, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt, ldr=C)
+            w0, b0, e0 = lw["norms"][0]
+            native.layernorm(t1, w0, b0, t1n, rows=rows, C=C, ldx=C, ldy=C, eps=e0)
+            # --- cross attention (PETRMultiheadFlashAttention): q=x+qpos, k=mem+pos, v=mem
+            native.gemm(t1n, lw["ca_wq"], qc, M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
+                        A2=qpos, lda2=C, a2_cols=C, headsplit_rows=Nq)
+            with timed("cross_attn"):
+                native.attention(qc, kv, kv, o, B=B, H=H, Nq=Nq, Nk=Nk,
+                                 q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
+                                 v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
+                                     v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
+                                 round_output=prec.round_cross_out)
+            native.gemm(o, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n, ldr=C)
+            w1, b1, e1 = lw["norms"][1]
+            native.layernorm(t1, w1, b1, o, rows=rows, C=C, ldx=C, ldy=C, eps=e1)   # o <- LN1 output
+            # --- FFN
+            native.gemm(o, lw["f1_w"], hf, M=rows, N=FF, K=C, lda=C, ldw=C, ldc=FF, bias=lw["f1_b"], relu=True)
+            native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o, ldr=C)
+            # --- norms.2 -> next query, fused with post_norm -> out[l]
+            w2, b2, e2 = lw["norms"][2]
+            pw, pb, _pe = pk["post"]
+            native.layernorm(t1, w2, b2, tgt, rows=rows, C=C, ldx=C, ldy=C, eps=e2, W2=pw, B2=pb, Y2=out,
+                             ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
+        return out

@@ -1,0 +1,285 @@
+"""ctypes binding of libcmt_hip.so (the C ABI declared in include/cmt_hip.h).
+
+This is the ONLY way the product path computes: every wrapper below checks
+that its tensors live on a HIP device and raises if the library is missing --
+there is no CPU or eager-PyTorch fallback.  PyTorch provides device memory,
+the current stream and graph capture (plumbing); the arithmetic happens in the
+hand-written gfx950 kernels.
+"""
+import ctypes
+import os
+
+import torch
+
+__all__ = ["lib", "available", "gemm", "attention", "layernorm", "pos2embed", "rv_pe_coords",
+           "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
+           "voxelize", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_DEFAULT_LIB = os.path.join(_PKG_ROOT, "lib", "libcmt_hip.so")
+
+F32, F16, BF16 = 0, 1, 2
+DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
+LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
+A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
+C_ROWS, C_HEADSPLIT = 0, 1
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_flt = ctypes.c_float
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [("M", _int), ("N", _int), ("K", _int), ("batch", _int),
+                ("A", _vp), ("lda", _i64), ("a_bstride", _i64), ("a_dtype", _int),
+                ("A2", _vp), ("lda2", _i64), ("a2_cols", _int),
+                ("a_mode", _int), ("conv_h", _int), ("conv_w", _int), ("conv_c", _int), ("seg_len", _int),
+                ("W", _vp), ("ldw", _i64), ("w_bstride", _i64), ("w_dtype", _int),
+                ("bias", _vp), ("bias_bstride", _i64),
+                ("R", _vp), ("ldr", _i64), ("r_bstride", _i64),
+                ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int),
+                ("c_mode", _int), ("rows_per_batch", _int), ("relu", _int)]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [("B", _int), ("H", _int), ("Nq", _int), ("Nk", _int), ("dtype", _int),
+                ("Q", _vp), ("q_bstride", _i64), ("q_hstride", _i64), ("q_rstride", _i64),
+                ("K", _vp), ("k_bstride", _i64), ("k_hstride", _i64), ("k_rstride", _i64),
+                ("V", _vp), ("v_bstride", _i64), ("v_hstride", _i64), ("v_rstride", _i64),
+                ("O", _vp), ("o_bstride", _i64), ("o_rstride", _i64), ("scale", _flt), ("kv_splits", _int),
+                ("flags", _int),
+                ("workspace", _vp), ("workspace_bytes", _i64)]
+
+
+_LIB = None
+
+
+def _load():
+    path = os.environ.get("CMT_HIP_LIB", _DEFAULT_LIB)
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libcmt_hip.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C cmt-cooperative-perception_amd/csrc`).  There is no fallback path.")
+    torch.cuda.init() if torch.cuda.is_available() else None  # share torch's HIP runtime (same soname)
+    L = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    sig = {
+        "cmt_abi_version": ([], _int),
+        "cmt_last_error": ([], ctypes.c_char_p),
+        "cmt_gemm": ([P(GemmArgs), _vp], _int),
+        "cmt_attn_workspace_bytes": ([P(AttnArgs)], _i64),
+        "cmt_attn_fwd": ([P(AttnArgs), _vp], _int),
+        "cmt_layernorm": ([_vp, _i64, _int, _int, _vp, _vp, _flt, _vp, _i64, _int, _vp, _vp, _vp, _i64, _int, _vp],
+                          _int),
+        "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _i64, _vp], _int),
+        "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _vp], _int),
+        "cmt_rv_query_coords": ([_vp, _int, _int, _int, _int, _flt, _flt, _vp, _vp, P(_flt), _vp, _vp, _vp], _int),
+        "cmt_masked_view_sum": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp], _int),
+        "cmt_nchw_to_rows": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp], _int),
+        "cmt_cast": ([_vp, _int, _vp, _int, _i64, _vp], _int),
+        "cmt_task_head_tail": ([_vp, _int, _int, _int, _int, _int, _vp, _vp, _vp, _vp, P(_int), _int, _int, _vp,
+                                _int, _int, P(_flt), _vp, _vp], _int),
+        "cmt_voxelize_workspace_bytes": ([_int, _int], _i64),
+        "cmt_voxelize": ([_vp, _int, _int, P(_flt), P(_flt), P(_int), _int, _int, _int, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _i64, _vp], _int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    if L.cmt_abi_version() != 1:
+        raise RuntimeError("libcmt_hip.so ABI version mismatch")
+    return L
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = _load()
+    return _LIB
+
+
+def available():
+    try:
+        lib()
+        return True
+    except (RuntimeError, OSError):
+        return False
+
+
+def _check(rc, name):
+    if rc != 0:
+        msg = lib().cmt_last_error().decode("utf-8", "replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("CMT HIP ops need tensors on a HIP device (no CPU fallback)")
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dtype_code(dt):
+    return DT[dt]
+
+
+def _farr(vals, n):
+    arr = (ctypes.c_float * n)(*[float(v) for v in vals])
+    return arr
+
+
+# ---------------------------------------------------------------------------
+def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0, a2_cols=0,
+         a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0, bias_bstride=0,
+         r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0):
+    """C = act(A W^T + bias) + R with the fused prologue/epilogue of cmt_gemm.
+    Offsets are in elements of the respective tensor."""
+    _dev(A, W, C, bias, R, A2)
+    g = GemmArgs()
+    g.M, g.N, g.K, g.batch = M, N, K, batch
+    g.A = A.data_ptr() + a_offset * A.element_size()
+    g.lda, g.a_bstride, g.a_dtype = lda, a_bstride, DT[A.dtype]
+    g.A2 = None if A2 is None else A2.data_ptr() + a2_offset * 4
+    g.lda2, g.a2_cols = lda2, a2_cols
+    g.a_mode = a_mode
+    g.conv_h, g.conv_w, g.conv_c = conv
+    g.seg_len = seg_len
+    g.W, g.ldw, g.w_bstride, g.w_dtype = W.data_ptr(), ldw, w_bstride, DT[W.dtype]
+    g.bias = None if bias is None else bias.data_ptr()
+    g.bias_bstride = bias_bstride
+    g.R = None if R is None else R.data_ptr() + r_offset * 4
+    g.ldr, g.r_bstride = ldr, r_bstride
+    g.C = C.data_ptr() + c_offset * C.element_size()
+    g.ldc, g.c_bstride, g.c_dtype = ldc, c_bstride, DT[C.dtype]
+    g.c_mode = C_HEADSPLIT if headsplit_rows else C_ROWS
+    g.rows_per_batch = headsplit_rows
+    g.relu = int(bool(relu))
+    _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
+
+
+def linear(X, W, bias=None, *, relu=False, R=None, out=None, out_dtype=torch.float32, A2=None, a2_cols=0,
+           headsplit_rows=0):
+    """Row-major linear layer: X [M, K] (f32 or compute dtype), W [N, K]."""
+    M, K = X.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty((M, N), device=X.device, dtype=out_dtype)
+    gemm(X, W, out, M=M, N=N, K=K, lda=X.stride(0), ldw=W.stride(0), ldc=N, bias=bias, relu=relu, R=R,
+         ldr=(R.stride(0) if R is not None else 0), A2=A2, lda2=(A2.stride(0) if A2 is not None else 0),
+         a2_cols=a2_cols, headsplit_rows=headsplit_rows)
+    return out
+
+
+_WS_CACHE = {}
+
+
+def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, q_offset=0,
+              k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False):
+    """Strides are (batch, head, row) in elements; o_strides = (batch, row)."""
+    _dev(Q, K, V, O)
+    a = AttnArgs()
+    a.B, a.H, a.Nq, a.Nk, a.dtype = B, H, Nq, Nk, DT[Q.dtype]
+    es = Q.element_size()
+    a.Q = Q.data_ptr() + q_offset * es
+    a.q_bstride, a.q_hstride, a.q_rstride = q_strides
+    a.K = K.data_ptr() + k_offset * es
+    a.k_bstride, a.k_hstride, a.k_rstride = k_strides
+    a.V = V.data_ptr() + v_offset * es
+    a.v_bstride, a.v_hstride, a.v_rstride = v_strides
+    a.O = O.data_ptr() + o_offset * 4
+    a.o_bstride, a.o_rstride = o_strides
+    a.scale, a.kv_splits = scale, kv_splits
+    a.flags = 1 if round_output else 0
+    need = lib().cmt_attn_workspace_bytes(ctypes.byref(a))
+    if need > 0:
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty(need, dtype=torch.uint8, device=O.device)
+        a.workspace, a.workspace_bytes = workspace.data_ptr(), workspace.numel()
+    _check(lib().cmt_attn_fwd(ctypes.byref(a), _stream()), "cmt_attn_fwd")
+
+
+def attn_workspace_bytes(*, B, H, Nq, Nk, kv_splits=0):
+    a = AttnArgs()
+    a.B, a.H, a.Nq, a.Nk, a.kv_splits = B, H, Nq, Nk, kv_splits
+    return int(lib().cmt_attn_workspace_bytes(ctypes.byref(a)))
+
+
+def layernorm(X, W, Bv, Y, *, rows, C, ldx, ldy, eps=1e-5, flags=0, W2=None, B2=None, Y2=None, ldy2=0,
+              flags2=0, x_offset=0, y_offset=0, y2_offset=0):
+    _dev(X, W, Bv, Y, W2, B2, Y2)
+    _check(lib().cmt_layernorm(X.data_ptr() + 4 * x_offset, ldx, rows, C, _p(W), _p(Bv), eps,
+                               Y.data_ptr() + 4 * y_offset, ldy, flags, _p(W2), _p(B2),
+                               None if Y2 is None else Y2.data_ptr() + 4 * y2_offset, ldy2, flags2, _stream()),
+           "cmt_layernorm")
+
+
+def pos2embed(pos, out, *, n, F, mode=0, pos_stride=2, grid=(0, 0), ldo=None):
+    _dev(pos, out)
+    _check(lib().cmt_pos2embed(_p(pos), pos_stride, n, F, mode, grid[0], grid[1], _p(out),
+                               ldo if ldo is not None else 2 * F, _stream()), "cmt_pos2embed")
+
+
+def rv_pe_coords(i2l, out, *, BV, h, w, D, pad_h, pad_w, depth_max, pc_range):
+    _dev(i2l, out)
+    _check(lib().cmt_rv_pe_coords(BV, h, w, D, pad_h, pad_w, depth_max, _p(i2l), _farr(pc_range, 6), _p(out),
+                                  _stream()), "cmt_rv_pe_coords")
+
+
+def rv_query_coords(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w, pc_range):
+    _dev(ref, l2i, i2l, out, mask)
+    _check(lib().cmt_rv_query_coords(_p(ref), B, V, Nq, D, pad_h, pad_w, _p(l2i), _p(i2l), _farr(pc_range, 6),
+                                     _p(out), _p(mask), _stream()), "cmt_rv_query_coords")
+
+
+def masked_view_sum(X, mask, Y, *, B, V, Nq, C):
+    _dev(X, mask, Y)
+    _check(lib().cmt_masked_view_sum(_p(X), _p(mask), B, V, Nq, C, _p(Y), _stream()), "cmt_masked_view_sum")
+
+
+def nchw_to_rows(X, Y, *, nb, nv, C, HW, ldy, rows_per_batch, row_offset=0):
+    _dev(X, Y)
+    _check(lib().cmt_nchw_to_rows(_p(X), nb, nv, C, HW, _p(Y), DT[Y.dtype], ldy, rows_per_batch, row_offset,
+                                  _stream()), "cmt_nchw_to_rows")
+
+
+def cast(X, Y):
+    _dev(X, Y)
+    _check(lib().cmt_cast(_p(X), DT[X.dtype], _p(Y), DT[Y.dtype], X.numel(), _stream()), "cmt_cast")
+
+
+def task_head_tail(H1, gw, gb, W2, B2, ref, out, *, L, B, Nq, nheads, hc, head_out, k, center_col, height_col,
+                   pc_range):
+    _dev(H1, gw, gb, W2, B2, ref, out)
+    ho = (ctypes.c_int * len(head_out))(*head_out)
+    _check(lib().cmt_task_head_tail(_p(H1), L, B, Nq, nheads, hc, _p(gw), _p(gb), _p(W2), _p(B2), ho,
+                                    int(sum(head_out)), k, _p(ref), center_col, height_col, _farr(pc_range, 6),
+                                    _p(out), _stream()), "cmt_task_head_tail")
+
+
+def voxelize(points, *, voxel_size, coors_range, grid, max_points, max_voxels, nfeat_mean):
+    """points [N, F] f32 on device -> (voxels, coors, num_points, means, num_voxels_dev) sized max_voxels."""
+    _dev(points)
+    points = points.contiguous()
+    N, F = points.shape
+    dev = points.device
+    voxels = torch.empty((max_voxels, max_points, F), dtype=torch.float32, device=dev)
+    coors = torch.empty((max_voxels, 3), dtype=torch.int32, device=dev)
+    num = torch.empty((max_voxels,), dtype=torch.int32, device=dev)
+    means = torch.empty((max_voxels, nfeat_mean), dtype=torch.float32, device=dev)
+    nvox = torch.empty((1,), dtype=torch.int32, device=dev)
+    wsb = int(lib().cmt_voxelize_workspace_bytes(N, max_voxels))
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=dev)
+    g = (ctypes.c_int * 3)(*[int(x) for x in grid])
+    _check(lib().cmt_voxelize(_p(points), N, F, _farr(voxel_size, 3), _farr(coors_range, 6), g, max_points,
+                              max_voxels, nfeat_mean, _p(voxels), _p(coors), _p(num), _p(means), _p(nvox), _p(ws),
+                              wsb, _stream()), "cmt_voxelize")
+    return voxels, coors, num, means, nvox

@@ -1,0 +1,213 @@
+/*
+ * cmt_hip.h -- C ABI of the MI355X-native CMT / CMTCoop decoder-head hot path.
+ *
+ * Build: libcmt_hip.so (hipcc --offload-arch=gfx950), see
+ * cmt-cooperative-perception_amd/csrc/Makefile.  Consumers: the registered
+ * Python classes in cmt-cooperative-perception_amd/projects/mmdet3d_plugin
+ * (ctypes, native.py) -- the drop-in for the reference's
+ * projects/mmdet3d_plugin heads/transformer/attention/voxelization.
+ *
+ * Contract:
+ *   - plain pointers + sizes; every pointer is a device pointer unless noted;
+ *   - the caller (PyTorch) owns every buffer; nothing here allocates device
+ *     memory -- scratch space is a caller-provided workspace whose size is
+ *     returned by the matching *_workspace_bytes query;
+ *   - stream-ordered and reentrant: every call takes the stream (a hipStream_t
+ *     passed as void*), launches asynchronously on it, never synchronises and
+ *     keeps no global mutable state (graph-capturable);
+ *   - errors: every entry point returns 0 on success, a CMT_E* argument-check
+ *     code, or the hipError_t of a failed launch; cmt_last_error() returns a
+ *     thread-local message describing the last failure.
+ *
+ * Element type codes (dtype arguments).
+ */
+#ifndef CMT_HIP_H
+#define CMT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMT_ABI_VERSION 1
+
+enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
+
+enum cmt_status {
+    CMT_OK = 0,
+    CMT_EINVAL = 1001,    /* bad argument (shape, alignment, dtype combination) */
+    CMT_ENOTSUP = 1002,   /* unsupported configuration */
+    CMT_EWORKSPACE = 1003 /* workspace too small */
+};
+
+int cmt_abi_version(void);
+const char* cmt_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * GEMM with fused prologue/epilogue (MFMA, gfx950).
+ *   C[m, n] = act( sum_k Aeff[m, k] * W[n, k] + bias[n] ) + R[m, n]
+ * Replaces the cuBLAS GEMMs of the reference:
+ *   FlashMHA _in_projection_packed      models/utils/attention.py:21-27,130
+ *   FlashMHA out_proj                   models/utils/attention.py:117,138
+ *   nn.MultiheadAttention in/out proj   (mmcv MultiheadAttention, attn_cfgs[0])
+ *   mmcv FFN fc1/fc2                    (ffn_cfgs, e.g. configs/.../cmt_lidar_voxel0075_cbgs.py:232-239)
+ *   bev_embedding / rv_embedding MLPs   models/dense_heads/cmt_head.py:292-301
+ *   shared_conv Conv2d 3x3 (+BN fold)   models/dense_heads/cmt_head.py:280-287  (a_mode = CONV3X3)
+ *   SeparateTaskHead grouped Conv1d     models/dense_heads/cmt_head.py:136-159  (a_mode = CONV1D3, batch = groups)
+ * Aeff = A (+ A2 for output columns n < a2_cols; the positional-encoding add
+ * `key = key + key_pos`, petr_transformer.py:296-299, fused into the load).
+ * Compute dtype = w_dtype: CMT_F32 (exact-f32 MFMA 32x32x2), CMT_F16 or
+ * CMT_BF16 (MFMA 32x32x16, A converted on load, fp32 accumulate).
+ * Requirements: N % 64 == 0, K % 32 == 0, 16-byte aligned A/W rows.
+ * ------------------------------------------------------------------------ */
+enum cmt_gemm_amode { CMT_A_ROWS = 0, CMT_A_CONV3X3 = 1, CMT_A_CONV1D3 = 2 };
+enum cmt_gemm_cmode { CMT_C_ROWS = 0, CMT_C_HEADSPLIT = 1 };
+
+typedef struct cmt_gemm_args {
+    int M, N, K;
+    int batch;                 /* grid z; per-batch strides below (elements) */
+    const void* A; int64_t lda; int64_t a_bstride; int a_dtype;
+    const float* A2; int64_t lda2; int a2_cols;
+    int a_mode;                /* cmt_gemm_amode */
+    int conv_h, conv_w, conv_c;/* CONV3X3: NHWC input [M/(h*w)][h][w][c], K = 9*c */
+    int seg_len;               /* CONV1D3: rows form segments of seg_len (zero pad), K = 3*C */
+    const void* W; int64_t ldw; int64_t w_bstride; int w_dtype;
+    const float* bias; int64_t bias_bstride;
+    const float* R; int64_t ldr; int64_t r_bstride;
+    void* C; int64_t ldc; int64_t c_bstride; int c_dtype;
+    int c_mode;                /* cmt_gemm_cmode; HEADSPLIT: C[(b*(N/32)+n/32)*rows_per_batch + r][32] */
+    int rows_per_batch;
+    int relu;
+} cmt_gemm_args;
+
+int cmt_gemm(const cmt_gemm_args* args, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Multi-head attention core, head_dim = 32 (flash-style, online softmax,
+ * f16/bf16 MFMA with fp32 accumulate, or exact-f32 MFMA for dtype CMT_F32;
+ * no mask).
+ * Replaces flash_attn_unpadded_kvpacked_func (flash-attn 0.2.2) called at
+ *   models/utils/attention.py:70-74 (FlashAttention.forward 46-92, fp16 core)
+ * and the softmax(QK^T/sqrt(d))V core of nn.MultiheadAttention used by the
+ * self-attention (mmcv MultiheadAttention, attn_cfgs[0]).
+ * Element (b, h, row, d) of Q/K/V is at X[b*x_bstride + h*x_hstride + row*x_rstride + d]
+ * (head-split layout: rstride = 32; token-major [B,S,H*32]: rstride = H*32;
+ * sequence-first [S,B,H*32]: rstride = B*H*32).  Row strides must keep
+ * 16-byte alignment (multiples of 8 elements).
+ * Output O is fp32 with heads concatenated per row (normalised).
+ * Nk is split into kv_splits chunks processed by separate workgroups and
+ * merged by a combine pass (workspace: cmt_attn_workspace_bytes).
+ * ------------------------------------------------------------------------ */
+enum { CMT_ATTN_ROUND_OUTPUT = 1 };
+
+typedef struct cmt_attn_args {
+    int B, H, Nq, Nk;
+    int dtype;                 /* CMT_F16 or CMT_BF16 (Q, K, V) */
+    const void* Q; int64_t q_bstride, q_hstride, q_rstride;
+    const void* K; int64_t k_bstride, k_hstride, k_rstride;
+    const void* V; int64_t v_bstride, v_hstride, v_rstride;
+    float* O; int64_t o_bstride, o_rstride;  /* O[b*o_bstride + q*o_rstride + h*32 + d] */
+    float scale;               /* softmax scale, usually 1/sqrt(32) */
+    int kv_splits;             /* 0 = choose automatically */
+    int flags;                 /* CMT_ATTN_ROUND_OUTPUT: round O to dtype (flash-attn returns fp16) */
+    void* workspace; int64_t workspace_bytes;
+} cmt_attn_args;
+
+int64_t cmt_attn_workspace_bytes(const cmt_attn_args* args);
+int cmt_attn_fwd(const cmt_attn_args* args, void* stream);
+
+/* ------------------------------------------------------------------------
+ * LayerNorm over the last dim C (C % 64 == 0, C <= 1024), eps given.
+ *   y = LN(x) * w + b   (nn.LayerNorm; mmcv build_norm_layer LN, eps 1e-5)
+ * flags: CMT_LN_NAN_TO_NUM  apply torch.nan_to_num to y (cmt_head.py:499)
+ *        CMT_LN_MAX_INTO    y = max(y, Y_old) (coop max-fusion, cmt_head_coop.py:388-389)
+ * If W2/B2/Y2 are non-null a second LN is applied to the first LN's output
+ * (the decoder post_norm of each layer output, petr_transformer.py:364-368)
+ * and written to Y2 with its own flags2.
+ * Pointer arguments named *_range6, *3 (voxel geometry) and head_out are HOST
+ * arrays (read at launch); all other pointers are device pointers.
+ * ------------------------------------------------------------------------ */
+enum { CMT_LN_NAN_TO_NUM = 1, CMT_LN_MAX_INTO = 2 };
+int cmt_layernorm(const float* X, int64_t ldx, int rows, int C,
+                  const float* W, const float* Bv, float eps, float* Y, int64_t ldy, int flags,
+                  const float* W2, const float* B2, float* Y2, int64_t ldy2, int flags2,
+                  void* stream);
+
+/* ------------------------------------------------------------------------
+ * Coordinate encodings.
+ * cmt_pos2embed: cmt_head.py:40-50.  pos [n, pos_stride] (x, y in the first two
+ *   fp32 lanes), out [n, 2F] fp32 (F = num_pos_feats); mode 1 applies
+ *   sigmoid(inverse_sigmoid(p)) first (query_embed, cmt_head.py:470).
+ *   If pos == NULL the BEV grid centres (coords_bev, cmt_head.py:324-337) of a
+ *   grid_h x grid_w map are generated in place of the input.
+ * cmt_rv_pe_coords: _rv_pe geometry (cmt_head.py:417-432): out [BV*h*w, 3*D]
+ *   normalised lidar coordinates of D depth samples per image token; i2l is a
+ *   [BV,4,4] fp32 device array of inv(lidar2img) (fp64 host inverse).
+ * cmt_rv_query_coords: _rv_query_embed geometry (cmt_head.py:446-463):
+ *   ref [B,Nq,3] (raw reference points; clamped + sigmoid(inverse_sigmoid)),
+ *   l2i / i2l [B,V,4,4] fp32 -> out [B,V,Nq,3*D], mask [B,V,Nq] fp32 {0,1}.
+ * cmt_masked_view_sum: (rv * mask).sum(dim=1) (cmt_head.py:466) added into Y:
+ *   Y[b,q,:] += sum_v X[b,v,q,:] * mask[b,v,q].
+ * ------------------------------------------------------------------------ */
+int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F, int mode,
+                  int grid_h, int grid_w, float* out, int64_t ldo, void* stream);
+int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float pad_w, float depth_max,
+                     const float* i2l, const float* pc_range6, float* out, void* stream);
+int cmt_rv_query_coords(const float* ref, int B, int V, int Nq, int D, float pad_h, float pad_w,
+                        const float* l2i, const float* i2l, const float* pc_range6,
+                        float* out, float* mask, void* stream);
+int cmt_masked_view_sum(const float* X, const float* mask, int B, int V, int Nq, int C,
+                        float* Y, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Layout / dtype plumbing.
+ * cmt_nchw_to_rows: X [B, C, H*W] (optionally grouped as B = nb*nv images)
+ *   -> rows: Y[(b_outer*rows_per_batch + row_offset + v*H*W + p)*ldy + c],
+ *   i.e. rearrange "(bs v) c h w -> bs (v h w) c" (cmt_transformer.py:104-105),
+ *   output dtype ydtype (CMT_F32/F16/BF16).
+ * cmt_cast: elementwise dtype conversion of n elements.
+ * ------------------------------------------------------------------------ */
+int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype,
+                     int64_t ldy, int64_t rows_per_batch, int64_t row_offset, void* stream);
+int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------------
+ * SeparateTaskHead tail (cmt_head.py:136-203) + box epilogue (501-513).
+ * H1 [L, B*Nq, nheads*hc] is the output of the first grouped conv (one GEMM
+ * for all heads).  For every head: GroupLayerNorm1d over its hc channels
+ * (eps 1e-6, biased var, cmt_head.py:56-66) -> ReLU -> grouped Conv1d
+ * (kernel k along queries, zero pad) with weights W2 [L][out_total][k][hc]
+ * packed per head, bias B2 [L][out_total].  Outputs are written to
+ * OUT[L, B, Nq, out_total] (heads concatenated in order, widths head_out[]).
+ * Columns listed by center_col/height_col receive the box epilogue:
+ * sigmoid(x + inverse_sigmoid(ref)) * (max - min) + min.
+ * ------------------------------------------------------------------------ */
+int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nheads, int hc,
+                       const float* gln_w, const float* gln_b, const float* W2, const float* B2,
+                       const int* head_out, int out_total, int k,
+                       const float* ref, int center_col, int height_col, const float* pc_range6,
+                       float* OUT, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Point -> voxel scatter-mean (SPConvVoxelization + HardSimpleVFE).
+ * Replaces spconv PointToVoxel at mmcv_custom/ops/voxel/spconv_voxelize.py:25-32,58-61
+ * (called per sample at models/detectors/cmt.py:101-105) and mmdet3d
+ * HardSimpleVFE.  Deterministic CPU semantics: voxels in first-appearance
+ * order of their points, each keeps its first max_points points in input
+ * order, at most max_voxels voxels, coordinates z,y,x.
+ * points [N, F] fp32 (F >= nfeat_mean); outputs sized for max_voxels:
+ *   voxels [max_voxels, max_points, F] (zero padded), coors [max_voxels, 3],
+ *   num_points [max_voxels], means [max_voxels, nfeat_mean],
+ *   num_voxels [1] (device int, M).
+ * ------------------------------------------------------------------------ */
+int64_t cmt_voxelize_workspace_bytes(int N, int max_voxels);
+int cmt_voxelize(const float* points, int N, int F, const float* voxel_size3,
+                 const float* coors_range6, const int* grid3, int max_points, int max_voxels,
+                 int nfeat_mean, float* voxels, int* coors, int* num_points, float* means,
+                 int* num_voxels, void* workspace, int64_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMT_HIP_H */

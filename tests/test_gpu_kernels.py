@@ -1,0 +1,224 @@
+"""Kernel-level numerics of libcmt_hip.so against plain PyTorch (CPU, fp64 /
+fp32) references of the same op, on seeded inputs including ragged edges.
+Every call goes through the C ABI (ctypes) -- no torch compute on the device."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def N():
+    from projects.mmdet3d_plugin import native
+    native.lib()
+    return native
+
+
+def _rt(x, dt):
+    return x.to(dt).to(torch.float64)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,N_,K", [(900, 256, 256), (130, 768, 512), (2000, 3072, 256), (64, 1024, 192)])
+def test_gemm_plain(N, dev, dt, M, N_, K):
+    g = torch.Generator().manual_seed(M + N_ + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N_, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N_, generator=g)
+    R = torch.randn(M, N_, generator=g)
+    C = torch.empty(M, N_, device=dev)
+    N.gemm(A.to(dev), W.to(dt).to(dev), C, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_, bias=b.to(dev), relu=True,
+           R=R.to(dev), ldr=N_)
+    ref = torch.relu(_rt(A, dt) @ _rt(W, dt).T + b.double()) + R.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    tol = 1e-4 if dt == torch.float32 else 5e-3
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_pos_add_headsplit(N, dev, dt):
+    g = torch.Generator().manual_seed(3)
+    B, S, C, K = 2, 300, 768, 256
+    A = torch.randn(B * S, K, generator=g)
+    A2 = torch.randn(B * S, K, generator=g)
+    W = torch.randn(C, K, generator=g) / 16
+    bias = torch.randn(C, generator=g)
+    out_dt = torch.float16 if dt == torch.float32 else torch.bfloat16
+    Y = torch.empty(B * 3 * 256 * S, dtype=out_dt, device=dev)
+    N.gemm(A.to(dev), W.to(dt).to(dev), Y, M=B * S, N=C, K=K, lda=K, ldw=K, ldc=0, bias=bias.to(dev),
+           A2=A2.to(dev), lda2=K, a2_cols=512, headsplit_rows=S)
+    Aeff = torch.cat([A + A2, A], 0)
+    full = (_rt(Aeff.float(), dt) @ _rt(W, dt).T + bias.double())
+    ref_qk = full[:B * S, :512]
+    ref_v = full[B * S:, 512:]
+    ref = torch.cat([ref_qk, ref_v], 1).view(B, S, 24, 32).permute(0, 2, 1, 3).reshape(-1)
+    got = Y.cpu().double()
+    rel = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_conv3x3(N, dev, dt):
+    g = torch.Generator().manual_seed(5)
+    B, Cin, H, W, Cout = 2, 64, 13, 17, 128
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / 24
+    b = torch.randn(Cout, generator=g)
+    xin = torch.empty(B * H * W, Cin, dtype=dt if dt != torch.float32 else torch.float32, device=dev)
+    N.nchw_to_rows(x.to(dev), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).to(dt).to(dev).contiguous()
+    Nk = H * W + 5   # rows per batch in the destination (leaves a gap, as in the fusion memory)
+    out = torch.full((B * Nk, Cout), float("nan"), device=dev)
+    N.gemm(xin, wp, out, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout, bias=b.to(dev), relu=True,
+           a_mode=N.A_CONV3X3, conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin, c_bstride=Nk * Cout)
+    ref = torch.relu(torch.nn.functional.conv2d(_rt(x, dt), _rt(w, dt), b.double(), padding=1))
+    ref = ref.flatten(2).permute(0, 2, 1)
+    got = out.view(B, Nk, Cout)[:, :H * W].cpu().double()
+    tol = 1e-4 if dt == torch.float32 else 5e-3
+    assert (got - ref).abs().max().item() < tol
+    assert torch.isnan(out.view(B, Nk, Cout)[:, H * W:]).all(), "conv wrote outside its rows"
+
+
+def test_gemm_conv1d3_grouped(N, dev):
+    g = torch.Generator().manual_seed(6)
+    L, B, Nq, C, O = 3, 2, 37, 256, 128
+    x = torch.randn(L, B * Nq, C, generator=g)
+    w = torch.randn(L * O, C, 3, generator=g) / 30
+    wp = w.view(L, O, C, 3).permute(0, 1, 3, 2).reshape(L, O, 3 * C).contiguous()
+    out = torch.empty(L, B * Nq, O, device=dev)
+    N.gemm(x.to(dev), wp.to(dev), out, M=B * Nq, N=O, K=3 * C, lda=C, ldw=3 * C, ldc=O, batch=L,
+           a_bstride=B * Nq * C, w_bstride=O * 3 * C, c_bstride=B * Nq * O, a_mode=N.A_CONV1D3, seg_len=Nq)
+    xin = x.view(L, B, Nq, C).permute(1, 0, 3, 2).reshape(B, L * C, Nq).double()
+    ref = torch.nn.functional.conv1d(xin, w.double(), padding=1, groups=L)        # [B, L*O, Nq]
+    ref = ref.view(B, L, O, Nq).permute(1, 0, 3, 2).reshape(L, B * Nq, O)
+    assert (out.cpu().double() - ref).abs().max().item() < 1e-4
+
+
+def _attn_ref(q, k, v, scale):
+    s = (q.double() @ k.double().transpose(-1, -2)) * scale
+    return torch.softmax(s, -1) @ v.double()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,H,Nq,Nk,splits", [(1, 8, 900, 32400, 0), (2, 8, 130, 1000, 0), (1, 2, 33, 65, 1),
+                                              (1, 8, 900, 900, 0), (1, 1, 1, 1, 1), (2, 3, 200, 4097, 3)])
+def test_attention(N, dev, dt, B, H, Nq, Nk, splits):
+    g = torch.Generator().manual_seed(B * 1000 + Nk)
+    q = (torch.randn(B, H, Nq, 32, generator=g) * 1.5).to(dt)
+    k = (torch.randn(B, H, Nk, 32, generator=g) * 1.5).to(dt)
+    v = torch.randn(B, H, Nk, 32, generator=g).to(dt)
+    O = torch.empty(B, Nq, H * 32, device=dev)
+    N.attention(q.to(dev), k.to(dev), v.to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk,
+                q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
+                kv_splits=splits)
+    ref = _attn_ref(q, k, v, 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
+    err = (O.cpu().double() - ref).abs().max().item()
+    tol = {torch.float32: 2e-5, torch.float16: 3e-3, torch.bfloat16: 2e-2}[dt]
+    assert err < tol, err
+
+
+def test_attention_spike_rescale(N, dev):
+    """Force the online-softmax running max to jump late (rule 26)."""
+    B, H, Nq, Nk = 1, 1, 64, 2048
+    g = torch.Generator().manual_seed(11)
+    q = torch.randn(B, H, Nq, 32, generator=g).half()
+    k = (torch.randn(B, H, Nk, 32, generator=g) * 0.1).half()
+    k[0, 0, 1900] = q[0, 0, 5] * 4          # spike for query 5 in a late tile
+    v = torch.randn(B, H, Nk, 32, generator=g).half()
+    for splits in (1, 4):
+        O = torch.empty(B, Nq, 32, device=dev)
+        N.attention(q.to(dev), k.to(dev), v.to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * 32, Nq * 32, 32),
+                    k_strides=(Nk * 32, Nk * 32, 32), v_strides=(Nk * 32, Nk * 32, 32), o_strides=(Nq * 32, 32),
+                    scale=1 / math.sqrt(32), kv_splits=splits)
+        ref = _attn_ref(q, k, v, 1 / math.sqrt(32))[0].transpose(0, 1).reshape(Nq, 32)
+        assert (O.cpu().double()[0] - ref).abs().max().item() < 3e-3
+
+
+def test_attention_seq_first_strides(N, dev):
+    """sequence-first [S, B, C] layout via strides (module-level API path)."""
+    B, H, S = 2, 8, 100
+    C = H * 32
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(S, B, C, generator=g).half()
+    O = torch.empty(S, B, C, device=dev)
+    xd = x.to(dev)
+    N.attention(xd, xd, xd, O, B=B, H=H, Nq=S, Nk=S, q_strides=(C, 32, B * C), k_strides=(C, 32, B * C),
+                v_strides=(C, 32, B * C), o_strides=(C, B * C), scale=0.2)
+    xb = x.permute(1, 0, 2).reshape(B, S, H, 32).permute(0, 2, 1, 3)
+    ref = _attn_ref(xb, xb, xb, 0.2).permute(2, 0, 1, 3).reshape(S, B, C)
+    assert (O.cpu().double() - ref).abs().max().item() < 3e-3
+
+
+def test_layernorm_fused_post(N, dev):
+    g = torch.Generator().manual_seed(4)
+    rows, C = 333, 256
+    x = torch.randn(rows, C, generator=g) * 3 + 1
+    w, b = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    w2, b2 = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    prev = torch.randn(rows, C, generator=g)
+    x[7, 3] = float("inf")
+    Y = torch.empty(rows, C, device=dev)
+    Y2 = prev.clone().to(dev)
+    N.layernorm(x.to(dev), w.to(dev), b.to(dev), Y, rows=rows, C=C, ldx=C, ldy=C, W2=w2.to(dev), B2=b2.to(dev),
+                Y2=Y2, ldy2=C, flags2=N.LN_NAN_TO_NUM | N.LN_MAX_INTO)
+    F = torch.nn.functional
+    r1 = F.layer_norm(x, (C,), w, b, 1e-5)
+    r2 = torch.maximum(torch.nan_to_num(F.layer_norm(r1, (C,), w2, b2, 1e-5)), prev)
+    ok = torch.isfinite(r1).all(1)
+    assert (Y.cpu()[ok] - r1[ok]).abs().max().item() < 1e-4
+    assert torch.isfinite(Y2.cpu()).all()
+    assert (Y2.cpu()[ok] - r2[ok]).abs().max().item() < 1e-4
+
+
+def test_pos2embed_kat(N, dev):
+    """SURVEY 8(a) row a1 KAT: (x, y) = (0.4963, 0.7682), F = 256."""
+    pos = torch.tensor([[0.4963, 0.7682]], device=dev)
+    out = torch.empty(1, 512, device=dev)
+    N.pos2embed(pos, out, n=1, F=256)
+    exp = [math.sin(2 * math.pi * 0.7682), math.cos(2 * math.pi * 0.7682),
+           math.sin(2 * math.pi * 0.7682 / 1.0078125), math.cos(2 * math.pi * 0.7682 / 1.0078125)]
+    assert np.allclose(out[0, :4].cpu().numpy(), exp, atol=2e-5)
+    assert abs(out[0, 256].item() - math.sin(2 * math.pi * 0.4963)) < 2e-5
+
+
+def test_voxelize_bitexact(N, dev):
+    """Scatter-mean vs the C restatement: bit-exact voxel sets and means,
+    including an overfull voxel, out-of-range points and the voxel budget."""
+    import ctypes
+    import os
+    from conftest import ROOT
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libvoxel_oracle.so"))
+    g = torch.Generator().manual_seed(9)
+    pc = [-54.0, -54.0, -5.0, 54.0, 54.0, 3.0]
+    vs = [0.075, 0.075, 0.2]
+    grid = [1440, 1440, 40]
+    for N_pts, max_vox, dense in ((30000, 160000, False), (5000, 1000, True), (1, 10, False)):
+        lo, hi = torch.tensor(pc[:3]) - 1.0, torch.tensor(pc[3:]) + 1.0
+        xyz = lo + torch.rand(N_pts, 3, generator=g) * (hi - lo)
+        if dense:   # pile points into a few voxels -> overfull voxels
+            xyz[: N_pts // 2] = torch.tensor([1.01, 2.02, 0.05]) + torch.rand(N_pts // 2, 3, generator=g) * 0.1
+        pts = torch.cat([xyz, torch.rand(N_pts, 2, generator=g)], 1).contiguous()
+        vox, coors, num, means, nvox = N.voxelize(pts.to(dev), voxel_size=vs, coors_range=pc, grid=grid,
+                                                  max_points=10, max_voxels=max_vox, nfeat_mean=5)
+        M = int(nvox.item())
+        rv = np.zeros((max_vox, 10, 5), np.float32)
+        rc = np.zeros((max_vox, 3), np.int32)
+        rn = np.zeros((max_vox,), np.int32)
+        rm = np.zeros((max_vox, 5), np.float32)
+        fp = ctypes.POINTER(ctypes.c_float)
+        ip = ctypes.POINTER(ctypes.c_int)
+        pn = pts.numpy()
+        Mr = lib.cmt_oracle_voxelize(pn.ctypes.data_as(fp), N_pts, 5, np.array(vs, np.float32).ctypes.data_as(fp),
+                                     np.array(pc, np.float32).ctypes.data_as(fp),
+                                     np.array(grid, np.int32).ctypes.data_as(ip), 10, max_vox, 5,
+                                     rv.ctypes.data_as(fp), rc.ctypes.data_as(ip), rn.ctypes.data_as(ip),
+                                     rm.ctypes.data_as(fp))
+        assert M == Mr
+        assert np.array_equal(coors[:M].cpu().numpy(), rc[:M])
+        assert np.array_equal(num[:M].cpu().numpy(), rn[:M])
+        assert np.array_equal(vox[:M].cpu().numpy(), rv[:M])
+        assert np.array_equal(means[:M].cpu().numpy(), rm[:M])

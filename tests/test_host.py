@@ -1,0 +1,148 @@
+"""Host-side logic on CPU: drop-in registry/config surface, state_dict layout,
+the C-ABI library's exports, and the no-fallback contract."""
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+PKG = os.path.join(ROOT, "cmt-cooperative-perception_amd")
+
+
+def test_registry_has_reference_type_names():
+    import projects.mmdet3d_plugin as P
+    for name in ("CmtHead", "CmtLidarHead", "CmtImageHead", "CmtHeadCoop", "CmtLidarHeadCoop", "CmtImageHeadCoop",
+                 "SeparateTaskHead"):
+        assert name in P.HEADS
+    for name in ("CmtTransformer", "CmtLidarTransformer", "CmtImageTransformer"):
+        assert name in P.TRANSFORMER
+    for name in ("PETRMultiheadFlashAttention", "MultiheadAttention", "PETRMultiheadAttention"):
+        assert name in P.ATTENTION
+    assert "PETRTransformerDecoder" in P.TRANSFORMER_LAYER_SEQUENCE
+    assert "PETRTransformerDecoderLayer" in P.TRANSFORMER_LAYER
+    assert "MultiTaskBBoxCoder" in P.BBOX_CODERS
+
+
+@pytest.mark.parametrize("name", ["cmt_lidar_nus", "cmt_fusion_nus", "cmtcoop_fusion_tumtraf", "cmtcoop_lidar_tumtraf"])
+def test_build_heads_from_configs(name):
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head(name, num_query=900)
+    n = sum(p.numel() for p in head.parameters())
+    # 8.76 M (fusion, k=1, with rv_embedding) / 9.50 M (LiDAR, k=3, no rv_embedding)
+    expect = 9.50e6 if "lidar" in name else 8.76e6
+    assert abs(n - expect) / expect < 0.01, n
+
+
+def test_state_dict_keys_match_reference_layout():
+    """mmcv module naming, e.g. convert_cmtcoop_checkpoints.py:188-193 prefixes."""
+    from projects.mmdet3d_plugin import synthetic as S
+    head, _, _ = S.build_synthetic_head("cmt_fusion_nus", num_query=900, jitter=False)
+    keys = set(head.state_dict().keys())
+    must = [
+        "shared_conv.conv.weight", "shared_conv.bn.weight", "shared_conv.bn.running_mean", "reference_points.weight",
+        "bev_embedding.0.weight", "bev_embedding.2.bias", "rv_embedding.0.weight", "rv_embedding.2.weight",
+        "transformer.decoder.layers.0.attentions.0.attn.in_proj_weight",
+        "transformer.decoder.layers.0.attentions.0.attn.out_proj.weight",
+        "transformer.decoder.layers.5.attentions.1.attn.in_proj_weight",
+        "transformer.decoder.layers.5.attentions.1.attn.in_proj_bias",
+        "transformer.decoder.layers.5.attentions.1.attn.out_proj.bias",
+        "transformer.decoder.layers.3.ffns.0.layers.0.0.weight", "transformer.decoder.layers.3.ffns.0.layers.1.bias",
+        "transformer.decoder.layers.2.norms.2.weight", "transformer.decoder.post_norm.weight",
+        "task_heads.0.center.0.weight", "task_heads.0.center.1.weight", "task_heads.0.cls_logits.3.bias",
+    ]
+    for k in must:
+        assert k in keys, k
+    assert head.transformer.decoder.layers[0].attentions[1].attn.in_proj_weight.shape == (768, 256)
+    assert head.task_heads[0].cls_logits[3].weight.shape == (6 * 10, 64, 1)
+    assert torch.allclose(head.task_heads[0].cls_logits[3].bias, torch.full((60,), -2.19))
+
+
+def test_lidar_head_has_no_rv_embedding_and_image_head_no_shared_conv():
+    from projects.mmdet3d_plugin import build_head
+    from projects.mmdet3d_plugin import synthetic as S
+    h, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=16, num_layers=1)
+    assert h.rv_embedding is None and not any(k.startswith("rv_embedding") for k in h.state_dict())
+    cfg, _ = S.make_head_cfg("cmt_fusion_nus", num_query=16, num_layers=1, head_type="CmtImageHead")
+    cfg["transformer"]["type"] = "CmtImageTransformer"
+    h2 = build_head(cfg)
+    assert h2.shared_conv is None
+
+
+def test_config_loader_non_executing(tmp_path):
+    from projects.mmdet3d_plugin.config import ConfigError, load_config, loads_config
+    c = load_config(os.path.join(PKG, "projects", "configs", "cmt_fusion_nus.py"))
+    assert c["head_type"] == "CmtHead" and c["point_cloud_range"][3] == 54.0
+    env = loads_config("a = [1, 2]\nb = dict(x=len(a), y=a[1] * 2, z='p' + '/q', t=(1, 2))\n")
+    assert env["b"] == {"x": 2, "y": 4, "z": "p/q", "t": (1, 2)}
+    for bad in ("import os\n", "a = open('x')\n", "a = __import__('os')\n", "def f():\n  pass\n", "a = b\n"):
+        with pytest.raises(ConfigError):
+            loads_config(bad)
+
+
+def _declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "cmt_hip.h")).read()
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(cmt_\w+)\s*\(", hdr, re.M)))
+
+
+def test_c_abi_exports_every_declared_symbol():
+    from projects.mmdet3d_plugin import native
+    L = native.lib()
+    syms = _declared_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert L.cmt_abi_version() == 1
+
+
+def test_c_abi_argument_errors_without_device():
+    """Argument checks run before any launch and report through cmt_last_error."""
+    import ctypes
+    from projects.mmdet3d_plugin import native
+    L = native.lib()
+    g = native.GemmArgs()
+    g.M, g.N, g.K, g.batch = 10, 60, 32, 1          # N not a multiple of 64
+    rc = L.cmt_gemm(ctypes.byref(g), None)
+    assert rc == 1001 and b"multiple of 64" in L.cmt_last_error()
+    a = native.AttnArgs()
+    a.B, a.H, a.Nq, a.Nk, a.dtype = 1, 1, 1, 1, 7
+    assert L.cmt_attn_fwd(ctypes.byref(a), None) == 1001
+    assert L.cmt_voxelize_workspace_bytes(30000, 160000) > 0
+
+
+def test_native_ops_refuse_cpu_tensors():
+    """No CPU fallback: the product path raises on host tensors."""
+    from projects.mmdet3d_plugin import native
+    x = torch.zeros(4, 256)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        native.layernorm(x, torch.ones(256), torch.zeros(256), x, rows=4, C=256, ldx=256, ldy=256)
+
+
+def test_head_forward_refuses_cpu():
+    from projects.mmdet3d_plugin import synthetic as S
+    head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=16, num_layers=1, grid_size=[128, 128, 40])
+    with pytest.raises(RuntimeError):
+        head([torch.zeros(1, 512, 16, 16)], None, [dict()])
+
+
+def test_training_forward_not_silently_supported():
+    from projects.mmdet3d_plugin import synthetic as S
+    head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=16, num_layers=1, grid_size=[128, 128, 40])
+    head.train()
+    with pytest.raises(NotImplementedError):
+        head([torch.zeros(1, 512, 16, 16)], None, [dict()])
+
+
+def test_pack_cache_invalidates_on_weight_change():
+    from projects.mmdet3d_plugin.models.utils.packing import PackCache
+    pc = PackCache()
+    w = torch.nn.Parameter(torch.ones(4))
+    calls = []
+    pc.get("a", [w], "x", lambda: calls.append(1) or w.detach().clone())
+    pc.get("a", [w], "x", lambda: calls.append(1) or w.detach().clone())
+    assert len(calls) == 1
+    with torch.no_grad():
+        w.add_(1)
+    pc.get("a", [w], "x", lambda: calls.append(1) or w.detach().clone())
+    assert len(calls) == 2
