@@ -23,7 +23,7 @@ namespace {
 
 constexpr int KT = 64;     // keys per tile
 constexpr int QW = 32;     // queries per wave
-constexpr int NW = 4;      // waves per workgroup
+constexpr int NW = 4;      // waves per workgroup (f32 kernel; the f16/bf16 kernel takes it as a template arg)
 constexpr int QB = QW * NW;
 constexpr int D = 32;
 
@@ -40,9 +40,91 @@ struct AttnKParams {
     int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnKParams p) {
+// One 64-key tile for one wave: S^T = K Q^T, online softmax, O^T += V^T P^T.
+// MASK = keys >= Nk in this tile are set to -inf (only the ragged last tile).
+template <typename T, bool MASK>
+__device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T* __restrict__ Vt,
+                                               const typename mfma_traits<T>::frag (&qf)[2], f32x16& o,
+                                               float& m_run, float& l_run, float c, int key0, int Nk, int lane) {
     typedef typename mfma_traits<T>::frag frag;
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+        const int row = kb * 32 + lr;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const frag kf = *(const frag*)(&Kt[row * D + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
+            s[kb] = mfma_traits<T>::mma(kf, qf[ks], s[kb]);
+        }
+    }
+    if (MASK) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (key >= Nk) s[kb][r] = -__builtin_inff();
+            }
+    }
+    // tile max (two v_max3 chains), then across the lane pair holding the same query
+    float m0 = vmax(s[0][0], s[0][1]), m1 = vmax(s[1][0], s[1][1]);
+#pragma unroll
+    for (int r = 2; r < 16; r += 2) {
+        m0 = vmax3(m0, s[0][r], s[0][r + 1]);
+        m1 = vmax3(m1, s[1][r], s[1][r + 1]);
+    }
+    const float mt = pair_max(vmax(m0, m1));
+    const float m_new = vmax(m_run, mt);
+    // exact lazy rescale: alpha == 1 for every lane whose max did not grow
+    if (__any(m_new > m_run)) {
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+        l_run *= alpha;
+        m_run = m_new;
+    }
+    const float mc = m_run * c;
+    float ls0 = 0.f, ls1 = 0.f;
+    frag pf[2][2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float e0 = __builtin_amdgcn_exp2f(fmaf(s[0][r], c, -mc));
+        const float e1 = __builtin_amdgcn_exp2f(fmaf(s[1][r], c, -mc));
+        ls0 += e0;
+        ls1 += e1;
+        pf[0][r >> 3][r & 7] = (T)e0;
+        pf[1][r >> 3][r & 7] = (T)e1;
+    }
+    l_run += ls0 + ls1;
+    // V^T fragments by transposed LDS reads: lane 4q+p of each 16-lane group
+    // addresses row (r0 + q), columns dgrp + 4p .. +3
+    const int dgrp = 16 * ((lane >> 4) & 1);
+    const int tq = (lane & 15) >> 2;
+    const int tp = lane & 3;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            const int r0 = kb * 32 + 16 * ss + 4 * lh + tq;
+            const T* base0 = &Vt[r0 * D + dgrp + 4 * tp];
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)(base0 + 8 * D));
+            s16x8 vv;
+            vv[0] = lo[0]; vv[1] = lo[1]; vv[2] = lo[2]; vv[3] = lo[3];
+            vv[4] = hi[0]; vv[5] = hi[1]; vv[6] = hi[2]; vv[7] = hi[3];
+            o = mfma_traits<T>::mma(__builtin_bit_cast(frag, vv), pf[kb][ss], o);
+        }
+}
+
+template <typename T, int NWAVES>
+__global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    constexpr int NTH = NWAVES * 64;
+    constexpr int CHUNKS = KT * D / 8;            // 16-byte chunks per K (or V) tile = 256
     __shared__ __attribute__((aligned(16))) T Ks[2][KT * D];
     __shared__ __attribute__((aligned(16))) T Vs[2][KT * D];
 
@@ -60,10 +142,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnKParams p) {
     const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
     const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
 
-    const int q0 = blockIdx.x * QB + wave * QW;
-    const int q = q0 + lr;
+    const int q = blockIdx.x * (NWAVES * QW) + wave * QW + lr;
     const int qc = q < p.Nq ? q : p.Nq - 1;
-
     // Q^T fragments (B operand): B[k = 8*lh + j][col = q] = Q[q][16*ks + 8*lh + j]
     frag qf[2];
     qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
@@ -72,24 +152,38 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnKParams p) {
     const int ntiles = (p.Nk + KT - 1) / KT;
     const int t_begin = split * p.tiles_per_split;
     const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+    const bool ragged = (p.Nk % KT) != 0;
 
-    // staging: thread -> (key row, 16-byte chunk) of the K and V tiles
-    const int srow = tid >> 2;
-    const int schunk = tid & 3;
-    frag kreg, vreg;
+    // staging: 2 x 256 chunks (K then V) over NTH threads
+    constexpr int PER = 2 * CHUNKS / NTH;
+    frag reg[PER];
     auto load_tile = [&](int t) {
-        const int key = t * KT + srow;
-        if (key < p.Nk) {
-            kreg = *(const frag*)(Kb + (int64_t)key * p.k_rs + schunk * 8);
-            vreg = *(const frag*)(Vb + (int64_t)key * p.v_rs + schunk * 8);
-        } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { kreg[j] = (T)0.f; vreg[j] = (T)0.f; }
+        for (int i = 0; i < PER; ++i) {
+            const int idx = tid + NTH * i;
+            const int kv = idx / CHUNKS;                   // 0 = K, 1 = V
+            const int rem = idx - kv * CHUNKS;
+            const int row = rem >> 2, ch = rem & 3;
+            const int key = t * KT + row;
+            const T* src = (kv == 0 ? Kb + (int64_t)key * p.k_rs : Vb + (int64_t)key * p.v_rs) + ch * 8;
+            if (key < p.Nk) {
+                reg[i] = *(const frag*)src;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) reg[i][j] = (T)0.f;
+            }
         }
     };
     auto store_tile = [&](int buf) {
-        *(frag*)(&Ks[buf][srow * D + 8 * (schunk ^ ((srow >> 2) & 3))]) = kreg;
-        *(frag*)(&Vs[buf][srow * D + 8 * schunk]) = vreg;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int idx = tid + NTH * i;
+            const int kv = idx / CHUNKS;
+            const int rem = idx - kv * CHUNKS;
+            const int row = rem >> 2, ch = rem & 3;
+            if (kv == 0) *(frag*)(&Ks[buf][row * D + 8 * (ch ^ ((row >> 2) & 3))]) = reg[i];
+            else *(frag*)(&Vs[buf][row * D + 8 * ch]) = reg[i];
+        }
     };
 
     f32x16 o;
@@ -107,75 +201,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnKParams p) {
     for (int t = t_begin; t < t_end; ++t) {
         const int cur = (t - t_begin) & 1;
         if (t + 1 < t_end) load_tile(t + 1);
-
-        // ---- S^T = K Q^T for the two 32-key blocks --------------------------
-        f32x16 s[2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
-            const int row = kb * 32 + lr;
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                frag kf = *(const frag*)(&Ks[cur][row * D + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
-                s[kb] = mfma_traits<T>::mma(kf, qf[ks], s[kb]);
-            }
-        }
-        // ---- mask the ragged tail -------------------------------------------
-        if ((t + 1) * KT > p.Nk) {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    int key = t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    if (key >= p.Nk) s[kb][r] = -__builtin_inff();
-                }
-        }
-        // ---- online softmax ---------------------------------------------------
-        float mt = s[0][0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) mt = fmaxf(mt, s[0][r]);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[1][r]);
-        mt = fmaxf(mt, __shfl_xor(mt, 32));
-        const float m_new = fmaxf(m_run, mt);
-        const float alpha = exp2f((m_run - m_new) * c);
-        const float mc = m_new * c;
-        float ls = 0.f;
-        frag pf[2][2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float e = exp2f(fmaf(s[kb][r], c, -mc));
-                ls += e;
-                pf[kb][r >> 3][r & 7] = (T)e;
-            }
-        l_run = l_run * alpha + ls;
-        m_run = m_new;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] *= alpha;
-
-        // ---- O^T += V^T P^T ----------------------------------------------------
-        const int dgrp = 16 * ((lane >> 4) & 1);
-        const int tq = (lane & 15) >> 2;
-        const int tp = lane & 3;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                const int r0 = kb * 32 + 16 * ss + 4 * lh + tq;
-                const T* base0 = &Vs[cur][r0 * D + dgrp + 4 * tp];
-                const T* base1 = base0 + 8 * D;
-                s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base0);
-                s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base1);
-                s16x8 vv;
-                vv[0] = lo[0]; vv[1] = lo[1]; vv[2] = lo[2]; vv[3] = lo[3];
-                vv[4] = hi[0]; vv[5] = hi[1]; vv[6] = hi[2]; vv[7] = hi[3];
-                frag vf = __builtin_bit_cast(frag, vv);
-                o = mfma_traits<T>::mma(vf, pf[kb][ss], o);
-            }
-
+        if (ragged && t == ntiles - 1)
+            attn_tile_lowp<T, true>(Ks[cur], Vs[cur], qf, o, m_run, l_run, c, t * KT, p.Nk, lane);
+        else
+            attn_tile_lowp<T, false>(Ks[cur], Vs[cur], qf, o, m_run, l_run, c, t * KT, p.Nk, lane);
         if (t + 1 < t_end) store_tile(cur ^ 1);
         __syncthreads();
     }
@@ -370,41 +399,58 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(AttnKParams p) {
     }
 }
 
-// One thread per (b, h, q, d): merge the kv-split partials.
-__global__ void attn_combine_kernel(AttnKParams p) {
+// Merge the kv-split partials: 8 threads per (b, h, q), each owning 4 of the
+// 32 head dims (16-byte loads of every split's partial row; the split maxima
+// and row sums are read once per thread).
+__global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)p.B * p.H * p.Nq * D;
-    if (idx >= total) return;
-    const int d = idx & (D - 1);
-    const int64_t bhq = idx >> 5;
-    const int q = bhq % p.Nq;
+    const int64_t rows = (int64_t)p.B * p.H * p.Nq;
+    if (idx >= rows * 8) return;
+    const int d4 = (int)(idx & 7) * 4;
+    const int64_t bhq = idx >> 3;
+    const int q = (int)(bhq % p.Nq);
     const int64_t bh = bhq / p.Nq;
-    const int h = bh % p.H;
-    const int b = bh / p.H;
-    const int64_t stride = (int64_t)p.B * p.H * p.Nq;
+    const int h = (int)(bh % p.H);
+    const int b = (int)(bh / p.H);
     float M = -__builtin_inff();
-    for (int s = 0; s < p.splits; ++s) M = fmaxf(M, p.Mp[s * stride + bhq]);
-    float num = 0.f, den = 0.f;
+    for (int s = 0; s < p.splits; ++s) M = fmaxf(M, p.Mp[s * rows + bhq]);
+    f32x4 num = {0.f, 0.f, 0.f, 0.f};
+    float den = 0.f;
     for (int s = 0; s < p.splits; ++s) {
-        const float ms = p.Mp[s * stride + bhq];
+        const float ms = p.Mp[s * rows + bhq];
         if (ms == -__builtin_inff()) continue;
-        const float w = exp2f((ms - M) * p.c);
-        num += w * p.Op[(s * stride + bhq) * D + d];
-        den += w * p.Lp[s * stride + bhq];
+        const float w = __builtin_amdgcn_exp2f((ms - M) * p.c);
+        num += w * *(const f32x4*)(p.Op + (s * rows + bhq) * D + d4);
+        den += w * p.Lp[s * rows + bhq];
     }
-    float r = num / den;
-    if (p.round_out == CMT_F16) r = (float)(f16_t)r;
-    else if (p.round_out == CMT_BF16) r = (float)(bf16_t)r;
-    p.O[(int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D + d] = r;
+    const float inv = 1.f / den;
+    f32x4 r = num * inv;
+    if (p.round_out == CMT_F16) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = (float)(f16_t)r[j];
+    } else if (p.round_out == CMT_BF16) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = (float)(bf16_t)r[j];
+    }
+    *(f32x4*)(p.O + (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D + d4) = r;
+}
+
+// 8-wave workgroups (256 queries share each staged K/V tile) for long key
+// ranges; 4-wave ones otherwise.
+int lowp_waves(const cmt_attn_args& a) {
+    return (a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128) ? 8 : 4;
 }
 
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
     const int ntiles = (a.Nk + KT - 1) / KT;
-    const int base = cdiv(a.Nq, QB) * a.B * a.H;
+    const int qrows = a.dtype == CMT_F32 ? QB : lowp_waves(a) * QW;
+    const int base = cdiv(a.Nq, qrows) * a.B * a.H;
     int s = 1;
-    // aim for >= 1024 workgroups (4 per CU) while keeping >= 8 tiles per split
-    while (base * s < 1024 && ntiles / (2 * s) >= 8) s *= 2;
+    // aim for >= 1024 workgroups (4 per CU) while keeping >= 8 tiles per split;
+    // short key ranges (self-attention) split down to 2 tiles per split
+    const int min_tiles = ntiles >= 64 ? 8 : 2;
+    while (base * s < 1024 && ntiles / (2 * s) >= min_tiles) s *= 2;
     return s;
 }
 
@@ -454,13 +500,16 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         p.Lp = p.Mp + rows;
     }
     hipStream_t s = (hipStream_t)stream;
-    dim3 grid(cdiv(a.Nq, QB), a.B * a.H, splits);
-    if (a.dtype == CMT_F16) attn_fwd_kernel<f16_t><<<grid, 256, 0, s>>>(p);
-    else if (a.dtype == CMT_BF16) attn_fwd_kernel<bf16_t><<<grid, 256, 0, s>>>(p);
-    else attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
+    const int nw = lowp_waves(a);
+    dim3 grid(cdiv(a.Nq, a.dtype == CMT_F32 ? QB : nw * QW), a.B * a.H, splits);
+    if (a.dtype == CMT_F32) attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
+    else if (a.dtype == CMT_F16 && nw == 8) attn_fwd_kernel<f16_t, 8><<<grid, 512, 0, s>>>(p);
+    else if (a.dtype == CMT_F16) attn_fwd_kernel<f16_t, 4><<<grid, 256, 0, s>>>(p);
+    else if (nw == 8) attn_fwd_kernel<bf16_t, 8><<<grid, 512, 0, s>>>(p);
+    else attn_fwd_kernel<bf16_t, 4><<<grid, 256, 0, s>>>(p);
     int rc = cmt_check_launch("cmt_attn_fwd");
     if (rc || splits == 1) return rc;
-    const int64_t total = (int64_t)a.B * a.H * a.Nq * D;
+    const int64_t total = (int64_t)a.B * a.H * a.Nq * 8;
     attn_combine_kernel<<<(unsigned)cdiv64(total, 256), 256, 0, s>>>(p);
     return cmt_check_launch("cmt_attn_combine");
 }

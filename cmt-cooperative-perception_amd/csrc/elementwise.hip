@@ -283,40 +283,64 @@ struct TailParams {
     float* OUT;
 };
 
-__global__ void task_head_conv2_kernel(TailParams p) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)p.L * p.B * p.Nq * p.out_total;
-    if (idx >= total) return;
-    const int o = (int)(idx % p.out_total);
-    const int64_t lbq = idx / p.out_total;
-    const int q = (int)(lbq % p.Nq);
-    const int64_t lb = lbq / p.Nq;
-    const int b = (int)(lb % p.B);
-    const int l = (int)(lb / p.B);
-    const int hd = p.head_of[o];
+// One workgroup per (layer, 32-query block, batch): the hidden rows of the
+// block (+1 halo row each side for k = 3) and the layer's conv-2 weights are
+// staged in LDS once, then each thread produces (query, output) pairs.
+constexpr int TQ = 32;
+
+__global__ __launch_bounds__(256) void task_head_conv2_kernel(TailParams p) {
+    extern __shared__ __attribute__((aligned(16))) float tsm[];
+    const int l = blockIdx.x;
+    const int q0 = blockIdx.y * TQ;
+    const int b = blockIdx.z;
     const int width = p.nheads * p.hc;
-    const float* w = p.W2 + (((int64_t)l * p.out_total + o) * p.k) * p.hc;
-    float acc = p.B2[(int64_t)l * p.out_total + o];
     const int half = p.k >> 1;
-    for (int t = 0; t < p.k; ++t) {
-        const int qq = q + t - half;
-        if (qq < 0 || qq >= p.Nq) continue;
-        const float* g = p.G + (((int64_t)l * p.B + b) * p.Nq + qq) * width + hd * p.hc;
-        const float* wt = w + t * p.hc;
-        float s = 0.f;
-        for (int c = 0; c < p.hc; ++c) s = fmaf(wt[c], g[c], s);
-        acc += s;
+    const int nrows = TQ + 2 * half;
+    float* G = tsm;                                   // [nrows][width]
+    float* W = tsm + nrows * width;                   // [out_total][k][hc]
+    const float* Gsrc = p.G + ((int64_t)l * p.B + b) * p.Nq * width;
+    for (int i = threadIdx.x; i < nrows * width / 4; i += blockDim.x) {
+        const int r = (i * 4) / width, c = (i * 4) - r * width;
+        const int q = q0 - half + r;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (q >= 0 && q < p.Nq) v = *(const f32x4*)(Gsrc + (int64_t)q * width + c);
+        *(f32x4*)(G + r * width + c) = v;
     }
-    const int rel_c = o - p.center_col;
-    const int rel_h = o - p.height_col;
-    if (p.center_col >= 0 && rel_c >= 0 && rel_c < 2) {
-        const float rf = inv_sigmoid_dev(p.ref[((int64_t)b * p.Nq + q) * 3 + rel_c]);
-        acc = sigmoid_dev(acc + rf) * (p.pc[3 + rel_c] - p.pc[rel_c]) + p.pc[rel_c];
-    } else if (p.height_col >= 0 && rel_h == 0) {
-        const float rf = inv_sigmoid_dev(p.ref[((int64_t)b * p.Nq + q) * 3 + 2]);
-        acc = sigmoid_dev(acc + rf) * (p.pc[5] - p.pc[2]) + p.pc[2];
+    const int wsz = p.out_total * p.k * p.hc;
+    const float* Wsrc = p.W2 + (int64_t)l * wsz;
+    for (int i = threadIdx.x; i < wsz / 4; i += blockDim.x) *(f32x4*)(W + 4 * i) = *(const f32x4*)(Wsrc + 4 * i);
+    __syncthreads();
+    const int qi = threadIdx.x % TQ;
+    const int q = q0 + qi;
+    if (q >= p.Nq) return;
+    for (int o = threadIdx.x / TQ; o < p.out_total; o += blockDim.x / TQ) {
+        const int hd = p.head_of[o];
+        float acc = p.B2[(int64_t)l * p.out_total + o];
+        for (int t = 0; t < p.k; ++t) {
+            const float* g = G + (qi + t) * width + hd * p.hc;
+            const float* w = W + (o * p.k + t) * p.hc;
+            float s0 = 0.f, s1 = 0.f;
+            for (int c = 0; c < p.hc; c += 8) {
+                const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
+                const f32x4 w0 = *(const f32x4*)(w + c), w1 = *(const f32x4*)(w + c + 4);
+                s0 = fmaf(w0[0], g0[0], s0); s0 = fmaf(w0[1], g0[1], s0);
+                s0 = fmaf(w0[2], g0[2], s0); s0 = fmaf(w0[3], g0[3], s0);
+                s1 = fmaf(w1[0], g1[0], s1); s1 = fmaf(w1[1], g1[1], s1);
+                s1 = fmaf(w1[2], g1[2], s1); s1 = fmaf(w1[3], g1[3], s1);
+            }
+            acc += s0 + s1;
+        }
+        const int rel_c = o - p.center_col;
+        const int rel_h = o - p.height_col;
+        if (p.center_col >= 0 && rel_c >= 0 && rel_c < 2) {
+            const float rf = inv_sigmoid_dev(p.ref[((int64_t)b * p.Nq + q) * 3 + rel_c]);
+            acc = sigmoid_dev(acc + rf) * (p.pc[3 + rel_c] - p.pc[rel_c]) + p.pc[rel_c];
+        } else if (p.height_col >= 0 && rel_h == 0) {
+            const float rf = inv_sigmoid_dev(p.ref[((int64_t)b * p.Nq + q) * 3 + 2]);
+            acc = sigmoid_dev(acc + rf) * (p.pc[5] - p.pc[2]) + p.pc[2];
+        }
+        p.OUT[(((int64_t)l * p.B + b) * p.Nq + q) * p.out_total + o] = acc;
     }
-    p.OUT[idx] = acc;
 }
 
 inline unsigned nblocks(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -451,7 +475,10 @@ extern "C" int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nhe
         }
     }
     CMT_REQUIRE(o == out_total, "cmt_task_head_tail: head_out does not sum to out_total");
-    const int64_t total = (int64_t)L * B * Nq * out_total;
-    task_head_conv2_kernel<<<nblocks(total, 256), 256, 0, s>>>(p);
+    const int width = nheads * hc;
+    const size_t smem = sizeof(float) * ((size_t)(TQ + 2 * (k >> 1)) * width + (size_t)out_total * k * hc);
+    CMT_REQUIRE(smem <= 160 * 1024, "cmt_task_head_tail: head too wide for LDS staging");
+    dim3 g2(L, cdiv(Nq, TQ), B);
+    task_head_conv2_kernel<<<g2, 256, smem, s>>>(p);
     return cmt_check_launch("cmt_task_head_tail/conv2");
 }

@@ -87,13 +87,25 @@ __device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[B
     void* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
     const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
     const float* Rz = a.R ? a.R + (int64_t)z * a.r_bstride : nullptr;
+#pragma unroll
     for (int tn = 0; tn < BN / 64; ++tn) {
         const int col = n0 + wn * (BN / 2) + tn * 32 + col_l;
         const float bias = biasz ? biasz[col] : 0.f;
+#pragma unroll
         for (int tm = 0; tm < BM / 64; ++tm) {
+            // head-split addressing: one division per 32-row tile, the 32 rows
+            // cross at most one batch boundary when rows_per_batch >= 32
+            const int row0 = m0 + wm * (BM / 2) + tm * 32;
+            const int rpb = a.rows_per_batch;
+            int b0 = 0, rr0 = 0;
+            if (a.c_mode != CMT_C_ROWS) {
+                b0 = row0 / rpb;
+                rr0 = row0 - b0 * rpb;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int off = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int row = row0 + off;
                 if (row >= a.M) continue;
                 float v = acc[tm][tn][r] + bias;
                 if (a.relu) v = fmaxf(v, 0.f);
@@ -102,9 +114,13 @@ __device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[B
                 if (a.c_mode == CMT_C_ROWS) {
                     idx = (int64_t)row * a.ldc + col;
                 } else {
-                    const int rpb = a.rows_per_batch;
-                    const int b = row / rpb;
-                    const int rr = row - b * rpb;
+                    int b = b0, rr = rr0 + off;
+                    if (rpb >= 32) {
+                        if (rr >= rpb) { rr -= rpb; ++b; }
+                    } else {
+                        b = row / rpb;
+                        rr = row - b * rpb;
+                    }
                     idx = (((int64_t)b * (a.N >> 5) + (col >> 5)) * rpb + rr) * 32 + (col & 31);
                 }
                 store_out<float>(Cz, idx, a.c_dtype, v);
@@ -116,13 +132,23 @@ __device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[B
 // ---------------------------------------------------------------------------
 // f16 / bf16 compute
 // ---------------------------------------------------------------------------
-template <typename CT, int BM, int BN, int AMODE, bool A_F32>
+template <int CPR>
+__device__ __forceinline__ int swz(int row, int c) {
+    // 16-byte chunk permutation of an LDS row holding CPR chunks: the 16-lane
+    // groups of ds_read_b128 (rows {0-3,12-15,20-27} / {4-11,16-19,28-31} at a
+    // fixed chunk) land on 16 distinct bank slots for CPR = 4, 8, 16.
+    return c ^ ((row / (16 / CPR)) & (CPR - 1));
+}
+
+template <typename CT, int BM, int BN, int LBK, int AMODE, bool A_F32>
 __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
     typedef typename mfma_traits<CT>::frag frag;
-    constexpr int ACH = BM / 64;  // 16-byte chunks of A per thread per k-step
-    constexpr int BCH = BN / 64;
-    __shared__ __attribute__((aligned(16))) CT As[2][BM * BK];
-    __shared__ __attribute__((aligned(16))) CT Bs[2][BN * BK];
+    constexpr int CPR = LBK / 8;               // 16-byte chunks per LDS row
+    constexpr int ACH = BM * CPR / NT;         // A chunks staged per thread per k-step
+    constexpr int BCH = BN * CPR / NT;
+    static_assert(ACH >= 1 && BCH >= 1, "tile too small for the thread count");
+    __shared__ __attribute__((aligned(16))) CT As[2][BM * LBK];
+    __shared__ __attribute__((aligned(16))) CT Bs[2][BN * LBK];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -137,14 +163,8 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
     const bool use_a2 = (AMODE == CMT_A_ROWS) && a.A2 != nullptr && n0 < a.a2_cols;
 
     RowInfo ri[ACH];
-    int arow[ACH], achunk[ACH];
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-        int idx = tid + NT * i;
-        arow[i] = idx >> 2;
-        achunk[i] = idx & 3;
-        ri[i] = make_row_info<AMODE>(a, m0 + arow[i]);
-    }
+    for (int i = 0; i < ACH; ++i) ri[i] = make_row_info<AMODE>(a, m0 + (tid + NT * i) / CPR);
 
     frag areg[ACH];
     frag breg[BCH];
@@ -152,8 +172,10 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
     auto load_tiles = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < ACH; ++i) {
-            const int kk = k0 + achunk[i] * 8;
-            int64_t off = a_offset<AMODE>(a, ri[i], m0 + arow[i], kk);
+            const int idx = tid + NT * i;
+            const int row = idx / CPR, c = idx % CPR;
+            const int kk = k0 + c * 8;
+            const int64_t off = a_offset<AMODE>(a, ri[i], m0 + row, kk);
             if (off < 0) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) areg[i][j] = (CT)0.f;
@@ -162,7 +184,7 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
                 f32x4 v0 = *(const f32x4*)p;
                 f32x4 v1 = *(const f32x4*)(p + 4);
                 if (use_a2) {
-                    const float* p2 = a.A2 + (int64_t)(m0 + arow[i]) * a.lda2 + kk;
+                    const float* p2 = a.A2 + (int64_t)(m0 + row) * a.lda2 + kk;
                     v0 += *(const f32x4*)p2;
                     v1 += *(const f32x4*)(p2 + 4);
                 }
@@ -177,22 +199,23 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
         }
 #pragma unroll
         for (int i = 0; i < BCH; ++i) {
-            int idx = tid + NT * i;
-            int row = idx >> 2, c = idx & 3;
+            const int idx = tid + NT * i;
+            const int row = idx / CPR, c = idx % CPR;
             breg[i] = *(const frag*)(Wb + (int64_t)(n0 + row) * a.ldw + k0 + c * 8);
         }
     };
     auto store_tiles = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < ACH; ++i) {
-            int row = arow[i];
-            *(frag*)(&As[buf][row * BK + 8 * (achunk[i] ^ ((row >> 2) & 3))]) = areg[i];
+            const int idx = tid + NT * i;
+            const int row = idx / CPR, c = idx % CPR;
+            *(frag*)(&As[buf][row * LBK + 8 * swz<CPR>(row, c)]) = areg[i];
         }
 #pragma unroll
         for (int i = 0; i < BCH; ++i) {
-            int idx = tid + NT * i;
-            int row = idx >> 2, c = idx & 3;
-            *(frag*)(&Bs[buf][row * BK + 8 * (c ^ ((row >> 2) & 3))]) = breg[i];
+            const int idx = tid + NT * i;
+            const int row = idx / CPR, c = idx % CPR;
+            *(frag*)(&Bs[buf][row * LBK + 8 * swz<CPR>(row, c)]) = breg[i];
         }
     };
 
@@ -204,7 +227,7 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nk = a.K / BK;
+    const int nk = a.K / LBK;
     load_tiles(0);
     store_tiles(0);
     __syncthreads();
@@ -212,19 +235,19 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
     const int lh = lane >> 5;
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+        if (kt + 1 < nk) load_tiles((kt + 1) * LBK);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < LBK / 16; ++ks) {
             frag af[BM / 64], bfr[BN / 64];
 #pragma unroll
             for (int tm = 0; tm < BM / 64; ++tm) {
-                int row = wm * (BM / 2) + tm * 32 + lr;
-                af[tm] = *(const frag*)(&As[cur][row * BK + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
+                const int row = wm * (BM / 2) + tm * 32 + lr;
+                af[tm] = *(const frag*)(&As[cur][row * LBK + 8 * swz<CPR>(row, 2 * ks + lh)]);
             }
 #pragma unroll
             for (int tn = 0; tn < BN / 64; ++tn) {
-                int row = wn * (BN / 2) + tn * 32 + lr;
-                bfr[tn] = *(const frag*)(&Bs[cur][row * BK + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
+                const int row = wn * (BN / 2) + tn * 32 + lr;
+                bfr[tn] = *(const frag*)(&Bs[cur][row * LBK + 8 * swz<CPR>(row, 2 * ks + lh)]);
             }
 #pragma unroll
             for (int tm = 0; tm < BM / 64; ++tm)
@@ -342,17 +365,34 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(cmt_gemm_args a) {
     epilogue<BM, BN>(a, acc, m0, n0, wm, wn, lane);
 }
 
+template <int BM, int BN, int LBK, int AMODE>
+void launch_lowp(const cmt_gemm_args& a, dim3 grid, hipStream_t s) {
+    if constexpr (AMODE == CMT_A_CONV3X3) {
+        // the conv gather reads NHWC rows already in the compute dtype
+        if (a.w_dtype == CMT_BF16) gemm_lowp_kernel<bf16_t, BM, BN, LBK, AMODE, false><<<grid, NT, 0, s>>>(a);
+        else gemm_lowp_kernel<f16_t, BM, BN, LBK, AMODE, false><<<grid, NT, 0, s>>>(a);
+    } else {
+        if (a.w_dtype == CMT_BF16) {
+            if (a.a_dtype == CMT_F32) gemm_lowp_kernel<bf16_t, BM, BN, LBK, AMODE, true><<<grid, NT, 0, s>>>(a);
+            else gemm_lowp_kernel<bf16_t, BM, BN, LBK, AMODE, false><<<grid, NT, 0, s>>>(a);
+        } else {
+            if (a.a_dtype == CMT_F32) gemm_lowp_kernel<f16_t, BM, BN, LBK, AMODE, true><<<grid, NT, 0, s>>>(a);
+            else gemm_lowp_kernel<f16_t, BM, BN, LBK, AMODE, false><<<grid, NT, 0, s>>>(a);
+        }
+    }
+}
+
 template <int BM, int BN, int AMODE>
 int launch_mode(const cmt_gemm_args& a, hipStream_t s) {
     dim3 grid(a.N / BN, cdiv(a.M, BM), a.batch);
     if (a.w_dtype == CMT_F32) {
         gemm_f32_kernel<BM, BN, AMODE><<<grid, NT, 0, s>>>(a);
-    } else if (a.w_dtype == CMT_BF16) {
-        if (a.a_dtype == CMT_F32) gemm_lowp_kernel<bf16_t, BM, BN, AMODE, true><<<grid, NT, 0, s>>>(a);
-        else gemm_lowp_kernel<bf16_t, BM, BN, AMODE, false><<<grid, NT, 0, s>>>(a);
     } else {
-        if (a.a_dtype == CMT_F32) gemm_lowp_kernel<f16_t, BM, BN, AMODE, true><<<grid, NT, 0, s>>>(a);
-        else gemm_lowp_kernel<f16_t, BM, BN, AMODE, false><<<grid, NT, 0, s>>>(a);
+        // deepest K step that divides K (and, for the gathered modes, the per-tap channel count)
+        const int kdiv = AMODE == CMT_A_CONV3X3 ? a.conv_c : (AMODE == CMT_A_CONV1D3 ? a.K / 3 : a.K);
+        if (BM == 64 && kdiv % 128 == 0) launch_lowp<BM, BN, 128, AMODE>(a, grid, s);
+        else if (kdiv % 64 == 0) launch_lowp<BM, BN, 64, AMODE>(a, grid, s);
+        else launch_lowp<BM, BN, 32, AMODE>(a, grid, s);
     }
     return cmt_check_launch("cmt_gemm");
 }
@@ -377,6 +417,8 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
     CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16, "cmt_gemm: bad w_dtype");
     CMT_REQUIRE(a.a_dtype == CMT_F32 || a.a_dtype == a.w_dtype, "cmt_gemm: A must be f32 or the compute dtype");
+    CMT_REQUIRE(a.a_mode != CMT_A_CONV3X3 || a.a_dtype == a.w_dtype,
+                "cmt_gemm: the conv3x3 gather needs A in the compute dtype");
     CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16, "cmt_gemm: bad c_dtype");
     CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0, "cmt_gemm: lda/ldw must be multiples of 8 elements");
     CMT_REQUIRE(a.A2 == nullptr || (a.a_mode == CMT_A_ROWS && a.a_dtype == CMT_F32 && a.lda2 % 4 == 0 &&
@@ -393,6 +435,6 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     // Tile choice: 128x128 when the grid still fills the chip, else 64x64.
     const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
-    if (a.N % 128 == 0 && big_tiles >= 512) return launch_tiles<128, 128>(a, s);
+    if (a.N % 128 == 0 && big_tiles >= 384) return launch_tiles<128, 128>(a, s);
     return launch_tiles<64, 64>(a, s);
 }

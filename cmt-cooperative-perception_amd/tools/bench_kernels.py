@@ -1,0 +1,101 @@
+"""Per-kernel microbenchmark of libcmt_hip.so at the CMT-L frame's shapes
+(HIP events on the launching stream, median of N launches).
+
+    python cmt-cooperative-perception_amd/tools/bench_kernels.py [--only gemm|attn|misc]
+"""
+import argparse
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "cmt-cooperative-perception_amd"))
+
+import torch  # noqa: E402
+
+from projects.mmdet3d_plugin import native as N  # noqa: E402
+
+
+def timeit(fn, reps=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2] * 1e3   # us
+
+
+def gemm_case(name, M, Nn, K, dt, a_f32=True, A2_cols=0, out_dt=torch.float32, headsplit=0, relu=False, R=False,
+              conv=None, batch=1):
+    dev = torch.device("cuda")
+    A = torch.randn(M * batch if conv is None else M * batch, K if conv is None else conv[2], device=dev)
+    if not a_f32:
+        A = A.to(dt)
+    W = (torch.randn(Nn, K, device=dev) / math.sqrt(K)).to(dt)
+    bias = torch.randn(Nn, device=dev)
+    A2 = torch.randn_like(A) if A2_cols else None
+    Rt = torch.randn(M, Nn, device=dev) if R else None
+    C = torch.empty(M * Nn * batch, dtype=out_dt, device=dev)
+    kw = dict(M=M, N=Nn, K=K, lda=A.shape[1], ldw=K, ldc=Nn, bias=bias, relu=relu, R=Rt, ldr=Nn, A2=A2,
+              lda2=K if A2 is not None else 0, a2_cols=A2_cols, headsplit_rows=headsplit)
+    if conv is not None:
+        kw.update(a_mode=N.A_CONV3X3, conv=conv, batch=batch, a_bstride=M * conv[2], c_bstride=M * Nn)
+    us = timeit(lambda: N.gemm(A, W, C, **kw))
+    tf = 2.0 * M * Nn * K * batch / (us * 1e-6) / 1e12
+    print(f"gemm {name:28s} M={M:6d} N={Nn:5d} K={K:5d} {str(dt)[6:]:9s} {us:9.2f} us {tf:8.1f} TF/s", flush=True)
+
+
+def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0):
+    dev = torch.device("cuda")
+    q = torch.randn(B * H * Nq * 32, device=dev).to(dt)
+    k = torch.randn(B * H * Nk * 32, device=dev).to(dt)
+    v = torch.randn(B * H * Nk * 32, device=dev).to(dt)
+    O = torch.empty(B * Nq * H * 32, device=dev)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+
+    def run():
+        N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(H * Nq * 32, Nq * 32, 32),
+                    k_strides=(H * Nk * 32, Nk * 32, 32), v_strides=(H * Nk * 32, Nk * 32, 32),
+                    o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32), kv_splits=splits, workspace=ws)
+    us = timeit(run)
+    tf = 4.0 * B * Nq * Nk * H * 32 / (us * 1e-6) / 1e12
+    print(f"attn {name:28s} Nq={Nq:5d} Nk={Nk:6d} {str(dt)[6:]:9s} splits={splits:3d} {us:9.2f} us {tf:8.1f} TF/s",
+          flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    N.lib()
+    bf = torch.bfloat16
+    if args.only in ("", "gemm"):
+        gemm_case("kv (all layers, pos add)", 32400, 3072, 256, bf, A2_cols=1536, out_dt=bf, headsplit=32400)
+        gemm_case("bev mlp fc1 (relu)", 32400, 256, 512, bf, relu=True)
+        gemm_case("bev mlp fc2", 32400, 256, 256, bf)
+        gemm_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, bf, a_f32=False, conv=(180, 180, 512), relu=True)
+        gemm_case("self qkv (pos add)", 900, 768, 256, bf, A2_cols=512, out_dt=bf, headsplit=900)
+        gemm_case("out proj (+res)", 900, 256, 256, bf, R=True)
+        gemm_case("cross q (pos add)", 900, 256, 256, bf, A2_cols=256, out_dt=bf, headsplit=900)
+        gemm_case("ffn fc1 (relu)", 900, 1024, 256, bf, relu=True)
+        gemm_case("ffn fc2 (+res)", 900, 256, 1024, bf, R=True)
+        gemm_case("ffn fc1 f32", 900, 1024, 256, torch.float32, relu=True)
+        gemm_case("square 4096 bf16", 4096, 4096, 4096, bf, a_f32=False)
+    if args.only in ("", "attn"):
+        for s in (0, 8, 16, 32):
+            attn_case("cross 900x32400", 900, 32400, bf, splits=s)
+        attn_case("cross fp16", 900, 32400, torch.float16)
+        attn_case("self 900x900", 900, 900, bf)
+        attn_case("self f32", 900, 900, torch.float32)
+        attn_case("cross fusion 900x56400", 900, 56400, bf)
+
+
+if __name__ == "__main__":
+    main()
