@@ -32,7 +32,8 @@ struct AttnKParams {
     const void* Q; int64_t q_bs, q_hs, q_rs;
     const void* K; int64_t k_bs, k_hs, k_rs;
     const void* V; int64_t v_bs, v_hs, v_rs;
-    float* O; int64_t o_bs, o_rs;   // splits == 1: final output
+    void* O; int64_t o_bs, o_rs;    // splits == 1: final output (o_dtype)
+    int o_dtype;
     float* Op; float* Mp; float* Lp; // splits > 1: partials [split][b][h][q]
     float c;                        // scale * log2(e)
     int splits;
@@ -40,26 +41,50 @@ struct AttnKParams {
     int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
 };
 
+// Final normalised output: 4 consecutive head dims of one query row.
+__device__ __forceinline__ void store_o4(const AttnKParams& p, int b, int q, int d0, f32x4 v) {
+    const int64_t idx = (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + d0;
+    if (p.o_dtype == CMT_F32) {
+        *(f32x4*)((float*)p.O + idx) = v;
+    } else if (p.o_dtype == CMT_F16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *(h4*)((f16_t*)p.O + idx) = h4{(f16_t)v[0], (f16_t)v[1], (f16_t)v[2], (f16_t)v[3]};
+    } else {
+        typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+        *(b4*)((bf16_t*)p.O + idx) = b4{(bf16_t)v[0], (bf16_t)v[1], (bf16_t)v[2], (bf16_t)v[3]};
+    }
+}
+
 // One 64-key tile for one wave: S^T = K Q^T, online softmax, O^T += V^T P^T.
 // MASK = keys >= Nk in this tile are set to -inf (only the ragged last tile).
-template <typename T, bool MASK>
+// FOLD = Q was pre-multiplied by c = scale*log2(e): the running maximum m
+//   (already in exp2 units) enters the QK^T chain as its accumulator input, so
+//   the MFMA returns c*s - m and the exponent needs no per-score FMA.
+// The row sums run on the MFMA pipe: lsum += ones . P^T (every register of a
+// lane then holds its query's full sum over both lane halves).
+template <typename T, bool MASK, bool FOLD>
 __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T* __restrict__ Vt,
                                                const typename mfma_traits<T>::frag (&qf)[2], f32x16& o,
-                                               float& m_run, float& l_run, float c, int key0, int Nk, int lane) {
+                                               f32x16& lsum, f32x16& negm, float& m_run, bool first, float c,
+                                               int key0, int Nk, int lane) {
     typedef typename mfma_traits<T>::frag frag;
     const int lr = lane & 31;
     const int lh = lane >> 5;
     f32x16 s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
         const int row = kb * 32 + lr;
+        const frag k0 = *(const frag*)(&Kt[row * D + 8 * ((lh) ^ ((row >> 2) & 3))]);
+        const frag k1 = *(const frag*)(&Kt[row * D + 8 * ((2 + lh) ^ ((row >> 2) & 3))]);
+        if (FOLD) {
+            s[kb] = mfma_traits<T>::mma(k0, qf[0], negm);
+        } else {
+            f32x16 z;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const frag kf = *(const frag*)(&Kt[row * D + 8 * ((2 * ks + lh) ^ ((row >> 2) & 3))]);
-            s[kb] = mfma_traits<T>::mma(kf, qf[ks], s[kb]);
+            for (int r = 0; r < 16; ++r) z[r] = 0.f;
+            s[kb] = mfma_traits<T>::mma(k0, qf[0], z);
         }
+        s[kb] = mfma_traits<T>::mma(k1, qf[1], s[kb]);
     }
     if (MASK) {
 #pragma unroll
@@ -78,28 +103,51 @@ __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T
         m1 = vmax3(m1, s[1][r], s[1][r + 1]);
     }
     const float mt = pair_max(vmax(m0, m1));
-    const float m_new = vmax(m_run, mt);
-    // exact lazy rescale: alpha == 1 for every lane whose max did not grow
-    if (__any(m_new > m_run)) {
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] *= alpha;
-        l_run *= alpha;
-        m_run = m_new;
-    }
-    const float mc = m_run * c;
-    float ls0 = 0.f, ls1 = 0.f;
     frag pf[2][2];
+    if (FOLD) {
+        // s = c*score - m_run.  Shift where the tile max is above the running
+        // max (always on a split's first tile, whose m_run is a placeholder 0).
+        if (first || __any(mt > 0.f)) {
+            const float d = first ? mt : vmax(mt, 0.f);
+            const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float e0 = __builtin_amdgcn_exp2f(fmaf(s[0][r], c, -mc));
-        const float e1 = __builtin_amdgcn_exp2f(fmaf(s[1][r], c, -mc));
-        ls0 += e0;
-        ls1 += e1;
-        pf[0][r >> 3][r & 7] = (T)e0;
-        pf[1][r >> 3][r & 7] = (T)e1;
+            for (int r = 0; r < 16; ++r) {
+                o[r] *= alpha;
+                lsum[r] *= alpha;
+                s[0][r] -= d;
+                s[1][r] -= d;
+            }
+            m_run += d;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[0][r]);
+            pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[1][r]);
+        }
+    } else {
+        const float m_new = vmax(m_run, mt);
+        // exact lazy rescale: alpha == 1 for every lane whose max did not grow
+        if (__any(m_new > m_run)) {
+            const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                o[r] *= alpha;
+                lsum[r] *= alpha;
+            }
+            m_run = m_new;
+        }
+        const float mc = m_run * c;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(fmaf(s[0][r], c, -mc));
+            pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(fmaf(s[1][r], c, -mc));
+        }
     }
-    l_run += ls0 + ls1;
+    frag ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
     // V^T fragments by transposed LDS reads: lane 4q+p of each 16-lane group
     // addresses row (r0 + q), columns dgrp + 4p .. +3
     const int dgrp = 16 * ((lane >> 4) & 1);
@@ -117,10 +165,11 @@ __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T
             vv[0] = lo[0]; vv[1] = lo[1]; vv[2] = lo[2]; vv[3] = lo[3];
             vv[4] = hi[0]; vv[5] = hi[1]; vv[6] = hi[2]; vv[7] = hi[3];
             o = mfma_traits<T>::mma(__builtin_bit_cast(frag, vv), pf[kb][ss], o);
+            lsum = mfma_traits<T>::mma(ones, pf[kb][ss], lsum);
         }
 }
 
-template <typename T, int NWAVES>
+template <typename T, int NWAVES, bool FOLD>
 __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
     constexpr int NTH = NWAVES * 64;
@@ -148,6 +197,12 @@ __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
     frag qf[2];
     qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
     qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+    if (FOLD) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * p.c);
+    }
 
     const int ntiles = (p.Nk + KT - 1) / KT;
     const int t_begin = split * p.tiles_per_split;
@@ -186,11 +241,15 @@ __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
         }
     };
 
-    f32x16 o;
+    f32x16 o, lsum, negm;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    float m_run = -__builtin_inff();
-    float l_run = 0.f;
+    for (int r = 0; r < 16; ++r) {
+        o[r] = 0.f;
+        lsum[r] = 0.f;
+        negm[r] = 0.f;
+    }
+    // running max: exp2 units (c * score) with FOLD, score units otherwise
+    float m_run = FOLD ? 0.f : -__builtin_inff();
     const float c = p.c;
 
     if (t_begin < t_end) {
@@ -200,21 +259,21 @@ __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
     __syncthreads();
     for (int t = t_begin; t < t_end; ++t) {
         const int cur = (t - t_begin) & 1;
+        const bool first = t == t_begin;
         if (t + 1 < t_end) load_tile(t + 1);
         if (ragged && t == ntiles - 1)
-            attn_tile_lowp<T, true>(Ks[cur], Vs[cur], qf, o, m_run, l_run, c, t * KT, p.Nk, lane);
+            attn_tile_lowp<T, true, FOLD>(Ks[cur], Vs[cur], qf, o, lsum, negm, m_run, first, c, t * KT, p.Nk, lane);
         else
-            attn_tile_lowp<T, false>(Ks[cur], Vs[cur], qf, o, m_run, l_run, c, t * KT, p.Nk, lane);
+            attn_tile_lowp<T, false, FOLD>(Ks[cur], Vs[cur], qf, o, lsum, negm, m_run, first, c, t * KT, p.Nk, lane);
         if (t + 1 < t_end) store_tile(cur ^ 1);
         __syncthreads();
     }
 
     // ---- write ---------------------------------------------------------------
-    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    const float l_tot = lsum[0];
     if (q >= p.Nq) return;
     if (p.splits == 1) {
         const float inv = 1.f / l_tot;
-        float* dst = p.O + (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
@@ -222,7 +281,7 @@ __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
             }
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
         }
     } else {
         const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
@@ -233,7 +292,7 @@ __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
             *(f32x4*)(dst + 8 * g + 4 * lh) = v;
         }
         if (lh == 0) {
-            p.Mp[row] = m_run;
+            p.Mp[row] = FOLD ? m_run : m_run * c;   // exp2 units for the combine
             p.Lp[row] = l_tot;
         }
     }
@@ -378,11 +437,10 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(AttnKParams p) {
     if (q >= p.Nq) return;
     if (p.splits == 1) {
         const float inv = 1.f / l_tot;
-        float* dst = p.O + (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
         }
     } else {
         const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
@@ -393,7 +451,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(AttnKParams p) {
             *(f32x4*)(dst + 8 * g + 4 * lh) = v;
         }
         if (lh == 0) {
-            p.Mp[row] = m_run;
+            p.Mp[row] = m_run * c;   // exp2 units for the combine
             p.Lp[row] = l_tot;
         }
     }
@@ -419,7 +477,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     for (int s = 0; s < p.splits; ++s) {
         const float ms = p.Mp[s * rows + bhq];
         if (ms == -__builtin_inff()) continue;
-        const float w = __builtin_amdgcn_exp2f((ms - M) * p.c);
+        const float w = __builtin_amdgcn_exp2f(ms - M);   // maxima are stored in exp2 units
         num += w * *(const f32x4*)(p.Op + (s * rows + bhq) * D + d4);
         den += w * p.Lp[s * rows + bhq];
     }
@@ -432,7 +490,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = (float)(bf16_t)r[j];
     }
-    *(f32x4*)(p.O + (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + h * D + d4) = r;
+    store_o4(p, b, q, h * D + d4, r);
 }
 
 // 8-wave workgroups (256 queries share each staged K/V tile) for long key
@@ -446,11 +504,12 @@ int choose_splits(const cmt_attn_args& a) {
     const int ntiles = (a.Nk + KT - 1) / KT;
     const int qrows = a.dtype == CMT_F32 ? QB : lowp_waves(a) * QW;
     const int base = cdiv(a.Nq, qrows) * a.B * a.H;
+    const int nw = a.dtype == CMT_F32 ? NW : lowp_waves(a);
     int s = 1;
-    // aim for >= 1024 workgroups (4 per CU) while keeping >= 8 tiles per split;
+    // aim for >= 4096 waves (4 per SIMD) while keeping >= 8 tiles per split;
     // short key ranges (self-attention) split down to 2 tiles per split
     const int min_tiles = ntiles >= 64 ? 8 : 2;
-    while (base * s < 1024 && ntiles / (2 * s) >= min_tiles) s *= 2;
+    while ((int64_t)base * s * nw < 4096 && ntiles / (2 * s) >= min_tiles) s *= 2;
     return s;
 }
 
@@ -474,6 +533,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     CMT_REQUIRE(a.dtype != CMT_F32 || ((a.q_rstride | a.k_rstride | a.v_rstride) % 4 == 0),
                 "cmt_attn_fwd: f32 rows must be 16-byte aligned");
     CMT_REQUIRE(a.o_rstride % 4 == 0 && a.o_bstride % 4 == 0, "cmt_attn_fwd: O strides must be multiples of 4");
+    CMT_REQUIRE(a.o_dtype == CMT_F32 || a.o_dtype == CMT_F16 || a.o_dtype == CMT_BF16, "cmt_attn_fwd: bad o_dtype");
     CMT_REQUIRE(a.q_rstride % 8 == 0 && a.k_rstride % 8 == 0 && a.v_rstride % 8 == 0 && a.q_hstride % 8 == 0 &&
                 a.k_hstride % 8 == 0 && a.v_hstride % 8 == 0 && a.q_bstride % 8 == 0 && a.k_bstride % 8 == 0 &&
                 a.v_bstride % 8 == 0, "cmt_attn_fwd: Q/K/V strides must be multiples of 8 elements");
@@ -484,7 +544,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     p.Q = a.Q; p.q_bs = a.q_bstride; p.q_hs = a.q_hstride; p.q_rs = a.q_rstride;
     p.K = a.K; p.k_bs = a.k_bstride; p.k_hs = a.k_hstride; p.k_rs = a.k_rstride;
     p.V = a.V; p.v_bs = a.v_bstride; p.v_hs = a.v_hstride; p.v_rs = a.v_rstride;
-    p.O = a.O; p.o_bs = a.o_bstride; p.o_rs = a.o_rstride;
+    p.O = a.O; p.o_bs = a.o_bstride; p.o_rs = a.o_rstride; p.o_dtype = a.o_dtype;
     p.c = a.scale * 1.4426950408889634f;
     p.splits = splits;
     p.tiles_per_split = cdiv(ntiles, splits);
@@ -502,11 +562,18 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const int nw = lowp_waves(a);
     dim3 grid(cdiv(a.Nq, a.dtype == CMT_F32 ? QB : nw * QW), a.B * a.H, splits);
+    const bool fold = (a.flags & CMT_ATTN_FOLD_SCALE) != 0;
+#define ATTN_LAUNCH(T, NWV)                                                                   \
+    do {                                                                                      \
+        if (fold) attn_fwd_kernel<T, NWV, true><<<grid, NWV * 64, 0, s>>>(p);                 \
+        else attn_fwd_kernel<T, NWV, false><<<grid, NWV * 64, 0, s>>>(p);                     \
+    } while (0)
     if (a.dtype == CMT_F32) attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
-    else if (a.dtype == CMT_F16 && nw == 8) attn_fwd_kernel<f16_t, 8><<<grid, 512, 0, s>>>(p);
-    else if (a.dtype == CMT_F16) attn_fwd_kernel<f16_t, 4><<<grid, 256, 0, s>>>(p);
-    else if (nw == 8) attn_fwd_kernel<bf16_t, 8><<<grid, 512, 0, s>>>(p);
-    else attn_fwd_kernel<bf16_t, 4><<<grid, 256, 0, s>>>(p);
+    else if (a.dtype == CMT_F16 && nw == 8) ATTN_LAUNCH(f16_t, 8);
+    else if (a.dtype == CMT_F16) ATTN_LAUNCH(f16_t, 4);
+    else if (nw == 8) ATTN_LAUNCH(bf16_t, 8);
+    else ATTN_LAUNCH(bf16_t, 4);
+#undef ATTN_LAUNCH
     int rc = cmt_check_launch("cmt_attn_fwd");
     if (rc || splits == 1) return rc;
     const int64_t total = (int64_t)a.B * a.H * a.Nq * 8;

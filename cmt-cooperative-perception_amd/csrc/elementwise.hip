@@ -13,24 +13,45 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// Typed scalar store / 8-wide vector store for the dtype-generic outputs.
+__device__ __forceinline__ void store_dt(void* p, int64_t idx, int dt, float v) {
+    if (dt == CMT_F32) ((float*)p)[idx] = v;
+    else if (dt == CMT_F16) ((f16_t*)p)[idx] = (f16_t)v;
+    else ((bf16_t*)p)[idx] = (bf16_t)v;
+}
+
 // ---------------------------------------------------------------------------
 // LayerNorm: one wave per row, VPT = C / 64 values per lane (lane-strided so
-// the loads are 256-byte coalesced per instruction).
+// the loads are 256-byte coalesced per instruction).  Optional outputs from
+// the same registers: a second LN of the result (post_norm), and the next
+// GEMMs' operands in the compute dtype (lowp(y), lowp(y + P)).
 // ---------------------------------------------------------------------------
-template <int VPT>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ X, int64_t ldx, int rows,
-                                                        const float* __restrict__ W, const float* __restrict__ B,
-                                                        float eps, float* Y, int64_t ldy, int flags,
-                                                        const float* __restrict__ W2, const float* __restrict__ B2,
-                                                        float* Y2, int64_t ldy2, int flags2) {
+template <int VPT, typename LT>
+__global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (row >= rows) return;
+    if (row >= a.rows) return;
     constexpr int C = VPT * 64;
     float v[VPT];
-    const float* x = X + (int64_t)row * ldx;
+    const float* x = a.X + (int64_t)row * a.ldx;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) v[i] = x[lane + 64 * i];
+    float pv[VPT];
+    if (a.Yp) {
+        const float* pr = a.P + (int64_t)row * a.ldp;
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) pv[i] = pr[lane + 64 * i];
+    }
+    float yold[VPT];
+    if (a.Y && (a.flags & CMT_LN_MAX_INTO)) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) yold[i] = a.Y[(int64_t)row * a.ldy + lane + 64 * i];
+    }
+    float y2old[VPT];
+    if (a.Y2 && (a.flags2 & CMT_LN_MAX_INTO)) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) y2old[i] = a.Y2[(int64_t)row * a.ldy2 + lane + 64 * i];
+    }
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) s += v[i];
@@ -38,18 +59,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) { float d = v[i] - mean; ss += d * d; }
-    const float rstd = rsqrtf(wave_sum(ss) / (float)C + eps);
-    float* y = Y + (int64_t)row * ldy;
+    const float rstd = rsqrtf(wave_sum(ss) / (float)C + a.eps);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = lane + 64 * i;
-        float o = (v[i] - mean) * rstd * W[c] + B[c];
+        float o = (v[i] - mean) * rstd * a.W[c] + a.B[c];
         v[i] = o;   // the second LN consumes the first LN's output
-        if (flags & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
-        if (flags & CMT_LN_MAX_INTO) o = fmaxf(o, y[c]);
-        y[c] = o;
+        if (a.flags & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
+        if (a.flags & CMT_LN_MAX_INTO) o = fmaxf(o, yold[i]);
+        if (a.Y) a.Y[(int64_t)row * a.ldy + c] = o;
+        if (a.Yl) ((LT*)a.Yl)[(int64_t)row * a.ldyl + c] = (LT)o;
+        if (a.Yp) ((LT*)a.Yp)[(int64_t)row * a.ldyp + c] = (LT)(o + pv[i]);
     }
-    if (Y2 == nullptr) return;
+    if (a.Y2 == nullptr) return;
     s = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) s += v[i];
@@ -57,15 +79,29 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     ss = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) { float d = v[i] - mean2; ss += d * d; }
-    const float rstd2 = rsqrtf(wave_sum(ss) / (float)C + eps);
-    float* y2 = Y2 + (int64_t)row * ldy2;
+    const float rstd2 = rsqrtf(wave_sum(ss) / (float)C + a.eps);
+    float* y2 = a.Y2 + (int64_t)row * a.ldy2;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = lane + 64 * i;
-        float o = (v[i] - mean2) * rstd2 * W2[c] + B2[c];
-        if (flags2 & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
-        if (flags2 & CMT_LN_MAX_INTO) o = fmaxf(o, y2[c]);
+        float o = (v[i] - mean2) * rstd2 * a.W2[c] + a.B2[c];
+        if (a.flags2 & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
+        if (a.flags2 & CMT_LN_MAX_INTO) o = fmaxf(o, y2old[i]);
         y2[c] = o;
+    }
+}
+
+template <typename LT>
+__global__ __launch_bounds__(256) void add_cast_kernel(const float* __restrict__ X, const float* __restrict__ P,
+                                                       int64_t n4, LT* Yl, LT* Yp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const f32x4 x = ((const f32x4*)X)[i];
+    typedef LT l4 __attribute__((ext_vector_type(4)));
+    if (Yl) ((l4*)Yl)[i] = l4{(LT)x[0], (LT)x[1], (LT)x[2], (LT)x[3]};
+    if (Yp) {
+        const f32x4 y = x + ((const f32x4*)P)[i];
+        ((l4*)Yp)[i] = l4{(LT)y[0], (LT)y[1], (LT)y[2], (LT)y[3]};
     }
 }
 
@@ -82,13 +118,16 @@ __device__ __forceinline__ float inv_sigmoid_dev(float x) {
 }
 __device__ __forceinline__ float sigmoid_dev(float x) { return 1.f / (1.f + expf(-x)); }
 
-__global__ void pos2embed_kernel(const float* __restrict__ pos, int64_t pos_stride, int n, int F, int mode,
-                                 int x_size, int y_size, float* out, int64_t ldo) {
+template <typename OT>
+__global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict__ pos, int64_t pos_stride, int n,
+                                                        int F, int mode, int x_size, int y_size, OT* out,
+                                                        int64_t ldo) {
+    // one thread = 8 consecutive outputs (4 sin/cos pairs sharing an argument)
+    const int groups = (2 * F) >> 3;
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)n * 2 * F;
-    if (idx >= total) return;
-    const int i = (int)(idx / (2 * F));
-    const int f = (int)(idx - (int64_t)i * 2 * F);
+    if (idx >= (int64_t)n * groups) return;
+    const int i = (int)(idx / groups);
+    const int f0 = (int)(idx - (int64_t)i * groups) * 8;
     float px, py;
     if (pos == nullptr) {
         // coords_bev: token t = r * y_size + c  ->  x = (c+0.5)/x_size, y = (r+0.5)/y_size
@@ -105,11 +144,24 @@ __global__ void pos2embed_kernel(const float* __restrict__ pos, int64_t pos_stri
         }
     }
     const float scale = 6.283185307179586f;
-    const int j = f < F ? f : f - F;          // first F outputs embed y, the next F embed x
-    const float p = (f < F ? py : px) * scale;
-    const float dim_t = 2.f * (float)(j >> 1) / (float)F + 1.f;
-    const float v = p / dim_t;
-    out[(int64_t)i * ldo + f] = (j & 1) ? cosf(v) : sinf(v);
+    const float p = (f0 < F ? py : px) * scale;   // first F outputs embed y, the next F embed x
+    const int j0 = f0 < F ? f0 : f0 - F;
+    float o[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float dim_t = 2.f * (float)((j0 >> 1) + t) / (float)F + 1.f;
+        const float v = p / dim_t;                 // |v| <= 2*pi: v_sin/v_cos are accurate here
+        o[2 * t] = __sinf(v);
+        o[2 * t + 1] = __cosf(v);
+    }
+    OT* dst = out + (int64_t)i * ldo + f0;
+    if constexpr (sizeof(OT) == 4) {
+        *(f32x4*)dst = f32x4{o[0], o[1], o[2], o[3]};
+        *(f32x4*)(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    } else {
+        typedef OT o8 __attribute__((ext_vector_type(8)));
+        *(o8*)dst = o8{(OT)o[0], (OT)o[1], (OT)o[2], (OT)o[3], (OT)o[4], (OT)o[5], (OT)o[6], (OT)o[7]};
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -117,8 +169,9 @@ __global__ void pos2embed_kernel(const float* __restrict__ pos, int64_t pos_stri
 // ---------------------------------------------------------------------------
 struct PcRange { float v[6]; };
 
+template <typename OT>
 __global__ void rv_pe_coords_kernel(int BV, int H, int W, int D, float pad_h, float pad_w, float dstep,
-                                    const float* __restrict__ i2l, PcRange pc, float* out) {
+                                    const float* __restrict__ i2l, PcRange pc, OT* out) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)BV * H * W * D;
     if (idx >= total) return;
@@ -132,14 +185,14 @@ __global__ void rv_pe_coords_kernel(int BV, int H, int W, int D, float pad_h, fl
     const float d = 1.f + (float)k * dstep / (float)D;
     const float c[4] = {u * d, v * d, d, 1.f};
     const float* M = i2l + (int64_t)bv * 16;
-    float* o = out + tok * (3 * D) + 3 * k;
+    OT* o = out + tok * (3 * D) + 3 * k;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         float a = M[r * 4 + 0] * c[0];
         a = fmaf(M[r * 4 + 1], c[1], a);
         a = fmaf(M[r * 4 + 2], c[2], a);
         a = fmaf(M[r * 4 + 3], c[3], a);
-        o[r] = (a - pc.v[r]) / (pc.v[3 + r] - pc.v[r]);
+        o[r] = (OT)((a - pc.v[r]) / (pc.v[3 + r] - pc.v[r]));
     }
 }
 
@@ -347,21 +400,24 @@ inline unsigned nblocks(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs
 
 }  // namespace
 
-extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const float* W, const float* Bv,
-                             float eps, float* Y, int64_t ldy, int flags, const float* W2, const float* B2,
-                             float* Y2, int64_t ldy2, int flags2, void* stream) {
-    CMT_REQUIRE(X && W && Bv && Y && rows >= 0, "cmt_layernorm: null pointer");
-    CMT_REQUIRE(C % 64 == 0 && C >= 64 && C <= 1024, "cmt_layernorm: C must be a multiple of 64 in [64, 1024]");
-    CMT_REQUIRE(Y2 == nullptr || (W2 && B2), "cmt_layernorm: second LN needs W2/B2");
-    if (rows == 0) return 0;
+extern "C" int cmt_layernorm_ex(const cmt_ln_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_layernorm: null args");
+    const cmt_ln_args& a = *ap;
+    CMT_REQUIRE(a.X && a.W && a.B && a.rows >= 0 && (a.Y || a.Yl || a.Yp || a.Y2), "cmt_layernorm: null pointer");
+    CMT_REQUIRE(a.C % 64 == 0 && a.C >= 64 && a.C <= 1024, "cmt_layernorm: C must be a multiple of 64 in [64, 1024]");
+    CMT_REQUIRE(a.Y2 == nullptr || (a.W2 && a.B2), "cmt_layernorm: second LN needs W2/B2");
+    CMT_REQUIRE(a.Yp == nullptr || a.P != nullptr, "cmt_layernorm: Yp needs P");
+    CMT_REQUIRE((a.Yl == nullptr && a.Yp == nullptr) || a.lowp_dtype == CMT_F16 || a.lowp_dtype == CMT_BF16,
+                "cmt_layernorm: lowp_dtype must be f16 or bf16");
+    if (a.rows == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    dim3 grid(cdiv(rows, 4));
-#define LN_CASE(V)                                                                                   \
-    case V:                                                                                          \
-        layernorm_kernel<V><<<grid, 256, 0, s>>>(X, ldx, rows, W, Bv, eps, Y, ldy, flags, W2, B2, Y2, \
-                                                 ldy2, flags2);                                       \
+    dim3 grid(cdiv(a.rows, 4));
+#define LN_CASE(V)                                                                              \
+    case V:                                                                                     \
+        if (a.lowp_dtype == CMT_F16) layernorm_kernel<V, f16_t><<<grid, 256, 0, s>>>(a);        \
+        else layernorm_kernel<V, bf16_t><<<grid, 256, 0, s>>>(a);                               \
         break;
-    switch (C / 64) {
+    switch (a.C / 64) {
         LN_CASE(1) LN_CASE(2) LN_CASE(3) LN_CASE(4) LN_CASE(5) LN_CASE(6) LN_CASE(7) LN_CASE(8)
         LN_CASE(9) LN_CASE(10) LN_CASE(11) LN_CASE(12) LN_CASE(13) LN_CASE(14) LN_CASE(15) LN_CASE(16)
     }
@@ -369,26 +425,70 @@ extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const
     return cmt_check_launch("cmt_layernorm");
 }
 
+extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const float* W, const float* Bv,
+                             float eps, float* Y, int64_t ldy, int flags, const float* W2, const float* B2,
+                             float* Y2, int64_t ldy2, int flags2, void* stream) {
+    CMT_REQUIRE(Y != nullptr, "cmt_layernorm: null pointer");
+    cmt_ln_args a = {};
+    a.X = X; a.ldx = ldx; a.rows = rows; a.C = C; a.W = W; a.B = Bv; a.eps = eps;
+    a.Y = Y; a.ldy = ldy; a.flags = flags;
+    a.W2 = W2; a.B2 = B2; a.Y2 = Y2; a.ldy2 = ldy2; a.flags2 = flags2;
+    a.lowp_dtype = CMT_BF16;
+    return cmt_layernorm_ex(&a, stream);
+}
+
+extern "C" int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,
+                            void* stream) {
+    CMT_REQUIRE(X && rows >= 0 && C % 4 == 0 && (Yp == nullptr || P), "cmt_add_cast: bad arguments");
+    CMT_REQUIRE(lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16, "cmt_add_cast: lowp_dtype must be f16 or bf16");
+    const int64_t n4 = (int64_t)rows * C / 4;
+    if (n4 == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (lowp_dtype == CMT_F16)
+        add_cast_kernel<f16_t><<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, (f16_t*)Yl, (f16_t*)Yp);
+    else
+        add_cast_kernel<bf16_t><<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, (bf16_t*)Yl, (bf16_t*)Yp);
+    return cmt_check_launch("cmt_add_cast");
+}
+
 extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F, int mode, int grid_h,
-                             int grid_w, float* out, int64_t ldo, void* stream) {
-    CMT_REQUIRE(out && n >= 0 && F > 0 && F % 2 == 0, "cmt_pos2embed: bad arguments");
+                             int grid_w, void* out, int odtype, int64_t ldo, void* stream) {
+    CMT_REQUIRE(out && n >= 0 && F > 0 && F % 4 == 0 && ldo % 8 == 0, "cmt_pos2embed: bad arguments");
     CMT_REQUIRE(pos != nullptr || (grid_h > 0 && grid_w > 0 && n == grid_h * grid_w),
                 "cmt_pos2embed: grid mode needs n == grid_h*grid_w");
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_pos2embed: bad odtype");
     if (n == 0) return 0;
-    const int64_t total = (int64_t)n * 2 * F;
-    pos2embed_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(pos, pos_stride, n, F, mode, grid_h,
-                                                                            grid_w, out, ldo);
+    const int64_t total = (int64_t)n * (2 * F / 8);
+    hipStream_t s = (hipStream_t)stream;
+    if (odtype == CMT_F32)
+        pos2embed_kernel<float><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
+                                                                    (float*)out, ldo);
+    else if (odtype == CMT_F16)
+        pos2embed_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
+                                                                    (f16_t*)out, ldo);
+    else
+        pos2embed_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
+                                                                     (bf16_t*)out, ldo);
     return cmt_check_launch("cmt_pos2embed");
 }
 
 extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float pad_w, float depth_max,
-                                const float* i2l, const float* pc_range6, float* out, void* stream) {
+                                const float* i2l, const float* pc_range6, void* out, int odtype, void* stream) {
     CMT_REQUIRE(i2l && pc_range6 && out && BV > 0 && h > 0 && w > 0 && D > 0, "cmt_rv_pe_coords: bad arguments");
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_rv_pe_coords: bad odtype");
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
     const int64_t total = (int64_t)BV * h * w * D;
-    rv_pe_coords_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(BV, h, w, D, pad_h, pad_w,
-                                                                               depth_max - 1.f, i2l, pc, out);
+    hipStream_t s = (hipStream_t)stream;
+    if (odtype == CMT_F32)
+        rv_pe_coords_kernel<float><<<nblocks(total, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
+                                                                       i2l, pc, (float*)out);
+    else if (odtype == CMT_F16)
+        rv_pe_coords_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
+                                                                       i2l, pc, (f16_t*)out);
+    else
+        rv_pe_coords_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
+                                                                        i2l, pc, (bf16_t*)out);
     return cmt_check_launch("cmt_rv_pe_coords");
 }
 

@@ -69,6 +69,12 @@ __device__ __forceinline__ int64_t a_offset(const cmt_gemm_args& a, const RowInf
     }
 }
 
+__device__ __forceinline__ float load_elem(const void* p, int64_t idx, int dt) {
+    if (dt == CMT_F32) return ((const float*)p)[idx];
+    if (dt == CMT_F16) return (float)((const f16_t*)p)[idx];
+    return (float)((const bf16_t*)p)[idx];
+}
+
 template <typename T>
 __device__ __forceinline__ void store_out(void* C, int64_t idx, int dt, float v) {
     (void)sizeof(T);
@@ -86,11 +92,30 @@ __device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[B
     const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
     void* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
     const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
-    const float* Rz = a.R ? a.R + (int64_t)z * a.r_bstride : nullptr;
+    const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
+    // pass 1: bias, activation, residual (all loads before the first store --
+    // vmcnt counts stores on CDNA4, so a load after a store would wait for it)
 #pragma unroll
     for (int tn = 0; tn < BN / 64; ++tn) {
         const int col = n0 + wn * (BN / 2) + tn * 32 + col_l;
         const float bias = biasz ? biasz[col] : 0.f;
+#pragma unroll
+        for (int tm = 0; tm < BM / 64; ++tm) {
+            const int row0 = m0 + wm * (BM / 2) + tm * 32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = min(row0 + (r & 3) + 8 * (r >> 2) + 4 * h, a.M - 1);
+                float v = acc[tm][tn][r] + bias;
+                if (a.relu) v = fmaxf(v, 0.f);
+                if (Rz) v += load_elem(Rz, (int64_t)row * a.ldr + col, a.r_dtype);
+                acc[tm][tn][r] = v;
+            }
+        }
+    }
+    // pass 2: stores
+#pragma unroll
+    for (int tn = 0; tn < BN / 64; ++tn) {
+        const int col = n0 + wn * (BN / 2) + tn * 32 + col_l;
 #pragma unroll
         for (int tm = 0; tm < BM / 64; ++tm) {
             // head-split addressing: one division per 32-row tile, the 32 rows
@@ -107,9 +132,6 @@ __device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[B
                 const int off = (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int row = row0 + off;
                 if (row >= a.M) continue;
-                float v = acc[tm][tn][r] + bias;
-                if (a.relu) v = fmaxf(v, 0.f);
-                if (Rz) v += Rz[(int64_t)row * a.ldr + col];
                 int64_t idx;
                 if (a.c_mode == CMT_C_ROWS) {
                     idx = (int64_t)row * a.ldc + col;
@@ -123,7 +145,7 @@ __device__ __forceinline__ void epilogue(const cmt_gemm_args& a, f32x16 (&acc)[B
                     }
                     idx = (((int64_t)b * (a.N >> 5) + (col >> 5)) * rpb + rr) * 32 + (col & 31);
                 }
-                store_out<float>(Cz, idx, a.c_dtype, v);
+                store_out<float>(Cz, idx, a.c_dtype, acc[tm][tn][r]);
             }
         }
     }
@@ -184,7 +206,7 @@ __global__ __launch_bounds__(NT) void gemm_lowp_kernel(cmt_gemm_args a) {
                 f32x4 v0 = *(const f32x4*)p;
                 f32x4 v1 = *(const f32x4*)(p + 4);
                 if (use_a2) {
-                    const float* p2 = a.A2 + (int64_t)(m0 + row) * a.lda2 + kk;
+                    const float* p2 = (const float*)a.A2 + (int64_t)(m0 + row) * a.lda2 + kk;
                     v0 += *(const f32x4*)p2;
                     v1 += *(const f32x4*)(p2 + 4);
                 }
@@ -305,7 +327,7 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(cmt_gemm_args a) {
                 areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
                 areg[i] = *(const f32x4*)(Ab + off);
-                if (use_a2) areg[i] += *(const f32x4*)(a.A2 + (int64_t)(m0 + arow[i]) * a.lda2 + kk);
+                if (use_a2) areg[i] += *(const f32x4*)((const float*)a.A2 + (int64_t)(m0 + arow[i]) * a.lda2 + kk);
             }
         }
 #pragma unroll
@@ -365,6 +387,279 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(cmt_gemm_args a) {
     epilogue<BM, BN>(a, acc, m0, n0, wm, wn, lane);
 }
 
+
+// ---------------------------------------------------------------------------
+// LDS-DMA path (A already in the compute dtype).
+//
+// Tiles are copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging):
+// one wave-instruction moves 8 rows x 128 B (64 k of one stage) into a
+// lane-linear LDS image; the 16-byte chunk permutation (row>>1)&7 is applied
+// to the SOURCE address and undone on the ds_read_b128 side (guide rule 21),
+// so the fragment reads are bank-conflict free.  S stages are kept in flight
+// with counted vmcnt waits and one raw s_barrier per k-step.  Gathered A rows
+// (3x3 / 1D-3 convolution taps outside the map) read a zero page.
+//
+// The MFMA is issued as C^T = W . A^T (W rows on the A operand), so each lane
+// ends with 4 consecutive output columns of one row: 16-byte (fp32) / 8-byte
+// stores, 4 per 32x32 tile instead of 16 scalar ones.
+//
+// Workgroups are numbered XCD-aware: the round-robin dispatch order is
+// remapped so one XCD walks a contiguous band of M tiles with every N tile,
+// and the band's A rows and all of W stay in that XCD's L2.
+// ---------------------------------------------------------------------------
+__device__ __attribute__((aligned(64))) char g_zero_page[256];
+
+typedef const __attribute__((address_space(1))) void* gaddr_t;
+typedef __attribute__((address_space(3))) void* laddr_t;
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds((gaddr_t)src, (laddr_t)lds, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+template <int PER, int S>
+__device__ __forceinline__ void wait_tiles(int inflight) {
+    if (S > 3 && inflight >= 3) wait_vm_lgkm<(S > 3 ? 3 * PER : 0)>();
+    else if (S > 2 && inflight == 2) wait_vm_lgkm<(S > 2 ? 2 * PER : 0)>();
+    else if (inflight == 1) wait_vm_lgkm<PER>();
+    else wait_vm_lgkm<0>();
+}
+
+template <typename CT>
+__device__ __forceinline__ void store4(void* C, int64_t idx, int dt, f32x4 v) {
+    if (dt == CMT_F32) {
+        *(f32x4*)((float*)C + idx) = v;
+    } else if (dt == CMT_F16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 h = {(f16_t)v[0], (f16_t)v[1], (f16_t)v[2], (f16_t)v[3]};
+        *(h4*)((f16_t*)C + idx) = h;
+    } else {
+        typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+        b4 h = {(bf16_t)v[0], (bf16_t)v[1], (bf16_t)v[2], (bf16_t)v[3]};
+        *(b4*)((bf16_t*)C + idx) = h;
+    }
+}
+
+__device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt) {
+    if (dt == CMT_F32) return *(const f32x4*)((const float*)p + idx);
+    if (dt == CMT_F16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 h = *(const h4*)((const f16_t*)p + idx);
+        return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    }
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    b4 h = *(const b4*)((const bf16_t*)p + idx);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+
+template <typename CT, int BM, int BN, int S, int AMODE>
+__global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
+    typedef typename mfma_traits<CT>::frag frag;
+    constexpr int KS = 64;                          // k per stage: one 128-byte LDS row per tile row
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+    constexpr int APER = BM / 32, BPER = BN / 32;   // 256 lanes x 16 B = 32 rows per block-wide copy
+    constexpr int PER = APER + BPER;                // glds per thread per stage
+    constexpr int TM = BM / 64, TN = BN / 64;
+    __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+
+    // XCD-aware tile order (bijective remap of the round-robin dispatch)
+    const int nwg = tiles_m * tiles_n * a.batch;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int per_z = tiles_m * tiles_n;
+    const int z = wg / per_z;
+    const int rem = wg - z * per_z;
+    const int mt = rem / tiles_n;
+    const int m0 = mt * BM, n0 = (rem - mt * tiles_n) * BN;
+
+    const bool sel_a2 = AMODE == CMT_A_ROWS && a.A2 != nullptr && n0 < a.a2_cols;
+    const CT* Ab = (const CT*)(sel_a2 ? a.A2 : a.A) + (int64_t)z * a.a_bstride;
+    const int64_t lda = sel_a2 ? a.lda2 : a.lda;
+    const CT* Wb = (const CT*)a.W + (int64_t)z * a.w_bstride;
+
+    // per-thread source rows: copy i of this wave covers tile rows (4i + wave)*8 + lane/8
+    const int ch = lane & 7;
+    const CT* asrc[APER];
+    RowInfo ri[APER];
+    int acs[APER];
+#pragma unroll
+    for (int i = 0; i < APER; ++i) {
+        const int row = (4 * i + wave) * 8 + (lane >> 3);
+        acs[i] = (ch ^ ((row >> 1) & 7)) * 8;
+        const int m = m0 + row;
+        ri[i] = make_row_info<AMODE>(a, m);
+        asrc[i] = Ab + (int64_t)min(m, a.M - 1) * lda + acs[i];
+    }
+    const CT* bsrc[BPER];
+#pragma unroll
+    for (int i = 0; i < BPER; ++i) {
+        const int row = (4 * i + wave) * 8 + (lane >> 3);
+        bsrc[i] = Wb + (int64_t)(n0 + row) * a.ldw + (ch ^ ((row >> 1) & 7)) * 8;
+    }
+
+    auto issue = [&](int buf, int kt) {
+        char* sb = smem + buf * STAGE;
+        const int k0 = kt * KS;
+#pragma unroll
+        for (int i = 0; i < APER; ++i) {
+            const void* src;
+            if (AMODE == CMT_A_ROWS) {
+                src = asrc[i] + k0;
+            } else {
+                const int64_t off = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), k0);
+                src = off < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + off + acs[i]);
+            }
+            glds16(src, sb + (4 * i + wave) * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < BPER; ++i) glds16(bsrc[i] + k0, sb + A_BYTES + (4 * i + wave) * 1024);
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = a.K / KS;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (s < nk) issue(s, s);
+
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int last = min(nk - 1, kt == 0 ? S - 1 : kt + S - 2);
+        wait_tiles<PER, S>(last - kt);
+        __builtin_amdgcn_s_barrier();
+        // every wave is past its reads of stage kt-1: refill that buffer
+        if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
+        const char* As = smem + (kt % S) * STAGE;
+        const char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < KS / 16; ++ks) {
+            frag af[TM], bfr[TN];
+            const int kc = 2 * ks + lh;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                const int r = wm * (BM / 2) + tm * 32 + lr;
+                af[tm] = *(const frag*)(As + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int r = wn * (BN / 2) + tn * 32 + lr;
+                bfr[tn] = *(const frag*)(Bs + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<CT>::mma(bfr[tn], af[tm], acc[tm][tn]);
+        }
+    }
+
+    // ---- epilogue: lane = output row, 4 consecutive columns per register group.
+    // Every bias / residual load is issued before the first store: vmcnt counts
+    // stores too on CDNA4, so a load waited for after a store would drain it.
+    const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
+    char* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
+    const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
+    const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
+    f32x4 bv[TN][4];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;
+            bv[tn][g] = biasz ? *(const f32x4*)(biasz + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    if (Rz) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int m = min(m0 + wm * (BM / 2) + tm * 32 + lr, a.M - 1);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;
+                    const f32x4 r = load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype);
+                    // bias + relu come first; keep R apart only when relu is on
+                    if (a.relu) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] = fmaxf(acc[tm][tn][4 * g + j] + bv[tn][g][j], 0.f) + r[j];
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                    }
+                }
+        }
+    } else {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float v = acc[tm][tn][4 * g + j] + bv[tn][g][j];
+                        acc[tm][tn][4 * g + j] = a.relu ? fmaxf(v, 0.f) : v;
+                    }
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int m = m0 + wm * (BM / 2) + tm * 32 + lr;
+        if (m >= a.M) continue;
+        int b = 0, rr = m;
+        if (a.c_mode != CMT_C_ROWS) {
+            b = m / a.rows_per_batch;
+            rr = m - b * a.rows_per_batch;
+        }
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;
+                const f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
+                                 acc[tm][tn][4 * g + 3]};
+                const int64_t idx = a.c_mode == CMT_C_ROWS
+                                        ? (int64_t)m * a.ldc + n
+                                        : (((int64_t)b * (a.N >> 5) + (n >> 5)) * a.rows_per_batch + rr) * 32 + (n & 31);
+                store4<CT>(Cz, idx, a.c_dtype, v);
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int S, int AMODE>
+int launch_dma_mode(const cmt_gemm_args& a, hipStream_t s) {
+    const int tm = cdiv(a.M, BM), tn = a.N / BN;
+    const int64_t nwg = (int64_t)tm * tn * a.batch;
+    if (a.w_dtype == CMT_BF16) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
+    else gemm_dma_kernel<f16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
+    return cmt_check_launch("cmt_gemm");
+}
+
+template <int BM, int BN, int S>
+int launch_dma(const cmt_gemm_args& a, hipStream_t s) {
+    switch (a.a_mode) {
+        case CMT_A_ROWS: return launch_dma_mode<BM, BN, S, CMT_A_ROWS>(a, s);
+        case CMT_A_CONV3X3: return launch_dma_mode<BM, BN, S, CMT_A_CONV3X3>(a, s);
+        default: return launch_dma_mode<BM, BN, S, CMT_A_CONV1D3>(a, s);
+    }
+}
+
 template <int BM, int BN, int LBK, int AMODE>
 void launch_lowp(const cmt_gemm_args& a, dim3 grid, hipStream_t s) {
     if constexpr (AMODE == CMT_A_CONV3X3) {
@@ -421,9 +716,14 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
                 "cmt_gemm: the conv3x3 gather needs A in the compute dtype");
     CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16, "cmt_gemm: bad c_dtype");
     CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0, "cmt_gemm: lda/ldw must be multiples of 8 elements");
-    CMT_REQUIRE(a.A2 == nullptr || (a.a_mode == CMT_A_ROWS && a.a_dtype == CMT_F32 && a.lda2 % 4 == 0 &&
-                                    a.a2_cols % 128 == 0),
-                "cmt_gemm: A2 needs row mode, f32 A, 128-aligned a2_cols");
+    CMT_REQUIRE(a.r_dtype == CMT_F32 || a.r_dtype == a.w_dtype, "cmt_gemm: R must be f32 or the compute dtype");
+    CMT_REQUIRE(a.A2 == nullptr || (a.a_mode == CMT_A_ROWS && a.a2_cols % 128 == 0),
+                "cmt_gemm: A2 needs row mode and 128-aligned a2_cols");
+    CMT_REQUIRE(a.A2 == nullptr || a.a2_mode == CMT_A2_SELECT || (a.a_dtype == CMT_F32 && a.lda2 % 4 == 0),
+                "cmt_gemm: A2 add mode needs f32 A");
+    CMT_REQUIRE(a.A2 == nullptr || a.a2_mode == CMT_A2_ADD || (a.a_dtype == a.w_dtype && a.a_dtype != CMT_F32 &&
+                                                               a.lda2 % 8 == 0),
+                "cmt_gemm: A2 select mode needs A in the f16/bf16 compute dtype");
     if (a.a_mode == CMT_A_CONV3X3)
         CMT_REQUIRE(a.conv_c % BK == 0 && a.K == 9 * a.conv_c && a.conv_h > 0 && a.conv_w > 0 &&
                     a.M % (a.conv_h * a.conv_w) == 0, "cmt_gemm: bad conv3x3 geometry");
@@ -433,6 +733,16 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     if (a.c_mode == CMT_C_HEADSPLIT)
         CMT_REQUIRE(a.rows_per_batch > 0 && a.M % a.rows_per_batch == 0, "cmt_gemm: bad head-split rows");
     hipStream_t s = (hipStream_t)stream;
+    if (a.w_dtype != CMT_F32 && a.a_dtype == a.w_dtype) {
+        // LDS-DMA path: 64-deep k stages
+        const int kdiv = a.a_mode == CMT_A_CONV3X3 ? a.conv_c : (a.a_mode == CMT_A_CONV1D3 ? a.K / 3 : a.K);
+        CMT_REQUIRE(kdiv % 64 == 0, "cmt_gemm: compute-dtype A needs K (per tap) % 64 == 0");
+        CMT_REQUIRE(a.ldc % 4 == 0 && (a.R == nullptr || a.ldr % 4 == 0) && a.bias_bstride % 4 == 0,
+                    "cmt_gemm: ldc/ldr/bias_bstride must be multiples of 4");
+        const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
+        if (a.N % 128 == 0 && big_tiles >= 480) return launch_dma<128, 128, 2>(a, s);
+        return launch_dma<64, 64, 4>(a, s);
+    }
     // Tile choice: 128x128 when the grid still fills the chip, else 64x64.
     const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
     if (a.N % 128 == 0 && big_tiles >= 384) return launch_tiles<128, 128>(a, s);

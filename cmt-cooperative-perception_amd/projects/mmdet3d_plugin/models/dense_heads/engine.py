@@ -71,17 +71,21 @@ class HeadEngineMixin:
         return self._pack.get("engine", params, prec.name, build)
 
     # ------------------------------------------------------------------ pieces
-    def _mlp(self, x, w, out=None, *, batch=1, a_bstride=0, c_bstride=0, c_offset=0, M=None):
+    def _mlp(self, x, w, out=None, *, batch=1, a_bstride=0, c_bstride=0, c_offset=0, M=None, R=None, r_offset=0):
         """Linear-ReLU-Linear with the second GEMM optionally scattering rows
-        into a larger buffer (batched)."""
+        into a larger buffer (batched) and adding a residual R laid out like
+        ``out``.  The hidden activation is kept in x's dtype when that is the
+        compute dtype (LDS-DMA operand for the second GEMM)."""
         w0, b0, w2, b2 = w
-        h = native.linear(x, w0, b0, relu=True)
+        hdt = x.dtype if x.dtype == w0.dtype else torch.float32
+        h = native.linear(x, w0, b0, relu=True, out_dtype=hdt)
         if out is None:
             return native.linear(h, w2, b2)
         M = M if M is not None else h.shape[0]
         native.gemm(h, w2, out, M=M, N=w2.shape[0], K=w2.shape[1], lda=h.shape[1], ldw=w2.shape[1],
                     ldc=out.shape[-1], bias=b2, batch=batch, a_bstride=a_bstride * h.shape[1] if batch > 1 else 0,
-                    c_bstride=c_bstride, c_offset=c_offset)
+                    c_bstride=c_bstride, c_offset=c_offset, R=R, ldr=out.shape[-1] if R is not None else 0,
+                    r_bstride=c_bstride if R is not None else 0, r_offset=r_offset)
         return out
 
     def _shared_conv_into(self, x, mem, Nk, pk, prec):
@@ -94,18 +98,22 @@ class HeadEngineMixin:
                     bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B,
                     a_bstride=H * W * Cin, c_bstride=Nk * Cout)
 
-    def _bev_pos_into(self, pos, B, Nk, H, W, pk):
+    def _bev_pos_into(self, pos, B, Nk, H, W, pk, R=None):
+        """bev_pos_embed (cmt_head.py:324-337, 489) into the pos rows of every
+        batch element; with R (the memory rows in the compute dtype) the
+        output is lowp(memory + pos) -- the K-projection operand."""
         C = self.hidden_dim
         cfg = self.train_cfg if self.train_cfg else self.test_cfg
         x_size = cfg["grid_size"][1] // self.downsample_scale
         y_size = cfg["grid_size"][0] // self.downsample_scale
         if x_size * y_size != H * W:
             raise ValueError(f"BEV map {H}x{W} does not match grid_size/downsample ({x_size}x{y_size})")
-        pe = torch.empty((H * W, 2 * C), dtype=torch.float32, device=pos.device)
+        pe_dt = pk["bev"][0].dtype
+        pe = torch.empty((H * W, 2 * C), dtype=pe_dt, device=pos.device)
         native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
-        self._mlp(pe, pk["bev"], pos, batch=B, a_bstride=0, c_bstride=Nk * C, M=H * W)
+        self._mlp(pe, pk["bev"], pos, batch=B, a_bstride=0, c_bstride=Nk * C, M=H * W, R=R)
 
-    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk):
+    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None):
         C = self.hidden_dim
         BV, _, h, w = x_img.shape
         V = BV // B
@@ -113,20 +121,24 @@ class HeadEngineMixin:
         i2l = np.concatenate([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64)) for m in metas])
         i2l = torch.from_numpy(i2l).float().to(pos.device)
         D = self.depth_num
-        coords = torch.empty((BV * h * w, 3 * D), dtype=torch.float32, device=pos.device)
+        w0, b0, w2, b2 = pk["rv"]
+        cdt = w0.dtype if (3 * D) % 64 == 0 else torch.float32
+        coords = torch.empty((BV * h * w, 3 * D), dtype=cdt, device=pos.device)
         native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w, D=D, pad_h=float(pad_h), pad_w=float(pad_w),
                             depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
-        w0, b0, w2, b2 = pk["rv"]
-        hid = native.linear(coords, w0, b0, relu=True)                       # [BV*h*w, 4C]
+        hdt = cdt if cdt == w0.dtype else torch.float32
+        hid = native.linear(coords, w0, b0, relu=True, out_dtype=hdt)       # [BV*h*w, 4C]
         native.gemm(hid, w2, pos, M=V * h * w, N=C, K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
-                    bias=b2, batch=B, a_bstride=V * h * w * hid.shape[1], c_bstride=Nk * C, c_offset=offset * C)
+                    bias=b2, batch=B, a_bstride=V * h * w * hid.shape[1], c_bstride=Nk * C, c_offset=offset * C,
+                    R=R, ldr=C if R is not None else 0, r_bstride=Nk * C if R is not None else 0,
+                    r_offset=offset * C)
 
     def _query_pos(self, B, metas, with_rv, pk):
         C = self.hidden_dim
         ref = self.reference_points.weight.detach().contiguous()
         Nq = ref.shape[0]
         dev = ref.device
-        pe = torch.empty((Nq, 2 * C), dtype=torch.float32, device=dev)
+        pe = torch.empty((Nq, 2 * C), dtype=pk["bev"][0].dtype, device=dev)
         native.pos2embed(ref, pe, n=Nq, F=C, mode=1, pos_stride=3)
         qpos = torch.empty((B * Nq, C), dtype=torch.float32, device=dev)
         self._mlp(pe, pk["bev"], qpos, batch=B, a_bstride=0, c_bstride=Nq * C, M=Nq)
@@ -138,7 +150,7 @@ class HeadEngineMixin:
             i2l = torch.from_numpy(i2l).float().to(dev)
             refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
             D = self.depth_num
-            coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)
+            coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)   # kernel writes fp32
             mask = torch.empty((B * V * Nq,), dtype=torch.float32, device=dev)
             native.rv_query_coords(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
                                    pad_w=float(pad_w), pc_range=self.pc_range)
@@ -165,19 +177,25 @@ class HeadEngineMixin:
             BV, _, hi, wi = x_img.shape
             V, hw = BV // B, hi * wi
         Nk = HW + V * hw
-        mem = torch.empty((B * Nk, C), dtype=torch.float32, device=dev)
-        pos = torch.empty((B * Nk, C), dtype=torch.float32, device=dev)
+        lowp = prec.gemm != torch.float32
+        # fp32 policy: memory / pos rows in fp32.  f16/bf16 policy: the K/V
+        # GEMM operands lowp(memory) and lowp(memory + pos) are written
+        # directly by the conv / layout epilogues and the pos-MLP epilogues.
+        mdt = prec.gemm if lowp else torch.float32
+        mem = torch.empty((B * Nk, C), dtype=mdt, device=dev)
+        pos = torch.empty((B * Nk, C), dtype=mdt, device=dev)
+        R = mem if lowp else None
         if use_bev:
             self._shared_conv_into(x, mem, Nk, pk, prec)
-            self._bev_pos_into(pos, B, Nk, H, W, pk)
+            self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
         if use_img:
             native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C, rows_per_batch=Nk,
                                 row_offset=HW)
-            self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk)
+            self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R)
         qpos = self._query_pos(B, metas, use_img, pk)
         Nq = self.num_query
         self.transformer.decoder.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
-                                          prec=prec)
+                                          prec=prec, kv_operands=(mem, pos) if lowp else None)
         return out
 
     # ------------------------------------------------------------------ task heads

@@ -373,13 +373,19 @@ class PETRTransformerDecoder(nn.Module):
         return self._pack.get("decoder", params, prec.name, build)
 
     def run_rows(self, mem, pos, qpos, *, B, Nk, Nq, out=None, post_flags=native.LN_NAN_TO_NUM, prec=None,
-                 tgt0=None):
+                 tgt0=None, kv_operands=None):
         """Fused decoder.  mem/pos: [B*Nk, C] fp32 batch-major rows, qpos:
         [B*Nq, C] fp32.  Writes the post-normed layer outputs to
-        out [L, B*Nq, C] (fp32) with ``post_flags`` (nan_to_num / max-into)."""
+        out [L, B*Nq, C] (fp32) with ``post_flags`` (nan_to_num / max-into).
+        Under an f16/bf16 policy the producers may hand over the K/V GEMM
+        operands already in the compute dtype: kv_operands = (lowp(mem),
+        lowp(mem + pos)); mem/pos are then unused."""
         if not self.fused_supported():
             raise NotImplementedError("fused decoder supports the CMT post-norm layout (C=256, 8x32 heads)")
         prec = get_precision(prec)
+        if prec.gemm != torch.float32:
+            return self._run_rows_lowp(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
+                                       tgt0=tgt0, kv_operands=kv_operands)
         pk = self.packed(prec)
         L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
         dev = mem.device
@@ -436,4 +442,79 @@ class PETRTransformerDecoder(nn.Module):
             pw, pb, _pe = pk["post"]
             native.layernorm(t1, w2, b2, tgt, rows=rows, C=C, ldx=C, ldy=C, eps=e2, W2=pw, B2=pb, Y2=out,
                              ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
+        return out
+
+    def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands):
+        """run_rows under an f16/bf16 policy: every GEMM operand is produced in
+        the compute dtype by the kernel before it (LayerNorm writes lowp(y) and
+        lowp(y + query_pos) beside the fp32 residual stream, attention writes
+        its output in the compute dtype, FFN fc1 writes its activation in it),
+        so every GEMM stages A and W by LDS-DMA.  The residual stream, the
+        LayerNorm statistics and the decoder outputs stay fp32."""
+        pk = self.packed(prec)
+        L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
+        lp = prec.gemm
+        dev = qpos.device
+        f32 = torch.float32
+        rows = B * Nq
+        if out is None:
+            out = torch.empty((L, rows, C), dtype=f32, device=dev)
+        scale = 1.0 / math.sqrt(32.0)
+        if kv_operands is None:
+            memb = torch.empty((B * Nk, C), dtype=lp, device=dev)
+            mposb = torch.empty_like(memb)
+            native.add_cast(mem, rows=B * Nk, C=C, Yl=memb, Yp=mposb, P=pos)
+        else:
+            memb, mposb = kv_operands
+        # K/V of every layer in one GEMM: K columns read lowp(mem + pos), V columns lowp(mem)
+        kv = torch.empty((B * 2 * L * C * Nk,), dtype=prec.attn, device=dev)
+        native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
+                    A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk)
+        # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114)
+        tgt = tgt0.clone() if tgt0 is not None else torch.zeros((rows, C), dtype=f32, device=dev)
+        tl = torch.empty((rows, C), dtype=lp, device=dev)          # lowp(tgt)
+        tp = torch.empty_like(tl)                                  # lowp(tgt + qpos)
+        native.add_cast(tgt, rows=rows, C=C, Yl=tl, Yp=tp, P=qpos)
+        qkv = torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=dev)
+        qc = torch.empty((B * C * Nq,), dtype=prec.attn, device=dev)
+        ob = torch.empty((rows, C), dtype=lp, device=dev)          # attention output (out-proj operand)
+        t1 = torch.empty((rows, C), dtype=f32, device=dev)
+        t1n = torch.empty_like(t1)
+        o = torch.empty_like(t1)
+        FF = pk["layers"][0]["f1_w"].shape[0]
+        hf = torch.empty((rows, FF), dtype=lp, device=dev)
+        ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
+                       native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
+        ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
+        pw, pb, _pe = pk["post"]
+        for l, lw in enumerate(pk["layers"]):
+            # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
+            native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
+                        A2=tp, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
+            native.attention(qkv, qkv, qkv, ob, B=B, H=H, Nq=Nq, Nk=Nq,
+                             q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
+                             v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
+                             o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
+            native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt, ldr=C)
+            w0, b0, e0 = lw["norms"][0]
+            native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos)
+            # --- cross attention: q = lowp(x + qpos); K/V from the hoisted GEMM
+            native.gemm(tp, lw["ca_wq"], qc, M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
+                        headsplit_rows=Nq)
+            with timed("cross_attn"):
+                native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
+                                 q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
+                                 v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
+                                 v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
+                                 round_output=prec.round_cross_out, fold_scale=True)
+            native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n, ldr=C)
+            w1, b1, e1 = lw["norms"][1]
+            native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl)
+            # --- FFN (fc1 activation written in the compute dtype)
+            native.gemm(tl, lw["f1_w"], hf, M=rows, N=FF, K=C, lda=C, ldw=C, ldc=FF, bias=lw["f1_b"], relu=True)
+            native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o, ldr=C)
+            # --- norms.2 -> next query (fp32 + both lowp operands), fused with post_norm -> out[l]
+            w2, b2, e2 = lw["norms"][2]
+            native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
+                                W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         return out

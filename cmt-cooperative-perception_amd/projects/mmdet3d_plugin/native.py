@@ -11,7 +11,8 @@ import os
 
 import torch
 
-__all__ = ["lib", "available", "gemm", "attention", "layernorm", "pos2embed", "rv_pe_coords",
+__all__ = ["lib", "available", "gemm", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
+           "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
            "voxelize", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
 
@@ -23,6 +24,8 @@ DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
 LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
+A2_ADD, A2_SELECT = 0, 1
+ABI_VERSION = 2
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -33,11 +36,11 @@ _flt = ctypes.c_float
 class GemmArgs(ctypes.Structure):
     _fields_ = [("M", _int), ("N", _int), ("K", _int), ("batch", _int),
                 ("A", _vp), ("lda", _i64), ("a_bstride", _i64), ("a_dtype", _int),
-                ("A2", _vp), ("lda2", _i64), ("a2_cols", _int),
+                ("A2", _vp), ("lda2", _i64), ("a2_cols", _int), ("a2_mode", _int),
                 ("a_mode", _int), ("conv_h", _int), ("conv_w", _int), ("conv_c", _int), ("seg_len", _int),
                 ("W", _vp), ("ldw", _i64), ("w_bstride", _i64), ("w_dtype", _int),
                 ("bias", _vp), ("bias_bstride", _i64),
-                ("R", _vp), ("ldr", _i64), ("r_bstride", _i64),
+                ("R", _vp), ("ldr", _i64), ("r_bstride", _i64), ("r_dtype", _int),
                 ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int),
                 ("c_mode", _int), ("rows_per_batch", _int), ("relu", _int)]
 
@@ -47,9 +50,20 @@ class AttnArgs(ctypes.Structure):
                 ("Q", _vp), ("q_bstride", _i64), ("q_hstride", _i64), ("q_rstride", _i64),
                 ("K", _vp), ("k_bstride", _i64), ("k_hstride", _i64), ("k_rstride", _i64),
                 ("V", _vp), ("v_bstride", _i64), ("v_hstride", _i64), ("v_rstride", _i64),
-                ("O", _vp), ("o_bstride", _i64), ("o_rstride", _i64), ("scale", _flt), ("kv_splits", _int),
+                ("O", _vp), ("o_bstride", _i64), ("o_rstride", _i64), ("o_dtype", _int), ("scale", _flt),
+                ("kv_splits", _int),
                 ("flags", _int),
                 ("workspace", _vp), ("workspace_bytes", _i64)]
+
+
+class LnArgs(ctypes.Structure):
+    _fields_ = [("X", _vp), ("ldx", _i64), ("rows", _int), ("C", _int),
+                ("W", _vp), ("B", _vp), ("eps", _flt),
+                ("Y", _vp), ("ldy", _i64), ("flags", _int),
+                ("W2", _vp), ("B2", _vp), ("Y2", _vp), ("ldy2", _i64), ("flags2", _int),
+                ("lowp_dtype", _int),
+                ("Yl", _vp), ("ldyl", _i64),
+                ("Yp", _vp), ("ldyp", _i64), ("P", _vp), ("ldp", _i64)]
 
 
 _LIB = None
@@ -72,8 +86,10 @@ def _load():
         "cmt_attn_fwd": ([P(AttnArgs), _vp], _int),
         "cmt_layernorm": ([_vp, _i64, _int, _int, _vp, _vp, _flt, _vp, _i64, _int, _vp, _vp, _vp, _i64, _int, _vp],
                           _int),
-        "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _i64, _vp], _int),
-        "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _vp], _int),
+        "cmt_layernorm_ex": ([P(LnArgs), _vp], _int),
+        "cmt_add_cast": ([_vp, _vp, _int, _int, _int, _vp, _vp, _vp], _int),
+        "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _int, _i64, _vp], _int),
+        "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _int, _vp], _int),
         "cmt_rv_query_coords": ([_vp, _int, _int, _int, _int, _flt, _flt, _vp, _vp, P(_flt), _vp, _vp, _vp], _int),
         "cmt_masked_view_sum": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp], _int),
         "cmt_nchw_to_rows": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp], _int),
@@ -88,7 +104,7 @@ def _load():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    if L.cmt_abi_version() != 1:
+    if L.cmt_abi_version() != ABI_VERSION:
         raise RuntimeError("libcmt_hip.so ABI version mismatch")
     return L
 
@@ -142,22 +158,26 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
          a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0, bias_bstride=0,
          r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0):
     """C = act(A W^T + bias) + R with the fused prologue/epilogue of cmt_gemm.
-    Offsets are in elements of the respective tensor."""
+    Offsets are in elements of the respective tensor.  A2 of A's dtype selects
+    (replaces A for output columns < a2_cols); an fp32 A2 beside fp32 A is
+    added on load."""
     _dev(A, W, C, bias, R, A2)
     g = GemmArgs()
     g.M, g.N, g.K, g.batch = M, N, K, batch
     g.A = A.data_ptr() + a_offset * A.element_size()
     g.lda, g.a_bstride, g.a_dtype = lda, a_bstride, DT[A.dtype]
-    g.A2 = None if A2 is None else A2.data_ptr() + a2_offset * 4
+    g.A2 = None if A2 is None else A2.data_ptr() + a2_offset * A2.element_size()
     g.lda2, g.a2_cols = lda2, a2_cols
+    g.a2_mode = A2_ADD if (A2 is None or A.dtype == torch.float32) else A2_SELECT
     g.a_mode = a_mode
     g.conv_h, g.conv_w, g.conv_c = conv
     g.seg_len = seg_len
     g.W, g.ldw, g.w_bstride, g.w_dtype = W.data_ptr(), ldw, w_bstride, DT[W.dtype]
     g.bias = None if bias is None else bias.data_ptr()
     g.bias_bstride = bias_bstride
-    g.R = None if R is None else R.data_ptr() + r_offset * 4
+    g.R = None if R is None else R.data_ptr() + r_offset * R.element_size()
     g.ldr, g.r_bstride = ldr, r_bstride
+    g.r_dtype = F32 if R is None else DT[R.dtype]
     g.C = C.data_ptr() + c_offset * C.element_size()
     g.ldc, g.c_bstride, g.c_dtype = ldc, c_bstride, DT[C.dtype]
     g.c_mode = C_HEADSPLIT if headsplit_rows else C_ROWS
@@ -183,8 +203,11 @@ _WS_CACHE = {}
 
 
 def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, q_offset=0,
-              k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False):
-    """Strides are (batch, head, row) in elements; o_strides = (batch, row)."""
+              k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False,
+              fold_scale=False):
+    """Strides are (batch, head, row) in elements; o_strides = (batch, row).
+    fold_scale lets the kernel fold scale*log2(e) into Q on load (one extra
+    rounding of Q; the f16/bf16 policies only)."""
     _dev(Q, K, V, O)
     a = AttnArgs()
     a.B, a.H, a.Nq, a.Nk, a.dtype = B, H, Nq, Nk, DT[Q.dtype]
@@ -195,10 +218,11 @@ def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_st
     a.k_bstride, a.k_hstride, a.k_rstride = k_strides
     a.V = V.data_ptr() + v_offset * es
     a.v_bstride, a.v_hstride, a.v_rstride = v_strides
-    a.O = O.data_ptr() + o_offset * 4
+    a.O = O.data_ptr() + o_offset * O.element_size()
     a.o_bstride, a.o_rstride = o_strides
+    a.o_dtype = DT[O.dtype]
     a.scale, a.kv_splits = scale, kv_splits
-    a.flags = 1 if round_output else 0
+    a.flags = (1 if round_output else 0) | (2 if fold_scale else 0)
     need = lib().cmt_attn_workspace_bytes(ctypes.byref(a))
     if need > 0:
         if workspace is None or workspace.numel() < need:
@@ -222,16 +246,42 @@ def layernorm(X, W, Bv, Y, *, rows, C, ldx, ldy, eps=1e-5, flags=0, W2=None, B2=
            "cmt_layernorm")
 
 
+def layernorm_ex(X, W, Bv, *, rows, C, ldx, eps=1e-5, Y=None, ldy=0, flags=0, W2=None, B2=None, Y2=None, ldy2=0,
+                 flags2=0, Yl=None, Yp=None, P=None, y2_offset=0):
+    """LayerNorm with optional second LN (Y2) and compute-dtype copies
+    Yl = lowp(y), Yp = lowp(y + P) (rows of width C, contiguous)."""
+    _dev(X, W, Bv, Y, W2, B2, Y2, Yl, Yp, P)
+    a = LnArgs()
+    a.X, a.ldx, a.rows, a.C = X.data_ptr(), ldx, rows, C
+    a.W, a.B, a.eps = W.data_ptr(), Bv.data_ptr(), eps
+    a.Y, a.ldy, a.flags = _p(Y), ldy, flags
+    a.W2, a.B2 = _p(W2), _p(B2)
+    a.Y2 = None if Y2 is None else Y2.data_ptr() + 4 * y2_offset
+    a.ldy2, a.flags2 = ldy2, flags2
+    low = Yl if Yl is not None else Yp
+    a.lowp_dtype = DT[low.dtype] if low is not None else BF16
+    a.Yl, a.ldyl = _p(Yl), C
+    a.Yp, a.ldyp, a.P, a.ldp = _p(Yp), C, _p(P), C
+    _check(lib().cmt_layernorm_ex(ctypes.byref(a), _stream()), "cmt_layernorm_ex")
+
+
+def add_cast(X, *, rows, C, Yl=None, Yp=None, P=None):
+    _dev(X, Yl, Yp, P)
+    low = Yl if Yl is not None else Yp
+    _check(lib().cmt_add_cast(X.data_ptr(), _p(P), rows, C, DT[low.dtype], _p(Yl), _p(Yp), _stream()),
+           "cmt_add_cast")
+
+
 def pos2embed(pos, out, *, n, F, mode=0, pos_stride=2, grid=(0, 0), ldo=None):
     _dev(pos, out)
-    _check(lib().cmt_pos2embed(_p(pos), pos_stride, n, F, mode, grid[0], grid[1], _p(out),
+    _check(lib().cmt_pos2embed(_p(pos), pos_stride, n, F, mode, grid[0], grid[1], _p(out), DT[out.dtype],
                                ldo if ldo is not None else 2 * F, _stream()), "cmt_pos2embed")
 
 
 def rv_pe_coords(i2l, out, *, BV, h, w, D, pad_h, pad_w, depth_max, pc_range):
     _dev(i2l, out)
     _check(lib().cmt_rv_pe_coords(BV, h, w, D, pad_h, pad_w, depth_max, _p(i2l), _farr(pc_range, 6), _p(out),
-                                  _stream()), "cmt_rv_pe_coords")
+                                  DT[out.dtype], _stream()), "cmt_rv_pe_coords")
 
 
 def rv_query_coords(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w, pc_range):

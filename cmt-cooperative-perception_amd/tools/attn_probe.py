@@ -1,0 +1,43 @@
+"""Run the CMT-L cross-attention core (900 queries x 32400 keys, 8 heads,
+bf16) a few times -- a small target for rocprofv3 counter passes.
+
+    python cmt-cooperative-perception_amd/tools/attn_probe.py [--fold] [--splits S] [--iters N]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "cmt-cooperative-perception_amd"))
+
+import torch  # noqa: E402
+
+from projects.mmdet3d_plugin import native as N  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fold", action="store_true")
+    ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--nk", type=int, default=32400)
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    B, H, Nq, Nk = 1, 8, 900, args.nk
+    g = torch.Generator(device="cpu").manual_seed(0)
+    q = torch.randn(B * H * Nq * 32, generator=g).bfloat16().to(dev)
+    k = torch.randn(B * H * Nk * 32, generator=g).bfloat16().to(dev)
+    v = torch.randn(B * H * Nk * 32, generator=g).bfloat16().to(dev)
+    O = torch.empty(B * Nq * H * 32, dtype=torch.bfloat16, device=dev)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+    for _ in range(args.iters):
+        N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(H * Nq * 32, Nq * 32, 32),
+                    k_strides=(H * Nk * 32, Nk * 32, 32), v_strides=(H * Nk * 32, Nk * 32, 32),
+                    o_strides=(Nq * H * 32, H * 32), scale=32 ** -0.5, kv_splits=args.splits, workspace=ws,
+                    fold_scale=args.fold)
+    torch.cuda.synchronize()
+    print("ok")
+
+
+if __name__ == "__main__":
+    main()

@@ -16,18 +16,22 @@ import torch  # noqa: E402
 from projects.mmdet3d_plugin import native as N  # noqa: E402
 
 
-def timeit(fn, reps=20, warm=3):
+def timeit(fn, reps=5, inner=50, warm=3):
+    """Median over `reps` of the mean time of `inner` back-to-back launches
+    (queued ahead, so host-side argument packing does not show)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(2_000_000)   # let the host queue the launches ahead of the GPU
         a.record()
-        fn()
+        for _ in range(inner):
+            fn()
         b.record()
         b.synchronize()
-        ts.append(a.elapsed_time(b))
+        ts.append(a.elapsed_time(b) / inner)
     ts.sort()
     return ts[len(ts) // 2] * 1e3   # us
 
@@ -41,6 +45,8 @@ def gemm_case(name, M, Nn, K, dt, a_f32=True, A2_cols=0, out_dt=torch.float32, h
     W = (torch.randn(Nn, K, device=dev) / math.sqrt(K)).to(dt)
     bias = torch.randn(Nn, device=dev)
     A2 = torch.randn_like(A) if A2_cols else None
+    if conv is None and K % 64:   # pragma: no cover
+        raise ValueError(K)
     Rt = torch.randn(M, Nn, device=dev) if R else None
     C = torch.empty(M * Nn * batch, dtype=out_dt, device=dev)
     kw = dict(M=M, N=Nn, K=K, lda=A.shape[1], ldw=K, ldc=Nn, bias=bias, relu=relu, R=Rt, ldr=Nn, A2=A2,
@@ -49,10 +55,16 @@ def gemm_case(name, M, Nn, K, dt, a_f32=True, A2_cols=0, out_dt=torch.float32, h
         kw.update(a_mode=N.A_CONV3X3, conv=conv, batch=batch, a_bstride=M * conv[2], c_bstride=M * Nn)
     us = timeit(lambda: N.gemm(A, W, C, **kw))
     tf = 2.0 * M * Nn * K * batch / (us * 1e-6) / 1e12
-    print(f"gemm {name:28s} M={M:6d} N={Nn:5d} K={K:5d} {str(dt)[6:]:9s} {us:9.2f} us {tf:8.1f} TF/s", flush=True)
+    line = f"gemm {name:28s} M={M:6d} N={Nn:5d} K={K:5d} {str(dt)[6:]:9s} {us:9.2f} us {tf:8.1f} TF/s"
+    if conv is None and batch == 1:   # hipBLASLt on the same shape, same dtype A
+        Al = A.to(dt)
+        Ct = torch.empty(M, Nn, dtype=dt, device=dev)
+        ut = timeit(lambda: torch.matmul(Al, W.t(), out=Ct))
+        line += f"   | torch {ut:8.2f} us"
+    print(line, flush=True)
 
 
-def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0):
+def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0, fold=False):
     dev = torch.device("cuda")
     q = torch.randn(B * H * Nq * 32, device=dev).to(dt)
     k = torch.randn(B * H * Nk * 32, device=dev).to(dt)
@@ -63,11 +75,12 @@ def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0):
     def run():
         N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(H * Nq * 32, Nq * 32, 32),
                     k_strides=(H * Nk * 32, Nk * 32, 32), v_strides=(H * Nk * 32, Nk * 32, 32),
-                    o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32), kv_splits=splits, workspace=ws)
+                    o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32), kv_splits=splits, workspace=ws,
+                    fold_scale=fold)
     us = timeit(run)
     tf = 4.0 * B * Nq * Nk * H * 32 / (us * 1e-6) / 1e12
-    print(f"attn {name:28s} Nq={Nq:5d} Nk={Nk:6d} {str(dt)[6:]:9s} splits={splits:3d} {us:9.2f} us {tf:8.1f} TF/s",
-          flush=True)
+    print(f"attn {name:28s} Nq={Nq:5d} Nk={Nk:6d} {str(dt)[6:]:9s} splits={splits:3d} fold={int(fold)} {us:9.2f} us "
+          f"{tf:8.1f} TF/s", flush=True)
 
 
 def main():
@@ -88,11 +101,21 @@ def main():
         gemm_case("ffn fc2 (+res)", 900, 256, 1024, bf, R=True)
         gemm_case("ffn fc1 f32", 900, 1024, 256, torch.float32, relu=True)
         gemm_case("square 4096 bf16", 4096, 4096, 4096, bf, a_f32=False)
+        print("-- compute-dtype A (LDS-DMA path)")
+        gemm_case("kv (select)", 32400, 3072, 256, bf, a_f32=False, A2_cols=1536, out_dt=bf, headsplit=32400)
+        gemm_case("bev mlp fc1 (relu)", 32400, 256, 512, bf, a_f32=False, relu=True, out_dt=bf)
+        gemm_case("bev mlp fc2 (+R)", 32400, 256, 256, bf, a_f32=False, R=True, out_dt=bf)
+        gemm_case("self qkv (select)", 900, 768, 256, bf, a_f32=False, A2_cols=512, out_dt=bf, headsplit=900)
+        gemm_case("out proj (+res)", 900, 256, 256, bf, a_f32=False, R=True)
+        gemm_case("ffn fc1 (relu)", 900, 1024, 256, bf, a_f32=False, relu=True, out_dt=bf)
+        gemm_case("ffn fc2 (+res)", 900, 256, 1024, bf, a_f32=False, R=True)
     if args.only in ("", "attn"):
         for s in (0, 8, 16, 32):
-            attn_case("cross 900x32400", 900, 32400, bf, splits=s)
+            for fold in (False, True):
+                attn_case("cross 900x32400", 900, 32400, bf, splits=s, fold=fold)
         attn_case("cross fp16", 900, 32400, torch.float16)
         attn_case("self 900x900", 900, 900, bf)
+        attn_case("self 900x900", 900, 900, bf, fold=True)
         attn_case("self f32", 900, 900, torch.float32)
         attn_case("cross fusion 900x56400", 900, 56400, bf)
 

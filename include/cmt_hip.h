@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 1
+#define CMT_ABI_VERSION 2
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -55,26 +55,34 @@ const char* cmt_last_error(void);
  *   bev_embedding / rv_embedding MLPs   models/dense_heads/cmt_head.py:292-301
  *   shared_conv Conv2d 3x3 (+BN fold)   models/dense_heads/cmt_head.py:280-287  (a_mode = CONV3X3)
  *   SeparateTaskHead grouped Conv1d     models/dense_heads/cmt_head.py:136-159  (a_mode = CONV1D3, batch = groups)
- * Aeff = A (+ A2 for output columns n < a2_cols; the positional-encoding add
- * `key = key + key_pos`, petr_transformer.py:296-299, fused into the load).
+ * Output columns n < a2_cols see a modified A (the positional-encoding add
+ * `key = key + key_pos`, petr_transformer.py:296-299):
+ *   a2_mode CMT_A2_ADD     Aeff = A + A2 (both fp32, added on load);
+ *   a2_mode CMT_A2_SELECT  Aeff = A2 (same dtype/strides as A: the caller
+ *                          already holds the sum, e.g. written by the LN that
+ *                          produced A), so one launch serves Q|K (pos) and V.
  * Compute dtype = w_dtype: CMT_F32 (exact-f32 MFMA 32x32x2), CMT_F16 or
- * CMT_BF16 (MFMA 32x32x16, A converted on load, fp32 accumulate).
- * Requirements: N % 64 == 0, K % 32 == 0, 16-byte aligned A/W rows.
+ * CMT_BF16 (MFMA 32x32x16, fp32 accumulate).  With A in the compute dtype the
+ * tiles are staged by LDS-DMA (global_load_lds); fp32 A is converted on load.
+ * R may be fp32 or the compute dtype (r_dtype).
+ * Requirements: N % 64 == 0, K % 32 == 0 (K % 64 for compute-dtype A),
+ * 16-byte aligned A/W rows, ldc/ldr multiples of 4.
  * ------------------------------------------------------------------------ */
 enum cmt_gemm_amode { CMT_A_ROWS = 0, CMT_A_CONV3X3 = 1, CMT_A_CONV1D3 = 2 };
 enum cmt_gemm_cmode { CMT_C_ROWS = 0, CMT_C_HEADSPLIT = 1 };
+enum cmt_gemm_a2mode { CMT_A2_ADD = 0, CMT_A2_SELECT = 1 };
 
 typedef struct cmt_gemm_args {
     int M, N, K;
     int batch;                 /* grid z; per-batch strides below (elements) */
     const void* A; int64_t lda; int64_t a_bstride; int a_dtype;
-    const float* A2; int64_t lda2; int a2_cols;
+    const void* A2; int64_t lda2; int a2_cols; int a2_mode;
     int a_mode;                /* cmt_gemm_amode */
     int conv_h, conv_w, conv_c;/* CONV3X3: NHWC input [M/(h*w)][h][w][c], K = 9*c */
     int seg_len;               /* CONV1D3: rows form segments of seg_len (zero pad), K = 3*C */
     const void* W; int64_t ldw; int64_t w_bstride; int w_dtype;
     const float* bias; int64_t bias_bstride;
-    const float* R; int64_t ldr; int64_t r_bstride;
+    const void* R; int64_t ldr; int64_t r_bstride; int r_dtype;
     void* C; int64_t ldc; int64_t c_bstride; int c_dtype;
     int c_mode;                /* cmt_gemm_cmode; HEADSPLIT: C[(b*(N/32)+n/32)*rows_per_batch + r][32] */
     int rows_per_batch;
@@ -95,11 +103,17 @@ int cmt_gemm(const cmt_gemm_args* args, void* stream);
  * (head-split layout: rstride = 32; token-major [B,S,H*32]: rstride = H*32;
  * sequence-first [S,B,H*32]: rstride = B*H*32).  Row strides must keep
  * 16-byte alignment (multiples of 8 elements).
- * Output O is fp32 with heads concatenated per row (normalised).
+ * Output O (o_dtype: fp32, or f16/bf16 when it only feeds the out-projection
+ * GEMM) has the heads concatenated per row (normalised).
  * Nk is split into kv_splits chunks processed by separate workgroups and
  * merged by a combine pass (workspace: cmt_attn_workspace_bytes).
  * ------------------------------------------------------------------------ */
-enum { CMT_ATTN_ROUND_OUTPUT = 1 };
+/* flags: CMT_ATTN_ROUND_OUTPUT  round O to dtype (flash-attn returns fp16)
+ *        CMT_ATTN_FOLD_SCALE    the kernel may fold scale*log2(e) into Q when
+ *                               it loads Q (one extra rounding of Q in the
+ *                               compute dtype; used by the f16/bf16 policies,
+ *                               not by the reference-numerics policy) */
+enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2 };
 
 typedef struct cmt_attn_args {
     int B, H, Nq, Nk;
@@ -107,10 +121,11 @@ typedef struct cmt_attn_args {
     const void* Q; int64_t q_bstride, q_hstride, q_rstride;
     const void* K; int64_t k_bstride, k_hstride, k_rstride;
     const void* V; int64_t v_bstride, v_hstride, v_rstride;
-    float* O; int64_t o_bstride, o_rstride;  /* O[b*o_bstride + q*o_rstride + h*32 + d] */
+    void* O; int64_t o_bstride, o_rstride;   /* O[b*o_bstride + q*o_rstride + h*32 + d] */
+    int o_dtype;               /* CMT_F32 / CMT_F16 / CMT_BF16 */
     float scale;               /* softmax scale, usually 1/sqrt(32) */
     int kv_splits;             /* 0 = choose automatically */
-    int flags;                 /* CMT_ATTN_ROUND_OUTPUT: round O to dtype (flash-attn returns fp16) */
+    int flags;                 /* CMT_ATTN_ROUND_OUTPUT | CMT_ATTN_FOLD_SCALE */
     void* workspace; int64_t workspace_bytes;
 } cmt_attn_args;
 
@@ -134,14 +149,35 @@ int cmt_layernorm(const float* X, int64_t ldx, int rows, int C,
                   const float* W2, const float* B2, float* Y2, int64_t ldy2, int flags2,
                   void* stream);
 
+/* cmt_layernorm_ex: cmt_layernorm plus the next GEMMs' operands in the
+ * compute dtype (lowp_dtype), written from the same registers:
+ *   Yl[row] = lowp(y)            (e.g. the FFN / V-projection input)
+ *   Yp[row] = lowp(y + P[row])   (query + query_pos, petr_transformer.py:296-297)
+ * Y may be NULL when only the compute-dtype copies are needed. */
+typedef struct cmt_ln_args {
+    const float* X; int64_t ldx; int rows; int C;
+    const float* W; const float* B; float eps;
+    float* Y; int64_t ldy; int flags;
+    const float* W2; const float* B2; float* Y2; int64_t ldy2; int flags2;
+    int lowp_dtype;
+    void* Yl; int64_t ldyl;
+    void* Yp; int64_t ldyp; const float* P; int64_t ldp;
+} cmt_ln_args;
+int cmt_layernorm_ex(const cmt_ln_args* args, void* stream);
+
+/* cmt_add_cast: Yl = lowp(X), Yp = lowp(X + P) over rows x C (either output
+ * may be NULL) -- the decoder's first-layer operands from the initial target. */
+int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,
+                 void* stream);
+
 /* ------------------------------------------------------------------------
  * Coordinate encodings.
  * cmt_pos2embed: cmt_head.py:40-50.  pos [n, pos_stride] (x, y in the first two
- *   fp32 lanes), out [n, 2F] fp32 (F = num_pos_feats); mode 1 applies
+ *   fp32 lanes), out [n, 2F] of odtype (F = num_pos_feats); mode 1 applies
  *   sigmoid(inverse_sigmoid(p)) first (query_embed, cmt_head.py:470).
  *   If pos == NULL the BEV grid centres (coords_bev, cmt_head.py:324-337) of a
  *   grid_h x grid_w map are generated in place of the input.
- * cmt_rv_pe_coords: _rv_pe geometry (cmt_head.py:417-432): out [BV*h*w, 3*D]
+ * cmt_rv_pe_coords: _rv_pe geometry (cmt_head.py:417-432): out [BV*h*w, 3*D] (odtype)
  *   normalised lidar coordinates of D depth samples per image token; i2l is a
  *   [BV,4,4] fp32 device array of inv(lidar2img) (fp64 host inverse).
  * cmt_rv_query_coords: _rv_query_embed geometry (cmt_head.py:446-463):
@@ -151,9 +187,9 @@ int cmt_layernorm(const float* X, int64_t ldx, int rows, int C,
  *   Y[b,q,:] += sum_v X[b,v,q,:] * mask[b,v,q].
  * ------------------------------------------------------------------------ */
 int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F, int mode,
-                  int grid_h, int grid_w, float* out, int64_t ldo, void* stream);
+                  int grid_h, int grid_w, void* out, int odtype, int64_t ldo, void* stream);
 int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float pad_w, float depth_max,
-                     const float* i2l, const float* pc_range6, float* out, void* stream);
+                     const float* i2l, const float* pc_range6, void* out, int odtype, void* stream);
 int cmt_rv_query_coords(const float* ref, int B, int V, int Nq, int D, float pad_h, float pad_w,
                         const float* l2i, const float* i2l, const float* pc_range6,
                         float* out, float* mask, void* stream);

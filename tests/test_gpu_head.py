@@ -14,7 +14,14 @@ center/height normalised by the point-cloud range extent
   * precision 'ref' vs oracle with the reference's numerics: max <= 2.5e-3,
     mean <= 5e-4 (the measured fp16-core noise floor; typical max 2e-4..1e-3)
   * precision 'ref' vs oracle exact fp32 math:               max <= 5e-3
-  * precision 'bf16' (bench policy) vs oracle fp32:          max <= 6e-2 (reported)
+  Each bound is raised to 1.5x the reference numerics' OWN deviation from
+  exact fp32 on that case (oracle fp16 core vs oracle fp32, measured in the
+  test) when that is larger -- e.g. the image-only head, whose larger outputs
+  (|rot| ~ 11) put the reference's fp16 noise at ~7e-3 max / 9e-4 mean.
+  * precision 'bf16' (the bench policy, BASELINE.json configs[1]) vs oracle
+    fp32: max abs error of each output <= 2.5 % of that output's scale
+    (center/height: the range extent as above; others: max |value|); bf16
+    keeps 8 significant bits (2^-9 = 0.2 % per rounding); reported.
 """
 import pytest
 import torch
@@ -36,6 +43,11 @@ def _cmp(got, ref, pc_range, reduce="max"):
 
 
 def _check(got, refs, pc_range, tol16=2.5e-3, tol16_mean=5e-4, tol32=5e-3):
+    floor = max(_cmp(refs["fp16"], refs["fp32"], pc_range).values())
+    floor_mean = max(_cmp(refs["fp16"], refs["fp32"], pc_range, "mean").values())
+    tol16, tol32 = max(tol16, 1.5 * floor), max(tol32, 1.5 * floor)
+    tol16_mean = max(tol16_mean, 1.5 * floor_mean)
+    print(f"reference fp16-core noise floor: max {floor:.2e} mean {floor_mean:.2e}")
     e16 = _cmp(got, refs["fp16"], pc_range)
     m16 = _cmp(got, refs["fp16"], pc_range, "mean")
     e32 = _cmp(got, refs["fp32"], pc_range)
@@ -94,9 +106,19 @@ def test_head_parity(dev, name, variant, Nq, L, grid, B, cams):
     got = _run(head, dev, "ref", lambda: head([x.to(dev)], [xi.to(dev)] if xi is not None else None, metas))
     _check([g[0] for g in got], refs, oc["pc_range"])
     gotb = _run(head, dev, "bf16", lambda: head([x.to(dev)], [xi.to(dev)] if xi is not None else None, metas))
-    errb = _cmp([g[0] for g in gotb], refs["fp32"], oc["pc_range"])
-    print("bf16 max err", max(errb.values()))
-    assert max(errb.values()) <= 6e-2, errb
+    _check_bf16(gotb, refs["fp32"], oc["pc_range"])
+
+
+def _check_bf16(gotb, ref, pc_range, tol=2.5e-2):
+    ext = {"center": max(pc_range[3] - pc_range[0], pc_range[4] - pc_range[1]), "height": pc_range[5] - pc_range[2]}
+    rel = {}
+    for t, (g, r) in enumerate(zip([g[0] for g in gotb], ref)):
+        for k in KEYS:
+            rr = r[k].double()
+            scale = ext.get(k, max(rr.abs().max().item(), 1e-6))
+            rel[f"{t}.{k}"] = (g[k].detach().cpu().double() - rr).abs().max().item() / scale
+    print("bf16 max rel err", max(rel.values()), rel)
+    assert max(rel.values()) <= tol, rel
 
 
 def test_image_head_parity(dev):
@@ -118,6 +140,7 @@ def test_image_head_parity(dev):
     refs = _refs(O, lambda c: O.head_forward(oc, sd, None, xi, metas, "image", cross_core=c, self_core="fp32"))
     got = _run(head, dev, "ref", lambda: head([None], [xi.to(dev)], metas))
     _check([g[0] for g in got], refs, oc["pc_range"])
+    _check_bf16(_run(head, dev, "bf16", lambda: head([None], [xi.to(dev)], metas)), refs["fp32"], oc["pc_range"])
 
 
 @pytest.mark.parametrize("variant,name", [("fusion", "cmtcoop_fusion_tumtraf"), ("lidar", "cmtcoop_lidar_tumtraf")])
@@ -138,10 +161,12 @@ def test_coop_parity(dev, variant, name):
     agents = [("vehicle_", xv, iv), ("infrastructure_", xi_, ii)]
     refs = _refs(O, lambda c: O.head_coop_forward(oc, sd, agents, metas, variant, cross_core=c, self_core="fp32"))
     d = dev
-    got = _run(head, dev, "ref", lambda: head([xv.to(d)], [xi_.to(d)],
-                                              [iv.to(d)] if iv is not None else None,
-                                              [ii.to(d)] if ii is not None else None, metas))
+    def fwd():
+        return head([xv.to(d)], [xi_.to(d)], [iv.to(d)] if iv is not None else None,
+                    [ii.to(d)] if ii is not None else None, metas)
+    got = _run(head, dev, "ref", fwd)
     _check([g[0] for g in got], refs, oc["pc_range"])
+    _check_bf16(_run(head, dev, "bf16", fwd), refs["fp32"], oc["pc_range"])
 
 
 def test_coop_identical_agents_equals_single(dev):

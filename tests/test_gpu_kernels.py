@@ -97,15 +97,97 @@ def test_gemm_conv1d3_grouped(N, dev):
     assert (out.cpu().double() - ref).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,N_,K,r_lowp,out_lowp", [(900, 256, 256, False, False), (130, 768, 512, True, True),
+                                                    (8200, 1024, 256, True, False), (64, 1024, 192, False, True),
+                                                    (900, 256, 1024, False, False)])
+def test_gemm_dma_lowp_a(N, dev, dt, M, N_, K, r_lowp, out_lowp):
+    """A already in the compute dtype: the LDS-DMA kernel (both tile shapes,
+    ragged M, bf16/fp32 residual and output)."""
+    g = torch.Generator().manual_seed(M * 7 + N_ + K)
+    A = torch.randn(M, K, generator=g).to(dt)
+    W = (torch.randn(N_, K, generator=g) / math.sqrt(K)).to(dt)
+    b = torch.randn(N_, generator=g)
+    R = torch.randn(M, N_, generator=g)
+    if r_lowp:
+        R = R.to(dt)
+    C = torch.empty(M, N_, device=dev, dtype=dt if out_lowp else torch.float32)
+    N.gemm(A.to(dev), W.to(dev), C, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_, bias=b.to(dev), relu=True,
+           R=R.to(dev), ldr=N_)
+    ref = torch.relu(A.double() @ W.double().T + b.double()) + R.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    tol = 5e-3 + (ref.abs().max().item() * (2 ** -7 if out_lowp else 0))
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_gemm_dma_select_headsplit(N, dev, dt):
+    """A2 select mode: columns < a2_cols read A2 (e.g. LN(x)+pos written by the
+    LN kernel), the rest read A; head-split [B][N/32][S][32] output."""
+    g = torch.Generator().manual_seed(11)
+    B, S, C, K = 2, 300, 768, 256
+    A = torch.randn(B * S, K, generator=g).to(dt)
+    A2 = torch.randn(B * S, K, generator=g).to(dt)
+    W = (torch.randn(C, K, generator=g) / 16).to(dt)
+    bias = torch.randn(C, generator=g)
+    Y = torch.empty(B * C * S, dtype=dt, device=dev)
+    N.gemm(A.to(dev), W.to(dev), Y, M=B * S, N=C, K=K, lda=K, ldw=K, ldc=0, bias=bias.to(dev),
+           A2=A2.to(dev), lda2=K, a2_cols=512, headsplit_rows=S)
+    qk = A2.double() @ W.double()[:512].T + bias.double()[:512]
+    v = A.double() @ W.double()[512:].T + bias.double()[512:]
+    ref = torch.cat([qk, v], 1).view(B, S, 24, 32).permute(0, 2, 1, 3).reshape(-1)
+    got = Y.cpu().double()
+    rel = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < 1e-2, rel
+
+
+def test_gemm_dma_conv1d3_lowp(N, dev):
+    g = torch.Generator().manual_seed(12)
+    L, B, Nq, C, O = 3, 2, 37, 256, 128
+    x = torch.randn(L, B * Nq, C, generator=g).bfloat16()
+    w = (torch.randn(L * O, C, 3, generator=g) / 30).bfloat16()
+    wp = w.view(L, O, C, 3).permute(0, 1, 3, 2).reshape(L, O, 3 * C).contiguous()
+    out = torch.empty(L, B * Nq, O, device=dev)
+    N.gemm(x.to(dev), wp.to(dev), out, M=B * Nq, N=O, K=3 * C, lda=C, ldw=3 * C, ldc=O, batch=L,
+           a_bstride=B * Nq * C, w_bstride=O * 3 * C, c_bstride=B * Nq * O, a_mode=N.A_CONV1D3, seg_len=Nq)
+    xin = x.view(L, B, Nq, C).permute(1, 0, 3, 2).reshape(B, L * C, Nq).double()
+    ref = torch.nn.functional.conv1d(xin, w.double(), padding=1, groups=L)
+    ref = ref.view(B, L, O, Nq).permute(1, 0, 3, 2).reshape(L, B * Nq, O)
+    assert (out.cpu().double() - ref).abs().max().item() < 1e-3
+
+
+def test_gemm_dma_conv3x3_big(N, dev):
+    """Implicit 3x3 conv on the 128x128 DMA tiles (gathered rows, zero page)."""
+    g = torch.Generator().manual_seed(13)
+    B, Cin, H, W, Cout = 1, 128, 61, 67, 256
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / 34
+    b = torch.randn(Cout, generator=g)
+    xin = torch.empty(B * H * W, Cin, dtype=torch.bfloat16, device=dev)
+    N.nchw_to_rows(x.to(dev), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).bfloat16().to(dev).contiguous()
+    out = torch.empty((B * H * W, Cout), dtype=torch.bfloat16, device=dev)
+    N.gemm(xin, wp, out, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout, bias=b.to(dev), relu=True,
+           a_mode=N.A_CONV3X3, conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin, c_bstride=H * W * Cout)
+    ref = torch.relu(torch.nn.functional.conv2d(_rt(x, torch.bfloat16), _rt(w, torch.bfloat16), b.double(),
+                                                padding=1))
+    ref = ref.flatten(2).permute(0, 2, 1).reshape(-1, Cout)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err < 1e-2 + ref.abs().max().item() * 2 ** -8, err
+
+
 def _attn_ref(q, k, v, scale):
     s = (q.double() @ k.double().transpose(-1, -2)) * scale
     return torch.softmax(s, -1) @ v.double()
 
 
+@pytest.mark.parametrize("fold", [False, True])
 @pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("B,H,Nq,Nk,splits", [(1, 8, 900, 32400, 0), (2, 8, 130, 1000, 0), (1, 2, 33, 65, 1),
                                               (1, 8, 900, 900, 0), (1, 1, 1, 1, 1), (2, 3, 200, 4097, 3)])
-def test_attention(N, dev, dt, B, H, Nq, Nk, splits):
+def test_attention(N, dev, dt, B, H, Nq, Nk, splits, fold):
+    if fold and dt == torch.float32:
+        pytest.skip("the exact-f32 kernel never folds the scale")
     g = torch.Generator().manual_seed(B * 1000 + Nk)
     q = (torch.randn(B, H, Nq, 32, generator=g) * 1.5).to(dt)
     k = (torch.randn(B, H, Nk, 32, generator=g) * 1.5).to(dt)
@@ -114,7 +196,7 @@ def test_attention(N, dev, dt, B, H, Nq, Nk, splits):
     N.attention(q.to(dev), k.to(dev), v.to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk,
                 q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
                 v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
-                kv_splits=splits)
+                kv_splits=splits, fold_scale=fold)
     ref = _attn_ref(q, k, v, 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
     err = (O.cpu().double() - ref).abs().max().item()
     tol = {torch.float32: 2e-5, torch.float16: 3e-3, torch.bfloat16: 2e-2}[dt]
@@ -129,11 +211,11 @@ def test_attention_spike_rescale(N, dev):
     k = (torch.randn(B, H, Nk, 32, generator=g) * 0.1).half()
     k[0, 0, 1900] = q[0, 0, 5] * 4          # spike for query 5 in a late tile
     v = torch.randn(B, H, Nk, 32, generator=g).half()
-    for splits in (1, 4):
+    for splits, fold in ((1, False), (4, False), (1, True), (4, True)):
         O = torch.empty(B, Nq, 32, device=dev)
         N.attention(q.to(dev), k.to(dev), v.to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * 32, Nq * 32, 32),
                     k_strides=(Nk * 32, Nk * 32, 32), v_strides=(Nk * 32, Nk * 32, 32), o_strides=(Nq * 32, 32),
-                    scale=1 / math.sqrt(32), kv_splits=splits)
+                    scale=1 / math.sqrt(32), kv_splits=splits, fold_scale=fold)
         ref = _attn_ref(q, k, v, 1 / math.sqrt(32))[0].transpose(0, 1).reshape(Nq, 32)
         assert (O.cpu().double()[0] - ref).abs().max().item() < 3e-3
 
@@ -172,6 +254,60 @@ def test_layernorm_fused_post(N, dev):
     assert (Y.cpu()[ok] - r1[ok]).abs().max().item() < 1e-4
     assert torch.isfinite(Y2.cpu()).all()
     assert (Y2.cpu()[ok] - r2[ok]).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("lp", [torch.float16, torch.bfloat16])
+def test_layernorm_ex_lowp_outputs(N, dev, lp):
+    """lowp(y) and lowp(y + P) written beside the fp32 output (decoder operands)."""
+    g = torch.Generator().manual_seed(9)
+    rows, C = 301, 256
+    x = torch.randn(rows, C, generator=g) * 2
+    w, b = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    P = torch.randn(rows, C, generator=g)
+    Y = torch.empty(rows, C, device=dev)
+    Yl = torch.empty(rows, C, dtype=lp, device=dev)
+    Yp = torch.empty(rows, C, dtype=lp, device=dev)
+    N.layernorm_ex(x.to(dev), w.to(dev), b.to(dev), rows=rows, C=C, ldx=C, Y=Y, ldy=C, Yl=Yl, Yp=Yp, P=P.to(dev))
+    r = torch.nn.functional.layer_norm(x, (C,), w, b, 1e-5)
+    assert (Y.cpu() - r).abs().max().item() < 1e-4
+    assert torch.equal(Yl.cpu(), Y.cpu().to(lp))
+    assert torch.equal(Yp.cpu(), (Y.cpu() + P).to(lp))
+    # add_cast: the first-layer operands from the initial target
+    Zl = torch.empty_like(Yl)
+    Zp = torch.empty_like(Yp)
+    N.add_cast(Y, rows=rows, C=C, Yl=Zl, Yp=Zp, P=P.to(dev))
+    assert torch.equal(Zl, Yl) and torch.equal(Zp, Yp)
+
+
+@pytest.mark.parametrize("odt", [torch.float16, torch.bfloat16])
+def test_attention_lowp_output(N, dev, odt):
+    g = torch.Generator().manual_seed(21)
+    B, H, Nq, Nk = 1, 8, 200, 3000
+    q = torch.randn(B, H, Nq, 32, generator=g)
+    k = torch.randn(B, H, Nk, 32, generator=g)
+    v = torch.randn(B, H, Nk, 32, generator=g)
+    dt = torch.bfloat16
+    O32 = torch.empty(B, Nq, H * 32, device=dev)
+    Ol = torch.empty(B, Nq, H * 32, device=dev, dtype=odt)
+    for O in (O32, Ol):
+        N.attention(q.to(dt).to(dev), k.to(dt).to(dev), v.to(dt).to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk,
+                    q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                    v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=32 ** -0.5)
+    assert torch.equal(Ol.cpu(), O32.cpu().to(odt))
+
+
+def test_pos2embed_lowp_matches_f32(N, dev):
+    pos = torch.rand(1000, 3, device=dev)
+    o32 = torch.empty(1000, 512, device=dev)
+    ob = torch.empty(1000, 512, device=dev, dtype=torch.bfloat16)
+    N.pos2embed(pos, o32, n=1000, F=256, mode=1, pos_stride=3)
+    N.pos2embed(pos, ob, n=1000, F=256, mode=1, pos_stride=3)
+    assert torch.equal(ob, o32.to(torch.bfloat16))
+    g32 = torch.empty(180 * 180, 512, device=dev)
+    N.pos2embed(None, g32, n=180 * 180, F=256, grid=(180, 180))
+    from oracle import cmt_oracle as O
+    ref = O.pos2embed(O.coords_bev([1440, 1440, 40], 8), 256)
+    assert (g32.cpu() - ref).abs().max().item() < 2e-5
 
 
 def test_pos2embed_kat(N, dev):
