@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from projects.mmdet3d_plugin import native, set_precision  # noqa: E402
+from projects.mmdet3d_plugin import dp, native, set_precision  # noqa: E402
 from projects.mmdet3d_plugin import synthetic as S  # noqa: E402
 from projects.mmdet3d_plugin.mmcv_custom.ops.voxel import SPConvVoxelization  # noqa: E402
 from projects.mmdet3d_plugin.profiling import region_timer  # noqa: E402
@@ -50,13 +50,11 @@ def decoder_frame_flops(nq=NQ, nk=NK, c=C, layers=L, ffn=1024):
 
 
 def init_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    return world, rank, local
+    env = dp.dp_env()
+    if env.world > 1:
+        torch.cuda.set_device(env.local_rank)
+        dp.init(env, backend="nccl", device=torch.device("cuda", env.local_rank))
+    return env
 
 
 def cpu_baseline(head_cfg_name, seconds, seed):
@@ -109,14 +107,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world, rank, local = init_dist(args)
+    env = init_dist(args)
+    world, rank, local = env.world, env.rank, env.local_rank
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     native.lib()
     set_precision(args.precision)
 
     head, cfg, meta = S.build_synthetic_head("cmt_lidar_nus", seed=0, device=dev)
-    x = S.synthetic_bev(1, 180, 180, seed=1 + rank, device=dev)
+    x = S.synthetic_bev(1, 180, 180, seed=dp.frame_seed(1, env), device=dev)
     metas = [dict()]
 
     def step():
@@ -140,23 +139,8 @@ def main():
             run = graph.replay
         else:
             run = step
-        for _ in range(args.warmup):
-            run()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            run()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([elapsed], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = t.item()
+        elapsed, value = dp.timed_frames(run, steps=args.steps, warmup=args.warmup, env=env,
+                                         sync=torch.cuda.synchronize, device=dev)
 
         # --- dominant kernel: cross-attention, HIP events on its launch stream
         with region_timer() as rt:
@@ -178,8 +162,6 @@ def main():
         torch.cuda.synchronize()
         vox_ms = (time.perf_counter() - tv) / nvox * 1e3
 
-    frames = args.steps * world
-    value = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     achieved = cross_attn_flops() / (attn_ms * 1e-3) / 1e12
     result = {

@@ -57,17 +57,22 @@ __device__ __forceinline__ void store_o4(const AttnKParams& p, int b, int q, int
 
 // One 64-key tile for one wave: S^T = K Q^T, online softmax, O^T += V^T P^T.
 // MASK = keys >= Nk in this tile are set to -inf (only the ragged last tile).
-// FOLD = Q was pre-multiplied by c = scale*log2(e): the running maximum m
-//   (already in exp2 units) enters the QK^T chain as its accumulator input, so
-//   the MFMA returns c*s - m and the exponent needs no per-score FMA.
-// The row sums run on the MFMA pipe: lsum += ones . P^T (every register of a
-// lane then holds its query's full sum over both lane halves).
+// The running maximum enters the QK^T chain as its accumulator input (negm =
+// -m_run, kept in registers across tiles), so the MFMA returns s' = s - m and
+// no accumulator is zero-filled per tile.  FOLD = Q was pre-multiplied by
+// c = scale*log2(e) (s' is then already in exp2 units); otherwise the
+// exponent is exp2(c * s').  Scores above the running max shift m (always on
+// a split's first tile, where m_run = 0 is a placeholder); the shift
+// rescales O and the row sums (exact lazy rescale, rare after the first tiles).
+// Row sums run on the MFMA pipe: lsum += ones . P^T (every register of a lane
+// then holds its query's full sum over both lane halves).
 template <typename T, bool MASK, bool FOLD>
 __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T* __restrict__ Vt,
                                                const typename mfma_traits<T>::frag (&qf)[2], f32x16& o,
                                                f32x16& lsum, f32x16& negm, float& m_run, bool first, float c,
                                                int key0, int Nk, int lane) {
     typedef typename mfma_traits<T>::frag frag;
+    const float u = FOLD ? 1.f : c;   // s' units -> exp2 units
     const int lr = lane & 31;
     const int lh = lane >> 5;
     f32x16 s[2];
@@ -76,14 +81,7 @@ __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T
         const int row = kb * 32 + lr;
         const frag k0 = *(const frag*)(&Kt[row * D + 8 * ((lh) ^ ((row >> 2) & 3))]);
         const frag k1 = *(const frag*)(&Kt[row * D + 8 * ((2 + lh) ^ ((row >> 2) & 3))]);
-        if (FOLD) {
-            s[kb] = mfma_traits<T>::mma(k0, qf[0], negm);
-        } else {
-            f32x16 z;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) z[r] = 0.f;
-            s[kb] = mfma_traits<T>::mma(k0, qf[0], z);
-        }
+        s[kb] = mfma_traits<T>::mma(k0, qf[0], negm);
         s[kb] = mfma_traits<T>::mma(k1, qf[1], s[kb]);
     }
     if (MASK) {
@@ -103,47 +101,25 @@ __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T
         m1 = vmax3(m1, s[1][r], s[1][r + 1]);
     }
     const float mt = pair_max(vmax(m0, m1));
+    if (first || __any(mt > 0.f)) {
+        const float d = first ? mt : vmax(mt, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-d * u);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            o[r] *= alpha;
+            lsum[r] *= alpha;
+            s[0][r] -= d;
+            s[1][r] -= d;
+        }
+        m_run += d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+    }
     frag pf[2][2];
-    if (FOLD) {
-        // s = c*score - m_run.  Shift where the tile max is above the running
-        // max (always on a split's first tile, whose m_run is a placeholder 0).
-        if (first || __any(mt > 0.f)) {
-            const float d = first ? mt : vmax(mt, 0.f);
-            const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                o[r] *= alpha;
-                lsum[r] *= alpha;
-                s[0][r] -= d;
-                s[1][r] -= d;
-            }
-            m_run += d;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) negm[r] = -m_run;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[0][r]);
-            pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[1][r]);
-        }
-    } else {
-        const float m_new = vmax(m_run, mt);
-        // exact lazy rescale: alpha == 1 for every lane whose max did not grow
-        if (__any(m_new > m_run)) {
-            const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                o[r] *= alpha;
-                lsum[r] *= alpha;
-            }
-            m_run = m_new;
-        }
-        const float mc = m_run * c;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(fmaf(s[0][r], c, -mc));
-            pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(fmaf(s[1][r], c, -mc));
-        }
+    for (int r = 0; r < 16; ++r) {
+        pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[0][r] : s[0][r] * u);
+        pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[1][r] : s[1][r] * u);
     }
     frag ones;
 #pragma unroll
@@ -169,13 +145,118 @@ __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T
         }
 }
 
-template <typename T, int NWAVES, bool FOLD>
-__global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
+// Two independent 32-query sub-blocks per wave (64 queries): the K and V
+// fragments read from LDS serve both, and the two dependency chains
+// (QK^T MFMA -> max -> exp -> PV MFMA) interleave in one instruction stream, so
+// one sub-block's softmax VALU work overlaps the other's MFMAs.
+template <typename T, bool MASK, bool FOLD>
+__device__ __forceinline__ void attn_tile2_lowp(const T* __restrict__ Kt, const T* __restrict__ Vt,
+                                                const typename mfma_traits<T>::frag (&qf)[2][2], f32x16 (&o)[2],
+                                                f32x16 (&lsum)[2], f32x16 (&negm)[2], float (&m_run)[2], bool first,
+                                                float c, int key0, int Nk, int lane) {
     typedef typename mfma_traits<T>::frag frag;
-    constexpr int NTH = NWAVES * 64;
-    constexpr int CHUNKS = KT * D / 8;            // 16-byte chunks per K (or V) tile = 256
-    __shared__ __attribute__((aligned(16))) T Ks[2][KT * D];
-    __shared__ __attribute__((aligned(16))) T Vs[2][KT * D];
+    const float u = FOLD ? 1.f : c;   // s' units -> exp2 units
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    f32x16 s[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        const int row = kb * 32 + lr;
+        const frag k0 = *(const frag*)(&Kt[row * D + 8 * ((lh) ^ ((row >> 2) & 3))]);
+        const frag k1 = *(const frag*)(&Kt[row * D + 8 * ((2 + lh) ^ ((row >> 2) & 3))]);
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+            s[sb][kb] = mfma_traits<T>::mma(k0, qf[sb][0], negm[sb]);
+            s[sb][kb] = mfma_traits<T>::mma(k1, qf[sb][1], s[sb][kb]);
+        }
+    }
+    if (MASK) {
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (key >= Nk) s[sb][kb][r] = -__builtin_inff();
+                }
+    }
+    frag pf[2][2][2];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+        float m0 = vmax(s[sb][0][0], s[sb][0][1]), m1 = vmax(s[sb][1][0], s[sb][1][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            m0 = vmax3(m0, s[sb][0][r], s[sb][0][r + 1]);
+            m1 = vmax3(m1, s[sb][1][r], s[sb][1][r + 1]);
+        }
+        const float mt = pair_max(vmax(m0, m1));
+        if (first || __any(mt > 0.f)) {
+            const float d = first ? mt : vmax(mt, 0.f);
+            const float alpha = __builtin_amdgcn_exp2f(-d * u);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                o[sb][r] *= alpha;
+                lsum[sb][r] *= alpha;
+                s[sb][0][r] -= d;
+                s[sb][1][r] -= d;
+            }
+            m_run[sb] += d;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) negm[sb][r] = -m_run[sb];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            pf[sb][0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[sb][0][r] : s[sb][0][r] * u);
+            pf[sb][1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[sb][1][r] : s[sb][1][r] * u);
+        }
+    }
+    frag ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
+    const int dgrp = 16 * ((lane >> 4) & 1);
+    const int tq = (lane & 15) >> 2;
+    const int tp = lane & 3;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            const int r0 = kb * 32 + 16 * ss + 4 * lh + tq;
+            const T* base0 = &Vt[r0 * D + dgrp + 4 * tp];
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)(base0 + 8 * D));
+            s16x8 vv;
+            vv[0] = lo[0]; vv[1] = lo[1]; vv[2] = lo[2]; vv[3] = lo[3];
+            vv[4] = hi[0]; vv[5] = hi[1]; vv[6] = hi[2]; vv[7] = hi[3];
+            const frag vf = __builtin_bit_cast(frag, vv);
+#pragma unroll
+            for (int sb = 0; sb < 2; ++sb) {
+                o[sb] = mfma_traits<T>::mma(vf, pf[sb][kb][ss], o[sb]);
+                lsum[sb] = mfma_traits<T>::mma(ones, pf[sb][kb][ss], lsum[sb]);
+            }
+        }
+}
+
+// K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4) into a ring of
+// RING stages, RING-1 tiles ahead of the compute, with counted vmcnt waits and
+// one barrier per tile: a wave-instruction copies 16 key rows (1 KB) of K or V;
+// the K image's 16-byte chunk swizzle is applied to the source address.
+constexpr int RING = 4;
+typedef const __attribute__((address_space(1))) void* gaddr_t;
+typedef __attribute__((address_space(3))) void* laddr_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+template <typename T, int NWAVES, bool FOLD, int SUB>
+__global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : 2) void attn_fwd_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    static_assert(SUB == 1 || SUB == 2, "1 or 2 query sub-blocks per wave");
+    constexpr int PERT = 8 / NWAVES;               // glds per thread per tile (8 KB / (NWAVES KB))
+    constexpr int STAGE = 2 * KT * D;              // elements: K tile then V tile
+    __shared__ __attribute__((aligned(16))) T ring[RING * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -191,109 +272,120 @@ __global__ __launch_bounds__(NWAVES * 64) void attn_fwd_kernel(AttnKParams p) {
     const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
     const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
 
-    const int q = blockIdx.x * (NWAVES * QW) + wave * QW + lr;
-    const int qc = q < p.Nq ? q : p.Nq - 1;
+    int qs[SUB];
+    const float c = p.c;
     // Q^T fragments (B operand): B[k = 8*lh + j][col = q] = Q[q][16*ks + 8*lh + j]
-    frag qf[2];
-    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-    if (FOLD) {
+    frag qf[SUB][2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+    for (int sb = 0; sb < SUB; ++sb) {
+        qs[sb] = blockIdx.x * (NWAVES * QW * SUB) + (wave * SUB + sb) * QW + lr;
+        const int qc = qs[sb] < p.Nq ? qs[sb] : p.Nq - 1;
+        qf[sb][0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+        qf[sb][1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+        if (FOLD) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * p.c);
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qf[sb][i][j] = (T)((float)qf[sb][i][j] * c);
+        }
     }
 
     const int ntiles = (p.Nk + KT - 1) / KT;
     const int t_begin = split * p.tiles_per_split;
     const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+    const int nt = t_end - t_begin;
     const bool ragged = (p.Nk % KT) != 0;
 
-    // staging: 2 x 256 chunks (K then V) over NTH threads
-    constexpr int PER = 2 * CHUNKS / NTH;
-    frag reg[PER];
-    auto load_tile = [&](int t) {
+    // this thread's copies: id = i*NWAVES + wave -> (K|V, 16-row block); lane -> (row, chunk)
+    const int crow = lane >> 2, cch = lane & 3;
+    auto issue = [&](int slot, int t) {
+        T* st = ring + slot * STAGE;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int idx = tid + NTH * i;
-            const int kv = idx / CHUNKS;                   // 0 = K, 1 = V
-            const int rem = idx - kv * CHUNKS;
-            const int row = rem >> 2, ch = rem & 3;
-            const int key = t * KT + row;
-            const T* src = (kv == 0 ? Kb + (int64_t)key * p.k_rs : Vb + (int64_t)key * p.v_rs) + ch * 8;
-            if (key < p.Nk) {
-                reg[i] = *(const frag*)src;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) reg[i][j] = (T)0.f;
-            }
-        }
-    };
-    auto store_tile = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int idx = tid + NTH * i;
-            const int kv = idx / CHUNKS;
-            const int rem = idx - kv * CHUNKS;
-            const int row = rem >> 2, ch = rem & 3;
-            if (kv == 0) *(frag*)(&Ks[buf][row * D + 8 * (ch ^ ((row >> 2) & 3))]) = reg[i];
-            else *(frag*)(&Vs[buf][row * D + 8 * ch]) = reg[i];
+        for (int i = 0; i < PERT; ++i) {
+            const int id = i * NWAVES + wave;
+            const int kv = id >> 2;
+            const int row = (id & 3) * 16 + crow;
+            const int key = min(t * KT + row, p.Nk - 1);       // ragged tail: clamped, masked in compute
+            const T* src = kv == 0 ? Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((row >> 2) & 3))
+                                   : Vb + (int64_t)key * p.v_rs + 8 * cch;
+            __builtin_amdgcn_global_load_lds((gaddr_t)src, (laddr_t)(st + kv * KT * D + (id & 3) * 16 * D), 16, 0, 0);
         }
     };
 
-    f32x16 o, lsum, negm;
+    f32x16 o[SUB], lsum[SUB], negm[SUB];
+    float m_run[SUB];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        o[r] = 0.f;
-        lsum[r] = 0.f;
-        negm[r] = 0.f;
+    for (int sb = 0; sb < SUB; ++sb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            o[sb][r] = 0.f;
+            lsum[sb][r] = 0.f;
+            negm[sb][r] = 0.f;
+        }
+        m_run[sb] = 0.f;   // placeholder until the first tile sets it
     }
-    // running max: exp2 units (c * score) with FOLD, score units otherwise
-    float m_run = FOLD ? 0.f : -__builtin_inff();
-    const float c = p.c;
 
-    if (t_begin < t_end) {
-        load_tile(t_begin);
-        store_tile(0);
-    }
-    __syncthreads();
-    for (int t = t_begin; t < t_end; ++t) {
-        const int cur = (t - t_begin) & 1;
-        const bool first = t == t_begin;
-        if (t + 1 < t_end) load_tile(t + 1);
-        if (ragged && t == ntiles - 1)
-            attn_tile_lowp<T, true, FOLD>(Ks[cur], Vs[cur], qf, o, lsum, negm, m_run, first, c, t * KT, p.Nk, lane);
-        else
-            attn_tile_lowp<T, false, FOLD>(Ks[cur], Vs[cur], qf, o, lsum, negm, m_run, first, c, t * KT, p.Nk, lane);
-        if (t + 1 < t_end) store_tile(cur ^ 1);
-        __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RING - 1; ++i)
+        if (i < nt) issue(i, t_begin + i);
+    for (int i = 0; i < nt; ++i) {
+        const int issued = min(nt, RING - 1 + i);
+        const int inflight = issued - i - 1;                   // tiles allowed to stay in flight
+        if (inflight >= 2) wait_vm_lgkm<2 * PERT>();
+        else if (inflight == 1) wait_vm_lgkm<PERT>();
+        else wait_vm_lgkm<0>();
+        barrier_mem();
+        // every wave is past tile i-1: its slot takes tile i + RING - 1
+        if (i + RING - 1 < nt) issue((i + RING - 1) % RING, t_begin + i + RING - 1);
+        const T* Kt = ring + (i % RING) * STAGE;
+        const T* Vt = Kt + KT * D;
+        const int t = t_begin + i;
+        const bool last_ragged = ragged && t == ntiles - 1;
+        if constexpr (SUB == 2) {
+            if (last_ragged)
+                attn_tile2_lowp<T, true, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, i == 0, c, t * KT, p.Nk, lane);
+            else
+                attn_tile2_lowp<T, false, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, i == 0, c, t * KT, p.Nk, lane);
+        } else {
+            if (last_ragged)
+                attn_tile_lowp<T, true, FOLD>(Kt, Vt, qf[0], o[0], lsum[0], negm[0], m_run[0], i == 0, c, t * KT,
+                                              p.Nk, lane);
+            else
+                attn_tile_lowp<T, false, FOLD>(Kt, Vt, qf[0], o[0], lsum[0], negm[0], m_run[0], i == 0, c, t * KT,
+                                               p.Nk, lane);
+        }
     }
 
     // ---- write ---------------------------------------------------------------
-    const float l_tot = lsum[0];
-    if (q >= p.Nq) return;
-    if (p.splits == 1) {
-        const float inv = 1.f / l_tot;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-            if (p.round_out) {   // flash-attn returns the input dtype (attention.py:46 out_fp32 cast after)
+    for (int sb = 0; sb < SUB; ++sb) {
+        const int q = qs[sb];
+        const float l_tot = lsum[sb][0];
+        if (q >= p.Nq) continue;
+        if (p.splits == 1) {
+            const float inv = 1.f / l_tot;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = {o[sb][4 * g] * inv, o[sb][4 * g + 1] * inv, o[sb][4 * g + 2] * inv,
+                           o[sb][4 * g + 3] * inv};
+                if (p.round_out) {   // flash-attn returns the input dtype (attention.py:46 out_fp32 cast after)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+                }
+                store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
             }
-            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
-        }
-    } else {
-        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
-        float* dst = p.Op + row * D;
+        } else {
+            const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
+            float* dst = p.Op + row * D;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
-        }
-        if (lh == 0) {
-            p.Mp[row] = FOLD ? m_run : m_run * c;   // exp2 units for the combine
-            p.Lp[row] = l_tot;
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = {o[sb][4 * g], o[sb][4 * g + 1], o[sb][4 * g + 2], o[sb][4 * g + 3]};
+                *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+            }
+            if (lh == 0) {
+                p.Mp[row] = FOLD ? m_run[sb] : m_run[sb] * c;   // exp2 units for the combine
+                p.Lp[row] = l_tot;
+            }
         }
     }
 }
@@ -493,23 +585,27 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     store_o4(p, b, q, h * D + d4, r);
 }
 
-// 8-wave workgroups (256 queries share each staged K/V tile) for long key
-// ranges; 4-wave ones otherwise.
-int lowp_waves(const cmt_attn_args& a) {
-    return (a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128) ? 8 : 4;
+// Launch shape of the f16/bf16 kernel: waves per workgroup x query
+// sub-blocks per wave.  Long key ranges: 4 waves x 2 sub-blocks (256 queries
+// share each staged K/V tile); short ones (self-attention): 4 waves x 1.
+struct LowpShape { int waves, sub; };
+LowpShape lowp_shape(const cmt_attn_args& a) {
+    if (a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128) return {4, 2};
+    return {4, 1};
 }
 
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
     const int ntiles = (a.Nk + KT - 1) / KT;
-    const int qrows = a.dtype == CMT_F32 ? QB : lowp_waves(a) * QW;
+    const LowpShape sh = lowp_shape(a);
+    const int nw = a.dtype == CMT_F32 ? NW : sh.waves;
+    const int qrows = a.dtype == CMT_F32 ? QB : sh.waves * sh.sub * QW;
     const int base = cdiv(a.Nq, qrows) * a.B * a.H;
-    const int nw = a.dtype == CMT_F32 ? NW : lowp_waves(a);
     int s = 1;
-    // aim for >= 4096 waves (4 per SIMD) while keeping >= 8 tiles per split;
+    // aim for >= 1024 waves (one per SIMD) while keeping >= 8 tiles per split;
     // short key ranges (self-attention) split down to 2 tiles per split
     const int min_tiles = ntiles >= 64 ? 8 : 2;
-    while ((int64_t)base * s * nw < 4096 && ntiles / (2 * s) >= min_tiles) s *= 2;
+    while ((int64_t)base * s * nw < 1024 && ntiles / (2 * s) >= min_tiles) s *= 2;
     return s;
 }
 
@@ -560,19 +656,22 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         p.Lp = p.Mp + rows;
     }
     hipStream_t s = (hipStream_t)stream;
-    const int nw = lowp_waves(a);
-    dim3 grid(cdiv(a.Nq, a.dtype == CMT_F32 ? QB : nw * QW), a.B * a.H, splits);
+    const LowpShape sh = lowp_shape(a);
+    dim3 grid(cdiv(a.Nq, a.dtype == CMT_F32 ? QB : sh.waves * sh.sub * QW), a.B * a.H, splits);
     const bool fold = (a.flags & CMT_ATTN_FOLD_SCALE) != 0;
-#define ATTN_LAUNCH(T, NWV)                                                                   \
-    do {                                                                                      \
-        if (fold) attn_fwd_kernel<T, NWV, true><<<grid, NWV * 64, 0, s>>>(p);                 \
-        else attn_fwd_kernel<T, NWV, false><<<grid, NWV * 64, 0, s>>>(p);                     \
+#define ATTN_LAUNCH(T)                                                                                   \
+    do {                                                                                                 \
+        if (sh.sub == 2) {                                                                               \
+            if (fold) attn_fwd_kernel<T, 4, true, 2><<<grid, 256, 0, s>>>(p);                            \
+            else attn_fwd_kernel<T, 4, false, 2><<<grid, 256, 0, s>>>(p);                                \
+        } else {                                                                                         \
+            if (fold) attn_fwd_kernel<T, 4, true, 1><<<grid, 256, 0, s>>>(p);                            \
+            else attn_fwd_kernel<T, 4, false, 1><<<grid, 256, 0, s>>>(p);                                \
+        }                                                                                                \
     } while (0)
     if (a.dtype == CMT_F32) attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
-    else if (a.dtype == CMT_F16 && nw == 8) ATTN_LAUNCH(f16_t, 8);
-    else if (a.dtype == CMT_F16) ATTN_LAUNCH(f16_t, 4);
-    else if (nw == 8) ATTN_LAUNCH(bf16_t, 8);
-    else ATTN_LAUNCH(bf16_t, 4);
+    else if (a.dtype == CMT_F16) ATTN_LAUNCH(f16_t);
+    else ATTN_LAUNCH(bf16_t);
 #undef ATTN_LAUNCH
     int rc = cmt_check_launch("cmt_attn_fwd");
     if (rc || splits == 1) return rc;

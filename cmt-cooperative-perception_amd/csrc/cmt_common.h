@@ -75,6 +75,13 @@ __device__ __forceinline__ float pair_sum(float x) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// Workgroup barrier that is also a compiler memory barrier: LDS-DMA
+// (global_load_lds) writes are invisible to the compiler, so ds_reads of a
+// freshly DMA'd buffer must not be scheduled above the s_barrier that orders
+// them after the other waves' counted vmcnt waits (the bare builtin does not
+// prevent that hoisting).
+__device__ __forceinline__ void barrier_mem() { asm volatile("s_barrier" ::: "memory"); }
+
 // Non-finite sanitiser with torch.nan_to_num defaults.
 __device__ __forceinline__ float nan_to_num(float x) {
     if (x != x) return 0.f;

@@ -543,7 +543,7 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     for (int kt = 0; kt < nk; ++kt) {
         const int last = min(nk - 1, kt == 0 ? S - 1 : kt + S - 2);
         wait_tiles<PER, S>(last - kt);
-        __builtin_amdgcn_s_barrier();
+        barrier_mem();
         // every wave is past its reads of stage kt-1: refill that buffer
         if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
         const char* As = smem + (kt % S) * STAGE;
