@@ -550,8 +550,9 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(AttnKParams p) {
 }
 
 // Merge the kv-split partials: 8 threads per (b, h, q), each owning 4 of the
-// 32 head dims (16-byte loads of every split's partial row; the split maxima
-// and row sums are read once per thread).
+// 32 head dims.  NS = split count (compile-time, so every partial load is
+// issued before the first use; the maxima are in exp2 units).
+template <int NS>
 __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t rows = (int64_t)p.B * p.H * p.Nq;
@@ -562,16 +563,25 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     const int64_t bh = bhq / p.Nq;
     const int h = (int)(bh % p.H);
     const int b = (int)(bh / p.H);
+    float ms[NS], ls[NS];
+    f32x4 os[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        ms[s] = p.Mp[s * rows + bhq];
+        ls[s] = p.Lp[s * rows + bhq];
+        os[s] = *(const f32x4*)(p.Op + (s * rows + bhq) * D + d4);
+    }
     float M = -__builtin_inff();
-    for (int s = 0; s < p.splits; ++s) M = fmaxf(M, p.Mp[s * rows + bhq]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) M = ls[s] > 0.f ? fmaxf(M, ms[s]) : M;   // empty splits (l == 0) excluded
     f32x4 num = {0.f, 0.f, 0.f, 0.f};
     float den = 0.f;
-    for (int s = 0; s < p.splits; ++s) {
-        const float ms = p.Mp[s * rows + bhq];
-        if (ms == -__builtin_inff()) continue;
-        const float w = __builtin_amdgcn_exp2f(ms - M);   // maxima are stored in exp2 units
-        num += w * *(const f32x4*)(p.Op + (s * rows + bhq) * D + d4);
-        den += w * p.Lp[s * rows + bhq];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        // an empty split (no keys) has l == 0 and contributes nothing
+        const float w = ls[s] > 0.f ? __builtin_amdgcn_exp2f(ms[s] - M) : 0.f;
+        num += w * os[s];
+        den += w * ls[s];
     }
     const float inv = 1.f / den;
     f32x4 r = num * inv;
@@ -634,6 +644,8 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
                 a.k_hstride % 8 == 0 && a.v_hstride % 8 == 0 && a.q_bstride % 8 == 0 && a.k_bstride % 8 == 0 &&
                 a.v_bstride % 8 == 0, "cmt_attn_fwd: Q/K/V strides must be multiples of 8 elements");
     const int splits = choose_splits(a);
+    CMT_REQUIRE(splits <= 16 || splits == 24 || splits == 32 || splits == 48 || splits == 64,
+                "cmt_attn_fwd: kv_splits must be <= 16, 24, 32, 48 or 64");
     const int ntiles = (a.Nk + KT - 1) / KT;
     AttnKParams p;
     p.B = a.B; p.H = a.H; p.Nq = a.Nq; p.Nk = a.Nk;
@@ -676,6 +688,13 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     int rc = cmt_check_launch("cmt_attn_fwd");
     if (rc || splits == 1) return rc;
     const int64_t total = (int64_t)a.B * a.H * a.Nq * 8;
-    attn_combine_kernel<<<(unsigned)cdiv64(total, 256), 256, 0, s>>>(p);
+    const unsigned nb = (unsigned)cdiv64(total, 256);
+    switch (splits) {
+#define COMB(NS) case NS: attn_combine_kernel<NS><<<nb, 256, 0, s>>>(p); break;
+        COMB(2) COMB(3) COMB(4) COMB(5) COMB(6) COMB(7) COMB(8) COMB(9) COMB(10) COMB(11) COMB(12) COMB(13)
+        COMB(14) COMB(15) COMB(16) COMB(24) COMB(32) COMB(48) COMB(64)
+#undef COMB
+        default: return cmt_fail(CMT_ENOTSUP, "cmt_attn_fwd: kv_splits must be <= 16, 24, 32, 48 or 64");
+    }
     return cmt_check_launch("cmt_attn_combine");
 }

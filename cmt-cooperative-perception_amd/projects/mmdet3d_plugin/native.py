@@ -14,7 +14,7 @@ import torch
 __all__ = ["lib", "available", "gemm", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
            "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
-           "voxelize", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
+           "voxelize", "box_decode", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 _DEFAULT_LIB = os.path.join(_PKG_ROOT, "lib", "libcmt_hip.so")
@@ -96,6 +96,8 @@ def _load():
         "cmt_cast": ([_vp, _int, _vp, _int, _i64, _vp], _int),
         "cmt_task_head_tail": ([_vp, _int, _int, _int, _int, _int, _vp, _vp, _vp, _vp, P(_int), _int, _int, _vp,
                                 _int, _int, P(_flt), _vp, _vp], _int),
+        "cmt_box_decode": ([_vp, _i64, _vp, _i64, _vp, _int, _int, _int, _int, _int, P(_flt), _flt, _int,
+                            _vp, _vp, _vp, _vp, _vp], _int),
         "cmt_voxelize_workspace_bytes": ([_int, _int], _i64),
         "cmt_voxelize": ([_vp, _int, _int, P(_flt), P(_flt), P(_int), _int, _int, _int, _vp, _vp, _vp, _vp, _vp,
                           _vp, _i64, _vp], _int),
@@ -313,6 +315,25 @@ def task_head_tail(H1, gw, gb, W2, B2, ref, out, *, L, B, Nq, nheads, hc, head_o
     _check(lib().cmt_task_head_tail(_p(H1), L, B, Nq, nheads, hc, _p(gw), _p(gb), _p(W2), _p(B2), ho,
                                     int(sum(head_out)), k, _p(ref), center_col, height_col, _farr(pc_range, 6),
                                     _p(out), _stream()), "cmt_task_head_tail")
+
+
+def box_decode(logits, bbox, class_task, *, Nq, ncls, max_num, post_center_range, score_threshold=None):
+    """logits [B, Nq*ncls] f32, bbox [B, T*Nq, code] f32, class_task [ncls] int32 (device) ->
+    (boxes [B, max_num, code-1], scores [B, max_num], labels [B, max_num] int32, count [B] int32),
+    rows [:count[b]] valid, in descending score order."""
+    _dev(logits, bbox, class_task)
+    B = logits.shape[0]
+    code = bbox.shape[-1]
+    dev = logits.device
+    boxes = torch.empty((B, max_num, code - 1), dtype=torch.float32, device=dev)
+    scores = torch.empty((B, max_num), dtype=torch.float32, device=dev)
+    labels = torch.empty((B, max_num), dtype=torch.int32, device=dev)
+    count = torch.empty((B,), dtype=torch.int32, device=dev)
+    thr = 0.0 if score_threshold is None else float(score_threshold)
+    _check(lib().cmt_box_decode(_p(logits), logits.stride(0), _p(bbox), bbox.stride(0), _p(class_task), B, Nq, ncls,
+                                code, max_num, _farr(post_center_range, 6), thr, int(bool(score_threshold)),
+                                _p(boxes), _p(scores), _p(labels), _p(count), _stream()), "cmt_box_decode")
+    return boxes, scores, labels, count
 
 
 def voxelize(points, *, voxel_size, coors_range, grid, max_points, max_voxels, nfeat_mean):

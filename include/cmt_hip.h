@@ -243,6 +243,25 @@ int cmt_voxelize(const float* points, int N, int F, const float* voxel_size3,
                  int nfeat_mean, float* voxels, int* coors, int* num_points, float* means,
                  int* num_voxels, void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * NMS-free box decode.  Replaces
+ * MultiTaskBBoxCoder.decode_single (core/bbox/coders/multi_task_bbox_coder.py:46-100)
+ * + denormalize_bbox (core/bbox/util.py:37-68) for every sample b < B:
+ *   logits [B][Nq*ncls] (last decoder layer, tasks' classes concatenated),
+ *   bbox   [B][T*Nq][code] (center2, height1, dim3, rot2, vel2 per task block),
+ *   class_task [ncls] = task index of each class label (device int32).
+ * top-k (k = max_num) of sigmoid(logits), ties at the k-th value by lowest
+ * index, score-descending; boxes denormalised (exp dims, atan2 yaw) to
+ * code-1 values; kept if the center lies in post_center_range6 (HOST array)
+ * and, when use_threshold, score > score_threshold.  Outputs are compacted in
+ * rank order: out_boxes [B][max_num][code-1], out_scores/out_labels
+ * [B][max_num], out_count [B] (device).  Nq*ncls <= 32768, max_num <= 1024.
+ * ------------------------------------------------------------------------ */
+int cmt_box_decode(const float* logits, int64_t logit_bstride, const float* bbox, int64_t bbox_bstride,
+                   const int* class_task, int B, int Nq, int ncls, int code, int max_num,
+                   const float* post_center_range6, float score_threshold, int use_threshold,
+                   float* out_boxes, float* out_scores, int* out_labels, int* out_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

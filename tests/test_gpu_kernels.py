@@ -220,6 +220,28 @@ def test_attention_spike_rescale(N, dev):
         assert (O.cpu().double()[0] - ref).abs().max().item() < 3e-3
 
 
+@pytest.mark.parametrize("fold", [False, True])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_empty_split_negative_scores(N, dev, dt, fold):
+    """Nk = 200 (4 key tiles) in 3 splits of 2 tiles: the last split is empty.
+    All scores ~ -140 (exp2 units ~ -200): an empty split must not enter the
+    combine's maximum, or every weight underflows."""
+    B, H, Nq, Nk = 1, 2, 70, 200
+    g = torch.Generator().manual_seed(5)
+    q = (5 + 0.1 * torch.randn(B, H, Nq, 32, generator=g)).to(dt)
+    k = (-5 + 0.1 * torch.randn(B, H, Nk, 32, generator=g)).to(dt)
+    v = torch.randn(B, H, Nk, 32, generator=g).to(dt)
+    O = torch.empty(B, Nq, H * 32, device=dev)
+    N.attention(q.to(dev), k.to(dev), v.to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk,
+                q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
+                kv_splits=3, fold_scale=fold)
+    ref = _attn_ref(q, k, v, 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
+    got = O.cpu().double()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 3e-2
+
+
 def test_attention_seq_first_strides(N, dev):
     """sequence-first [S, B, C] layout via strides (module-level API path)."""
     B, H, S = 2, 8, 100
