@@ -456,118 +456,145 @@ __device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt) {
     return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
 }
 
-template <typename CT, int BM, int BN, int S, int AMODE>
-__global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
-    typedef typename mfma_traits<CT>::frag frag;
-    constexpr int KS = 64;                          // k per stage: one 128-byte LDS row per tile row
-    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-    constexpr int APER = BM / 32, BPER = BN / 32;   // 256 lanes x 16 B = 32 rows per block-wide copy
-    constexpr int PER = APER + BPER;                // glds per thread per stage
-    constexpr int TM = BM / 64, TN = BN / 64;
-    __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+// Main loop of the LDS-DMA GEMM for one BM x BN output tile (4 waves in a
+// WM x (4/WM) grid; each wave owns (BM/WM) x (BN*WM/4) as TM x TN 32x32 MFMA
+// tiles).  Accumulators are in the swapped C^T layout: lane = output row.
+template <typename CT, int BM, int BN, int S, int AMODE, int WM>
+struct DmaTile {
+    static constexpr int KS = 64;                          // k per stage: one 128-byte LDS row per tile row
+    static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+    static constexpr int APER = BM / 32, BPER = BN / 32;   // 256 lanes x 16 B = 32 rows per block-wide copy
+    static constexpr int PER = APER + BPER;                // glds per thread per stage
+    static constexpr int WN = 4 / WM;
+    static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    static constexpr int SMEM = S * STAGE;
+    static_assert(TM >= 1 && TN >= 1 && APER >= 1, "tile too small");
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    static __device__ __forceinline__ void run(const cmt_gemm_args& a, char* smem, int m0, int n0, int z,
+                                               f32x16 (&acc)[TM][TN]) {
+        typedef typename mfma_traits<CT>::frag frag;
+        const int tid = threadIdx.x;
+        const int lane = tid & 63;
+        const int wave = tid >> 6;
+        const int wm = wave / WN, wn = wave % WN;
 
-    // XCD-aware tile order (bijective remap of the round-robin dispatch)
-    const int nwg = tiles_m * tiles_n * a.batch;
+        const bool sel_a2 = AMODE == CMT_A_ROWS && a.A2 != nullptr && n0 < a.a2_cols;
+        const CT* Ab = (const CT*)(sel_a2 ? a.A2 : a.A) + (int64_t)z * a.a_bstride;
+        const int64_t lda = sel_a2 ? a.lda2 : a.lda;
+        const CT* Wb = (const CT*)a.W + (int64_t)z * a.w_bstride;
+
+        // per-thread source rows: copy i of this wave covers tile rows (4i + wave)*8 + lane/8
+        const int ch = lane & 7;
+        const CT* asrc[APER];
+        RowInfo ri[APER];
+        int acs[APER];
+#pragma unroll
+        for (int i = 0; i < APER; ++i) {
+            const int row = (4 * i + wave) * 8 + (lane >> 3);
+            acs[i] = (ch ^ ((row >> 1) & 7)) * 8;
+            const int m = m0 + row;
+            ri[i] = make_row_info<AMODE>(a, m);
+            asrc[i] = Ab + (int64_t)min(m, a.M - 1) * lda + acs[i];
+        }
+        const CT* bsrc[BPER];
+#pragma unroll
+        for (int i = 0; i < BPER; ++i) {
+            const int row = (4 * i + wave) * 8 + (lane >> 3);
+            bsrc[i] = Wb + (int64_t)(n0 + row) * a.ldw + (ch ^ ((row >> 1) & 7)) * 8;
+        }
+
+        auto issue = [&](int buf, int kt) {
+            char* sb = smem + buf * STAGE;
+            const int k0 = kt * KS;
+#pragma unroll
+            for (int i = 0; i < APER; ++i) {
+                const void* src;
+                if (AMODE == CMT_A_ROWS) {
+                    src = asrc[i] + k0;
+                } else {
+                    const int64_t off = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), k0);
+                    src = off < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + off + acs[i]);
+                }
+                glds16(src, sb + (4 * i + wave) * 1024);
+            }
+#pragma unroll
+            for (int i = 0; i < BPER; ++i) glds16(bsrc[i] + k0, sb + A_BYTES + (4 * i + wave) * 1024);
+        };
+
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        const int nk = a.K / KS;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (s < nk) issue(s, s);
+
+        const int lr = lane & 31;
+        const int lh = lane >> 5;
+        for (int kt = 0; kt < nk; ++kt) {
+            const int last = min(nk - 1, kt == 0 ? S - 1 : kt + S - 2);
+            wait_tiles<PER, S>(last - kt);
+            barrier_mem();
+            // every wave is past its reads of stage kt-1: refill that buffer
+            if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
+            const char* As = smem + (kt % S) * STAGE;
+            const char* Bs = As + A_BYTES;
+#pragma unroll
+            for (int ks = 0; ks < KS / 16; ++ks) {
+                frag af[TM], bfr[TN];
+                const int kc = 2 * ks + lh;
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const int r = wm * (BM / WM) + tm * 32 + lr;
+                    af[tm] = *(const frag*)(As + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+                }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    const int r = wn * (BN / WN) + tn * 32 + lr;
+                    bfr[tn] = *(const frag*)(Bs + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<CT>::mma(bfr[tn], af[tm], acc[tm][tn]);
+            }
+        }
+    }
+};
+
+// XCD-aware tile order (bijective remap of the round-robin dispatch): one XCD
+// walks a contiguous band of M tiles with every N tile.
+__device__ __forceinline__ void xcd_tile(int tiles_m, int tiles_n, int batch, int& z, int& mt, int& nt) {
+    const int nwg = tiles_m * tiles_n * batch;
     const int orig = blockIdx.x;
     const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
     const int per_z = tiles_m * tiles_n;
-    const int z = wg / per_z;
+    z = wg / per_z;
     const int rem = wg - z * per_z;
-    const int mt = rem / tiles_n;
-    const int m0 = mt * BM, n0 = (rem - mt * tiles_n) * BN;
+    mt = rem / tiles_n;
+    nt = rem - mt * tiles_n;
+}
 
-    const bool sel_a2 = AMODE == CMT_A_ROWS && a.A2 != nullptr && n0 < a.a2_cols;
-    const CT* Ab = (const CT*)(sel_a2 ? a.A2 : a.A) + (int64_t)z * a.a_bstride;
-    const int64_t lda = sel_a2 ? a.lda2 : a.lda;
-    const CT* Wb = (const CT*)a.W + (int64_t)z * a.w_bstride;
-
-    // per-thread source rows: copy i of this wave covers tile rows (4i + wave)*8 + lane/8
-    const int ch = lane & 7;
-    const CT* asrc[APER];
-    RowInfo ri[APER];
-    int acs[APER];
-#pragma unroll
-    for (int i = 0; i < APER; ++i) {
-        const int row = (4 * i + wave) * 8 + (lane >> 3);
-        acs[i] = (ch ^ ((row >> 1) & 7)) * 8;
-        const int m = m0 + row;
-        ri[i] = make_row_info<AMODE>(a, m);
-        asrc[i] = Ab + (int64_t)min(m, a.M - 1) * lda + acs[i];
-    }
-    const CT* bsrc[BPER];
-#pragma unroll
-    for (int i = 0; i < BPER; ++i) {
-        const int row = (4 * i + wave) * 8 + (lane >> 3);
-        bsrc[i] = Wb + (int64_t)(n0 + row) * a.ldw + (ch ^ ((row >> 1) & 7)) * 8;
-    }
-
-    auto issue = [&](int buf, int kt) {
-        char* sb = smem + buf * STAGE;
-        const int k0 = kt * KS;
-#pragma unroll
-        for (int i = 0; i < APER; ++i) {
-            const void* src;
-            if (AMODE == CMT_A_ROWS) {
-                src = asrc[i] + k0;
-            } else {
-                const int64_t off = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), k0);
-                src = off < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + off + acs[i]);
-            }
-            glds16(src, sb + (4 * i + wave) * 1024);
-        }
-#pragma unroll
-        for (int i = 0; i < BPER; ++i) glds16(bsrc[i] + k0, sb + A_BYTES + (4 * i + wave) * 1024);
-    };
-
+template <typename CT, int BM, int BN, int S, int AMODE>
+__global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
+    typedef DmaTile<CT, BM, BN, S, AMODE, 2> Tile;
+    constexpr int TM = Tile::TM, TN = Tile::TN;
+    __shared__ __attribute__((aligned(16))) char smem[Tile::SMEM];
+    int z, mt, nt;
+    xcd_tile(tiles_m, tiles_n, a.batch, z, mt, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
     f32x16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const int nk = a.K / KS;
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-        if (s < nk) issue(s, s);
-
+    Tile::run(a, smem, m0, n0, z, acc);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
     const int lr = lane & 31;
     const int lh = lane >> 5;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int last = min(nk - 1, kt == 0 ? S - 1 : kt + S - 2);
-        wait_tiles<PER, S>(last - kt);
-        barrier_mem();
-        // every wave is past its reads of stage kt-1: refill that buffer
-        if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
-        const char* As = smem + (kt % S) * STAGE;
-        const char* Bs = As + A_BYTES;
-#pragma unroll
-        for (int ks = 0; ks < KS / 16; ++ks) {
-            frag af[TM], bfr[TN];
-            const int kc = 2 * ks + lh;
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-                const int r = wm * (BM / 2) + tm * 32 + lr;
-                af[tm] = *(const frag*)(As + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                const int r = wn * (BN / 2) + tn * 32 + lr;
-                bfr[tn] = *(const frag*)(Bs + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<CT>::mma(bfr[tn], af[tm], acc[tm][tn]);
-        }
-    }
 
     // ---- epilogue: lane = output row, 4 consecutive columns per register group.
     // Every bias / residual load is issued before the first store: vmcnt counts
@@ -617,28 +644,174 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
                         acc[tm][tn][4 * g + j] = a.relu ? fmaxf(v, 0.f) : v;
                     }
     }
+    // ---- stores staged through LDS: the swapped layout leaves each lane 4
+    // columns of one row (8/16-byte pieces at a row stride); the tile is
+    // written to LDS (16-byte chunks XOR-swizzled by row) and read back so
+    // every wave instruction stores 1 KB of contiguous memory (head-split:
+    // 16 rows x 64 B of one head; rows: whole row segments).
+    barrier_mem();                                       // every wave is done with the staging ring
+    const int cpr = BN * esz / 16;                       // 16-byte chunks per tile row
+    const int cpe = 16 / esz;                            // elements per chunk
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
-        const int m = m0 + wm * (BM / 2) + tm * 32 + lr;
-        if (m >= a.M) continue;
-        int b = 0, rr = m;
-        if (a.c_mode != CMT_C_ROWS) {
-            b = m / a.rows_per_batch;
-            rr = m - b * a.rows_per_batch;
-        }
+        const int row = wm * (BM / 2) + tm * 32 + lr;
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
+        for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int n = n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;
+                const int c0 = wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;     // first of 4 columns
+                const int ch = c0 / cpe;
+                char* dst = smem + row * (BN * esz) + ((ch ^ (row & (cpr - 1))) << 4) + (c0 % cpe) * esz;
                 const f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
                                  acc[tm][tn][4 * g + 3]};
-                const int64_t idx = a.c_mode == CMT_C_ROWS
-                                        ? (int64_t)m * a.ldc + n
-                                        : (((int64_t)b * (a.N >> 5) + (n >> 5)) * a.rows_per_batch + rr) * 32 + (n & 31);
-                store4<CT>(Cz, idx, a.c_dtype, v);
+                store4<CT>(dst, 0, a.c_dtype, v);
             }
+    }
+    barrier_mem();
+    const int nchunks = BM * cpr;
+    const bool headsplit = a.c_mode != CMT_C_ROWS;
+    const int cph = 32 * esz / 16;                       // chunks per 32-column head slice of a row
+    for (int q = threadIdx.x; q < nchunks; q += NT) {
+        int row, c;
+        if (headsplit) {                                 // head-major, then row, then chunk: contiguous in memory
+            const int h = q / (BM * cph);
+            const int rem = q - h * (BM * cph);
+            row = rem / cph;
+            c = h * cph + (rem - row * cph);
+        } else {
+            row = q / cpr;
+            c = q - row * cpr;
         }
+        const int m = m0 + row;
+        if (m >= a.M) continue;
+        const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4));
+        const int n = n0 + c * cpe;
+        int64_t idx;
+        if (headsplit) {
+            const int bb = m / a.rows_per_batch;
+            const int rr = m - bb * a.rows_per_batch;
+            idx = (((int64_t)bb * (a.N >> 5) + (n >> 5)) * a.rows_per_batch + rr) * 32 + (n & 31);
+        } else {
+            idx = (int64_t)m * a.ldc + n;
+        }
+        *(f32x4*)(Cz + idx * esz) = v;                   // 16 bytes: 4 fp32 or 8 f16/bf16 values
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GEMM + residual + LayerNorm, fused (cmt_gemm_ln).  One workgroup owns 32
+// full output rows (BN = N = 256): waves 1 x 4, each wave 32 rows x 64
+// columns.  The epilogue adds bias and R, reduces each row's mean / variance
+// across the two lane halves (permlane32_swap) and the 4 waves (a slot after
+// the staging ring in the same LDS array), then writes what cmt_layernorm_ex
+// would: Y, lowp(y), lowp(y + P) and the second LN (post_norm) Y2.
+// ---------------------------------------------------------------------------
+template <typename CT, int S>
+__global__ __launch_bounds__(NT) void gemm_ln_kernel(cmt_gemm_args a, cmt_ln_args ln) {
+    typedef DmaTile<CT, 32, 256, S, CMT_A_ROWS, 1> Tile;
+    static_assert(Tile::TM == 1 && Tile::TN == 2, "32 x 256 tile, 1 x 4 waves");
+    __shared__ __attribute__((aligned(16))) char smem[Tile::SMEM + 2 * 4 * 32 * 4];
+    float* red = (float*)(smem + Tile::SMEM);       // [2][4 waves][32 rows]
+    const int m0 = blockIdx.x * 32;
+    f32x16 acc[1][2];
+    Tile::run(a, smem, m0, 0, 0, acc);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    const int m = m0 + lr;
+    const int mc = min(m, a.M - 1);
+    constexpr int C = 256;
+    // column of value group t = (tn, g): wave*64 + tn*32 + 8g + 4lh -> 8 groups of 4 per lane
+    auto col = [&](int t) { return wave * 64 + (t >> 2) * 32 + 8 * (t & 3) + 4 * lh; };
+
+    // ---- every load first (vmcnt counts stores too)
+    f32x4 v[8], bw[8], bb[8], pv[8], yo[8], w2[8], b2[8], y2o[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const int n = col(t);
+        v[t] = f32x4{acc[0][t >> 2][4 * (t & 3)], acc[0][t >> 2][4 * (t & 3) + 1], acc[0][t >> 2][4 * (t & 3) + 2],
+                     acc[0][t >> 2][4 * (t & 3) + 3]};
+        if (a.bias) v[t] += *(const f32x4*)(a.bias + n);
+        if (a.R) v[t] += load4(a.R, (int64_t)mc * a.ldr + n, a.r_dtype);
+        bw[t] = *(const f32x4*)(ln.W + n);
+        bb[t] = *(const f32x4*)(ln.B + n);
+        if (ln.Yp) pv[t] = *(const f32x4*)(ln.P + (int64_t)mc * ln.ldp + n);
+        if (ln.Y && (ln.flags & CMT_LN_MAX_INTO)) yo[t] = *(const f32x4*)(ln.Y + (int64_t)mc * ln.ldy + n);
+        if (ln.Y2) {
+            w2[t] = *(const f32x4*)(ln.W2 + n);
+            b2[t] = *(const f32x4*)(ln.B2 + n);
+            if (ln.flags2 & CMT_LN_MAX_INTO) y2o[t] = *(const f32x4*)(ln.Y2 + (int64_t)mc * ln.ldy2 + n);
+        }
+    }
+    // row reduction: 32 values per lane -> lane pair -> 4 waves
+    auto row_sum = [&](float x, int slot) {
+        x = pair_sum(x);
+        if (lh == 0) red[(slot * 4 + wave) * 32 + lr] = x;
+        barrier_mem();
+        return red[(slot * 4 + 0) * 32 + lr] + red[(slot * 4 + 1) * 32 + lr] + red[(slot * 4 + 2) * 32 + lr] +
+               red[(slot * 4 + 3) * 32 + lr];
+    };
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) sum += v[t][0] + v[t][1] + v[t][2] + v[t][3];
+    const float mean = row_sum(sum, 0) / (float)C;
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float d = v[t][j] - mean;
+            ss += d * d;
+        }
+    const float rstd = rsqrtf(row_sum(ss, 1) / (float)C + ln.eps);
+    f32x4 y[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[t][j] = (v[t][j] - mean) * rstd * bw[t][j] + bb[t][j];
+    // second LN (post_norm) statistics on the first LN's raw output
+    f32x4 y2[8];
+    if (ln.Y2) {
+        barrier_mem();   // slots reused
+        float s2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s2 += y[t][0] + y[t][1] + y[t][2] + y[t][3];
+        const float mean2 = row_sum(s2, 0) / (float)C;
+        float q2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float d = y[t][j] - mean2;
+                q2 += d * d;
+            }
+        const float rstd2 = rsqrtf(row_sum(q2, 1) / (float)C + ln.eps);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float o = (y[t][j] - mean2) * rstd2 * w2[t][j] + b2[t][j];
+                if (ln.flags2 & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
+                if (ln.flags2 & CMT_LN_MAX_INTO) o = fmaxf(o, y2o[t][j]);
+                y2[t][j] = o;
+            }
+    }
+    if (m >= a.M) return;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const int n = col(t);
+        f32x4 o = y[t];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (ln.flags & CMT_LN_NAN_TO_NUM) o[j] = nan_to_num(o[j]);
+            if (ln.flags & CMT_LN_MAX_INTO) o[j] = fmaxf(o[j], yo[t][j]);
+        }
+        if (ln.Y) *(f32x4*)(ln.Y + (int64_t)m * ln.ldy + n) = o;
+        if (ln.Yl) store4<CT>(ln.Yl, (int64_t)m * ln.ldyl + n, ln.lowp_dtype, o);
+        if (ln.Yp) store4<CT>(ln.Yp, (int64_t)m * ln.ldyp + n, ln.lowp_dtype, o + pv[t]);
+        if (ln.Y2) *(f32x4*)(ln.Y2 + (int64_t)m * ln.ldy2 + n) = y2[t];
     }
 }
 
@@ -702,6 +875,31 @@ int launch_tiles(const cmt_gemm_args& a, hipStream_t s) {
 }
 
 }  // namespace
+
+extern "C" int cmt_gemm_ln(const cmt_gemm_args* gp, const cmt_ln_args* lp, void* stream) {
+    CMT_REQUIRE(gp != nullptr && lp != nullptr, "cmt_gemm_ln: null args");
+    const cmt_gemm_args& a = *gp;
+    const cmt_ln_args& l = *lp;
+    CMT_REQUIRE(a.M > 0 && a.N == 256 && l.C == 256 && a.K % 64 == 0 && a.batch == 1,
+                "cmt_gemm_ln: needs N == C == 256, K % 64 == 0, batch 1");
+    CMT_REQUIRE(a.A && a.W && (a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16) && a.a_dtype == a.w_dtype,
+                "cmt_gemm_ln: A and W in the f16/bf16 compute dtype");
+    CMT_REQUIRE(a.a_mode == CMT_A_ROWS && a.A2 == nullptr && a.c_mode == CMT_C_ROWS && !a.relu,
+                "cmt_gemm_ln: plain row GEMM (no A2, no head split, no relu)");
+    CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0 && (a.R == nullptr || a.ldr % 4 == 0) &&
+                (a.r_dtype == CMT_F32 || a.r_dtype == a.w_dtype), "cmt_gemm_ln: bad A/W/R strides or R dtype");
+    CMT_REQUIRE(l.W && l.B && (l.Y || l.Yl || l.Yp || l.Y2) && (l.Yp == nullptr || l.P) &&
+                (l.Y2 == nullptr || (l.W2 && l.B2)), "cmt_gemm_ln: bad LN outputs");
+    CMT_REQUIRE((l.Yl == nullptr && l.Yp == nullptr) || l.lowp_dtype == a.w_dtype,
+                "cmt_gemm_ln: lowp outputs must use the compute dtype");
+    CMT_REQUIRE(l.ldy % 4 == 0 && l.ldyl % 4 == 0 && l.ldyp % 4 == 0 && l.ldp % 4 == 0 && l.ldy2 % 4 == 0,
+                "cmt_gemm_ln: LN strides must be multiples of 4");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned grid = (unsigned)cdiv(a.M, 32);
+    if (a.w_dtype == CMT_BF16) gemm_ln_kernel<bf16_t, 3><<<grid, NT, 0, s>>>(a, l);
+    else gemm_ln_kernel<f16_t, 3><<<grid, NT, 0, s>>>(a, l);
+    return cmt_check_launch("cmt_gemm_ln");
+}
 
 extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm: null args");

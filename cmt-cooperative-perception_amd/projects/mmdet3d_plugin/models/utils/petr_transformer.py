@@ -20,6 +20,7 @@ Two execution paths:
 """
 import copy
 import math
+import os
 import warnings
 
 import torch
@@ -487,6 +488,8 @@ class PETRTransformerDecoder(nn.Module):
                        native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
         ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
         pw, pb, _pe = pk["post"]
+        # out-projection / fc2 GEMMs fused with their residual + LayerNorm (cmt_gemm_ln)
+        fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "1") != "0"
         for l, lw in enumerate(pk["layers"]):
             # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
             native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
@@ -495,9 +498,14 @@ class PETRTransformerDecoder(nn.Module):
                              q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
                              v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
                              o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
-            native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt, ldr=C)
             w0, b0, e0 = lw["norms"][0]
-            native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos)
+            if fuse_ln:
+                native.gemm_ln(ob, lw["sa_ow"], M=rows, K=C, lda=C, ldw=C, bias=lw["sa_ob"], R=tgt, ldr=C, ln_w=w0,
+                               ln_b=b0, eps=e0, Y=t1n, Yp=tp, P=qpos)
+            else:
+                native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt,
+                            ldr=C)
+                native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos)
             # --- cross attention: q = lowp(x + qpos); K/V from the hoisted GEMM
             native.gemm(tp, lw["ca_wq"], qc, M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
                         headsplit_rows=Nq)
@@ -507,14 +515,25 @@ class PETRTransformerDecoder(nn.Module):
                                  v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
                                  v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
                                  round_output=prec.round_cross_out, fold_scale=True)
-            native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n, ldr=C)
             w1, b1, e1 = lw["norms"][1]
-            native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl)
+            if fuse_ln:
+                native.gemm_ln(ob, lw["ca_ow"], M=rows, K=C, lda=C, ldw=C, bias=lw["ca_ob"], R=t1n, ldr=C, ln_w=w1,
+                               ln_b=b1, eps=e1, Y=o, Yl=tl)
+            else:
+                native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n,
+                            ldr=C)
+                native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl)
             # --- FFN (fc1 activation written in the compute dtype)
             native.gemm(tl, lw["f1_w"], hf, M=rows, N=FF, K=C, lda=C, ldw=C, ldc=FF, bias=lw["f1_b"], relu=True)
-            native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o, ldr=C)
-            # --- norms.2 -> next query (fp32 + both lowp operands), fused with post_norm -> out[l]
+            # --- fc2 + residual + norms.2 -> next query (fp32 + both lowp operands), + post_norm -> out[l]
             w2, b2, e2 = lw["norms"][2]
-            native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
-                                W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
+            if fuse_ln:
+                native.gemm_ln(hf, lw["f2_w"], M=rows, K=FF, lda=FF, ldw=FF, bias=lw["f2_b"], R=o, ldr=C, ln_w=w2,
+                               ln_b=b2, eps=e2, Y=tgt, Yl=tl, Yp=tp, P=qpos, W2=pw, B2=pb, Y2=out,
+                               flags2=post_flags, y2_offset=l * rows * C)
+            else:
+                native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o,
+                            ldr=C)
+                native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
+                                    W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         return out

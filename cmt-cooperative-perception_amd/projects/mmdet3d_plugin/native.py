@@ -11,7 +11,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "available", "gemm", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
+__all__ = ["lib", "available", "gemm", "gemm_ln", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
            "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
            "voxelize", "box_decode", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
@@ -87,6 +87,7 @@ def _load():
         "cmt_layernorm": ([_vp, _i64, _int, _int, _vp, _vp, _flt, _vp, _i64, _int, _vp, _vp, _vp, _i64, _int, _vp],
                           _int),
         "cmt_layernorm_ex": ([P(LnArgs), _vp], _int),
+        "cmt_gemm_ln": ([P(GemmArgs), P(LnArgs), _vp], _int),
         "cmt_add_cast": ([_vp, _vp, _int, _int, _int, _vp, _vp, _vp], _int),
         "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _int, _i64, _vp], _int),
         "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _int, _vp], _int),
@@ -163,6 +164,18 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
     Offsets are in elements of the respective tensor.  A2 of A's dtype selects
     (replaces A for output columns < a2_cols); an fp32 A2 beside fp32 A is
     added on load."""
+    g = _gemm_args(A, W, C, M=M, N=N, K=K, lda=lda, ldw=ldw, ldc=ldc, bias=bias, relu=relu, R=R, ldr=ldr, A2=A2,
+                   lda2=lda2, a2_cols=a2_cols, a_mode=a_mode, conv=conv, seg_len=seg_len, batch=batch,
+                   a_bstride=a_bstride, w_bstride=w_bstride, bias_bstride=bias_bstride, r_bstride=r_bstride,
+                   c_bstride=c_bstride, headsplit_rows=headsplit_rows, a_offset=a_offset, c_offset=c_offset,
+                   r_offset=r_offset, a2_offset=a2_offset)
+    _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
+
+
+def _gemm_args(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0,
+               a2_cols=0, a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0,
+               bias_bstride=0, r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0,
+               a2_offset=0):
     _dev(A, W, C, bias, R, A2)
     g = GemmArgs()
     g.M, g.N, g.K, g.batch = M, N, K, batch
@@ -180,12 +193,12 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
     g.R = None if R is None else R.data_ptr() + r_offset * R.element_size()
     g.ldr, g.r_bstride = ldr, r_bstride
     g.r_dtype = F32 if R is None else DT[R.dtype]
-    g.C = C.data_ptr() + c_offset * C.element_size()
-    g.ldc, g.c_bstride, g.c_dtype = ldc, c_bstride, DT[C.dtype]
+    g.C = None if C is None else C.data_ptr() + c_offset * C.element_size()
+    g.ldc, g.c_bstride, g.c_dtype = ldc, c_bstride, DT[C.dtype] if C is not None else F32
     g.c_mode = C_HEADSPLIT if headsplit_rows else C_ROWS
     g.rows_per_batch = headsplit_rows
     g.relu = int(bool(relu))
-    _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
+    return g
 
 
 def linear(X, W, bias=None, *, relu=False, R=None, out=None, out_dtype=torch.float32, A2=None, a2_cols=0,
@@ -252,9 +265,16 @@ def layernorm_ex(X, W, Bv, *, rows, C, ldx, eps=1e-5, Y=None, ldy=0, flags=0, W2
                  flags2=0, Yl=None, Yp=None, P=None, y2_offset=0):
     """LayerNorm with optional second LN (Y2) and compute-dtype copies
     Yl = lowp(y), Yp = lowp(y + P) (rows of width C, contiguous)."""
+    a = _ln_args(X, W, Bv, rows=rows, C=C, ldx=ldx, eps=eps, Y=Y, ldy=ldy, flags=flags, W2=W2, B2=B2, Y2=Y2,
+                 ldy2=ldy2, flags2=flags2, Yl=Yl, Yp=Yp, P=P, y2_offset=y2_offset)
+    _check(lib().cmt_layernorm_ex(ctypes.byref(a), _stream()), "cmt_layernorm_ex")
+
+
+def _ln_args(X, W, Bv, *, rows, C, ldx, eps=1e-5, Y=None, ldy=0, flags=0, W2=None, B2=None, Y2=None, ldy2=0,
+             flags2=0, Yl=None, Yp=None, P=None, y2_offset=0):
     _dev(X, W, Bv, Y, W2, B2, Y2, Yl, Yp, P)
     a = LnArgs()
-    a.X, a.ldx, a.rows, a.C = X.data_ptr(), ldx, rows, C
+    a.X, a.ldx, a.rows, a.C = _p(X), ldx, rows, C
     a.W, a.B, a.eps = W.data_ptr(), Bv.data_ptr(), eps
     a.Y, a.ldy, a.flags = _p(Y), ldy, flags
     a.W2, a.B2 = _p(W2), _p(B2)
@@ -264,7 +284,18 @@ def layernorm_ex(X, W, Bv, *, rows, C, ldx, eps=1e-5, Y=None, ldy=0, flags=0, W2
     a.lowp_dtype = DT[low.dtype] if low is not None else BF16
     a.Yl, a.ldyl = _p(Yl), C
     a.Yp, a.ldyp, a.P, a.ldp = _p(Yp), C, _p(P), C
-    _check(lib().cmt_layernorm_ex(ctypes.byref(a), _stream()), "cmt_layernorm_ex")
+    return a
+
+
+def gemm_ln(A, W, *, M, K, lda, ldw, bias=None, R=None, ldr=0, ln_w, ln_b, eps=1e-5, Y=None, flags=0,
+            W2=None, B2=None, Y2=None, flags2=0, Yl=None, Yp=None, P=None, y2_offset=0):
+    """One launch of  y = LN(A W^T + bias + R)  with cmt_layernorm_ex's
+    outputs (N = C = 256, compute-dtype A/W, contiguous [M, 256] rows)."""
+    N = W.shape[0]
+    g = _gemm_args(A, W, None, M=M, N=N, K=K, lda=lda, ldw=ldw, ldc=0, bias=bias, R=R, ldr=ldr)
+    a = _ln_args(None, ln_w, ln_b, rows=M, C=N, ldx=0, eps=eps, Y=Y, ldy=N, flags=flags, W2=W2, B2=B2, Y2=Y2,
+                 ldy2=N, flags2=flags2, Yl=Yl, Yp=Yp, P=P, y2_offset=y2_offset)
+    _check(lib().cmt_gemm_ln(ctypes.byref(g), ctypes.byref(a), _stream()), "cmt_gemm_ln")
 
 
 def add_cast(X, *, rows, C, Yl=None, Yp=None, P=None):

@@ -165,6 +165,14 @@ typedef struct cmt_ln_args {
 } cmt_ln_args;
 int cmt_layernorm_ex(const cmt_ln_args* args, void* stream);
 
+/* cmt_gemm_ln: cmt_gemm followed by cmt_layernorm_ex on its output rows, in
+ * one launch (the post-norm "x = LN(x + sublayer(x))" of
+ * petr_transformer.py:374-487 for the attention out-projections and FFN fc2):
+ * t = A W^T + bias + R is never written; ln->X is ignored and every LN output
+ * of ln (Y, Yl, Yp, Y2) is produced.  Needs N == ln->C == 256, compute-dtype
+ * A/W, row mode, batch 1. */
+int cmt_gemm_ln(const cmt_gemm_args* gemm, const cmt_ln_args* ln, void* stream);
+
 /* cmt_add_cast: Yl = lowp(X), Yp = lowp(X + P) over rows x C (either output
  * may be NULL) -- the decoder's first-layer operands from the initial target. */
 int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,

@@ -301,6 +301,42 @@ def test_layernorm_ex_lowp_outputs(N, dev, lp):
     assert torch.equal(Zl, Yl) and torch.equal(Zp, Yp)
 
 
+@pytest.mark.parametrize("lp", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,K,r_lowp", [(900, 256, False), (133, 1024, True), (32, 256, False)])
+def test_gemm_ln_matches_unfused(N, dev, lp, M, K, r_lowp):
+    """cmt_gemm_ln == cmt_gemm (+bias +R) followed by cmt_layernorm_ex, for
+    every LN output (Y, lowp(y), lowp(y + P), post-norm Y2 with nan_to_num and
+    coop max-into)."""
+    g = torch.Generator().manual_seed(M + K)
+    C = 256
+    A = torch.randn(M, K, generator=g).to(lp).to(dev)
+    W = (torch.randn(C, K, generator=g) / math.sqrt(K)).to(lp).to(dev)
+    bias = torch.randn(C, generator=g).to(dev)
+    R = torch.randn(M, C, generator=g).to(dev)
+    if r_lowp:
+        R = R.to(lp)
+    lw, lb, w2, b2 = (torch.randn(C, generator=g).to(dev) for _ in range(4))
+    P = torch.randn(M, C, generator=g).to(dev)
+    prev = torch.randn(M, C, generator=g).to(dev)
+    # unfused reference path (both native)
+    t = torch.empty(M, C, device=dev)
+    N.gemm(A, W, t, M=M, N=C, K=K, lda=K, ldw=K, ldc=C, bias=bias, R=R, ldr=C)
+    Y0, Yl0, Yp0 = torch.empty(M, C, device=dev), torch.empty(M, C, device=dev, dtype=lp), torch.empty(M, C, device=dev, dtype=lp)
+    Y20 = prev.clone()
+    N.layernorm_ex(t, lw, lb, rows=M, C=C, ldx=C, Y=Y0, ldy=C, Yl=Yl0, Yp=Yp0, P=P, W2=w2, B2=b2, Y2=Y20, ldy2=C,
+                   flags2=N.LN_NAN_TO_NUM | N.LN_MAX_INTO)
+    Y1, Yl1, Yp1 = torch.empty_like(Y0), torch.empty_like(Yl0), torch.empty_like(Yp0)
+    Y21 = prev.clone()
+    N.gemm_ln(A, W, M=M, K=K, lda=K, ldw=K, bias=bias, R=R, ldr=C, ln_w=lw, ln_b=lb, Y=Y1, Yl=Yl1, Yp=Yp1, P=P,
+              W2=w2, B2=b2, Y2=Y21, flags2=N.LN_NAN_TO_NUM | N.LN_MAX_INTO)
+    assert (Y1 - Y0).abs().max().item() < 2e-4
+    assert (Y21 - Y20).abs().max().item() < 2e-4
+    ulp = 2 ** -7 if lp == torch.bfloat16 else 2 ** -10
+    for a_, b_ in ((Yl1, Yl0), (Yp1, Yp0)):
+        d = (a_.float() - b_.float()).abs()
+        assert (d <= ulp * b_.float().abs().clamp(min=1.0) + 1e-4).all()
+
+
 @pytest.mark.parametrize("odt", [torch.float16, torch.bfloat16])
 def test_attention_lowp_output(N, dev, odt):
     g = torch.Generator().manual_seed(21)
