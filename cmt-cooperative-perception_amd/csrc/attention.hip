@@ -19,9 +19,19 @@
 // 900-query problem still fills 256 CUs.
 #include "cmt_common.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace {
 
 constexpr int KT = 64;     // keys per tile
+// Deferred rescale (guide T13): the running max is only raised when a score
+// exceeds it by more than this many exp2 units, so P <= 2^8 (safe for f16 P)
+// and the O / row-sum rescale runs on a few tiles instead of whenever any
+// lane's max grows.  O = sum(P V) / sum(P) is invariant to the offset; only
+// the magnitude at which P is rounded to f16/bf16 changes (same relative
+// precision).
+constexpr float kDeferMax = 8.f;
 constexpr int QW = 32;     // queries per wave
 constexpr int NW = 4;      // waves per workgroup (f32 kernel; the f16/bf16 kernel takes it as a template arg)
 constexpr int QB = QW * NW;
@@ -39,6 +49,7 @@ struct AttnKParams {
     int splits;
     int tiles_per_split;
     int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
+    int sync_all;                   // diagnostics: drain every LDS-DMA before each tile (flag bit 1 << 8)
 };
 
 // Final normalised output: 4 consecutive head dims of one query row.
@@ -101,9 +112,10 @@ __device__ __forceinline__ void attn_tile_lowp(const T* __restrict__ Kt, const T
         m1 = vmax3(m1, s[1][r], s[1][r + 1]);
     }
     const float mt = pair_max(vmax(m0, m1));
-    if (first || __any(mt > 0.f)) {
+    if (first || __any(mt > (FOLD ? kDeferMax : kDeferMax / c))) {
         const float d = first ? mt : vmax(mt, 0.f);
-        const float alpha = __builtin_amdgcn_exp2f(-d * u);
+        // first tile: O and the sums are still 0 and -d may be huge (exp2 overflow -> 0*inf)
+        const float alpha = first ? 1.f : __builtin_amdgcn_exp2f(-d * u);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             o[r] *= alpha;
@@ -191,9 +203,10 @@ __device__ __forceinline__ void attn_tile2_lowp(const T* __restrict__ Kt, const 
             m1 = vmax3(m1, s[sb][1][r], s[sb][1][r + 1]);
         }
         const float mt = pair_max(vmax(m0, m1));
-        if (first || __any(mt > 0.f)) {
+        if (first || __any(mt > (FOLD ? kDeferMax : kDeferMax / c))) {
             const float d = first ? mt : vmax(mt, 0.f);
-            const float alpha = __builtin_amdgcn_exp2f(-d * u);
+            // first tile: O and the sums are still 0 and -d may be huge (exp2 overflow -> 0*inf)
+        const float alpha = first ? 1.f : __builtin_amdgcn_exp2f(-d * u);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 o[sb][r] *= alpha;
@@ -251,7 +264,7 @@ __device__ __forceinline__ void wait_vm_lgkm() {
 }
 
 template <typename T, int NWAVES, bool FOLD, int SUB>
-__global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : 2) void attn_fwd_kernel(AttnKParams p) {
+__global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : (NWAVES == 8 ? 2 : 2)) void attn_fwd_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
     static_assert(SUB == 1 || SUB == 2, "1 or 2 query sub-blocks per wave");
     constexpr int PERT = 8 / NWAVES;               // glds per thread per tile (8 KB / (NWAVES KB))
@@ -330,7 +343,7 @@ __global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : 2) void attn_fwd_kernel
         if (i < nt) issue(i, t_begin + i);
     for (int i = 0; i < nt; ++i) {
         const int issued = min(nt, RING - 1 + i);
-        const int inflight = issued - i - 1;                   // tiles allowed to stay in flight
+        const int inflight = p.sync_all ? 0 : issued - i - 1;  // tiles allowed to stay in flight
         if (inflight >= 2) wait_vm_lgkm<2 * PERT>();
         else if (inflight == 1) wait_vm_lgkm<PERT>();
         else wait_vm_lgkm<0>();
@@ -596,11 +609,21 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
 }
 
 // Launch shape of the f16/bf16 kernel: waves per workgroup x query
-// sub-blocks per wave.  Long key ranges: 4 waves x 2 sub-blocks (256 queries
-// share each staged K/V tile); short ones (self-attention): 4 waves x 1.
+// sub-blocks per wave.  Long key ranges: 8 waves x 1 (256 queries share each
+// staged K/V tile, 2 waves per SIMD); short ones (self-attention): 4 x 1.
+// The 4 x 2 shape (two chains per wave) needs ~370 registers, and hipcc then
+// parks the accumulators in AGPRs and copies them back for every VALU use
+// (measured 125 us vs 79 us at the CMT-L cross-attention shape).
 struct LowpShape { int waves, sub; };
 LowpShape lowp_shape(const cmt_attn_args& a) {
-    if (a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128) return {4, 2};
+    // diagnostics: CMT_ATTN_SHAPE="waves,sub" (4|8, 1|2) overrides the choice
+    static const char* ov = getenv("CMT_ATTN_SHAPE");
+    if (ov && ov[0]) {
+        int w = 4, sb = 1;
+        if (sscanf(ov, "%d,%d", &w, &sb) == 2 && (w == 4 || w == 8) && (sb == 1 || sb == 2) && !(w == 8 && sb == 2))
+            return {w, sb};
+    }
+    if (a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128) return {8, 1};
     return {4, 1};
 }
 
@@ -612,10 +635,10 @@ int choose_splits(const cmt_attn_args& a) {
     const int qrows = a.dtype == CMT_F32 ? QB : sh.waves * sh.sub * QW;
     const int base = cdiv(a.Nq, qrows) * a.B * a.H;
     int s = 1;
-    // aim for >= 1024 waves (one per SIMD) while keeping >= 8 tiles per split;
+    // aim for >= 2048 waves (two per SIMD) while keeping >= 8 tiles per split;
     // short key ranges (self-attention) split down to 2 tiles per split
     const int min_tiles = ntiles >= 64 ? 8 : 2;
-    while ((int64_t)base * s * nw < 1024 && ntiles / (2 * s) >= min_tiles) s *= 2;
+    while ((int64_t)base * s * nw < 2048 && ntiles / (2 * s) >= min_tiles) s *= 2;
     return s;
 }
 
@@ -657,6 +680,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     p.splits = splits;
     p.tiles_per_split = cdiv(ntiles, splits);
     p.round_out = (a.flags & CMT_ATTN_ROUND_OUTPUT) && a.dtype != CMT_F32 ? a.dtype : 0;
+    p.sync_all = (a.flags >> 8) & 1;
     p.Op = p.Mp = p.Lp = nullptr;
     if (splits > 1) {
         const int64_t need = cmt_attn_workspace_bytes(&a);
@@ -676,6 +700,9 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         if (sh.sub == 2) {                                                                               \
             if (fold) attn_fwd_kernel<T, 4, true, 2><<<grid, 256, 0, s>>>(p);                            \
             else attn_fwd_kernel<T, 4, false, 2><<<grid, 256, 0, s>>>(p);                                \
+        } else if (sh.waves == 8) {                                                                      \
+            if (fold) attn_fwd_kernel<T, 8, true, 1><<<grid, 512, 0, s>>>(p);                            \
+            else attn_fwd_kernel<T, 8, false, 1><<<grid, 512, 0, s>>>(p);                                \
         } else {                                                                                         \
             if (fold) attn_fwd_kernel<T, 4, true, 1><<<grid, 256, 0, s>>>(p);                            \
             else attn_fwd_kernel<T, 4, false, 1><<<grid, 256, 0, s>>>(p);                                \

@@ -52,19 +52,13 @@ template <> struct mfma_traits<f16_t> {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// Single-instruction max helpers: fmaxf on MFMA results makes hipcc emit a
-// canonicalising v_max_f32 x,x per operand (MI355X guide, attention pitfalls);
-// inputs here are finite or -inf, so the raw instruction is exact.
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ float vmax(float a, float b) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
+// Max helpers.  These must stay compiler-visible (no inline asm): their
+// inputs are often MFMA results, and a VALU read of an MFMA destination needs
+// hazard wait states that hipcc only inserts for instructions it can see.
+// attention.hip is built with -fno-honor-nans, so fmaxf lowers to a single
+// v_max/v_max3 without the NaN-canonicalising v_max_f32 x,x per operand.
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+__device__ __forceinline__ float vmax(float a, float b) { return fmaxf(a, b); }
 // max of x over the lane pair (l, l ^ 32) via v_permlane32_swap (no LDS round trip)
 __device__ __forceinline__ float pair_max(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);

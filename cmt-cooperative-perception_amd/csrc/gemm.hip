@@ -650,7 +650,7 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     // every wave instruction stores 1 KB of contiguous memory (head-split:
     // 16 rows x 64 B of one head; rows: whole row segments).
     barrier_mem();                                       // every wave is done with the staging ring
-    const int cpr = BN * esz / 16;                       // 16-byte chunks per tile row
+    const int cpr = BN * esz / 16;                       // 16-byte chunks per tile row (power of two)
     const int cpe = 16 / esz;                            // elements per chunk
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -668,29 +668,40 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
             }
     }
     barrier_mem();
-    const int nchunks = BM * cpr;
     const bool headsplit = a.c_mode != CMT_C_ROWS;
-    const int cph = 32 * esz / 16;                       // chunks per 32-column head slice of a row
-    for (int q = threadIdx.x; q < nchunks; q += NT) {
+    const int lcpr = esz == 4 ? __builtin_ctz(BN / 4) : __builtin_ctz(BN / 8);   // log2 chunks per row
+    const int lcph = esz == 4 ? 3 : 2;                   // log2 chunks per 32-column head slice
+    constexpr int LBM = __builtin_ctz(BM);
+    // batch of the tile's first row; a tile spans at most two batches when rows_per_batch >= BM
+    const int rpb = headsplit ? a.rows_per_batch : 1;
+    const int b0 = headsplit ? m0 / rpb : 0;
+    const int rr0 = m0 - b0 * rpb;
+#pragma unroll 4
+    for (int q = threadIdx.x; q < (BM << lcpr); q += NT) {
         int row, c;
         if (headsplit) {                                 // head-major, then row, then chunk: contiguous in memory
-            const int h = q / (BM * cph);
-            const int rem = q - h * (BM * cph);
-            row = rem / cph;
-            c = h * cph + (rem - row * cph);
+            const int h = q >> (LBM + lcph);
+            const int rem = q & ((BM << lcph) - 1);
+            row = rem >> lcph;
+            c = (h << lcph) + (rem & ((1 << lcph) - 1));
         } else {
-            row = q / cpr;
-            c = q - row * cpr;
+            row = q >> lcpr;
+            c = q & ((1 << lcpr) - 1);
         }
         const int m = m0 + row;
         if (m >= a.M) continue;
-        const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4));
+        const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & ((1 << lcpr) - 1))) << 4));
         const int n = n0 + c * cpe;
         int64_t idx;
         if (headsplit) {
-            const int bb = m / a.rows_per_batch;
-            const int rr = m - bb * a.rows_per_batch;
-            idx = (((int64_t)bb * (a.N >> 5) + (n >> 5)) * a.rows_per_batch + rr) * 32 + (n & 31);
+            int bb = b0, rr = rr0 + row;
+            if (rpb >= BM) {
+                if (rr >= rpb) { rr -= rpb; ++bb; }
+            } else {
+                bb = m / rpb;
+                rr = m - bb * rpb;
+            }
+            idx = (((int64_t)bb * (a.N >> 5) + (n >> 5)) * rpb + rr) * 32 + (n & 31);
         } else {
             idx = (int64_t)m * a.ldc + n;
         }

@@ -489,7 +489,7 @@ class PETRTransformerDecoder(nn.Module):
         ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
         pw, pb, _pe = pk["post"]
         # out-projection / fc2 GEMMs fused with their residual + LayerNorm (cmt_gemm_ln)
-        fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "1") != "0"
+        fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "0") == "1"
         for l, lw in enumerate(pk["layers"]):
             # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
             native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],

@@ -219,7 +219,7 @@ _WS_CACHE = {}
 
 def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, q_offset=0,
               k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False,
-              fold_scale=False):
+              fold_scale=False, _diag_flags=0):
     """Strides are (batch, head, row) in elements; o_strides = (batch, row).
     fold_scale lets the kernel fold scale*log2(e) into Q on load (one extra
     rounding of Q; the f16/bf16 policies only)."""
@@ -237,7 +237,7 @@ def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_st
     a.o_bstride, a.o_rstride = o_strides
     a.o_dtype = DT[O.dtype]
     a.scale, a.kv_splits = scale, kv_splits
-    a.flags = (1 if round_output else 0) | (2 if fold_scale else 0)
+    a.flags = (1 if round_output else 0) | (2 if fold_scale else 0) | _diag_flags
     need = lib().cmt_attn_workspace_bytes(ctypes.byref(a))
     if need > 0:
         if workspace is None or workspace.numel() < need:

@@ -110,7 +110,7 @@ def main():
         gemm_case("ffn fc1 (relu)", 900, 1024, 256, bf, a_f32=False, relu=True, out_dt=bf)
         gemm_case("ffn fc2 (+res)", 900, 256, 1024, bf, a_f32=False, R=True)
     if args.only in ("", "attn"):
-        for s in (0, 4, 8, 12, 16, 32):
+        for s in (0, 8, 16):
             for fold in (False, True):
                 attn_case("cross 900x32400", 900, 32400, bf, splits=s, fold=fold)
         attn_case("cross fp16", 900, 32400, torch.float16)

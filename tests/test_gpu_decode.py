@@ -25,7 +25,7 @@ def _preds(B, Nq, class_split, seed, ties=False):
 @pytest.mark.parametrize("B,Nq,split,max_num,thr,ties", [(1, 900, [10], 300, None, False),
                                                         (2, 300, [3, 4], 100, 0.3, False),
                                                         (1, 200, [10], 150, None, True),
-                                                        (3, 50, [7], 350, 0.05, False)])
+                                                        (3, 400, [7], 350, 0.05, False)])
 def test_native_decode_matches_oracle(dev, B, Nq, split, max_num, thr, ties):
     from oracle import cmt_oracle as O
     from projects.mmdet3d_plugin.core.bbox.coders import MultiTaskBBoxCoder
