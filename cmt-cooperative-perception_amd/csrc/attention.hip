@@ -21,6 +21,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -37,8 +38,16 @@ constexpr int NW = 4;      // waves per workgroup (f32 kernel; the f16/bf16 kern
 constexpr int QB = QW * NW;
 constexpr int D = 32;
 
+// Bounded-max mode (bf16 P only): exp2 units below which the Cauchy-Schwarz
+// bound |q| * max|k| may serve as the fixed softmax offset of a query row
+// (s - bound >= -2 * bound >= -2 * kBoundMax stays a normal bf16/f32 number).
+constexpr float kBoundMax = 60.f;
+
 struct AttnKParams {
     int B, H, Nq, Nk;
+    int nqb;                        // query blocks per (b, h) (ping-pong kernel's 1-D grid)
+    const float* kmax2;             // optional: per-row-block max |k|^2 partials [e][kmax_ld]
+    int kmax_ld, kmax_plane0, kmax_rows;
     const void* Q; int64_t q_bs, q_hs, q_rs;
     const void* K; int64_t k_bs, k_hs, k_rs;
     const void* V; int64_t v_bs, v_hs, v_rs;
@@ -404,6 +413,376 @@ __global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : (NWAVES == 8 ? 2 : 2)) 
 }
 
 // ---------------------------------------------------------------------------
+// Ping-pong kernel for long key ranges (the cross-attention shape), f16/bf16.
+//
+// 8 waves = two halves of 4 (wave w sits on SIMD w % 4, so every SIMD holds
+// one wave of each half).  A wave's work per 64-key tile is split into a
+// matrix segment M(i) = {QK^T of tile i, PV + row sums of tile i-1} and a
+// vector segment V(i) = {softmax of tile i's scores}.  Every segment ends at a
+// workgroup barrier.  Both halves run the same straight-line program, but half
+// B passes one extra barrier first (and half A one at the end), so between two
+// barriers one wave of each SIMD issues MFMAs while its partner issues the
+// exponentials (MI355X_MICROARCH.md 'Two waves per SIMD'):
+//     window 2i   : A: M(i)     B: V(i-1)
+//     window 2i+1 : A: V(i)     B: M(i)
+// Half A stages the K/V tiles (LDS-DMA, two 1-KB pieces per wave and tile):
+// tile t's K is read in windows 2t, 2t+1 and its V in 2t+2, 2t+3, so its slot
+// is refilled at window 2t+4 with tile t + PPR, first read 2(PPR-2) windows
+// later.  Only full 64-key tiles run through the ping-pong loop; a ragged last
+// tile is masked and processed by all waves after it.
+//
+// Bounded-max mode (bf16 with the optional max-|k| partials): the softmax
+// offset of a query is fixed at bound = |q| * max_k |k| >= every score
+// (Cauchy-Schwarz), so V(i) is only exp2 + convert -- no running max, no
+// rescale.  O = sum(P V) / sum(P) is invariant to the offset; P <= 1 and
+// s - bound >= -2 * kBoundMax keeps P a normal bf16.  Waves with a larger
+// bound (or f16, or no partials) track the running max online as above.
+// ---------------------------------------------------------------------------
+constexpr int PPR = 6;   // K/V ring slots (8 KB per tile)
+
+__device__ __forceinline__ void pp_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS -> register fragments of one tile: K rows (A operand of S^T = K Q^T,
+// XOR-swizzled image) and V^T (A operand of O^T += V^T P^T, transposed reads).
+// The lane-dependent parts of the addresses are byte offsets (PpLane) that the
+// caller re-launders per use (empty asm), so every read is lane base +
+// compile-time immediate -- no per-slot address registers kept live.
+struct PpLane {
+    int k0, k1;   // K row lr, chunks (lh ^ sw) and (2 + lh) ^ sw
+    int v;        // V^T transposed-read base
+};
+
+__device__ __forceinline__ PpLane pp_lane(int lane, int esz) {
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    const int sw = (lr >> 2) & 3;
+    PpLane l;
+    l.k0 = (lr * D + 8 * (lh ^ sw)) * esz;
+    l.k1 = (lr * D + 8 * ((2 + lh) ^ sw)) * esz;
+    l.v = ((4 * lh + ((lane & 15) >> 2)) * D + 16 * ((lane >> 4) & 1) + 4 * (lane & 3)) * esz;
+    return l;
+}
+
+__device__ __forceinline__ PpLane pp_launder(PpLane l) {
+    asm volatile("" : "+v"(l.k0), "+v"(l.k1), "+v"(l.v));
+    return l;
+}
+
+// Kt / Vt: tile base (compile-time offset into the ring), byte-addressed
+template <typename T>
+__device__ __forceinline__ void pp_load_k(const char* Kt, const PpLane& l, typename mfma_traits<T>::frag (&kf)[2][2]) {
+    typedef typename mfma_traits<T>::frag frag;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        kf[kb][0] = *(const frag*)(Kt + l.k0 + kb * 32 * D * (int)sizeof(T));
+        kf[kb][1] = *(const frag*)(Kt + l.k1 + kb * 32 * D * (int)sizeof(T));
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void pp_load_v(const char* Vt, const PpLane& l, typename mfma_traits<T>::frag (&vf)[2][2]) {
+    typedef typename mfma_traits<T>::frag frag;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            const char* base0 = Vt + l.v + (kb * 32 + 16 * ss) * D * (int)sizeof(T);
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)(base0 + 8 * D * sizeof(T)));
+            s16x8 vv;
+            vv[0] = lo[0]; vv[1] = lo[1]; vv[2] = lo[2]; vv[3] = lo[3];
+            vv[4] = hi[0]; vv[5] = hi[1]; vv[6] = hi[2]; vv[7] = hi[3];
+            vf[kb][ss] = __builtin_bit_cast(frag, vv);
+        }
+}
+
+// M segment on prefetched fragments: QK^T (accumulator init -m_run) into s
+// (QK = true), then O += V^T P^T and the row sums of the previous tile's P
+// (PV = true) -- MFMAs only.
+template <typename T, bool QK, bool PV>
+__device__ __forceinline__ void pp_mseg(const typename mfma_traits<T>::frag (&kf)[2][2],
+                                        const typename mfma_traits<T>::frag (&vf)[2][2],
+                                        const typename mfma_traits<T>::frag (&qf)[2], const f32x16& negm,
+                                        const typename mfma_traits<T>::frag (&pf)[2][2], f32x16 (&s)[2], f32x16& o,
+                                        f32x16& lsum) {
+    typedef typename mfma_traits<T>::frag frag;
+    if (QK) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            s[kb] = mfma_traits<T>::mma(kf[kb][0], qf[0], negm);
+            s[kb] = mfma_traits<T>::mma(kf[kb][1], qf[1], s[kb]);
+        }
+    }
+    if (PV) {
+        frag ones;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                o = mfma_traits<T>::mma(vf[kb][ss], pf[kb][ss], o);
+                lsum = mfma_traits<T>::mma(ones, pf[kb][ss], lsum);
+            }
+    }
+}
+
+// V segment: softmax of one full tile's scores (s' = s - m_run from the MFMA) into P.
+template <typename T, bool FOLD>
+__device__ __forceinline__ void pp_vseg(f32x16 (&s)[2], typename mfma_traits<T>::frag (&pf)[2][2], f32x16& o,
+                                        f32x16& lsum, f32x16& negm, float& m_run, bool online, bool first, float c) {
+    const float u = FOLD ? 1.f : c;   // s' units -> exp2 units
+    if (online) {
+        float m0 = vmax(s[0][0], s[0][1]), m1 = vmax(s[1][0], s[1][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            m0 = vmax3(m0, s[0][r], s[0][r + 1]);
+            m1 = vmax3(m1, s[1][r], s[1][r + 1]);
+        }
+        const float mt = pair_max(vmax(m0, m1));
+        if (first || __any(mt > (FOLD ? kDeferMax : kDeferMax / c))) {
+            const float d = first ? mt : vmax(mt, 0.f);
+            // first tile: O and the sums are still 0 and -d may be huge (exp2 overflow -> 0*inf)
+            const float alpha = first ? 1.f : __builtin_amdgcn_exp2f(-d * u);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                o[r] *= alpha;
+                lsum[r] *= alpha;
+                s[0][r] -= d;
+                s[1][r] -= d;
+            }
+            m_run += d;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[0][r] : s[0][r] * u);
+        pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[1][r] : s[1][r] * u);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void pp_wait_n() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+// tiles still allowed in flight (two LDS-DMA pieces each) behind the one needed now
+__device__ __forceinline__ void pp_wait(int tiles) {
+    static_assert(PPR - 3 == 3, "wait ladder below covers 0..3 tiles");
+    if (tiles >= 3) pp_wait_n<6>();
+    else if (tiles == 2) pp_wait_n<4>();
+    else if (tiles == 1) pp_wait_n<2>();
+    else pp_wait_n<0>();
+}
+
+template <typename T, bool FOLD>
+__global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
+    __shared__ __attribute__((aligned(16))) T ring[PPR * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool hb = wave >= 4;          // wave-uniform: second half runs one segment behind
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+
+    // XCD-aware block order: the query blocks of one (b, h, split) -- which
+    // stream the same K/V -- are consecutive logical blocks on one XCD (L2).
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int qb = wg % p.nqb;
+    const int rest = wg / p.nqb;
+    const int BH = p.B * p.H;
+    const int bh = rest % BH;
+    const int split = rest / BH;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+
+    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+    const float c = p.c;
+
+    // ---- Q^T fragments (B operand), ordinary loads: all before the first LDS-DMA
+    const int q = qb * (8 * QW) + wave * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    frag qf[2];
+    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+    if (FOLD) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
+    }
+
+    f32x16 o, lsum, negm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o[r] = 0.f;
+        lsum[r] = 0.f;
+        negm[r] = 0.f;
+    }
+    float m_run = 0.f;   // online: placeholder until the first tile sets it
+    bool online = true;
+    if (p.kmax2 != nullptr) {
+        // max |k|^2 over this batch's key rows (partials cover kmax_rows rows each)
+        const int64_t r0 = (int64_t)b * p.Nk;
+        const int e0 = (int)(r0 / p.kmax_rows), e1 = (int)((r0 + p.Nk - 1) / p.kmax_rows);
+        float km = 0.f;
+        for (int e = e0 + lane; e <= e1; e += 64) km = fmaxf(km, p.kmax2[(int64_t)e * p.kmax_ld + p.kmax_plane0 + h]);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
+        float qq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
+        qq = pair_sum(qq);
+        // >= max_k q.k in the MFMA's units (the margin covers fp32 accumulation)
+        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
+        const float u = FOLD ? 1.f : c;
+        if (__all(bound * u <= kBoundMax)) {
+            online = false;
+            m_run = bound;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) negm[r] = -bound;
+        }
+    }
+
+    const int ntiles = (p.Nk + KT - 1) / KT;
+    const int t_begin = split * p.tiles_per_split;
+    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+    const bool tail = (p.Nk % KT) != 0 && t_end == ntiles && t_begin < t_end;   // ragged last tile here
+    const int nt = max(0, t_end - t_begin - (tail ? 1 : 0));                    // full tiles
+
+    // half A's two 1-KB pieces of every tile: K and V rows (wave & 3) * 16 .. +15
+    // of the tile, issued in tile order from running source pointers (full
+    // tiles only: no clamp), into compile-time ring slots
+    const int crow = lane >> 2, cch = lane & 3;
+    const int prow = (wave & 3) * 16 + crow;
+    const T* ksrc = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+    const T* vsrc = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
+    const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
+    T* const my_k = ring + (wave & 3) * 16 * D;      // this wave's piece of slot 0 (K), + KT*D for V
+    auto issue_next = [&](int slot) {
+        __builtin_amdgcn_global_load_lds((gaddr_t)ksrc, (laddr_t)(my_k + slot * STAGE), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gaddr_t)vsrc, (laddr_t)(my_k + slot * STAGE + KT * D), 16, 0, 0);
+        ksrc += kstep;
+        vsrc += vstep;
+    };
+
+    const char* const rb = (const char*)ring;
+    constexpr int STAGE_B = STAGE * (int)sizeof(T), KV_B = KT * D * (int)sizeof(T);
+    const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
+    f32x16 s[2];
+    frag pf[2][2], kf[2][2], vf[2][2];
+    if (!hb) {
+#pragma unroll
+        for (int i = 0; i < PPR - 2; ++i)
+            if (i < nt) issue_next(i);
+    } else {
+        pp_barrier();   // half B: one segment behind
+    }
+    // Tile t is complete for every wave from window 2t-1 on (half A waits
+    // before that barrier): the V segment of tile t-1 prefetches K(t) and
+    // V(t-1) into registers, so each M segment is MFMAs only.
+    if (nt > 0) {
+        // M(0): QK^T of tile 0
+        if (!hb) pp_wait(min(nt - 1, PPR - 3));
+        pp_barrier();
+        if (!hb && PPR - 2 < nt) issue_next(PPR - 2);
+        pp_load_k<T>(rb, pp_launder(lane_ofs), kf);
+        pp_mseg<T, true, false>(kf, vf, qf, negm, pf, s, o, lsum);
+        // V(0)
+        if (!hb && nt > 1) pp_wait(min(nt - 1, PPR - 2) - 1);
+        pp_barrier();
+        pp_vseg<T, FOLD>(s, pf, o, lsum, negm, m_run, online, true, c);
+        {
+            const PpLane l = pp_launder(lane_ofs);
+            pp_load_k<T>(rb + 1 * STAGE_B, l, kf);   // stale (unused) when nt == 1
+            pp_load_v<T>(rb + KV_B, l, vf);
+        }
+        // slots as wave-uniform counters: K of tile i+1, V of tile i, DMA target of tile i+PPR-2
+        int kslot = 1, vslot = 0, islot = PPR - 1;
+        for (int i = 1; i < nt; ++i) {
+            // M(i): QK^T of tile i, PV of tile i-1
+            pp_barrier();
+            if (!hb && i + PPR - 2 < nt) issue_next(islot);
+            pp_mseg<T, true, true>(kf, vf, qf, negm, pf, s, o, lsum);
+            // V(i): softmax of tile i; prefetch K(i+1) (stale after the last tile) and V(i)
+            if (!hb && i + 1 < nt) pp_wait(min(nt - 1, i + PPR - 2) - (i + 1));
+            pp_barrier();
+            pp_vseg<T, FOLD>(s, pf, o, lsum, negm, m_run, online, false, c);
+            kslot = kslot == PPR - 1 ? 0 : kslot + 1;
+            vslot = vslot == PPR - 1 ? 0 : vslot + 1;
+            islot = islot == PPR - 1 ? 0 : islot + 1;
+            const PpLane l = pp_launder(lane_ofs);
+            pp_load_k<T>(rb + kslot * STAGE_B, l, kf);
+            pp_load_v<T>(rb + vslot * STAGE_B + KV_B, l, vf);
+        }
+        // last M: PV of tile nt-1
+        pp_barrier();
+        pp_mseg<T, false, true>(kf, vf, qf, negm, pf, s, o, lsum);
+    }
+    if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
+
+    if (tail) {
+        // ragged last tile: masked, every wave at once (slots are free: all waves passed the last barrier)
+        pp_barrier();
+        if (!hb) {
+            const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked in compute
+            const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+            const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
+            __builtin_amdgcn_global_load_lds((gaddr_t)ks, (laddr_t)my_k, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gaddr_t)vs, (laddr_t)(my_k + KT * D), 16, 0, 0);
+            pp_wait_n<0>();
+        }
+        pp_barrier();
+        attn_tile_lowp<T, true, FOLD>(ring, ring + KT * D, qf, o, lsum, negm, m_run, nt == 0, c, (ntiles - 1) * KT,
+                                      p.Nk, lane);
+    }
+
+    // ---- write ---------------------------------------------------------------
+    const float l_tot = lsum[0];
+    if (q >= p.Nq) return;
+    if (p.splits == 1) {
+        const float inv = 1.f / l_tot;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+            if (p.round_out) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+            }
+            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
+        }
+    } else {
+        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
+        float* dst = p.Op + row * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+        if (lh == 0) {
+            p.Mp[row] = FOLD ? m_run : m_run * c;   // exp2 units for the combine
+            p.Lp[row] = l_tot;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Exact-f32 variant (v_mfma_f32_32x32x2_f32): same tiling and online softmax;
 // used where the reference computes attention in fp32 (nn.MultiheadAttention
 // self-attention).  K image rows padded to 36 floats (conflict-free
@@ -627,6 +1006,15 @@ LowpShape lowp_shape(const cmt_attn_args& a) {
     return {4, 1};
 }
 
+// The ping-pong kernel takes the 8 x 1 shape (long key ranges); CMT_ATTN_PP=0
+// selects the single-phase 8 x 1 kernel instead (diagnostics / A-B timing).
+bool use_pp(const cmt_attn_args& a) {
+    static const char* ov = getenv("CMT_ATTN_PP");
+    if (ov && ov[0] == '0') return false;
+    const LowpShape sh = lowp_shape(a);
+    return a.dtype != CMT_F32 && sh.waves == 8 && sh.sub == 1;
+}
+
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
     const int ntiles = (a.Nk + KT - 1) / KT;
@@ -670,8 +1058,15 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     CMT_REQUIRE(splits <= 16 || splits == 24 || splits == 32 || splits == 48 || splits == 64,
                 "cmt_attn_fwd: kv_splits must be <= 16, 24, 32, 48 or 64");
     const int ntiles = (a.Nk + KT - 1) / KT;
+    CMT_REQUIRE(a.kmax2 == nullptr || (a.kmax_rows > 0 && a.kmax_ld > 0 && a.kmax_plane0 >= 0 &&
+                                       a.kmax_plane0 + a.H <= a.kmax_ld),
+                "cmt_attn_fwd: bad kmax2 partials geometry");
     AttnKParams p;
     p.B = a.B; p.H = a.H; p.Nq = a.Nq; p.Nk = a.Nk;
+    p.nqb = cdiv(a.Nq, 8 * QW);
+    // bounded-max mode needs bf16 P (f16's range cannot hold exp2(-2 * bound))
+    p.kmax2 = a.dtype == CMT_BF16 ? a.kmax2 : nullptr;
+    p.kmax_ld = a.kmax_ld; p.kmax_plane0 = a.kmax_plane0; p.kmax_rows = a.kmax_rows;
     p.Q = a.Q; p.q_bs = a.q_bstride; p.q_hs = a.q_hstride; p.q_rs = a.q_rstride;
     p.K = a.K; p.k_bs = a.k_bstride; p.k_hs = a.k_hstride; p.k_rs = a.k_rstride;
     p.V = a.V; p.v_bs = a.v_bstride; p.v_hs = a.v_hstride; p.v_rs = a.v_rstride;
@@ -708,9 +1103,22 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
             else attn_fwd_kernel<T, 4, false, 1><<<grid, 256, 0, s>>>(p);                                \
         }                                                                                                \
     } while (0)
-    if (a.dtype == CMT_F32) attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
-    else if (a.dtype == CMT_F16) ATTN_LAUNCH(f16_t);
-    else ATTN_LAUNCH(bf16_t);
+    if (a.dtype == CMT_F32) {
+        attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
+    } else if (use_pp(a)) {
+        const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
+        if (a.dtype == CMT_F16) {
+            if (fold) attn_pp_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);
+            else attn_pp_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
+        } else {
+            if (fold) attn_pp_kernel<bf16_t, true><<<nwg, 512, 0, s>>>(p);
+            else attn_pp_kernel<bf16_t, false><<<nwg, 512, 0, s>>>(p);
+        }
+    } else if (a.dtype == CMT_F16) {
+        ATTN_LAUNCH(f16_t);
+    } else {
+        ATTN_LAUNCH(bf16_t);
+    }
 #undef ATTN_LAUNCH
     int rc = cmt_check_launch("cmt_attn_fwd");
     if (rc || splits == 1) return rc;

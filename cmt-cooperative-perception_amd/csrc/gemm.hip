@@ -676,6 +676,53 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     const int rpb = headsplit ? a.rows_per_batch : 1;
     const int b0 = headsplit ? m0 / rpb : 0;
     const int rr0 = m0 - b0 * rpb;
+    // head-plane max of squared row norms (cmt_gemm_args.plane_max2, 16-bit C):
+    // with 4 chunks per 32-column head row one iteration of the loop below
+    // covers one head plane x 64 rows -- one entry
+    if (headsplit && a.plane_max2 != nullptr && esz == 2) {
+        constexpr int PITERS = BM * BN / 8 / NT;         // 16-byte chunks of the 16-bit tile per thread
+        float* red = (float*)(smem + BM * BN * 2);       // [iteration][wave], after the staged tile
+#pragma unroll
+        for (int it = 0; it < PITERS; ++it) {
+            const int q = threadIdx.x + it * NT;
+            const int h = q >> (LBM + 2);
+            const int rem = q & ((BM << 2) - 1);
+            const int row = rem >> 2;
+            const int c = (h << 2) + (rem & 3);
+            const f32x4 v = *(const f32x4*)(smem + row * (BN * 2) + ((c ^ (row & ((1 << lcpr) - 1))) << 4));
+            float ss = 0.f;
+            if (m0 + row < a.M && n0 + c * 8 < a.plane_max_cols) {
+                if (a.c_dtype == CMT_BF16) {
+                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 w = __builtin_bit_cast(u32x4, v);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float lo = __uint_as_float(w[j] << 16), hi = __uint_as_float(w[j] & 0xffff0000u);
+                        ss += lo * lo + hi * hi;
+                    }
+                } else {
+                    const f16x8 hv = __builtin_bit_cast(f16x8, v);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ss += (float)hv[j] * (float)hv[j];
+                }
+            }
+            ss += __shfl_xor(ss, 1);                     // the 4 chunks of one head row
+            ss += __shfl_xor(ss, 2);
+#pragma unroll
+            for (int off = 4; off < 64; off <<= 1) ss = fmaxf(ss, __shfl_xor(ss, off));
+            if ((threadIdx.x & 63) == 0) red[it * 4 + (threadIdx.x >> 6)] = ss;
+        }
+        barrier_mem();
+        if ((int)threadIdx.x < PITERS) {
+            const int itx = threadIdx.x;
+            const float mx = fmaxf(fmaxf(red[itx * 4], red[itx * 4 + 1]), fmaxf(red[itx * 4 + 2], red[itx * 4 + 3]));
+            const int q0 = itx * NT;
+            const int plane = (n0 >> 5) + (q0 >> (LBM + 2));
+            const int row0 = (q0 & ((BM << 2) - 1)) >> 2;
+            if (plane * 32 < a.plane_max_cols)
+                a.plane_max2[(int64_t)((m0 + row0) >> 6) * (a.plane_max_cols >> 5) + plane] = mx;
+        }
+    }
 #pragma unroll 4
     for (int q = threadIdx.x; q < (BM << lcpr); q += NT) {
         int row, c;
@@ -941,6 +988,11 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
                     "cmt_gemm: bad conv1d3 geometry");
     if (a.c_mode == CMT_C_HEADSPLIT)
         CMT_REQUIRE(a.rows_per_batch > 0 && a.M % a.rows_per_batch == 0, "cmt_gemm: bad head-split rows");
+    if (a.plane_max2 != nullptr)
+        CMT_REQUIRE(a.c_mode == CMT_C_HEADSPLIT && (a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16) &&
+                    a.w_dtype != CMT_F32 && a.a_dtype == a.w_dtype && a.plane_max_cols % 32 == 0 &&
+                    a.plane_max_cols <= a.N,
+                    "cmt_gemm: plane_max2 needs a head-split 16-bit C, compute-dtype A and plane_max_cols % 32 == 0");
     hipStream_t s = (hipStream_t)stream;
     if (a.w_dtype != CMT_F32 && a.a_dtype == a.w_dtype) {
         // LDS-DMA path: 64-deep k stages

@@ -469,8 +469,13 @@ class PETRTransformerDecoder(nn.Module):
             memb, mposb = kv_operands
         # K/V of every layer in one GEMM: K columns read lowp(mem + pos), V columns lowp(mem)
         kv = torch.empty((B * 2 * L * C * Nk,), dtype=prec.attn, device=dev)
+        # bf16: the K columns' per-64-row max |k|^2 (epilogue by-product) bounds every score,
+        # so the cross-attention kernel needs no running max (cmt_hip.h kmax2)
+        kmax2 = None
+        if prec.attn == torch.bfloat16 and os.environ.get("CMT_ATTN_BOUND", "1") != "0":
+            kmax2 = torch.empty((-(-B * Nk // native.PLANE_MAX_ROWS), L * H), dtype=f32, device=dev)
         native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
-                    A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk)
+                    A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
         # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114)
         tgt = tgt0.clone() if tgt0 is not None else torch.zeros((rows, C), dtype=f32, device=dev)
         tl = torch.empty((rows, C), dtype=lp, device=dev)          # lowp(tgt)
@@ -514,7 +519,8 @@ class PETRTransformerDecoder(nn.Module):
                                  q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
                                  v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
                                  v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
-                                 round_output=prec.round_cross_out, fold_scale=True)
+                                 round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2, kmax_ld=L * H,
+                                 kmax_plane0=l * H)
             w1, b1, e1 = lw["norms"][1]
             if fuse_ln:
                 native.gemm_ln(ob, lw["ca_ow"], M=rows, K=C, lda=C, ldw=C, bias=lw["ca_ob"], R=t1n, ldr=C, ln_w=w1,

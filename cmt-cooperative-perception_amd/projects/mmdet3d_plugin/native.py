@@ -25,7 +25,8 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
+PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -42,7 +43,8 @@ class GemmArgs(ctypes.Structure):
                 ("bias", _vp), ("bias_bstride", _i64),
                 ("R", _vp), ("ldr", _i64), ("r_bstride", _i64), ("r_dtype", _int),
                 ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int),
-                ("c_mode", _int), ("rows_per_batch", _int), ("relu", _int)]
+                ("c_mode", _int), ("rows_per_batch", _int), ("relu", _int),
+                ("plane_max2", _vp), ("plane_max_cols", _int)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -53,7 +55,8 @@ class AttnArgs(ctypes.Structure):
                 ("O", _vp), ("o_bstride", _i64), ("o_rstride", _i64), ("o_dtype", _int), ("scale", _flt),
                 ("kv_splits", _int),
                 ("flags", _int),
-                ("workspace", _vp), ("workspace_bytes", _i64)]
+                ("workspace", _vp), ("workspace_bytes", _i64),
+                ("kmax2", _vp), ("kmax_ld", _int), ("kmax_plane0", _int), ("kmax_rows", _int)]
 
 
 class LnArgs(ctypes.Structure):
@@ -159,16 +162,23 @@ def _farr(vals, n):
 # ---------------------------------------------------------------------------
 def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0, a2_cols=0,
          a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0, bias_bstride=0,
-         r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0):
+         r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0,
+         plane_max2=None, plane_max_cols=0):
     """C = act(A W^T + bias) + R with the fused prologue/epilogue of cmt_gemm.
     Offsets are in elements of the respective tensor.  A2 of A's dtype selects
     (replaces A for output columns < a2_cols); an fp32 A2 beside fp32 A is
-    added on load."""
+    added on load.  plane_max2 (fp32 [ceil(M/64), plane_max_cols/32], head-split
+    16-bit C only) receives the per-64-row max squared row norm of each head plane."""
     g = _gemm_args(A, W, C, M=M, N=N, K=K, lda=lda, ldw=ldw, ldc=ldc, bias=bias, relu=relu, R=R, ldr=ldr, A2=A2,
                    lda2=lda2, a2_cols=a2_cols, a_mode=a_mode, conv=conv, seg_len=seg_len, batch=batch,
                    a_bstride=a_bstride, w_bstride=w_bstride, bias_bstride=bias_bstride, r_bstride=r_bstride,
                    c_bstride=c_bstride, headsplit_rows=headsplit_rows, a_offset=a_offset, c_offset=c_offset,
                    r_offset=r_offset, a2_offset=a2_offset)
+    if plane_max2 is not None:
+        _dev(plane_max2)
+        if plane_max2.dtype != torch.float32 or plane_max2.numel() < -(-M // PLANE_MAX_ROWS) * (plane_max_cols // 32):
+            raise RuntimeError("plane_max2 must be fp32 with ceil(M/64) * plane_max_cols/32 entries")
+        g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
     _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
 
 
@@ -219,11 +229,13 @@ _WS_CACHE = {}
 
 def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, q_offset=0,
               k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False,
-              fold_scale=False, _diag_flags=0):
+              fold_scale=False, kmax2=None, kmax_ld=0, kmax_plane0=0, _diag_flags=0):
     """Strides are (batch, head, row) in elements; o_strides = (batch, row).
     fold_scale lets the kernel fold scale*log2(e) into Q on load (one extra
-    rounding of Q; the f16/bf16 policies only)."""
-    _dev(Q, K, V, O)
+    rounding of Q; the f16/bf16 policies only).  kmax2: the K projection's
+    plane_max2 partials (see gemm) -- lets the bf16 long-key kernel fix each
+    query's softmax offset at |q| max|k| instead of tracking a running max."""
+    _dev(Q, K, V, O, kmax2)
     a = AttnArgs()
     a.B, a.H, a.Nq, a.Nk, a.dtype = B, H, Nq, Nk, DT[Q.dtype]
     es = Q.element_size()
@@ -238,6 +250,8 @@ def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_st
     a.o_dtype = DT[O.dtype]
     a.scale, a.kv_splits = scale, kv_splits
     a.flags = (1 if round_output else 0) | (2 if fold_scale else 0) | _diag_flags
+    if kmax2 is not None:
+        a.kmax2, a.kmax_ld, a.kmax_plane0, a.kmax_rows = kmax2.data_ptr(), kmax_ld, kmax_plane0, PLANE_MAX_ROWS
     need = lib().cmt_attn_workspace_bytes(ctypes.byref(a))
     if need > 0:
         if workspace is None or workspace.numel() < need:

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--nk", type=int, default=32400)
+    ap.add_argument("--bound", action="store_true", help="pass max-|k| partials (bounded-max mode)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     B, H, Nq, Nk = 1, 8, 900, args.nk
@@ -30,11 +31,17 @@ def main():
     v = torch.randn(B * H * Nk * 32, generator=g).bfloat16().to(dev)
     O = torch.empty(B * Nq * H * 32, dtype=torch.bfloat16, device=dev)
     ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+    kmax2 = None
+    if args.bound:   # max |k|^2 partials per 64 key rows (what the K projection's epilogue writes)
+        nb = -(-Nk // 64)
+        ss = (k.float().view(H, Nk, 32) ** 2).sum(-1)
+        ss = torch.cat([ss, ss.new_zeros(H, nb * 64 - Nk)], 1).view(H, nb, 64).amax(-1)
+        kmax2 = ss.t().contiguous()
     for _ in range(args.iters):
         N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(H * Nq * 32, Nq * 32, 32),
                     k_strides=(H * Nk * 32, Nk * 32, 32), v_strides=(H * Nk * 32, Nk * 32, 32),
                     o_strides=(Nq * H * 32, H * 32), scale=32 ** -0.5, kv_splits=args.splits, workspace=ws,
-                    fold_scale=args.fold)
+                    fold_scale=args.fold, kmax2=kmax2, kmax_ld=H, kmax_plane0=0)
     torch.cuda.synchronize()
     print("ok")
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 2
+#define CMT_ABI_VERSION 3
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -87,6 +87,11 @@ typedef struct cmt_gemm_args {
     int c_mode;                /* cmt_gemm_cmode; HEADSPLIT: C[(b*(N/32)+n/32)*rows_per_batch + r][32] */
     int rows_per_batch;
     int relu;
+    /* optional (HEADSPLIT with a 16-bit C only): plane_max2[(m/64)*(plane_max_cols/32) + n/32]
+     * = max over the 64-row block's rows m of sum_{32 cols of head plane n/32} C[m,n]^2
+     * (of the stored, rounded values), for n < plane_max_cols; every entry is written
+     * (rows >= M count as 0).  Feeds cmt_attn_args.kmax2. */
+    float* plane_max2; int plane_max_cols;
 } cmt_gemm_args;
 
 int cmt_gemm(const cmt_gemm_args* args, void* stream);
@@ -127,6 +132,13 @@ typedef struct cmt_attn_args {
     int kv_splits;             /* 0 = choose automatically */
     int flags;                 /* CMT_ATTN_ROUND_OUTPUT | CMT_ATTN_FOLD_SCALE */
     void* workspace; int64_t workspace_bytes;
+    /* optional (NULL = off): max squared key-row norms written by the K
+     * projection GEMM (cmt_gemm_args.plane_max2): entry [e][kmax_ld] covers key
+     * rows e*kmax_rows .. +kmax_rows-1 of the batch-major K rows (b*Nk + row),
+     * head h reads column kmax_plane0 + h.  With bf16 the long-key kernel then
+     * fixes each query's softmax offset at the Cauchy-Schwarz bound |q|*max|k|
+     * (no running max) when that bound is <= 60 in exp2 units. */
+    const float* kmax2; int kmax_ld; int kmax_plane0; int kmax_rows;
 } cmt_attn_args;
 
 int64_t cmt_attn_workspace_bytes(const cmt_attn_args* args);

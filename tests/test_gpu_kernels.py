@@ -141,6 +141,64 @@ def test_gemm_dma_select_headsplit(N, dev, dt):
     assert rel < 1e-2, rel
 
 
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,S,big", [(2, 300, False), (1, 32400, True), (2, 4100, True)])
+def test_gemm_plane_max2(N, dev, dt, B, S, big):
+    """Head-split GEMM epilogue by-product: per 64-row block and head plane the
+    max squared row norm of the stored (rounded) values, planes < plane_max_cols
+    (the K half of a K|V projection); 64x64 and 128x128 tiles, ragged M,
+    blocks straddling the batch boundary."""
+    g = torch.Generator().manual_seed(S + B)
+    K, Nc = 256, (3072 if big else 512)
+    M = B * S
+    A = torch.randn(M, K, generator=g).to(dt)
+    W = (torch.randn(Nc, K, generator=g) / 16).to(dt)
+    Y = torch.empty(M * Nc, dtype=dt, device=dev)
+    cols = Nc // 2
+    nb = -(-M // 64)
+    pm = torch.full((nb, cols // 32), -1.0, device=dev)
+    N.gemm(A.to(dev), W.to(dev), Y, M=M, N=Nc, K=K, lda=K, ldw=K, ldc=0, headsplit_rows=S, plane_max2=pm,
+           plane_max_cols=cols)
+    y = Y.cpu().view(B, Nc // 32, S, 32).permute(0, 2, 1, 3).reshape(M, Nc // 32, 32).double()
+    ss = (y[:, :cols // 32] ** 2).sum(-1)                       # [M, planes]
+    pad = nb * 64 - M
+    ref = torch.cat([ss, torch.zeros(pad, cols // 32, dtype=ss.dtype)], 0).view(nb, 64, -1).amax(1)
+    assert torch.allclose(pm.cpu().double(), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("scale_q", [1.0, 40.0])
+@pytest.mark.parametrize("B,Nq,Nk,splits", [(1, 900, 32400, 0), (2, 300, 4097, 3), (1, 257, 8192, 1)])
+def test_attention_bounded_max(N, dev, B, Nq, Nk, splits, scale_q):
+    """bf16 long-key kernel with the K max-norm partials: every query's softmax
+    offset is the Cauchy-Schwarz bound (scale_q = 1); with large |q| (40) the
+    bound exceeds 60 exp2 units and the waves fall back to the running max
+    (there without the scale fold: rounding q*scale*log2e to bf16 moves scores
+    of ~100 exp2 units by ~0.2, beyond any tolerance of this check)."""
+    H = 8
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(Nk + B)
+    q = (torch.randn(B, H, Nq, 32, generator=g) * scale_q).to(dt)
+    k = torch.randn(B, H, Nk, 32, generator=g).to(dt)
+    k[:, :, Nk // 3] *= 3                                       # one long key per plane
+    v = torch.randn(B, H, Nk, 32, generator=g).to(dt)
+    kr = k.double().permute(0, 2, 1, 3).reshape(B * Nk, H, 32)
+    ss = (kr ** 2).sum(-1)
+    nb = -(-B * Nk // 64)
+    km = torch.cat([ss, torch.zeros(nb * 64 - B * Nk, H, dtype=ss.dtype)], 0).view(nb, 64, H).amax(1)
+    kmax2 = torch.cat([torch.zeros(nb, 3), km.float(), torch.zeros(nb, 5)], 1).contiguous()   # planes 3..10
+    for fold in ((False, True) if scale_q == 1.0 else (False,)):
+        O = torch.empty(B, Nq, H * 32, device=dev)
+        N.attention(q.to(dev), k.to(dev), v.to(dev), O, B=B, H=H, Nq=Nq, Nk=Nk,
+                    q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                    v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
+                    kv_splits=splits, fold_scale=fold, kmax2=kmax2.to(dev), kmax_ld=16, kmax_plane0=3)
+        ref = _attn_ref(q, k, v, 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
+        got = O.cpu().double()
+        assert torch.isfinite(got).all()
+        err = (got - ref).abs().max().item()
+        assert err < 2e-2, (fold, err)
+
+
 def test_gemm_dma_conv1d3_lowp(N, dev):
     g = torch.Generator().manual_seed(12)
     L, B, Nq, C, O = 3, 2, 37, 256, 128
