@@ -1,0 +1,442 @@
+// Row-block chains of the decoder layer's query side (gfx950).
+//
+// One workgroup owns 32 complete query rows (all C = 256 columns) and runs a
+// chain of 256 x 256 (K = 256) sub-GEMMs whose operands stay in LDS, with the
+// post-norm decoder layer's bias / residual / LayerNorm epilogues in between
+// (petr_transformer.py:374-487, operation_order self_attn, norm, cross_attn,
+// norm, ffn, norm; mmcv FFN add_identity; LN eps from the module):
+//
+//   chain A (after self-attention):  out_proj + bias + residual -> norms[0] -> Y
+//                                    -> lowp(Y + query_pos) -> cross-attn Q projection
+//   chain B (after cross-attention): out_proj + bias + residual -> norms[1]
+//                                    -> FFN fc1 + ReLU -> fc2 + bias + residual -> norms[2] -> Y
+//                                    (next query) and post_norm -> OUT (layer output)
+//                                    -> next layer's self-attn in_proj (Q|K read lowp(Y + pos),
+//                                       V reads lowp(Y))
+//
+// The FFN runs as four (fc1 column block, fc2 K block) pairs, so its hidden
+// activation never leaves LDS (16 KB at a time).  Every weight reaches LDS as
+// a stream of 16 KB stages (256 weight rows x 32 k) through a ring of NSTG
+// slots by LDS-DMA; the stream runs across sub-GEMM boundaries.  MFMA
+// 32x32x16 in the swapped form (lane = query row), so a row's LayerNorm
+// reduces over registers, the lane pair and the 4 waves.  All global stores
+// happen after the last stage and all ordinary global loads before the first,
+// so no counted LDS-DMA wait is ever drained early.
+#include "cmt_common.h"
+
+namespace {
+
+constexpr int RB = 32;                         // query rows per workgroup
+constexpr int CE = 256;                        // embed dims
+constexpr int NTC = 256;                       // threads (4 waves)
+constexpr int KSTG = 32;                       // k per weight stage
+constexpr int NSTG = 6;                        // weight ring depth
+constexpr int STG_BYTES = CE * KSTG * 2;       // 16 KB
+constexpr int SUB_STAGES = CE / KSTG;          // 8 stages per sub-GEMM
+constexpr int ACT_BYTES = RB * CE * 2;         // 16 KB operand image [32][256] 16-bit
+constexpr int OFF_ACT_A = NSTG * STG_BYTES;    // 96 KB
+constexpr int OFF_ACT_B = OFF_ACT_A + ACT_BYTES;
+constexpr int OFF_PRM = OFF_ACT_B + ACT_BYTES; // fp32 parameter block
+constexpr int PRM_A = 1024, PRM_B = 3840;      // floats (cmt_hip.h cmt_chain_args.prm)
+constexpr int OFF_RED = OFF_PRM + PRM_B * 4;
+constexpr int LDS_TOTAL = OFF_RED + 2 * 4 * RB * 4;
+
+typedef const __attribute__((address_space(1))) void* rc_gaddr_t;
+typedef __attribute__((address_space(3))) void* rc_laddr_t;
+
+// counted LDS-DMA wait + every outstanding LDS access of this wave (the
+// barrier that follows hands LDS writes to the other waves)
+template <int N>
+__device__ __forceinline__ void rc_wait() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+template <typename T>
+struct Eng {
+    typedef typename mfma_traits<T>::frag frag;
+    char* lds;
+    int tid, lane, wave, lr, lh;
+    int issued, consumed, nstages, kind;
+    const T *Wo, *W1, *W2, *Wn;
+
+    // weight base / leading dim of sub-GEMM `sub` (wave-uniform arithmetic, no tables):
+    // A: out_proj, Q proj.  B: out_proj, (fc1 block j, fc2 K block j) x 4, in_proj Q, K, V.
+    __device__ __forceinline__ const T* sub_base(int sub, int& ld) const {
+        ld = CE;
+        if (kind == 0) return sub == 0 ? Wo : W1;
+        if (sub == 0) return Wo;
+        if (sub <= 8) {
+            const int j = (sub - 1) >> 1;
+            if (sub & 1) return W1 + (int64_t)j * CE * CE;
+            ld = 4 * CE;
+            return W2 + j * CE;
+        }
+        return Wn + (int64_t)(sub - 9) * CE * CE;
+    }
+
+    __device__ __forceinline__ void issue() {
+        if (issued >= nstages) return;
+        const int sub = issued / SUB_STAGES, kc = issued % SUB_STAGES;
+        int ld;
+        const T* W = sub_base(sub, ld);
+        char* dst = lds + (issued % NSTG) * STG_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = tid + NTC * i;
+            const int n = piece >> 2;
+            const int lc = (piece & 3) ^ ((n >> 2) & 3);
+            __builtin_amdgcn_global_load_lds((rc_gaddr_t)(W + (int64_t)n * ld + kc * KSTG + 8 * lc),
+                                             (rc_laddr_t)(dst + piece * 16), 16, 0, 0);
+        }
+        ++issued;
+    }
+
+    // stage `consumed` landed for every wave; then refill the slot of stage consumed-1
+    __device__ __forceinline__ void acquire() {
+        const int ahead = issued - consumed - 1;   // stages issued after the one needed now
+        static_assert(NSTG - 2 == 4, "wait ladder covers 0..4 stages");
+        if (ahead >= 4) rc_wait<16>();
+        else if (ahead == 3) rc_wait<12>();
+        else if (ahead == 2) rc_wait<8>();
+        else if (ahead == 1) rc_wait<4>();
+        else rc_wait<0>();
+        barrier_mem();
+        issue();
+    }
+
+    // one stage: acc[nt] += W[wave*64 + nt*32 + i][k] * A[row][k] (swapped: lane = row)
+    __device__ __forceinline__ void mma_stage(const char* A, f32x16 (&acc)[2]) {
+        const char* Wt = lds + (consumed % NSTG) * STG_BYTES;
+        const int kc = consumed % SUB_STAGES;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const frag af = *(const frag*)(A + lr * (CE * 2) + (((kc * 4 + 2 * ks + lh) ^ (lr & 15)) << 4));
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int n = wave * 64 + nt * 32 + lr;
+                const frag wf = *(const frag*)(Wt + n * (KSTG * 2) + (((2 * ks + lh) ^ ((n >> 2) & 3)) << 4));
+                acc[nt] = mfma_traits<T>::mma(wf, af, acc[nt]);
+            }
+        }
+        ++consumed;
+    }
+
+    __device__ __forceinline__ void sub_gemm(const char* A, f32x16 (&acc)[2], bool zero) {
+        if (zero) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
+        }
+        for (int kc = 0; kc < SUB_STAGES; ++kc) {
+            acquire();
+            mma_stage(A, acc);
+        }
+    }
+
+    // column of value r of n-tile nt for this lane (4 consecutive per group r >> 2)
+    __device__ __forceinline__ int col(int nt, int r) const {
+        return wave * 64 + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    }
+
+    __device__ __forceinline__ const float* prm() const { return (const float*)(lds + OFF_PRM); }
+
+    // sum over the row's 256 columns (this lane's 32, the lane pair, the 4 waves); slots alternate
+    __device__ __forceinline__ float row_sum(float x, int slot) {
+        x = pair_sum(x);
+        float* red = (float*)(lds + OFF_RED);
+        if (lh == 0) red[(slot * 4 + wave) * RB + lr] = x;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_mem();
+        return red[(slot * 4 + 0) * RB + lr] + red[(slot * 4 + 1) * RB + lr] + red[(slot * 4 + 2) * RB + lr] +
+               red[(slot * 4 + 3) * RB + lr];
+    }
+
+    // in-place LayerNorm (nn.LayerNorm: biased variance) with weight / bias at parameter offsets
+    __device__ __forceinline__ void layernorm(float (&v)[32], int w_off, int b_off, float eps) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) s += v[i];
+        const float mean = row_sum(s, 0) * (1.f / CE);
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const float d = v[i] - mean;
+            q += d * d;
+        }
+        const float rstd = rsqrtf(row_sum(q, 1) * (1.f / CE) + eps);
+        const float* pw = prm() + w_off;
+        const float* pb = prm() + b_off;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int c = col(nt, r);
+                v[nt * 16 + r] = (v[nt * 16 + r] - mean) * rstd * pw[c] + pb[c];
+            }
+    }
+
+    // this lane's 32 values of its row into an operand image [32][256] (16-B chunks XOR row & 15)
+    __device__ __forceinline__ void put_act(char* act, const float (&v)[32]) {
+        typedef T t4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c0 = col(nt, 4 * g);
+                const t4 x = {(T)v[nt * 16 + 4 * g], (T)v[nt * 16 + 4 * g + 1], (T)v[nt * 16 + 4 * g + 2],
+                              (T)v[nt * 16 + 4 * g + 3]};
+                *(t4*)(act + lr * (CE * 2) + (((c0 >> 3) ^ (lr & 15)) << 4) + (c0 & 7) * 2) = x;
+            }
+    }
+};
+
+// this lane's 32 fp32 values of `row` (columns of Eng::col) from a [rows][256] fp32 matrix
+__device__ __forceinline__ void load_row32(const float* M, int row, int wave, int lh, float (&v)[32]) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 x = *(const f32x4*)(M + (int64_t)row * CE + wave * 64 + nt * 32 + 8 * g + 4 * lh);
+            v[nt * 16 + 4 * g] = x[0];
+            v[nt * 16 + 4 * g + 1] = x[1];
+            v[nt * 16 + 4 * g + 2] = x[2];
+            v[nt * 16 + 4 * g + 3] = x[3];
+        }
+}
+
+__device__ __forceinline__ void store_row32(float* M, int row, int wave, int lh, const float (&v)[32]) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *(f32x4*)(M + (int64_t)row * CE + wave * 64 + nt * 32 + 8 * g + 4 * lh) =
+                f32x4{v[nt * 16 + 4 * g], v[nt * 16 + 4 * g + 1], v[nt * 16 + 4 * g + 2], v[nt * 16 + 4 * g + 3]};
+}
+
+template <typename T>
+__global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) char lds[LDS_TOTAL];
+    Eng<T> e;
+    e.lds = lds;
+    e.tid = threadIdx.x;
+    e.lane = threadIdx.x & 63;
+    e.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    e.lr = e.lane & 31;
+    e.lh = e.lane >> 5;
+    e.kind = a.kind;
+    e.Wo = (const T*)a.Wo;
+    e.W1 = (const T*)a.W1;
+    e.W2 = (const T*)a.W2;
+    e.Wn = (const T*)a.Wn;
+    e.issued = e.consumed = 0;
+    const bool chainB = a.kind == 1;
+    const bool has_next = chainB && a.Wn != nullptr;
+    e.nstages = (chainB ? (has_next ? 12 : 9) : 2) * SUB_STAGES;
+    const int nheads = chainB ? 24 : 8;
+    const int nprm = chainB ? PRM_B : PRM_A;
+    const int m0 = blockIdx.x * RB;
+    const int row = min(m0 + e.lr, a.rows - 1);
+    const bool row_ok = m0 + e.lr < a.rows;
+    char* actA = lds + OFF_ACT_A;
+    char* actB = lds + OFF_ACT_B;
+
+    // ---- prologue: every ordinary load and the first LDS-DMAs, then one full wait
+    float res[32], qp[32], oold[32];
+    if (a.R) {
+        load_row32(a.R, row, e.wave, e.lh, res);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) res[i] = 0.f;
+    }
+    const bool need_p = chainB ? has_next : true;
+    if (need_p) {
+        load_row32(a.P, row, e.wave, e.lh, qp);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) qp[i] = 0.f;
+    }
+    const bool max_into = chainB && (a.out_flags & CMT_LN_MAX_INTO);
+    if (max_into) {
+        load_row32(a.OUT, row, e.wave, e.lh, oold);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) oold[i] = 0.f;
+    }
+    // attention output rows -> actA (32 rows x 32 chunks, swizzled), parameter block -> LDS
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int piece = e.tid + NTC * i;
+        const int r = piece >> 5;
+        const int lc = (piece & 31) ^ (r & 15);
+        const int src_row = min(m0 + r, a.rows - 1);
+        __builtin_amdgcn_global_load_lds((rc_gaddr_t)((const T*)a.X + (int64_t)src_row * CE + 8 * lc),
+                                         (rc_laddr_t)(actA + piece * 16), 16, 0, 0);
+    }
+    for (int piece = e.tid; piece < (nprm >> 2); piece += NTC)
+        __builtin_amdgcn_global_load_lds((rc_gaddr_t)(a.prm + 4 * piece), (rc_laddr_t)(lds + OFF_PRM + piece * 16),
+                                         16, 0, 0);
+#pragma unroll
+    for (int s = 0; s < NSTG - 1; ++s) e.issue();
+    // first use of the ordinary loads: everything issued so far has landed after this
+    asm volatile("" ::"v"(res[0]), "v"(res[31]), "v"(qp[0]), "v"(qp[31]), "v"(oold[0]), "v"(oold[31]));
+    rc_wait<0>();
+    barrier_mem();
+
+    f32x16 acc[2];
+    float v[32];
+    const float eps = a.eps;
+    if (!chainB) {
+        // ---------------- chain A
+        e.sub_gemm(actA, acc, true);                                   // out_proj
+        {
+            const float* bo = e.prm();
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
+        }
+        e.layernorm(v, 256, 512, eps);                                 // norms[0]
+        float y[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            y[i] = v[i];
+            v[i] += qp[i];
+        }
+        e.put_act(actB, v);                                            // lowp(y + query_pos)
+        e.sub_gemm(actB, acc, true);                                   // cross-attn Q projection
+        const float* bq = e.prm() + 768;
+        t4 qo[8];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c0 = e.col(nt, 4 * g);
+                qo[nt * 4 + g] = t4{(T)(acc[nt][4 * g] + bq[c0]), (T)(acc[nt][4 * g + 1] + bq[c0 + 1]),
+                                    (T)(acc[nt][4 * g + 2] + bq[c0 + 2]), (T)(acc[nt][4 * g + 3] + bq[c0 + 3])};
+            }
+        if (row_ok) {
+            store_row32(a.Y, row, e.wave, e.lh, y);
+            const int b = row / a.Nq, rr = row - b * a.Nq;
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c0 = e.col(nt, 4 * g);
+                    *(t4*)((T*)a.Q + (((int64_t)b * nheads + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
+                        qo[nt * 4 + g];
+                }
+        }
+        return;
+    }
+
+    // ---------------- chain B
+    e.sub_gemm(actA, acc, true);                                       // out_proj
+    {
+        const float* bo = e.prm();
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
+    }
+    e.layernorm(v, 256, 512, eps);                                     // norms[1] -> o (FFN residual)
+    float o[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) o[i] = v[i];
+    e.put_act(actB, o);                                                // lowp(o): fc1 operand
+    f32x16 acc2[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[nt][r] = 0.f;
+    for (int j = 0; j < 4; ++j) {
+        e.sub_gemm(actB, acc, true);                                   // fc1 column block j
+        const float* b1 = e.prm() + 768 + 256 * j;
+        float h[32];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h[nt * 16 + r] = fmaxf(acc[nt][r] + b1[e.col(nt, r)], 0.f);
+        e.put_act(actA, h);                                            // hidden block j = fc2 K block j
+        e.sub_gemm(actA, acc2, false);                                 // fc2 partial sum over K block j
+    }
+    {
+        const float* b2 = e.prm() + 1792;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc2[nt][r] + b2[e.col(nt, r)] + o[nt * 16 + r];
+    }
+    e.layernorm(v, 2048, 2304, eps);                                   // norms[2] -> next query
+    float y[32], out[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) y[i] = out[i] = v[i];
+    e.layernorm(out, 2560, 2816, eps);                                 // post_norm -> layer output
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        float x = out[i];
+        if (a.out_flags & CMT_LN_NAN_TO_NUM) x = nan_to_num(x);
+        if (max_into) x = fmaxf(x, oold[i]);
+        out[i] = x;
+    }
+    t4 qo[24];
+    if (has_next) {
+        e.put_act(actA, y);                                            // lowp(y): V columns
+#pragma unroll
+        for (int i = 0; i < 32; ++i) v[i] = y[i] + qp[i];
+        e.put_act(actB, v);                                            // lowp(y + pos): Q|K columns
+        const float* bqkv = e.prm() + 3072;
+#pragma unroll
+        for (int blk = 0; blk < 3; ++blk) {
+            e.sub_gemm(blk < 2 ? actB : actA, acc, true);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c0 = blk * CE + e.col(nt, 4 * g);
+                    qo[blk * 8 + nt * 4 + g] =
+                        t4{(T)(acc[nt][4 * g] + bqkv[c0]), (T)(acc[nt][4 * g + 1] + bqkv[c0 + 1]),
+                           (T)(acc[nt][4 * g + 2] + bqkv[c0 + 2]), (T)(acc[nt][4 * g + 3] + bqkv[c0 + 3])};
+                }
+        }
+    }
+    if (row_ok) {
+        store_row32(a.Y, row, e.wave, e.lh, y);
+        store_row32(a.OUT, row, e.wave, e.lh, out);
+        if (has_next) {
+            const int b = row / a.Nq, rr = row - b * a.Nq;
+#pragma unroll
+            for (int blk = 0; blk < 3; ++blk)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int c0 = blk * CE + e.col(nt, 4 * g);
+                        *(t4*)((T*)a.Q + (((int64_t)b * nheads + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
+                            qo[blk * 8 + nt * 4 + g];
+                    }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_chain: null args");
+    const cmt_chain_args& a = *ap;
+    CMT_REQUIRE(a.kind == 0 || a.kind == 1, "cmt_chain: kind must be 0 (A) or 1 (B)");
+    CMT_REQUIRE(a.rows > 0 && a.Nq > 0 && a.rows % a.Nq == 0, "cmt_chain: rows must be B * Nq");
+    CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16, "cmt_chain: dtype must be f16 or bf16");
+    CMT_REQUIRE(a.X && a.P && a.prm && a.Wo && a.W1 && a.Y, "cmt_chain: null pointer");
+    CMT_REQUIRE(a.kind == 0 || (a.W2 && a.OUT), "cmt_chain: chain B needs W2 and OUT");
+    CMT_REQUIRE(a.Q != nullptr || (a.kind == 1 && a.Wn == nullptr), "cmt_chain: null Q output");
+    CMT_REQUIRE(((uintptr_t)a.X | (uintptr_t)a.prm | (uintptr_t)a.Wo | (uintptr_t)a.W1 | (uintptr_t)a.W2 |
+                 (uintptr_t)a.Wn | (uintptr_t)a.P | (uintptr_t)a.Y | (uintptr_t)a.R | (uintptr_t)a.OUT) % 16 == 0,
+                "cmt_chain: buffers must be 16-byte aligned");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned grid = (unsigned)cdiv(a.rows, RB);
+    if (a.dtype == CMT_BF16) chain_kernel<bf16_t><<<grid, NTC, 0, s>>>(a);
+    else chain_kernel<f16_t><<<grid, NTC, 0, s>>>(a);
+    return cmt_check_launch("cmt_chain");
+}

@@ -338,6 +338,38 @@ class PETRTransformerDecoder(nn.Module):
                 and all(a.num_heads * 32 == self.embed_dims for l in self.layers for a in l.attentions))
 
     # ------------------------------------------------------------------
+    def _chain_ok(self):
+        """Row-block chains (cmt_chain) need C = 256, FFN 1024 and one LN eps."""
+        if self.embed_dims != 256 or self.post_norm is None:
+            return False
+        eps = {n.eps for l in self.layers for n in l.norms} | {self.post_norm.eps}
+        return len(eps) == 1 and all(l.ffns[0].feedforward_channels == 1024 for l in self.layers)
+
+    def _chain_pack(self, prec):
+        """Per layer the fp32 parameter blocks of chains A and B (cmt_hip.h cmt_chain_args.prm)."""
+        params = [p for p in self.parameters()]
+
+        def build():
+            C, L = self.embed_dims, self.num_layers
+            dev = self.post_norm.weight.device
+
+            def vec(t, n):
+                return t.detach().float().reshape(-1) if t is not None else torch.zeros(n, device=dev)
+
+            A, Bk = [], []
+            for l, lay in enumerate(self.layers):
+                sa, ca, ffn, nm = lay.attentions[0].attn, lay.attentions[1].attn, lay.ffns[0], lay.norms
+                cbq = ca.in_proj_bias[:C] if ca.in_proj_bias is not None else None
+                A.append(torch.cat([vec(sa.out_proj.bias, C), vec(nm[0].weight, C), vec(nm[0].bias, C),
+                                    vec(cbq, C)]).contiguous())
+                nxt = self.layers[l + 1].attentions[0].attn.in_proj_bias if l + 1 < L else None
+                Bk.append(torch.cat([vec(ca.out_proj.bias, C), vec(nm[1].weight, C), vec(nm[1].bias, C),
+                                     vec(ffn.layers[0][0].bias, 4 * C), vec(ffn.layers[1].bias, C),
+                                     vec(nm[2].weight, C), vec(nm[2].bias, C), vec(self.post_norm.weight, C),
+                                     vec(self.post_norm.bias, C), vec(nxt, 3 * C)]).contiguous())
+            return dict(A=A, B=Bk)
+        return self._pack.get("chain", params, prec.name, build)
+
     def packed(self, prec):
         params = [p for p in self.parameters()]
 
@@ -493,6 +525,34 @@ class PETRTransformerDecoder(nn.Module):
                        native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
         ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
         pw, pb, _pe = pk["post"]
+        if self._chain_ok() and os.environ.get("CMT_CHAIN", "1") != "0":
+            # per layer: self-attn core, chain A (out_proj + norms[0] + cross Q proj),
+            # cross-attn core, chain B (out_proj + norms[1] + FFN + norms[2] + post_norm
+            # + next layer's in_proj) -- see rowchain.hip
+            ch = self._chain_pack(prec)
+            eps = self.post_norm.eps
+            l0 = pk["layers"][0]
+            native.gemm(tl, l0["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
+                        A2=tp, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
+            for l, lw in enumerate(pk["layers"]):
+                native.attention(qkv, qkv, qkv, ob, B=B, H=H, Nq=Nq, Nk=Nq,
+                                 q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
+                                 v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
+                                 o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
+                native.chain(0, ob, qpos, ch["A"][l], lw["sa_ow"], lw["ca_wq"], t1n, rows=rows, Nq=Nq, eps=eps,
+                             R=tgt if (l > 0 or tgt0 is not None) else None, Q=qc)
+                with timed("cross_attn"):
+                    native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
+                                     q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
+                                     v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
+                                     v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
+                                     round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2,
+                                     kmax_ld=L * H, kmax_plane0=l * H)
+                nxt = pk["layers"][l + 1]["sa_w"] if l + 1 < L else None
+                native.chain(1, ob, qpos, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
+                             R=t1n, W2=lw["f2_w"], Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
+                             Q=qkv if nxt is not None else None)
+            return out
         # out-projection / fc2 GEMMs fused with their residual + LayerNorm (cmt_gemm_ln)
         fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "0") == "1"
         for l, lw in enumerate(pk["layers"]):

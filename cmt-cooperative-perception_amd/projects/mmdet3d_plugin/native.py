@@ -11,7 +11,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "available", "gemm", "gemm_ln", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
+__all__ = ["lib", "available", "gemm", "gemm_ln", "chain", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
            "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
            "voxelize", "box_decode", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
@@ -59,6 +59,13 @@ class AttnArgs(ctypes.Structure):
                 ("kmax2", _vp), ("kmax_ld", _int), ("kmax_plane0", _int), ("kmax_rows", _int)]
 
 
+class ChainArgs(ctypes.Structure):
+    _fields_ = [("kind", _int), ("rows", _int), ("Nq", _int), ("dtype", _int), ("eps", _flt),
+                ("X", _vp), ("R", _vp), ("P", _vp), ("prm", _vp),
+                ("Wo", _vp), ("W1", _vp), ("W2", _vp), ("Wn", _vp),
+                ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp)]
+
+
 class LnArgs(ctypes.Structure):
     _fields_ = [("X", _vp), ("ldx", _i64), ("rows", _int), ("C", _int),
                 ("W", _vp), ("B", _vp), ("eps", _flt),
@@ -91,6 +98,7 @@ def _load():
                           _int),
         "cmt_layernorm_ex": ([P(LnArgs), _vp], _int),
         "cmt_gemm_ln": ([P(GemmArgs), P(LnArgs), _vp], _int),
+        "cmt_chain": ([P(ChainArgs), _vp], _int),
         "cmt_add_cast": ([_vp, _vp, _int, _int, _int, _vp, _vp, _vp], _int),
         "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _int, _i64, _vp], _int),
         "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _int, _vp], _int),
@@ -310,6 +318,30 @@ def gemm_ln(A, W, *, M, K, lda, ldw, bias=None, R=None, ldr=0, ln_w, ln_b, eps=1
     a = _ln_args(None, ln_w, ln_b, rows=M, C=N, ldx=0, eps=eps, Y=Y, ldy=N, flags=flags, W2=W2, B2=B2, Y2=Y2,
                  ldy2=N, flags2=flags2, Yl=Yl, Yp=Yp, P=P, y2_offset=y2_offset)
     _check(lib().cmt_gemm_ln(ctypes.byref(g), ctypes.byref(a), _stream()), "cmt_gemm_ln")
+
+
+CHAIN_PRM = {0: 1024, 1: 3840}
+
+
+def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
+          out_flags=0, Q=None):
+    """One row-block chain of a decoder layer's query side (cmt_chain):
+    kind 0 after self-attention, kind 1 after cross-attention (cmt_hip.h)."""
+    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q)
+    if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:
+        raise RuntimeError(f"cmt_chain: parameter block must be {CHAIN_PRM[kind]} fp32 values")
+    a = ChainArgs()
+    a.kind, a.rows, a.Nq, a.dtype, a.eps = kind, rows, Nq, DT[X.dtype], eps
+
+    def ptr(t):
+        return None if t is None else t.data_ptr()
+    a.X, a.R, a.P, a.prm = ptr(X), ptr(R), ptr(P), ptr(prm)
+    a.Wo, a.W1, a.W2, a.Wn = ptr(Wo), ptr(W1), ptr(W2), ptr(Wn)
+    a.Y = ptr(Y)
+    a.OUT = None if OUT is None else OUT.data_ptr() + 4 * out_offset
+    a.out_flags = out_flags
+    a.Q = ptr(Q)
+    _check(lib().cmt_chain(ctypes.byref(a), _stream()), "cmt_chain")
 
 
 def add_cast(X, *, rows, C, Yl=None, Yp=None, P=None):

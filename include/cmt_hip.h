@@ -185,6 +185,47 @@ int cmt_layernorm_ex(const cmt_ln_args* args, void* stream);
  * A/W, row mode, batch 1. */
 int cmt_gemm_ln(const cmt_gemm_args* gemm, const cmt_ln_args* ln, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Row-block chains of the decoder layer's query side (rowchain.hip): one
+ * workgroup owns 32 complete query rows (C = 256) and runs the layer's GEMMs
+ * back to back with their operands in LDS and the post-norm epilogues fused
+ * (petr_transformer.py:374-487; mmcv FFN / LN).  Replaces, per layer, the
+ * cuBLAS out_proj / in_proj / FFN GEMMs and the three LayerNorms around the
+ * two attention cores (attention.py:117, mmcv MultiheadAttention, mmcv FFN).
+ *   kind 0 (chain A, after self-attention):
+ *     Y = norms[0](X Wo^T + bo + R);  Q = lowp(Y + P) Wq^T + bq  (head split [B][8][Nq][32])
+ *   kind 1 (chain B, after cross-attention):
+ *     o = norms[1](X Wo^T + bo + R);  f = relu(lowp(o) W1^T + b1);
+ *     Y = norms[2](lowp(f) W2^T + b2 + o)   (the next layer's query)
+ *     OUT = post_norm(Y) (+ CMT_LN_NAN_TO_NUM / CMT_LN_MAX_INTO per out_flags)
+ *     if Wn: Q = [lowp(Y + P) | lowp(Y + P) | lowp(Y)] Wn^T + bn  (next layer's
+ *            self-attn in_proj, head split [B][24][Nq][32])
+ * prm: packed fp32 parameter block, layout (floats)
+ *   A (1024): bo | norms[0].weight | norms[0].bias | bq
+ *   B (3840): bo | norms[1].w | norms[1].b | b1 (1024) | b2 | norms[2].w | norms[2].b |
+ *             post_norm.w | post_norm.b | bn (768, zeros without Wn)
+ * One eps for every LayerNorm of the layer.  Weights / X / Q in the compute
+ * dtype (f16 / bf16), residuals and outputs fp32; every buffer 16-byte aligned.
+ * ------------------------------------------------------------------------ */
+typedef struct cmt_chain_args {
+    int kind;                  /* 0 = chain A, 1 = chain B */
+    int rows, Nq;              /* rows = B * Nq */
+    int dtype;                 /* CMT_F16 / CMT_BF16 */
+    float eps;
+    const void* X;             /* attention output [rows][256] */
+    const float* R;            /* residual [rows][256] fp32 (NULL = zeros) */
+    const float* P;            /* query_pos [rows][256] fp32 */
+    const float* prm;          /* packed parameter block */
+    const void* Wo;            /* out_proj.weight [256][256] */
+    const void* W1;            /* A: cross-attn in_proj_weight[:256]; B: fc1.weight [1024][256] */
+    const void* W2;            /* B: fc2.weight [256][1024] */
+    const void* Wn;            /* B: next layer's self-attn in_proj_weight [768][256] (NULL: last layer) */
+    float* Y;                  /* [rows][256] fp32 */
+    float* OUT; int out_flags; /* B: layer output [rows][256] fp32 */
+    void* Q;                   /* head-split projection output */
+} cmt_chain_args;
+int cmt_chain(const cmt_chain_args* args, void* stream);
+
 /* cmt_add_cast: Yl = lowp(X), Yp = lowp(X + P) over rows x C (either output
  * may be NULL) -- the decoder's first-layer operands from the initial target. */
 int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,

@@ -192,3 +192,6 @@ def test_full_size_lidar_one_layer(dev):
     refs = _refs(O, lambda c: O.head_forward(oc, sd, x, None, [dict()], "lidar", cross_core=c, self_core="fp32"))
     got = _run(head, dev, "ref", lambda: head([x.to(dev)], None, [dict()]))
     _check([g[0] for g in got], refs, oc["pc_range"])
+    # the bench policy on the same full-size frame: ping-pong bounded-max cross-attention,
+    # row-block chains, K/V max-norm partials
+    _check_bf16(_run(head, dev, "bf16", lambda: head([x.to(dev)], None, [dict()])), refs["fp32"], oc["pc_range"])

@@ -474,3 +474,83 @@ def test_voxelize_bitexact(N, dev):
         assert np.array_equal(num[:M].cpu().numpy(), rn[:M])
         assert np.array_equal(vox[:M].cpu().numpy(), rv[:M])
         assert np.array_equal(means[:M].cpu().numpy(), rm[:M])
+
+
+def _ln64(x, w, b, eps=1e-5):
+    m = x.mean(-1, keepdim=True)
+    v = ((x - m) ** 2).mean(-1, keepdim=True)
+    return (x - m) / torch.sqrt(v + eps) * w + b
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,Nq,with_r", [(1, 900, True), (2, 37, False)])
+def test_chain_a(N, dev, dt, B, Nq, with_r):
+    """Row-block chain A (out_proj + bias + residual -> norms[0] -> lowp(y + pos)
+    -> cross-attn Q projection, head split) vs fp64 math on the same rounded
+    operands; ragged last row block, no-residual (layer 0) form."""
+    g = torch.Generator().manual_seed(B * 100 + Nq)
+    C, rows = 256, B * Nq
+    X = torch.randn(rows, C, generator=g).to(dt)
+    R = torch.randn(rows, C, generator=g) if with_r else None
+    P = torch.randn(rows, C, generator=g)
+    Wo = (torch.randn(C, C, generator=g) / 16).to(dt)
+    Wq = (torch.randn(C, C, generator=g) / 16).to(dt)
+    bo, lb, bq = (torch.randn(C, generator=g) * 0.1 for _ in range(3))
+    lw = 1 + 0.1 * torch.randn(C, generator=g)
+    prm = torch.cat([bo, lw, lb, bq])
+    Y = torch.empty(rows, C, device=dev)
+    Q = torch.empty(B * 8 * Nq * 32, dtype=dt, device=dev)
+    N.chain(0, X.to(dev), P.to(dev), prm.to(dev), Wo.to(dev), Wq.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
+            R=R.to(dev) if R is not None else None, Q=Q)
+    d = lambda t: t.double()
+    t = d(X) @ d(Wo).T + d(bo) + (d(R) if R is not None else 0)
+    y = _ln64(t, d(lw), d(lb))
+    q = d((y + d(P)).to(dt)) @ d(Wq).T + d(bq)
+    qref = q.view(B, Nq, 8, 32).permute(0, 2, 1, 3).reshape(-1)
+    assert (Y.cpu().double() - y).abs().max().item() < 2e-3
+    rel = (Q.cpu().double() - qref).abs().max().item() / qref.abs().max().item()
+    assert rel < 1.5e-2, rel
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,Nq,last,flags", [(1, 900, False, 1), (2, 37, True, 3)])
+def test_chain_b(N, dev, dt, B, Nq, last, flags):
+    """Row-block chain B (out_proj + residual -> norms[1] -> FFN in four fc1/fc2
+    block pairs -> norms[2] and post_norm (nan_to_num / coop max-into) -> next
+    in_proj, head split) vs fp64 math on the same rounded operands."""
+    g = torch.Generator().manual_seed(B * 1000 + Nq)
+    C, F, rows = 256, 1024, B * Nq
+    X = torch.randn(rows, C, generator=g).to(dt)
+    R = torch.randn(rows, C, generator=g)
+    P = torch.randn(rows, C, generator=g)
+    Wo = (torch.randn(C, C, generator=g) / 16).to(dt)
+    W1 = (torch.randn(F, C, generator=g) / 16).to(dt)
+    W2 = (torch.randn(C, F, generator=g) / 32).to(dt)
+    Wn = (torch.randn(3 * C, C, generator=g) / 16).to(dt)
+    v = lambda n, s=0.1: torch.randn(n, generator=g) * s
+    bo, b1, b2, bn = v(C), v(F), v(C), v(3 * C)
+    l1w, l2w, pw = (1 + v(C) for _ in range(3))
+    l1b, l2b, pb = v(C), v(C), v(C)
+    prm = torch.cat([bo, l1w, l1b, b1, b2, l2w, l2b, pw, pb, torch.zeros(3 * C) if last else bn])
+    Y = torch.empty(rows, C, device=dev)
+    old = torch.randn(rows, C, generator=g)
+    OUT = old.clone().to(dev)
+    QKV = torch.empty(B * 24 * Nq * 32, dtype=dt, device=dev)
+    N.chain(1, X.to(dev), P.to(dev), prm.to(dev), Wo.to(dev), W1.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
+            R=R.to(dev), W2=W2.to(dev), Wn=None if last else Wn.to(dev), OUT=OUT, out_flags=flags,
+            Q=None if last else QKV)
+    d = lambda t: t.double()
+    o = _ln64(d(X) @ d(Wo).T + d(bo) + d(R), d(l1w), d(l1b))
+    h = torch.relu(d(o.to(dt)) @ d(W1).T + d(b1)).to(dt)
+    y = _ln64(d(h) @ d(W2).T + d(b2) + o, d(l2w), d(l2b))
+    out = _ln64(y, d(pw), d(pb))
+    if flags & 2:
+        out = torch.maximum(out, d(old))
+    assert (Y.cpu().double() - y).abs().max().item() < 2e-2
+    assert (OUT.cpu().double() - out).abs().max().item() < 2e-2
+    if not last:
+        qk = d((y + d(P)).to(dt)) @ d(Wn[:2 * C]).T + d(bn[:2 * C])
+        vv = d(y.to(dt)) @ d(Wn[2 * C:]).T + d(bn[2 * C:])
+        ref = torch.cat([qk, vv], 1).view(B, Nq, 24, 32).permute(0, 2, 1, 3).reshape(-1)
+        rel = (QKV.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+        assert rel < 2e-2, rel
