@@ -89,10 +89,11 @@ def load_traffic():
     """HBM bytes per cross-attention launch from the committed rocprofv3 PMC
     summary (profiles/*pmc*.json), corrected as MI355X_MICROARCH.md prescribes
     (FETCH_SIZE x2 for wide streaming reads).  None when absent."""
-    p = os.path.join(ROOT, "profiles", "attn_pmc_summary.json")
-    if not os.path.exists(p):
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*attn_pmc_summary.json")))
+    if not cands:
         return None
-    with open(p) as f:
+    with open(cands[-1]) as f:
         return json.load(f).get("hbm_bytes_per_launch")
 
 

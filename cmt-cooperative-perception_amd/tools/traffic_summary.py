@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--out", default="profiles/attn_pmc_summary.json")
-    ap.add_argument("--match", default="attn_fwd_kernel")
+    ap.add_argument("--match", default="attn_pp_kernel")
     a = ap.parse_args()
     fdb = glob.glob(os.path.join(a.dir, "fetch", "**", "*.db"), recursive=True)[0]
     wdb = glob.glob(os.path.join(a.dir, "write", "**", "*.db"), recursive=True)[0]
