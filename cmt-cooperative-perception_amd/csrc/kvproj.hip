@@ -1,0 +1,254 @@
+// Cross-attention K/V projection of ALL decoder layers in one launch (gfx950).
+//
+// Replaces, per layer, FlashMHA's packed in_proj on the memory side
+// (attention.py:21-27 _in_projection_packed, petr_transformer.py:296-299
+// key = key + key_pos): K_l = lowp(mem + pos) Wk_l^T + bk_l, V_l = lowp(mem) Wv_l^T + bv_l,
+// written head-split [B][2L*8][Nk][32] for the attention kernel, plus the
+// per-(64 keys, head) max squared key norm that bounds its softmax offset
+// (cmt_gemm_args.plane_max2).
+//
+// Shape: M = B*Nk ~ 32k token rows, N = 2*L*256 = 3072, K = 256.  A general
+// 128x128-tile GEMM re-reads both operands per tile: ~780 MB of L2->LDS
+// traffic for 51 GFLOP, and one CU's load path moves only ~30-60 GB/s
+// (MI355X_MICROARCH.md ldsdma-fill), so it ran at ~1/5 of MFMA peak.  Here a
+// workgroup keeps ONE 128-row A tile resident (LDS -> VGPRs, read once) and
+// sweeps half of the N columns (the K half with A2 = lowp(mem + pos), or the V
+// half with A = lowp(mem)); each wave owns whole 32-column head planes, so
+// its W fragments are private and come straight from L2 into VGPRs -- no W
+// staging, no barriers in the main loop.  W is pre-packed once per weight
+// version (fragment-major, 1 KB per plane and k-step), so every W load
+// instruction is 1 KB contiguous.  Operand ingest per workgroup: 64 KB of A +
+// 768 KB of W (L2-resident, 1.5 MB total).  Each finished plane (128 tokens x
+// 64 B, contiguous in the head-split output) is transposed through the wave's
+// LDS slice and leaves as 16-B non-temporal stores.
+//
+// MFMA 32x32x16 in the swapped form D[col][token] = W_frag x A_frag^T: lane
+// (lr, lh) holds token lr and columns (r & 3) + 8 (r >> 2) + 4 lh of its
+// 32-column plane, so a plane's row of 32 values is two lanes' 16 -- the
+// squared-norm reduction is one permlane32 swap.
+#include "cmt_common.h"
+
+namespace {
+
+constexpr int KP_BM = 128;            // token rows per workgroup
+constexpr int KP_K = 256;             // reduction depth (embed dims)
+constexpr int KP_NT = 256;            // 4 waves
+constexpr int KP_KS = KP_K / 16;      // MFMA k-steps
+constexpr int KP_MAXB = 2048;         // bias floats per column part held in LDS
+
+typedef const __attribute__((address_space(1))) void* kp_gaddr_t;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* kp_laddr_t;
+template <typename T> using frag_of = typename mfma_traits<T>::frag;
+
+// One head plane of one 64-token half: 32 MFMAs on the fragment set wf (the
+// freed slots refill with plane `nxt`, two planes ahead), then round, stage
+// [token][32] in the wave's LDS slice, key-norm max, and 16-B stores.
+template <typename T, bool MAXQ>
+__device__ __forceinline__ void kv_plane(const cmt_gemm_args& a, char* stg, const float* bw, const T* Wl,
+                                         typename mfma_traits<T>::frag (&wf)[KP_KS],
+                                         const typename mfma_traits<T>::frag (&af)[2][KP_KS], int j, int nxt,
+                                         int plane, int mg, const uint32_t (&soff)[4], __amdgpu_buffer_rsrc_t crsrc,
+                                         __amdgpu_buffer_rsrc_t prsrc, int lane) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    const int lr = lane & 31, lh = lane >> 5;
+    const T* Wn = Wl + (int64_t)nxt * (KP_KS * 512);
+    f32x16 acc[2];
+    {
+        // accumulators start at the bias (columns (r & 3) + 8 (r >> 2) + 4 lh)
+        f32x16 b16;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 b4 = *(const f32x4*)(bw + 32 * j + 8 * g + 4 * lh);
+            b16[4 * g] = b4[0]; b16[4 * g + 1] = b4[1]; b16[4 * g + 2] = b4[2]; b16[4 * g + 3] = b4[3];
+        }
+        acc[0] = b16;
+        acc[1] = b16;
+    }
+#pragma unroll
+    for (int ks = 0; ks < KP_KS; ++ks) {
+        acc[0] = mfma_traits<T>::mma(wf[ks], af[0][ks], acc[0]);
+        acc[1] = mfma_traits<T>::mma(wf[ks], af[1][ks], acc[1]);
+        wf[ks] = *(const frag_of<T>*)(Wn + ks * 512);   // plane `nxt` into the freed slot
+    }
+    float pm = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int tok = 32 * t + lr;
+        float ss = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const t4 v = t4{(T)acc[t][4 * g], (T)acc[t][4 * g + 1], (T)acc[t][4 * g + 2], (T)acc[t][4 * g + 3]};
+            const int c0 = 8 * g + 4 * lh;
+            *(t4*)(stg + tok * 64 + ((((c0 >> 3) ^ (tok >> 1)) & 3) << 4) + (c0 & 7) * 2) = v;
+            if (MAXQ) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
+            }
+        }
+        if (MAXQ) {
+            ss = pair_sum(mg + tok < a.M ? ss : 0.f);
+            pm = t ? fmaxf(pm, ss) : ss;
+        }
+    }
+    if (MAXQ) {
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) pm = fmaxf(pm, __shfl_xor(pm, off));
+        const int pm_planes = a.plane_max_cols >> 5;
+        const uint32_t po = (lane == 0 && mg < a.M) ? (uint32_t)((((int64_t)(mg >> 6)) * pm_planes + plane) * 4)
+                                                     : 0xffffffffu;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pm), prsrc, po, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t pl = (uint32_t)((int64_t)plane * a.rows_per_batch * 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int tok = 16 * i + (lane >> 2), ch = lane & 3;
+        const f32x4 v = *(const f32x4*)(stg + tok * 64 + (((ch ^ (tok >> 1)) & 3) << 4));
+        // streamed once (non-temporal): keeps W resident in L2
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), crsrc,
+                                              soff[i] == 0xffffffffu ? soff[i] : soff[i] + pl, 0, 2);
+    }
+}
+
+// The two 64-token halves x this wave's planes (an even count); MAXQ = this
+// part's planes all feed the key-norm maxima.  Every global access in the loop
+// is unconditional (stores masked by the buffer range check, not branches), so
+// the compiler counts the in-order vm counter exactly.  W fragments are
+// fetched TWO planes ahead into two alternating sets: a load issued after a
+// plane's stores completes only after those stores do (one counter, in
+// order), so one plane of distance exposed the HBM store latency every plane.
+template <typename T, bool MAXQ>
+__device__ __forceinline__ void kv_sweep(const cmt_gemm_args& a, const char* lds, char* stg, const float* bw,
+                                         const T* Wl, typename mfma_traits<T>::frag (&wa)[KP_KS],
+                                         typename mfma_traits<T>::frag (&wb)[KP_KS], int nplanes, int plane0,
+                                         int m0, int lane) {
+    typedef typename mfma_traits<T>::frag frag;
+    const int lr = lane & 31, lh = lane >> 5;
+    const uint32_t cbytes = (uint32_t)((int64_t)a.M * a.N * 2);
+    const auto crsrc = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, cbytes, 0x00020000);
+    const uint32_t pmbytes = MAXQ ? (uint32_t)(((a.M + 63) / 64) * (a.plane_max_cols >> 5) * 4) : 0u;
+    const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(MAXQ ? (void*)a.plane_max2 : a.C, 0, pmbytes, 0x00020000);
+    const int rpb = a.rows_per_batch;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        // B fragments of this half's 64 tokens: [token tile][k-step]
+        frag af[2][KP_KS];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int ks = 0; ks < KP_KS; ++ks)
+                af[t][ks] = *(const frag*)(lds + (64 * half + 32 * t + lr) * (KP_K * 2) +
+                                           (((2 * ks + lh) ^ (lr & 15)) << 4));
+        // byte offsets of this lane's 4 store rows (tokens 16 i + lane / 4, chunk lane & 3), plane 0
+        uint32_t soff[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + 64 * half + 16 * i + (lane >> 2);
+            const int bb = m / rpb;
+            const int64_t row = (int64_t)bb * (a.N >> 5) * rpb + (m - bb * rpb);
+            soff[i] = m < a.M ? (uint32_t)((row * 32 + 8 * (lane & 3)) * 2) : 0xffffffffu;
+        }
+        const int mg = m0 + 64 * half;                   // this half's 64-row key-norm group
+        for (int j = 0; j < nplanes; j += 2) {
+            const int n0 = j + 2 < nplanes ? j + 2 : j + 2 - nplanes;   // wraps to the next half's first two
+            kv_plane<T, MAXQ>(a, stg, bw, Wl, wa, af, j, n0, plane0 + j, mg, soff, crsrc, prsrc, lane);
+            kv_plane<T, MAXQ>(a, stg, bw, Wl, wb, af, j + 1, n0 + 1, plane0 + j + 1, mg, soff, crsrc, prsrc, lane);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(KP_NT, 1) void kvproj_kernel(cmt_gemm_args a, int parts) {
+    typedef typename mfma_traits<T>::frag frag;
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    // 64 KB A tile | 4 x 4 KB per-wave store staging | the part's bias (<= 8 KB)
+    __shared__ __attribute__((aligned(16))) char lds[KP_BM * KP_K * 2 + 4 * 4096 + KP_MAXB * 4];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+    // workgroup -> (row tile, column part); the parts of one row tile are
+    // consecutive blocks (their A tiles differ only in A vs A2)
+    const int rt = blockIdx.x / parts, part = blockIdx.x - rt * parts;
+    const int m0 = rt * KP_BM;
+    const int ncols = a.N / parts;                      // columns per part (multiple of 128)
+    const int n_part = part * ncols;
+    const bool sel_a2 = a.A2 != nullptr && n_part < a.a2_cols;
+    const T* Ab = (const T*)(sel_a2 ? a.A2 : a.A);
+    const int64_t lda = sel_a2 ? a.lda2 : a.lda;
+
+    // ---- A tile -> LDS (16-B chunks XOR-swizzled by row & 15)
+#pragma unroll
+    for (int i = 0; i < KP_BM * KP_K * 2 / 16 / KP_NT; ++i) {
+        const int piece = tid + KP_NT * i;
+        const int r = piece >> 5;
+        const int lc = (piece & 31) ^ (r & 15);
+        const int src = min(m0 + r, a.M - 1);
+        __builtin_amdgcn_global_load_lds((kp_gaddr_t)(Ab + (int64_t)src * lda + 8 * lc),
+                                         (kp_laddr_t)(lds + piece * 16), 16, 0, 0);
+    }
+    // the part's bias -> LDS: the epilogue reads it with no vmcnt wait (a global
+    // bias load there would drain the W prefetch and the stores before it, which
+    // count on the same in-order counter)
+    float* bsm = (float*)(lds + KP_BM * KP_K * 2 + 4 * 4096);
+    for (int piece = tid; piece < (ncols >> 2); piece += KP_NT) {
+        if (a.bias)
+            __builtin_amdgcn_global_load_lds((kp_gaddr_t)(a.bias + n_part + 4 * piece), (kp_laddr_t)(bsm + 4 * piece),
+                                             16, 0, 0);
+        else
+            *(f32x4*)(bsm + 4 * piece) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int planes_w = ncols / 32 / 4;                // head planes per wave
+    const int plane0 = (n_part >> 5) + wave * planes_w;
+    const T* W = (const T*)a.W;
+    // W in the fragment-packed layout (cmt_hip.h cmt_kv_proj): plane p, k-step ks
+    // is 1 KB contiguous, lane-major -- every W load instruction touches 8 lines
+    const T* Wl = W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
+    frag wa[KP_KS], wb[KP_KS];   // planes 0 and 1 (two planes of prefetch distance)
+#pragma unroll
+    for (int ks = 0; ks < KP_KS; ++ks) {
+        wa[ks] = *(const frag*)(Wl + ks * 512);
+        wb[ks] = *(const frag*)(Wl + KP_KS * 512 + ks * 512);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_mem();
+
+    char* stg = lds + KP_BM * KP_K * 2 + wave * 4096;   // [64 tokens][32] 16-bit
+    const float* bw = bsm + 32 * (plane0 - (n_part >> 5));
+
+    // output stores: rows >= M (and non-writer lanes of the key-norm max) get an
+    // out-of-range offset and the buffer range check drops them -- no branches
+    const bool maxq = a.plane_max2 != nullptr && n_part < a.plane_max_cols;
+    if (maxq) kv_sweep<T, true>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
+    else kv_sweep<T, false>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
+}
+
+}  // namespace
+
+extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_kv_proj: null args");
+    const cmt_gemm_args& a = *ap;
+    const int parts = a.A2 ? 2 : 1;
+    CMT_REQUIRE(a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16, "cmt_kv_proj: w_dtype must be f16 or bf16");
+    CMT_REQUIRE(a.a_dtype == a.w_dtype && a.c_dtype == a.w_dtype, "cmt_kv_proj: A and C in the compute dtype");
+    CMT_REQUIRE(a.A && a.W && a.C && a.M > 0 && a.K == KP_K && a.batch == 1, "cmt_kv_proj: needs A/W/C, K = 256");
+    CMT_REQUIRE(a.a_mode == CMT_A_ROWS && a.c_mode == CMT_C_HEADSPLIT && a.R == nullptr && !a.relu,
+                "cmt_kv_proj: row A, head-split C, no residual / relu");
+    CMT_REQUIRE(a.rows_per_batch > 0 && a.M % a.rows_per_batch == 0, "cmt_kv_proj: bad head-split rows");
+    CMT_REQUIRE(a.N % (256 * parts) == 0 && a.N / parts <= KP_MAXB,
+                "cmt_kv_proj: N must be a multiple of 256 per column part, at most 2048 per part");
+    CMT_REQUIRE(a.A2 == nullptr || (a.a2_mode == CMT_A2_SELECT && a.a2_cols * 2 == a.N && a.lda2 % 8 == 0),
+                "cmt_kv_proj: A2 selects the first half of the columns");
+    CMT_REQUIRE(a.plane_max2 == nullptr || (a.plane_max_cols % (a.N / parts) == 0 && a.plane_max_cols <= a.N),
+                "cmt_kv_proj: plane_max_cols must be a multiple of the column part (N / parts) <= N");
+    CMT_REQUIRE((int64_t)a.M * a.N * 2 < ((int64_t)1 << 32) - 1, "cmt_kv_proj: C must be < 4 GiB (32-bit offsets)");
+    CMT_REQUIRE(a.lda % 8 == 0 && ((uintptr_t)a.A | (uintptr_t)a.W | (uintptr_t)a.C | (uintptr_t)a.A2 |
+                                    (uintptr_t)a.bias) % 16 == 0, "cmt_kv_proj: 16-byte aligned operands");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned grid = (unsigned)(cdiv(a.M, KP_BM) * parts);
+    if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t><<<grid, KP_NT, 0, s>>>(a, parts);
+    else kvproj_kernel<f16_t><<<grid, KP_NT, 0, s>>>(a, parts);
+    return cmt_check_launch("cmt_kv_proj");
+}

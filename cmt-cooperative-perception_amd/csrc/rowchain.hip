@@ -1,27 +1,32 @@
 // Row-block chains of the decoder layer's query side (gfx950).
 //
-// One workgroup owns 32 complete query rows (all C = 256 columns) and runs a
-// chain of 256 x 256 (K = 256) sub-GEMMs whose operands stay in LDS, with the
-// post-norm decoder layer's bias / residual / LayerNorm epilogues in between
+// A workgroup owns 32 complete query rows (all C = 256 columns) and runs a
+// short chain of 256 x 256 (K = 256) sub-GEMMs whose operands stay in LDS, with
+// the post-norm decoder layer's bias / residual / LayerNorm epilogues in between
 // (petr_transformer.py:374-487, operation_order self_attn, norm, cross_attn,
 // norm, ffn, norm; mmcv FFN add_identity; LN eps from the module):
 //
-//   chain A (after self-attention):  out_proj + bias + residual -> norms[0] -> Y
-//                                    -> lowp(Y + query_pos) -> cross-attn Q projection
-//   chain B (after cross-attention): out_proj + bias + residual -> norms[1]
-//                                    -> FFN fc1 + ReLU -> fc2 + bias + residual -> norms[2] -> Y
-//                                    (next query) and post_norm -> OUT (layer output)
-//                                    -> next layer's self-attn in_proj (Q|K read lowp(Y + pos),
-//                                       V reads lowp(Y))
+//   kind 0, chain A (after self-attention), 1 workgroup per row block:
+//       out_proj + bias + residual -> norms[0] -> Y -> lowp(Y + query_pos) -> cross-attn Q projection
+//   kind 1, chain B1 (after cross-attention), 4 workgroups per row block (g = FFN quarter):
+//       out_proj + bias + residual -> norms[1] -> o -> fc1 rows [256g, 256g+256) + ReLU
+//       -> fc2 K block g -> fp32 partial WS[g] (g = 0 adds fc2.bias + o, the FFN residual)
+//   kind 2, chain B2, 3 workgroups per row block (1 on the last layer; g = Q|K|V block):
+//       sum of the 4 partials -> norms[2] -> Y (next query); g = 0: post_norm -> OUT
+//       -> next layer's self-attn in_proj block g (Q|K read lowp(Y + pos), V reads lowp(Y))
 //
-// The FFN runs as four (fc1 column block, fc2 K block) pairs, so its hidden
-// activation never leaves LDS (16 KB at a time).  Every weight reaches LDS as
-// a stream of 16 KB stages (256 weight rows x 32 k) through a ring of NSTG
-// slots by LDS-DMA; the stream runs across sub-GEMM boundaries.  MFMA
-// 32x32x16 in the swapped form (lane = query row), so a row's LayerNorm
-// reduces over registers, the lane pair and the 4 waves.  All global stores
-// happen after the last stage and all ordinary global loads before the first,
-// so no counted LDS-DMA wait is ever drained early.
+// Why split B: every workgroup streams its sub-GEMMs' weights through LDS, and
+// one CU's LDS-DMA stream moves only ~30-90 GB/s (MI355X_MICROARCH.md
+// ldsdma-fill), so a 900-row layer is bound by weight bytes per workgroup, not
+// by MFMA.  One-workgroup chain B (12 sub-GEMMs, 1.5 MB per workgroup on 29
+// CUs) took 54 us; B1 + B2 stream 384 KB / 128 KB per workgroup on 116 / 87.
+//
+// Every weight reaches LDS as a stream of 16 KB stages (256 weight rows x 32 k)
+// through a ring of NSTG slots by LDS-DMA; the stream runs across sub-GEMM
+// boundaries.  MFMA 32x32x16 in the swapped form (lane = query row), so a row's
+// LayerNorm reduces over registers, the lane pair and the 4 waves.  All global
+// stores happen after the last stage and all ordinary global loads before the
+// first, so no counted LDS-DMA wait is ever drained early.
 #include "cmt_common.h"
 
 namespace {
@@ -56,22 +61,15 @@ struct Eng {
     typedef typename mfma_traits<T>::frag frag;
     char* lds;
     int tid, lane, wave, lr, lh;
-    int issued, consumed, nstages, kind;
-    const T *Wo, *W1, *W2, *Wn;
+    int issued, consumed, nstages;
+    const T *w0, *w1, *w2;   // weights of sub-GEMMs 0, 1, 2 ([256 rows][K], leading dims below)
+    int ld0, ld1, ld2;
 
-    // weight base / leading dim of sub-GEMM `sub` (wave-uniform arithmetic, no tables):
-    // A: out_proj, Q proj.  B: out_proj, (fc1 block j, fc2 K block j) x 4, in_proj Q, K, V.
     __device__ __forceinline__ const T* sub_base(int sub, int& ld) const {
-        ld = CE;
-        if (kind == 0) return sub == 0 ? Wo : W1;
-        if (sub == 0) return Wo;
-        if (sub <= 8) {
-            const int j = (sub - 1) >> 1;
-            if (sub & 1) return W1 + (int64_t)j * CE * CE;
-            ld = 4 * CE;
-            return W2 + j * CE;
-        }
-        return Wn + (int64_t)(sub - 9) * CE * CE;
+        if (sub == 0) { ld = ld0; return w0; }
+        if (sub == 1) { ld = ld1; return w1; }
+        ld = ld2;
+        return w2;
     }
 
     __device__ __forceinline__ void issue() {
@@ -225,55 +223,79 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     e.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     e.lr = e.lane & 31;
     e.lh = e.lane >> 5;
-    e.kind = a.kind;
-    e.Wo = (const T*)a.Wo;
-    e.W1 = (const T*)a.W1;
-    e.W2 = (const T*)a.W2;
-    e.Wn = (const T*)a.Wn;
     e.issued = e.consumed = 0;
-    const bool chainB = a.kind == 1;
-    const bool has_next = chainB && a.Wn != nullptr;
-    e.nstages = (chainB ? (has_next ? 12 : 9) : 2) * SUB_STAGES;
-    const int nheads = chainB ? 24 : 8;
-    const int nprm = chainB ? PRM_B : PRM_A;
-    const int m0 = blockIdx.x * RB;
+    const int kind = a.kind;
+    const bool has_next = a.Wn != nullptr;
+    // workgroup -> (row block, part g)
+    const int parts = kind == 0 ? 1 : kind == 1 ? 4 : (has_next ? 3 : 1);
+    const int rb = blockIdx.x / parts, g = blockIdx.x - rb * parts;
+    const T* Wo = (const T*)a.Wo;
+    if (kind == 0) {
+        e.w0 = Wo; e.ld0 = CE;
+        e.w1 = (const T*)a.W1; e.ld1 = CE;
+        e.nstages = 2 * SUB_STAGES;
+    } else if (kind == 1) {
+        e.w0 = Wo; e.ld0 = CE;
+        e.w1 = (const T*)a.W1 + (int64_t)g * CE * CE; e.ld1 = CE;       // fc1 rows [256g, 256g + 256)
+        e.w2 = (const T*)a.W2 + g * CE; e.ld2 = 4 * CE;                  // fc2 columns (K) [256g, ...)
+        e.nstages = 3 * SUB_STAGES;
+    } else {
+        e.w0 = has_next ? (const T*)a.Wn + (int64_t)g * CE * CE : Wo; e.ld0 = CE;   // in_proj block g
+        e.nstages = has_next ? SUB_STAGES : 0;
+    }
+    const int m0 = rb * RB;
     const int row = min(m0 + e.lr, a.rows - 1);
     const bool row_ok = m0 + e.lr < a.rows;
     char* actA = lds + OFF_ACT_A;
     char* actB = lds + OFF_ACT_B;
+    float* ws = (float*)a.WS;
+    const int64_t plane = (int64_t)a.rows * CE;
 
     // ---- prologue: every ordinary load and the first LDS-DMAs, then one full wait
     float res[32], qp[32], oold[32];
-    if (a.R) {
+    if (kind == 2) {
+        // the FFN output + residual: sum of the four B1 partials
+        float t[32];
+        load_row32(ws, row, e.wave, e.lh, res);
+#pragma unroll
+        for (int p = 1; p < 4; ++p) {
+            load_row32(ws + p * plane, row, e.wave, e.lh, t);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) res[i] += t[i];
+        }
+    } else if (a.R) {
         load_row32(a.R, row, e.wave, e.lh, res);
     } else {
 #pragma unroll
         for (int i = 0; i < 32; ++i) res[i] = 0.f;
     }
-    const bool need_p = chainB ? has_next : true;
+    const bool need_p = kind == 0 || (kind == 2 && has_next && g < 2);
     if (need_p) {
         load_row32(a.P, row, e.wave, e.lh, qp);
     } else {
 #pragma unroll
         for (int i = 0; i < 32; ++i) qp[i] = 0.f;
     }
-    const bool max_into = chainB && (a.out_flags & CMT_LN_MAX_INTO);
+    const bool max_into = kind == 2 && g == 0 && (a.out_flags & CMT_LN_MAX_INTO);
     if (max_into) {
         load_row32(a.OUT, row, e.wave, e.lh, oold);
     } else {
 #pragma unroll
         for (int i = 0; i < 32; ++i) oold[i] = 0.f;
     }
-    // attention output rows -> actA (32 rows x 32 chunks, swizzled), parameter block -> LDS
+    if (kind != 2) {
+        // attention output rows -> actA (32 rows x 32 chunks, swizzled)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int piece = e.tid + NTC * i;
-        const int r = piece >> 5;
-        const int lc = (piece & 31) ^ (r & 15);
-        const int src_row = min(m0 + r, a.rows - 1);
-        __builtin_amdgcn_global_load_lds((rc_gaddr_t)((const T*)a.X + (int64_t)src_row * CE + 8 * lc),
-                                         (rc_laddr_t)(actA + piece * 16), 16, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+            const int piece = e.tid + NTC * i;
+            const int r = piece >> 5;
+            const int lc = (piece & 31) ^ (r & 15);
+            const int src_row = min(m0 + r, a.rows - 1);
+            __builtin_amdgcn_global_load_lds((rc_gaddr_t)((const T*)a.X + (int64_t)src_row * CE + 8 * lc),
+                                             (rc_laddr_t)(actA + piece * 16), 16, 0, 0);
+        }
     }
+    const int nprm = kind == 0 ? PRM_A : PRM_B;
     for (int piece = e.tid; piece < (nprm >> 2); piece += NTC)
         __builtin_amdgcn_global_load_lds((rc_gaddr_t)(a.prm + 4 * piece), (rc_laddr_t)(lds + OFF_PRM + piece * 16),
                                          16, 0, 0);
@@ -287,7 +309,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     f32x16 acc[2];
     float v[32];
     const float eps = a.eps;
-    if (!chainB) {
+    if (kind == 0) {
         // ---------------- chain A
         e.sub_gemm(actA, acc, true);                                   // out_proj
         {
@@ -311,10 +333,10 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int c0 = e.col(nt, 4 * g);
-                qo[nt * 4 + g] = t4{(T)(acc[nt][4 * g] + bq[c0]), (T)(acc[nt][4 * g + 1] + bq[c0 + 1]),
-                                    (T)(acc[nt][4 * g + 2] + bq[c0 + 2]), (T)(acc[nt][4 * g + 3] + bq[c0 + 3])};
+            for (int gg = 0; gg < 4; ++gg) {
+                const int c0 = e.col(nt, 4 * gg);
+                qo[nt * 4 + gg] = t4{(T)(acc[nt][4 * gg] + bq[c0]), (T)(acc[nt][4 * gg + 1] + bq[c0 + 1]),
+                                     (T)(acc[nt][4 * gg + 2] + bq[c0 + 2]), (T)(acc[nt][4 * gg + 3] + bq[c0 + 3])};
             }
         if (row_ok) {
             store_row32(a.Y, row, e.wave, e.lh, y);
@@ -322,100 +344,100 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int c0 = e.col(nt, 4 * g);
-                    *(t4*)((T*)a.Q + (((int64_t)b * nheads + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
-                        qo[nt * 4 + g];
+                for (int gg = 0; gg < 4; ++gg) {
+                    const int c0 = e.col(nt, 4 * gg);
+                    *(t4*)((T*)a.Q + (((int64_t)b * 8 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
+                        qo[nt * 4 + gg];
                 }
         }
         return;
     }
 
-    // ---------------- chain B
-    e.sub_gemm(actA, acc, true);                                       // out_proj
-    {
-        const float* bo = e.prm();
+    if (kind == 1) {
+        // ---------------- chain B1: out_proj + norms[1], then FFN quarter g
+        e.sub_gemm(actA, acc, true);                                   // out_proj
+        {
+            const float* bo = e.prm();
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
-    }
-    e.layernorm(v, 256, 512, eps);                                     // norms[1] -> o (FFN residual)
-    float o[32];
+                for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
+        }
+        e.layernorm(v, 256, 512, eps);                                 // norms[1] -> o (FFN residual)
+        e.put_act(actB, v);                                            // lowp(o): fc1 operand
+        e.sub_gemm(actB, acc, true);                                   // fc1 rows [256g, 256g + 256)
+        {
+            const float* b1 = e.prm() + 768 + 256 * g;
+            float h[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) o[i] = v[i];
-    e.put_act(actB, o);                                                // lowp(o): fc1 operand
-    f32x16 acc2[2];
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc2[nt][r] = 0.f;
-    for (int j = 0; j < 4; ++j) {
-        e.sub_gemm(actB, acc, true);                                   // fc1 column block j
-        const float* b1 = e.prm() + 768 + 256 * j;
-        float h[32];
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) h[nt * 16 + r] = fmaxf(acc[nt][r] + b1[e.col(nt, r)], 0.f);
-        e.put_act(actA, h);                                            // hidden block j = fc2 K block j
-        e.sub_gemm(actA, acc2, false);                                 // fc2 partial sum over K block j
-    }
-    {
+                for (int r = 0; r < 16; ++r) h[nt * 16 + r] = fmaxf(acc[nt][r] + b1[e.col(nt, r)], 0.f);
+            e.put_act(actA, h);                                        // hidden quarter g = fc2 K block g
+        }
+        e.sub_gemm(actA, acc, true);                                   // fc2 partial over K block g
         const float* b2 = e.prm() + 1792;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc2[nt][r] + b2[e.col(nt, r)] + o[nt * 16 + r];
+            for (int r = 0; r < 16; ++r) {
+                float x = acc[nt][r];
+                if (g == 0) x += b2[e.col(nt, r)] + v[nt * 16 + r];
+                v[nt * 16 + r] = x;
+            }
+        if (row_ok) store_row32(ws + g * plane, row, e.wave, e.lh, v);
+        return;
     }
+
+    // ---------------- chain B2: norms[2] (+ post_norm), next layer's in_proj block g
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = res[i];
     e.layernorm(v, 2048, 2304, eps);                                   // norms[2] -> next query
-    float y[32], out[32];
+    float y[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) y[i] = out[i] = v[i];
-    e.layernorm(out, 2560, 2816, eps);                                 // post_norm -> layer output
+    for (int i = 0; i < 32; ++i) y[i] = v[i];
+    if (g == 0) {
+        e.layernorm(v, 2560, 2816, eps);                               // post_norm -> layer output
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        float x = out[i];
-        if (a.out_flags & CMT_LN_NAN_TO_NUM) x = nan_to_num(x);
-        if (max_into) x = fmaxf(x, oold[i]);
-        out[i] = x;
-    }
-    t4 qo[24];
-    if (has_next) {
-        e.put_act(actA, y);                                            // lowp(y): V columns
-#pragma unroll
-        for (int i = 0; i < 32; ++i) v[i] = y[i] + qp[i];
-        e.put_act(actB, v);                                            // lowp(y + pos): Q|K columns
-        const float* bqkv = e.prm() + 3072;
-#pragma unroll
-        for (int blk = 0; blk < 3; ++blk) {
-            e.sub_gemm(blk < 2 ? actB : actA, acc, true);
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int c0 = blk * CE + e.col(nt, 4 * g);
-                    qo[blk * 8 + nt * 4 + g] =
-                        t4{(T)(acc[nt][4 * g] + bqkv[c0]), (T)(acc[nt][4 * g + 1] + bqkv[c0 + 1]),
-                           (T)(acc[nt][4 * g + 2] + bqkv[c0 + 2]), (T)(acc[nt][4 * g + 3] + bqkv[c0 + 3])};
-                }
+        for (int i = 0; i < 32; ++i) {
+            float x = v[i];
+            if (a.out_flags & CMT_LN_NAN_TO_NUM) x = nan_to_num(x);
+            if (max_into) x = fmaxf(x, oold[i]);
+            v[i] = x;
         }
     }
+    t4 qo[8];
+    if (has_next) {
+        float u[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) u[i] = y[i] + qp[i];              // qp = 0 for the V block
+        e.put_act(actA, u);                                            // lowp(y + pos) (Q|K) / lowp(y) (V)
+        e.sub_gemm(actA, acc, true);
+        const float* bqkv = e.prm() + 3072 + g * CE;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const int c0 = e.col(nt, 4 * gg);
+                qo[nt * 4 + gg] = t4{(T)(acc[nt][4 * gg] + bqkv[c0]), (T)(acc[nt][4 * gg + 1] + bqkv[c0 + 1]),
+                                     (T)(acc[nt][4 * gg + 2] + bqkv[c0 + 2]), (T)(acc[nt][4 * gg + 3] + bqkv[c0 + 3])};
+            }
+    }
     if (row_ok) {
-        store_row32(a.Y, row, e.wave, e.lh, y);
-        store_row32(a.OUT, row, e.wave, e.lh, out);
+        if (g == 0) {
+            store_row32(a.Y, row, e.wave, e.lh, y);
+            store_row32(a.OUT, row, e.wave, e.lh, v);
+        }
         if (has_next) {
             const int b = row / a.Nq, rr = row - b * a.Nq;
 #pragma unroll
-            for (int blk = 0; blk < 3; ++blk)
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int c0 = blk * CE + e.col(nt, 4 * g);
-                        *(t4*)((T*)a.Q + (((int64_t)b * nheads + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
-                            qo[blk * 8 + nt * 4 + g];
-                    }
+                for (int gg = 0; gg < 4; ++gg) {
+                    const int c0 = g * CE + e.col(nt, 4 * gg);
+                    *(t4*)((T*)a.Q + (((int64_t)b * 24 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
+                        qo[nt * 4 + gg];
+                }
         }
     }
 }
@@ -425,17 +447,23 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_chain: null args");
     const cmt_chain_args& a = *ap;
-    CMT_REQUIRE(a.kind == 0 || a.kind == 1, "cmt_chain: kind must be 0 (A) or 1 (B)");
+    CMT_REQUIRE(a.kind >= 0 && a.kind <= 2, "cmt_chain: kind must be 0 (A), 1 (B1) or 2 (B2)");
     CMT_REQUIRE(a.rows > 0 && a.Nq > 0 && a.rows % a.Nq == 0, "cmt_chain: rows must be B * Nq");
     CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16, "cmt_chain: dtype must be f16 or bf16");
-    CMT_REQUIRE(a.X && a.P && a.prm && a.Wo && a.W1 && a.Y, "cmt_chain: null pointer");
-    CMT_REQUIRE(a.kind == 0 || (a.W2 && a.OUT), "cmt_chain: chain B needs W2 and OUT");
-    CMT_REQUIRE(a.Q != nullptr || (a.kind == 1 && a.Wn == nullptr), "cmt_chain: null Q output");
+    CMT_REQUIRE(a.prm && a.Y, "cmt_chain: null pointer");
+    if (a.kind == 0) CMT_REQUIRE(a.X && a.P && a.Wo && a.W1 && a.Q, "cmt_chain: chain A needs X, P, Wo, W1, Q");
+    if (a.kind == 1) CMT_REQUIRE(a.X && a.Wo && a.W1 && a.W2 && a.WS, "cmt_chain: chain B1 needs X, Wo, W1, W2, WS");
+    if (a.kind == 2) {
+        CMT_REQUIRE(a.WS && a.OUT, "cmt_chain: chain B2 needs WS and OUT");
+        CMT_REQUIRE(a.Wn == nullptr || (a.P && a.Q), "cmt_chain: chain B2 with Wn needs P and Q");
+    }
     CMT_REQUIRE(((uintptr_t)a.X | (uintptr_t)a.prm | (uintptr_t)a.Wo | (uintptr_t)a.W1 | (uintptr_t)a.W2 |
-                 (uintptr_t)a.Wn | (uintptr_t)a.P | (uintptr_t)a.Y | (uintptr_t)a.R | (uintptr_t)a.OUT) % 16 == 0,
+                 (uintptr_t)a.Wn | (uintptr_t)a.P | (uintptr_t)a.Y | (uintptr_t)a.R | (uintptr_t)a.OUT |
+                 (uintptr_t)a.WS | (uintptr_t)a.Q) % 16 == 0,
                 "cmt_chain: buffers must be 16-byte aligned");
     hipStream_t s = (hipStream_t)stream;
-    const unsigned grid = (unsigned)cdiv(a.rows, RB);
+    const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
+    const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
     if (a.dtype == CMT_BF16) chain_kernel<bf16_t><<<grid, NTC, 0, s>>>(a);
     else chain_kernel<f16_t><<<grid, NTC, 0, s>>>(a);
     return cmt_check_launch("cmt_chain");

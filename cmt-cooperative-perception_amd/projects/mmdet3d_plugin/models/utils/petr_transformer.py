@@ -400,7 +400,8 @@ class PETRTransformerDecoder(nn.Module):
                     vb.append(ca.in_proj_bias[2 * C:])
             kv_w = to_dtype(torch.cat(kw + vw, 0), g)
             kv_b = torch.cat(kb + vb, 0).detach().contiguous() if kb else None
-            return dict(layers=layers, kv_w=kv_w, kv_b=kv_b,
+            kv_wp = native.kv_pack(kv_w) if (C == 256 and kv_w.dtype != torch.float32) else None
+            return dict(layers=layers, kv_w=kv_w, kv_wp=kv_wp, kv_b=kv_b,
                         post=(self.post_norm.weight.detach().contiguous(),
                               self.post_norm.bias.detach().contiguous(), self.post_norm.eps))
         return self._pack.get("decoder", params, prec.name, build)
@@ -506,8 +507,12 @@ class PETRTransformerDecoder(nn.Module):
         kmax2 = None
         if prec.attn == torch.bfloat16 and os.environ.get("CMT_ATTN_BOUND", "1") != "0":
             kmax2 = torch.empty((-(-B * Nk // native.PLANE_MAX_ROWS), L * H), dtype=f32, device=dev)
-        native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
-                    A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
+        if pk["kv_wp"] is not None and memb.dtype == pk["kv_wp"].dtype and os.environ.get("CMT_KVPROJ", "1") != "0":
+            native.kv_proj(memb, pk["kv_wp"], kv, M=B * Nk, N=2 * L * C, bias=pk["kv_b"], A2=mposb,
+                           headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
+        else:
+            native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
+                        A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
         # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114)
         tgt = tgt0.clone() if tgt0 is not None else torch.zeros((rows, C), dtype=f32, device=dev)
         tl = torch.empty((rows, C), dtype=lp, device=dev)          # lowp(tgt)
@@ -527,9 +532,10 @@ class PETRTransformerDecoder(nn.Module):
         pw, pb, _pe = pk["post"]
         if self._chain_ok() and os.environ.get("CMT_CHAIN", "1") != "0":
             # per layer: self-attn core, chain A (out_proj + norms[0] + cross Q proj),
-            # cross-attn core, chain B (out_proj + norms[1] + FFN + norms[2] + post_norm
-            # + next layer's in_proj) -- see rowchain.hip
+            # cross-attn core, chain B1 (out_proj + norms[1] + FFN quarter -> fp32 partials),
+            # chain B2 (partials -> norms[2] + post_norm + next layer's in_proj) -- see rowchain.hip
             ch = self._chain_pack(prec)
+            cws = torch.empty(native.chain_ws_numel(rows), dtype=torch.float32, device=dev)
             eps = self.post_norm.eps
             l0 = pk["layers"][0]
             native.gemm(tl, l0["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
@@ -549,9 +555,11 @@ class PETRTransformerDecoder(nn.Module):
                                      round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2,
                                      kmax_ld=L * H, kmax_plane0=l * H)
                 nxt = pk["layers"][l + 1]["sa_w"] if l + 1 < L else None
-                native.chain(1, ob, qpos, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
-                             R=t1n, W2=lw["f2_w"], Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
-                             Q=qkv if nxt is not None else None)
+                native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
+                             R=t1n, W2=lw["f2_w"], WS=cws)
+                native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
+                             Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
+                             Q=qkv if nxt is not None else None, WS=cws)
             return out
         # out-projection / fc2 GEMMs fused with their residual + LayerNorm (cmt_gemm_ln)
         fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "0") == "1"

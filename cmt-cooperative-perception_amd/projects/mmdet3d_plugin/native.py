@@ -11,7 +11,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "available", "gemm", "gemm_ln", "chain", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
+__all__ = ["lib", "available", "gemm", "gemm_ln", "chain", "kv_proj", "kv_pack", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
            "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
            "voxelize", "box_decode", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
@@ -63,7 +63,7 @@ class ChainArgs(ctypes.Structure):
     _fields_ = [("kind", _int), ("rows", _int), ("Nq", _int), ("dtype", _int), ("eps", _flt),
                 ("X", _vp), ("R", _vp), ("P", _vp), ("prm", _vp),
                 ("Wo", _vp), ("W1", _vp), ("W2", _vp), ("Wn", _vp),
-                ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp)]
+                ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp), ("WS", _vp)]
 
 
 class LnArgs(ctypes.Structure):
@@ -99,6 +99,7 @@ def _load():
         "cmt_layernorm_ex": ([P(LnArgs), _vp], _int),
         "cmt_gemm_ln": ([P(GemmArgs), P(LnArgs), _vp], _int),
         "cmt_chain": ([P(ChainArgs), _vp], _int),
+        "cmt_kv_proj": ([P(GemmArgs), _vp], _int),
         "cmt_add_cast": ([_vp, _vp, _int, _int, _int, _vp, _vp, _vp], _int),
         "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _int, _i64, _vp], _int),
         "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _int, _vp], _int),
@@ -188,6 +189,30 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
             raise RuntimeError("plane_max2 must be fp32 with ceil(M/64) * plane_max_cols/32 entries")
         g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
     _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
+
+
+def kv_pack(W):
+    """Fragment-packed copy of a [N][256] K/V projection weight for cmt_kv_proj
+    (cmt_hip.h): plane p, k-step ks, lane -> 8 consecutive k of row 32p + lane % 32."""
+    n, k = W.shape
+    if n % 32 or k != 256:
+        raise RuntimeError("kv_pack: W must be [N % 32 == 0][256]")
+    return W.reshape(n // 32, 32, 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
+def kv_proj(A, Wp, C, *, M, N, bias=None, A2=None, headsplit_rows, plane_max2=None, plane_max_cols=0):
+    """All-layer cross-attention K/V projection (cmt_kv_proj): columns < N/2 read
+    A2 (lowp(mem + pos)) when given, the rest A (lowp(mem)); Wp from kv_pack;
+    head-split C; optional per-64-row key-norm maxima (as cmt_gemm)."""
+    g = _gemm_args(A, Wp, C, M=M, N=N, K=256, lda=256, ldw=256, ldc=0, bias=bias, A2=A2,
+                   lda2=256 if A2 is not None else 0, a2_cols=N // 2 if A2 is not None else 0,
+                   headsplit_rows=headsplit_rows)
+    if plane_max2 is not None:
+        _dev(plane_max2)
+        if plane_max2.dtype != torch.float32 or plane_max2.numel() < -(-M // PLANE_MAX_ROWS) * (plane_max_cols // 32):
+            raise RuntimeError("plane_max2 must be fp32 with ceil(M/64) * plane_max_cols/32 entries")
+        g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
+    _check(lib().cmt_kv_proj(ctypes.byref(g), _stream()), "cmt_kv_proj")
 
 
 def _gemm_args(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0,
@@ -320,18 +345,27 @@ def gemm_ln(A, W, *, M, K, lda, ldw, bias=None, R=None, ldr=0, ln_w, ln_b, eps=1
     _check(lib().cmt_gemm_ln(ctypes.byref(g), ctypes.byref(a), _stream()), "cmt_gemm_ln")
 
 
-CHAIN_PRM = {0: 1024, 1: 3840}
+CHAIN_PRM = {0: 1024, 1: 3840, 2: 3840}
+
+
+def chain_ws_numel(rows):
+    """fp32 elements of the chain B1 -> B2 partials workspace."""
+    return 4 * rows * 256
 
 
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
-          out_flags=0, Q=None):
-    """One row-block chain of a decoder layer's query side (cmt_chain):
-    kind 0 after self-attention, kind 1 after cross-attention (cmt_hip.h)."""
-    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q)
+          out_flags=0, Q=None, WS=None):
+    """One row-block chain of a decoder layer's query side (cmt_chain): kind 0
+    after self-attention; kinds 1 then 2 after cross-attention (cmt_hip.h)."""
+    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS)
     if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:
         raise RuntimeError(f"cmt_chain: parameter block must be {CHAIN_PRM[kind]} fp32 values")
+    if WS is not None and (WS.dtype != torch.float32 or WS.numel() < chain_ws_numel(rows)):
+        raise RuntimeError("cmt_chain: WS must hold 4 * rows * 256 fp32")
     a = ChainArgs()
-    a.kind, a.rows, a.Nq, a.dtype, a.eps = kind, rows, Nq, DT[X.dtype], eps
+    a.kind, a.rows, a.Nq, a.eps = kind, rows, Nq, eps
+    lowp = next((t for t in (X, Q, Wn, Wo) if t is not None), None)
+    a.dtype = DT[lowp.dtype] if lowp is not None else BF16   # B2 without in_proj: no 16-bit operand
 
     def ptr(t):
         return None if t is None else t.data_ptr()
@@ -341,6 +375,7 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     a.OUT = None if OUT is None else OUT.data_ptr() + 4 * out_offset
     a.out_flags = out_flags
     a.Q = ptr(Q)
+    a.WS = ptr(WS)
     _check(lib().cmt_chain(ctypes.byref(a), _stream()), "cmt_chain")
 
 

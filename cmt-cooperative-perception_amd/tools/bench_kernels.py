@@ -83,6 +83,35 @@ def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0, fold=False):
           f"{tf:8.1f} TF/s", flush=True)
 
 
+def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
+    """Row-block chain A (kind 0), B1 (1) or B2 (2) at the decoder's query shape."""
+    dev = torch.device("cuda")
+    C, F = 256, 1024
+    X = torch.randn(rows, C, device=dev).to(dt)
+    R, P = torch.randn(rows, C, device=dev), torch.randn(rows, C, device=dev)
+    Wo = (torch.randn(C, C, device=dev) / 16).to(dt)
+    W1 = (torch.randn(F if kind else C, C, device=dev) / 16).to(dt)
+    W2 = (torch.randn(C, F, device=dev) / 32).to(dt)
+    Wn = None if last else (torch.randn(3 * C, C, device=dev) / 16).to(dt)
+    prm = torch.randn(N.CHAIN_PRM[kind], device=dev) * 0.1
+    Y, OUT = torch.empty(rows, C, device=dev), torch.empty(rows, C, device=dev)
+    WS = torch.randn(N.chain_ws_numel(rows), device=dev)
+    Q = torch.empty(rows * 3 * C, dtype=dt, device=dev)
+    if kind == 0:
+        fn = lambda: N.chain(0, X, P, prm, Wo, W1, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, Q=Q)
+        fl = 2 * rows * C * C * 2
+    elif kind == 1:
+        fn = lambda: N.chain(1, X, None, prm, Wo, W1, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, W2=W2, WS=WS)
+        fl = 2 * rows * C * C * 9
+    else:
+        fn = lambda: N.chain(2, None, None if last else P, prm, None, None, Y, rows=rows, Nq=Nq, eps=1e-5,
+                             Wn=Wn, OUT=OUT, Q=None if last else Q, WS=WS)
+        fl = 2 * rows * C * C * (0 if last else 3)
+    us = timeit(fn)
+    print(f"chain {['A ', 'B1', 'B2'][kind]}{' last' if last else '     '} rows={rows:5d} {us:9.2f} us "
+          f"{fl / (us * 1e-6) / 1e12:8.1f} TF/s", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -109,6 +138,22 @@ def main():
         gemm_case("out proj (+res)", 900, 256, 256, bf, a_f32=False, R=True)
         gemm_case("ffn fc1 (relu)", 900, 1024, 256, bf, a_f32=False, relu=True, out_dt=bf)
         gemm_case("ffn fc2 (+res)", 900, 256, 1024, bf, a_f32=False, R=True)
+    if args.only in ("", "gemm", "kv"):
+        dev = torch.device("cuda")
+        A = torch.randn(32400, 256, device=dev).to(bf)
+        A2 = torch.randn(32400, 256, device=dev).to(bf)
+        Wp = N.kv_pack((torch.randn(3072, 256, device=dev) / 16).to(bf))
+        bias = torch.randn(3072, device=dev)
+        C = torch.empty(32400 * 3072, dtype=bf, device=dev)
+        pm = torch.empty(507, 48, device=dev)
+        us = timeit(lambda: N.kv_proj(A, Wp, C, M=32400, N=3072, bias=bias, A2=A2, headsplit_rows=32400,
+                                      plane_max2=pm, plane_max_cols=1536))
+        print(f"kv_proj (A-stationary, packed W)  M= 32400 N= 3072 K=  256 {us:9.2f} us "
+              f"{2 * 32400 * 3072 * 256 / (us * 1e-6) / 1e12:8.1f} TF/s", flush=True)
+    if args.only in ("", "chain"):
+        for kind, last in ((0, False), (1, False), (2, False), (2, True)):
+            chain_case(kind, last=last)
+        chain_case(1, rows=1800)
     if args.only in ("", "attn"):
         for s in (0, 8, 16):
             for fold in (False, True):

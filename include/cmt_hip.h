@@ -96,6 +96,17 @@ typedef struct cmt_gemm_args {
 
 int cmt_gemm(const cmt_gemm_args* args, void* stream);
 
+/* cmt_kv_proj: the cross-attention K/V projection of ALL decoder layers in one
+ * launch (kvproj.hip) -- FlashMHA's packed in_proj on the memory side
+ * (attention.py:21-27, 126-138; key = key + key_pos at petr_transformer.py:
+ * 296-299).  Same cmt_gemm_args contract as cmt_gemm restricted to: K = 256,
+ * f16/bf16 A / W / C, row A, head-split C, no R / relu, batch 1, A2 (if any)
+ * in select mode on exactly the first N/2 columns, N % (256 * parts) == 0,
+ * optional plane_max2.  W is in the FRAGMENT-PACKED layout
+ *   Wp[((p * 16 + ks) * 64 + lane) * 8 + e] = W[32 p + (lane & 31)][16 ks + 8 (lane >> 5) + e]
+ * (torch: W.view(N/32, 32, 16, 2, 8).permute(0, 2, 3, 1, 4)), ldw unused. */
+int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
+
 /* ------------------------------------------------------------------------
  * Multi-head attention core, head_dim = 32 (flash-style, online softmax,
  * f16/bf16 MFMA with fp32 accumulate, or exact-f32 MFMA for dtype CMT_F32;
@@ -186,43 +197,47 @@ int cmt_layernorm_ex(const cmt_ln_args* args, void* stream);
 int cmt_gemm_ln(const cmt_gemm_args* gemm, const cmt_ln_args* ln, void* stream);
 
 /* ------------------------------------------------------------------------
- * Row-block chains of the decoder layer's query side (rowchain.hip): one
+ * Row-block chains of the decoder layer's query side (rowchain.hip): each
  * workgroup owns 32 complete query rows (C = 256) and runs the layer's GEMMs
  * back to back with their operands in LDS and the post-norm epilogues fused
  * (petr_transformer.py:374-487; mmcv FFN / LN).  Replaces, per layer, the
  * cuBLAS out_proj / in_proj / FFN GEMMs and the three LayerNorms around the
  * two attention cores (attention.py:117, mmcv MultiheadAttention, mmcv FFN).
- *   kind 0 (chain A, after self-attention):
+ *   kind 0 (chain A, after self-attention; 1 workgroup per 32 rows):
  *     Y = norms[0](X Wo^T + bo + R);  Q = lowp(Y + P) Wq^T + bq  (head split [B][8][Nq][32])
- *   kind 1 (chain B, after cross-attention):
- *     o = norms[1](X Wo^T + bo + R);  f = relu(lowp(o) W1^T + b1);
- *     Y = norms[2](lowp(f) W2^T + b2 + o)   (the next layer's query)
+ *   kind 1 (chain B1, after cross-attention; 4 workgroups per 32 rows, g = FFN quarter):
+ *     o = norms[1](X Wo^T + bo + R);  h_g = relu(lowp(o) W1[256g:256g+256]^T + b1[...]);
+ *     WS[g] = lowp(h_g) W2[:, 256g:256g+256]^T  (+ b2 + o for g = 0)     fp32 partials
+ *   kind 2 (chain B2; 3 workgroups per 32 rows with Wn, else 1):
+ *     Y = norms[2](WS[0] + WS[1] + WS[2] + WS[3])   (the next layer's query)
  *     OUT = post_norm(Y) (+ CMT_LN_NAN_TO_NUM / CMT_LN_MAX_INTO per out_flags)
  *     if Wn: Q = [lowp(Y + P) | lowp(Y + P) | lowp(Y)] Wn^T + bn  (next layer's
  *            self-attn in_proj, head split [B][24][Nq][32])
  * prm: packed fp32 parameter block, layout (floats)
  *   A (1024): bo | norms[0].weight | norms[0].bias | bq
- *   B (3840): bo | norms[1].w | norms[1].b | b1 (1024) | b2 | norms[2].w | norms[2].b |
- *             post_norm.w | post_norm.b | bn (768, zeros without Wn)
+ *   B (3840, the same block for B1 and B2): bo | norms[1].w | norms[1].b | b1 (1024) | b2 |
+ *             norms[2].w | norms[2].b | post_norm.w | post_norm.b | bn (768, zeros without Wn)
+ * WS: caller workspace of 4 * rows * 256 fp32 (B1 writes, B2 reads).
  * One eps for every LayerNorm of the layer.  Weights / X / Q in the compute
  * dtype (f16 / bf16), residuals and outputs fp32; every buffer 16-byte aligned.
  * ------------------------------------------------------------------------ */
 typedef struct cmt_chain_args {
-    int kind;                  /* 0 = chain A, 1 = chain B */
+    int kind;                  /* 0 = chain A, 1 = chain B1, 2 = chain B2 */
     int rows, Nq;              /* rows = B * Nq */
     int dtype;                 /* CMT_F16 / CMT_BF16 */
     float eps;
-    const void* X;             /* attention output [rows][256] */
-    const float* R;            /* residual [rows][256] fp32 (NULL = zeros) */
-    const float* P;            /* query_pos [rows][256] fp32 */
+    const void* X;             /* A, B1: attention output [rows][256] */
+    const float* R;            /* A, B1: residual [rows][256] fp32 (NULL = zeros) */
+    const float* P;            /* query_pos [rows][256] fp32 (A; B2 with Wn) */
     const float* prm;          /* packed parameter block */
-    const void* Wo;            /* out_proj.weight [256][256] */
-    const void* W1;            /* A: cross-attn in_proj_weight[:256]; B: fc1.weight [1024][256] */
-    const void* W2;            /* B: fc2.weight [256][1024] */
-    const void* Wn;            /* B: next layer's self-attn in_proj_weight [768][256] (NULL: last layer) */
-    float* Y;                  /* [rows][256] fp32 */
-    float* OUT; int out_flags; /* B: layer output [rows][256] fp32 */
-    void* Q;                   /* head-split projection output */
+    const void* Wo;            /* A, B1: out_proj.weight [256][256] */
+    const void* W1;            /* A: cross-attn in_proj_weight[:256]; B1: fc1.weight [1024][256] */
+    const void* W2;            /* B1: fc2.weight [256][1024] */
+    const void* Wn;            /* B2: next layer's self-attn in_proj_weight [768][256] (NULL: last layer) */
+    float* Y;                  /* A: norms[0] output; B2: norms[2] output; [rows][256] fp32 */
+    float* OUT; int out_flags; /* B2: layer output [rows][256] fp32 */
+    void* Q;                   /* head-split projection output (A; B2 with Wn) */
+    float* WS;                 /* B1 / B2: partials workspace [4][rows][256] fp32 */
 } cmt_chain_args;
 int cmt_chain(const cmt_chain_args* args, void* stream);
 

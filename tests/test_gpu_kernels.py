@@ -166,6 +166,36 @@ def test_gemm_plane_max2(N, dev, dt, B, S, big):
     assert torch.allclose(pm.cpu().double(), ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100)])
+def test_kvproj_select_plane_max(N, dev, dt, B, S):
+    """All-layer K/V projection shape (N = 3072, K = 256, A2 select on the K half,
+    head-split output, K-half key-norm maxima) through cmt_kv_proj, the
+    A-stationary kernel on fragment-packed W (kvproj.hip); ragged M, row tiles
+    straddling the batch boundary, a grid smaller than one 128-row tile pair."""
+    g = torch.Generator().manual_seed(S * 7 + B)
+    K, Nc = 256, 3072
+    M, cols = B * S, Nc // 2
+    A = torch.randn(M, K, generator=g).to(dt)
+    A2 = torch.randn(M, K, generator=g).to(dt)
+    W = (torch.randn(Nc, K, generator=g) / 16).to(dt)
+    bias = torch.randn(Nc, generator=g) * 0.1
+    Y = torch.empty(M * Nc, dtype=dt, device=dev)
+    nb = -(-M // 64)
+    pm = torch.full((nb, cols // 32), -1.0, device=dev)
+    N.kv_proj(A.to(dev), N.kv_pack(W.to(dev)), Y, M=M, N=Nc, bias=bias.to(dev), A2=A2.to(dev), headsplit_rows=S,
+              plane_max2=pm, plane_max_cols=cols)
+    d = lambda t: t.double()
+    ref = torch.cat([d(A2) @ d(W[:cols]).T, d(A) @ d(W[cols:]).T], 1) + d(bias)
+    y = Y.cpu().view(B, Nc // 32, S, 32).permute(0, 2, 1, 3).reshape(M, Nc).double()
+    rel = (y - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < 1e-2, rel
+    ss = (y[:, :cols].view(M, cols // 32, 32) ** 2).sum(-1)
+    pad = nb * 64 - M
+    pref = torch.cat([ss, torch.zeros(pad, cols // 32, dtype=ss.dtype)], 0).view(nb, 64, -1).amax(1)
+    assert torch.allclose(pm.cpu().double(), pref, rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("scale_q", [1.0, 40.0])
 @pytest.mark.parametrize("B,Nq,Nk,splits", [(1, 900, 32400, 0), (2, 300, 4097, 3), (1, 257, 8192, 1)])
 def test_attention_bounded_max(N, dev, B, Nq, Nk, splits, scale_q):
@@ -515,9 +545,10 @@ def test_chain_a(N, dev, dt, B, Nq, with_r):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,Nq,last,flags", [(1, 900, False, 1), (2, 37, True, 3)])
 def test_chain_b(N, dev, dt, B, Nq, last, flags):
-    """Row-block chain B (out_proj + residual -> norms[1] -> FFN in four fc1/fc2
-    block pairs -> norms[2] and post_norm (nan_to_num / coop max-into) -> next
-    in_proj, head split) vs fp64 math on the same rounded operands."""
+    """Row-block chains B1 (out_proj + residual -> norms[1] -> one FFN quarter per
+    workgroup -> fp32 partials) and B2 (partials -> norms[2] and post_norm
+    (nan_to_num / coop max-into) -> next in_proj, head split) vs fp64 math on the
+    same rounded operands."""
     g = torch.Generator().manual_seed(B * 1000 + Nq)
     C, F, rows = 256, 1024, B * Nq
     X = torch.randn(rows, C, generator=g).to(dt)
@@ -536,9 +567,12 @@ def test_chain_b(N, dev, dt, B, Nq, last, flags):
     old = torch.randn(rows, C, generator=g)
     OUT = old.clone().to(dev)
     QKV = torch.empty(B * 24 * Nq * 32, dtype=dt, device=dev)
-    N.chain(1, X.to(dev), P.to(dev), prm.to(dev), Wo.to(dev), W1.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
-            R=R.to(dev), W2=W2.to(dev), Wn=None if last else Wn.to(dev), OUT=OUT, out_flags=flags,
-            Q=None if last else QKV)
+    WS = torch.full((N.chain_ws_numel(rows),), float("nan"), device=dev)
+    prm_d = prm.to(dev)
+    N.chain(1, X.to(dev), None, prm_d, Wo.to(dev), W1.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
+            R=R.to(dev), W2=W2.to(dev), WS=WS)
+    N.chain(2, None, None if last else P.to(dev), prm_d, None, None, Y, rows=rows, Nq=Nq, eps=1e-5,
+            Wn=None if last else Wn.to(dev), OUT=OUT, out_flags=flags, Q=None if last else QKV, WS=WS)
     d = lambda t: t.double()
     o = _ln64(d(X) @ d(Wo).T + d(bo) + d(R), d(l1w), d(l1b))
     h = torch.relu(d(o.to(dt)) @ d(W1).T + d(b1)).to(dt)
