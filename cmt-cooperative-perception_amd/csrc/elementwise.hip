@@ -297,71 +297,77 @@ __global__ void cast_kernel(const TI* __restrict__ X, TO* Y, int64_t n) {
 }
 
 // ---------------------------------------------------------------------------
-// Task-head tail (cmt_head.py:136-203, 501-513).
-// (1) GroupLayerNorm1d (per head, hc channels, biased var, eps 1e-6) + ReLU,
-//     in place on H1 [L][B*Nq][nheads*hc]; one wave per (l, row), hc == 64.
-// (2) grouped Conv1d #2 (+bias) with kernel k along the query axis and the
-//     center/height box epilogue; one thread per output element.
+// Task-head tail (cmt_head.py:136-203, 501-513), one launch.
+// A workgroup owns (layer l, TQ-query block, batch b).  It stages the block's
+// conv-1 rows H1 [l][b*Nq + q][nheads*hc] (+ k/2 halo rows each side) in LDS,
+// applies GroupLayerNorm1d (per head, hc = 64 channels, biased var, eps 1e-6,
+// cmt_head.py:56-66) + ReLU there -- one wave per (row, head) -- and then the
+// grouped Conv1d #2 (+bias, kernel k along queries, zero pad: halo rows
+// outside [0, Nq) stay 0 AFTER the norm, as the conv pads its input) with the
+// center/height box epilogue; one thread per (query, output) pair.  H1 is only
+// read.  LDS rows are padded by 4 floats so the query-strided f32x4 reads of
+// a wave spread over all banks (an unpadded 384-float row put the 16..32
+// queries of a wave on one bank).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void group_ln_relu_kernel(float* H1, int rows, int nheads,
-                                                            const float* __restrict__ gw,
-                                                            const float* __restrict__ gb) {
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (row >= rows) return;
-    const int li = blockIdx.y;  // decoder layer = conv group
-    const int width = nheads * 64;
-    float* x = H1 + ((int64_t)li * rows + row) * width;
-    const float* w = gw + (int64_t)li * width;
-    const float* b = gb + (int64_t)li * width;
-    for (int hd = 0; hd < nheads; ++hd) {
-        const int c = hd * 64 + lane;
-        const float v = x[c];
-        const float mu = wave_sum(v) / 64.f;
-        const float d = v - mu;
-        const float var = wave_sum(d * d) / 64.f;
-        float y = d / sqrtf(var + 1e-6f);
-        y = w[c] * y + b[c];
-        x[c] = fmaxf(y, 0.f);
-    }
-}
-
 struct TailParams {
     const float* G; int L, B, Nq, nheads, hc;
+    const float* gw; const float* gb;
     const float* W2; const float* B2;
-    int head_start[16]; int head_of[64];
+    int head_of[64];
     int out_total, k;
     const float* ref; int center_col, height_col;
     float pc[6];
     float* OUT;
 };
 
-// One workgroup per (layer, 32-query block, batch): the hidden rows of the
-// block (+1 halo row each side for k = 3) and the layer's conv-2 weights are
-// staged in LDS once, then each thread produces (query, output) pairs.
-constexpr int TQ = 32;
+constexpr int TQ = 16;
 
-__global__ __launch_bounds__(256) void task_head_conv2_kernel(TailParams p) {
+__device__ __forceinline__ int tail_gstride(int width) { return width + 4; }
+__device__ __forceinline__ int tail_wstride(int hc) { return hc + 4; }
+
+__global__ __launch_bounds__(256) void task_head_tail_kernel(TailParams p) {
     extern __shared__ __attribute__((aligned(16))) float tsm[];
     const int l = blockIdx.x;
     const int q0 = blockIdx.y * TQ;
     const int b = blockIdx.z;
     const int width = p.nheads * p.hc;
+    const int gs = tail_gstride(width), ws = tail_wstride(p.hc);
     const int half = p.k >> 1;
     const int nrows = TQ + 2 * half;
-    float* G = tsm;                                   // [nrows][width]
-    float* W = tsm + nrows * width;                   // [out_total][k][hc]
+    float* G = tsm;                                   // [nrows][gs]
+    float* W = tsm + nrows * gs;                      // [out_total * k][ws]
     const float* Gsrc = p.G + ((int64_t)l * p.B + b) * p.Nq * width;
     for (int i = threadIdx.x; i < nrows * width / 4; i += blockDim.x) {
         const int r = (i * 4) / width, c = (i * 4) - r * width;
         const int q = q0 - half + r;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (q >= 0 && q < p.Nq) v = *(const f32x4*)(Gsrc + (int64_t)q * width + c);
-        *(f32x4*)(G + r * width + c) = v;
+        *(f32x4*)(G + r * gs + c) = v;
     }
-    const int wsz = p.out_total * p.k * p.hc;
-    const float* Wsrc = p.W2 + (int64_t)l * wsz;
-    for (int i = threadIdx.x; i < wsz / 4; i += blockDim.x) *(f32x4*)(W + 4 * i) = *(const f32x4*)(Wsrc + 4 * i);
+    const int wrows = p.out_total * p.k;
+    const float* Wsrc = p.W2 + (int64_t)l * wrows * p.hc;
+    for (int i = threadIdx.x; i < wrows * p.hc / 4; i += blockDim.x) {
+        const int r = (i * 4) / p.hc, c = (i * 4) - r * p.hc;
+        *(f32x4*)(W + r * ws + c) = *(const f32x4*)(Wsrc + 4 * i);
+    }
+    __syncthreads();
+    {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const float* w = p.gw + (int64_t)l * width;
+        const float* bb = p.gb + (int64_t)l * width;
+        for (int g = wave; g < nrows * p.nheads; g += blockDim.x >> 6) {
+            const int r = g / p.nheads, hd = g - r * p.nheads;
+            const int q = q0 - half + r;
+            if (q < 0 || q >= p.Nq) continue;         // zero pad of conv #2's input
+            const int c = hd * 64 + lane;
+            const float v = G[r * gs + c];
+            const float mu = wave_sum(v) / 64.f;
+            const float d = v - mu;
+            const float var = wave_sum(d * d) / 64.f;
+            const float y = w[c] * (d / sqrtf(var + 1e-6f)) + bb[c];
+            G[r * gs + c] = fmaxf(y, 0.f);
+        }
+    }
     __syncthreads();
     const int qi = threadIdx.x % TQ;
     const int q = q0 + qi;
@@ -370,8 +376,8 @@ __global__ __launch_bounds__(256) void task_head_conv2_kernel(TailParams p) {
         const int hd = p.head_of[o];
         float acc = p.B2[(int64_t)l * p.out_total + o];
         for (int t = 0; t < p.k; ++t) {
-            const float* g = G + (qi + t) * width + hd * p.hc;
-            const float* w = W + (o * p.k + t) * p.hc;
+            const float* g = G + (qi + t) * gs + hd * p.hc;
+            const float* w = W + (o * p.k + t) * ws;
             float s0 = 0.f, s1 = 0.f;
             for (int c = 0; c < p.hc; c += 8) {
                 const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
@@ -555,20 +561,15 @@ extern "C" int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nhe
     CMT_REQUIRE(nheads > 0 && nheads <= 16 && out_total > 0 && out_total <= 64 && (k == 1 || k == 3),
                 "cmt_task_head_tail: unsupported head geometry");
     hipStream_t s = (hipStream_t)stream;
-    const int rows = B * Nq;
-    dim3 g1(cdiv(rows, 4), L);
-    group_ln_relu_kernel<<<g1, 256, 0, s>>>(const_cast<float*>(H1), rows, nheads, gln_w, gln_b);
-    int rc = cmt_check_launch("cmt_task_head_tail/gln");
-    if (rc) return rc;
     TailParams p;
     p.G = H1; p.L = L; p.B = B; p.Nq = Nq; p.nheads = nheads; p.hc = hc;
+    p.gw = gln_w; p.gb = gln_b;
     p.W2 = W2; p.B2 = B2; p.out_total = out_total; p.k = k;
     p.ref = ref; p.center_col = center_col; p.height_col = height_col;
     for (int i = 0; i < 6; ++i) p.pc[i] = pc_range6[i];
     p.OUT = OUT;
     int o = 0;
     for (int hd = 0; hd < nheads; ++hd) {
-        p.head_start[hd] = o;
         for (int j = 0; j < head_out[hd]; ++j) {
             if (o >= 64) return cmt_fail(CMT_EINVAL, "cmt_task_head_tail: too many outputs");
             p.head_of[o++] = hd;
@@ -576,9 +577,9 @@ extern "C" int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nhe
     }
     CMT_REQUIRE(o == out_total, "cmt_task_head_tail: head_out does not sum to out_total");
     const int width = nheads * hc;
-    const size_t smem = sizeof(float) * ((size_t)(TQ + 2 * (k >> 1)) * width + (size_t)out_total * k * hc);
+    const size_t smem = sizeof(float) * ((size_t)(TQ + 2 * (k >> 1)) * (width + 4) + (size_t)out_total * k * (hc + 4));
     CMT_REQUIRE(smem <= 160 * 1024, "cmt_task_head_tail: head too wide for LDS staging");
     dim3 g2(L, cdiv(Nq, TQ), B);
-    task_head_conv2_kernel<<<g2, 256, smem, s>>>(p);
-    return cmt_check_launch("cmt_task_head_tail/conv2");
+    task_head_tail_kernel<<<g2, 256, smem, s>>>(p);
+    return cmt_check_launch("cmt_task_head_tail");
 }

@@ -293,7 +293,8 @@ int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* st
  * packed per head, bias B2 [L][out_total].  Outputs are written to
  * OUT[L, B, Nq, out_total] (heads concatenated in order, widths head_out[]).
  * Columns listed by center_col/height_col receive the box epilogue:
- * sigmoid(x + inverse_sigmoid(ref)) * (max - min) + min.
+ * sigmoid(x + inverse_sigmoid(ref)) * (max - min) + min.  H1 is only read;
+ * the norm is applied to the LDS copy (one launch).
  * ------------------------------------------------------------------------ */
 int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nheads, int hc,
                        const float* gln_w, const float* gln_b, const float* W2, const float* B2,
