@@ -57,14 +57,61 @@ def init_dist(args):
     return env
 
 
-def cpu_baseline(head_cfg_name, seconds, seed):
+WORKLOADS = {
+    # name: (head config, agents as (meta prefix, camera yaws or None), description)
+    "lidar": ("cmt_lidar_nus", [("", None)],
+              "CMT-L (LiDAR-only) nuScenes-shape: BEV 512x180x180 (32400 tokens), 900 queries, 6-layer decoder, "
+              "CmtLidarHead forward (shared_conv + encodings + decoder + task heads), batch 1 frame per GPU"),
+    "fusion": ("cmt_fusion_nus", [("", S.NUS_YAWS)],
+               "CMT camera+LiDAR nuScenes-shape (configs[2]): BEV 512x180x180 + 6 views x 256x40x100 image feats "
+               "(56400 tokens), 900 queries, 6-layer decoder, CmtHead forward, batch 1 frame per GPU"),
+    "coop": ("cmtcoop_fusion_tumtraf", [("vehicle_", S.VEHICLE_YAWS), ("infrastructure_", S.INFRA_YAWS)],
+             "CMTCoop TUMTraf-shape forward (configs[3] forward leg): vehicle BEV 180x180 + 1 cam, infrastructure "
+             "BEV 180x180 + 3 cams (36400 + 44400 tokens), 900 queries, 6-layer decoder per agent, max fusion, "
+             "CmtHeadCoop forward, batch 1 frame per GPU"),
+}
+
+
+def make_workload(name, seed, device=None):
+    """(head, head cfg, forward closure, per-agent memory lengths, oracle closure)
+    for one synthetic frame of ``name``; tensors on ``device`` (CPU if None)."""
+    cfg_name, agents, _ = WORKLOADS[name]
+    head, cfg, _ = S.build_synthetic_head(cfg_name, seed=0, device=device)
+    inputs, nks, metas = [], [], [dict()]
+    for i, (prefix, yaws) in enumerate(agents):
+        x = S.synthetic_bev(1, 180, 180, seed=seed + 1 + 10 * i, device=device)
+        xi = None
+        if yaws is not None:
+            xi = S.synthetic_img(len(yaws), 40, 100, seed=seed + 2 + 10 * i, device=device)
+            m = S.synthetic_metas(1, yaws=yaws, prefix=prefix, seed=seed + 3 + 10 * i)[0]
+            metas[0].update(m)
+        inputs.append((prefix, x, xi))
+        nks.append(180 * 180 + (0 if yaws is None else len(yaws) * 40 * 100))
+    if len(agents) == 1:
+        _, x, xi = inputs[0]
+        fwd = lambda: head([x], [xi] if xi is not None else None, metas)  # noqa: E731
+    else:
+        (_, xv, iv), (_, xi_, ii) = inputs
+        fwd = lambda: head([xv], [xi_], [iv], [ii], metas)  # noqa: E731
+
+    def oracle_fwd():
+        from oracle import cmt_oracle as O
+        oc = O.cfg_from_head_cfg(cfg)
+        sd = S.head_state_dict(head)
+        cpu = [(p, x.cpu(), None if xi is None else xi.cpu()) for p, x, xi in inputs]
+        variant = "lidar" if name == "lidar" else "fusion"
+        if len(cpu) == 1:
+            return lambda: O.head_forward(oc, sd, cpu[0][1], cpu[0][2], metas, variant)
+        return lambda: O.head_coop_forward(oc, sd, cpu, metas, variant)
+
+    return head, cfg, fwd, nks, oracle_fwd
+
+
+def cpu_baseline(workload, seconds, seed):
     """The oracle (CPU restatement, fp32 exact math, PyTorch CPU) on the same
     workload, bounded to about ``seconds`` of host time."""
-    from oracle import cmt_oracle as O
-    head, cfg, _ = S.build_synthetic_head(head_cfg_name, seed=seed)
-    sd = S.head_state_dict(head)
-    oc = O.cfg_from_head_cfg(cfg)
-    x = S.synthetic_bev(1, 180, 180, seed=seed + 1)
+    _, _, _, nks, oracle_fwd = make_workload(workload, seed)
+    run = oracle_fwd()
     threads = torch.get_num_threads()
     t0 = time.perf_counter()
     n = 0
@@ -72,7 +119,7 @@ def cpu_baseline(head_cfg_name, seconds, seed):
     with torch.no_grad():
         while True:
             t = time.perf_counter()
-            O.head_forward(oc, sd, x, None, [dict()], "lidar")
+            run()
             times.append(time.perf_counter() - t)
             n += 1
             if time.perf_counter() - t0 > seconds or n >= 20:
@@ -80,9 +127,9 @@ def cpu_baseline(head_cfg_name, seconds, seed):
     times.sort()
     med = times[len(times) // 2]
     return {"value": round(1.0 / med, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} full CMT-L frames (Nq 900, 32400 BEV tokens, 6 layers, shared_conv + coordinate "
-                      f"encodings + decoder + task heads) through oracle/cmt_oracle.py in fp32 on {threads} host "
-                      f"threads; median frame time {med:.3f} s"}
+            "sample": f"{n} full {workload} frames (Nq 900, memory tokens {'+'.join(map(str, nks))}, 6 layers, "
+                      f"shared_conv + coordinate encodings + decoder + task heads) through oracle/cmt_oracle.py in "
+                      f"fp32 on {threads} host threads; median frame time {med:.3f} s"}
 
 
 def load_traffic():
@@ -106,6 +153,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="lidar", choices=sorted(WORKLOADS),
+                    help="lidar = BASELINE configs[1] (the headline line); fusion / coop = configs[2] / [3] forward")
     args = ap.parse_args()
 
     env = init_dist(args)
@@ -115,13 +164,7 @@ def main():
     native.lib()
     set_precision(args.precision)
 
-    head, cfg, meta = S.build_synthetic_head("cmt_lidar_nus", seed=0, device=dev)
-    x = S.synthetic_bev(1, 180, 180, seed=dp.frame_seed(1, env), device=dev)
-    metas = [dict()]
-
-    def step():
-        return head([x], None, metas)
-
+    head, cfg, step, nks, _ = make_workload(args.workload, seed=dp.frame_seed(0, env), device=dev)
     with torch.no_grad():
         for _ in range(2):
             step()
@@ -147,7 +190,8 @@ def main():
         with region_timer() as rt:
             for _ in range(3):
                 step()
-        attn_ms = rt.mean_ms("cross_attn")
+        attn_ms_all = rt.durations_ms("cross_attn")
+        attn_ms = sum(attn_ms_all) / len(attn_ms_all)
 
         # --- voxel scatter-mean of ~30k points (timed separately)
         vl = SPConvVoxelization(voxel_size=[0.075, 0.075, 0.2], point_cloud_range=[-54.0, -54.0, -5.0, 54.0, 54.0, 3.0],
@@ -164,7 +208,9 @@ def main():
         vox_ms = (time.perf_counter() - tv) / nvox * 1e3
 
     ms_per_step = elapsed / args.steps * 1e3
-    achieved = cross_attn_flops() / (attn_ms * 1e-3) / 1e12
+    # mean algorithmic FLOPs of one cross-attention launch (agents may differ in Nk)
+    flop_launch = sum(cross_attn_flops(nk=nk) for nk in nks) / len(nks)
+    achieved = flop_launch / (attn_ms * 1e-3) / 1e12
     result = {
         "metric": "decoder frames/sec at 900 queries x (BEV+6-cam) tokens; 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -177,23 +223,23 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": {"bf16": "bf16", "fp16": "fp16", "ref": "fp32+fp16attn"}[args.precision],
-        "data": "synthetic (seeded BEV features relu(N(0,1)), random-init weights of the CMT-L head)",
-        "config": {"workload": "CMT-L (LiDAR-only) nuScenes-shape: BEV 512x180x180 (32400 tokens), 900 queries, "
-                               "6-layer decoder, CmtLidarHead forward (shared_conv + encodings + decoder + task "
-                               "heads), batch 1 frame per GPU",
-                   "global_batch": world, "seq_len": NK, "parallelism": f"dp{world}",
+        "data": "synthetic (seeded BEV features relu(N(0,1)), image feats N(0,1) where used, random-init weights "
+                "of the head)",
+        "config": {"workload": WORKLOADS[args.workload][2],
+                   "global_batch": world, "seq_len": sum(nks), "parallelism": f"dp{world}",
                    "graph": graph is not None,
-                   "decoder_gflop_per_frame": round(decoder_frame_flops() / 1e9, 2)},
+                   "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nk=nk) for nk in nks) / 1e9, 2)},
         "roofline": {"kernel": "cmt_attn_fwd (cross-attention core, + split combine)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic() if args.workload == "lidar" else None,
                      "avg_launch_ms": round(attn_ms, 5),
-                     "flop_per_launch": cross_attn_flops()},
+                     "flop_per_launch": flop_launch},
         "voxel_scatter_mean_ms": round(vox_ms, 4),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline("cmt_lidar_nus", args.cpu_seconds, seed=0)
+        result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds,
+                                                seed=dp.frame_seed(0, env))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

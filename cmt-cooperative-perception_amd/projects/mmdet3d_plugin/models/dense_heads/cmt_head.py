@@ -302,6 +302,7 @@ class CmtHead(HeadEngineMixin, nn.Module):
         L = self.transformer.decoder.num_layers
         outs = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=torch.float32,
                            device=self.reference_points.weight.device)
+        self._h2d_seq = 0    # staging-buffer slot of each camera-matrix upload in this forward (engine._h2d)
         for i, (x, x_img, metas) in enumerate(agents):
             flags = native.LN_NAN_TO_NUM | (native.LN_MAX_INTO if i > 0 else 0)
             self._decode_agent(x, x_img, metas, B, outs, flags, self.variant, prec)

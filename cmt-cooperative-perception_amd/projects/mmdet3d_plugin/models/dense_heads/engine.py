@@ -98,6 +98,30 @@ class HeadEngineMixin:
                     bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B,
                     a_bstride=H * W * Cin, c_bstride=Nk * Cout)
 
+    def _h2d(self, arr, dev, tag):
+        """Host camera matrices (fp64 inverse on the host, as the reference) ->
+        fp32 device tensor.  Every eager call also sets up a pinned staging
+        buffer per (tag, shape, upload index in the forward); under HIP-graph capture the values go through
+        that buffer, so the graph holds a host->device copy node that re-reads
+        it on each replay (pinned allocation itself is not capturable, hence
+        the eager warm-up torch's graph capture needs anyway)."""
+        t = torch.from_numpy(np.ascontiguousarray(arr)).float()
+        pool = self.__dict__.setdefault("_pinned_meta", {})
+        seq = self.__dict__.get("_h2d_seq", 0)
+        self._h2d_seq = seq + 1
+        key = (tag, tuple(t.shape), seq)
+        if torch.cuda.is_current_stream_capturing():
+            if key not in pool:
+                raise RuntimeError("camera metas of this shape were never seen eagerly: run one eager forward "
+                                   "before capturing the head in a HIP graph")
+            pool[key].copy_(t)
+            d = torch.empty(t.shape, dtype=t.dtype, device=dev)
+            d.copy_(pool[key], non_blocking=True)
+            return d
+        if key not in pool and dev.type == "cuda":
+            pool[key] = torch.empty(t.shape, dtype=t.dtype).pin_memory()
+        return t.to(dev)
+
     def _bev_pos_into(self, pos, B, Nk, H, W, pk, R=None):
         """bev_pos_embed (cmt_head.py:324-337, 489) into the pos rows of every
         batch element; with R (the memory rows in the compute dtype) the
@@ -119,7 +143,7 @@ class HeadEngineMixin:
         V = BV // B
         pad_h, pad_w, _ = metas[0]["pad_shape"][0]
         i2l = np.concatenate([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64)) for m in metas])
-        i2l = torch.from_numpy(i2l).float().to(pos.device)
+        i2l = self._h2d(i2l, pos.device, "rv_pe.i2l")
         D = self.depth_num
         w0, b0, w2, b2 = pk["rv"]
         cdt = w0.dtype if (3 * D) % 64 == 0 else torch.float32
@@ -146,8 +170,8 @@ class HeadEngineMixin:
             V = len(metas[0]["lidar2img"])
             pad_h, pad_w, _ = metas[0]["pad_shape"][0]
             l2i, i2l = _inv_lidar2img(metas)
-            l2i = torch.from_numpy(l2i).float().to(dev)
-            i2l = torch.from_numpy(i2l).float().to(dev)
+            l2i = self._h2d(l2i, dev, "rv_query.l2i")
+            i2l = self._h2d(i2l, dev, "rv_query.i2l")
             refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
             D = self.depth_num
             coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)   # kernel writes fp32

@@ -195,3 +195,34 @@ def test_full_size_lidar_one_layer(dev):
     # the bench policy on the same full-size frame: ping-pong bounded-max cross-attention,
     # row-block chains, K/V max-norm partials
     _check_bf16(_run(head, dev, "bf16", lambda: head([x.to(dev)], None, [dict()])), refs["fp32"], oc["pc_range"])
+
+
+def test_fusion_head_graph_replay_matches_eager(dev):
+    """The fusion head captured as a HIP graph (camera matrices uploaded from
+    pinned host buffers inside the graph) replays to the eager outputs."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=0, num_query=64, num_layers=2,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=21).to(dev)
+    xi = S.synthetic_img(6, 8, 20, seed=22).to(dev)
+    metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=23)
+    set_precision("bf16")
+    with torch.no_grad():
+        eager = head([x], [xi], metas)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            head([x], [xi], metas)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                static = head([x], [xi], metas)
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+    for k in KEYS:
+        a, b = eager[0][0][k], static[0][0][k]
+        assert torch.equal(a, b), (k, (a - b).abs().max().item())
+    set_precision("ref")
