@@ -337,35 +337,66 @@ __global__ __launch_bounds__(256) void task_head_tail_kernel(TailParams p) {
     float* G = tsm;                                   // [nrows][gs]
     float* W = tsm + nrows * gs;                      // [out_total * k][ws]
     const float* Gsrc = p.G + ((int64_t)l * p.B + b) * p.Nq * width;
-    for (int i = threadIdx.x; i < nrows * width / 4; i += blockDim.x) {
-        const int r = (i * 4) / width, c = (i * 4) - r * width;
-        const int q = q0 - half + r;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (q >= 0 && q < p.Nq) v = *(const f32x4*)(Gsrc + (int64_t)q * width + c);
-        *(f32x4*)(G + r * gs + c) = v;
-    }
-    const int wrows = p.out_total * p.k;
-    const float* Wsrc = p.W2 + (int64_t)l * wrows * p.hc;
-    for (int i = threadIdx.x; i < wrows * p.hc / 4; i += blockDim.x) {
-        const int r = (i * 4) / p.hc, c = (i * 4) - r * p.hc;
-        *(f32x4*)(W + r * ws + c) = *(const f32x4*)(Wsrc + 4 * i);
+    const float* Wsrc = p.W2 + (int64_t)l * p.out_total * p.k * p.hc;
+    // staging: batches of 8 independent 16-B loads per thread before their LDS stores
+    const int ng = nrows * width / 4, nw = p.out_total * p.k * p.hc / 4;
+    for (int i0 = 0; i0 < ng + nw; i0 += 8 * 256) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + threadIdx.x;
+            v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (i < ng) {
+                const int r = (i * 4) / width, c = (i * 4) - r * width;
+                const int q = q0 - half + r;
+                if (q >= 0 && q < p.Nq) v[u] = *(const f32x4*)(Gsrc + (int64_t)q * width + c);
+            } else if (i < ng + nw) {
+                v[u] = *(const f32x4*)(Wsrc + 4 * (i - ng));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + threadIdx.x;
+            if (i < ng) {
+                const int r = (i * 4) / width, c = (i * 4) - r * width;
+                *(f32x4*)(G + r * gs + c) = v[u];
+            } else if (i < ng + nw) {
+                const int r = ((i - ng) * 4) / p.hc, c = ((i - ng) * 4) - r * p.hc;
+                *(f32x4*)(W + r * ws + c) = v[u];
+            }
+        }
     }
     __syncthreads();
     {
+        // GroupLayerNorm1d + ReLU: 16 lanes per (row, head) group, 4 channels per lane
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int sub = lane >> 4, j = lane & 15;
+        const int ngroups = nrows * p.nheads;
         const float* w = p.gw + (int64_t)l * width;
         const float* bb = p.gb + (int64_t)l * width;
-        for (int g = wave; g < nrows * p.nheads; g += blockDim.x >> 6) {
+        for (int g0 = wave * 4; g0 < ngroups; g0 += 16) {
+            const int g = g0 + sub;
             const int r = g / p.nheads, hd = g - r * p.nheads;
             const int q = q0 - half + r;
-            if (q < 0 || q >= p.Nq) continue;         // zero pad of conv #2's input
-            const int c = hd * 64 + lane;
-            const float v = G[r * gs + c];
-            const float mu = wave_sum(v) / 64.f;
-            const float d = v - mu;
-            const float var = wave_sum(d * d) / 64.f;
-            const float y = w[c] * (d / sqrtf(var + 1e-6f)) + bb[c];
-            G[r * gs + c] = fmaxf(y, 0.f);
+            const bool ok = g < ngroups && q >= 0 && q < p.Nq;   // rows outside [0, Nq) stay 0 (conv #2 pad)
+            const int c = hd * 64 + 4 * j;
+            f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            if (ok) x = *(const f32x4*)(G + r * gs + c);
+            float s = (x[0] + x[1]) + (x[2] + x[3]);
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off);
+            const float mu = s / 64.f;
+            const f32x4 d = {x[0] - mu, x[1] - mu, x[2] - mu, x[3] - mu};
+            float v2 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) v2 += __shfl_xor(v2, off);
+            const float inv = 1.f / sqrtf(v2 / 64.f + 1e-6f);
+            if (ok) {
+                f32x4 y;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[e] = fmaxf(w[c + e] * (d[e] * inv) + bb[c + e], 0.f);
+                *(f32x4*)(G + r * gs + c) = y;
+            }
         }
     }
     __syncthreads();

@@ -427,6 +427,15 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
         if (g == 0) {
             store_row32(a.Y, row, e.wave, e.lh, y);
             store_row32(a.OUT, row, e.wave, e.lh, v);
+            if (a.OUT16) {
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int gg = 0; gg < 4; ++gg)
+                        *(t4*)((T*)a.OUT16 + (int64_t)row * CE + e.col(nt, 4 * gg)) =
+                            t4{(T)v[nt * 16 + 4 * gg], (T)v[nt * 16 + 4 * gg + 1], (T)v[nt * 16 + 4 * gg + 2],
+                               (T)v[nt * 16 + 4 * gg + 3]};
+            }
         }
         if (has_next) {
             const int b = row / a.Nq, rr = row - b * a.Nq;
@@ -456,10 +465,12 @@ extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
     if (a.kind == 2) {
         CMT_REQUIRE(a.WS && a.OUT, "cmt_chain: chain B2 needs WS and OUT");
         CMT_REQUIRE(a.Wn == nullptr || (a.P && a.Q), "cmt_chain: chain B2 with Wn needs P and Q");
+    } else {
+        CMT_REQUIRE(a.OUT16 == nullptr, "cmt_chain: OUT16 is a chain B2 output");
     }
     CMT_REQUIRE(((uintptr_t)a.X | (uintptr_t)a.prm | (uintptr_t)a.Wo | (uintptr_t)a.W1 | (uintptr_t)a.W2 |
                  (uintptr_t)a.Wn | (uintptr_t)a.P | (uintptr_t)a.Y | (uintptr_t)a.R | (uintptr_t)a.OUT |
-                 (uintptr_t)a.WS | (uintptr_t)a.Q) % 16 == 0,
+                 (uintptr_t)a.WS | (uintptr_t)a.Q) % 16 == 0 && (uintptr_t)a.OUT16 % 8 == 0,
                 "cmt_chain: buffers must be 16-byte aligned");
     hipStream_t s = (hipStream_t)stream;
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);

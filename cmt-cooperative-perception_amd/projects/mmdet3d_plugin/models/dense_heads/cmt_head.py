@@ -302,11 +302,14 @@ class CmtHead(HeadEngineMixin, nn.Module):
         L = self.transformer.decoder.num_layers
         outs = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=torch.float32,
                            device=self.reference_points.weight.device)
+        outs16 = None
+        if prec.gemm != torch.float32:
+            outs16 = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=prec.gemm, device=outs.device)
         self._h2d_seq = 0    # staging-buffer slot of each camera-matrix upload in this forward (engine._h2d)
         for i, (x, x_img, metas) in enumerate(agents):
             flags = native.LN_NAN_TO_NUM | (native.LN_MAX_INTO if i > 0 else 0)
-            self._decode_agent(x, x_img, metas, B, outs, flags, self.variant, prec)
-        return self._task_outputs(outs, B, prec)
+            self._decode_agent(x, x_img, metas, B, outs, flags, self.variant, prec, out16=outs16)
+        return self._task_outputs(outs, B, prec, outs16)
 
     def forward_single(self, x, x_img, img_metas):
         B = x.shape[0] if x is not None else len(img_metas)

@@ -183,11 +183,12 @@ class HeadEngineMixin:
         return qpos
 
     # ------------------------------------------------------------------ per agent
-    def _decode_agent(self, x, x_img, metas, B, out, post_flags, variant, prec):
+    def _decode_agent(self, x, x_img, metas, B, out, post_flags, variant, prec, out16=None):
         """One get_outs_dec (cmt_head_coop.py:341-360) / the decoder part of
         forward_single (cmt_head.py:481-499); writes post-normed, nan_to_num'ed
         decoder outputs [L, B*Nq, C] into ``out`` (max-merged when post_flags
-        has LN_MAX_INTO)."""
+        has LN_MAX_INTO); ``out16`` receives the same values in the compute
+        dtype (f16/bf16 policy)."""
         pk = self._engine_pack(prec)
         C = self.hidden_dim
         dev = self.reference_points.weight.device
@@ -219,12 +220,16 @@ class HeadEngineMixin:
         qpos = self._query_pos(B, metas, use_img, pk)
         Nq = self.num_query
         self.transformer.decoder.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
-                                          prec=prec, kv_operands=(mem, pos) if lowp else None)
+                                          prec=prec, kv_operands=(mem, pos) if lowp else None,
+                                          out16=out16 if lowp else None)
         return out
 
     # ------------------------------------------------------------------ task heads
-    def _task_outputs(self, outs_dec, B, prec):
-        """SeparateTaskHead for every task + box epilogue.  outs_dec [L, B*Nq, C]."""
+    def _task_outputs(self, outs_dec, B, prec, outs16=None):
+        """SeparateTaskHead for every task + box epilogue.  outs_dec [L, B*Nq, C]
+        fp32; ``outs16`` (optional) the same in the compute dtype, read by the
+        first grouped conv's GEMM directly (LDS-DMA path) instead of
+        converting fp32 on load -- the same bf16/f16 rounding either way."""
         L = outs_dec.shape[0]
         Nq = self.num_query
         C = self.hidden_dim
@@ -236,7 +241,8 @@ class HeadEngineMixin:
             nh, k = len(tp["names"]), tp["k"]
             width = nh * 64
             H1 = torch.empty((L, B * Nq, width), dtype=torch.float32, device=outs_dec.device)
-            native.gemm(outs_dec, tp["w1"], H1, M=B * Nq, N=width, K=k * C, lda=C, ldw=k * C, ldc=width, batch=L,
+            A = outs16 if outs16 is not None and outs16.dtype == tp["w1"].dtype else outs_dec
+            native.gemm(A, tp["w1"], H1, M=B * Nq, N=width, K=k * C, lda=C, ldw=k * C, ldc=width, batch=L,
                         a_bstride=B * Nq * C, w_bstride=width * k * C, c_bstride=B * Nq * width,
                         a_mode=native.A_CONV1D3 if k == 3 else native.A_ROWS, seg_len=Nq)
             OUT = torch.empty((L, B, Nq, tp["out_total"]), dtype=torch.float32, device=outs_dec.device)

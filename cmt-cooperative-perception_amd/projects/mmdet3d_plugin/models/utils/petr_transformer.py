@@ -407,19 +407,20 @@ class PETRTransformerDecoder(nn.Module):
         return self._pack.get("decoder", params, prec.name, build)
 
     def run_rows(self, mem, pos, qpos, *, B, Nk, Nq, out=None, post_flags=native.LN_NAN_TO_NUM, prec=None,
-                 tgt0=None, kv_operands=None):
+                 tgt0=None, kv_operands=None, out16=None):
         """Fused decoder.  mem/pos: [B*Nk, C] fp32 batch-major rows, qpos:
         [B*Nq, C] fp32.  Writes the post-normed layer outputs to
         out [L, B*Nq, C] (fp32) with ``post_flags`` (nan_to_num / max-into).
         Under an f16/bf16 policy the producers may hand over the K/V GEMM
         operands already in the compute dtype: kv_operands = (lowp(mem),
-        lowp(mem + pos)); mem/pos are then unused."""
+        lowp(mem + pos)); mem/pos are then unused.  ``out16`` (f16/bf16 policy
+        only): a compute-dtype copy of ``out`` for the task-head GEMM."""
         if not self.fused_supported():
             raise NotImplementedError("fused decoder supports the CMT post-norm layout (C=256, 8x32 heads)")
         prec = get_precision(prec)
         if prec.gemm != torch.float32:
             return self._run_rows_lowp(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
-                                       tgt0=tgt0, kv_operands=kv_operands)
+                                       tgt0=tgt0, kv_operands=kv_operands, out16=out16)
         pk = self.packed(prec)
         L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
         dev = mem.device
@@ -478,7 +479,7 @@ class PETRTransformerDecoder(nn.Module):
                              ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         return out
 
-    def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands):
+    def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands, out16=None):
         """run_rows under an f16/bf16 policy: every GEMM operand is produced in
         the compute dtype by the kernel before it (LayerNorm writes lowp(y) and
         lowp(y + query_pos) beside the fp32 residual stream, attention writes
@@ -559,7 +560,7 @@ class PETRTransformerDecoder(nn.Module):
                              R=t1n, W2=lw["f2_w"], WS=cws)
                 native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                              Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
-                             Q=qkv if nxt is not None else None, WS=cws)
+                             Q=qkv if nxt is not None else None, WS=cws, OUT16=out16)
             return out
         # out-projection / fc2 GEMMs fused with their residual + LayerNorm (cmt_gemm_ln)
         fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "0") == "1"
@@ -610,4 +611,6 @@ class PETRTransformerDecoder(nn.Module):
                             ldr=C)
                 native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
                                     W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
+        if out16 is not None:
+            native.cast(out, out16)
         return out

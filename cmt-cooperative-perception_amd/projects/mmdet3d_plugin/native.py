@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -63,7 +63,8 @@ class ChainArgs(ctypes.Structure):
     _fields_ = [("kind", _int), ("rows", _int), ("Nq", _int), ("dtype", _int), ("eps", _flt),
                 ("X", _vp), ("R", _vp), ("P", _vp), ("prm", _vp),
                 ("Wo", _vp), ("W1", _vp), ("W2", _vp), ("Wn", _vp),
-                ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp), ("WS", _vp)]
+                ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp), ("WS", _vp),
+                ("OUT16", _vp)]
 
 
 class LnArgs(ctypes.Structure):
@@ -354,17 +355,19 @@ def chain_ws_numel(rows):
 
 
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
-          out_flags=0, Q=None, WS=None):
+          out_flags=0, Q=None, WS=None, OUT16=None):
     """One row-block chain of a decoder layer's query side (cmt_chain): kind 0
     after self-attention; kinds 1 then 2 after cross-attention (cmt_hip.h)."""
-    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS)
+    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16)
+    if OUT16 is not None and (OUT is None or OUT16.dtype not in (torch.float16, torch.bfloat16)):
+        raise RuntimeError("cmt_chain: OUT16 must be a 16-bit copy target beside OUT")
     if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:
         raise RuntimeError(f"cmt_chain: parameter block must be {CHAIN_PRM[kind]} fp32 values")
     if WS is not None and (WS.dtype != torch.float32 or WS.numel() < chain_ws_numel(rows)):
         raise RuntimeError("cmt_chain: WS must hold 4 * rows * 256 fp32")
     a = ChainArgs()
     a.kind, a.rows, a.Nq, a.eps = kind, rows, Nq, eps
-    lowp = next((t for t in (X, Q, Wn, Wo) if t is not None), None)
+    lowp = next((t for t in (X, Q, Wn, Wo, OUT16) if t is not None), None)
     a.dtype = DT[lowp.dtype] if lowp is not None else BF16   # B2 without in_proj: no 16-bit operand
 
     def ptr(t):
@@ -376,6 +379,7 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     a.out_flags = out_flags
     a.Q = ptr(Q)
     a.WS = ptr(WS)
+    a.OUT16 = None if OUT16 is None else OUT16.data_ptr() + 2 * out_offset
     _check(lib().cmt_chain(ctypes.byref(a), _stream()), "cmt_chain")
 
 

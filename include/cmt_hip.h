@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 3
+#define CMT_ABI_VERSION 4
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -238,6 +238,7 @@ typedef struct cmt_chain_args {
     float* OUT; int out_flags; /* B2: layer output [rows][256] fp32 */
     void* Q;                   /* head-split projection output (A; B2 with Wn) */
     float* WS;                 /* B1 / B2: partials workspace [4][rows][256] fp32 */
+    void* OUT16;               /* B2 (optional): the layer output again in dtype (the task-head GEMM operand) */
 } cmt_chain_args;
 int cmt_chain(const cmt_chain_args* args, void* stream);
 

@@ -566,13 +566,15 @@ def test_chain_b(N, dev, dt, B, Nq, last, flags):
     Y = torch.empty(rows, C, device=dev)
     old = torch.randn(rows, C, generator=g)
     OUT = old.clone().to(dev)
+    OUT16 = torch.full(OUT.shape, float("nan"), dtype=dt, device=dev)
     QKV = torch.empty(B * 24 * Nq * 32, dtype=dt, device=dev)
     WS = torch.full((N.chain_ws_numel(rows),), float("nan"), device=dev)
     prm_d = prm.to(dev)
     N.chain(1, X.to(dev), None, prm_d, Wo.to(dev), W1.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
             R=R.to(dev), W2=W2.to(dev), WS=WS)
     N.chain(2, None, None if last else P.to(dev), prm_d, None, None, Y, rows=rows, Nq=Nq, eps=1e-5,
-            Wn=None if last else Wn.to(dev), OUT=OUT, out_flags=flags, Q=None if last else QKV, WS=WS)
+            Wn=None if last else Wn.to(dev), OUT=OUT, out_flags=flags, Q=None if last else QKV, WS=WS,
+            OUT16=OUT16)
     d = lambda t: t.double()
     o = _ln64(d(X) @ d(Wo).T + d(bo) + d(R), d(l1w), d(l1b))
     h = torch.relu(d(o.to(dt)) @ d(W1).T + d(b1)).to(dt)
@@ -582,6 +584,7 @@ def test_chain_b(N, dev, dt, B, Nq, last, flags):
         out = torch.maximum(out, d(old))
     assert (Y.cpu().double() - y).abs().max().item() < 2e-2
     assert (OUT.cpu().double() - out).abs().max().item() < 2e-2
+    assert torch.equal(OUT16, OUT.to(dt))      # the 16-bit copy is the rounded fp32 output
     if not last:
         qk = d((y + d(P)).to(dt)) @ d(Wn[:2 * C]).T + d(bn[:2 * C])
         vv = d(y.to(dt)) @ d(Wn[2 * C:]).T + d(bn[2 * C:])
