@@ -122,7 +122,8 @@ def main():
         gemm_case("kv (all layers, pos add)", 32400, 3072, 256, bf, A2_cols=1536, out_dt=bf, headsplit=32400)
         gemm_case("bev mlp fc1 (relu)", 32400, 256, 512, bf, relu=True)
         gemm_case("bev mlp fc2", 32400, 256, 256, bf)
-        gemm_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, bf, a_f32=False, conv=(180, 180, 512), relu=True)
+        gemm_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, bf, a_f32=False, conv=(180, 180, 512), relu=True,
+                  out_dt=bf)
         gemm_case("self qkv (pos add)", 900, 768, 256, bf, A2_cols=512, out_dt=bf, headsplit=900)
         gemm_case("out proj (+res)", 900, 256, 256, bf, R=True)
         gemm_case("cross q (pos add)", 900, 256, 256, bf, A2_cols=256, out_dt=bf, headsplit=900)
