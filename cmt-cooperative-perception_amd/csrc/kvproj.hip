@@ -161,14 +161,12 @@ __device__ __forceinline__ void kv_sweep(const cmt_gemm_args& a, const char* lds
 template <typename T>
 __global__ __launch_bounds__(KP_NT, 1) void kvproj_kernel(cmt_gemm_args a, int parts) {
     typedef typename mfma_traits<T>::frag frag;
-    typedef T t4 __attribute__((ext_vector_type(4)));
     // 64 KB A tile | 4 x 4 KB per-wave store staging | the part's bias (<= 8 KB)
     __shared__ __attribute__((aligned(16))) char lds[KP_BM * KP_K * 2 + 4 * 4096 + KP_MAXB * 4];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lr = lane & 31, lh = lane >> 5;
     // workgroup -> (row tile, column part); the parts of one row tile are
     // consecutive blocks (their A tiles differ only in A vs A2)
     const int rt = blockIdx.x / parts, part = blockIdx.x - rt * parts;

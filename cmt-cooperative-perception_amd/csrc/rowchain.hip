@@ -212,6 +212,29 @@ __device__ __forceinline__ void store_row32(float* M, int row, int wave, int lh,
                 f32x4{v[nt * 16 + 4 * g], v[nt * 16 + 4 * g + 1], v[nt * 16 + 4 * g + 2], v[nt * 16 + 4 * g + 3]};
 }
 
+// The B1 -> B2 partials workspace is private to the chains, so it is kept in
+// the lanes' own order: per (plane, row block, wave, 16-byte group j = nt*4+g)
+// one contiguous 1 KB slab, lane-major.  Every wave instruction then moves 1 KB
+// of consecutive bytes (8 cache lines) instead of 32-byte pieces of 32 rows
+// (32 lines), which is what bounded chain B2 (~9 us for one workgroup).
+__device__ __forceinline__ void load_tile32(const float* M, int rb, int wave, int lane, float (&v)[32]) {
+    const float* p = M + (int64_t)rb * RB * CE + wave * 2048 + lane * 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const f32x4 x = *(const f32x4*)(p + j * 256);
+        v[4 * j] = x[0];
+        v[4 * j + 1] = x[1];
+        v[4 * j + 2] = x[2];
+        v[4 * j + 3] = x[3];
+    }
+}
+
+__device__ __forceinline__ void store_tile32(float* M, int rb, int wave, int lane, const float (&v)[32]) {
+    float* p = M + (int64_t)rb * RB * CE + wave * 2048 + lane * 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *(f32x4*)(p + j * 256) = f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+}
+
 template <typename T>
 __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     typedef T t4 __attribute__((ext_vector_type(4)));
@@ -249,17 +272,17 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     char* actA = lds + OFF_ACT_A;
     char* actB = lds + OFF_ACT_B;
     float* ws = (float*)a.WS;
-    const int64_t plane = (int64_t)a.rows * CE;
+    const int64_t plane = (int64_t)((a.rows + RB - 1) / RB) * RB * CE;   // one partial in tile order
 
     // ---- prologue: every ordinary load and the first LDS-DMAs, then one full wait
     float res[32], qp[32], oold[32];
     if (kind == 2) {
         // the FFN output + residual: sum of the four B1 partials
         float t[32];
-        load_row32(ws, row, e.wave, e.lh, res);
+        load_tile32(ws, rb, e.wave, e.lane, res);
 #pragma unroll
         for (int p = 1; p < 4; ++p) {
-            load_row32(ws + p * plane, row, e.wave, e.lh, t);
+            load_tile32(ws + p * plane, rb, e.wave, e.lane, t);
 #pragma unroll
             for (int i = 0; i < 32; ++i) res[i] += t[i];
         }
@@ -385,7 +408,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                 if (g == 0) x += b2[e.col(nt, r)] + v[nt * 16 + r];
                 v[nt * 16 + r] = x;
             }
-        if (row_ok) store_row32(ws + g * plane, row, e.wave, e.lh, v);
+        store_tile32(ws + g * plane, rb, e.wave, e.lane, v);     // whole row block (clamped rows too)
         return;
     }
 

@@ -350,8 +350,9 @@ CHAIN_PRM = {0: 1024, 1: 3840, 2: 3840}
 
 
 def chain_ws_numel(rows):
-    """fp32 elements of the chain B1 -> B2 partials workspace."""
-    return 4 * rows * 256
+    """fp32 elements of the chain B1 -> B2 partials workspace (4 partials of
+    whole 32-row blocks, in the chains' private tile order)."""
+    return 4 * ((rows + 31) // 32) * 32 * 256
 
 
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
@@ -364,7 +365,7 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:
         raise RuntimeError(f"cmt_chain: parameter block must be {CHAIN_PRM[kind]} fp32 values")
     if WS is not None and (WS.dtype != torch.float32 or WS.numel() < chain_ws_numel(rows)):
-        raise RuntimeError("cmt_chain: WS must hold 4 * rows * 256 fp32")
+        raise RuntimeError("cmt_chain: WS must hold chain_ws_numel(rows) fp32")
     a = ChainArgs()
     a.kind, a.rows, a.Nq, a.eps = kind, rows, Nq, eps
     lowp = next((t for t in (X, Q, Wn, Wo, OUT16) if t is not None), None)

@@ -1,7 +1,7 @@
 """Per-kernel microbenchmark of libcmt_hip.so at the CMT-L frame's shapes
 (HIP events on the launching stream, median of N launches).
 
-    python cmt-cooperative-perception_amd/tools/bench_kernels.py [--only gemm|attn|misc]
+    python cmt-cooperative-perception_amd/tools/bench_kernels.py [--only gemm|attn|attn_sweep|chain|misc]
 """
 import argparse
 import math
@@ -164,6 +164,17 @@ def main():
         attn_case("self 900x900", 900, 900, bf, fold=True)
         attn_case("self f32", 900, 900, torch.float32)
         attn_case("cross fusion 900x56400", 900, 56400, bf)
+    if args.only == "chain_sweep":
+        for rows in (32, 288, 900, 1800, 3600):
+            chain_case(2, rows=rows, Nq=rows, last=True)
+            chain_case(2, rows=rows, Nq=rows)
+            chain_case(0, rows=rows, Nq=rows)
+    if args.only == "attn_sweep":
+        # split-count sweep at the decoder's shapes (0 = the library's choice)
+        for s in (0, 1, 2, 3, 4, 6, 8):
+            attn_case("self 900x900", 900, 900, bf, splits=s, fold=True)
+        for s in (0, 4, 6, 8, 12, 16):
+            attn_case("cross 900x32400", 900, 32400, bf, splits=s, fold=True)
 
 
 if __name__ == "__main__":

@@ -237,7 +237,7 @@ typedef struct cmt_chain_args {
     float* Y;                  /* A: norms[0] output; B2: norms[2] output; [rows][256] fp32 */
     float* OUT; int out_flags; /* B2: layer output [rows][256] fp32 */
     void* Q;                   /* head-split projection output (A; B2 with Wn) */
-    float* WS;                 /* B1 / B2: partials workspace [4][rows][256] fp32 */
+    float* WS;                 /* B1 / B2: partials workspace, 4 * ceil(rows/32) * 32 * 256 fp32 (private order) */
     void* OUT16;               /* B2 (optional): the layer output again in dtype (the task-head GEMM operand) */
 } cmt_chain_args;
 int cmt_chain(const cmt_chain_args* args, void* stream);
