@@ -123,11 +123,13 @@ __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict_
                                                         int F, int mode, int x_size, int y_size, OT* out,
                                                         int64_t ldo) {
     // one thread = 8 consecutive outputs (4 sin/cos pairs sharing an argument)
-    const int groups = (2 * F) >> 3;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)n * groups) return;
+    // 32-bit index math (the host checks n * groups < 2^31): a 64-bit division
+    // per thread was most of this kernel's VALU time
+    const unsigned groups = (unsigned)(2 * F) >> 3;
+    const unsigned idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (unsigned)n * groups) return;
     const int i = (int)(idx / groups);
-    const int f0 = (int)(idx - (int64_t)i * groups) * 8;
+    const int f0 = (int)(idx - (unsigned)i * groups) * 8;
     float px, py;
     if (pos == nullptr) {
         // coords_bev: token t = r * y_size + c  ->  x = (c+0.5)/x_size, y = (r+0.5)/y_size
@@ -147,9 +149,13 @@ __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict_
     const float p = (f0 < F ? py : px) * scale;   // first F outputs embed y, the next F embed x
     const int j0 = f0 < F ? f0 : f0 - F;
     float o[8];
+    // 2k / F is exact as 2k * (1/F) when F is a power of two (every CMT config)
+    const bool f_pow2 = (F & (F - 1)) == 0;
+    const float inv_f = 1.f / (float)F;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const float dim_t = 2.f * (float)((j0 >> 1) + t) / (float)F + 1.f;
+        const float two_k = 2.f * (float)((j0 >> 1) + t);
+        const float dim_t = (f_pow2 ? two_k * inv_f : two_k / (float)F) + 1.f;
         const float v = p / dim_t;                 // |v| <= 2*pi: v_sin/v_cos are accurate here
         o[2 * t] = __sinf(v);
         o[2 * t + 1] = __cosf(v);
@@ -496,6 +502,7 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
     CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_pos2embed: bad odtype");
     if (n == 0) return 0;
     const int64_t total = (int64_t)n * (2 * F / 8);
+    CMT_REQUIRE(total < ((int64_t)1 << 31), "cmt_pos2embed: n * F too large for one launch");
     hipStream_t s = (hipStream_t)stream;
     if (odtype == CMT_F32)
         pos2embed_kernel<float><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
