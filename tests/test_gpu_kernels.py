@@ -591,3 +591,20 @@ def test_chain_b(N, dev, dt, B, Nq, last, flags):
         ref = torch.cat([qk, vv], 1).view(B, Nq, 24, 32).permute(0, 2, 1, 3).reshape(-1)
         rel = (QKV.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
         assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nb,nv,C,HW,off", [(1, 1, 512, 32400, 0), (2, 3, 128, 100, 7), (1, 2, 64, 4, 3),
+                                            (1, 1, 96, 44, 0)])
+def test_nchw_to_rows_layouts(N, dev, dt, nb, nv, C, HW, off):
+    """NCHW fp32 -> batch-major rows (vector path when HW % 4 == 0 and C % 64 == 0,
+    scalar path otherwise): exact against permute + cast, gap rows untouched."""
+    g = torch.Generator().manual_seed(HW + C)
+    x = torch.randn(nb * nv, C, HW, generator=g)
+    rpb = off + nv * HW + 5
+    y = torch.full((nb * rpb, C), float("nan"), dtype=dt, device=dev)
+    N.nchw_to_rows(x.to(dev), y, nb=nb, nv=nv, C=C, HW=HW, ldy=C, rows_per_batch=rpb, row_offset=off)
+    ref = x.view(nb, nv, C, HW).permute(0, 1, 3, 2).reshape(nb, nv * HW, C).to(dt)
+    got = y.view(nb, rpb, C).cpu()
+    assert torch.equal(got[:, off:off + nv * HW], ref)
+    assert torch.isnan(got[:, :off].float()).all() and torch.isnan(got[:, off + nv * HW:].float()).all()
