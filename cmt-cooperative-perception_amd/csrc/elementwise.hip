@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void add_cast_kernel(const float* __restrict__
                                                        int64_t n4, LT* Yl, LT* Yp) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
-    const f32x4 x = ((const f32x4*)X)[i];
+    const f32x4 x = X ? ((const f32x4*)X)[i] : f32x4{0.f, 0.f, 0.f, 0.f};   // X == NULL: zeros
     typedef LT l4 __attribute__((ext_vector_type(4)));
     if (Yl) ((l4*)Yl)[i] = l4{(LT)x[0], (LT)x[1], (LT)x[2], (LT)x[3]};
     if (Yp) {
@@ -535,7 +535,7 @@ extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const
 
 extern "C" int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,
                             void* stream) {
-    CMT_REQUIRE(X && rows >= 0 && C % 4 == 0 && (Yp == nullptr || P), "cmt_add_cast: bad arguments");
+    CMT_REQUIRE(rows >= 0 && C % 4 == 0 && (Yp == nullptr || P), "cmt_add_cast: bad arguments");
     CMT_REQUIRE(lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16, "cmt_add_cast: lowp_dtype must be f16 or bf16");
     const int64_t n4 = (int64_t)rows * C / 4;
     if (n4 == 0) return 0;

@@ -514,11 +514,20 @@ class PETRTransformerDecoder(nn.Module):
         else:
             native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
                         A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
-        # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114)
-        tgt = tgt0.clone() if tgt0 is not None else torch.zeros((rows, C), dtype=f32, device=dev)
+        # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114).
+        # The chains never read the layer-0 target (chain A's residual is None), so there
+        # it is only an output buffer and the first operands come from add_cast's zeros.
+        use_chain = self._chain_ok() and os.environ.get("CMT_CHAIN", "1") != "0"
+        if tgt0 is not None:
+            tgt = tgt0.clone()
+        elif use_chain:
+            tgt = torch.empty((rows, C), dtype=f32, device=dev)
+        else:
+            tgt = torch.zeros((rows, C), dtype=f32, device=dev)
         tl = torch.empty((rows, C), dtype=lp, device=dev)          # lowp(tgt)
         tp = torch.empty_like(tl)                                  # lowp(tgt + qpos)
-        native.add_cast(tgt, rows=rows, C=C, Yl=tl, Yp=tp, P=qpos)
+        native.add_cast(tgt if (tgt0 is not None or not use_chain) else None, rows=rows, C=C, Yl=tl, Yp=tp,
+                        P=qpos)
         qkv = torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=dev)
         qc = torch.empty((B * C * Nq,), dtype=prec.attn, device=dev)
         ob = torch.empty((rows, C), dtype=lp, device=dev)          # attention output (out-proj operand)
@@ -531,7 +540,7 @@ class PETRTransformerDecoder(nn.Module):
                        native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
         ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
         pw, pb, _pe = pk["post"]
-        if self._chain_ok() and os.environ.get("CMT_CHAIN", "1") != "0":
+        if use_chain:
             # per layer: self-attn core, chain A (out_proj + norms[0] + cross Q proj),
             # cross-attn core, chain B1 (out_proj + norms[1] + FFN quarter -> fp32 partials),
             # chain B2 (partials -> norms[2] + post_norm + next layer's in_proj) -- see rowchain.hip

@@ -385,9 +385,10 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
 
 
 def add_cast(X, *, rows, C, Yl=None, Yp=None, P=None):
+    """Yl = lowp(X), Yp = lowp(X + P); X None = zeros."""
     _dev(X, Yl, Yp, P)
     low = Yl if Yl is not None else Yp
-    _check(lib().cmt_add_cast(X.data_ptr(), _p(P), rows, C, DT[low.dtype], _p(Yl), _p(Yp), _stream()),
+    _check(lib().cmt_add_cast(_p(X), _p(P), rows, C, DT[low.dtype], _p(Yl), _p(Yp), _stream()),
            "cmt_add_cast")
 
 

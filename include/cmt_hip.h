@@ -243,7 +243,8 @@ typedef struct cmt_chain_args {
 int cmt_chain(const cmt_chain_args* args, void* stream);
 
 /* cmt_add_cast: Yl = lowp(X), Yp = lowp(X + P) over rows x C (either output
- * may be NULL) -- the decoder's first-layer operands from the initial target. */
+ * may be NULL; X == NULL reads zeros, the zero target of cmt_transformer.py:114)
+ * -- the decoder's first-layer operands from the initial target. */
 int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,
                  void* stream);
 
