@@ -178,6 +178,13 @@ class HeadEngineMixin:
             mask = torch.empty((B * V * Nq,), dtype=torch.float32, device=dev)
             native.rv_query_coords(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
                                    pad_w=float(pad_w), pc_range=self.pc_range)
+            w0 = pk["rv"][0]
+            if w0.dtype != torch.float32 and (3 * D) % 64 == 0:
+                # compute-dtype operand (the same RNE rounding the GEMM would apply on load):
+                # both MLP GEMMs then run on the LDS-DMA path
+                c16 = torch.empty(coords.shape, dtype=w0.dtype, device=dev)
+                native.cast(coords, c16)
+                coords = c16
             r = self._mlp(coords, pk["rv"])
             native.masked_view_sum(r, mask, qpos, B=B, V=V, Nq=Nq, C=C)
         return qpos
