@@ -137,13 +137,19 @@ class HeadEngineMixin:
         native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
         self._mlp(pe, pk["bev"], pos, batch=B, a_bstride=0, c_bstride=Nk * C, M=H * W, R=R)
 
-    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None):
+    def _cams(self, metas, dev):
+        """(lidar2img, inv(lidar2img)) of every camera as [B, V, 4, 4] fp32 device
+        views of ONE upload (fp64 host inverse, cmt_head.py:428, 441-444)."""
+        l2i, i2l = _inv_lidar2img(metas)
+        both = self._h2d(np.stack([l2i, i2l]), dev, "cams")
+        return both[0], both[1]
+
+    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None, cams=None):
         C = self.hidden_dim
         BV, _, h, w = x_img.shape
         V = BV // B
         pad_h, pad_w, _ = metas[0]["pad_shape"][0]
-        i2l = np.concatenate([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64)) for m in metas])
-        i2l = self._h2d(i2l, pos.device, "rv_pe.i2l")
+        i2l = (cams if cams is not None else self._cams(metas, pos.device))[1]
         D = self.depth_num
         w0, b0, w2, b2 = pk["rv"]
         cdt = w0.dtype if (3 * D) % 64 == 0 else torch.float32
@@ -157,7 +163,7 @@ class HeadEngineMixin:
                     R=R, ldr=C if R is not None else 0, r_bstride=Nk * C if R is not None else 0,
                     r_offset=offset * C)
 
-    def _query_pos(self, B, metas, with_rv, pk):
+    def _query_pos(self, B, metas, with_rv, pk, cams=None):
         C = self.hidden_dim
         ref = self.reference_points.weight.detach().contiguous()
         Nq = ref.shape[0]
@@ -169,9 +175,7 @@ class HeadEngineMixin:
         if with_rv:
             V = len(metas[0]["lidar2img"])
             pad_h, pad_w, _ = metas[0]["pad_shape"][0]
-            l2i, i2l = _inv_lidar2img(metas)
-            l2i = self._h2d(l2i, dev, "rv_query.l2i")
-            i2l = self._h2d(i2l, dev, "rv_query.i2l")
+            l2i, i2l = cams if cams is not None else self._cams(metas, dev)
             refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
             D = self.depth_num
             coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)   # kernel writes fp32
@@ -217,14 +221,15 @@ class HeadEngineMixin:
         mem = torch.empty((B * Nk, C), dtype=mdt, device=dev)
         pos = torch.empty((B * Nk, C), dtype=mdt, device=dev)
         R = mem if lowp else None
+        cams = self._cams(metas, dev) if use_img else None
         if use_bev:
             self._shared_conv_into(x, mem, Nk, pk, prec)
             self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
         if use_img:
             native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C, rows_per_batch=Nk,
                                 row_offset=HW)
-            self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R)
-        qpos = self._query_pos(B, metas, use_img, pk)
+            self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R, cams=cams)
+        qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
         Nq = self.num_query
         self.transformer.decoder.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
                                           prec=prec, kv_operands=(mem, pos) if lowp else None,
