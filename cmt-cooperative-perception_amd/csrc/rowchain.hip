@@ -132,6 +132,40 @@ struct Eng {
         }
     }
 
+    // chain B2's single sub-GEMM: each wave owns weight rows [64 wave, 64 wave + 64) of its
+    // in_proj block, so its fragments come from global memory straight into registers (all
+    // issued in the prologue) instead of through the LDS-DMA ring, whose per-CU landing
+    // cadence (~0.6 us per 16 KB stage) bounded the kernel.  Wn is fragment-major
+    // (cmt_hip.h cmt_chain_args.Wn): every load instruction reads 1 KB contiguous.
+    __device__ __forceinline__ void load_wregs(const T* Wp, int g, frag (&wr)[SUB_STAGES][2][2]) const {
+        const T* base = Wp + (int64_t)((g * 4 + wave) * SUB_STAGES) * 4 * 512 + lane * 8;
+#pragma unroll
+        for (int kc = 0; kc < SUB_STAGES; ++kc)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) wr[kc][ks][nt] = *(const frag*)(base + ((kc * 2 + ks) * 2 + nt) * 512);
+    }
+
+    __device__ __forceinline__ void sub_gemm_regs(const char* A, const frag (&wr)[SUB_STAGES][2][2],
+                                                  f32x16 (&acc)[2]) const {
+        // the operand image was written by all four waves (put_act)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_mem();
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
+#pragma unroll
+        for (int kc = 0; kc < SUB_STAGES; ++kc)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const frag af = *(const frag*)(A + lr * (CE * 2) + (((kc * 4 + 2 * ks + lh) ^ (lr & 15)) << 4));
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma_traits<T>::mma(wr[kc][ks][nt], af, acc[nt]);
+            }
+    }
+
     // column of value r of n-tile nt for this lane (4 consecutive per group r >> 2)
     __device__ __forceinline__ int col(int nt, int r) const {
         return wave * 64 + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -263,8 +297,8 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
         e.w2 = (const T*)a.W2 + g * CE; e.ld2 = 4 * CE;                  // fc2 columns (K) [256g, ...)
         e.nstages = 3 * SUB_STAGES;
     } else {
-        e.w0 = has_next ? (const T*)a.Wn + (int64_t)g * CE * CE : Wo; e.ld0 = CE;   // in_proj block g
-        e.nstages = has_next ? SUB_STAGES : 0;
+        e.w0 = Wo; e.ld0 = CE;             // unused: B2's in_proj block streams into registers
+        e.nstages = 0;
     }
     const int m0 = rb * RB;
     const int row = min(m0 + e.lr, a.rows - 1);
@@ -324,6 +358,8 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                                          16, 0, 0);
 #pragma unroll
     for (int s = 0; s < NSTG - 1; ++s) e.issue();
+    typename Eng<T>::frag wr[SUB_STAGES][2][2];
+    if (kind == 2 && has_next) e.load_wregs((const T*)a.Wn, g, wr);
     // first use of the ordinary loads: everything issued so far has landed after this
     asm volatile("" ::"v"(res[0]), "v"(res[31]), "v"(qp[0]), "v"(qp[31]), "v"(oold[0]), "v"(oold[31]));
     rc_wait<0>();
@@ -435,7 +471,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 #pragma unroll
         for (int i = 0; i < 32; ++i) u[i] = y[i] + qp[i];              // qp = 0 for the V block
         e.put_act(actA, u);                                            // lowp(y + pos) (Q|K) / lowp(y) (V)
-        e.sub_gemm(actA, acc, true);
+        e.sub_gemm_regs(actA, wr, acc);
         const float* bqkv = e.prm() + 3072 + g * CE;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)

@@ -384,6 +384,9 @@ class PETRTransformerDecoder(nn.Module):
                 ffn = lay.ffns[0]
                 layers.append(dict(
                     sa_w=to_dtype(sa.in_proj_weight, g), sa_b=sa.in_proj_bias.detach().contiguous(),
+                    # chain B2's copy of the in_proj weights, fragment-major (cmt_hip.h cmt_chain_args.Wn)
+                    sa_wp=(native.pack_chain_wn(to_dtype(sa.in_proj_weight, g))
+                           if g != torch.float32 and tuple(sa.in_proj_weight.shape) == (768, 256) else None),
                     sa_ow=to_dtype(sa.out_proj.weight, g), sa_ob=sa.out_proj.bias.detach().contiguous(),
                     ca_wq=to_dtype(ca.in_proj_weight[:C], g),
                     ca_bq=ca.in_proj_bias[:C].detach().contiguous() if ca.in_proj_bias is not None else None,
@@ -564,7 +567,7 @@ class PETRTransformerDecoder(nn.Module):
                                      v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
                                      round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2,
                                      kmax_ld=L * H, kmax_plane0=l * H)
-                nxt = pk["layers"][l + 1]["sa_w"] if l + 1 < L else None
+                nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
                 native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
                              R=t1n, W2=lw["f2_w"], WS=cws)
                 native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,

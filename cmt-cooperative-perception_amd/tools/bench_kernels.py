@@ -92,7 +92,7 @@ def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
     Wo = (torch.randn(C, C, device=dev) / 16).to(dt)
     W1 = (torch.randn(F if kind else C, C, device=dev) / 16).to(dt)
     W2 = (torch.randn(C, F, device=dev) / 32).to(dt)
-    Wn = None if last else (torch.randn(3 * C, C, device=dev) / 16).to(dt)
+    Wn = None if last else N.pack_chain_wn((torch.randn(3 * C, C, device=dev) / 16).to(dt))
     prm = torch.randn(N.CHAIN_PRM[kind], device=dev) * 0.1
     Y, OUT = torch.empty(rows, C, device=dev), torch.empty(rows, C, device=dev)
     WS = torch.randn(N.chain_ws_numel(rows), device=dev)
