@@ -289,8 +289,8 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     const T* Wo = (const T*)a.Wo;
     if (kind == 0) {
         e.w0 = Wo; e.ld0 = CE;
-        e.w1 = (const T*)a.W1; e.ld1 = CE;
-        e.nstages = 2 * SUB_STAGES;
+        e.w1 = nullptr; e.ld1 = CE;        // the Q projection streams into registers (fragment-major W1)
+        e.nstages = SUB_STAGES;
     } else if (kind == 1) {
         e.w0 = Wo; e.ld0 = CE;
         e.w1 = (const T*)a.W1 + (int64_t)g * CE * CE; e.ld1 = CE;       // fc1 rows [256g, 256g + 256)
@@ -360,6 +360,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     for (int s = 0; s < NSTG - 1; ++s) e.issue();
     typename Eng<T>::frag wr[SUB_STAGES][2][2];
     if (kind == 2 && has_next) e.load_wregs((const T*)a.Wn, g, wr);
+    if (kind == 0) e.load_wregs((const T*)a.W1, 0, wr);
     // first use of the ordinary loads: everything issued so far has landed after this
     asm volatile("" ::"v"(res[0]), "v"(res[31]), "v"(qp[0]), "v"(qp[31]), "v"(oold[0]), "v"(oold[31]));
     rc_wait<0>();
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
             v[i] += qp[i];
         }
         e.put_act(actB, v);                                            // lowp(y + query_pos)
-        e.sub_gemm(actB, acc, true);                                   // cross-attn Q projection
+        e.sub_gemm_regs(actB, wr, acc);                                // cross-attn Q projection
         const float* bq = e.prm() + 768;
         t4 qo[8];
 #pragma unroll

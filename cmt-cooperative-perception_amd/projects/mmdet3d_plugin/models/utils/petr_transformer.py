@@ -389,6 +389,8 @@ class PETRTransformerDecoder(nn.Module):
                            if g != torch.float32 and tuple(sa.in_proj_weight.shape) == (768, 256) else None),
                     sa_ow=to_dtype(sa.out_proj.weight, g), sa_ob=sa.out_proj.bias.detach().contiguous(),
                     ca_wq=to_dtype(ca.in_proj_weight[:C], g),
+                    ca_wqp=(native.pack_chain_wn(to_dtype(ca.in_proj_weight[:C], g))
+                            if g != torch.float32 and C == 256 else None),
                     ca_bq=ca.in_proj_bias[:C].detach().contiguous() if ca.in_proj_bias is not None else None,
                     ca_ow=to_dtype(ca.out_proj.weight, g),
                     ca_ob=ca.out_proj.bias.detach().contiguous() if ca.out_proj.bias is not None else None,
@@ -558,7 +560,7 @@ class PETRTransformerDecoder(nn.Module):
                                  q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
                                  v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
                                  o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
-                native.chain(0, ob, qpos, ch["A"][l], lw["sa_ow"], lw["ca_wq"], t1n, rows=rows, Nq=Nq, eps=eps,
+                native.chain(0, ob, qpos, ch["A"][l], lw["sa_ow"], lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
                              R=tgt if (l > 0 or tgt0 is not None) else None, Q=qc)
                 with timed("cross_attn"):
                     native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,

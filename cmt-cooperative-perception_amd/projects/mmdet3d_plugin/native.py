@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -356,11 +356,13 @@ def chain_ws_numel(rows):
 
 
 def pack_chain_wn(W):
-    """Row-major in_proj_weight [768, 256] -> the fragment-major 1-D layout chain
-    B2 reads (cmt_hip.h cmt_chain_args.Wn): index (g, wave, kc, ks, nt, lh, lr, e)."""
-    if W.shape != (768, 256):
-        raise RuntimeError("pack_chain_wn: in_proj_weight must be [768, 256]")
-    return W.reshape(3, 4, 2, 32, 8, 2, 2, 8).permute(0, 1, 4, 5, 2, 6, 3, 7).contiguous().view(-1)
+    """Row-major weight [256 G, 256] -> the fragment-major 1-D layout the chains
+    stream into registers (cmt_hip.h cmt_chain_args.Wn; chain A's W1 is G = 1):
+    index (g, wave, kc, ks, nt, lh, lr, e)."""
+    if W.dim() != 2 or W.shape[1] != 256 or W.shape[0] % 256:
+        raise RuntimeError("pack_chain_wn: weight must be [256 G, 256]")
+    G = W.shape[0] // 256
+    return W.reshape(G, 4, 2, 32, 8, 2, 2, 8).permute(0, 1, 4, 5, 2, 6, 3, 7).contiguous().view(-1)
 
 
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
@@ -370,6 +372,8 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16)
     if Wn is not None and (Wn.dim() != 1 or Wn.numel() != 768 * 256):
         raise RuntimeError("cmt_chain: Wn must be fragment-major (pack_chain_wn)")
+    if kind == 0 and (W1 is None or W1.dim() != 1 or W1.numel() != 256 * 256):
+        raise RuntimeError("cmt_chain: chain A's W1 must be fragment-major (pack_chain_wn)")
     if OUT16 is not None and (OUT is None or OUT16.dtype not in (torch.float16, torch.bfloat16)):
         raise RuntimeError("cmt_chain: OUT16 must be a 16-bit copy target beside OUT")
     if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:

@@ -98,7 +98,8 @@ def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
     WS = torch.randn(N.chain_ws_numel(rows), device=dev)
     Q = torch.empty(rows * 3 * C, dtype=dt, device=dev)
     if kind == 0:
-        fn = lambda: N.chain(0, X, P, prm, Wo, W1, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, Q=Q)
+        W1p = N.pack_chain_wn(W1[:256].contiguous())
+        fn = lambda: N.chain(0, X, P, prm, Wo, W1p, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, Q=Q)
         fl = 2 * rows * C * C * 2
     elif kind == 1:
         fn = lambda: N.chain(1, X, None, prm, Wo, W1, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, W2=W2, WS=WS)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 5
+#define CMT_ABI_VERSION 6
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -231,7 +231,8 @@ typedef struct cmt_chain_args {
     const float* P;            /* query_pos [rows][256] fp32 (A; B2 with Wn) */
     const float* prm;          /* packed parameter block */
     const void* Wo;            /* A, B1: out_proj.weight [256][256] */
-    const void* W1;            /* A: cross-attn in_proj_weight[:256]; B1: fc1.weight [1024][256] */
+    const void* W1;            /* A: cross-attn in_proj_weight[:256], FRAGMENT-MAJOR (the Wn layout, g = 0);
+                                  B1: fc1.weight [1024][256] row-major */
     const void* W2;            /* B1: fc2.weight [256][1024] */
     const void* Wn;            /* B2: next layer's self-attn in_proj_weight [768][256], FRAGMENT-MAJOR:
                                   element W[256g + 64w + 32nt + r][32kc + 16ks + 8h + e] at

@@ -530,7 +530,7 @@ def test_chain_a(N, dev, dt, B, Nq, with_r):
     prm = torch.cat([bo, lw, lb, bq])
     Y = torch.empty(rows, C, device=dev)
     Q = torch.empty(B * 8 * Nq * 32, dtype=dt, device=dev)
-    N.chain(0, X.to(dev), P.to(dev), prm.to(dev), Wo.to(dev), Wq.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
+    N.chain(0, X.to(dev), P.to(dev), prm.to(dev), Wo.to(dev), N.pack_chain_wn(Wq.to(dev)), Y, rows=rows, Nq=Nq, eps=1e-5,
             R=R.to(dev) if R is not None else None, Q=Q)
     d = lambda t: t.double()
     t = d(X) @ d(Wo).T + d(bo) + (d(R) if R is not None else 0)
