@@ -294,8 +294,8 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     } else if (kind == 1) {
         e.w0 = Wo; e.ld0 = CE;
         e.w1 = (const T*)a.W1 + (int64_t)g * CE * CE; e.ld1 = CE;       // fc1 rows [256g, 256g + 256)
-        e.w2 = (const T*)a.W2 + g * CE; e.ld2 = 4 * CE;                  // fc2 columns (K) [256g, ...)
-        e.nstages = 3 * SUB_STAGES;
+        e.w2 = nullptr; e.ld2 = 4 * CE;    // fc2 K block g streams into registers (fragment-major W2)
+        e.nstages = 2 * SUB_STAGES;
     } else {
         e.w0 = Wo; e.ld0 = CE;             // unused: B2's in_proj block streams into registers
         e.nstages = 0;
@@ -361,6 +361,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     typename Eng<T>::frag wr[SUB_STAGES][2][2];
     if (kind == 2 && has_next) e.load_wregs((const T*)a.Wn, g, wr);
     if (kind == 0) e.load_wregs((const T*)a.W1, 0, wr);
+    if (kind == 1) e.load_wregs((const T*)a.W2, g, wr);
     // first use of the ordinary loads: everything issued so far has landed after this
     asm volatile("" ::"v"(res[0]), "v"(res[31]), "v"(qp[0]), "v"(qp[31]), "v"(oold[0]), "v"(oold[31]));
     rc_wait<0>();
@@ -435,7 +436,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                 for (int r = 0; r < 16; ++r) h[nt * 16 + r] = fmaxf(acc[nt][r] + b1[e.col(nt, r)], 0.f);
             e.put_act(actA, h);                                        // hidden quarter g = fc2 K block g
         }
-        e.sub_gemm(actA, acc, true);                                   // fc2 partial over K block g
+        e.sub_gemm_regs(actA, wr, acc);                                // fc2 partial over K block g
         const float* b2 = e.prm() + 1792;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)

@@ -396,6 +396,8 @@ class PETRTransformerDecoder(nn.Module):
                     ca_ob=ca.out_proj.bias.detach().contiguous() if ca.out_proj.bias is not None else None,
                     f1_w=to_dtype(ffn.layers[0][0].weight, g), f1_b=ffn.layers[0][0].bias.detach().contiguous(),
                     f2_w=to_dtype(ffn.layers[1].weight, g), f2_b=ffn.layers[1].bias.detach().contiguous(),
+                    f2_wp=(native.pack_chain_fc2(to_dtype(ffn.layers[1].weight, g))
+                           if g != torch.float32 and tuple(ffn.layers[1].weight.shape) == (256, 1024) else None),
                     norms=[(n.weight.detach().contiguous(), n.bias.detach().contiguous(), n.eps)
                            for n in lay.norms]))
                 kw.append(ca.in_proj_weight[C:2 * C])
@@ -571,7 +573,7 @@ class PETRTransformerDecoder(nn.Module):
                                      kmax_ld=L * H, kmax_plane0=l * H)
                 nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
                 native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
-                             R=t1n, W2=lw["f2_w"], WS=cws)
+                             R=t1n, W2=lw["f2_wp"], WS=cws)
                 native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                              Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
                              Q=qkv if nxt is not None else None, WS=cws, OUT16=out16)

@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -365,6 +365,14 @@ def pack_chain_wn(W):
     return W.reshape(G, 4, 2, 32, 8, 2, 2, 8).permute(0, 1, 4, 5, 2, 6, 3, 7).contiguous().view(-1)
 
 
+def pack_chain_fc2(W2):
+    """fc2.weight [256, 1024] -> its four K blocks [256, 256] stacked and packed
+    fragment-major (cmt_hip.h cmt_chain_args.W2)."""
+    if W2.shape != (256, 1024):
+        raise RuntimeError("pack_chain_fc2: fc2.weight must be [256, 1024]")
+    return pack_chain_wn(torch.cat([W2[:, 256 * g:256 * (g + 1)] for g in range(4)], 0))
+
+
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
           out_flags=0, Q=None, WS=None, OUT16=None):
     """One row-block chain of a decoder layer's query side (cmt_chain): kind 0
@@ -372,6 +380,8 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16)
     if Wn is not None and (Wn.dim() != 1 or Wn.numel() != 768 * 256):
         raise RuntimeError("cmt_chain: Wn must be fragment-major (pack_chain_wn)")
+    if kind == 1 and (W2 is None or W2.dim() != 1 or W2.numel() != 256 * 1024):
+        raise RuntimeError("cmt_chain: chain B1's W2 must be fragment-major (pack_chain_fc2)")
     if kind == 0 and (W1 is None or W1.dim() != 1 or W1.numel() != 256 * 256):
         raise RuntimeError("cmt_chain: chain A's W1 must be fragment-major (pack_chain_wn)")
     if OUT16 is not None and (OUT is None or OUT16.dtype not in (torch.float16, torch.bfloat16)):

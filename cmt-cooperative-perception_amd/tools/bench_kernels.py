@@ -102,7 +102,8 @@ def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
         fn = lambda: N.chain(0, X, P, prm, Wo, W1p, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, Q=Q)
         fl = 2 * rows * C * C * 2
     elif kind == 1:
-        fn = lambda: N.chain(1, X, None, prm, Wo, W1, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, W2=W2, WS=WS)
+        W2p = N.pack_chain_fc2(W2)
+        fn = lambda: N.chain(1, X, None, prm, Wo, W1, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, W2=W2p, WS=WS)
         fl = 2 * rows * C * C * 9
     else:
         fn = lambda: N.chain(2, None, None if last else P, prm, None, None, Y, rows=rows, Nq=Nq, eps=1e-5,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 6
+#define CMT_ABI_VERSION 7
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -233,7 +233,8 @@ typedef struct cmt_chain_args {
     const void* Wo;            /* A, B1: out_proj.weight [256][256] */
     const void* W1;            /* A: cross-attn in_proj_weight[:256], FRAGMENT-MAJOR (the Wn layout, g = 0);
                                   B1: fc1.weight [1024][256] row-major */
-    const void* W2;            /* B1: fc2.weight [256][1024] */
+    const void* W2;            /* B1: fc2.weight [256][1024] as its 4 K blocks [256][256g..256g+256),
+                                  each FRAGMENT-MAJOR (the Wn layout, g = K block) */
     const void* Wn;            /* B2: next layer's self-attn in_proj_weight [768][256], FRAGMENT-MAJOR:
                                   element W[256g + 64w + 32nt + r][32kc + 16ks + 8h + e] at
                                   ((((((g*4 + w)*8 + kc)*2 + ks)*2 + nt)*2 + h)*32 + r)*8 + e

@@ -571,7 +571,7 @@ def test_chain_b(N, dev, dt, B, Nq, last, flags):
     WS = torch.full((N.chain_ws_numel(rows),), float("nan"), device=dev)
     prm_d = prm.to(dev)
     N.chain(1, X.to(dev), None, prm_d, Wo.to(dev), W1.to(dev), Y, rows=rows, Nq=Nq, eps=1e-5,
-            R=R.to(dev), W2=W2.to(dev), WS=WS)
+            R=R.to(dev), W2=N.pack_chain_fc2(W2.to(dev)), WS=WS)
     N.chain(2, None, None if last else P.to(dev), prm_d, None, None, Y, rows=rows, Nq=Nq, eps=1e-5,
             Wn=None if last else N.pack_chain_wn(Wn.to(dev)), OUT=OUT, out_flags=flags, Q=None if last else QKV, WS=WS,
             OUT16=OUT16)
