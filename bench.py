@@ -1,23 +1,34 @@
 #!/usr/bin/env python3
-"""Decoder-frame throughput of the MI355X-native CMT head (BASELINE.json metric).
+"""Decoder-frame throughput of the MI355X-native CMT head (BASELINE.json metric:
+"decoder frames/sec at 900 queries x (BEV+6-cam) tokens").
 
-Workload (BASELINE.json configs[1]): CMT-L (LiDAR-only) nuScenes-shape
-synthetic frame -- BEV [1, 512, 180, 180] (= 32 400 memory tokens), 900
-queries, 6-layer decoder, bf16 compute (fp32 accumulate), the whole
-CmtLidarHead forward per step: shared_conv, coordinate encodings, decoder,
-task heads, box epilogue.  The ~30k-point voxel scatter-mean is timed
-separately.  Inputs and weights are resident in HBM before
-the timed region; one step = one frame per rank, captured as a HIP graph.
+Default workload (BASELINE.json configs[2], the metric's own shape): CMT
+camera+LiDAR nuScenes-shape synthetic frame -- BEV [1, 512, 180, 180] plus
+6 views x [256, 40, 100] pre-extracted image features (32 400 + 24 000 =
+56 400 memory tokens), 900 queries, 6-layer decoder, the whole CmtHead forward
+per step: shared_conv, BEV / RV / query coordinate encodings, decoder, task
+heads, box epilogue; bf16 compute (fp32 accumulate, fp32 residual stream).
+The ~30k-point voxel scatter-mean is timed separately.
+Inputs and weights are resident in HBM before the timed region; one step = one
+frame per rank, captured as a HIP graph.  The reference-numerics policy
+('ref': fp32 GEMMs, fp16 cross-attention core) is timed on the same frame and
+reported beside the headline as ``ref_policy``.
+
+Other workloads (--workload): lidar (configs[1], 32 400 tokens), coop
+(configs[3] forward: vehicle 36 400 + infrastructure 44 400 tokens), stress4
+(configs[4]: 4 agents x 48 400 tokens, 1500 queries, fp16).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-For N > 1 launch one process per GPU with torch.distributed.run; frames are
-independent, so ranks share nothing on the data path (weak scaling) and the
-only collectives are the barrier and the max-over-ranks of the elapsed time.
-Prints ONE JSON line on rank 0.
+With --gpus N > 1 and no torch.distributed environment, this process starts
+the N ranks itself (python -m torch.distributed.run, before any GPU call
+here) and exits with their status.  Frames are independent, so ranks share
+nothing on the data path (weak scaling); the only collectives are the
+barrier and the max-over-ranks of the elapsed time.  Prints ONE JSON line on
+rank 0.
 """
 import argparse
+import glob
 import json
-import math
 import os
 import sys
 import time
@@ -26,7 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cmt-cooperative-perception_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 from projects.mmdet3d_plugin import dp, native, set_precision  # noqa: E402
@@ -34,9 +45,10 @@ from projects.mmdet3d_plugin import synthetic as S  # noqa: E402
 from projects.mmdet3d_plugin.mmcv_custom.ops.voxel import SPConvVoxelization  # noqa: E402
 from projects.mmdet3d_plugin.profiling import region_timer  # noqa: E402
 
-PEAK_BF16_TFLOPS = 2500.0      # dense bf16 MFMA, MI355X_MICROARCH.md (no sparsity)
-PEAK_HBM_GBS = 8000.0
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}   # dense MFMA, MI355X_MICROARCH.md (no sparsity)
 C, NQ, NK, L, H = 256, 900, 32400, 6, 8
+METRIC = "decoder frames/sec at 900 queries x (BEV+6-cam) tokens; 1/2/4/8 MI355X"
+STRESS_YAWS = (0.0, 90.0, 180.0, -90.0)
 
 
 def cross_attn_flops(nq=NQ, nk=NK, c=C):
@@ -49,36 +61,35 @@ def decoder_frame_flops(nq=NQ, nk=NK, c=C, layers=L, ffn=1024):
     return layers * (12 * nq * c * c + 4 * nq * nq * c + 4 * nk * c * c + 4 * nq * nk * c + 4 * nq * c * ffn)
 
 
-def init_dist(args):
-    env = dp.dp_env()
-    if env.world > 1:
-        torch.cuda.set_device(env.local_rank)
-        dp.init(env, backend="nccl", device=torch.device("cuda", env.local_rank))
-    return env
-
-
 WORKLOADS = {
-    # name: (head config, agents as (meta prefix, camera yaws or None), description)
-    "lidar": ("cmt_lidar_nus", [("", None)],
-              "CMT-L (LiDAR-only) nuScenes-shape: BEV 512x180x180 (32400 tokens), 900 queries, 6-layer decoder, "
-              "CmtLidarHead forward (shared_conv + encodings + decoder + task heads), batch 1 frame per GPU"),
-    "fusion": ("cmt_fusion_nus", [("", S.NUS_YAWS)],
-               "CMT camera+LiDAR nuScenes-shape (configs[2]): BEV 512x180x180 + 6 views x 256x40x100 image feats "
-               "(56400 tokens), 900 queries, 6-layer decoder, CmtHead forward, batch 1 frame per GPU"),
-    "coop": ("cmtcoop_fusion_tumtraf", [("vehicle_", S.VEHICLE_YAWS), ("infrastructure_", S.INFRA_YAWS)],
-             "CMTCoop TUMTraf-shape forward (configs[3] forward leg): vehicle BEV 180x180 + 1 cam, infrastructure "
-             "BEV 180x180 + 3 cams (36400 + 44400 tokens), 900 queries, 6-layer decoder per agent, max fusion, "
-             "CmtHeadCoop forward, batch 1 frame per GPU"),
+    # cfg: head config; agents: (meta prefix, camera yaws or None); nq: queries; precision: compute policy
+    "fusion": dict(cfg="cmt_fusion_nus", agents=[("", S.NUS_YAWS)], nq=900, precision="bf16", head="CmtHead",
+                   desc="CMT camera+LiDAR nuScenes-shape (BASELINE configs[2]): BEV 512x180x180 + 6 views x "
+                        "256x40x100 image feats (56400 tokens), 900 queries, 6-layer decoder, CmtHead forward "
+                        "(shared_conv + BEV/RV/query encodings + decoder + task heads), batch 1 frame per GPU"),
+    "lidar": dict(cfg="cmt_lidar_nus", agents=[("", None)], nq=900, precision="bf16", head="CmtLidarHead",
+                  desc="CMT-L (LiDAR-only) nuScenes-shape (BASELINE configs[1]): BEV 512x180x180 (32400 tokens), "
+                       "900 queries, 6-layer decoder, CmtLidarHead forward, batch 1 frame per GPU"),
+    "coop": dict(cfg="cmtcoop_fusion_tumtraf", agents=[("vehicle_", S.VEHICLE_YAWS), ("infrastructure_", S.INFRA_YAWS)],
+                 nq=900, precision="bf16", head="CmtHeadCoop",
+                 desc="CMTCoop TUMTraf-shape forward (BASELINE configs[3] forward leg): vehicle BEV 180x180 + 1 cam, "
+                      "infrastructure BEV 180x180 + 3 cams (36400 + 44400 tokens), 900 queries, 6-layer decoder per "
+                      "agent, max fusion, CmtHeadCoop forward, batch 1 frame per GPU"),
+    "stress4": dict(cfg="cmtcoop_fusion_tumtraf", agents=[(f"agent{i}_", STRESS_YAWS) for i in range(4)], nq=1500,
+                    precision="fp16", head="CmtHeadCoop",
+                    desc="CMTCoop 4-agent stress (BASELINE configs[4]): 4 x (BEV 180x180 + 4 cams) = 4 x 48400 "
+                         "tokens, 1500 queries, 6-layer decoder per agent, max fusion over 4 agents, fp16, "
+                         "batch 1 frame per GPU"),
 }
 
 
 def make_workload(name, seed, device=None):
     """(head, head cfg, forward closure, per-agent memory lengths, oracle closure)
     for one synthetic frame of ``name``; tensors on ``device`` (CPU if None)."""
-    cfg_name, agents, _ = WORKLOADS[name]
-    head, cfg, _ = S.build_synthetic_head(cfg_name, seed=0, device=device)
+    w = WORKLOADS[name]
+    head, cfg, _ = S.build_synthetic_head(w["cfg"], seed=0, num_query=w["nq"], device=device)
     inputs, nks, metas = [], [], [dict()]
-    for i, (prefix, yaws) in enumerate(agents):
+    for i, (prefix, yaws) in enumerate(w["agents"]):
         x = S.synthetic_bev(1, 180, 180, seed=seed + 1 + 10 * i, device=device)
         xi = None
         if yaws is not None:
@@ -87,12 +98,14 @@ def make_workload(name, seed, device=None):
             metas[0].update(m)
         inputs.append((prefix, x, xi))
         nks.append(180 * 180 + (0 if yaws is None else len(yaws) * 40 * 100))
-    if len(agents) == 1:
+    if len(inputs) == 1:
         _, x, xi = inputs[0]
         fwd = lambda: head([x], [xi] if xi is not None else None, metas)  # noqa: E731
-    else:
+    elif len(inputs) == 2:
         (_, xv, iv), (_, xi_, ii) = inputs
         fwd = lambda: head([xv], [xi_], [iv], [ii], metas)  # noqa: E731
+    else:
+        fwd = lambda: head.forward_agents(inputs, metas)  # noqa: E731
 
     def oracle_fwd():
         from oracle import cmt_oracle as O
@@ -107,41 +120,77 @@ def make_workload(name, seed, device=None):
     return head, cfg, fwd, nks, oracle_fwd
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: every CPU this process may run on,
+    capped by OMP_NUM_THREADS when the launcher sets it (the GPU box sets it to
+    its 16-CPU share; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(workload, seconds, seed):
     """The oracle (CPU restatement, fp32 exact math, PyTorch CPU) on the same
-    workload, bounded to about ``seconds`` of host time."""
+    workload: one untimed warm-up frame, then the median of up
+    to 20 timed frames within about ``seconds`` of host time (at least one)."""
     _, _, _, nks, oracle_fwd = make_workload(workload, seed)
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
     run = oracle_fwd()
-    threads = torch.get_num_threads()
-    t0 = time.perf_counter()
-    n = 0
     times = []
     with torch.no_grad():
-        while True:
+        run()   # warm-up (allocator, thread pool)
+        t0 = time.perf_counter()
+        while len(times) < 20 and (not times or time.perf_counter() - t0 < seconds):
             t = time.perf_counter()
             run()
             times.append(time.perf_counter() - t)
-            n += 1
-            if time.perf_counter() - t0 > seconds or n >= 20:
-                break
     times.sort()
     med = times[len(times) // 2]
     return {"value": round(1.0 / med, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} full {workload} frames (Nq 900, memory tokens {'+'.join(map(str, nks))}, 6 layers, "
-                      f"shared_conv + coordinate encodings + decoder + task heads) through oracle/cmt_oracle.py in "
-                      f"fp32 on {threads} host threads; median frame time {med:.3f} s"}
+            "sample": f"1 warm-up + {len(times)} timed full {workload} frames (median; memory tokens "
+                      f"{'+'.join(map(str, nks))}, {WORKLOADS[workload]['nq']} queries, 6 layers, shared_conv + "
+                      f"coordinate encodings + decoder + task heads) through oracle/cmt_oracle.py in fp32 on "
+                      f"{threads} host threads (torch.set_num_threads); median frame {med:.3f} s"}
 
 
-def load_traffic():
-    """HBM bytes per cross-attention launch from the committed rocprofv3 PMC
-    summary (profiles/*pmc*.json), corrected as MI355X_MICROARCH.md prescribes
-    (FETCH_SIZE x2 for wide streaming reads).  None when absent."""
-    import glob
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*attn_pmc_summary.json")))
-    if not cands:
-        return None
-    with open(cands[-1]) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+def load_traffic(workload, nk):
+    """HBM bytes per launch of the dominant kernel (cross-attention core + its
+    split combine) for THIS workload's shape, from the committed rocprofv3 PMC
+    summary profiles/*_<workload>_attn_pmc_summary.json (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, separate passes; tools/traffic_summary.py).
+    Raises when no summary matches the workload and key length."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_attn_pmc_summary.json")))
+    for path in reversed(cands):
+        with open(path) as f:
+            s = json.load(f)
+        if s.get("workload") == workload and int(s.get("nk", -1)) == int(nk):
+            return s["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    raise RuntimeError(f"no committed PMC traffic summary for workload {workload!r} at Nk={nk} under profiles/ "
+                       "(collect one with tools/gpu_check.sh ... prof; or pass --no-traffic)")
+
+
+def spawn_ranks(args):
+    """--gpus N without a torch.distributed environment: start the N ranks as
+    children (this process has not touched the GPU) and return their status."""
+    return dp.spawn(os.path.abspath(__file__), sys.argv[1:], args.gpus)
+
+
+def capture(step):
+    """Warm the step eagerly, then capture it as a HIP graph; returns replay."""
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    return graph
 
 
 def main():
@@ -149,40 +198,36 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "ref"])
+    ap.add_argument("--workload", default="fusion", choices=sorted(WORKLOADS),
+                    help="fusion = BASELINE configs[2] (the headline line); lidar / coop / stress4 = configs[1] / "
+                         "[3] forward / [4]")
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "ref"],
+                    help="compute policy of the headline value (default: the workload's, bf16 / fp16 for stress4)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-ref", action="store_true", help="skip the 'ref'-policy frames/s key")
+    ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="lidar", choices=sorted(WORKLOADS),
-                    help="lidar = BASELINE configs[1] (the headline line); fusion / coop = configs[2] / [3] forward")
+    ap.add_argument("--no-traffic", action="store_true", help="profiling runs: do not read the committed PMC summary")
     args = ap.parse_args()
 
-    env = init_dist(args)
+    env = dp.dp_env()
+    if args.gpus > 1 and env.world == 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    if args.gpus != env.world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env.world}: launch one process per GPU")
     world, rank, local = env.world, env.rank, env.local_rank
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dp.init(env, backend="nccl", device=dev)
     native.lib()
-    set_precision(args.precision)
+    w = WORKLOADS[args.workload]
+    prec = args.precision or w["precision"]
+    set_precision(prec)
 
     head, cfg, step, nks, _ = make_workload(args.workload, seed=dp.frame_seed(0, env), device=dev)
     with torch.no_grad():
-        for _ in range(2):
-            step()
-        torch.cuda.synchronize()
-        graph = None
-        if not args.no_graph:
-            graph = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                step()
-                torch.cuda.synchronize()
-                with torch.cuda.graph(graph):
-                    static_out = step()
-            torch.cuda.current_stream().wait_stream(s)
-            run = graph.replay
-        else:
-            run = step
+        run = capture(step).replay if not args.no_graph else step
         elapsed, value = dp.timed_frames(run, steps=args.steps, warmup=args.warmup, env=env,
                                          sync=torch.cuda.synchronize, device=dev)
 
@@ -192,6 +237,18 @@ def main():
                 step()
         attn_ms_all = rt.durations_ms("cross_attn")
         attn_ms = sum(attn_ms_all) / len(attn_ms_all)
+
+        # --- the reference-numerics policy on the same frame (fp32 GEMMs, fp16 cross core)
+        ref_policy = None
+        if not args.no_ref and prec != "ref":
+            set_precision("ref")
+            run_ref = capture(step).replay if not args.no_graph else step
+            e_ref, v_ref = dp.timed_frames(run_ref, steps=max(5, args.steps // 5), warmup=2, env=env,
+                                           sync=torch.cuda.synchronize, device=dev)
+            ref_policy = {"value": round(v_ref, 3), "unit": "frames/s", "steps": max(5, args.steps // 5),
+                          "ms_per_step": round(e_ref / max(5, args.steps // 5) * 1e3, 4),
+                          "dtype": "fp32 GEMMs + fp16 cross-attention core (reference numerics)"}
+            set_precision(prec)
 
         # --- voxel scatter-mean of ~30k points (timed separately)
         vl = SPConvVoxelization(voxel_size=[0.075, 0.075, 0.2], point_cloud_range=[-54.0, -54.0, -5.0, 54.0, 54.0, 3.0],
@@ -209,10 +266,15 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     # mean algorithmic FLOPs of one cross-attention launch (agents may differ in Nk)
-    flop_launch = sum(cross_attn_flops(nk=nk) for nk in nks) / len(nks)
+    nq = w["nq"]
+    flop_launch = sum(cross_attn_flops(nq=nq, nk=nk) for nk in nks) / len(nks)
     achieved = flop_launch / (attn_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS.get(prec, PEAK_TFLOPS["bf16"])
+    traffic, traffic_src = (None, None)
+    if not args.no_traffic:
+        traffic, traffic_src = load_traffic(args.workload, sum(nks) // len(nks))
     result = {
-        "metric": "decoder frames/sec at 900 queries x (BEV+6-cam) tokens; 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "frames/s",
         "n_gpus": world,
@@ -222,24 +284,22 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"bf16": "bf16", "fp16": "fp16", "ref": "fp32+fp16attn"}[args.precision],
-        "data": "synthetic (seeded BEV features relu(N(0,1)), image feats N(0,1) where used, random-init weights "
-                "of the head)",
-        "config": {"workload": WORKLOADS[args.workload][2],
-                   "global_batch": world, "seq_len": sum(nks), "parallelism": f"dp{world}",
-                   "graph": graph is not None,
-                   "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nk=nk) for nk in nks) / 1e9, 2)},
-        "roofline": {"kernel": "cmt_attn_fwd (cross-attention core, + split combine)", "bound": "mfma",
-                     "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic() if args.workload == "lidar" else None,
-                     "avg_launch_ms": round(attn_ms, 5),
-                     "flop_per_launch": flop_launch},
+        "dtype": {"bf16": "bf16", "fp16": "fp16", "ref": "fp32+fp16attn"}[prec],
+        "data": "synthetic (seeded BEV features relu(N(0,1)), image feats N(0,1), nuScenes/TUMTraf-like camera "
+                "matrices, random-init weights of the head)",
+        "config": {"workload": w["desc"], "global_batch": world, "seq_len": sum(nks), "num_query": nq,
+                   "parallelism": f"dp{world}", "graph": not args.no_graph,
+                   "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nq=nq, nk=nk) for nk in nks) / 1e9, 2)},
+        "roofline": {"kernel": "cmt_attn_fwd (cross-attention core + split combine)", "bound": "mfma",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "avg_launch_ms": round(attn_ms, 5), "flop_per_launch": flop_launch},
+        "ref_policy": ref_policy,
         "voxel_scatter_mean_ms": round(vox_ms, 4),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds,
-                                                seed=dp.frame_seed(0, env))
+        result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, seed=dp.frame_seed(0, env))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -22,3 +22,15 @@ int cmt_check_launch(const char* what) {
 extern "C" int cmt_abi_version(void) { return CMT_ABI_VERSION; }
 
 extern "C" const char* cmt_last_error(void) { return g_last_error.c_str(); }
+
+// sizeof of every argument struct, so a binding (ctypes / cffi) can assert its
+// mirror against the library it loaded instead of trusting the header copy
+extern "C" int64_t cmt_gemm_args_size(void) { return (int64_t)sizeof(cmt_gemm_args); }
+extern "C" int64_t cmt_attn_args_size(void) { return (int64_t)sizeof(cmt_attn_args); }
+extern "C" int64_t cmt_ln_args_size(void) { return (int64_t)sizeof(cmt_ln_args); }
+extern "C" int64_t cmt_chain_args_size(void) { return (int64_t)sizeof(cmt_chain_args); }
+
+extern "C" int64_t cmt_chain_ws_bytes(int rows) {
+    if (rows <= 0) return 0;
+    return (int64_t)4 * cdiv(rows, 32) * 32 * 256 * (int64_t)sizeof(float);
+}

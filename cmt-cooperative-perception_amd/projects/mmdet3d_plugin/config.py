@@ -53,7 +53,12 @@ def _eval(node, env):
         return base[_eval(sl, env)]
     if isinstance(node, ast.Call) and isinstance(node.func, ast.Name) and node.func.id in _FUNCS:
         args = [_eval(a, env) for a in node.args]
-        kwargs = {k.arg: _eval(k.value, env) for k in node.keywords}
+        kwargs = {}
+        for k in node.keywords:
+            if k.arg is None:          # dict(type=..., **img_norm_cfg)
+                kwargs.update(_eval(k.value, env))
+            else:
+                kwargs[k.arg] = _eval(k.value, env)
         return _FUNCS[node.func.id](*args, **kwargs)
     if isinstance(node, ast.ListComp) or isinstance(node, ast.Lambda):
         raise ConfigError(f"unsupported construct at line {node.lineno}")

@@ -37,6 +37,24 @@ def init(env, backend="nccl", device=None):
         dist.init_process_group(backend=backend, **kw)
 
 
+def spawn(script, argv, nproc, env=None):
+    """Start ``nproc`` ranks of ``script argv`` as child processes through
+    torch.distributed.run on 127.0.0.1 (one process per GPU; the caller must
+    not have touched the GPU) and return their exit status."""
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", script] + list(argv)
+    e = dict(os.environ if env is None else env)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=e)
+
+
 def frame_seed(base, env, i=0):
     """Per-rank, per-frame seed: ranks never share frames."""
     return base + env.rank + i * env.world

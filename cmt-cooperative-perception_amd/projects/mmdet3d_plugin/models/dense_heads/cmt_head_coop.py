@@ -70,9 +70,29 @@ class CmtHeadCoop(CmtHead):
 
     def forward_agents(self, agents, img_metas):
         """Any number of agents: ``agents`` = list of (prefix, pts_feat, img_feat);
-        outputs max-fused over agents (the reference fuses exactly two)."""
+        outputs max-fused over agents (the reference fuses exactly two).  Agent
+        metas are selected by key prefix as filter_img_metas does for the two
+        reference agents; with other prefixes (e.g. 'agent2_') every other
+        agent's prefixed keys are dropped."""
         B = len(img_metas)
-        return self._forward_agents([(x, xi, self._agent_metas(img_metas, p)) for p, x, xi in agents], img_metas, B)
+        prefixes = [p for p, _, _ in agents]
+        if set(prefixes) <= {"vehicle_", "infrastructure_"}:
+            metas = [self._agent_metas(img_metas, p) for p in prefixes]
+        else:
+            metas = [[self._select_metas(m, p, prefixes) for m in img_metas] if self.variant != "lidar" else img_metas
+                     for p in prefixes]
+        return self._forward_agents([(x, xi, m) for (_, x, xi), m in zip(agents, metas)], img_metas, B)
+
+    @staticmethod
+    def _select_metas(meta, prefix, prefixes):
+        out = {}
+        for k, v in meta.items():
+            if k.startswith(prefix):
+                out[k[len(prefix):]] = v
+            elif not any(k.startswith(p) for p in prefixes):
+                out[k] = v
+        out["node"] = prefix
+        return out
 
 
 @HEADS.register_module()

@@ -258,9 +258,13 @@ class HeadEngineMixin:
                         a_bstride=B * Nq * C, w_bstride=width * k * C, c_bstride=B * Nq * width,
                         a_mode=native.A_CONV1D3 if k == 3 else native.A_ROWS, seg_len=Nq)
             OUT = torch.empty((L, B, Nq, tp["out_total"]), dtype=torch.float32, device=outs_dec.device)
+            # box_epilogue = False (diagnostics / parity at the logit level): center and height
+            # come out as the raw task-head logits, before + inverse_sigmoid(ref) and sigmoid
+            epi = getattr(self, "box_epilogue", True)
             native.task_head_tail(H1, tp["gw"], tp["gb"], tp["w2"], tp["b2"], refB, OUT, L=L, B=B, Nq=Nq,
-                                  nheads=nh, hc=64, head_out=tp["head_out"], k=k, center_col=tp["center_col"],
-                                  height_col=tp["height_col"], pc_range=self.pc_range)
+                                  nheads=nh, hc=64, head_out=tp["head_out"], k=k,
+                                  center_col=tp["center_col"] if epi else -1,
+                                  height_col=tp["height_col"] if epi else -1, pc_range=self.pc_range)
             outs = {}
             start = 0
             for name, n in zip(tp["names"], tp["head_out"]):

@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -77,6 +77,8 @@ class LnArgs(ctypes.Structure):
                 ("Yp", _vp), ("ldyp", _i64), ("P", _vp), ("ldp", _i64)]
 
 
+STRUCTS = {"gemm": GemmArgs, "attn": AttnArgs, "ln": LnArgs, "chain": ChainArgs}
+
 _LIB = None
 
 
@@ -115,6 +117,11 @@ def _load():
         "cmt_voxelize_workspace_bytes": ([_int, _int], _i64),
         "cmt_voxelize": ([_vp, _int, _int, P(_flt), P(_flt), P(_int), _int, _int, _int, _vp, _vp, _vp, _vp, _vp,
                           _vp, _i64, _vp], _int),
+        "cmt_gemm_args_size": ([], _i64),
+        "cmt_attn_args_size": ([], _i64),
+        "cmt_ln_args_size": ([], _i64),
+        "cmt_chain_args_size": ([], _i64),
+        "cmt_chain_ws_bytes": ([_int], _i64),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -122,6 +129,11 @@ def _load():
         fn.restype = res
     if L.cmt_abi_version() != ABI_VERSION:
         raise RuntimeError("libcmt_hip.so ABI version mismatch")
+    for name, st in STRUCTS.items():
+        got = getattr(L, f"cmt_{name}_args_size")()
+        if got != ctypes.sizeof(st):
+            raise RuntimeError(f"cmt_{name}_args: library struct is {got} bytes, the ctypes mirror "
+                               f"{ctypes.sizeof(st)} (stale binding)")
     return L
 
 
@@ -390,10 +402,12 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
         raise RuntimeError(f"cmt_chain: parameter block must be {CHAIN_PRM[kind]} fp32 values")
     if WS is not None and (WS.dtype != torch.float32 or WS.numel() < chain_ws_numel(rows)):
         raise RuntimeError("cmt_chain: WS must hold chain_ws_numel(rows) fp32")
+    lows = [t for t in (X, Wo, W1, W2, Wn, Q, OUT16) if t is not None]
+    if any(t.dtype != lows[0].dtype for t in lows) or (lows and lows[0].dtype not in (torch.float16, torch.bfloat16)):
+        raise RuntimeError("cmt_chain: X, Wo, W1, W2, Wn, Q and OUT16 must share one 16-bit dtype (f16 or bf16)")
     a = ChainArgs()
     a.kind, a.rows, a.Nq, a.eps = kind, rows, Nq, eps
-    lowp = next((t for t in (X, Q, Wn, Wo, OUT16) if t is not None), None)
-    a.dtype = DT[lowp.dtype] if lowp is not None else BF16   # B2 without in_proj: no 16-bit operand
+    a.dtype = DT[lows[0].dtype] if lows else BF16   # B2 without in_proj: no 16-bit operand
 
     def ptr(t):
         return None if t is None else t.data_ptr()

@@ -1,10 +1,13 @@
-"""HBM traffic per launch of the cross-attention kernel from the FETCH_SIZE /
-WRITE_SIZE rocprofv3 passes of tools/profile_bench.sh, corrected as
-MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE reports half the bytes of
-wide coalesced streaming reads -> x2; WRITE_SIZE exact for 16-B stores).
-Writes profiles/attn_pmc_summary.json.
+"""HBM traffic per launch of the cross-attention kernel (core + its split
+combine) from the FETCH_SIZE / WRITE_SIZE rocprofv3 passes of
+tools/gpu_check.sh (prof), corrected as MI355X_MICROARCH.md prescribes
+(gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads ->
+x2; WRITE_SIZE exact for 16-B stores).  Writes
+profiles/<tag>_<workload>_attn_pmc_summary.json, which bench.py's
+load_traffic() keys on (workload, nk).
 
-    python cmt-cooperative-perception_amd/tools/traffic_summary.py gpurun_out/prof_r1 [--out profiles/attn_pmc_summary.json]
+    python cmt-cooperative-perception_amd/tools/traffic_summary.py gpurun_out/<tag>/prof \
+        --tag r2a --workload fusion --nk 56400 [--match attn_pp_kernel --match 'attn_combine_kernel<8>']
 """
 import argparse
 import glob
@@ -27,27 +30,39 @@ def per_kernel(db_path, counter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--out", default="profiles/attn_pmc_summary.json")
-    ap.add_argument("--match", default="attn_pp_kernel")
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--workload", required=True)
+    ap.add_argument("--nk", type=int, required=True)
+    ap.add_argument("--match", action="append", default=None,
+                    help="kernel-name substrings whose per-launch medians add up to one cross-attention launch")
+    ap.add_argument("--outdir", default="profiles")
     a = ap.parse_args()
+    match = a.match or ["attn_pp_kernel", "attn_combine_kernel<8>"]
     fdb = glob.glob(os.path.join(a.dir, "fetch", "**", "*.db"), recursive=True)[0]
     wdb = glob.glob(os.path.join(a.dir, "write", "**", "*.db"), recursive=True)[0]
     fetch = per_kernel(fdb, "FETCH_SIZE")
     write = per_kernel(wdb, "WRITE_SIZE")
     res = {"method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py (no graph); "
-                     "FETCH_SIZE x2 (gfx950 wide-read correction), units KB -> bytes",
-           "kernels": {}}
+                     "FETCH_SIZE x2 (gfx950 wide-read correction), units KB -> bytes; per-launch medians",
+           "workload": a.workload, "nk": a.nk, "match": match, "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = statistics.median(fetch.get(k, [0])) * 1024 * 2
         w = statistics.median(write.get(k, [0])) * 1024
         res["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "launches": len(fetch.get(k, []))}
-    attn = [v for k, v in res["kernels"].items() if a.match in k]
-    if attn:
-        res["hbm_bytes_per_launch"] = max(v["fetch_bytes"] + v["write_bytes"] for v in attn)
-    os.makedirs(os.path.dirname(a.out), exist_ok=True)
-    with open(a.out, "w") as fh:
+    parts = {}
+    for m in match:
+        hits = [(k, v) for k, v in res["kernels"].items() if m in k]
+        if not hits:
+            raise SystemExit(f"no kernel matches {m!r}")
+        k, v = max(hits, key=lambda kv: kv[1]["fetch_bytes"] + kv[1]["write_bytes"])
+        parts[k] = v["fetch_bytes"] + v["write_bytes"]
+    res["parts"] = parts
+    res["hbm_bytes_per_launch"] = sum(parts.values())
+    out = os.path.join(a.outdir, f"{a.tag}_{a.workload}_attn_pmc_summary.json")
+    os.makedirs(a.outdir, exist_ok=True)
+    with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
-    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    print(out, json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 7
+#define CMT_ABI_VERSION 8
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -43,6 +43,14 @@ enum cmt_status {
 
 int cmt_abi_version(void);
 const char* cmt_last_error(void);
+
+/* sizeof() of each argument struct as compiled into the library: a binding
+ * that mirrors a struct (ctypes, cffi) asserts its own size against these
+ * before the first call (native.py does; so does the INTEGRATION.md stub). */
+int64_t cmt_gemm_args_size(void);
+int64_t cmt_attn_args_size(void);
+int64_t cmt_ln_args_size(void);
+int64_t cmt_chain_args_size(void);
 
 /* ------------------------------------------------------------------------
  * GEMM with fused prologue/epilogue (MFMA, gfx950).
@@ -217,7 +225,8 @@ int cmt_gemm_ln(const cmt_gemm_args* gemm, const cmt_ln_args* ln, void* stream);
  *   A (1024): bo | norms[0].weight | norms[0].bias | bq
  *   B (3840, the same block for B1 and B2): bo | norms[1].w | norms[1].b | b1 (1024) | b2 |
  *             norms[2].w | norms[2].b | post_norm.w | post_norm.b | bn (768, zeros without Wn)
- * WS: caller workspace of 4 * rows * 256 fp32 (B1 writes, B2 reads).
+ * WS: caller workspace of cmt_chain_ws_bytes(rows) bytes = 4 * ceil(rows/32) * 32 * 256
+ *     fp32 (B1 writes whole 32-row tiles, B2 reads them; private tile order).
  * One eps for every LayerNorm of the layer.  Weights / X / Q in the compute
  * dtype (f16 / bf16), residuals and outputs fp32; every buffer 16-byte aligned.
  * ------------------------------------------------------------------------ */
@@ -246,6 +255,8 @@ typedef struct cmt_chain_args {
     void* OUT16;               /* B2 (optional): the layer output again in dtype (the task-head GEMM operand) */
 } cmt_chain_args;
 int cmt_chain(const cmt_chain_args* args, void* stream);
+/* bytes of the B1 -> B2 partials workspace WS for `rows` query rows */
+int64_t cmt_chain_ws_bytes(int rows);
 
 /* cmt_add_cast: Yl = lowp(X), Yp = lowp(X + P) over rows x C (either output
  * may be NULL; X == NULL reads zeros, the zero target of cmt_transformer.py:114)

@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 __all__ = [
     "inverse_sigmoid", "pos2embed", "coords_bev", "rv_pe", "rv_query_embed",
-    "mha", "decoder", "separate_task_head", "group_layer_norm", "shared_conv",
+    "flash_core_fp16", "mha", "decoder", "separate_task_head", "group_layer_norm", "shared_conv",
     "head_forward", "head_coop_forward", "box_epilogue", "decode",
     "denormalize_bbox", "filter_img_metas",
 ]
@@ -154,6 +154,19 @@ def _round_fp16(t):
     return t.to(torch.float16).to(torch.float32)
 
 
+def flash_core_fp16(q, k, v, scale):
+    """The fp16 attention core of flash-attn 0.2.2 as FlashAttention.forward
+    calls it (attention.py:46-92): q/k/v rounded to fp16 (auto_fp16), scores and
+    row statistics in fp32, P rounded to fp16 before P.V, fp32 accumulation,
+    fp16 output (returned here as fp32 values).  q [..., Sq, D], k/v [..., Sk, D]."""
+    q, k, v = _round_fp16(q.float()), _round_fp16(k.float()), _round_fp16(v.float())
+    s = torch.matmul(q, k.transpose(-1, -2)) * scale
+    m = s.amax(dim=-1, keepdim=True)
+    p = torch.exp(s - m)
+    l = p.sum(dim=-1, keepdim=True)
+    return _round_fp16(torch.matmul(_round_fp16(p), v) / l)
+
+
 def mha(query, key, value, in_w, in_b, out_w, out_b, num_heads, core="fp32"):
     """Multi-head attention with a packed in-projection.
 
@@ -179,13 +192,7 @@ def mha(query, key, value, in_w, in_b, out_w, out_b, num_heads, core="fp32"):
         p = torch.softmax(s, dim=-1)
         o = torch.matmul(p, v)
     elif core == "fp16":
-        q, k, v = _round_fp16(q), _round_fp16(k), _round_fp16(v)
-        s = torch.matmul(q, k.transpose(-1, -2)) * scale
-        m = s.amax(dim=-1, keepdim=True)
-        p = torch.exp(s - m)
-        l = p.sum(dim=-1, keepdim=True)
-        o = torch.matmul(_round_fp16(p), v) / l
-        o = _round_fp16(o)
+        o = flash_core_fp16(q, k, v, scale)
     else:
         raise ValueError(core)
     o = o.transpose(1, 2).reshape(B, Sq, C)
@@ -348,19 +355,21 @@ def _decoder_outputs(cfg, sd, x, x_img, img_metas, ref_points, variant, cross_co
     return torch.nan_to_num(out)
 
 
-def _task_outputs(cfg, sd, outs_dec, ref_points):
+def _task_outputs(cfg, sd, outs_dec, ref_points, epilogue=True):
+    """Task heads; epilogue=False returns the raw logits (center / height
+    before + inverse_sigmoid(ref) and sigmoid, cmt_head.py:503-513)."""
     L = cfg["num_layers"]
     reference = inverse_sigmoid(ref_points.clone())
     ret = []
     for t, num_cls in enumerate(cfg["num_classes"]):
         outs = separate_task_head(outs_dec, sd, f"task_heads.{t}", _heads_for(cfg, num_cls),
                                   cfg["final_kernel"], L)
-        ret.append(box_epilogue(outs, reference, cfg["pc_range"]))
+        ret.append(box_epilogue(outs, reference, cfg["pc_range"]) if epilogue else outs)
     return ret
 
 
 def head_forward(cfg, sd, x, x_img, img_metas, variant="fusion", cross_core="fp32",
-                 self_core="fp32"):
+                 self_core="fp32", epilogue=True):
     """CmtHead / CmtLidarHead / CmtImageHead ``forward_single`` at eval
     (cmt_head.py:475-547, 1014-1085, 929-999; prepare_for_dn eval branch
     410-413 = repeat of reference_points).  Returns list over tasks of dict
@@ -368,7 +377,7 @@ def head_forward(cfg, sd, x, x_img, img_metas, variant="fusion", cross_core="fp3
     B = x.shape[0] if x is not None else len(img_metas)
     ref = sd["reference_points.weight"].unsqueeze(0).repeat(B, 1, 1)
     outs_dec = _decoder_outputs(cfg, sd, x, x_img, img_metas, ref, variant, cross_core, self_core)
-    return _task_outputs(cfg, sd, outs_dec, ref)
+    return _task_outputs(cfg, sd, outs_dec, ref, epilogue)
 
 
 def filter_img_metas(img_meta, prefix="", ignore=""):
@@ -384,7 +393,7 @@ def filter_img_metas(img_meta, prefix="", ignore=""):
 
 
 def head_coop_forward(cfg, sd, agents, img_metas, variant="fusion", cross_core="fp32",
-                      self_core="fp32"):
+                      self_core="fp32", epilogue=True):
     """CmtHeadCoop / CmtLidarHeadCoop / CmtImageHeadCoop ``forward_single``
     (cmt_head_coop.py:362-437, 946-1017, 838-911).  ``agents`` is a list of
     (prefix, x, x_img); one decoder pass per agent with shared weights, then an
@@ -393,12 +402,20 @@ def head_coop_forward(cfg, sd, agents, img_metas, variant="fusion", cross_core="
     B = len(img_metas)
     ref = sd["reference_points.weight"].unsqueeze(0).repeat(B, 1, 1)
     outs = None
+    prefixes = [p for p, _, _ in agents]
     for prefix, x, x_img in agents:
-        other = "infrastructure_" if prefix == "vehicle_" else "vehicle_"
-        metas = [filter_img_metas(m, prefix, other) for m in img_metas] if variant != "lidar" else img_metas
+        if variant == "lidar":
+            metas = img_metas
+        elif set(prefixes) <= {"vehicle_", "infrastructure_"}:
+            other = "infrastructure_" if prefix == "vehicle_" else "vehicle_"
+            metas = [filter_img_metas(m, prefix, other) for m in img_metas]
+        else:   # N agents: drop every other agent's prefixed keys
+            metas = [{**{k: v for k, v in m.items() if not any(k.startswith(p) for p in prefixes)},
+                      **{k[len(prefix):]: v for k, v in m.items() if k.startswith(prefix)}, "node": prefix}
+                     for m in img_metas]
         o = _decoder_outputs(cfg, sd, x, x_img, metas, ref, variant, cross_core, self_core)
         outs = o if outs is None else torch.max(torch.stack([outs, o]), 0).values
-    return _task_outputs(cfg, sd, outs, ref)
+    return _task_outputs(cfg, sd, outs, ref, epilogue)
 
 
 # ---------------------------------------------------------------------------

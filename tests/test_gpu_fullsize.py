@@ -1,0 +1,108 @@
+"""Full-size parity at the BASELINE.json shapes (6 decoder layers, 900 queries):
+configs[1] CMT-L (32 400 BEV tokens), configs[2] CMT fusion (32 400 + 6 x 4 000
+= 56 400 tokens, nuScenes-like cameras), configs[3] forward CMTCoop (vehicle
+36 400 + infrastructure 44 400 tokens).
+
+Compared at the LOGIT level: the task-head outputs before the box epilogue
+(center / height before + inverse_sigmoid(ref) and sigmoid; head.box_epilogue
+= False, oracle epilogue=False), every decoder layer, every channel.
+
+  * precision 'ref' (the reference's numerics: fp32 projections, fp32
+    self-attention, fp16 flash cross-attention core) against the oracle with
+    the same numerics (oracle.flash_core_fp16): max abs error <= 1e-3
+    (north_star: "box/cls logits within 1e-3 abs of reference").
+  * precision 'bf16' (the bench policy) against the same oracle: reported, and
+    bounded by 2.5 % of each output's max |value| (bf16 keeps 8 significant
+    bits; DESIGN.md section 4 states the measured figure).
+The oracle takes a few seconds per frame on the host, so these run in the GPU
+suite directly at full size.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("center", "height", "dim", "rot", "vel", "cls_logits")
+TOL_REF = 1e-3
+TOL_BF16_REL = 2.5e-2
+
+
+def _errs(got, ref):
+    e, rel = {}, {}
+    for k in KEYS:
+        g, r = got[k].detach().cpu().double(), ref[k].double()
+        d = (g - r).abs().max().item()
+        e[k] = d
+        rel[k] = d / max(r.abs().max().item(), 1e-6)
+    return e, rel
+
+
+def _run(head, dev, prec, fwd):
+    from projects.mmdet3d_plugin import set_precision
+    set_precision(prec)
+    try:
+        with torch.no_grad():
+            out = fwd()
+        torch.cuda.synchronize()
+    finally:
+        set_precision("ref")
+    return out[0][0] if isinstance(out, tuple) else out[0]
+
+
+def _case(dev, parity_log, name, head, fwd, oracle):
+    head.box_epilogue = False
+    ref = oracle()[0]
+    got = _run(head, dev, "ref", fwd)
+    e, _ = _errs(got, ref)
+    worst = max(e.values())
+    parity_log.append(f"full-size {name} 'ref' vs fp16-core oracle (logits, 6 layers): max abs {worst:.2e} "
+                      f"[{', '.join(f'{k} {v:.1e}' for k, v in e.items())}] bound {TOL_REF:g}")
+    gotb = _run(head, dev, "bf16", fwd)
+    eb, rb = _errs(gotb, ref)
+    parity_log.append(f"full-size {name} 'bf16' vs oracle (logits): max abs {max(eb.values()):.2e}, max rel-to-scale "
+                      f"{max(rb.values()):.2e} bound {TOL_BF16_REL:g}")
+    assert worst <= TOL_REF, e
+    assert max(rb.values()) <= TOL_BF16_REL, rb
+
+
+def test_fullsize_lidar_configs1(dev, parity_log):
+    from oracle import cmt_oracle as O
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_lidar_nus", seed=0, num_query=900)
+    oc, sd = O.cfg_from_head_cfg(cfg), S.head_state_dict(head)
+    x = S.synthetic_bev(1, 180, 180, seed=41)
+    head.to(dev)
+    xd = x.to(dev)
+    _case(dev, parity_log, "configs[1] lidar Nk=32400", head, lambda: head([xd], None, [dict()]),
+          lambda: O.head_forward(oc, sd, x, None, [dict()], "lidar", cross_core="fp16", epilogue=False))
+
+
+def test_fullsize_fusion_configs2(dev, parity_log):
+    from oracle import cmt_oracle as O
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=0, num_query=900)
+    oc, sd = O.cfg_from_head_cfg(cfg), S.head_state_dict(head)
+    x = S.synthetic_bev(1, 180, 180, seed=42)
+    xi = S.synthetic_img(6, 40, 100, seed=43)
+    metas = S.synthetic_metas(1, yaws=S.NUS_YAWS, seed=44)
+    head.to(dev)
+    xd, xid = x.to(dev), xi.to(dev)
+    _case(dev, parity_log, "configs[2] fusion Nk=56400", head, lambda: head([xd], [xid], metas),
+          lambda: O.head_forward(oc, sd, x, xi, metas, "fusion", cross_core="fp16", epilogue=False))
+
+
+def test_fullsize_coop_configs3(dev, parity_log):
+    from oracle import cmt_oracle as O
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmtcoop_fusion_tumtraf", seed=0, num_query=900)
+    oc, sd = O.cfg_from_head_cfg(cfg), S.head_state_dict(head)
+    xv, xr = S.synthetic_bev(1, 180, 180, seed=45), S.synthetic_bev(1, 180, 180, seed=46)
+    iv, ir = S.synthetic_img(1, 40, 100, seed=47), S.synthetic_img(3, 40, 100, seed=48)
+    mv = S.synthetic_metas(1, yaws=S.VEHICLE_YAWS, prefix="vehicle_", seed=49)
+    mi = S.synthetic_metas(1, yaws=S.INFRA_YAWS, prefix="infrastructure_", seed=50)
+    metas = [dict(mv[0], **mi[0])]
+    head.to(dev)
+    d = [t.to(dev) for t in (xv, xr, iv, ir)]
+    agents = [("vehicle_", xv, iv), ("infrastructure_", xr, ir)]
+    _case(dev, parity_log, "configs[3] coop Nk=36400+44400", head, lambda: head([d[0]], [d[1]], [d[2]], [d[3]], metas),
+          lambda: O.head_coop_forward(oc, sd, agents, metas, "fusion", cross_core="fp16", epilogue=False))
