@@ -267,6 +267,19 @@ constexpr int RING = 4;
 typedef const __attribute__((address_space(1))) void* gaddr_t;
 typedef __attribute__((address_space(3))) void* laddr_t;
 
+// One 16-byte-per-lane LDS-DMA piece (global_load_lds_dwordx4, 1 KB per wave)
+// issued from inline asm.  Issued through the builtin, the compiler's waitcnt
+// pass treats every later ds_read as a possible reader of the DMA'd bytes and
+// puts an s_waitcnt vmcnt(0) in front of it (observed before the transposed V
+// reads: it drained the whole K/V prefetch ring every tile).  As asm the DMA
+// is invisible to that pass; the kernels order it themselves with counted
+// vmcnt waits + barriers (which over-wait, never under-wait, for the
+// compiler's own loads: in-order completion).
+__device__ __forceinline__ void dma16(const void* g, const void* lds_base) {
+    const uint32_t m = (uint32_t)(uintptr_t)(laddr_t)lds_base;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m) : "memory", "m0");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm() {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
@@ -581,8 +594,10 @@ __device__ __forceinline__ void pp_wait(int tiles) {
     else pp_wait_n<0>();
 }
 
-template <typename T, bool FOLD>
-__global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
+// OCC = workgroups per CU the register budget is sized for (1: <= 256 VGPRs,
+// 2: <= 128 VGPRs, 4 waves per SIMD)
+template <typename T, bool FOLD, int OCC>
+__global__ __launch_bounds__(512, 2 * OCC) void attn_pp_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
     constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
     __shared__ __attribute__((aligned(16))) T ring[PPR * STAGE];
@@ -676,8 +691,8 @@ __global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
     const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
     T* const my_k = ring + (wave & 3) * 16 * D;      // this wave's piece of slot 0 (K), + KT*D for V
     auto issue_next = [&](int slot) {
-        __builtin_amdgcn_global_load_lds((gaddr_t)ksrc, (laddr_t)(my_k + slot * STAGE), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gaddr_t)vsrc, (laddr_t)(my_k + slot * STAGE + KT * D), 16, 0, 0);
+        dma16(ksrc, my_k + slot * STAGE);
+        dma16(vsrc, my_k + slot * STAGE + KT * D);
         ksrc += kstep;
         vsrc += vstep;
     };
@@ -702,14 +717,14 @@ __global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
         if (!hb) pp_wait(min(nt - 1, PPR - 3));
         pp_barrier();
         if (!hb && PPR - 2 < nt) issue_next(PPR - 2);
-        pp_load_k<T>(rb, pp_launder(lane_ofs), kf);
+        pp_load_k<T>(rb, lane_ofs, kf);
         pp_mseg<T, true, false>(kf, vf, qf, negm, pf, s, o, lsum);
         // V(0)
         if (!hb && nt > 1) pp_wait(min(nt - 1, PPR - 2) - 1);
         pp_barrier();
         pp_vseg<T, FOLD>(s, pf, o, lsum, negm, m_run, online, true, c);
         {
-            const PpLane l = pp_launder(lane_ofs);
+            const PpLane l = lane_ofs;
             pp_load_k<T>(rb + 1 * STAGE_B, l, kf);   // stale (unused) when nt == 1
             pp_load_v<T>(rb + KV_B, l, vf);
         }
@@ -727,7 +742,7 @@ __global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
             kslot = kslot == PPR - 1 ? 0 : kslot + 1;
             vslot = vslot == PPR - 1 ? 0 : vslot + 1;
             islot = islot == PPR - 1 ? 0 : islot + 1;
-            const PpLane l = pp_launder(lane_ofs);
+            const PpLane l = lane_ofs;
             pp_load_k<T>(rb + kslot * STAGE_B, l, kf);
             pp_load_v<T>(rb + vslot * STAGE_B + KV_B, l, vf);
         }
@@ -744,8 +759,8 @@ __global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
             const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked in compute
             const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
             const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
-            __builtin_amdgcn_global_load_lds((gaddr_t)ks, (laddr_t)my_k, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gaddr_t)vs, (laddr_t)(my_k + KT * D), 16, 0, 0);
+            dma16(ks, my_k);
+            dma16(vs, my_k + KT * D);
             pp_wait_n<0>();
         }
         pp_barrier();
@@ -777,6 +792,312 @@ __global__ __launch_bounds__(512, 1) void attn_pp_kernel(AttnKParams p) {
         }
         if (lh == 0) {
             p.Mp[row] = FOLD ? m_run : m_run * c;   // exp2 units for the combine
+            p.Lp[row] = l_tot;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Offset-free ping-pong kernel: the bf16 long-key cross-attention with the
+// max-|k| partials (bounded mode).  Same ping-pong windows, LDS-DMA ring and
+// prefetched fragments as attn_pp_kernel; what differs:
+//  * no softmax offset on the fast path.  When every query of the wave has
+//    |q| max|k| <= kBoundMax (exp2 units; Q carries the folded scale), every
+//    score satisfies |s| <= 60, so P = exp2(s) lies in [2^-60, 2^60] -- a
+//    normal bf16 / f32 number whose relative rounding does not depend on its
+//    magnitude -- and O = sum(P V) / sum(P) needs no offset (it cancels).  The
+//    QK^T MFMAs start from a zero accumulator: no -m register block, no VALU
+//    subtraction, no max tree, no rescale.
+//  * a wave whose bound is larger tracks an online running max as ONE
+//    register per lane, subtracted on the VALU (exact lazy rescale, deferred
+//    by kDeferMax) -- the slow path, never taken on the decoder's data.
+//  * row sums: RSUM 0 on the MFMA pipe (ones . P^T), RSUM 1 as f32 VALU adds
+//    of P before rounding, RSUM 2 as v_dot2 of the rounded bf16 P; for 1 and 2
+//    each lane sums its own 32 keys of the tile (one register) and the lane
+//    pair is added once at the end.
+// ---------------------------------------------------------------------------
+template <int RSUM> struct pb_lsum { typedef float type; };
+template <> struct pb_lsum<0> { typedef f32x16 type; };
+
+template <typename T, bool QK, bool PV, int RSUM>
+__device__ __forceinline__ void pb_mseg(const typename mfma_traits<T>::frag (&kf)[2][2],
+                                        const typename mfma_traits<T>::frag (&vf)[2][2],
+                                        const typename mfma_traits<T>::frag (&qf)[2],
+                                        const typename mfma_traits<T>::frag (&pf)[2][2], f32x16 (&s)[2], f32x16& o,
+                                        typename pb_lsum<RSUM>::type& lsum) {
+    typedef typename mfma_traits<T>::frag frag;
+    if (QK) {
+        const f32x16 zero = {};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            s[kb] = mfma_traits<T>::mma(kf[kb][0], qf[0], zero);
+            s[kb] = mfma_traits<T>::mma(kf[kb][1], qf[1], s[kb]);
+        }
+    }
+    if (PV) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                o = mfma_traits<T>::mma(vf[kb][ss], pf[kb][ss], o);
+                if constexpr (RSUM == 0) {
+                    frag ones;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
+                    lsum = mfma_traits<T>::mma(ones, pf[kb][ss], lsum);
+                }
+            }
+    }
+}
+
+// V segment: P = exp2(s) (fast) or exp2(s - m) with the online max (fallback);
+// row sums for RSUM 1 / 2.  ``first``: the wave's first tile (sets m).
+template <typename T, int RSUM>
+__device__ __forceinline__ void pb_vseg(f32x16 (&s)[2], typename mfma_traits<T>::frag (&pf)[2][2], f32x16& o,
+                                        typename pb_lsum<RSUM>::type& lsum, float& m_run, bool fast, bool first) {
+    if (!fast) {
+        float m0 = vmax(s[0][0], s[0][1]), m1 = vmax(s[1][0], s[1][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            m0 = vmax3(m0, s[0][r], s[0][r + 1]);
+            m1 = vmax3(m1, s[1][r], s[1][r + 1]);
+        }
+        const float mt = pair_max(vmax(m0, m1));
+        if (first) {
+            m_run = mt;
+        } else if (__any(mt > m_run + kDeferMax)) {
+            const float mn = vmax(m_run, mt);
+            const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+            o *= alpha;
+            lsum *= alpha;
+            m_run = mn;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            s[0][r] -= m_run;
+            s[1][r] -= m_run;
+        }
+    }
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float e0 = __builtin_amdgcn_exp2f(s[0][r]);
+        const float e1 = __builtin_amdgcn_exp2f(s[1][r]);
+        pf[0][r >> 3][r & 7] = (T)e0;
+        pf[1][r >> 3][r & 7] = (T)e1;
+        if constexpr (RSUM == 1) {
+            a0 += e0;
+            a1 += e1;
+        }
+    }
+    if constexpr (RSUM == 1) lsum += a0 + a1;
+    if constexpr (RSUM == 2) {
+        typedef T t2 __attribute__((ext_vector_type(2)));
+        const t2 one2 = {(T)1.f, (T)1.f};
+        float acc = lsum;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const t2 pr = {pf[kb][ss][2 * j], pf[kb][ss][2 * j + 1]};
+                    if constexpr (std::is_same<T, bf16_t>::value)
+                        acc = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, acc, false);
+                    else
+                        acc = __builtin_amdgcn_fdot2(pr, one2, acc, false);
+                }
+        lsum = acc;
+    }
+}
+
+template <typename T, int RSUM, int OCC>
+__global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    typedef typename pb_lsum<RSUM>::type LT;
+    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
+    __shared__ __attribute__((aligned(16))) T ring[PPR * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool hb = wave >= 4;          // wave-uniform: second half runs one segment behind
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+
+    // XCD-aware block order (as attn_pp_kernel)
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int qb = wg % p.nqb;
+    const int rest = wg / p.nqb;
+    const int BH = p.B * p.H;
+    const int bh = rest % BH;
+    const int split = rest / BH;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+
+    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+    const float c = p.c;
+
+    // ---- Q^T fragments with the folded scale (s is in exp2 units)
+    const int q = qb * (8 * QW) + wave * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    frag qf[2];
+    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
+
+    // ---- fast path iff |q| max|k| <= kBoundMax for every query of the wave
+    bool fast;
+    {
+        const int64_t r0 = (int64_t)b * p.Nk;
+        const int e0 = (int)(r0 / p.kmax_rows), e1 = (int)((r0 + p.Nk - 1) / p.kmax_rows);
+        float km = 0.f;
+        for (int e = e0 + lane; e <= e1; e += 64) km = fmaxf(km, p.kmax2[(int64_t)e * p.kmax_ld + p.kmax_plane0 + h]);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
+        float qq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
+        qq = pair_sum(qq);
+        // km is the max squared norm of the UNSCALED keys; q already carries c
+        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
+        fast = __all(bound <= kBoundMax);
+    }
+
+    f32x16 o;
+    LT lsum;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    lsum = LT{};
+    float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tile
+
+    const int ntiles = (p.Nk + KT - 1) / KT;
+    const int t_begin = split * p.tiles_per_split;
+    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+    const bool tail = (p.Nk % KT) != 0 && t_end == ntiles && t_begin < t_end;   // ragged last tile here
+    const int nt = max(0, t_end - t_begin - (tail ? 1 : 0));                    // full tiles
+
+    const int crow = lane >> 2, cch = lane & 3;
+    const int prow = (wave & 3) * 16 + crow;
+    const T* ksrc = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+    const T* vsrc = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
+    const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
+    T* const my_k = ring + (wave & 3) * 16 * D;
+    auto issue_next = [&](int slot) {
+        dma16(ksrc, my_k + slot * STAGE);
+        dma16(vsrc, my_k + slot * STAGE + KT * D);
+        ksrc += kstep;
+        vsrc += vstep;
+    };
+
+    const char* const rb = (const char*)ring;
+    constexpr int STAGE_B = STAGE * (int)sizeof(T), KV_B = KT * D * (int)sizeof(T);
+    const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
+    f32x16 s[2];
+    frag pf[2][2], kf[2][2], vf[2][2];
+    if (!hb) {
+#pragma unroll
+        for (int i = 0; i < PPR - 2; ++i)
+            if (i < nt) issue_next(i);
+    } else {
+        pp_barrier();   // half B: one segment behind
+    }
+    if (nt > 0) {
+        if (!hb) pp_wait(min(nt - 1, PPR - 3));
+        pp_barrier();
+        if (!hb && PPR - 2 < nt) issue_next(PPR - 2);
+        pp_load_k<T>(rb, lane_ofs, kf);
+        pb_mseg<T, true, false, RSUM>(kf, vf, qf, pf, s, o, lsum);
+        if (!hb && nt > 1) pp_wait(min(nt - 1, PPR - 2) - 1);
+        pp_barrier();
+        pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, true);
+        {
+            const PpLane l = lane_ofs;
+            pp_load_k<T>(rb + 1 * STAGE_B, l, kf);   // stale (unused) when nt == 1
+            pp_load_v<T>(rb + KV_B, l, vf);
+        }
+        int kslot = 1, vslot = 0, islot = PPR - 1;
+        for (int i = 1; i < nt; ++i) {
+            pp_barrier();
+            if (!hb && i + PPR - 2 < nt) issue_next(islot);
+            pb_mseg<T, true, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
+            if (!hb && i + 1 < nt) pp_wait(min(nt - 1, i + PPR - 2) - (i + 1));
+            pp_barrier();
+            pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, false);
+            kslot = kslot == PPR - 1 ? 0 : kslot + 1;
+            vslot = vslot == PPR - 1 ? 0 : vslot + 1;
+            islot = islot == PPR - 1 ? 0 : islot + 1;
+            const PpLane l = lane_ofs;
+            pp_load_k<T>(rb + kslot * STAGE_B, l, kf);
+            pp_load_v<T>(rb + vslot * STAGE_B + KV_B, l, vf);
+        }
+        pp_barrier();
+        pb_mseg<T, false, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
+    }
+    if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
+
+    if (tail) {
+        // ragged last tile: masked, every wave at once
+        pp_barrier();
+        if (!hb) {
+            const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked below
+            const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+            const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
+            dma16(ks, my_k);
+            dma16(vs, my_k + KT * D);
+            pp_wait_n<0>();
+        }
+        pp_barrier();
+        const PpLane l = lane_ofs;
+        pp_load_k<T>(rb, l, kf);
+        pp_load_v<T>(rb + KV_B, l, vf);
+        pb_mseg<T, true, false, RSUM>(kf, vf, qf, pf, s, o, lsum);
+        const int key0 = (ntiles - 1) * KT;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s[kb][r] = -__builtin_inff();
+        pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, nt == 0);
+        pb_mseg<T, false, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
+    }
+
+    // ---- write ---------------------------------------------------------------
+    float l_tot;
+    if constexpr (RSUM == 0) l_tot = lsum[0];
+    else l_tot = pair_sum(lsum);
+    if (q >= p.Nq) return;
+    if (p.splits == 1) {
+        const float inv = 1.f / l_tot;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+            if (p.round_out) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+            }
+            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
+        }
+    } else {
+        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
+        float* dst = p.Op + row * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+        if (lh == 0) {
+            p.Mp[row] = m_run;   // exp2 units (0 on the fast path)
             p.Lp[row] = l_tot;
         }
     }
@@ -1008,11 +1329,29 @@ LowpShape lowp_shape(const cmt_attn_args& a) {
 
 // The ping-pong kernel takes the 8 x 1 shape (long key ranges); CMT_ATTN_PP=0
 // selects the single-phase 8 x 1 kernel instead (diagnostics / A-B timing).
+// offset-free bounded kernel (attn_pb_kernel): workgroups per CU it is built
+// for (CMT_ATTN_OCC) and its row-sum form (CMT_ATTN_RSUM); diagnostics knobs
+int pp_occ() {
+    static const char* ov = getenv("CMT_ATTN_OCC");
+    return (ov && ov[0] == '2') ? 2 : 1;
+}
+int pb_rsum() {
+    static const char* ov = getenv("CMT_ATTN_RSUM");
+    return (ov && ov[0] >= '0' && ov[0] <= '2') ? ov[0] - '0' : 0;
+}
+
 bool use_pp(const cmt_attn_args& a) {
     static const char* ov = getenv("CMT_ATTN_PP");
     if (ov && ov[0] == '0') return false;
     const LowpShape sh = lowp_shape(a);
     return a.dtype != CMT_F32 && sh.waves == 8 && sh.sub == 1;
+}
+
+// the bf16 long-key path with max-|k| partials and the folded scale
+bool use_pb(const cmt_attn_args& a) {
+    static const char* ov = getenv("CMT_ATTN_PB");
+    if (ov && ov[0] == '0') return false;
+    return use_pp(a) && a.dtype == CMT_BF16 && a.kmax2 != nullptr && (a.flags & CMT_ATTN_FOLD_SCALE);
 }
 
 int choose_splits(const cmt_attn_args& a) {
@@ -1026,7 +1365,8 @@ int choose_splits(const cmt_attn_args& a) {
     // aim for >= 2048 waves (two per SIMD) while keeping >= 8 tiles per split;
     // short key ranges (self-attention) split down to 2 tiles per split
     const int min_tiles = ntiles >= 64 ? 8 : 2;
-    while ((int64_t)base * s * nw < 2048 && ntiles / (2 * s) >= min_tiles) s *= 2;
+    const int64_t target = use_pb(a) ? 2048 * pp_occ() : 2048;
+    while ((int64_t)base * s * nw < target && ntiles / (2 * s) >= min_tiles) s *= 2;
     return s;
 }
 
@@ -1107,12 +1447,22 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
     } else if (use_pp(a)) {
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
-        if (a.dtype == CMT_F16) {
-            if (fold) attn_pp_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);
-            else attn_pp_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
+        if (use_pb(a)) {
+            const int rs = pb_rsum();
+#define PB_LAUNCH(OCC)                                                                                    \
+    do {                                                                                                  \
+        if (rs == 1) attn_pb_kernel<bf16_t, 1, OCC><<<nwg, 512, 0, s>>>(p);                                \
+        else if (rs == 2) attn_pb_kernel<bf16_t, 2, OCC><<<nwg, 512, 0, s>>>(p);                           \
+        else attn_pb_kernel<bf16_t, 0, OCC><<<nwg, 512, 0, s>>>(p);                                        \
+    } while (0)
+            if (pp_occ() == 2) PB_LAUNCH(2); else PB_LAUNCH(1);
+#undef PB_LAUNCH
+        } else if (a.dtype == CMT_F16) {
+            if (fold) attn_pp_kernel<f16_t, true, 1><<<nwg, 512, 0, s>>>(p);
+            else attn_pp_kernel<f16_t, false, 1><<<nwg, 512, 0, s>>>(p);
         } else {
-            if (fold) attn_pp_kernel<bf16_t, true><<<nwg, 512, 0, s>>>(p);
-            else attn_pp_kernel<bf16_t, false><<<nwg, 512, 0, s>>>(p);
+            if (fold) attn_pp_kernel<bf16_t, true, 1><<<nwg, 512, 0, s>>>(p);
+            else attn_pp_kernel<bf16_t, false, 1><<<nwg, 512, 0, s>>>(p);
         }
     } else if (a.dtype == CMT_F16) {
         ATTN_LAUNCH(f16_t);

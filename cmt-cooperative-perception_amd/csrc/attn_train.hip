@@ -1,0 +1,459 @@
+// Attention forward-with-statistics and backward for the training path
+// (exact f32, v_mfma_f32_32x32x2_f32, head_dim 32).  Reference: the
+// self-attention nn.MultiheadAttention (mmcv MultiheadAttention, with the
+// training-time DN mask of cmt_head.py:386-398 and attn_drop) and the
+// FlashMHA cross-attention core (attention.py:46-92, flash-attn 0.2.2 fp16
+// core: fp16_inputs rounds q, k, v, P and O to fp16 as that core does).
+//
+// Forward: one wave per 32 queries, 4 waves per workgroup share 64-key K/V
+// tiles in LDS (padded rows), swapped S^T = K Q^T so a lane owns one query,
+// online softmax in exp2 units, key range split over workgroups (combine
+// kernel) so ~1000-query problems fill the chip.  Writes O and the row
+// statistic LSE2 = m + log2(l) (exp2 units of c = scale * log2 e).
+//
+// Backward (flash-style, P recomputed from LSE2, delta = rowsum(dO * O)):
+//   dq kernel   one wave per 32 queries over a key slice:  S^T, dP^T = V dO^T,
+//               dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T  (f32 atomics into dQ
+//               when the key range is split)
+//   dkv kernel  one wave per 32 keys over all queries: S = Q K^T, dV^T += dO^T P,
+//               dP = dO V^T, dS = P (dP - delta), dK^T += Q^T dS
+// Every product is a chain of 32x32x2 MFMAs whose accumulator layout is the
+// next product's B operand (lane = the free index, register pairs = the
+// contraction index), so no tile is transposed through LDS.
+//
+// DN mask (dn_pad > 0): key k is hidden from query q if k < dn_pad and
+// (q >= dn_pad or k / dn_group != q / dn_group).  Dropout (p > 0) keeps
+// P(q, k) with probability 1 - p by a counter hash of (seed, b, h, q, k),
+// recomputed identically in the backward.
+#include "cmt_common.h"
+
+namespace {
+
+constexpr int D = 32;
+constexpr int KT = 64;
+constexpr int LDK = 36;      // padded f32 LDS row
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AP {                  // device-side copy of cmt_attn_train_args + derived values
+    cmt_attn_train_args a;
+    float c;                 // scale * log2(e)
+    int tiles_per_split;
+    float keep_scale;        // 1 / (1 - p)
+    uint32_t drop_thr;       // keep iff hash >= thr
+};
+
+__device__ __forceinline__ float r16(float x) { return (float)(_Float16)x; }
+
+__device__ __forceinline__ bool masked(const cmt_attn_train_args& a, int q, int k) {
+    if (a.dn_pad <= 0 || k >= a.dn_pad) return false;
+    return q >= a.dn_pad || (k / a.dn_group) != (q / a.dn_group);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ bool keep(const AP& p, int bh, int q, int k) {
+    uint32_t h = mix32(p.a.seed ^ mix32((uint32_t)bh * 0x9e3779b9U + (uint32_t)q));
+    h = mix32(h ^ (uint32_t)k * 0x85ebca6bU);
+    return h >= p.drop_thr;
+}
+
+__device__ __forceinline__ int key_of(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
+
+// stage a 64-row x 32 tile of X (row stride rs) into LDS rows of LDK floats
+__device__ __forceinline__ void stage64(float* lds, const float* X, int64_t rs, int r0, int nrows, bool f16, int tid) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int r = idx >> 3, c = (idx & 7) * 4;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (r0 + r < nrows) v = *(const f32x4*)(X + (int64_t)(r0 + r) * rs + c);
+        if (f16)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = r16(v[j]);
+        *(f32x4*)(lds + r * LDK + c) = v;
+    }
+}
+
+// acc (+)= X_rows . Y^T over d: lane supplies row (l & 31) of X (LDS, 32 rows
+// starting at xr) and Y fragments yf[4] (its own row, d = 16*lh + 4i + j)
+__device__ __forceinline__ void mma_rows(f32x16& acc, const float* xrow, const f32x4 (&yf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f32x4 xv = *(const f32x4*)(xrow + 4 * i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[j], yf[i][j], acc, 0, 0, 0);
+    }
+}
+
+// acc^T[d][col] += sum_k Z[k][d] * W[k][col] where W is an accumulator tile
+// (lane = col, register r <-> k = key_of(r, lh) + base) and Z rows are in LDS
+__device__ __forceinline__ void mma_acc(f32x16& acc, const float* zbase, const f32x16& w, int lane) {
+    const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(zbase[key_of(r, lh) * LDK + lr], w[r], acc, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void train_fwd_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) float Ks[KT * LDK];
+    __shared__ __attribute__((aligned(16))) float Vs[KT * LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H, split = blockIdx.z;
+    const bool f16 = a.fp16_inputs != 0;
+    const float* Qb = a.Q + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
+    const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
+    const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const int qc = min(q, a.Nq - 1);
+    f32x4 qf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        qf[i] = *(const f32x4*)(Qb + (int64_t)qc * a.q_rs + 16 * lh + 4 * i);
+        if (f16)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) qf[i][j] = r16(qf[i][j]);
+    }
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int t0 = split * p.tiles_per_split, t1 = min(ntiles, t0 + p.tiles_per_split);
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    float m_run = -__builtin_inff(), l_run = 0.f;
+    for (int t = t0; t < t1; ++t) {
+        __syncthreads();
+        stage64(Ks, Kb, a.k_rs, t * KT, a.Nk, f16, tid);
+        stage64(Vs, Vb, a.v_rs, t * KT, a.Nk, f16, tid);
+        __syncthreads();
+        f32x16 s[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+            mma_rows(s[kb], Ks + (kb * 32 + lr) * LDK + 16 * lh, qf);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = t * KT + kb * 32 + key_of(r, lh);
+                s[kb][r] = (k >= a.Nk || masked(a, q, k)) ? -__builtin_inff() : s[kb][r] * p.c;
+            }
+        }
+        float mt = -__builtin_inff();
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kb][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_run, mt);
+        const float m_use = m_new == -__builtin_inff() ? 0.f : m_new;   // fully masked so far
+        const float alpha = exp2f(m_run - m_use);
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = exp2f(s[kb][r] - m_use);
+                ls += e;
+                float pe = f16 ? r16(e) : e;
+                if (a.dropout_p > 0.f) {
+                    const int k = t * KT + kb * 32 + key_of(r, lh);
+                    pe = keep(p, bh, q, k) ? pe * p.keep_scale : 0.f;
+                }
+                s[kb][r] = pe;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) mma_acc(o, Vs + kb * 32 * LDK, s[kb], lane);
+    }
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    if (q >= a.Nq) return;
+    if (a.kv_splits <= 1) {
+        const float inv = 1.f / l_tot;
+        float* Ob = a.O + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs + (int64_t)q * a.o_rs;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float v = o[r] * inv;
+            Ob[key_of(r, lh)] = f16 ? r16(v) : v;
+        }
+        if (lh == 0) a.LSE[(int64_t)bh * a.Nq + q] = m_run + log2f(l_tot);
+    } else {
+        float* ws = (float*)a.workspace;
+        const int64_t rows = (int64_t)a.B * a.H * a.Nq;
+        const int64_t row = (int64_t)split * rows + (int64_t)bh * a.Nq + q;
+        float* Op = ws + row * D;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Op[key_of(r, lh)] = o[r];
+        if (lh == 0) {
+            ws[(int64_t)a.kv_splits * rows * D + row] = m_run;
+            ws[(int64_t)a.kv_splits * rows * (D + 1) + row] = l_tot;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void train_combine_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    const int64_t rows = (int64_t)a.B * a.H * a.Nq;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rows * D) return;
+    const int64_t row = i / D;
+    const int d = (int)(i - row * D);
+    const float* ws = (const float*)a.workspace;
+    const int S = a.kv_splits;
+    float M = -__builtin_inff();
+    for (int s = 0; s < S; ++s) {
+        const float l = ws[(int64_t)S * rows * (D + 1) + s * rows + row];
+        if (l > 0.f) M = fmaxf(M, ws[(int64_t)S * rows * D + s * rows + row]);
+    }
+    float num = 0.f, den = 0.f;
+    for (int s = 0; s < S; ++s) {
+        const float l = ws[(int64_t)S * rows * (D + 1) + s * rows + row];
+        if (!(l > 0.f)) continue;
+        const float w = exp2f(ws[(int64_t)S * rows * D + s * rows + row] - M);
+        num += w * ws[(s * rows + row) * D + d];
+        den += w * l;
+    }
+    const int bh = (int)(row / a.Nq), q = (int)(row - (int64_t)bh * a.Nq);
+    const int b = bh / a.H, h = bh - b * a.H;
+    const float v = num / den;
+    a.O[(int64_t)b * a.o_bs + (int64_t)h * a.o_hs + (int64_t)q * a.o_rs + d] = a.fp16_inputs ? r16(v) : v;
+    if (d == 0) a.LSE[row] = M + log2f(den);
+}
+
+// delta[b,h,q] = sum_d dO * O
+__global__ __launch_bounds__(256) void train_delta_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= (int64_t)a.B * a.H * a.Nq) return;
+    const int bh = (int)(row / a.Nq), q = (int)(row - (int64_t)bh * a.Nq);
+    const int b = bh / a.H, h = bh - b * a.H;
+    const int64_t off = (int64_t)b * a.o_bs + (int64_t)h * a.o_hs + (int64_t)q * a.o_rs;
+    float v = lane < D ? a.dO[off + lane] * a.O[off + lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) a.delta[row] = v;
+}
+
+// dQ: waves own 32 queries; key tiles [t0, t1) of this split; f32 atomics into dQ
+__global__ __launch_bounds__(256) void train_dq_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) float Ks[KT * LDK];
+    __shared__ __attribute__((aligned(16))) float Vs[KT * LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H, split = blockIdx.z;
+    const bool f16 = a.fp16_inputs != 0;
+    const float* Qb = a.Q + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
+    const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
+    const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
+    const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const int qc = min(q, a.Nq - 1);
+    f32x4 qf[4], df[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        qf[i] = *(const f32x4*)(Qb + (int64_t)qc * a.q_rs + 16 * lh + 4 * i);
+        df[i] = *(const f32x4*)(dOb + (int64_t)qc * a.o_rs + 16 * lh + 4 * i);
+        if (f16)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) qf[i][j] = r16(qf[i][j]);
+    }
+    const float lse = a.LSE[(int64_t)bh * a.Nq + qc];
+    const float dl = a.delta[(int64_t)bh * a.Nq + qc];
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int t0 = split * p.tiles_per_split, t1 = min(ntiles, t0 + p.tiles_per_split);
+    f32x16 dq;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+    for (int t = t0; t < t1; ++t) {
+        __syncthreads();
+        stage64(Ks, Kb, a.k_rs, t * KT, a.Nk, f16, tid);
+        stage64(Vs, Vb, a.v_rs, t * KT, a.Nk, f16, tid);
+        __syncthreads();
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+            mma_rows(s, Ks + (kb * 32 + lr) * LDK + 16 * lh, qf);     // S^T  (lane = query)
+            mma_rows(dp, Vs + (kb * 32 + lr) * LDK + 16 * lh, df);    // dP^T = V dO^T
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = t * KT + kb * 32 + key_of(r, lh);
+                float pr = (k >= a.Nk || masked(a, q, k)) ? 0.f : exp2f(s[r] * p.c - lse);
+                float g = dp[r];
+                if (a.dropout_p > 0.f) g = keep(p, bh, q, k) ? g * p.keep_scale : 0.f;
+                s[r] = pr * (g - dl);                                    // dS^T
+            }
+            mma_acc(dq, Ks + kb * 32 * LDK, s, lane);                    // dQ^T += K^T dS^T
+        }
+    }
+    if (q >= a.Nq) return;
+    float* dQb = a.dQ + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs + (int64_t)q * a.q_rs;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float v = dq[r] * a.scale;
+        if (a.kv_splits > 1) atomicAdd(dQb + key_of(r, lh), v);
+        else dQb[key_of(r, lh)] = v;
+    }
+}
+
+// dK, dV: waves own 32 keys; loop over 64-query tiles (Q, dO, LSE2, delta in LDS)
+__global__ __launch_bounds__(256) void train_dkv_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) float Qs[KT * LDK];
+    __shared__ __attribute__((aligned(16))) float Ds[KT * LDK];
+    __shared__ float Ls[KT], Dl[KT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+    const bool f16 = a.fp16_inputs != 0;
+    const float* Qb = a.Q + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
+    const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
+    const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
+    const int k = blockIdx.x * 128 + wave * 32 + lr;
+    const int kc = min(k, a.Nk - 1);
+    f32x4 kf[4], vf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        kf[i] = *(const f32x4*)(Kb + (int64_t)kc * a.k_rs + 16 * lh + 4 * i);
+        vf[i] = *(const f32x4*)(Vb + (int64_t)kc * a.v_rs + 16 * lh + 4 * i);
+        if (f16)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { kf[i][j] = r16(kf[i][j]); vf[i][j] = r16(vf[i][j]); }
+    }
+    f32x16 dk, dv;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
+    const int nqt = (a.Nq + KT - 1) / KT;
+    for (int t = 0; t < nqt; ++t) {
+        __syncthreads();
+        stage64(Qs, Qb, a.q_rs, t * KT, a.Nq, f16, tid);
+        stage64(Ds, dOb, a.o_rs, t * KT, a.Nq, false, tid);
+        if (tid < KT) {
+            const int qq = min(t * KT + tid, a.Nq - 1);
+            Ls[tid] = a.LSE[(int64_t)bh * a.Nq + qq];
+            Dl[tid] = a.delta[(int64_t)bh * a.Nq + qq];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+            mma_rows(s, Qs + (qb * 32 + lr) * LDK + 16 * lh, kf);     // S = Q K^T (lane = key)
+            mma_rows(dp, Ds + (qb * 32 + lr) * LDK + 16 * lh, vf);    // dP = dO V^T
+            f32x16 pd;                                                 // dropped P (dV operand)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int qi = qb * 32 + key_of(r, lh), qq = t * KT + qi;
+                const bool valid = qq < a.Nq && k < a.Nk && !masked(a, qq, k);
+                const float pr = valid ? exp2f(s[r] * p.c - Ls[qi]) : 0.f;
+                float g = dp[r], pe = f16 ? r16(pr) : pr;
+                if (a.dropout_p > 0.f) {
+                    const bool kp = keep(p, bh, qq, k);
+                    g = kp ? g * p.keep_scale : 0.f;
+                    pe = kp ? pe * p.keep_scale : 0.f;
+                }
+                pd[r] = pe;
+                s[r] = pr * (g - Dl[qi]);                              // dS
+            }
+            mma_acc(dv, Ds + qb * 32 * LDK, pd, lane);                 // dV^T += dO^T P
+            mma_acc(dk, Qs + qb * 32 * LDK, s, lane);                  // dK^T += Q^T dS
+        }
+    }
+    if (k >= a.Nk) return;
+    float* dKb = a.dK + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs + (int64_t)k * a.k_rs;
+    float* dVb = a.dV + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs + (int64_t)k * a.v_rs;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        dKb[key_of(r, lh)] = dk[r] * a.scale;
+        dVb[key_of(r, lh)] = dv[r];
+    }
+}
+
+AP make_ap(const cmt_attn_train_args& a, int splits) {
+    AP p;
+    p.a = a;
+    p.a.kv_splits = splits;
+    p.c = a.scale * LOG2E;
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    p.tiles_per_split = cdiv(ntiles, splits);
+    p.keep_scale = a.dropout_p > 0.f ? 1.f / (1.f - a.dropout_p) : 1.f;
+    const double thr = (double)a.dropout_p * 4294967296.0;
+    p.drop_thr = thr >= 4294967295.0 ? 0xffffffffU : (uint32_t)thr;
+    return p;
+}
+
+int train_splits(const cmt_attn_train_args& a) {
+    if (a.kv_splits > 0) return a.kv_splits;
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int base = cdiv(a.Nq, 128) * a.B * a.H;
+    int s = 1;
+    while (base * s < 512 && ntiles / (2 * s) >= 4) s *= 2;
+    return s;
+}
+
+int check_args(const cmt_attn_train_args& a, const char* who) {
+    CMT_REQUIRE(a.B > 0 && a.H > 0 && a.Nq > 0 && a.Nk > 0, std::string(who) + ": empty problem");
+    CMT_REQUIRE(a.Q && a.K && a.V && a.O && a.LSE, std::string(who) + ": null pointer");
+    CMT_REQUIRE(a.q_rs % 4 == 0 && a.k_rs % 4 == 0 && a.v_rs % 4 == 0 && a.o_rs % 4 == 0 && a.q_hs % 4 == 0 &&
+                a.k_hs % 4 == 0 && a.v_hs % 4 == 0 && a.q_bs % 4 == 0 && a.k_bs % 4 == 0 && a.v_bs % 4 == 0,
+                std::string(who) + ": strides must keep 16-byte rows");
+    CMT_REQUIRE(a.dn_pad <= 0 || a.dn_group > 0, std::string(who) + ": dn_group must be > 0 with dn_pad");
+    CMT_REQUIRE(a.dropout_p >= 0.f && a.dropout_p < 1.f, std::string(who) + ": dropout_p must be in [0, 1)");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int64_t cmt_attn_train_workspace_bytes(const cmt_attn_train_args* a) {
+    if (!a) return 0;
+    const int s = train_splits(*a);
+    if (s <= 1) return 0;
+    return (int64_t)s * a->B * a->H * a->Nq * (D + 2) * (int64_t)sizeof(float);
+}
+
+extern "C" int cmt_attn_train_fwd(const cmt_attn_train_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_attn_train_fwd: null args");
+    if (int rc = check_args(*ap, "cmt_attn_train_fwd")) return rc;
+    const int splits = train_splits(*ap);
+    if (splits > 1 && (ap->workspace == nullptr || ap->workspace_bytes < cmt_attn_train_workspace_bytes(ap)))
+        return cmt_fail(CMT_EWORKSPACE, "cmt_attn_train_fwd: workspace too small");
+    AP p = make_ap(*ap, splits);
+    hipStream_t s = (hipStream_t)stream;
+    train_fwd_kernel<<<dim3(cdiv(ap->Nq, 128), ap->B * ap->H, splits), 256, 0, s>>>(p);
+    if (splits > 1) {
+        const int64_t n = (int64_t)ap->B * ap->H * ap->Nq * D;
+        train_combine_kernel<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(p);
+    }
+    return cmt_check_launch("cmt_attn_train_fwd");
+}
+
+extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_attn_train_bwd: null args");
+    if (int rc = check_args(*ap, "cmt_attn_train_bwd")) return rc;
+    CMT_REQUIRE(ap->dO && ap->dQ && ap->dK && ap->dV && ap->delta, "cmt_attn_train_bwd: null gradient pointer");
+    const int ntiles = (ap->Nk + KT - 1) / KT;
+    const int base = cdiv(ap->Nq, 128) * ap->B * ap->H;
+    int qs = 1;   // key split of the dQ pass (atomics into a zeroed dQ)
+    while (base * qs < 1024 && ntiles / (2 * qs) >= 2) qs *= 2;
+    AP p = make_ap(*ap, qs);
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t rows = (int64_t)ap->B * ap->H * ap->Nq;
+    train_delta_kernel<<<(unsigned)cdiv64(rows, 4), 256, 0, s>>>(p);
+    if (qs > 1) {
+        // dQ is accumulated: zero it (its [Nq x 32] rows per (b, h), strided)
+        for (int b = 0; b < ap->B; ++b)
+            for (int h = 0; h < ap->H; ++h)
+                hipMemset2DAsync(ap->dQ + (int64_t)b * ap->q_bs + (int64_t)h * ap->q_hs, ap->q_rs * sizeof(float), 0,
+                                 D * sizeof(float), ap->Nq, s);
+    }
+    train_dq_kernel<<<dim3(cdiv(ap->Nq, 128), ap->B * ap->H, qs), 256, 0, s>>>(p);
+    train_dkv_kernel<<<dim3(cdiv(ap->Nk, 128), ap->B * ap->H), 256, 0, s>>>(p);
+    return cmt_check_launch("cmt_attn_train_bwd");
+}

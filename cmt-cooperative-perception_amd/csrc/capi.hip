@@ -34,3 +34,10 @@ extern "C" int64_t cmt_chain_ws_bytes(int rows) {
     if (rows <= 0) return 0;
     return (int64_t)4 * cdiv(rows, 32) * 32 * 256 * (int64_t)sizeof(float);
 }
+extern "C" int64_t cmt_gemm_ex_args_size(void) { return (int64_t)sizeof(cmt_gemm_ex_args); }
+extern "C" int64_t cmt_attn_train_args_size(void) { return (int64_t)sizeof(cmt_attn_train_args); }
+extern "C" int64_t cmt_ln_train_args_size(void) { return (int64_t)sizeof(cmt_ln_train_args); }
+extern "C" int64_t cmt_bn_args_size(void) { return (int64_t)sizeof(cmt_bn_args); }
+extern "C" int64_t cmt_det_loss_args_size(void) { return (int64_t)sizeof(cmt_det_loss_args); }
+extern "C" int64_t cmt_match_cost_args_size(void) { return (int64_t)sizeof(cmt_match_cost_args); }
+extern "C" int64_t cmt_adamw_args_size(void) { return (int64_t)sizeof(cmt_adamw_args); }

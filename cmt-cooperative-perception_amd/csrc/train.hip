@@ -1,0 +1,532 @@
+// Training-path kernels of the CMT / CMTCoop head for gfx950 (SURVEY.md
+// 8(f) next #2; reference training step: cmt_head.py:339-415 DN queries,
+// 556-903 losses, 68-81 GroupLayerNorm1d backward; torch autograd + mmcv
+// optimizer hook for the rest).  Exact-f32 throughout (the reference trains
+// the head in fp32: custom_fp16 keeps pts_bbox_head fp32):
+//
+//   cmt_gemm_f32_ex      general-stride GEMM on v_mfma_f32_32x32x2_f32 (any
+//                        operand transposed, batched, split-K by f32 atomics):
+//                        every Linear forward / dX / dW of the training step
+//   cmt_ln_train_fwd/bwd row LayerNorm (C = 64 / 256) with saved mean/rstd,
+//                        dW / dB sums; C = 64 with per-row-group weights is
+//                        the task heads' GroupLayerNorm1d (eps 1e-6)
+//   cmt_bn_relu_train    BatchNorm2d (batch statistics) + ReLU on NHWC rows,
+//                        running-stat update; and its backward
+//   cmt_im2col3x3        the shared_conv input gather for the weight gradient
+//   cmt_det_loss         FocalLoss (sigmoid) + L1Loss values and input grads
+//   cmt_match_cost       FocalLossCost + BBox3DL1Cost matrix of the Hungarian
+//                        assigner (hungarian_assigner_3d.py:68-156)
+//   cmt_adamw_step       torch AdamW step over one flat parameter buffer with
+//                        clip_grad_norm_ (mmcv OptimizerHook grad_clip)
+//   cmt_sumsq            partial sums of squares (the clip's global norm)
+#include "cmt_common.h"
+
+namespace {
+
+constexpr int TBK = 32;     // k-step
+constexpr int TLD = 36;     // padded LDS row (floats)
+constexpr int TNT = 256;
+
+enum { OP_KC = 0, OP_MC = 1, OP_SC = 2 };   // k-contiguous, row(m/n)-contiguous, scalar
+
+// Stage a 64-row x 32-k tile of X (rows r0.., k0..) into LDS [row][TLD]:
+// element (r, k) at X[r * s_r + k * s_k].
+template <int MODE>
+__device__ __forceinline__ void stage_tile(float* __restrict__ lds, const float* __restrict__ X, int64_t s_r,
+                                           int64_t s_k, int rows, int K, int r0, int k0, int tid) {
+    if (MODE == OP_KC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int r = idx >> 3, c = (idx & 7) * 4;
+            const int gr = r0 + r, gk = k0 + c;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (gr < rows) {
+                const float* p = X + (int64_t)gr * s_r + gk;
+                if (gk + 3 < K) v = *(const f32x4*)p;
+                else
+                    for (int j = 0; j < 4; ++j) v[j] = gk + j < K ? p[j] : 0.f;
+            }
+            *(f32x4*)(lds + r * TLD + c) = v;
+        }
+    } else if (MODE == OP_MC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int gr = r0 + r, gk = k0 + k;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (gk < K) {
+                const float* p = X + (int64_t)gk * s_k + gr;
+                if (gr + 3 < rows) v = *(const f32x4*)p;
+                else
+                    for (int j = 0; j < 4; ++j) v[j] = gr + j < rows ? p[j] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) lds[(r + j) * TLD + k] = v[j];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int idx = tid + TNT * i;
+            const int r = idx >> 5, k = idx & 31;
+            const int gr = r0 + r, gk = k0 + k;
+            lds[r * TLD + k] = (gr < rows && gk < K) ? X[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
+        }
+    }
+}
+
+template <int AM, int BM>
+__global__ __launch_bounds__(TNT) void gemm_ex_kernel(cmt_gemm_ex_args a, int kchunk) {
+    __shared__ __attribute__((aligned(16))) float As[64 * TLD];
+    __shared__ __attribute__((aligned(16))) float Bs[64 * TLD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
+    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    const int z = blockIdx.z / a.ksplit, ks = blockIdx.z - z * a.ksplit;
+    const float* A = a.A + (int64_t)z * a.a_bs;
+    const float* B = a.B + (int64_t)z * a.b_bs;
+    const int kb = ks * kchunk, ke = min(a.K, kb + kchunk);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int k0 = kb; k0 < ke; k0 += TBK) {
+        __syncthreads();
+        stage_tile<AM>(As, A, a.a_sm, a.a_sk, a.M, ke, m0, k0, tid);
+        stage_tile<BM>(Bs, B, a.b_sn, a.b_sk, a.N, ke, n0, k0, tid);
+        __syncthreads();
+        const float* ar = As + (wm * 32 + lr) * TLD + 16 * lh;
+        const float* br = Bs + (wn * 32 + lr) * TLD + 16 * lh;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const f32x4 av = *(const f32x4*)(ar + 4 * c);
+            const f32x4 bv = *(const f32x4*)(br + 4 * c);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bv[t], acc, 0, 0, 0);
+        }
+    }
+    float* C = a.C + (int64_t)z * a.c_bs;
+    const int col = n0 + wn * 32 + lr;
+    if (col >= a.N) return;
+    const float bias = (a.bias && ks == 0) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= a.M) continue;
+        float* c = C + (int64_t)row * a.ldc + col;
+        const float v = a.alpha * acc[r] + bias;
+        if (a.ksplit > 1) atomicAdd(c, v);
+        else *c = a.beta != 0.f ? v + a.beta * *c : v;
+    }
+}
+
+int op_mode(int64_t s_row, int64_t s_k, const float* p) {
+    const bool al = ((uintptr_t)p & 15) == 0;
+    if (s_k == 1 && s_row % 4 == 0 && al) return OP_KC;
+    if (s_row == 1 && s_k % 4 == 0 && al) return OP_MC;
+    return OP_SC;
+}
+
+// ---------------------------------------------------------------------------
+// Row LayerNorm, C = 64 or 256: one wave per row, C/64 elements per lane.
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(cmt_ln_train_args a) {
+    constexpr int E = C / 64;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= a.rows) return;
+    const int g = a.rows_per_wset > 0 ? row / a.rows_per_wset : 0;
+    const float* x = a.X + (int64_t)row * a.ldx;
+    float v[E], s = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { v[e] = x[lane + 64 * e]; s += v[e]; }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { const float d = v[e] - mean; q += d * d; }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = 1.f / sqrtf(q / C + a.eps);
+    float* y = a.Y + (int64_t)row * a.ldy;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int c = lane + 64 * e;
+        y[c] = (v[e] - mean) * rstd * a.W[g * C + c] + a.B[g * C + c];
+    }
+    if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+}
+
+// dx = rstd * (gw - mean(gw) - xhat * mean(gw * xhat)), gw = dy * w;
+// dW[g] += sum dy * xhat, dB[g] += sum dy over the rows of weight set g.
+template <int C>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(cmt_ln_train_args a) {
+    constexpr int E = C / 64;
+    const int lane = threadIdx.x & 63;
+    const int w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nw = gridDim.x * 4;
+    float dw[E], db[E];
+    int cur_g = -1;
+    auto flush = [&]() {
+        if (cur_g < 0) return;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (a.dW) atomicAdd(a.dW + cur_g * C + lane + 64 * e, dw[e]);
+            if (a.dB) atomicAdd(a.dB + cur_g * C + lane + 64 * e, db[e]);
+        }
+    };
+    for (int row = w0; row < a.rows; row += nw) {
+        const int g = a.rows_per_wset > 0 ? row / a.rows_per_wset : 0;
+        if (g != cur_g) {
+            flush();
+            cur_g = g;
+#pragma unroll
+            for (int e = 0; e < E; ++e) dw[e] = db[e] = 0.f;
+        }
+        const float* x = a.X + (int64_t)row * a.ldx;
+        const float* dy = a.dY + (int64_t)row * a.ldy;
+        const float mean = a.mean[row], rstd = a.rstd[row];
+        float xh[E], gw[E], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int c = lane + 64 * e;
+            xh[e] = (x[c] - mean) * rstd;
+            const float d = dy[c];
+            gw[e] = d * a.W[g * C + c];
+            s1 += gw[e];
+            s2 += gw[e] * xh[e];
+            dw[e] += d * xh[e];
+            db[e] += d;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) { s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); }
+        s1 /= C;
+        s2 /= C;
+        float* dx = a.dX + (int64_t)row * a.lddx;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int c = lane + 64 * e;
+            const float v = rstd * (gw[e] - s1 - xh[e] * s2);
+            dx[c] = a.accumulate ? dx[c] + v : v;
+        }
+    }
+    flush();
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm2d (training: batch statistics over all rows) + ReLU on [rows][C]
+// NHWC rows.  Column sums by 256-row slabs + f32 atomics (two passes: mean,
+// then centred squares).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ X, int rows, int C,
+                                                      const float* __restrict__ shift, float* __restrict__ out,
+                                                      int squares, int rows_per_block) {
+    const int c = blockIdx.y * 256 + threadIdx.x;
+    if (c >= C) return;
+    const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+    const float sh = shift ? shift[c] : 0.f;
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) {
+        const float v = X[(int64_t)r * C + c] - sh;
+        s += squares ? v * v : v;
+    }
+    atomicAdd(out + c, s);
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(cmt_bn_args a, const float* __restrict__ sums) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= a.C) return;
+    const float var = sums[c] / a.rows;   // biased (normalisation)
+    a.mean_save[c] = sums[a.C + c];        // the shift = batch mean (first pass)
+    a.rstd_save[c] = 1.f / sqrtf(var + a.eps);
+    if (a.running_mean) {
+        const float unb = a.rows > 1 ? var * a.rows / (a.rows - 1) : var;
+        a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * sums[a.C + c];
+        a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
+    }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(float* x, int n, float s) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] *= s;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(cmt_bn_args a) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)a.rows * a.C) return;
+    const int c = (int)(i % a.C);
+    const float v = (a.X[i] - a.mean_save[c]) * a.rstd_save[c] * a.W[c] + a.B[c];
+    a.Y[i] = fmaxf(v, 0.f);
+}
+
+// backward: g = dY * (Y > 0); sums[0:C] = sum g, sums[C:2C] = sum g * xhat
+__global__ __launch_bounds__(256) void bn_bwd_sums_kernel(cmt_bn_args a, float* __restrict__ sums, int rpb) {
+    const int c = blockIdx.y * 256 + threadIdx.x;
+    if (c >= a.C) return;
+    const int r0 = blockIdx.x * rpb, r1 = min(a.rows, r0 + rpb);
+    const float mu = a.mean_save[c], rs = a.rstd_save[c];
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = r0; r < r1; ++r) {
+        const int64_t i = (int64_t)r * a.C + c;
+        const float g = a.Y[i] > 0.f ? a.dY[i] : 0.f;
+        s1 += g;
+        s2 += g * (a.X[i] - mu) * rs;
+    }
+    atomicAdd(sums + c, s1);
+    atomicAdd(sums + a.C + c, s2);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(cmt_bn_args a, const float* __restrict__ sums) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)a.rows * a.C) return;
+    const int c = (int)(i % a.C);
+    const float g = a.Y[i] > 0.f ? a.dY[i] : 0.f;
+    const float xh = (a.X[i] - a.mean_save[c]) * a.rstd_save[c];
+    const float n = (float)a.rows;
+    a.dX[i] = a.W[c] * a.rstd_save[c] / n * (n * g - sums[c] - xh * sums[a.C + c]);
+}
+
+__global__ __launch_bounds__(256) void bn_param_grads_kernel(cmt_bn_args a, const float* __restrict__ sums) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= a.C) return;
+    if (a.dB) a.dB[c] = sums[c];
+    if (a.dW) a.dW[c] = sums[a.C + c];
+}
+
+// ---------------------------------------------------------------------------
+// im2col of a 3x3 / pad 1 convolution on NHWC rows: out[(img*H + y)*W + x][tap*C + c]
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void im2col3x3_kernel(const float* __restrict__ X, int nimg, int H, int W, int C,
+                                                        float* __restrict__ out) {
+    const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    const int64_t total = (int64_t)nimg * H * W * 9 * C;
+    if (i4 >= total) return;
+    const int K = 9 * C;
+    const int64_t row = i4 / K;
+    const int k = (int)(i4 - row * K);
+    const int tap = k / C, c = k - tap * C;
+    const int img = (int)(row / (H * W));
+    const int p = (int)(row - (int64_t)img * H * W);
+    const int y = p / W + tap / 3 - 1, x = p % W + tap % 3 - 1;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (y >= 0 && y < H && x >= 0 && x < W) v = *(const f32x4*)(X + (((int64_t)img * H + y) * W + x) * C + c);
+    *(f32x4*)(out + i4) = v;
+}
+
+// ---------------------------------------------------------------------------
+// Detection losses (one workgroup, deterministic reduction order).
+//  FocalLoss(use_sigmoid, gamma, alpha) over logits [R][ncls] with labels
+//  (ncls = background) and per-row weights, sum / cls_avg * cls_weight;
+//  L1Loss over boxes [Rb][10] with per-element weights, sum / box_avg * box_weight.
+//  Writes loss values and d(loss)/d(input) (mmdet 2.28.2 FocalLoss / L1Loss).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float softplus(float x) { return x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x)); }
+
+__global__ __launch_bounds__(1024) void det_loss_kernel(cmt_det_loss_args a) {
+    __shared__ float red[32];
+    float lc = 0.f, lb = 0.f;
+    const float g = a.gamma, al = a.alpha;
+    const float cls_k = a.cls_weight / a.cls_avg, box_k = a.box_weight / a.box_avg;
+    for (int i = threadIdx.x; i < a.R * a.ncls; i += blockDim.x) {
+        const int r = i / a.ncls, c = i - r * a.ncls;
+        const float x = a.logits[(int64_t)r * a.ld_logits + c];
+        const float w = a.label_w ? a.label_w[r] : 1.f;
+        const bool pos = a.labels[r] == c;
+        const float p = 1.f / (1.f + expf(-x));
+        float loss, grad;
+        if (pos) {   // -alpha (1-p)^g log p
+            const float omp = 1.f - p, pw = powf(omp, g), lp = -softplus(-x);
+            loss = -al * pw * lp;
+            grad = al * pw * (g * p * lp - omp);
+        } else {     // -(1-alpha) p^g log(1-p)
+            const float pw = powf(p, g), l1p = -softplus(x);
+            loss = -(1.f - al) * pw * l1p;
+            grad = (1.f - al) * pw * (p - g * (1.f - p) * l1p);
+        }
+        lc += loss * w;
+        if (a.dlogits) a.dlogits[(int64_t)r * a.ld_logits + c] = grad * w * cls_k * a.gscale;
+    }
+    for (int i = threadIdx.x; i < a.Rb * 10; i += blockDim.x) {
+        const int r = i / 10, c = i - r * 10;
+        const float d = a.boxes[(int64_t)r * a.ld_boxes + c] - a.targets[r * 10 + c];
+        const float w = a.box_w[r * 10 + c];
+        lb += fabsf(d) * w;
+        if (a.dboxes) a.dboxes[(int64_t)r * a.ld_boxes + c] = (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * w * box_k * a.gscale;
+    }
+    // block reductions (fixed order)
+    for (int pass = 0; pass < 2; ++pass) {
+        float v = pass == 0 ? lc : lb;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float s = 0.f;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+            a.out[pass] = s * (pass == 0 ? cls_k : box_k);
+        }
+    }
+}
+
+// cost[q][j] = w_cls * (pos(q, label_j) - neg(q, label_j)) + w_reg * sum_c |cw_c (box[q][c] - gt[j][c])|, c < 8
+__global__ __launch_bounds__(256) void match_cost_kernel(cmt_match_cost_args a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.Nq * a.ngt) return;
+    const int q = i / a.ngt, j = i - q * a.ngt;
+    const float x = a.logits[(int64_t)q * a.ld_logits + a.gt_labels[j]];
+    const float p = 1.f / (1.f + expf(-x));
+    const float eps = 1e-12f;
+    const float neg = -logf(1.f - p + eps) * (1.f - a.alpha) * powf(p, a.gamma);
+    const float pos = -logf(p + eps) * a.alpha * powf(1.f - p, a.gamma);
+    float l1 = 0.f;
+    for (int c = 0; c < 8; ++c)
+        l1 += fabsf(a.code_w[c] * a.boxes[(int64_t)q * a.ld_boxes + c] - a.code_w[c] * a.gt[j * 10 + c]);
+    a.cost[i] = a.cls_weight * (pos - neg) + a.reg_weight * l1;
+}
+
+// ---------------------------------------------------------------------------
+// AdamW over one flat buffer (torch.optim.AdamW, amsgrad off) with the
+// clip_grad_norm_ coefficient read from the device sum of squares.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) s += x[i] * x[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(cmt_adamw_args a) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    float coef = 1.f;
+    if (a.max_norm > 0.f && a.sumsq) {
+        const float norm = sqrtf(*a.sumsq);
+        coef = fminf(1.f, a.max_norm / (norm + 1e-6f));
+    }
+    const float g = a.grad[i] * coef;
+    float p = a.param[i];
+    p *= 1.f - a.lr * a.weight_decay;
+    const float m = a.beta1 * a.exp_avg[i] + (1.f - a.beta1) * g;
+    const float v = a.beta2 * a.exp_avg_sq[i] + (1.f - a.beta2) * g * g;
+    a.exp_avg[i] = m;
+    a.exp_avg_sq[i] = v;
+    const float bc1 = 1.f - powf(a.beta1, (float)a.step), bc2 = 1.f - powf(a.beta2, (float)a.step);
+    const float denom = sqrtf(v) / sqrtf(bc2) + a.eps;
+    a.param[i] = p - (a.lr / bc1) * m / denom;
+}
+
+}  // namespace
+
+extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_gemm_f32_ex: null args");
+    cmt_gemm_ex_args a = *ap;
+    CMT_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.batch > 0, "cmt_gemm_f32_ex: empty problem");
+    CMT_REQUIRE(a.A && a.B && a.C, "cmt_gemm_f32_ex: null pointer");
+    if (a.ksplit < 1) a.ksplit = 1;
+    CMT_REQUIRE(a.ksplit == 1 || a.beta == 1.f, "cmt_gemm_f32_ex: split-K accumulates (beta must be 1)");
+    const int am = op_mode(a.a_sm, a.a_sk, a.A), bm = op_mode(a.b_sn, a.b_sk, a.B);
+    int kchunk = cdiv(cdiv(a.K, a.ksplit), TBK) * TBK;
+    a.ksplit = cdiv(a.K, kchunk);
+    dim3 grid(cdiv(a.N, 64), cdiv(a.M, 64), a.batch * a.ksplit);
+    hipStream_t s = (hipStream_t)stream;
+#define GX(AM, BM) gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk)
+    switch (am * 3 + bm) {
+        case 0: GX(0, 0); break; case 1: GX(0, 1); break; case 2: GX(0, 2); break;
+        case 3: GX(1, 0); break; case 4: GX(1, 1); break; case 5: GX(1, 2); break;
+        case 6: GX(2, 0); break; case 7: GX(2, 1); break; default: GX(2, 2); break;
+    }
+#undef GX
+    return cmt_check_launch("cmt_gemm_f32_ex");
+}
+
+extern "C" int cmt_ln_train_fwd(const cmt_ln_train_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->rows > 0 && (ap->C == 64 || ap->C == 256), "cmt_ln_train_fwd: C must be 64 or 256");
+    CMT_REQUIRE(ap->X && ap->Y && ap->W && ap->B && ap->mean && ap->rstd, "cmt_ln_train_fwd: null pointer");
+    const unsigned g = (unsigned)cdiv(ap->rows, 4);
+    if (ap->C == 64) ln_fwd_kernel<64><<<g, 256, 0, (hipStream_t)stream>>>(*ap);
+    else ln_fwd_kernel<256><<<g, 256, 0, (hipStream_t)stream>>>(*ap);
+    return cmt_check_launch("cmt_ln_train_fwd");
+}
+
+extern "C" int cmt_ln_train_bwd(const cmt_ln_train_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->rows > 0 && (ap->C == 64 || ap->C == 256), "cmt_ln_train_bwd: C must be 64 or 256");
+    CMT_REQUIRE(ap->X && ap->dY && ap->dX && ap->W && ap->mean && ap->rstd, "cmt_ln_train_bwd: null pointer");
+    const unsigned g = (unsigned)min(cdiv(ap->rows, 4), 512);
+    if (ap->C == 64) ln_bwd_kernel<64><<<g, 256, 0, (hipStream_t)stream>>>(*ap);
+    else ln_bwd_kernel<256><<<g, 256, 0, (hipStream_t)stream>>>(*ap);
+    return cmt_check_launch("cmt_ln_train_bwd");
+}
+
+extern "C" int64_t cmt_bn_workspace_bytes(int C) { return (int64_t)2 * C * sizeof(float); }
+
+extern "C" int cmt_bn_relu_train_fwd(const cmt_bn_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->rows > 0 && ap->C > 0 && ap->X && ap->Y && ap->W && ap->B && ap->mean_save &&
+                ap->rstd_save && ap->workspace, "cmt_bn_relu_train_fwd: bad arguments");
+    const cmt_bn_args& a = *ap;
+    hipStream_t s = (hipStream_t)stream;
+    float* sums = (float*)a.workspace;   // [0:C) centred squares, [C:2C) mean
+    hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s);
+    const int rpb = 256;
+    dim3 grid(cdiv(a.rows, rpb), cdiv(a.C, 256));
+    col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, nullptr, sums + a.C, 0, rpb);
+    scale_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(sums + a.C, a.C, 1.f / a.rows);
+    col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, sums + a.C, sums, 1, rpb);
+    bn_finalize_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(a, sums);
+    bn_apply_kernel<<<(unsigned)cdiv64((int64_t)a.rows * a.C, 256), 256, 0, s>>>(a);
+    return cmt_check_launch("cmt_bn_relu_train_fwd");
+}
+
+extern "C" int cmt_bn_relu_train_bwd(const cmt_bn_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->rows > 0 && ap->X && ap->Y && ap->dY && ap->dX && ap->W && ap->mean_save &&
+                ap->rstd_save && ap->workspace, "cmt_bn_relu_train_bwd: bad arguments");
+    const cmt_bn_args& a = *ap;
+    hipStream_t s = (hipStream_t)stream;
+    float* sums = (float*)a.workspace;
+    hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s);
+    const int rpb = 256;
+    bn_bwd_sums_kernel<<<dim3(cdiv(a.rows, rpb), cdiv(a.C, 256)), 256, 0, s>>>(a, sums, rpb);
+    bn_bwd_apply_kernel<<<(unsigned)cdiv64((int64_t)a.rows * a.C, 256), 256, 0, s>>>(a, sums);
+    bn_param_grads_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(a, sums);
+    return cmt_check_launch("cmt_bn_relu_train_bwd");
+}
+
+extern "C" int cmt_im2col3x3(const float* X, int nimg, int H, int W, int C, float* out, void* stream) {
+    CMT_REQUIRE(X && out && nimg > 0 && H > 0 && W > 0 && C % 4 == 0, "cmt_im2col3x3: C must be a multiple of 4");
+    const int64_t total4 = (int64_t)nimg * H * W * 9 * C / 4;
+    im2col3x3_kernel<<<(unsigned)cdiv64(total4, 256), 256, 0, (hipStream_t)stream>>>(X, nimg, H, W, C, out);
+    return cmt_check_launch("cmt_im2col3x3");
+}
+
+extern "C" int cmt_det_loss(const cmt_det_loss_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->out && ap->ncls > 0 && (ap->R == 0 || (ap->logits && ap->labels)) &&
+                (ap->Rb == 0 || (ap->boxes && ap->targets && ap->box_w)), "cmt_det_loss: bad arguments");
+    CMT_REQUIRE(ap->cls_avg > 0.f && ap->box_avg > 0.f, "cmt_det_loss: average factors must be > 0");
+    det_loss_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(*ap);
+    return cmt_check_launch("cmt_det_loss");
+}
+
+extern "C" int cmt_match_cost(const cmt_match_cost_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->Nq > 0 && ap->ngt > 0 && ap->logits && ap->boxes && ap->gt && ap->gt_labels && ap->cost,
+                "cmt_match_cost: bad arguments");
+    match_cost_kernel<<<cdiv(ap->Nq * ap->ngt, 256), 256, 0, (hipStream_t)stream>>>(*ap);
+    return cmt_check_launch("cmt_match_cost");
+}
+
+extern "C" int cmt_sumsq(const float* x, int64_t n, float* out, void* stream) {
+    CMT_REQUIRE(x && out && n >= 0, "cmt_sumsq: bad arguments");
+    const int64_t nb = cdiv64(n, 256);
+    const unsigned g = (unsigned)(nb < 1024 ? nb : 1024);
+    if (g > 0) sumsq_kernel<<<g, 256, 0, (hipStream_t)stream>>>(x, n, out);
+    return cmt_check_launch("cmt_sumsq");
+}
+
+extern "C" int cmt_adamw_step(const cmt_adamw_args* ap, void* stream) {
+    CMT_REQUIRE(ap && ap->param && ap->grad && ap->exp_avg && ap->exp_avg_sq && ap->n > 0 && ap->step >= 1,
+                "cmt_adamw_step: bad arguments");
+    adamw_kernel<<<(unsigned)cdiv64(ap->n, 256), 256, 0, (hipStream_t)stream>>>(*ap);
+    return cmt_check_launch("cmt_adamw_step");
+}

@@ -22,6 +22,7 @@ from ...registry import HEADS, build_bbox_coder, build_from_cfg, build_transform
 from ...runtime import get_precision
 from ..utils.packing import PackCache, to_dtype
 from .engine import HeadEngineMixin
+from .train_engine import HeadTrainMixin
 
 __all__ = ["pos2embed", "GroupLayerNorm1d", "SeparateTaskHead", "ConvModule", "CmtHead", "CmtLidarHead",
            "CmtImageHead", "multi_apply"]
@@ -256,8 +257,25 @@ _DEFAULT_TASKS = [
 ]
 
 
+def gt_from_metas(img_metas):
+    """The GT the reference's prepare_for_dn reads from img_metas
+    (cmt_head.py:341-342): 'gt_bboxes_3d' (LiDARInstance3DBoxes-like, a
+    DataContainer around one, or a [n, 9] gravity-centre tensor) and
+    'gt_labels_3d'.  Returns (gravity-centre boxes list, labels list)."""
+    boxes, labels = [], []
+    for m in img_metas:
+        b, l = m["gt_bboxes_3d"], m["gt_labels_3d"]
+        b = getattr(b, "_data", b)
+        l = getattr(l, "_data", l)
+        if not torch.is_tensor(b):
+            b = torch.cat([b.gravity_center, b.tensor[:, 3:]], 1)
+        boxes.append(b)
+        labels.append(l)
+    return boxes, labels
+
+
 @HEADS.register_module()
-class CmtHead(HeadEngineMixin, nn.Module):
+class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
     """cmt_head.py:206-919 (fusion head: BEV + multi-view image memory)."""
     variant = "fusion"
 
@@ -317,6 +335,8 @@ class CmtHead(HeadEngineMixin, nn.Module):
             assert x_img is None
         if self.variant == "image":
             assert x is None
+        if self.training:
+            return self.forward_train([(x, x_img, img_metas)], img_metas, *gt_from_metas(img_metas))
         return self._forward_agents([(x, x_img, img_metas)], img_metas, B)
 
     def forward(self, pts_feats, img_feats=None, img_metas=None):

@@ -12,7 +12,7 @@ the two-agent max to any number of agents (the 4-agent stress config).
 import torch
 
 from ...registry import HEADS
-from .cmt_head import CmtHead, multi_apply
+from .cmt_head import CmtHead, gt_from_metas, multi_apply
 
 __all__ = ["filter_img_metas", "get_vehicle_image_metas", "get_infrastructure_image_metas", "CmtHeadCoop",
            "CmtLidarHeadCoop", "CmtImageHeadCoop"]
@@ -52,6 +52,8 @@ class CmtHeadCoop(CmtHead):
             agents.append((x_infrastructure, x_img_infrastructure, self._agent_metas(img_metas, "infrastructure_")))
         if not agents:
             raise ValueError("CmtHeadCoop needs at least one agent's features")
+        if self.training:   # cmt_head_coop.py:205-275 training branch (DN queries, shared GT)
+            return self.forward_train(agents, img_metas, *gt_from_metas(img_metas))
         return self._forward_agents(agents, img_metas, B)
 
     def _agent_metas(self, img_metas, prefix):

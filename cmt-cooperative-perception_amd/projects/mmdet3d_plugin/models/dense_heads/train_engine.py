@@ -1,0 +1,414 @@
+"""Training forward and loss of CmtHead / CmtHeadCoop on the native training
+kernels (BASELINE.json configs[3]).
+
+Reference: projects/mmdet3d_plugin/models/dense_heads/cmt_head.py
+  prepare_for_dn 339-415 (DN query groups, attention mask 386-398),
+  forward_single 475-547 (training branch: dn_* outputs split off the front),
+  _get_targets_single / get_targets 556-675 (HungarianAssigner3D,
+  core/bbox/assigners/hungarian_assigner_3d.py:68-156, scipy on the host),
+  _loss_single_task / loss_single 677-758, _dn_loss_single_task /
+  dn_loss_single 760-813 (reduce_mean all-reduce of num_tgt), loss 815-903;
+and cmt_head_coop.py:205-275, 362-437, 686 for the two-agent head.
+
+Every matrix product, attention core, LayerNorm, BatchNorm, conv weight
+gradient and loss runs in train.hip / attn_train.hip through
+models/utils/train_ops.py (autograd Functions with native forward AND
+backward); the glue here is index/reshape work on [B, Nq]-sized tensors,
+residual adds, ReLU, dropout masks and the sin/cos / camera geometry of the
+query embedding (a few thousand elements), all on the device.  The Hungarian
+assignment copies the [Nq, n_gt] cost matrix to the host and runs scipy's
+linear_sum_assignment, exactly as the reference does.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from scipy.optimize import linear_sum_assignment
+
+from ... import native
+from ... import native_train as T
+from ..utils import train_ops as ops
+
+__all__ = ["HeadTrainMixin", "Boxes3D", "inverse_sigmoid"]
+
+
+def inverse_sigmoid(x, eps=1e-5):
+    """mmdet 2.28.2 inverse_sigmoid."""
+    x = x.clamp(min=0, max=1)
+    return torch.log(x.clamp(min=eps) / (1 - x).clamp(min=eps))
+
+
+class Boxes3D:
+    """The part of mmdet3d LiDARInstance3DBoxes the head reads: ``tensor``
+    [n, 9] (x, y, z_bottom, w, l, h, yaw, vx, vy) and ``gravity_center``."""
+
+    def __init__(self, tensor):
+        self.tensor = tensor
+
+    @property
+    def gravity_center(self):
+        t = self.tensor
+        return torch.cat([t[:, :2], t[:, 2:3] + t[:, 5:6] * 0.5], 1)
+
+
+def _normalize_bbox(b):
+    """core/bbox/util.py:8-34."""
+    return torch.cat([b[..., 0:3], b[..., 3:6].log(), b[..., 6:7].sin(), b[..., 6:7].cos(), b[..., 7:9]], -1)
+
+
+def _pos2embed(pos, F_):
+    """cmt_head.py:40-50 as differentiable tensor ops (reference points carry
+    a gradient into reference_points.weight)."""
+    pos = pos * (2 * math.pi)
+    dim_t = torch.arange(F_, dtype=pos.dtype, device=pos.device)
+    dim_t = 2 * torch.div(dim_t, 2, rounding_mode="floor") / F_ + 1
+    px = pos[..., 0, None] / dim_t
+    py = pos[..., 1, None] / dim_t
+    px = torch.stack((px[..., 0::2].sin(), px[..., 1::2].cos()), -1).flatten(-2)
+    py = torch.stack((py[..., 0::2].sin(), py[..., 1::2].cos()), -1).flatten(-2)
+    return torch.cat((py, px), -1)
+
+
+class HeadTrainMixin:
+    """Mixed into CmtHead (and through it CmtHeadCoop and the LiDAR / image
+    variants)."""
+
+    train_dropout = True   # the reference trains with dropout 0.1 (attn_drop of the self-attention core and
+    #                        the dropout_layer after both attentions); parity tests switch it off
+
+    # ------------------------------------------------------------------ DN queries
+    def prepare_for_dn_train(self, B, gt_boxes, gt_labels, rand_prob=None, generator=None):
+        """prepare_for_dn training branch (cmt_head.py:339-415).  gt_boxes[b]:
+        [n_b, 9] gravity-centre boxes on the device; gt_labels[b] [n_b].
+        rand_prob: the U(-1, 1) centre noise (drawn here when None)."""
+        ref = self.reference_points.weight
+        dev = ref.device
+        known_num = [int(t.shape[0]) for t in gt_boxes]
+        if max(known_num, default=0) == 0:
+            return ref.unsqueeze(0).repeat(B, 1, 1), None
+        labels = torch.cat(gt_labels).long()
+        boxes = torch.cat(gt_boxes).float()
+        batch_idx = torch.cat([torch.full((n,), i, dtype=torch.long) for i, n in enumerate(known_num)]).to(dev)
+        groups = min(self.scalar, self.num_query // max(known_num))
+        known_indice = torch.arange(labels.numel(), device=dev).repeat(groups)
+        known_labels = labels.repeat(groups)
+        known_bid = batch_idx.repeat(groups)
+        known_bboxs = boxes.repeat(groups, 1)
+        center = known_bboxs[:, :3].clone()
+        scale = known_bboxs[:, 3:6]
+        if self.bbox_noise_scale > 0:
+            if rand_prob is None:
+                rand_prob = torch.rand(center.shape, generator=generator).to(dev) * 2 - 1.0
+            rand_prob = rand_prob.to(dev)
+            center = center + rand_prob * (scale / 2 + self.bbox_noise_trans) * self.bbox_noise_scale
+            pcr = self.pc_range
+            center = torch.stack([(center[:, 0] - pcr[0]) / (pcr[3] - pcr[0]),
+                                  (center[:, 1] - pcr[1]) / (pcr[4] - pcr[1]),
+                                  (center[:, 2] - pcr[2]) / (pcr[5] - pcr[2])], -1).clamp(0.0, 1.0)
+            mask = torch.norm(rand_prob, 2, 1) > self.split
+            known_labels = known_labels.clone()
+            known_labels[mask] = sum(self.num_classes)
+        single_pad = int(max(known_num))
+        pad = single_pad * groups
+        padded = torch.cat([ref.new_zeros(pad, 3), ref], 0).unsqueeze(0).repeat(B, 1, 1)
+        map_known = torch.cat([torch.arange(n, device=dev) for n in known_num])
+        map_known = torch.cat([map_known + single_pad * i for i in range(groups)]).long()
+        padded = padded.index_put((known_bid, map_known), center.to(padded.dtype))
+        mask_dict = dict(known_indice=known_indice, batch_idx=batch_idx, map_known_indice=map_known,
+                         known_lbs_bboxes=(known_labels, known_bboxs), known_labels_raw=labels.repeat(groups),
+                         pad_size=pad, single_pad=single_pad, groups=groups)
+        return padded, mask_dict
+
+    # ------------------------------------------------------------------ pieces
+    def _mlp_t(self, x, seq):
+        h = torch.relu(ops.linear(x, seq[0].weight, seq[0].bias))
+        return ops.linear(h, seq[2].weight, seq[2].bias)
+
+    def _drop(self, x):
+        return F.dropout(x, 0.1, True) if self.train_dropout else x
+
+    def _rv_query_embed_t(self, rp, metas):
+        """cmt_head.py:439-467 (geometry as device tensor ops, differentiable in rp)."""
+        pad_h, pad_w, _ = metas[0]["pad_shape"][0]
+        dev, dt = rp.device, rp.dtype
+        l2i = torch.from_numpy(np.stack([np.asarray(m["lidar2img"], dtype=np.float64) for m in metas])).to(dev, dt)
+        i2l = torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
+                                         for m in metas])).to(dev, dt)
+        pcr = torch.tensor(self.pc_range, dtype=dt, device=dev)
+        pts = rp * (pcr[3:] - pcr[:3]) + pcr[:3]
+        proj = torch.einsum("bnd,bvcd->bvnc", torch.cat([pts, torch.ones_like(pts[..., :1])], -1), l2i)
+        zm = proj[..., 2:3] > 0
+        den = proj[..., 2:3] + zm * 1e-6 - (~zm) * 1e-6
+        proj = torch.cat([proj[..., :3] / den, proj[..., 3:]], -1)
+        mask = (proj[..., 0] < pad_w) & (proj[..., 0] >= 0) & (proj[..., 1] < pad_h) & (proj[..., 1] >= 0) & zm[..., 0]
+        D = self.depth_num
+        cd = 1 + torch.arange(D, dtype=dt, device=dev) * (self.pc_range[3] - 1) / D
+        p3 = torch.einsum("bvnc,d->bvndc", proj, cd)
+        p3 = torch.cat([p3[..., :3], torch.ones_like(p3[..., :1])], -1)
+        back = torch.einsum("bvndo,bvco->bvndc", p3, i2l)
+        back = (back[..., :3] - pcr[:3]) / (pcr[3:] - pcr[:3])
+        rv = self._mlp_t(back.reshape(*back.shape[:-2], -1), self.rv_embedding)
+        return (rv * mask.unsqueeze(-1)).sum(1)
+
+    def _memory_t(self, x, x_img, metas, B):
+        """memory / pos rows [B, Nk, C] of one agent (shared_conv with batch
+        statistics, bev / rv position MLPs)."""
+        C = self.hidden_dim
+        mems, poss = [], []
+        if x is not None and self.shared_conv is not None:
+            _, Cin, H, W = x.shape
+            xr = torch.empty((B * H * W, Cin), dtype=torch.float32, device=x.device)
+            native.nchw_to_rows(x.contiguous().float(), xr, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+            conv = self.shared_conv.conv
+            w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1)
+            y = ops.bn_relu(ops.conv3x3(xr, w, (B, H, W, Cin)), self.shared_conv.bn)
+            mems.append(y.view(B, H * W, C))
+            cfg = self.train_cfg if self.train_cfg else self.test_cfg
+            xs, ys = cfg["grid_size"][1] // self.downsample_scale, cfg["grid_size"][0] // self.downsample_scale
+            pe = torch.empty((H * W, 2 * C), dtype=torch.float32, device=x.device)
+            native.pos2embed(None, pe, n=H * W, F=C, grid=(xs, ys))
+            poss.append(self._mlp_t(pe, self.bev_embedding).unsqueeze(0).expand(B, H * W, C))
+        if x_img is not None:
+            BV, _, h, w_ = x_img.shape
+            V = BV // B
+            xi = torch.empty((B * V * h * w_, C), dtype=torch.float32, device=x_img.device)
+            native.nchw_to_rows(x_img.contiguous().float(), xi, nb=B, nv=V, C=C, HW=h * w_, ldy=C,
+                                rows_per_batch=V * h * w_)
+            mems.append(xi.view(B, V * h * w_, C))
+            pad_h, pad_w, _ = metas[0]["pad_shape"][0]
+            i2l = torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
+                                             for m in metas])).float().to(x_img.device)
+            D = self.depth_num
+            coords = torch.empty((BV * h * w_, 3 * D), dtype=torch.float32, device=x_img.device)
+            native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w_, D=D, pad_h=float(pad_h), pad_w=float(pad_w),
+                                depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
+            poss.append(self._mlp_t(coords, self.rv_embedding).view(B, V * h * w_, C))
+        return torch.cat(mems, 1), torch.cat(poss, 1)
+
+    def _decoder_t(self, tgt, qpos, mem, pos, mask_dict):
+        """PETRTransformerDecoder with the training op walk (post-norm,
+        petr_transformer.py:324-487; mmcv BaseTransformerLayer)."""
+        dec = self.transformer.decoder
+        B, Nq, C = tgt.shape
+        H = dec.layers[0].attentions[0].num_heads
+        pad = mask_dict["pad_size"] if mask_dict else 0
+        grp = mask_dict["single_pad"] if mask_dict else 0
+        memk = mem + pos
+        outs = []
+        seed0 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if self.train_dropout else 0
+        for li, lay in enumerate(dec.layers):
+            sa, ca, ffn, nm = lay.attentions[0].attn, lay.attentions[1].attn, lay.ffns[0], lay.norms
+            wq, wk, wv = sa.in_proj_weight.chunk(3)
+            bq, bk, bv = sa.in_proj_bias.chunk(3)
+            qi = tgt + qpos
+            o = ops.attention(ops.linear(qi, wq, bq), ops.linear(qi, wk, bk), ops.linear(tgt, wv, bv), H, dn_pad=pad,
+                              dn_group=grp, dropout_p=sa.dropout if self.train_dropout else 0.0, seed=seed0 + li)
+            tgt = ops.layer_norm(tgt + self._drop(ops.linear(o, sa.out_proj.weight, sa.out_proj.bias)),
+                                 nm[0].weight, nm[0].bias, nm[0].eps)
+            wq, wk, wv = ca.in_proj_weight.chunk(3)
+            bq, bk, bv = ca.in_proj_bias.chunk(3) if ca.in_proj_bias is not None else (None, None, None)
+            o = ops.attention(ops.linear(tgt + qpos, wq, bq), ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H,
+                              fp16=True)
+            tgt = ops.layer_norm(tgt + self._drop(ops.linear(o, ca.out_proj.weight, ca.out_proj.bias)),
+                                 nm[1].weight, nm[1].bias, nm[1].eps)
+            l1, l2 = ffn.layers[0][0], ffn.layers[1]
+            h = torch.relu(ops.linear(tgt, l1.weight, l1.bias))
+            tgt = ops.layer_norm(tgt + ops.linear(h, l2.weight, l2.bias), nm[2].weight, nm[2].bias, nm[2].eps)
+            outs.append(ops.layer_norm(tgt, dec.post_norm.weight, dec.post_norm.bias, dec.post_norm.eps))
+        return torch.nan_to_num(torch.stack(outs))          # [L, B, Nq, C]
+
+    def _task_head_t(self, task, x, reference):
+        """SeparateTaskHead (cmt_head.py:136-203) + box epilogue (501-513).
+        x [L, B, Nq, C] -> dict of [L, B, Nq, k]."""
+        L, B, Nq, C = x.shape
+        k = task.final_kernel
+        if k == 3:   # conv along queries, zero padded per (layer, sample): taps q-1, q, q+1
+            xp = F.pad(x, (0, 0, 1, 1))
+            xin = torch.cat([xp[:, :, 0:Nq], xp[:, :, 1:Nq + 1], xp[:, :, 2:Nq + 2]], -1)   # [L, B, Nq, 3C]
+        else:
+            xin = x
+        out = {}
+        for name in task.heads:
+            seq = getattr(task, name)
+            c1, gln, c2 = seq[0], seq[1], seq[3]
+            hc = c1.weight.shape[0] // L
+            w1 = c1.weight.view(L, hc, C, k).permute(0, 1, 3, 2).reshape(L, hc, k * C)
+            h = torch.stack([ops.linear(xin[l], w1[l]) for l in range(L)])               # [L, B, Nq, hc]
+            h = ops.group_layer_norm(h.reshape(L, B * Nq, hc), gln.weight, gln.bias, gln.eps).view(L, B, Nq, hc)
+            h = torch.relu(h)
+            if k == 3:
+                hp = F.pad(h, (0, 0, 1, 1))
+                h = torch.cat([hp[:, :, 0:Nq], hp[:, :, 1:Nq + 1], hp[:, :, 2:Nq + 2]], -1)
+            on = c2.weight.shape[0] // L
+            w2 = c2.weight.view(L, on, hc, k).permute(0, 1, 3, 2).reshape(L, on, k * hc)
+            b2 = c2.bias.view(L, on)
+            out[name] = torch.stack([ops.linear(h[l], w2[l], b2[l]) for l in range(L)])
+        pcr = self.pc_range
+        c = (out["center"] + reference[None, :, :, :2]).sigmoid()
+        z = (out["height"] + reference[None, :, :, 2:3]).sigmoid()
+        out["center"] = torch.cat([c[..., 0:1] * (pcr[3] - pcr[0]) + pcr[0], c[..., 1:2] * (pcr[4] - pcr[1]) + pcr[1]],
+                                  -1)
+        out["height"] = z * (pcr[5] - pcr[2]) + pcr[2]
+        return out
+
+    # ------------------------------------------------------------------ forward
+    def forward_train(self, agents, img_metas, gt_boxes, gt_labels, rand_prob=None):
+        """Training forward: ``agents`` = list of (x [B,512,H,W] or None, x_img or
+        None, agent metas); gt_boxes[b] [n_b, 9] gravity-centre boxes, gt_labels[b].
+        Returns (preds: list over tasks of dicts incl. dn_* and dn_mask_dict, as
+        cmt_head.py:515-545)."""
+        B = len(img_metas)
+        C = self.hidden_dim
+        ref, mask_dict = self.prepare_for_dn_train(B, gt_boxes, gt_labels, rand_prob)
+        rp = inverse_sigmoid(ref.clone()).sigmoid()
+        qpos = self._mlp_t(_pos2embed(rp, C), self.bev_embedding)
+        dec = None
+        for x, x_img, metas in agents:
+            q = qpos
+            if x_img is not None and self.rv_embedding is not None:
+                q = q + self._rv_query_embed_t(rp, metas)
+            mem, pos = self._memory_t(x, x_img, metas, B)
+            d = self._decoder_t(torch.zeros_like(q), q, mem, pos, mask_dict)
+            dec = d if dec is None else torch.maximum(dec, d)     # coop max fusion (cmt_head_coop.py:383-389)
+        reference = inverse_sigmoid(ref.clone())
+        preds = []
+        flag = 0
+        pad = mask_dict["pad_size"] if mask_dict else 0
+        for t, task in enumerate(self.task_heads):
+            outs = self._task_head_t(task, dec, reference)
+            if pad:
+                names = self.class_names[t]
+                kl, kb = mask_dict["known_lbs_bboxes"]
+                raw = mask_dict["known_labels_raw"]
+                new_kl, new_raw = torch.full_like(kl, len(names)), torch.full_like(raw, len(names))
+                for ci in range(len(names)):
+                    new_kl[kl == ci + flag] = ci
+                    new_raw[raw == ci + flag] = ci
+                tmd = dict(mask_dict, known_lbs_bboxes=(new_kl, kb), known_labels_raw=new_raw)
+                for key in list(outs):
+                    outs["dn_" + key] = outs[key][:, :, :pad]
+                    outs[key] = outs[key][:, :, pad:]
+                outs["dn_mask_dict"] = tmd
+            flag += len(self.class_names[t])
+            preds.append(outs)
+        return preds
+
+    # ------------------------------------------------------------------ loss
+    def _loss_cfg(self):
+        lc, lb = self.loss_cls_cfg or {}, self.loss_bbox_cfg or {}
+        tc = (self.train_cfg or {}).get("pts", self.train_cfg or {}) if self.train_cfg else {}
+        asg = tc.get("assigner", {}) if tc else {}
+        cw = tc.get("code_weights", [2.0, 2.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 0.2, 0.2]) if tc else \
+            [2.0, 2.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 0.2, 0.2]
+        return dict(gamma=float(lc.get("gamma", 2.0)), alpha=float(lc.get("alpha", 0.25)),
+                    cls_weight=float(lc.get("loss_weight", 1.0)), box_weight=float(lb.get("loss_weight", 0.25)),
+                    match_cls_weight=float(asg.get("cls_cost", {}).get("weight", 2.0)),
+                    match_reg_weight=float(asg.get("reg_cost", {}).get("weight", 0.25)), code_weights=cw)
+
+    def _targets(self, pb, pl, gtb, gtl, cfg, code_w):
+        """_get_targets_single + HungarianAssigner3D for one (sample, task)."""
+        Nq, ncls = pl.shape
+        dev = pl.device
+        labels = torch.full((Nq,), ncls, dtype=torch.int32, device=dev)
+        tgt = torch.zeros((Nq, 9), dtype=torch.float32, device=dev)
+        bw = torch.zeros((Nq, 10), dtype=torch.float32, device=dev)
+        if gtb.shape[0] == 0:
+            return labels, tgt, bw, 0, Nq
+        cost = T.match_cost(pl.detach().contiguous(), pb.detach().contiguous(), _normalize_bbox(gtb).contiguous(),
+                            gtl.int().contiguous(), code_w, gamma=cfg["gamma"], alpha=cfg["alpha"],
+                            cls_weight=cfg["match_cls_weight"], reg_weight=cfg["match_reg_weight"])
+        r, c = linear_sum_assignment(cost.cpu().numpy())          # host, as the reference (scipy)
+        r = torch.from_numpy(r).to(dev)
+        c = torch.from_numpy(c).to(dev)
+        labels[r] = gtl[c].int()
+        tgt[r] = gtb[c].float()
+        bw[r] = 1.0
+        return labels, tgt, bw, int(r.numel()), Nq - int(r.numel())
+
+    def _box_terms(self, tgt, bw, code_w):
+        """normalize the targets, drop non-finite rows (isnotnan), code weights."""
+        nt = _normalize_bbox(tgt)
+        ok = torch.isfinite(nt).all(-1)
+        nt = torch.where(ok[:, None], nt, torch.zeros_like(nt))
+        w = bw * code_w[None] * ok[:, None].float()
+        return nt.contiguous(), w.contiguous()
+
+    def loss(self, gt_bboxes_3d, gt_labels_3d, preds_dicts, **kwargs):
+        """cmt_head.py:815-903 on the native loss / cost kernels.  preds_dicts:
+        the multi_apply layout (tuple over tasks of [dict]) or a list of dicts.
+        Returns the reference's loss dict."""
+        preds = [p[0] if isinstance(p, (list, tuple)) else p for p in preds_dicts]
+        cfg = self._loss_cfg()
+        dev = preds[0]["center"].device
+        code_w = torch.tensor(cfg["code_weights"], dtype=torch.float32, device=dev)
+        gtb = [(g.gravity_center if False else g).to(dev).float() if not isinstance(g, Boxes3D)
+               else torch.cat([g.gravity_center, g.tensor[:, 3:]], 1).to(dev).float() for g in gt_bboxes_3d]
+        gtl = [l.to(dev).long() for l in gt_labels_3d]
+        L, B = preds[0]["center"].shape[:2]
+        eps = float(torch.finfo(torch.float32).eps)   # mmdet weight_reduce_loss avg_factor + eps
+        losses = {}
+        for l in range(L):
+            tot = {"loss_cls": 0.0, "loss_bbox": 0.0, "dn_loss_cls": 0.0, "dn_loss_bbox": 0.0}
+            flag = 0
+            for t, d in enumerate(preds):
+                ncls = self.num_classes[t]
+                pb = torch.cat([d[k][l] for k in ("center", "height", "dim", "rot", "vel")], -1)    # [B, Nq, 10]
+                pl = d["cls_logits"][l]
+                labs, tgts, bws, npos, nneg = [], [], [], 0, 0
+                for b in range(B):
+                    m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
+                    lab, tg, bw, p_, n_ = self._targets(pb[b], pl[b], gtb[b][m], gtl[b][m] - flag, cfg, code_w)
+                    labs.append(lab); tgts.append(tg); bws.append(bw)
+                    npos += p_; nneg += n_
+                nt, w = self._box_terms(torch.cat(tgts), torch.cat(bws), code_w)
+                lw = torch.ones(B * pl.shape[1], dtype=torch.float32, device=dev)
+                out = ops.det_loss(pl.reshape(-1, ncls), pb.reshape(-1, 10), torch.cat(labs), lw, nt, w,
+                                   gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["cls_weight"],
+                                   box_weight=cfg["box_weight"], cls_avg=max(npos + 0.1 * nneg, 1.0) + eps,
+                                   box_avg=float(npos) + eps)
+                tot["loss_cls"] = tot["loss_cls"] + torch.nan_to_num(out[0])
+                tot["loss_bbox"] = tot["loss_bbox"] + torch.nan_to_num(out[1])
+                md = d.get("dn_mask_dict")
+                if md is not None and md["pad_size"] > 0:
+                    dout = self._dn_loss(d, l, md, ncls, cfg, code_w, eps)
+                    tot["dn_loss_cls"] = tot["dn_loss_cls"] + dout[0]
+                    tot["dn_loss_bbox"] = tot["dn_loss_bbox"] + dout[1]
+                flag += ncls
+            key = "" if l == L - 1 else f"d{l}."
+            for k, v in tot.items():
+                if isinstance(v, torch.Tensor):
+                    losses[key + k] = v
+        return losses
+
+    def _dn_loss(self, d, l, md, ncls, cfg, code_w, eps):
+        """_dn_loss_single_task (cmt_head.py:760-806)."""
+        kl, kb = md["known_lbs_bboxes"]
+        raw = md["known_labels_raw"]
+        bid = md["batch_idx"][md["known_indice"]]
+        mk = md["map_known_indice"]
+        pl = d["dn_cls_logits"][l][bid, mk]                                        # [nk, ncls]
+        pb = torch.cat([d["dn_" + k][l] for k in ("center", "height", "dim", "rot", "vel")], -1)[bid, mk]
+        num_tgt = md["known_indice"].numel()
+        task_mask = raw != ncls
+        any_task = bool(task_mask.any())
+        rows = task_mask if any_task else torch.ones_like(task_mask)
+        cls_avg = max(num_tgt * 3.14159 / 6 * self.split ** 3, 1)
+        nt_t = torch.tensor([float(num_tgt)], device=pl.device)
+        if dist.is_available() and dist.is_initialized():       # reduce_mean (cmt_head_coop.py:686)
+            dist.all_reduce(nt_t)
+            nt_t = nt_t / dist.get_world_size()
+        nt = max(float(nt_t.item()), 1.0)
+        ntg, w = self._box_terms(kb[rows].float(), torch.ones((int(rows.sum()), 10), device=pl.device), code_w)
+        # the classification term covers every DN row, the box term only the task's rows
+        lw = torch.ones(pl.shape[0], dtype=torch.float32, device=pl.device)
+        out_c = ops.det_loss(pl, pb[:0], kl.int(), lw, ntg[:0], w[:0], gamma=cfg["gamma"], alpha=cfg["alpha"],
+                             cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=cls_avg + eps,
+                             box_avg=1.0)
+        lab_dummy = torch.full((0,), ncls, dtype=torch.int32, device=pl.device)
+        out_b = ops.det_loss(pl[:0], pb[rows], lab_dummy, lw[:0], ntg, w, gamma=cfg["gamma"], alpha=cfg["alpha"],
+                             cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=1.0,
+                             box_avg=nt + eps)
+        lb = torch.nan_to_num(out_b[1]) * (1.0 if any_task else 0.0)
+        return self.dn_weight * torch.nan_to_num(out_c[0]), self.dn_weight * lb

@@ -1,0 +1,179 @@
+"""torch.autograd Functions of the training path: forward AND backward run on
+the gfx950 kernels of train.hip / attn_train.hip (native_train.py).  Autograd
+is only the bookkeeping (which gradient goes where); reshapes, residual adds,
+ReLU masks and the few-element box epilogue between these ops are plain
+tensor glue on the device.
+
+Reference semantics (training step of CmtHead / CmtHeadCoop):
+  Linear          nn.Linear / the packed in_proj of nn.MultiheadAttention and
+                  FlashMHA (attention.py:21-27), mmcv FFN, the MLPs
+  attention       nn.MultiheadAttention core (fp32, DN mask cmt_head.py:386-398,
+                  attn_drop) and the flash-attn 0.2.2 fp16 cross core
+  LayerNorm       nn.LayerNorm (eps 1e-5) and GroupLayerNorm1d (cmt_head.py:53-94)
+  BN + ReLU       shared_conv's BatchNorm2d (training statistics) + ReLU
+  conv3x3         shared_conv's Conv2d (no bias): forward on cmt_gemm's exact-f32
+                  implicit-GEMM path, weight gradient = dY^T im2col(X)
+"""
+import math
+
+import torch
+
+from ... import native
+from ... import native_train as T
+
+__all__ = ["linear", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "det_loss"]
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return T.linear_fwd(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx, dw, db = T.linear_bwd(dy, x, w, need_dx=ctx.needs_input_grad[0], need_dw=ctx.needs_input_grad[1],
+                                  need_db=ctx.has_b and ctx.needs_input_grad[2])
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    """x [..., K] -> [..., N] (rows flattened, fp32)."""
+    shape = x.shape
+    y = _Linear.apply(x.reshape(-1, shape[-1]).contiguous(), w.contiguous(), b)
+    return y.view(*shape[:-1], w.shape[0])
+
+
+class _Attention(torch.autograd.Function):
+    """q [B, Nq, H*32], k / v [B, Nk, H*32] (contiguous rows) -> o [B, Nq, H*32]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, H, scale, dn_pad, dn_group, fp16, dropout_p, seed):
+        B, Nq, C = q.shape
+        Nk = k.shape[1]
+        o = torch.empty_like(q)
+        lse = torch.empty((B * H * Nq,), dtype=torch.float32, device=q.device)
+        kw = dict(B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * C, 32, C), k_strides=(Nk * C, 32, C),
+                  v_strides=(Nk * C, 32, C), o_strides=(Nq * C, 32, C), scale=scale, dn_pad=dn_pad,
+                  dn_group=dn_group, fp16_inputs=fp16, dropout_p=dropout_p, seed=seed)
+        T.attn_train_fwd(q, k, v, o, lse, **kw)
+        ctx.kw = kw
+        ctx.save_for_backward(q, k, v, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        T.attn_train_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, **ctx.kw)
+        return dq, dk, dv, None, None, None, None, None, None, None
+
+
+def attention(q, k, v, num_heads, *, dn_pad=0, dn_group=0, fp16=False, dropout_p=0.0, seed=0):
+    return _Attention.apply(q.contiguous(), k.contiguous(), v.contiguous(), num_heads,
+                            1.0 / math.sqrt(q.shape[-1] // num_heads), dn_pad, dn_group, fp16, dropout_p, seed)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps, rows_per_wset, wsets):
+        y, mean, rstd = T.ln_train_fwd(x, w, b, eps=eps, rows_per_wset=rows_per_wset)
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.eps, ctx.rpw, ctx.wsets = eps, rows_per_wset, wsets
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = T.ln_train_bwd(dy, x, w, mean, rstd, eps=ctx.eps, rows_per_wset=ctx.rpw, wsets=ctx.wsets)
+        return dx, dw.view(w.shape), db.view(w.shape), None, None, None
+
+
+def layer_norm(x, w, b, eps=1e-5):
+    shape = x.shape
+    return _LayerNorm.apply(x.reshape(-1, shape[-1]).contiguous(), w, b, eps, 0, 1).view(shape)
+
+
+def group_layer_norm(x, w, b, eps=1e-6):
+    """x [G, R, 64]: LayerNorm over the 64 channels of every row with weight set
+    g for rows of group g (GroupLayerNorm1d, cmt_head.py:53-94); w, b [G*64]."""
+    G, R, Cg = x.shape
+    return _LayerNorm.apply(x.reshape(G * R, Cg).contiguous(), w, b, eps, R, G).view(G, R, Cg)
+
+
+class _BnRelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, running_mean, running_var, eps, momentum):
+        y, mean, rstd = T.bn_relu_train_fwd(x, w, b, running_mean, running_var, eps=eps, momentum=momentum)
+        ctx.save_for_backward(x, y, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = T.bn_relu_train_bwd(dy, x, y, w, mean, rstd)
+        return dx, dw, db, None, None, None, None
+
+
+def bn_relu(x, bn):
+    """relu(bn(x)) with training statistics; x rows [B*H*W, C]."""
+    return _BnRelu.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum)
+
+
+class _Conv3x3(torch.autograd.Function):
+    """NHWC rows [B*H*W, Cin] -> [B*H*W, Cout]; weight [Cout, 9*Cin] tap-major."""
+
+    @staticmethod
+    def forward(ctx, x, w, geom):
+        B, H, W, Cin = geom
+        Cout = w.shape[0]
+        y = torch.empty((B * H * W, Cout), dtype=torch.float32, device=x.device)
+        native.gemm(x, w, y, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout, a_mode=native.A_CONV3X3,
+                    conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin, c_bstride=H * W * Cout)
+        ctx.save_for_backward(x, w)
+        ctx.geom = geom
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        B, H, W, Cin = ctx.geom
+        Cout = w.shape[0]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            col = T.im2col3x3(x, B, H, W, Cin)                     # [rows, 9*Cin]
+            rows = col.shape[0]
+            ks = T._ksplit(rows, Cout, 9 * Cin)
+            dw = torch.zeros((Cout, 9 * Cin), dtype=torch.float32, device=x.device)
+            T.gemm_ex(dy.contiguous(), (1, Cout), col, (1, 9 * Cin), dw, M=Cout, N_=9 * Cin, K=rows, ldc=9 * Cin,
+                      beta=1.0, ksplit=max(ks, 2))
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("shared_conv input gradient (the BEV backbone is out of scope)")
+        return None, dw, None
+
+
+def conv3x3(x_rows, w_tap_major, geom):
+    return _Conv3x3.apply(x_rows, w_tap_major, geom)
+
+
+class _DetLoss(torch.autograd.Function):
+    """FocalLoss + L1Loss of one (layer, task): returns a [2] tensor (cls, box);
+    the kernel computes the input gradients in the same launch."""
+
+    @staticmethod
+    def forward(ctx, logits, boxes, labels, label_w, targets, box_w, cfg):
+        lg, bx = logits.contiguous(), boxes.contiguous()
+        out, dl, db = T.det_loss(lg, labels, label_w, bx, targets, box_w, **cfg)
+        ctx.save_for_backward(dl, db)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dl, db = ctx.saved_tensors
+        return dl * dout[0], db * dout[1], None, None, None, None, None
+
+
+def det_loss(logits, boxes, labels, label_w, targets, box_w, **cfg):
+    return _DetLoss.apply(logits, boxes, labels, label_w, targets, box_w, cfg)

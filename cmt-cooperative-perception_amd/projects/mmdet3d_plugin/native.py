@@ -77,7 +77,59 @@ class LnArgs(ctypes.Structure):
                 ("Yp", _vp), ("ldyp", _i64), ("P", _vp), ("ldp", _i64)]
 
 
-STRUCTS = {"gemm": GemmArgs, "attn": AttnArgs, "ln": LnArgs, "chain": ChainArgs}
+class GemmExArgs(ctypes.Structure):
+    _fields_ = [("M", _int), ("N", _int), ("K", _int), ("batch", _int), ("alpha", _flt), ("beta", _flt),
+                ("A", _vp), ("a_sm", _i64), ("a_sk", _i64), ("a_bs", _i64),
+                ("B", _vp), ("b_sn", _i64), ("b_sk", _i64), ("b_bs", _i64),
+                ("C", _vp), ("ldc", _i64), ("c_bs", _i64), ("bias", _vp), ("ksplit", _int)]
+
+
+class AttnTrainArgs(ctypes.Structure):
+    _fields_ = [("B", _int), ("H", _int), ("Nq", _int), ("Nk", _int),
+                ("Q", _vp), ("q_bs", _i64), ("q_hs", _i64), ("q_rs", _i64),
+                ("K", _vp), ("k_bs", _i64), ("k_hs", _i64), ("k_rs", _i64),
+                ("V", _vp), ("v_bs", _i64), ("v_hs", _i64), ("v_rs", _i64),
+                ("O", _vp), ("o_bs", _i64), ("o_hs", _i64), ("o_rs", _i64),
+                ("LSE", _vp), ("dO", _vp), ("dQ", _vp), ("dK", _vp), ("dV", _vp), ("delta", _vp),
+                ("scale", _flt), ("dn_pad", _int), ("dn_group", _int), ("fp16_inputs", _int),
+                ("dropout_p", _flt), ("seed", ctypes.c_uint32), ("kv_splits", _int),
+                ("workspace", _vp), ("workspace_bytes", _i64)]
+
+
+class LnTrainArgs(ctypes.Structure):
+    _fields_ = [("rows", _int), ("C", _int), ("X", _vp), ("ldx", _i64), ("W", _vp), ("B", _vp), ("eps", _flt),
+                ("rows_per_wset", _int), ("Y", _vp), ("ldy", _i64), ("mean", _vp), ("rstd", _vp),
+                ("dY", _vp), ("dX", _vp), ("lddx", _i64), ("accumulate", _int), ("dW", _vp), ("dB", _vp)]
+
+
+class BnArgs(ctypes.Structure):
+    _fields_ = [("rows", _int), ("C", _int), ("X", _vp), ("Y", _vp), ("W", _vp), ("B", _vp), ("eps", _flt),
+                ("momentum", _flt), ("running_mean", _vp), ("running_var", _vp), ("mean_save", _vp),
+                ("rstd_save", _vp), ("dY", _vp), ("dX", _vp), ("dW", _vp), ("dB", _vp), ("workspace", _vp)]
+
+
+class DetLossArgs(ctypes.Structure):
+    _fields_ = [("R", _int), ("ncls", _int), ("logits", _vp), ("ld_logits", _i64), ("labels", _vp), ("label_w", _vp),
+                ("Rb", _int), ("boxes", _vp), ("ld_boxes", _i64), ("targets", _vp), ("box_w", _vp),
+                ("gamma", _flt), ("alpha", _flt), ("cls_weight", _flt), ("box_weight", _flt), ("cls_avg", _flt),
+                ("box_avg", _flt), ("gscale", _flt), ("out", _vp), ("dlogits", _vp), ("dboxes", _vp)]
+
+
+class MatchCostArgs(ctypes.Structure):
+    _fields_ = [("Nq", _int), ("ngt", _int), ("logits", _vp), ("ld_logits", _i64), ("boxes", _vp), ("ld_boxes", _i64),
+                ("gt", _vp), ("gt_labels", _vp), ("code_w", _vp), ("gamma", _flt), ("alpha", _flt),
+                ("cls_weight", _flt), ("reg_weight", _flt), ("cost", _vp)]
+
+
+class AdamwArgs(ctypes.Structure):
+    _fields_ = [("n", _i64), ("step", _int), ("lr", _flt), ("beta1", _flt), ("beta2", _flt), ("eps", _flt),
+                ("weight_decay", _flt), ("max_norm", _flt), ("param", _vp), ("grad", _vp), ("exp_avg", _vp),
+                ("exp_avg_sq", _vp), ("sumsq", _vp)]
+
+
+STRUCTS = {"gemm": GemmArgs, "attn": AttnArgs, "ln": LnArgs, "chain": ChainArgs, "gemm_ex": GemmExArgs,
+           "attn_train": AttnTrainArgs, "ln_train": LnTrainArgs, "bn": BnArgs, "det_loss": DetLossArgs,
+           "match_cost": MatchCostArgs, "adamw": AdamwArgs}
 
 _LIB = None
 
@@ -122,6 +174,27 @@ def _load():
         "cmt_ln_args_size": ([], _i64),
         "cmt_chain_args_size": ([], _i64),
         "cmt_chain_ws_bytes": ([_int], _i64),
+        "cmt_gemm_ex_args_size": ([], _i64),
+        "cmt_attn_train_args_size": ([], _i64),
+        "cmt_ln_train_args_size": ([], _i64),
+        "cmt_bn_args_size": ([], _i64),
+        "cmt_det_loss_args_size": ([], _i64),
+        "cmt_match_cost_args_size": ([], _i64),
+        "cmt_adamw_args_size": ([], _i64),
+        "cmt_gemm_f32_ex": ([P(GemmExArgs), _vp], _int),
+        "cmt_attn_train_workspace_bytes": ([P(AttnTrainArgs)], _i64),
+        "cmt_attn_train_fwd": ([P(AttnTrainArgs), _vp], _int),
+        "cmt_attn_train_bwd": ([P(AttnTrainArgs), _vp], _int),
+        "cmt_ln_train_fwd": ([P(LnTrainArgs), _vp], _int),
+        "cmt_ln_train_bwd": ([P(LnTrainArgs), _vp], _int),
+        "cmt_bn_workspace_bytes": ([_int], _i64),
+        "cmt_bn_relu_train_fwd": ([P(BnArgs), _vp], _int),
+        "cmt_bn_relu_train_bwd": ([P(BnArgs), _vp], _int),
+        "cmt_im2col3x3": ([_vp, _int, _int, _int, _int, _vp, _vp], _int),
+        "cmt_det_loss": ([P(DetLossArgs), _vp], _int),
+        "cmt_match_cost": ([P(MatchCostArgs), _vp], _int),
+        "cmt_sumsq": ([_vp, _i64, _vp, _vp], _int),
+        "cmt_adamw_step": ([P(AdamwArgs), _vp], _int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,238 @@
+"""ctypes wrappers of the training-path kernels (include/cmt_hip.h "TRAINING
+PATH": train.hip, attn_train.hip).  Same contract as native.py: device
+tensors only, the current torch stream, no CPU or eager-PyTorch fallback."""
+import ctypes
+
+import torch
+
+from . import native as N
+
+__all__ = ["gemm_ex", "linear_fwd", "linear_bwd", "attn_train_fwd", "attn_train_bwd", "ln_train_fwd", "ln_train_bwd",
+           "bn_relu_train_fwd", "bn_relu_train_bwd", "im2col3x3", "det_loss", "match_cost", "sumsq", "adamw_step"]
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _f32(*ts):
+    N._dev(*ts)
+    for t in ts:
+        if t is not None and t.dtype != torch.float32:
+            raise RuntimeError("training kernels take fp32 tensors")
+
+
+def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0, bias=None, batch=1, a_bs=0,
+            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0):
+    """C[z][m][n] = alpha sum_k A(m,k) B(n,k) (+bias) + beta C; strides in elements:
+    a_strides = (s_m, s_k), b_strides = (s_n, s_k)."""
+    _f32(A, B, C, bias)
+    g = N.GemmExArgs()
+    g.M, g.N, g.K, g.batch, g.alpha, g.beta = M, N_, K, batch, alpha, beta
+    g.A, (g.a_sm, g.a_sk), g.a_bs = A.data_ptr() + 4 * a_offset, a_strides, a_bs
+    g.B, (g.b_sn, g.b_sk), g.b_bs = B.data_ptr() + 4 * b_offset, b_strides, b_bs
+    g.C, g.ldc, g.c_bs = C.data_ptr() + 4 * c_offset, ldc, c_bs
+    g.bias, g.ksplit = _ptr(bias), ksplit
+    N._check(N.lib().cmt_gemm_f32_ex(ctypes.byref(g), N._stream()), "cmt_gemm_f32_ex")
+
+
+def _ksplit(k, m, n):
+    """split the reduction when the output tile grid alone cannot fill the chip"""
+    tiles = -(-m // 64) * -(-n // 64)
+    s = 1
+    while tiles * s < 512 and k // (2 * s) >= 256:
+        s *= 2
+    return s
+
+
+def linear_fwd(X, W, b=None):
+    """Y = X W^T + b, X [M, K] (row stride X.stride(0)), W [N, K] contiguous."""
+    M, K = X.shape
+    Nn = W.shape[0]
+    Y = torch.empty((M, Nn), dtype=torch.float32, device=X.device)
+    gemm_ex(X, (X.stride(0), 1), W, (W.stride(0), 1), Y, M=M, N_=Nn, K=K, ldc=Nn, bias=b)
+    return Y
+
+
+def linear_bwd(dY, X, W, need_dx=True, need_dw=True, need_db=True):
+    """(dX, dW, dB) of Y = X W^T + b."""
+    M, K = X.shape
+    Nn = W.shape[0]
+    dY = dY.contiguous()
+    dX = dW = dB = None
+    if need_dx:
+        dX = torch.empty((M, K), dtype=torch.float32, device=X.device)
+        gemm_ex(dY, (Nn, 1), W, (1, W.stride(0)), dX, M=M, N_=K, K=Nn, ldc=K)
+    if need_dw:
+        ks = _ksplit(M, Nn, K)
+        dW = torch.zeros((Nn, K), dtype=torch.float32, device=X.device) if ks > 1 else \
+            torch.empty((Nn, K), dtype=torch.float32, device=X.device)
+        gemm_ex(dY, (1, Nn), X, (1, X.stride(0)), dW, M=Nn, N_=K, K=M, ldc=K, beta=1.0 if ks > 1 else 0.0, ksplit=ks)
+    if need_db:
+        ones = torch.ones((1, M), dtype=torch.float32, device=X.device)
+        ks = _ksplit(M, Nn, 1)
+        dB = torch.zeros((Nn, 1), dtype=torch.float32, device=X.device)
+        gemm_ex(dY, (1, Nn), ones, (M, 1), dB, M=Nn, N_=1, K=M, ldc=1, beta=1.0, ksplit=max(ks, 2))
+        dB = dB.view(Nn)
+    return dX, dW, dB
+
+
+def _attn_args(Q, K, V, O, LSE, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, dn_pad=0,
+               dn_group=0, fp16_inputs=False, dropout_p=0.0, seed=0):
+    a = N.AttnTrainArgs()
+    a.B, a.H, a.Nq, a.Nk = B, H, Nq, Nk
+    a.Q, (a.q_bs, a.q_hs, a.q_rs) = Q.data_ptr(), q_strides
+    a.K, (a.k_bs, a.k_hs, a.k_rs) = K.data_ptr(), k_strides
+    a.V, (a.v_bs, a.v_hs, a.v_rs) = V.data_ptr(), v_strides
+    a.O, (a.o_bs, a.o_hs, a.o_rs) = O.data_ptr(), o_strides
+    a.LSE = LSE.data_ptr()
+    a.scale, a.dn_pad, a.dn_group = scale, dn_pad, dn_group
+    a.fp16_inputs, a.dropout_p, a.seed = int(bool(fp16_inputs)), dropout_p, seed & 0xFFFFFFFF
+    return a
+
+
+def attn_train_fwd(Q, K, V, O, LSE, **kw):
+    _f32(Q, K, V, O, LSE)
+    a = _attn_args(Q, K, V, O, LSE, **kw)
+    need = N.lib().cmt_attn_train_workspace_bytes(ctypes.byref(a))
+    ws = None
+    if need > 0:
+        ws = torch.empty(need, dtype=torch.uint8, device=O.device)
+        a.workspace, a.workspace_bytes = ws.data_ptr(), need
+    N._check(N.lib().cmt_attn_train_fwd(ctypes.byref(a), N._stream()), "cmt_attn_train_fwd")
+
+
+def attn_train_bwd(Q, K, V, O, LSE, dO, dQ, dK, dV, **kw):
+    _f32(Q, K, V, O, LSE, dO, dQ, dK, dV)
+    a = _attn_args(Q, K, V, O, LSE, **kw)
+    delta = torch.empty(kw["B"] * kw["H"] * kw["Nq"], dtype=torch.float32, device=O.device)
+    a.dO, a.dQ, a.dK, a.dV, a.delta = dO.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dV.data_ptr(), delta.data_ptr()
+    N._check(N.lib().cmt_attn_train_bwd(ctypes.byref(a), N._stream()), "cmt_attn_train_bwd")
+
+
+def _ln_args(X, W, Bv, *, C, eps, rows_per_wset=0):
+    a = N.LnTrainArgs()
+    a.rows, a.C = X.shape[0], C
+    a.X, a.ldx = X.data_ptr(), X.stride(0)
+    a.W, a.B, a.eps, a.rows_per_wset = W.data_ptr(), Bv.data_ptr(), eps, rows_per_wset
+    return a
+
+
+def ln_train_fwd(X, W, Bv, *, eps, rows_per_wset=0):
+    """y, mean, rstd of a row LayerNorm over the last dim (C = 64 / 256)."""
+    _f32(X, W, Bv)
+    rows, C = X.shape
+    Y = torch.empty((rows, C), dtype=torch.float32, device=X.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=X.device)
+    rstd = torch.empty_like(mean)
+    a = _ln_args(X, W, Bv, C=C, eps=eps, rows_per_wset=rows_per_wset)
+    a.Y, a.ldy, a.mean, a.rstd = Y.data_ptr(), C, mean.data_ptr(), rstd.data_ptr()
+    N._check(N.lib().cmt_ln_train_fwd(ctypes.byref(a), N._stream()), "cmt_ln_train_fwd")
+    return Y, mean, rstd
+
+
+def ln_train_bwd(dY, X, W, mean, rstd, *, eps, rows_per_wset=0, wsets=1):
+    _f32(dY, X, W, mean, rstd)
+    rows, C = X.shape
+    dY = dY.contiguous()
+    dX = torch.empty((rows, C), dtype=torch.float32, device=X.device)
+    dW = torch.zeros((wsets, C), dtype=torch.float32, device=X.device)
+    dB = torch.zeros_like(dW)
+    a = _ln_args(X, W, W, C=C, eps=eps, rows_per_wset=rows_per_wset)
+    a.ldy, a.mean, a.rstd = C, mean.data_ptr(), rstd.data_ptr()
+    a.dY, a.dX, a.lddx, a.accumulate, a.dW, a.dB = dY.data_ptr(), dX.data_ptr(), C, 0, dW.data_ptr(), dB.data_ptr()
+    N._check(N.lib().cmt_ln_train_bwd(ctypes.byref(a), N._stream()), "cmt_ln_train_bwd")
+    return dX, dW.view(-1), dB.view(-1)
+
+
+def _bn_args(X, W, Bv, mean_save, rstd_save, ws, eps=1e-5, momentum=0.1):
+    a = N.BnArgs()
+    a.rows, a.C = X.shape
+    a.X, a.W, a.B, a.eps, a.momentum = X.data_ptr(), W.data_ptr(), Bv.data_ptr(), eps, momentum
+    a.mean_save, a.rstd_save, a.workspace = mean_save.data_ptr(), rstd_save.data_ptr(), ws.data_ptr()
+    return a
+
+
+def bn_relu_train_fwd(X, W, Bv, running_mean=None, running_var=None, *, eps=1e-5, momentum=0.1):
+    """relu(BatchNorm2d-train(X)) over rows [B*H*W, C]; returns (Y, mean, rstd)."""
+    _f32(X, W, Bv, running_mean, running_var)
+    rows, C = X.shape
+    Y = torch.empty_like(X)
+    mean = torch.empty(C, dtype=torch.float32, device=X.device)
+    rstd = torch.empty_like(mean)
+    ws = torch.empty(int(N.lib().cmt_bn_workspace_bytes(C)), dtype=torch.uint8, device=X.device)
+    a = _bn_args(X, W, Bv, mean, rstd, ws, eps, momentum)
+    a.Y = Y.data_ptr()
+    a.running_mean, a.running_var = _ptr(running_mean), _ptr(running_var)
+    N._check(N.lib().cmt_bn_relu_train_fwd(ctypes.byref(a), N._stream()), "cmt_bn_relu_train_fwd")
+    return Y, mean, rstd
+
+
+def bn_relu_train_bwd(dY, X, Y, W, mean, rstd):
+    _f32(dY, X, Y, W, mean, rstd)
+    C = X.shape[1]
+    dX = torch.empty_like(X)
+    dW = torch.empty(C, dtype=torch.float32, device=X.device)
+    dB = torch.empty_like(dW)
+    ws = torch.empty(int(N.lib().cmt_bn_workspace_bytes(C)), dtype=torch.uint8, device=X.device)
+    a = _bn_args(X, W, W, mean, rstd, ws)
+    a.Y, a.dY, a.dX, a.dW, a.dB = Y.data_ptr(), dY.contiguous().data_ptr(), dX.data_ptr(), dW.data_ptr(), dB.data_ptr()
+    N._check(N.lib().cmt_bn_relu_train_bwd(ctypes.byref(a), N._stream()), "cmt_bn_relu_train_bwd")
+    return dX, dW, dB
+
+
+def im2col3x3(X, nimg, H, W, C):
+    _f32(X)
+    out = torch.empty((nimg * H * W, 9 * C), dtype=torch.float32, device=X.device)
+    N._check(N.lib().cmt_im2col3x3(X.data_ptr(), nimg, H, W, C, out.data_ptr(), N._stream()), "cmt_im2col3x3")
+    return out
+
+
+def det_loss(logits, labels, label_w, boxes, targets, box_w, *, gamma, alpha, cls_weight, box_weight, cls_avg,
+             box_avg, need_grad=True):
+    """(loss [2] device tensor, dlogits, dboxes) of FocalLoss + L1Loss."""
+    _f32(logits, boxes, targets, box_w, label_w)
+    N._dev(labels)
+    out = torch.empty(2, dtype=torch.float32, device=logits.device)
+    dl = torch.zeros_like(logits) if need_grad else None
+    db = torch.zeros_like(boxes) if need_grad else None
+    a = N.DetLossArgs()
+    a.R, a.ncls = logits.shape
+    a.logits, a.ld_logits, a.labels, a.label_w = logits.data_ptr(), logits.stride(0), labels.data_ptr(), _ptr(label_w)
+    a.Rb = boxes.shape[0]
+    a.boxes, a.ld_boxes, a.targets, a.box_w = boxes.data_ptr(), boxes.stride(0), targets.data_ptr(), box_w.data_ptr()
+    a.gamma, a.alpha, a.cls_weight, a.box_weight = gamma, alpha, cls_weight, box_weight
+    a.cls_avg, a.box_avg, a.gscale = cls_avg, box_avg, 1.0
+    a.out, a.dlogits, a.dboxes = out.data_ptr(), _ptr(dl), _ptr(db)
+    N._check(N.lib().cmt_det_loss(ctypes.byref(a), N._stream()), "cmt_det_loss")
+    return out, dl, db
+
+
+def match_cost(logits, boxes, gt, gt_labels, code_w, *, gamma, alpha, cls_weight, reg_weight):
+    _f32(logits, boxes, gt, code_w)
+    N._dev(gt_labels)
+    Nq, ngt = logits.shape[0], gt.shape[0]
+    cost = torch.empty((Nq, ngt), dtype=torch.float32, device=logits.device)
+    a = N.MatchCostArgs()
+    a.Nq, a.ngt = Nq, ngt
+    a.logits, a.ld_logits, a.boxes, a.ld_boxes = logits.data_ptr(), logits.stride(0), boxes.data_ptr(), boxes.stride(0)
+    a.gt, a.gt_labels, a.code_w = gt.data_ptr(), gt_labels.data_ptr(), code_w.data_ptr()
+    a.gamma, a.alpha, a.cls_weight, a.reg_weight, a.cost = gamma, alpha, cls_weight, reg_weight, cost.data_ptr()
+    N._check(N.lib().cmt_match_cost(ctypes.byref(a), N._stream()), "cmt_match_cost")
+    return cost
+
+
+def sumsq(x, out):
+    _f32(x, out)
+    N._check(N.lib().cmt_sumsq(x.data_ptr(), x.numel(), out.data_ptr(), N._stream()), "cmt_sumsq")
+
+
+def adamw_step(param, grad, exp_avg, exp_avg_sq, *, step, lr, beta1, beta2, eps, weight_decay, max_norm=0.0,
+               sumsq_buf=None):
+    _f32(param, grad, exp_avg, exp_avg_sq, sumsq_buf)
+    a = N.AdamwArgs()
+    a.n, a.step, a.lr, a.beta1, a.beta2, a.eps = param.numel(), step, lr, beta1, beta2, eps
+    a.weight_decay, a.max_norm = weight_decay, max_norm
+    a.param, a.grad, a.exp_avg, a.exp_avg_sq = param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr()
+    a.sumsq = _ptr(sumsq_buf)
+    N._check(N.lib().cmt_adamw_step(ctypes.byref(a), N._stream()), "cmt_adamw_step")

@@ -51,6 +51,13 @@ int64_t cmt_gemm_args_size(void);
 int64_t cmt_attn_args_size(void);
 int64_t cmt_ln_args_size(void);
 int64_t cmt_chain_args_size(void);
+int64_t cmt_gemm_ex_args_size(void);
+int64_t cmt_attn_train_args_size(void);
+int64_t cmt_ln_train_args_size(void);
+int64_t cmt_bn_args_size(void);
+int64_t cmt_det_loss_args_size(void);
+int64_t cmt_match_cost_args_size(void);
+int64_t cmt_adamw_args_size(void);
 
 /* ------------------------------------------------------------------------
  * GEMM with fused prologue/epilogue (MFMA, gfx950).
@@ -356,6 +363,145 @@ int cmt_box_decode(const float* logits, int64_t logit_bstride, const float* bbox
                    const int* class_task, int B, int Nq, int ncls, int code, int max_num,
                    const float* post_center_range6, float score_threshold, int use_threshold,
                    float* out_boxes, float* out_scores, int* out_labels, int* out_count, void* stream);
+
+/* ========================================================================
+ * TRAINING PATH (BASELINE configs[3] DDP training).
+ * Exact-f32 kernels (the reference trains the head in fp32), used by the
+ * torch.autograd Functions of projects/mmdet3d_plugin/models/utils/train_ops.py.
+ * ======================================================================== */
+
+/* cmt_gemm_f32_ex: C[z][m][n] = alpha * sum_k A(m,k) B(n,k) (+ bias[n]) + beta * C
+ *   A(m,k) = A[z*a_bs + m*a_sm + k*a_sk],  B(n,k) = B[z*b_bs + n*b_sn + k*b_sk]
+ * Any operand may be transposed (strides); k- or row-contiguous operands with
+ * 16-byte alignment are staged by 16-byte loads.  ksplit > 1 splits K over
+ * workgroups that add their partial sums into C with f32 atomics (beta = 1,
+ * the caller initialises C).  Replaces the cuBLAS GEMMs of every nn.Linear
+ * forward and backward (dX = dY W, dW = dY^T X) in the reference's training step. */
+typedef struct cmt_gemm_ex_args {
+    int M, N, K, batch;
+    float alpha, beta;
+    const float* A; int64_t a_sm, a_sk, a_bs;
+    const float* B; int64_t b_sn, b_sk, b_bs;
+    float* C; int64_t ldc, c_bs;
+    const float* bias;         /* optional [N] */
+    int ksplit;
+} cmt_gemm_ex_args;
+int cmt_gemm_f32_ex(const cmt_gemm_ex_args* args, void* stream);
+
+/* Attention forward with row statistics, and its backward (attn_train.hip),
+ * exact f32, head_dim 32.  Replaces, in the training step, the fp32
+ * self-attention core of nn.MultiheadAttention (with the DN mask of
+ * cmt_head.py:386-398 and attn_drop) and the flash-attn 0.2.2 cross core
+ * (attention.py:46-92; fp16_inputs = 1 rounds q, k, v, P and O to fp16 like
+ * that core).  Element (b, h, row, d) of X at X[b*x_bs + h*x_hs + row*x_rs + d];
+ * dQ / dK / dV use the strides of Q / K / V, dO those of O.
+ * fwd writes O and LSE[b][h][q] = log2 sum_k exp2(c s_qk) (c = scale log2 e);
+ * bwd reads Q, K, V, O, dO, LSE and writes dQ, dK, dV (delta: [B*H*Nq] scratch).
+ * DN mask (dn_pad > 0): key k < dn_pad is hidden from query q if q >= dn_pad or
+ * k / dn_group != q / dn_group.  dropout_p > 0: keep(q, k) from a counter hash
+ * of (seed, b, h, q, k), identical in fwd and bwd (training only). */
+typedef struct cmt_attn_train_args {
+    int B, H, Nq, Nk;
+    const float* Q; int64_t q_bs, q_hs, q_rs;
+    const float* K; int64_t k_bs, k_hs, k_rs;
+    const float* V; int64_t v_bs, v_hs, v_rs;
+    float* O; int64_t o_bs, o_hs, o_rs;
+    float* LSE;
+    const float* dO; float* dQ; float* dK; float* dV; float* delta;
+    float scale;
+    int dn_pad, dn_group;
+    int fp16_inputs;
+    float dropout_p; uint32_t seed;
+    int kv_splits;             /* fwd: 0 = automatic */
+    void* workspace; int64_t workspace_bytes;
+} cmt_attn_train_args;
+int64_t cmt_attn_train_workspace_bytes(const cmt_attn_train_args* args);
+int cmt_attn_train_fwd(const cmt_attn_train_args* args, void* stream);
+int cmt_attn_train_bwd(const cmt_attn_train_args* args, void* stream);
+
+/* Row LayerNorm with saved statistics (C = 64 or 256): nn.LayerNorm
+ * (mmcv LN, eps 1e-5) of the decoder and, with C = 64, eps 1e-6 and one weight
+ * set per rows_per_wset rows, GroupLayerNorm1d (cmt_head.py:53-94) whose
+ * custom backward (68-81) is the LayerNorm backward:
+ *   dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy w;
+ *   dW[set] += sum dy xhat, dB[set] += sum dy (f32 atomics; zero them first). */
+typedef struct cmt_ln_train_args {
+    int rows, C;
+    const float* X; int64_t ldx;
+    const float* W; const float* B; float eps;
+    int rows_per_wset;         /* 0 = one weight set */
+    float* Y; int64_t ldy;     /* fwd output; bwd: dY reads ldy */
+    float* mean; float* rstd;  /* [rows] saved by fwd, read by bwd */
+    const float* dY; float* dX; int64_t lddx; int accumulate;
+    float* dW; float* dB;
+} cmt_ln_train_args;
+int cmt_ln_train_fwd(const cmt_ln_train_args* args, void* stream);
+int cmt_ln_train_bwd(const cmt_ln_train_args* args, void* stream);
+
+/* BatchNorm2d in training mode (batch statistics over all NHWC rows, running
+ * stats updated with momentum, unbiased running var) fused with ReLU: the
+ * shared_conv ConvModule (cmt_head.py:280-287) after its 3x3 conv; and its
+ * backward (dX, dW, dB).  workspace: cmt_bn_workspace_bytes(C). */
+typedef struct cmt_bn_args {
+    int rows, C;
+    const float* X; float* Y;
+    const float* W; const float* B; float eps; float momentum;
+    float* running_mean; float* running_var;   /* optional */
+    float* mean_save; float* rstd_save;        /* [C] */
+    const float* dY; float* dX; float* dW; float* dB;
+    void* workspace;
+} cmt_bn_args;
+int64_t cmt_bn_workspace_bytes(int C);
+int cmt_bn_relu_train_fwd(const cmt_bn_args* args, void* stream);
+int cmt_bn_relu_train_bwd(const cmt_bn_args* args, void* stream);
+
+/* im2col of the 3x3 / pad 1 conv on NHWC rows (the weight-gradient operand of
+ * shared_conv): out[(img*H+y)*W+x][tap*C + c], tap = 3*dy + dx. */
+int cmt_im2col3x3(const float* X, int nimg, int H, int W, int C, float* out, void* stream);
+
+/* FocalLoss(use_sigmoid, gamma, alpha) + L1Loss of one task / decoder layer
+ * (mmdet 2.28.2; cmt_head.py:702-720, 777-812): out[0] = cls loss, out[1] =
+ * box loss; dlogits / dboxes (optional) receive d(loss)/d(input) * gscale.
+ * labels == ncls is background.  One workgroup, fixed reduction order. */
+typedef struct cmt_det_loss_args {
+    int R, ncls;
+    const float* logits; int64_t ld_logits;
+    const int* labels; const float* label_w;
+    int Rb;
+    const float* boxes; int64_t ld_boxes;
+    const float* targets; const float* box_w;  /* [Rb][10] */
+    float gamma, alpha, cls_weight, box_weight, cls_avg, box_avg, gscale;
+    float* out;                                 /* [2] */
+    float* dlogits; float* dboxes;
+} cmt_det_loss_args;
+int cmt_det_loss(const cmt_det_loss_args* args, void* stream);
+
+/* Hungarian cost matrix of HungarianAssigner3D (hungarian_assigner_3d.py:
+ * 120-136): FocalLossCost (eps 1e-12) * cls_weight + BBox3DL1Cost over the
+ * first 8 code-weighted box channels * reg_weight.  cost [Nq][ngt]. */
+typedef struct cmt_match_cost_args {
+    int Nq, ngt;
+    const float* logits; int64_t ld_logits;
+    const float* boxes; int64_t ld_boxes;
+    const float* gt; const int* gt_labels;      /* gt [ngt][10] normalized */
+    const float* code_w;                         /* [10] device */
+    float gamma, alpha, cls_weight, reg_weight;
+    float* cost;
+} cmt_match_cost_args;
+int cmt_match_cost(const cmt_match_cost_args* args, void* stream);
+
+/* cmt_sumsq: *out += sum x^2 (zero *out first).  cmt_adamw_step:
+ * torch.optim.AdamW over a flat buffer; if max_norm > 0 the gradient is scaled
+ * by min(1, max_norm / (sqrt(*sumsq) + 1e-6)) (clip_grad_norm_, mmcv
+ * OptimizerHook grad_clip). */
+int cmt_sumsq(const float* x, int64_t n, float* out, void* stream);
+typedef struct cmt_adamw_args {
+    int64_t n; int step;
+    float lr, beta1, beta2, eps, weight_decay, max_norm;
+    float* param; const float* grad; float* exp_avg; float* exp_avg_sq;
+    const float* sumsq;
+} cmt_adamw_args;
+int cmt_adamw_step(const cmt_adamw_args* args, void* stream);
 
 #ifdef __cplusplus
 }

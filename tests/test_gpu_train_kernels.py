@@ -1,0 +1,219 @@
+"""Training-path kernels (train.hip, attn_train.hip) against float64 PyTorch CPU
+autograd of the same math: general-stride GEMM (every transpose), attention
+forward statistics + backward (DN mask, ragged shapes, fp16-core rounding,
+hash dropout), LayerNorm / GroupLayerNorm1d, BatchNorm2d+ReLU (training
+statistics), im2col, FocalLoss+L1Loss, the Hungarian cost matrix and AdamW
+with gradient-norm clipping."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _T():
+    from projects.mmdet3d_plugin import native_train as T
+    return T
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [(100, 70, 50, False, False), (256, 256, 900, True, True),
+                                         (33, 257, 64, False, True), (64, 64, 4000, True, False)])
+def test_gemm_ex_transposes(dev, M, N, K, ta, tb):
+    T = _T()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g) if tb else torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = (A.double().t() if ta else A.double()) @ (B.double() if tb else B.double().t()) * 0.5 + bias.double()
+    Ad, Bd = A.to(dev), B.to(dev)
+    C = torch.empty(M, N, device=dev)
+    a_str = (1, M) if ta else (K, 1)
+    b_str = (1, N) if tb else (K, 1)
+    T.gemm_ex(Ad, a_str, Bd, b_str, C, M=M, N_=N, K=K, ldc=N, alpha=0.5, bias=bias.to(dev))
+    C2 = torch.zeros(M, N, device=dev)
+    T.gemm_ex(Ad, a_str, Bd, b_str, C2, M=M, N_=N, K=K, ldc=N, alpha=0.5, beta=1.0, bias=bias.to(dev), ksplit=4)
+    torch.cuda.synchronize()
+    tol = 1e-5 * math.sqrt(K) * 4
+    assert (C.cpu().double() - ref).abs().max().item() < tol
+    assert (C2.cpu().double() - ref).abs().max().item() < tol
+
+
+def _mix32(x):
+    x = x.astype(np.uint64) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7feb352d) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846ca68b) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def keep_mask(seed, B, H, Nq, Nk, p):
+    """Host restatement of attn_train.hip keep(): keep iff hash >= p * 2^32."""
+    bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
+    q = np.arange(Nq, dtype=np.uint64)[None, :, None]
+    k = np.arange(Nk, dtype=np.uint64)[None, None, :]
+    h = _mix32(np.uint64(seed) ^ _mix32((bh * 0x9e3779b9 + q) & 0xFFFFFFFF))
+    h = _mix32(h ^ ((k * 0x85ebca6b) & 0xFFFFFFFF))
+    thr = min(int(p * 4294967296.0), 0xFFFFFFFF)
+    return torch.from_numpy(h >= thr).view(B, H, Nq, Nk)
+
+
+def dn_mask(Nq, Nk, pad, grp):
+    q = torch.arange(Nq)[:, None]
+    k = torch.arange(Nk)[None, :]
+    return (k < pad) & ((q >= pad) | (k // grp != q // grp))
+
+
+@pytest.mark.parametrize("B,Nq,Nk,pad,grp,fp16,p", [(1, 100, 1000, 0, 0, False, 0.0), (2, 70, 70, 30, 10, False, 0.0),
+                                                    (1, 140, 140, 40, 8, False, 0.25), (1, 96, 3000, 0, 0, True, 0.0)])
+def test_attention_train_fwd_bwd(dev, B, Nq, Nk, pad, grp, fp16, p):
+    T = _T()
+    H, C = 8, 256
+    g = torch.Generator().manual_seed(Nq * 7 + Nk)
+    q = torch.randn(B, Nq, C, generator=g)
+    k = torch.randn(B, Nk, C, generator=g)
+    v = torch.randn(B, Nk, C, generator=g)
+    do = torch.randn(B, Nq, C, generator=g)
+    seed = 1234
+
+    def ref_fn(q, k, v):
+        def r(t):
+            return t.half().double() if fp16 else t
+        qh = r(q).view(B, Nq, H, 32).transpose(1, 2)
+        kh = r(k).view(B, Nk, H, 32).transpose(1, 2)
+        vh = r(v).view(B, Nk, H, 32).transpose(1, 2)
+        s = qh @ kh.transpose(-1, -2) / math.sqrt(32)
+        if pad:
+            s = s.masked_fill(dn_mask(Nq, Nk, pad, grp), float("-inf"))
+        pr = torch.softmax(s, -1)
+        if p > 0:
+            pr = pr * keep_mask(seed, B, H, Nq, Nk, p).double() / (1 - p)
+        return (pr @ vh).transpose(1, 2).reshape(B, Nq, C)
+    qd, kd, vd = (t.double().requires_grad_() for t in (q, k, v))
+    ref = ref_fn(qd, kd, vd)
+    ref.backward(do.double())
+    qg, kg, vg = (t.to(dev).requires_grad_() for t in (q, k, v))
+    from projects.mmdet3d_plugin.models.utils import train_ops as O
+    out = O.attention(qg, kg, vg, H, dn_pad=pad, dn_group=grp, fp16=fp16, dropout_p=p, seed=seed)
+    out.backward(do.to(dev))
+    torch.cuda.synchronize()
+    tol = 2e-3 if fp16 else 2e-5
+    assert (out.detach().cpu().double() - ref.detach()).abs().max().item() < tol
+    for got, want, name in ((qg.grad, qd.grad, "dq"), (kg.grad, kd.grad, "dk"), (vg.grad, vd.grad, "dv")):
+        err = (got.cpu().double() - want).abs().max().item() / max(want.abs().max().item(), 1e-6)
+        assert err < (5e-3 if fp16 else 2e-5), (name, err)
+
+
+@pytest.mark.parametrize("rows,C,G,eps", [(333, 256, 1, 1e-5), (6 * 70, 64, 6, 1e-6)])
+def test_layernorm_train(dev, rows, C, G, eps):
+    from projects.mmdet3d_plugin.models.utils import train_ops as O
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randn(rows, C, generator=g) * 2 + 0.5
+    w = torch.randn(G * C, generator=g)
+    b = torch.randn(G * C, generator=g)
+    dy = torch.randn(rows, C, generator=g)
+    xd, wd, bd = (t.double().requires_grad_() for t in (x, w, b))
+    R = rows // G
+    ref = torch.cat([torch.nn.functional.layer_norm(xd[i * R:(i + 1) * R], (C,), wd[i * C:(i + 1) * C],
+                                                    bd[i * C:(i + 1) * C], eps) for i in range(G)])
+    ref.backward(dy.double())
+    xg, wg, bg = (t.to(dev).requires_grad_() for t in (x, w, b))
+    out = O.layer_norm(xg, wg, bg, eps) if G == 1 else O.group_layer_norm(xg.view(G, R, C), wg, bg, eps).view(rows, C)
+    out.backward(dy.to(dev))
+    torch.cuda.synchronize()
+    assert (out.detach().cpu().double() - ref.detach()).abs().max().item() < 1e-5
+    for got, want in ((xg.grad, xd.grad), (wg.grad, wd.grad), (bg.grad, bd.grad)):
+        assert (got.cpu().double() - want).abs().max().item() < 1e-4 * max(1.0, want.abs().max().item())
+
+
+def test_bn_relu_and_conv_weight_grad(dev):
+    from projects.mmdet3d_plugin.models.utils import train_ops as O
+    g = torch.Generator().manual_seed(5)
+    B, H, W, Cin, Cout = 2, 9, 11, 16, 32
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * 0.2
+    bn = torch.nn.BatchNorm2d(Cout).double()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    bn.train()
+    wd = w.double().requires_grad_()
+    ref = torch.relu(bn(torch.nn.functional.conv2d(x.double(), wd, padding=1)))
+    dy = torch.randn(ref.shape, generator=g).double()
+    ref.backward(dy)
+    bng = torch.nn.BatchNorm2d(Cout).to(dev)
+    with torch.no_grad():
+        bng.weight.copy_(bn.weight.float())
+        bng.bias.copy_(bn.bias.float())
+    xr = x.permute(0, 2, 3, 1).reshape(-1, Cin).contiguous().to(dev)
+    wt = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).contiguous().to(dev).requires_grad_()
+    y = O.bn_relu(O.conv3x3(xr, wt, (B, H, W, Cin)), bng)
+    y.backward(dy.float().permute(0, 2, 3, 1).reshape(-1, Cout).to(dev))
+    torch.cuda.synchronize()
+    got = y.detach().cpu().view(B, H, W, Cout).permute(0, 3, 1, 2).double()
+    assert (got - ref.detach()).abs().max().item() < 1e-4
+    gw = wt.grad.cpu().view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).double()
+    assert (gw - wd.grad).abs().max().item() < 1e-3 * max(1.0, wd.grad.abs().max().item())
+    assert (bng.weight.grad.cpu().double() - bn.weight.grad).abs().max().item() < 1e-3
+    assert (bng.bias.grad.cpu().double() - bn.bias.grad).abs().max().item() < 1e-3
+    assert (bng.running_mean.cpu().double() - bn.running_mean).abs().max().item() < 1e-5
+    assert (bng.running_var.cpu().double() - bn.running_var).abs().max().item() < 1e-4
+
+
+def test_det_loss_and_match_cost(dev):
+    from oracle import cmt_train_oracle as TO
+    T = _T()
+    g = torch.Generator().manual_seed(9)
+    R, ncls, Rb = 300, 10, 40
+    logits = torch.randn(R, ncls, generator=g) * 2
+    labels = torch.randint(0, ncls + 1, (R,), generator=g)
+    lw = torch.rand(R, generator=g)
+    boxes = torch.randn(Rb, 10, generator=g)
+    tg = torch.randn(Rb, 10, generator=g)
+    bw = torch.rand(Rb, 10, generator=g)
+    cfg = dict(gamma=2.0, alpha=0.25, cls_weight=2.0, box_weight=0.25, cls_avg=37.5, box_avg=12.0)
+    ld, bd = logits.double().requires_grad_(), boxes.double().requires_grad_()
+    lc = TO.focal_loss(ld, labels, lw.double(), 2.0, 0.25, 2.0, 37.5)
+    lb = TO.l1_loss(bd, tg.double(), bw.double(), 0.25, 12.0)
+    (lc + lb).backward()
+    out, dl, db = T.det_loss(logits.to(dev), labels.int().to(dev), lw.to(dev), boxes.to(dev), tg.to(dev), bw.to(dev),
+                             **cfg)
+    torch.cuda.synchronize()
+    assert abs(out[0].item() - lc.item()) < 1e-4 * max(1, abs(lc.item()))
+    assert abs(out[1].item() - lb.item()) < 1e-4 * max(1, abs(lb.item()))
+    assert (dl.cpu().double() - ld.grad).abs().max().item() < 1e-5
+    assert (db.cpu().double() - bd.grad).abs().max().item() < 1e-6
+    gt = torch.randn(7, 10, generator=g)
+    gl = torch.randint(0, ncls, (7,), generator=g)
+    cw = torch.tensor([2.0, 2.0, 1, 1, 1, 1, 1, 1, 0.2, 0.2])
+    ref = TO.match_cost(logits.double(), boxes[:1].repeat(R, 1).double(), gt.double(), gl, cw.double(), 2.0, 0.25)
+    got = T.match_cost(logits.to(dev), boxes[:1].repeat(R, 1).to(dev), gt.to(dev), gl.int().to(dev), cw.to(dev),
+                       gamma=2.0, alpha=0.25, cls_weight=2.0, reg_weight=0.25)
+    torch.cuda.synchronize()
+    assert (got.cpu().double() - ref).abs().max().item() < 1e-4
+
+
+def test_adamw_with_clip(dev):
+    T = _T()
+    g = torch.Generator().manual_seed(3)
+    n = 10000
+    p0 = torch.randn(n, generator=g)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01)
+    pd = p0.to(dev)
+    m, v = torch.zeros_like(pd), torch.zeros_like(pd)
+    for step in range(1, 4):
+        grad = torch.randn(n, generator=g) * 3
+        ref.grad = grad.clone()
+        torch.nn.utils.clip_grad_norm_([ref], 35.0)
+        opt.step()
+        ss = torch.zeros(1, device=dev)
+        gd = grad.to(dev)
+        T.sumsq(gd, ss)
+        T.adamw_step(pd, gd, m, v, step=step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01,
+                     max_norm=35.0, sumsq_buf=ss)
+    torch.cuda.synchronize()
+    assert (pd.cpu() - ref.detach()).abs().max().item() < 1e-5

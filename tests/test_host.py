@@ -93,7 +93,7 @@ def test_c_abi_exports_every_declared_symbol():
     assert len(syms) >= 15
     for s in syms:
         assert hasattr(L, s), s
-    assert L.cmt_abi_version() == native.ABI_VERSION == 7
+    assert L.cmt_abi_version() == native.ABI_VERSION == 8
 
 
 def test_c_abi_argument_errors_without_device():
@@ -126,12 +126,18 @@ def test_head_forward_refuses_cpu():
         head([torch.zeros(1, 512, 16, 16)], None, [dict()])
 
 
-def test_training_forward_not_silently_supported():
+def test_training_forward_reads_gt_and_has_no_cpu_fallback():
+    """Training-mode forward takes its GT from img_metas like the reference's
+    prepare_for_dn (cmt_head.py:341-342) and runs only on the HIP kernels."""
     from projects.mmdet3d_plugin import synthetic as S
     head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=16, num_layers=1, grid_size=[128, 128, 40])
     head.train()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(KeyError):
         head([torch.zeros(1, 512, 16, 16)], None, [dict()])
+    meta = dict(gt_bboxes_3d=torch.tensor([[1.0, 2.0, 0.5, 2.0, 4.0, 1.5, 0.3, 0.0, 0.0]]),
+                gt_labels_3d=torch.tensor([0]))
+    with pytest.raises(RuntimeError, match="HIP device"):
+        head([torch.zeros(1, 512, 16, 16)], None, [meta])
 
 
 def test_pack_cache_invalidates_on_weight_change():
