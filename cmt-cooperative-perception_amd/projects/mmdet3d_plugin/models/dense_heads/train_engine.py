@@ -77,6 +77,7 @@ class HeadTrainMixin:
 
     train_dropout = True   # the reference trains with dropout 0.1 (attn_drop of the self-attention core and
     #                        the dropout_layer after both attentions); parity tests switch it off
+    train_cross_fp16 = True   # the flash-attn fp16 cross core (reference numerics); off = exact f32 core
 
     # ------------------------------------------------------------------ DN queries
     def prepare_for_dn_train(self, B, gt_boxes, gt_labels, rand_prob=None, generator=None):
@@ -210,7 +211,7 @@ class HeadTrainMixin:
             wq, wk, wv = ca.in_proj_weight.chunk(3)
             bq, bk, bv = ca.in_proj_bias.chunk(3) if ca.in_proj_bias is not None else (None, None, None)
             o = ops.attention(ops.linear(tgt + qpos, wq, bq), ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H,
-                              fp16=True)
+                              fp16=self.train_cross_fp16)
             tgt = ops.layer_norm(tgt + self._drop(ops.linear(o, ca.out_proj.weight, ca.out_proj.bias)),
                                  nm[1].weight, nm[1].bias, nm[1].eps)
             l1, l2 = ffn.layers[0][0], ffn.layers[1]

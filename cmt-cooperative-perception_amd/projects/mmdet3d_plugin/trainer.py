@@ -1,0 +1,105 @@
+"""Data-parallel training step of the head (BASELINE.json configs[3]: CMTCoop
+DDP training on 8 GPUs with RCCL gradient all-reduce over xGMI).
+
+Reference: tools/dist_train.sh:10-20 (one process per GPU), tools/train.py:
+197-204 (init_dist 'nccl'), mmcv MMDistributedDataParallel (bucketed gradient
+all-reduce, sum then / world), mmcv OptimizerHook with grad_clip max_norm 35
+(configs e.g. CMTCoop_TUMTraf/fusion/coop/...py:373-376), torch.optim.AdamW
+(lr 1e-4, weight_decay 0.01, ...py:362-372).
+
+MI355X design: every trainable parameter of the head is re-pointed into ONE
+flat fp32 buffer and its .grad into ONE flat gradient buffer (autograd then
+accumulates straight into it), so the gradient exchange is a few large
+RCCL all-reduces over contiguous buckets (fewer, larger collectives: each
+xGMI ring step moves bucket/world bytes per link), the clip's global norm is
+one native sum-of-squares pass and the AdamW update one native launch over
+the whole buffer.  With world size 1 there is no collective at all.
+"""
+import torch
+import torch.distributed as dist
+
+from . import native_train as T
+
+__all__ = ["FlatParams", "Trainer", "allreduce_buckets"]
+
+
+class FlatParams:
+    """Trainable parameters of ``module`` as views of one flat buffer."""
+
+    def __init__(self, module):
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        self.slices = []
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            self.slices.append((off, k))
+            off += k
+
+    def zero_grad(self):
+        self.grad.zero_()
+        # autograd accumulates in place into existing .grad tensors (grad mode is off during backward);
+        # re-attach in case a caller replaced one
+        for p, (off, k) in zip(self.params, self.slices):
+            if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
+                p.grad = self.grad[off:off + k].view_as(p)
+
+
+def allreduce_buckets(flat, bucket_bytes=25 << 20, group=None):
+    """Mean over ranks of ``flat`` in place: contiguous buckets of at most
+    ``bucket_bytes``, all launched asynchronously (RCCL over xGMI on the GPU
+    box, gloo in the CPU tests), then one scale by 1/world."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0
+    world = dist.get_world_size(group)
+    if world == 1:
+        return 0
+    per = max(1, bucket_bytes // flat.element_size())
+    works = [dist.all_reduce(flat[i:i + per], group=group, async_op=True) for i in range(0, flat.numel(), per)]
+    for w in works:
+        w.wait()
+    flat.mul_(1.0 / world)
+    return len(works)
+
+
+class Trainer:
+    """One optimisation step: backward of the summed loss dict, bucketed
+    gradient all-reduce, clip_grad_norm_(max_norm), AdamW."""
+
+    def __init__(self, module, lr=1e-4, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-8, max_norm=35.0,
+                 bucket_mb=25, group=None):
+        self.module = module
+        self.fp = FlatParams(module)
+        self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.group = group
+        self.exp_avg = torch.zeros_like(self.fp.flat)
+        self.exp_avg_sq = torch.zeros_like(self.fp.flat)
+        self.sumsq = torch.zeros(1, dtype=torch.float32, device=self.fp.flat.device)
+        self.step_count = 0
+
+    def backward(self, losses):
+        total = sum(losses.values()) if isinstance(losses, dict) else losses
+        self.fp.zero_grad()
+        total.backward()
+        return total
+
+    def step(self, losses):
+        total = self.backward(losses)
+        allreduce_buckets(self.fp.grad, self.bucket_bytes, self.group)
+        self.step_count += 1
+        self.sumsq.zero_()
+        if self.max_norm and self.max_norm > 0:
+            T.sumsq(self.fp.grad, self.sumsq)
+        T.adamw_step(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, step=self.step_count, lr=self.lr,
+                     beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=self.wd,
+                     max_norm=self.max_norm or 0.0, sumsq_buf=self.sumsq)
+        return total.detach()

@@ -80,6 +80,7 @@ def linear(x, w, b=None):
 
 def mlp2(x, sd, prefix):
     """nn.Sequential(Linear, ReLU, Linear) -- cmt_head.py:292-301."""
+    x = x.to(sd[prefix + ".0.weight"].dtype)
     h = F.relu(linear(x, sd[prefix + ".0.weight"], sd[prefix + ".0.bias"]))
     return linear(h, sd[prefix + ".2.weight"], sd[prefix + ".2.bias"])
 
@@ -124,10 +125,11 @@ def rv_query_embed(ref_points, img_metas, pc_range, depth_num, sd, prefix="rv_em
     Quirks: z-divide with +-1e-6 sign epsilon (z becomes ~+-1), mask tested
     against pad_shape, masked sum over views."""
     pad_h, pad_w, _ = img_metas[0]["pad_shape"][0]
+    dt = ref_points.dtype   # fp32 (eval restatement) or fp64 (training-gradient checks)
     lidars2imgs = torch.from_numpy(np.stack([np.asarray(m["lidar2img"], dtype=np.float64)
-                                             for m in img_metas])).float()
-    imgs2lidars = torch.from_numpy(np.stack([_np_inv(m["lidar2img"]) for m in img_metas])).float()
-    pcr = torch.tensor(pc_range, dtype=torch.float32)
+                                             for m in img_metas])).float().to(dt)
+    imgs2lidars = torch.from_numpy(np.stack([_np_inv(m["lidar2img"]) for m in img_metas])).float().to(dt)
+    pcr = torch.tensor(pc_range, dtype=torch.float32).to(dt)
     ref_points = ref_points * (pcr[3:] - pcr[:3]) + pcr[:3]
     proj_points = torch.einsum(
         "bnd, bvcd -> bvnc",
@@ -138,7 +140,7 @@ def rv_query_embed(ref_points, img_metas, pc_range, depth_num, sd, prefix="rv_em
     proj[..., :3] = proj_points[..., :3] / (proj_points[..., 2:3] + z_mask * 1e-6 - (~z_mask) * 1e-6)
     mask = (proj[..., 0] < pad_w) & (proj[..., 0] >= 0) & (proj[..., 1] < pad_h) & (proj[..., 1] >= 0)
     mask &= z_mask.squeeze(-1)
-    coords_d = 1 + torch.arange(depth_num).float() * (pc_range[3] - 1) / depth_num
+    coords_d = (1 + torch.arange(depth_num).float() * (pc_range[3] - 1) / depth_num).to(dt)
     proj = torch.einsum("bvnc, d -> bvndc", proj, coords_d)
     proj = torch.cat([proj[..., :3], proj.new_ones(*proj.shape[:-1], 1)], dim=-1)
     back = torch.einsum("bvndo, bvco -> bvndc", proj, imgs2lidars)

@@ -1,0 +1,128 @@
+"""The native training step of the head against the float64 autograd
+restatement (oracle/cmt_train_oracle.py) on identical inputs: DN queries from
+the same centre noise, the DN self-attention mask, Hungarian matching, focal /
+L1 / DN losses, and the gradient of EVERY trainable parameter (shared_conv with
+batch statistics, bev / rv embedding MLPs, reference points through the DN
+padding and the query embedding, all decoder layers, task heads incl.
+GroupLayerNorm1d).  Dropout off (it is random in both); the cross-attention
+core in exact f32 for the tight comparison, then with the reference's fp16
+core emulation at a looser bound."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _gt(B, pc_range, ncls, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    boxes, labels = [], []
+    for b in range(B):
+        lo, hi = torch.tensor(pc_range[:3]), torch.tensor(pc_range[3:])
+        c = lo + (hi - lo) * (0.15 + 0.7 * torch.rand(n, 3, generator=g))
+        d = 1.0 + 3.0 * torch.rand(n, 3, generator=g)
+        yaw = (torch.rand(n, 1, generator=g) * 2 - 1) * 3.0
+        vel = torch.randn(n, 2, generator=g)
+        boxes.append(torch.cat([c, d, yaw, vel], 1))
+        labels.append(torch.randint(0, ncls, (n,), generator=g))
+    return boxes, labels
+
+
+def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5):
+    from oracle import cmt_oracle as O
+    from oracle import cmt_train_oracle as TO
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head(name, num_query=Nq, num_layers=L, grid_size=[128, 128, 40])
+    oc = O.cfg_from_head_cfg(cfg)
+    sd_cpu = {k: v.detach().double().clone() for k, v in head.state_dict().items()}
+    pcr = list(head.pc_range)
+    ncls = head.num_classes[0]
+    gtb, gtl = _gt(B, pcr, ncls, ngt, seed=3)
+    groups = min(head.scalar, Nq // ngt)
+    rand_prob = torch.rand(groups * B * ngt, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1
+    x = S.synthetic_bev(B, 16, 16, seed=5)
+    xi = S.synthetic_img(B * 2, 8, 20, seed=6) if variant == "fusion" else None
+    metas = S.synthetic_metas(B, yaws=S.NUS_YAWS[:2], pad_shape=(128, 320, 3), seed=7) if variant == "fusion" \
+        else [dict() for _ in range(B)]
+
+    # ---- oracle, float64
+    params = {k: v.clone().requires_grad_() for k, v in sd_cpu.items() if not k.endswith(("running_mean", "running_var",
+                                                                                          "num_batches_tracked"))}
+    sd64 = dict(sd_cpu, **params)
+    ref_p, pad, single_pad, _, md = TO.prepare_for_dn(sd64["reference_points.weight"], [b.double() for b in gtb], gtl,
+                                                      Nq, head.scalar, head.bbox_noise_scale, head.bbox_noise_trans,
+                                                      head.split, pcr, head.num_classes, rand_prob.double())
+    preds64 = TO.head_train_forward(oc, sd64, [("", x.double(), None if xi is None else xi.double())], metas,
+                                    variant, ref_p, pad, single_pad)
+    lc = head._loss_cfg()
+    code_w = torch.tensor(lc["code_weights"], dtype=torch.float64)
+    loss_cfg = dict(gamma=lc["gamma"], alpha=lc["alpha"], cls_weight=lc["cls_weight"], box_weight=lc["box_weight"],
+                    match_cls_weight=lc["match_cls_weight"], match_reg_weight=lc["match_reg_weight"])
+    l64 = TO.head_loss(preds64, [b.double() for b in gtb], gtl, md, head.class_names, pcr, code_w, loss_cfg,
+                       head.dn_weight, head.split)
+    sum(l64.values()).backward()
+
+    # ---- native, fp32 on the GPU
+    head.to(dev).train()
+    head.train_dropout = False
+    head.train_cross_fp16 = fp16
+    preds = head.forward_train([(x.to(dev), None if xi is None else xi.to(dev), metas)], metas,
+                               [b.to(dev) for b in gtb], [l.to(dev) for l in gtl], rand_prob=rand_prob.to(dev))
+    losses = head.loss([b.to(dev) for b in gtb], [l.to(dev) for l in gtl], [[p] for p in preds])
+    sum(losses.values()).backward()
+    torch.cuda.synchronize()
+
+    assert set(losses) == set(l64), (sorted(losses), sorted(l64))
+    lerr = max(abs(losses[k].item() - l64[k].item()) / max(abs(l64[k].item()), 1e-3) for k in l64)
+    gerr, worst = 0.0, None
+    named = dict(head.named_parameters())
+    # error of each parameter's gradient relative to its own scale, floored at 1e-3 of the largest
+    # gradient entry of the step: layer 0's self-attention sees a zero target (cmt_transformer.py:114),
+    # so V = bias for every key, dS = P (dP - delta) = 0 exactly and its Q / K in_proj gradients are
+    # pure rounding noise (~1e-9 of the step) in both computations
+    floor = 1e-3 * max(p.grad.abs().max().item() for p in params.values() if p.grad is not None)
+    for k, p in params.items():
+        want = p.grad
+        got = named[k].grad
+        if want is None:
+            assert got is None or got.abs().max().item() == 0.0, k
+            continue
+        e = (got.detach().cpu().double() - want).abs().max().item() / max(want.abs().max().item(), floor)
+        if e > gerr:
+            gerr, worst = e, k
+    parity_log.append(f"training step {name} ({variant}, Nq {Nq}+DN {pad}, L {L}, cross core "
+                      f"{'fp16' if fp16 else 'f32'}) vs float64 autograd: losses max rel {lerr:.1e}, "
+                      f"param grads max rel {gerr:.1e} ({worst})")
+    return lerr, gerr, worst
+
+
+@pytest.mark.parametrize("name,variant", [("cmt_fusion_nus", "fusion"), ("cmt_lidar_nus", "lidar")])
+def test_training_step_grads_match_float64(dev, parity_log, name, variant):
+    lerr, gerr, worst = _run(name, variant, dev, parity_log, fp16=False)
+    assert lerr < 2e-4
+    assert gerr < 5e-3, worst
+
+
+def test_training_step_fp16_core_close(dev, parity_log):
+    lerr, gerr, worst = _run("cmt_fusion_nus", "fusion", dev, parity_log, fp16=True)
+    assert lerr < 5e-3
+    assert gerr < 5e-2, worst
+
+
+def test_trainer_step_reduces_loss(dev):
+    """Native AdamW + clip on the flat buffers: a few steps on one batch lower the loss."""
+    from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.trainer import Trainer
+    head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=32, num_layers=1, grid_size=[128, 128, 40],
+                                        device=dev)
+    head.train()
+    head.train_dropout = False
+    gtb, gtl = _gt(1, list(head.pc_range), head.num_classes[0], 4, seed=8)
+    gtb, gtl = [b.to(dev) for b in gtb], [l.to(dev) for l in gtl]
+    x = S.synthetic_bev(1, 16, 16, seed=9).to(dev)
+    tr = Trainer(head, lr=1e-3)
+    rp = torch.rand(8 * 4, 3, generator=torch.Generator().manual_seed(1)).to(dev) * 2 - 1
+    vals = []
+    for _ in range(4):
+        preds = head.forward_train([(x, None, [dict()])], [dict()], gtb, gtl, rand_prob=rp)
+        vals.append(tr.step(head.loss(gtb, gtl, [[p] for p in preds])).item())
+    assert vals[-1] < vals[0], vals

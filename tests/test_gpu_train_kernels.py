@@ -132,7 +132,7 @@ def test_layernorm_train(dev, rows, C, G, eps):
 def test_bn_relu_and_conv_weight_grad(dev):
     from projects.mmdet3d_plugin.models.utils import train_ops as O
     g = torch.Generator().manual_seed(5)
-    B, H, W, Cin, Cout = 2, 9, 11, 16, 32
+    B, H, W, Cin, Cout = 2, 9, 11, 32, 64
     x = torch.randn(B, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, 3, 3, generator=g) * 0.2
     bn = torch.nn.BatchNorm2d(Cout).double()

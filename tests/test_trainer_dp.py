@@ -1,0 +1,77 @@
+"""The DDP gradient exchange of the training step (trainer.py) on CPU:
+world_size-2 gloo ranks, several buckets, the all-reduced (mean) gradients
+equal the single-process sum / world; FlatParams keeps every .grad a view of
+the flat buffer autograd accumulates into."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "cmt-cooperative-perception_amd"))
+    from projects.mmdet3d_plugin.trainer import FlatParams, allreduce_buckets
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 10))
+    fp = FlatParams(model)
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(32, 64, generator=g)
+    fp.zero_grad()
+    model(x).pow(2).sum().backward()
+    local = fp.grad.clone()
+    nb = allreduce_buckets(fp.grad, bucket_bytes=4096)
+    q.put((rank, local, fp.grad.clone(), nb, [p.grad.data_ptr() for p in fp.params], fp.grad.data_ptr()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_matches_single_process_sum():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, l0, r0, nb, ptrs, base), (_, l1, r1, _, _, _) = res
+    assert nb > 1                                              # several buckets
+    assert torch.allclose(r0, (l0 + l1) / 2, atol=1e-6) and torch.equal(r0, r1)
+    assert ptrs[0] == base                                      # grads are views of the flat buffer
+
+
+def test_flat_params_single_process_grads_alias():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "cmt-cooperative-perception_amd"))
+    from projects.mmdet3d_plugin.trainer import FlatParams, allreduce_buckets
+    torch.manual_seed(1)
+    m = torch.nn.Linear(8, 4)
+    ref = torch.nn.Linear(8, 4)
+    ref.load_state_dict(m.state_dict())
+    fp = FlatParams(m)
+    x = torch.randn(5, 8)
+    for _ in range(2):           # accumulation into the views across backward calls
+        fp.zero_grad()
+        m(x).sum().backward()
+    ref(x).sum().backward()
+    assert torch.allclose(fp.grad, torch.cat([ref.weight.grad.view(-1), ref.bias.grad.view(-1)]))
+    assert allreduce_buckets(fp.grad) == 0                      # no process group: no collective
