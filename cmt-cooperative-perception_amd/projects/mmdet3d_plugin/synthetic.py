@@ -51,6 +51,9 @@ def make_head_cfg(name, num_query=900, num_layers=None, grid_size=None, head_typ
                         num_classes=len(classes)),
         separate_head=dict(type="SeparateTaskHead", init_bias=-2.19, final_kernel=c["final_kernel"]),
         transformer=dict(type=c["transformer_type"], decoder=decoder),
+        # the reference configs' losses (e.g. CMTCoop_TUMTraf/fusion/coop/...py:327-328)
+        loss_cls=dict(type="FocalLoss", use_sigmoid=True, gamma=2, alpha=0.25, reduction="mean", loss_weight=2.0),
+        loss_bbox=dict(type="L1Loss", reduction="mean", loss_weight=0.25),
         train_cfg=None,
         test_cfg=dict(grid_size=grid, out_size_factor=8, pc_range=c["point_cloud_range"], voxel_size=c["voxel_size"],
                       nms_type=None, max_num=200),
@@ -135,6 +138,25 @@ def synthetic_img(BV, h=40, w=100, C=256, seed=0, device=None):
     g = torch.Generator().manual_seed(seed + 7)
     x = torch.randn((BV, C, h, w), generator=g)
     return x.to(device) if device is not None else x
+
+
+def synthetic_gt(B, pc_range, num_classes, n=20, seed=0, device=None):
+    """Training targets (20 boxes per frame):
+    gravity-centre boxes [n, 9] (x, y, z, w, l, h, yaw, vx, vy) inside the
+    central 70 % of the range, dims 1-4 m, and labels < num_classes."""
+    g = torch.Generator().manual_seed(seed + 29)
+    boxes, labels = [], []
+    lo, hi = torch.tensor(pc_range[:3]), torch.tensor(pc_range[3:])
+    for _ in range(B):
+        c = lo + (hi - lo) * (0.15 + 0.7 * torch.rand(n, 3, generator=g))
+        d = 1.0 + 3.0 * torch.rand(n, 3, generator=g)
+        yaw = (torch.rand(n, 1, generator=g) * 2 - 1) * math.pi
+        vel = torch.randn(n, 2, generator=g)
+        b = torch.cat([c, d, yaw, vel], 1)
+        l = torch.randint(0, num_classes, (n,), generator=g)
+        boxes.append(b.to(device) if device is not None else b)
+        labels.append(l.to(device) if device is not None else l)
+    return boxes, labels
 
 
 def synthetic_points(N, pc_range, seed=0, device=None, margin=0.0):
