@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 namespace {
 
@@ -59,7 +60,19 @@ struct AttnKParams {
     int tiles_per_split;
     int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
     int sync_all;                   // diagnostics: drain every LDS-DMA before each tile (flag bit 1 << 8)
+    unsigned long long* stamp;      // diagnostics build only (CMT_ATTN_STAMP): per-wave segment cycle sums
 };
+
+// In-kernel segment stamp (diagnostic build of attn_pb_kernel only): shader
+// clock, with the lgkmcnt(0) the s_memtime result needs inside the statement.
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+constexpr int kStampSlots = 16;
 
 // Final normalised output: 4 consecutive head dims of one query row.
 __device__ __forceinline__ void store_o4(const AttnKParams& p, int b, int q, int d0, f32x4 v) {
@@ -580,6 +593,35 @@ __device__ __forceinline__ void pp_vseg(f32x16 (&s)[2], typename mfma_traits<T>:
     }
 }
 
+// Wave-wide max of the max-|k|^2 partials (each covers kmax_rows key rows)
+// over the key range of this workgroup's split of batch b, head h: the bound
+// only has to hold for the keys this workgroup scores (the split combine
+// merges per-split offsets).  16 independent loads per lane in flight; the
+// first form reduced all Nk / kmax_rows partials of the head in every wave
+// (2048 waves x 882 scattered loads at the fusion shape, ~4 us of prologue).
+__device__ __forceinline__ float kmax_reduce(const AttnKParams& p, int b, int h, int split, int lane) {
+    const int key0 = split * p.tiles_per_split * KT;
+    const int key1 = min(p.Nk, key0 + p.tiles_per_split * KT);
+    if (key0 >= key1) return 0.f;
+    const int64_t r0 = (int64_t)b * p.Nk;
+    const int e0 = (int)((r0 + key0) / p.kmax_rows), e1 = (int)((r0 + key1 - 1) / p.kmax_rows);
+    const float* src = p.kmax2 + p.kmax_plane0 + h;
+    float km = 0.f;
+    for (int base = e0 + lane; base <= e1; base += 64 * 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int e = base + 64 * j;
+            v[j] = e <= e1 ? src[(int64_t)e * p.kmax_ld] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) km = fmaxf(km, v[j]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
+    return km;
+}
+
 template <int N>
 __device__ __forceinline__ void pp_wait_n() {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
@@ -651,13 +693,8 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pp_kernel(AttnKParams p) {
     float m_run = 0.f;   // online: placeholder until the first tile sets it
     bool online = true;
     if (p.kmax2 != nullptr) {
-        // max |k|^2 over this batch's key rows (partials cover kmax_rows rows each)
-        const int64_t r0 = (int64_t)b * p.Nk;
-        const int e0 = (int)(r0 / p.kmax_rows), e1 = (int)((r0 + p.Nk - 1) / p.kmax_rows);
-        float km = 0.f;
-        for (int e = e0 + lane; e <= e1; e += 64) km = fmaxf(km, p.kmax2[(int64_t)e * p.kmax_ld + p.kmax_plane0 + h]);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
+        // max |k|^2 over this split's key rows
+        const float km = kmax_reduce(p, b, h, split, lane);
         float qq = 0.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -911,10 +948,14 @@ __device__ __forceinline__ void pb_vseg(f32x16 (&s)[2], typename mfma_traits<T>:
     }
 }
 
-template <typename T, int RSUM, int OCC>
+template <typename T, int RSUM, int OCC, int STAMP = 0>
 __global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
     typedef typename pb_lsum<RSUM>::type LT;
+    unsigned long long t_entry = 0;
+    if constexpr (STAMP != 0) t_entry = stamp_now();
+    unsigned long long r_entry = 0;
+    if constexpr (STAMP == 2) r_entry = __builtin_amdgcn_s_memrealtime();
     constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
     __shared__ __attribute__((aligned(16))) T ring[PPR * STAGE];
 
@@ -943,44 +984,6 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
     const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
     const float c = p.c;
 
-    // ---- Q^T fragments with the folded scale (s is in exp2 units)
-    const int q = qb * (8 * QW) + wave * QW + lr;
-    const int qc = q < p.Nq ? q : p.Nq - 1;
-    frag qf[2];
-    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
-
-    // ---- fast path iff |q| max|k| <= kBoundMax for every query of the wave
-    bool fast;
-    {
-        const int64_t r0 = (int64_t)b * p.Nk;
-        const int e0 = (int)(r0 / p.kmax_rows), e1 = (int)((r0 + p.Nk - 1) / p.kmax_rows);
-        float km = 0.f;
-        for (int e = e0 + lane; e <= e1; e += 64) km = fmaxf(km, p.kmax2[(int64_t)e * p.kmax_ld + p.kmax_plane0 + h]);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
-        float qq = 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
-        qq = pair_sum(qq);
-        // km is the max squared norm of the UNSCALED keys; q already carries c
-        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
-        fast = __all(bound <= kBoundMax);
-    }
-
-    f32x16 o;
-    LT lsum;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    lsum = LT{};
-    float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tile
-
     const int ntiles = (p.Nk + KT - 1) / KT;
     const int t_begin = split * p.tiles_per_split;
     const int t_end = min(ntiles, t_begin + p.tiles_per_split);
@@ -1005,21 +1008,63 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
     const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
     f32x16 s[2];
     frag pf[2][2], kf[2][2], vf[2][2];
+    // the first tiles' LDS-DMA goes out before the Q / max-|k| loads: their
+    // latencies overlap (the compiler's waits for Q also cover these earlier
+    // pieces; pp_wait below then sees only LDS-DMA in flight)
     if (!hb) {
 #pragma unroll
         for (int i = 0; i < PPR - 2; ++i)
             if (i < nt) issue_next(i);
-    } else {
-        pp_barrier();   // half B: one segment behind
     }
+
+    // ---- Q^T fragments with the folded scale (s is in exp2 units)
+    const int q = qb * (8 * QW) + wave * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    frag qf[2];
+    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
+
+    // ---- fast path iff |q| max|k| <= kBoundMax for every query of the wave
+    bool fast;
+    {
+        const float km = kmax_reduce(p, b, h, split, lane);
+        float qq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
+        qq = pair_sum(qq);
+        // km is the max squared norm of the UNSCALED keys; q already carries c
+        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
+        fast = __all(bound <= kBoundMax);
+    }
+
+    f32x16 o;
+    LT lsum;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    lsum = LT{};
+    float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tile
+
+    unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};   // STAMP 1: prologue points
+    if constexpr (STAMP == 1) tp[0] = stamp_now();
+    if (hb) pp_barrier();   // half B: one segment behind
     if (nt > 0) {
         if (!hb) pp_wait(min(nt - 1, PPR - 3));
+        if constexpr (STAMP == 1) tp[1] = stamp_now();
         pp_barrier();
+        if constexpr (STAMP == 1) tp[2] = stamp_now();
         if (!hb && PPR - 2 < nt) issue_next(PPR - 2);
         pp_load_k<T>(rb, lane_ofs, kf);
         pb_mseg<T, true, false, RSUM>(kf, vf, qf, pf, s, o, lsum);
         if (!hb && nt > 1) pp_wait(min(nt - 1, PPR - 2) - 1);
+        if constexpr (STAMP == 1) tp[3] = stamp_now();
         pp_barrier();
+        if constexpr (STAMP == 1) tp[4] = stamp_now();
         pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, true);
         {
             const PpLane l = lane_ofs;
@@ -1027,19 +1072,46 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
             pp_load_v<T>(rb + KV_B, l, vf);
         }
         int kslot = 1, vslot = 0, islot = PPR - 1;
+        // STAMP: [0] barrier 1 + DMA issue, [1] M segment issue, [2] DMA wait + barrier 2,
+        // [3] V segment, [4] fragment loads, [5] iterations, [6] whole loop
+        unsigned long long st[7] = {0, 0, 0, 0, 0, 0, 0};
+        unsigned long long tl0 = 0;
+        if constexpr (STAMP == 1) tl0 = stamp_now();
         for (int i = 1; i < nt; ++i) {
+            unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+            if constexpr (STAMP == 1) t0 = stamp_now();
             pp_barrier();
             if (!hb && i + PPR - 2 < nt) issue_next(islot);
+            if constexpr (STAMP == 1) t1 = stamp_now();
             pb_mseg<T, true, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
+            if constexpr (STAMP == 1) t2 = stamp_now();
             if (!hb && i + 1 < nt) pp_wait(min(nt - 1, i + PPR - 2) - (i + 1));
             pp_barrier();
-            pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, false);
+            if constexpr (STAMP == 1) t3 = stamp_now();
             kslot = kslot == PPR - 1 ? 0 : kslot + 1;
             vslot = vslot == PPR - 1 ? 0 : vslot + 1;
             islot = islot == PPR - 1 ? 0 : islot + 1;
             const PpLane l = lane_ofs;
+            pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, false);
+            if constexpr (STAMP == 1) t4 = stamp_now();
             pp_load_k<T>(rb + kslot * STAGE_B, l, kf);
             pp_load_v<T>(rb + vslot * STAGE_B + KV_B, l, vf);
+            if constexpr (STAMP == 1) {
+                const unsigned long long t5 = stamp_now();
+                st[0] += t1 - t0; st[1] += t2 - t1; st[2] += t3 - t2; st[3] += t4 - t3; st[4] += t5 - t4;
+                st[5] += 1;
+            }
+        }
+        if constexpr (STAMP == 1) {
+            st[6] = stamp_now() - tl0;
+            if (lane == 0) {
+                unsigned long long* dst = p.stamp + ((int64_t)orig * 8 + wave) * kStampSlots;
+#pragma unroll
+                for (int j = 0; j < 7; ++j) dst[j] = st[j];
+                dst[7] = tl0 - t_entry;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) dst[10 + j] = tp[j] - t_entry;
+            }
         }
         pp_barrier();
         pb_mseg<T, false, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
@@ -1076,6 +1148,16 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
     float l_tot;
     if constexpr (RSUM == 0) l_tot = lsum[0];
     else l_tot = pair_sum(lsum);
+    if constexpr (STAMP != 0) {
+        const unsigned long long t_end = stamp_now();
+        unsigned long long r_end = 0;
+        if constexpr (STAMP == 2) r_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            unsigned long long* dst = p.stamp + ((int64_t)orig * 8 + wave) * kStampSlots;
+            dst[8] = t_end - t_entry;
+            dst[9] = STAMP == 2 ? r_end - r_entry : t_entry;
+        }
+    }
     if (q >= p.Nq) return;
     if (p.splits == 1) {
         const float inv = 1.f / l_tot;
@@ -1354,6 +1436,89 @@ bool use_pb(const cmt_attn_args& a) {
     return use_pp(a) && a.dtype == CMT_BF16 && a.kmax2 != nullptr && (a.flags & CMT_ATTN_FOLD_SCALE);
 }
 
+// diagnostics: CMT_ATTN_STAMP=1 runs the stamped build of attn_pb_kernel and
+// prints its per-segment cycle shares (per wave and tile iteration) to stderr;
+// its run time is not the real kernel's (every stamp drains lgkmcnt)
+// CMT_ATTN_STAMP=2: entry / exit stamps only (shader clock and the 100 MHz
+// real-time counter: the effective clock of the real loop)
+int stamp_mode() {
+    static const char* ov = getenv("CMT_ATTN_STAMP");
+    return (ov && (ov[0] == '1' || ov[0] == '2')) ? ov[0] - '0' : 0;
+}
+
+unsigned long long* stamp_buffer(unsigned nwg) {
+    if (stamp_mode() == 0) return nullptr;
+    static unsigned long long* buf = nullptr;
+    static size_t cap = 0;
+    const size_t need = (size_t)nwg * 8 * kStampSlots * sizeof(unsigned long long);
+    if (need > cap) {
+        if (buf) (void)hipFree(buf);
+        if (hipMalloc(&buf, need) != hipSuccess) return nullptr;
+        cap = need;
+    }
+    (void)hipMemset(buf, 0, need);
+    return buf;
+}
+
+void stamp_report(const AttnKParams& p, unsigned nwg, hipStream_t s) {
+    const size_t n = (size_t)nwg * 8 * kStampSlots;
+    std::vector<unsigned long long> h(n);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), p.stamp, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    if (stamp_mode() == 2) {
+        double tk = 0, rt = 0, nw = 0;
+        for (unsigned w = 0; w < nwg; ++w)
+            for (int v = 0; v < 8; ++v) {
+                const unsigned long long* x = &h[((size_t)w * 8 + v) * kStampSlots];
+                if (x[8] == 0) continue;   // waves the kernel does not have (4-wave workgroups)
+                tk += (double)x[8];
+                rt += (double)x[9];
+                nw += 1;
+            }
+        nw = nw > 0 ? nw : 1;
+        fprintf(stderr, "stamp light: wave entry->stores %.0f ticks, %.2f us real time, %.0f MHz\n", tk / nw,
+                rt / nw / 100.0, tk / (rt / 100.0));
+        return;
+    }
+    static const char* names[5] = {"bar1+dma", "mseg", "wait+bar2", "vseg", "loads"};
+    for (int half = 0; half < 2; ++half) {
+        double sum[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (unsigned w = 0; w < nwg; ++w)
+            for (int v = 4 * half; v < 4 * half + 4; ++v)
+                for (int j = 0; j < 7; ++j) sum[j] += (double)h[((size_t)w * 8 + v) * kStampSlots + j];
+        const double it = sum[5] > 0 ? sum[5] : 1.0;
+        fprintf(stderr, "stamp half %c:", half ? 'B' : 'A');
+        for (int j = 0; j < 5; ++j) fprintf(stderr, " %s %.0f", names[j], sum[j] / it);
+        fprintf(stderr, " | loop/iter %.0f (iters/wave %.1f)\n", sum[6] / it, it / (4.0 * nwg));
+    }
+    // whole-wave spans: prologue (entry -> loop), loop, entry -> before the stores; start skew
+    double pro = 0, loop = 0, tot = 0;
+    unsigned long long t0 = ~0ull, t1 = 0, e_max = 0;
+    for (unsigned w = 0; w < nwg; ++w)
+        for (int v = 0; v < 8; ++v) {
+            const unsigned long long* x = &h[((size_t)w * 8 + v) * kStampSlots];
+            pro += (double)x[7];
+            loop += (double)x[6];
+            tot += (double)x[8];
+            t0 = x[9] < t0 ? x[9] : t0;
+            t1 = x[9] > t1 ? x[9] : t1;
+            e_max = x[9] + x[8] > e_max ? x[9] + x[8] : e_max;
+        }
+    const double nw = 8.0 * nwg;
+    for (int half = 0; half < 2; ++half) {
+        double tps[5] = {0, 0, 0, 0, 0};
+        for (unsigned w = 0; w < nwg; ++w)
+            for (int v = 4 * half; v < 4 * half + 4; ++v)
+                for (int j = 0; j < 5; ++j) tps[j] += (double)h[((size_t)w * 8 + v) * kStampSlots + 10 + j];
+        fprintf(stderr, "stamp prologue half %c (since entry): Q+bound %.0f | wait %.0f | bar %.0f | M0+wait %.0f | bar %.0f\n",
+                half ? 'B' : 'A', tps[0] / (nw / 2), tps[1] / (nw / 2), tps[2] / (nw / 2), tps[3] / (nw / 2),
+                tps[4] / (nw / 2));
+    }
+    fprintf(stderr, "stamp waves: prologue %.0f loop %.0f to-store %.0f | start skew %llu span %llu ticks\n", pro / nw,
+            loop / nw, tot / nw, t1 - t0, e_max - t0);
+}
+
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
     const int ntiles = (a.Nk + KT - 1) / KT;
@@ -1416,6 +1581,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     p.tiles_per_split = cdiv(ntiles, splits);
     p.round_out = (a.flags & CMT_ATTN_ROUND_OUTPUT) && a.dtype != CMT_F32 ? a.dtype : 0;
     p.sync_all = (a.flags >> 8) & 1;
+    p.stamp = nullptr;
     p.Op = p.Mp = p.Lp = nullptr;
     if (splits > 1) {
         const int64_t need = cmt_attn_workspace_bytes(&a);
@@ -1449,13 +1615,17 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
         if (use_pb(a)) {
             const int rs = pb_rsum();
+            p.stamp = stamp_buffer(nwg);
 #define PB_LAUNCH(OCC)                                                                                    \
     do {                                                                                                  \
         if (rs == 1) attn_pb_kernel<bf16_t, 1, OCC><<<nwg, 512, 0, s>>>(p);                                \
         else if (rs == 2) attn_pb_kernel<bf16_t, 2, OCC><<<nwg, 512, 0, s>>>(p);                           \
         else attn_pb_kernel<bf16_t, 0, OCC><<<nwg, 512, 0, s>>>(p);                                        \
     } while (0)
-            if (pp_occ() == 2) PB_LAUNCH(2); else PB_LAUNCH(1);
+            if (p.stamp && stamp_mode() == 2) attn_pb_kernel<bf16_t, 0, 1, 2><<<nwg, 512, 0, s>>>(p);
+            else if (p.stamp) attn_pb_kernel<bf16_t, 0, 1, 1><<<nwg, 512, 0, s>>>(p);
+            else if (pp_occ() == 2) PB_LAUNCH(2);
+            else PB_LAUNCH(1);
 #undef PB_LAUNCH
         } else if (a.dtype == CMT_F16) {
             if (fold) attn_pp_kernel<f16_t, true, 1><<<nwg, 512, 0, s>>>(p);
@@ -1471,6 +1641,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     }
 #undef ATTN_LAUNCH
     int rc = cmt_check_launch("cmt_attn_fwd");
+    if (rc == 0 && p.stamp) stamp_report(p, (unsigned)p.nqb * a.B * a.H * splits, s);
     if (rc || splits == 1) return rc;
     const int64_t total = (int64_t)a.B * a.H * a.Nq * 8;
     const unsigned nb = (unsigned)cdiv64(total, 256);
