@@ -29,6 +29,10 @@
 // first, so no counted LDS-DMA wait is ever drained early.
 #include "cmt_common.h"
 
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 namespace {
 
 constexpr int RB = 32;                         // query rows per workgroup
@@ -269,8 +273,34 @@ __device__ __forceinline__ void store_tile32(float* M, int rb, int wave, int lan
     for (int j = 0; j < 8; ++j) *(f32x4*)(p + j * 256) = f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
 }
 
-template <typename T>
-__global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
+// diagnostics build (CMT_CHAIN_STAMP=1): shader-clock stamps of wave 0 at the
+// phase boundaries, written to a buffer no other code reads
+__device__ __forceinline__ unsigned long long rc_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+constexpr int kChainStamps = 8;
+
+template <typename T, bool STAMP = false>
+__global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigned long long* stamps) {
+    unsigned long long t0 = 0, ts[kChainStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int ns = 0;
+    if constexpr (STAMP) t0 = rc_stamp();
+    auto mark = [&]() {
+        if constexpr (STAMP) {
+            if (ns < kChainStamps) ts[ns] = rc_stamp() - t0;
+            ++ns;
+        }
+    };
+    auto flush = [&]() {
+        if constexpr (STAMP) {
+            if (threadIdx.x == 0)
+                for (int j = 0; j < kChainStamps; ++j) stamps[(int64_t)blockIdx.x * kChainStamps + j] = ts[j];
+        }
+    };
     typedef T t4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) char lds[LDS_TOTAL];
     Eng<T> e;
@@ -366,6 +396,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     asm volatile("" ::"v"(res[0]), "v"(res[31]), "v"(qp[0]), "v"(qp[31]), "v"(oold[0]), "v"(oold[31]));
     rc_wait<0>();
     barrier_mem();
+    mark();   // 0: prologue landed
 
     f32x16 acc[2];
     float v[32];
@@ -373,6 +404,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     if (kind == 0) {
         // ---------------- chain A
         e.sub_gemm(actA, acc, true);                                   // out_proj
+        mark();   // 1
         {
             const float* bo = e.prm();
 #pragma unroll
@@ -381,6 +413,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                 for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
         }
         e.layernorm(v, 256, 512, eps);                                 // norms[0]
+        mark();   // 2
         float y[32];
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
@@ -389,6 +422,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
         }
         e.put_act(actB, v);                                            // lowp(y + query_pos)
         e.sub_gemm_regs(actB, wr, acc);                                // cross-attn Q projection
+        mark();   // 3
         const float* bq = e.prm() + 768;
         t4 qo[8];
 #pragma unroll
@@ -411,12 +445,15 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                         qo[nt * 4 + gg];
                 }
         }
+        mark();   // 4: stores issued
+        flush();
         return;
     }
 
     if (kind == 1) {
         // ---------------- chain B1: out_proj + norms[1], then FFN quarter g
         e.sub_gemm(actA, acc, true);                                   // out_proj
+        mark();   // 1
         {
             const float* bo = e.prm();
 #pragma unroll
@@ -426,7 +463,9 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
         }
         e.layernorm(v, 256, 512, eps);                                 // norms[1] -> o (FFN residual)
         e.put_act(actB, v);                                            // lowp(o): fc1 operand
+        mark();   // 2
         e.sub_gemm(actB, acc, true);                                   // fc1 rows [256g, 256g + 256)
+        mark();   // 3
         {
             const float* b1 = e.prm() + 768 + 256 * g;
             float h[32];
@@ -437,6 +476,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
             e.put_act(actA, h);                                        // hidden quarter g = fc2 K block g
         }
         e.sub_gemm_regs(actA, wr, acc);                                // fc2 partial over K block g
+        mark();   // 4
         const float* b2 = e.prm() + 1792;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
@@ -447,6 +487,8 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                 v[nt * 16 + r] = x;
             }
         store_tile32(ws + g * plane, rb, e.wave, e.lane, v);     // whole row block (clamped rows too)
+        mark();   // 5
+        flush();
         return;
     }
 
@@ -454,6 +496,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 #pragma unroll
     for (int i = 0; i < 32; ++i) v[i] = res[i];
     e.layernorm(v, 2048, 2304, eps);                                   // norms[2] -> next query
+    mark();   // 1
     float y[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) y[i] = v[i];
@@ -473,7 +516,9 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 #pragma unroll
         for (int i = 0; i < 32; ++i) u[i] = y[i] + qp[i];              // qp = 0 for the V block
         e.put_act(actA, u);                                            // lowp(y + pos) (Q|K) / lowp(y) (V)
+        mark();   // 2
         e.sub_gemm_regs(actA, wr, acc);
+        mark();   // 3
         const float* bqkv = e.prm() + 3072 + g * CE;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
@@ -510,6 +555,38 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
                 }
         }
     }
+    mark();   // 4: stores issued
+    flush();
+}
+
+// CMT_CHAIN_STAMP=1: run the stamped build and print the mean phase times (shader clock,
+// since entry, wave 0) per chain kind to stderr
+unsigned long long* chain_stamp_buffer(unsigned grid) {
+    static const char* ov = getenv("CMT_CHAIN_STAMP");
+    if (!(ov && ov[0] == '1')) return nullptr;
+    static unsigned long long* buf = nullptr;
+    static size_t cap = 0;
+    const size_t need = (size_t)grid * kChainStamps * sizeof(unsigned long long);
+    if (need > cap) {
+        if (buf) (void)hipFree(buf);
+        if (hipMalloc(&buf, need) != hipSuccess) return nullptr;
+        cap = need;
+    }
+    (void)hipMemset(buf, 0, need);
+    return buf;
+}
+
+void chain_stamp_report(int kind, unsigned grid, const unsigned long long* dbuf, hipStream_t s) {
+    std::vector<unsigned long long> h((size_t)grid * kChainStamps);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), dbuf, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    double m[kChainStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (unsigned w = 0; w < grid; ++w)
+        for (int j = 0; j < kChainStamps; ++j) m[j] += (double)h[(size_t)w * kChainStamps + j] / grid;
+    fprintf(stderr, "chain stamp kind %d (%u workgroups):", kind, grid);
+    for (int j = 0; j < kChainStamps && m[j] > 0; ++j) fprintf(stderr, " %.0f", m[j]);
+    fprintf(stderr, "\n");
 }
 
 }  // namespace
@@ -536,7 +613,15 @@ extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
-    if (a.dtype == CMT_BF16) chain_kernel<bf16_t><<<grid, NTC, 0, s>>>(a);
-    else chain_kernel<f16_t><<<grid, NTC, 0, s>>>(a);
+    unsigned long long* st = chain_stamp_buffer(grid);
+    if (st) {
+        if (a.dtype == CMT_BF16) chain_kernel<bf16_t, true><<<grid, NTC, 0, s>>>(a, st);
+        else chain_kernel<f16_t, true><<<grid, NTC, 0, s>>>(a, st);
+        const int rc = cmt_check_launch("cmt_chain");
+        if (rc == 0) chain_stamp_report(a.kind, grid, st, s);
+        return rc;
+    }
+    if (a.dtype == CMT_BF16) chain_kernel<bf16_t><<<grid, NTC, 0, s>>>(a, nullptr);
+    else chain_kernel<f16_t><<<grid, NTC, 0, s>>>(a, nullptr);
     return cmt_check_launch("cmt_chain");
 }
