@@ -8,6 +8,12 @@ the first ``max_num_points`` points of each voxel in input order, at most
 zero-padded point slots -- spconv's CPU point2voxel order (its CUDA hash
 order is nondeterministic).  ``forward_mean`` additionally returns the
 HardSimpleVFE mean computed in the same kernel.
+
+The native voxelizer is three launches with no host synchronisation
+(csrc/voxelize.hip).  ``forward_padded`` keeps the voxel count on the device
+(outputs sized max_voxels + a device count) and is graph-capturable; the
+reference-shaped ``forward`` / ``forward_mean`` trim to the count, which is
+a host read.  The layer owns a reusable workspace (kept clean by the kernels).
 """
 import numpy as np
 import torch
@@ -34,13 +40,29 @@ class SPConvVoxelization(nn.Module):
         self.max_voxels = tuple(max_voxels) if isinstance(max_voxels, (tuple, list)) else (max_voxels, max_voxels)
         grid_size = (self.point_cloud_range[3:6] - self.point_cloud_range[0:3]) / np.array(voxel_size)
         self.grid_size = np.round(grid_size).astype(np.int64)
+        self._ws, self._ws_cap = None, 0
+
+    def _workspace(self, n, device):
+        if self._ws is None or self._ws.device != device or self._ws_cap < n:
+            cap = 1024
+            while cap < n:
+                cap <<= 1
+            self._ws, self._ws_cap = native.voxelize_workspace(cap, device), cap
+        return self._ws
+
+    def forward_padded(self, points, nfeat_mean=5):
+        """points [N, F] -> (voxels [V, max_points, F], coors [V, 3], num_points [V], mean [V, nfeat_mean],
+        num_voxels [1] device int32) with V = the active max_voxels; rows >= num_voxels are unspecified.
+        No host synchronisation: capturable in a HIP graph."""
+        mv = self.max_voxels[0] if self.training else self.max_voxels[1]
+        points = points.float()
+        return native.voxelize(points, voxel_size=self.voxel_size.tolist(), coors_range=self.point_cloud_range.tolist(),
+                               grid=self.grid_size.tolist(), max_points=self.max_num_points, max_voxels=mv,
+                               nfeat_mean=nfeat_mean, workspace=self._workspace(points.shape[0], points.device))
 
     def _run(self, points, nfeat_mean):
-        mv = self.max_voxels[0] if self.training else self.max_voxels[1]
-        vox, coors, num, means, nvox = native.voxelize(
-            points.float(), voxel_size=self.voxel_size.tolist(), coors_range=self.point_cloud_range.tolist(),
-            grid=self.grid_size.tolist(), max_points=self.max_num_points, max_voxels=mv, nfeat_mean=nfeat_mean)
-        m = int(nvox.item())
+        vox, coors, num, means, nvox = self.forward_padded(points, nfeat_mean)
+        m = int(nvox.item())   # the reference's outputs are sized by the voxel count (a host read)
         return vox[:m], coors[:m], num[:m], means[:m]
 
     def forward(self, points):

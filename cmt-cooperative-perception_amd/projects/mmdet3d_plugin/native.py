@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -167,6 +167,7 @@ def _load():
         "cmt_box_decode": ([_vp, _i64, _vp, _i64, _vp, _int, _int, _int, _int, _int, P(_flt), _flt, _int,
                             _vp, _vp, _vp, _vp, _vp], _int),
         "cmt_voxelize_workspace_bytes": ([_int, _int], _i64),
+        "cmt_voxelize_workspace_init": ([_vp, _i64, _vp], _int),
         "cmt_voxelize": ([_vp, _int, _int, P(_flt), P(_flt), P(_int), _int, _int, _int, _vp, _vp, _vp, _vp, _vp,
                           _vp, _i64, _vp], _int),
         "cmt_gemm_args_size": ([], _i64),
@@ -565,8 +566,19 @@ def box_decode(logits, bbox, class_task, *, Nq, ncls, max_num, post_center_range
     return boxes, scores, labels, count
 
 
-def voxelize(points, *, voxel_size, coors_range, grid, max_points, max_voxels, nfeat_mean):
-    """points [N, F] f32 on device -> (voxels, coors, num_points, means, num_voxels_dev) sized max_voxels."""
+def voxelize_workspace(n_points, device, max_voxels=1):
+    """A clean voxelizer workspace for up to ``n_points`` points (cmt_hip.h:
+    cmt_voxelize_workspace_init); calls leave it clean, so it is reused."""
+    wsb = int(lib().cmt_voxelize_workspace_bytes(int(n_points), int(max_voxels)))
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=device)
+    _check(lib().cmt_voxelize_workspace_init(_p(ws), wsb, _stream()), "cmt_voxelize_workspace_init")
+    return ws
+
+
+def voxelize(points, *, voxel_size, coors_range, grid, max_points, max_voxels, nfeat_mean, workspace=None):
+    """points [N, F] f32 on device -> (voxels, coors, num_points, means, num_voxels_dev) sized max_voxels.
+    Three launches, no host sync (graph-capturable).  ``workspace``: from
+    voxelize_workspace (capacity >= N); a fresh one is made when None."""
     _dev(points)
     points = points.contiguous()
     N, F = points.shape
@@ -576,10 +588,10 @@ def voxelize(points, *, voxel_size, coors_range, grid, max_points, max_voxels, n
     num = torch.empty((max_voxels,), dtype=torch.int32, device=dev)
     means = torch.empty((max_voxels, nfeat_mean), dtype=torch.float32, device=dev)
     nvox = torch.empty((1,), dtype=torch.int32, device=dev)
-    wsb = int(lib().cmt_voxelize_workspace_bytes(N, max_voxels))
-    ws = torch.empty((wsb,), dtype=torch.uint8, device=dev)
+    ws = workspace if workspace is not None else voxelize_workspace(N, dev, max_voxels)
+    _dev(ws)
     g = (ctypes.c_int * 3)(*[int(x) for x in grid])
     _check(lib().cmt_voxelize(_p(points), N, F, _farr(voxel_size, 3), _farr(coors_range, 6), g, max_points,
                               max_voxels, nfeat_mean, _p(voxels), _p(coors), _p(num), _p(means), _p(nvox), _p(ws),
-                              wsb, _stream()), "cmt_voxelize")
+                              ws.numel(), _stream()), "cmt_voxelize")
     return voxels, coors, num, means, nvox

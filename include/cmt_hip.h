@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 8
+#define CMT_ABI_VERSION 9
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -337,9 +337,16 @@ int cmt_task_head_tail(const float* H1, int L, int B, int Nq, int nheads, int hc
  * points [N, F] fp32 (F >= nfeat_mean); outputs sized for max_voxels:
  *   voxels [max_voxels, max_points, F] (zero padded), coors [max_voxels, 3],
  *   num_points [max_voxels], means [max_voxels, nfeat_mean],
- *   num_voxels [1] (device int, M).
+ *   num_voxels [1] (device int, M; -1 if the in-kernel scan gave up).
+ * Three launches, no host synchronisation (graph-capturable).
+ * Workspace (ABI 9): cmt_voxelize_workspace_bytes(N, .) bytes, filled once by
+ * cmt_voxelize_workspace_init; every call leaves it clean again, so one
+ * workspace serves any number of calls with N up to its capacity (the
+ * largest power of two >= 1024 whose layout fits workspace_bytes), on one
+ * stream at a time.
  * ------------------------------------------------------------------------ */
 int64_t cmt_voxelize_workspace_bytes(int N, int max_voxels);
+int cmt_voxelize_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
 int cmt_voxelize(const float* points, int N, int F, const float* voxel_size3,
                  const float* coors_range6, const int* grid3, int max_points, int max_voxels,
                  int nfeat_mean, float* voxels, int* coors, int* num_points, float* means,
