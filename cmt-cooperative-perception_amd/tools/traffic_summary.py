@@ -7,7 +7,7 @@ profiles/<tag>_<workload>_attn_pmc_summary.json, which bench.py's
 load_traffic() keys on (workload, nk).
 
     python cmt-cooperative-perception_amd/tools/traffic_summary.py gpurun_out/<tag>/prof \
-        --tag r2a --workload fusion --nk 56400 [--match attn_pp_kernel --match 'attn_combine_kernel<8>']
+        --tag r2a --workload fusion --nk 56400 [--match attn_pb_kernel --match 'attn_combine_kernel<8>']
 """
 import argparse
 import glob
@@ -37,7 +37,7 @@ def main():
                     help="kernel-name substrings whose per-launch medians add up to one cross-attention launch")
     ap.add_argument("--outdir", default="profiles")
     a = ap.parse_args()
-    match = a.match or ["attn_pp_kernel", "attn_combine_kernel<8>"]
+    match = a.match
     fdb = glob.glob(os.path.join(a.dir, "fetch", "**", "*.db"), recursive=True)[0]
     wdb = glob.glob(os.path.join(a.dir, "write", "**", "*.db"), recursive=True)[0]
     fetch = per_kernel(fdb, "FETCH_SIZE")
@@ -49,6 +49,10 @@ def main():
         f = statistics.median(fetch.get(k, [0])) * 1024 * 2
         w = statistics.median(write.get(k, [0])) * 1024
         res["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "launches": len(fetch.get(k, []))}
+    if match is None:
+        # the bounded bf16 core (attn_pb_kernel) or the ping-pong core (attn_pp_kernel), + its split combine
+        core = "attn_pb_kernel" if any("attn_pb_kernel" in k for k in res["kernels"]) else "attn_pp_kernel"
+        match = res["match"] = [core, "attn_combine_kernel<8>"]
     parts = {}
     for m in match:
         hits = [(k, v) for k, v in res["kernels"].items() if m in k]
