@@ -24,9 +24,15 @@
 // Every weight reaches LDS as a stream of 16 KB stages (256 weight rows x 32 k)
 // through a ring of NSTG slots by LDS-DMA; the stream runs across sub-GEMM
 // boundaries.  MFMA 32x32x16 in the swapped form (lane = query row), so a row's
-// LayerNorm reduces over registers, the lane pair and the 4 waves.  All global
+// LayerNorm reduces over registers, the lane pair and the 8 waves.  All global
 // stores happen after the last stage and all ordinary global loads before the
 // first, so no counted LDS-DMA wait is ever drained early.
+//
+// Eight waves per workgroup (two per SIMD), each owning 32 output columns (one
+// 32x32 MFMA tile) of every sub-GEMM: the weight fragments a wave holds in
+// registers halve, and the workgroup keeps twice as many loads in flight --
+// each workgroup is bound by how fast one CU pulls its 128-384 KB of weights
+// and row data from L2, not by its MFMAs.
 #include "cmt_common.h"
 
 #include <cstdio>
@@ -37,7 +43,9 @@ namespace {
 
 constexpr int RB = 32;                         // query rows per workgroup
 constexpr int CE = 256;                        // embed dims
-constexpr int NTC = 256;                       // threads (4 waves)
+constexpr int NWV = 8;                         // waves
+constexpr int NTC = 64 * NWV;                  // threads
+constexpr int VPL = CE / NWV / 2;              // values per lane of a row (its 32-column tile, lane pair)
 constexpr int KSTG = 32;                       // k per weight stage
 constexpr int NSTG = 6;                        // weight ring depth
 constexpr int STG_BYTES = CE * KSTG * 2;       // 16 KB
@@ -48,7 +56,8 @@ constexpr int OFF_ACT_B = OFF_ACT_A + ACT_BYTES;
 constexpr int OFF_PRM = OFF_ACT_B + ACT_BYTES; // fp32 parameter block
 constexpr int PRM_A = 1024, PRM_B = 3840;      // floats (cmt_hip.h cmt_chain_args.prm)
 constexpr int OFF_RED = OFF_PRM + PRM_B * 4;
-constexpr int LDS_TOTAL = OFF_RED + 2 * 4 * RB * 4;
+constexpr int LDS_TOTAL = OFF_RED + 2 * NWV * RB * 4;
+constexpr int DMA_PER_STAGE = STG_BYTES / 16 / NTC;   // 16-byte LDS-DMA pieces per thread per stage
 
 typedef const __attribute__((address_space(1))) void* rc_gaddr_t;
 typedef __attribute__((address_space(3))) void* rc_laddr_t;
@@ -83,7 +92,7 @@ struct Eng {
         const T* W = sub_base(sub, ld);
         char* dst = lds + (issued % NSTG) * STG_BYTES;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < DMA_PER_STAGE; ++i) {
             const int piece = tid + NTC * i;
             const int n = piece >> 2;
             const int lc = (piece & 3) ^ ((n >> 2) & 3);
@@ -97,38 +106,33 @@ struct Eng {
     __device__ __forceinline__ void acquire() {
         const int ahead = issued - consumed - 1;   // stages issued after the one needed now
         static_assert(NSTG - 2 == 4, "wait ladder covers 0..4 stages");
-        if (ahead >= 4) rc_wait<16>();
-        else if (ahead == 3) rc_wait<12>();
-        else if (ahead == 2) rc_wait<8>();
-        else if (ahead == 1) rc_wait<4>();
+        if (ahead >= 4) rc_wait<4 * DMA_PER_STAGE>();
+        else if (ahead == 3) rc_wait<3 * DMA_PER_STAGE>();
+        else if (ahead == 2) rc_wait<2 * DMA_PER_STAGE>();
+        else if (ahead == 1) rc_wait<DMA_PER_STAGE>();
         else rc_wait<0>();
         barrier_mem();
         issue();
     }
 
-    // one stage: acc[nt] += W[wave*64 + nt*32 + i][k] * A[row][k] (swapped: lane = row)
-    __device__ __forceinline__ void mma_stage(const char* A, f32x16 (&acc)[2]) {
+    // one stage: acc += W[wave*32 + i][k] * A[row][k] (swapped: lane = row)
+    __device__ __forceinline__ void mma_stage(const char* A, f32x16& acc) {
         const char* Wt = lds + (consumed % NSTG) * STG_BYTES;
         const int kc = consumed % SUB_STAGES;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const frag af = *(const frag*)(A + lr * (CE * 2) + (((kc * 4 + 2 * ks + lh) ^ (lr & 15)) << 4));
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                const int n = wave * 64 + nt * 32 + lr;
-                const frag wf = *(const frag*)(Wt + n * (KSTG * 2) + (((2 * ks + lh) ^ ((n >> 2) & 3)) << 4));
-                acc[nt] = mfma_traits<T>::mma(wf, af, acc[nt]);
-            }
+            const int n = wave * 32 + lr;
+            const frag wf = *(const frag*)(Wt + n * (KSTG * 2) + (((2 * ks + lh) ^ ((n >> 2) & 3)) << 4));
+            acc = mfma_traits<T>::mma(wf, af, acc);
         }
         ++consumed;
     }
 
-    __device__ __forceinline__ void sub_gemm(const char* A, f32x16 (&acc)[2], bool zero) {
+    __device__ __forceinline__ void sub_gemm(const char* A, f32x16& acc, bool zero) {
         if (zero) {
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         }
         for (int kc = 0; kc < SUB_STAGES; ++kc) {
             acquire();
@@ -141,62 +145,59 @@ struct Eng {
     // issued in the prologue) instead of through the LDS-DMA ring, whose per-CU landing
     // cadence (~0.6 us per 16 KB stage) bounded the kernel.  Wn is fragment-major
     // (cmt_hip.h cmt_chain_args.Wn): every load instruction reads 1 KB contiguous.
-    __device__ __forceinline__ void load_wregs(const T* Wp, int g, frag (&wr)[SUB_STAGES][2][2]) const {
-        const T* base = Wp + (int64_t)((g * 4 + wave) * SUB_STAGES) * 4 * 512 + lane * 8;
+    __device__ __forceinline__ void load_wregs(const T* Wp, int g, frag (&wr)[SUB_STAGES][2]) const {
+        // fragment-major layout (cmt_hip.h): wave w4 of the 4-wave geometry, n-tile nt, i.e. weight rows
+        // 64 w4 + 32 nt -- this wave's 32 rows for wave = 2 w4 + nt
+        const int w4 = wave >> 1, nt = wave & 1;
+        const T* base = Wp + (int64_t)((g * 4 + w4) * SUB_STAGES) * 4 * 512 + lane * 8;
 #pragma unroll
         for (int kc = 0; kc < SUB_STAGES; ++kc)
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt) wr[kc][ks][nt] = *(const frag*)(base + ((kc * 2 + ks) * 2 + nt) * 512);
+            for (int ks = 0; ks < 2; ++ks) wr[kc][ks] = *(const frag*)(base + ((kc * 2 + ks) * 2 + nt) * 512);
     }
 
-    __device__ __forceinline__ void sub_gemm_regs(const char* A, const frag (&wr)[SUB_STAGES][2][2],
-                                                  f32x16 (&acc)[2]) const {
-        // the operand image was written by all four waves (put_act)
+    __device__ __forceinline__ void sub_gemm_regs(const char* A, const frag (&wr)[SUB_STAGES][2], f32x16& acc) const {
+        // the operand image was written by all the waves (put_act)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_mem();
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int kc = 0; kc < SUB_STAGES; ++kc)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const frag af = *(const frag*)(A + lr * (CE * 2) + (((kc * 4 + 2 * ks + lh) ^ (lr & 15)) << 4));
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma_traits<T>::mma(wr[kc][ks][nt], af, acc[nt]);
+                acc = mfma_traits<T>::mma(wr[kc][ks], af, acc);
             }
     }
 
-    // column of value r of n-tile nt for this lane (4 consecutive per group r >> 2)
-    __device__ __forceinline__ int col(int nt, int r) const {
-        return wave * 64 + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-    }
+    // column of this lane's value r (4 consecutive per group r >> 2) in its wave's 32-column tile
+    __device__ __forceinline__ int col(int r) const { return wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh; }
 
     __device__ __forceinline__ const float* prm() const { return (const float*)(lds + OFF_PRM); }
 
-    // sum over the row's 256 columns (this lane's 32, the lane pair, the 4 waves); slots alternate
+    // sum over the row's 256 columns (this lane's 16, the lane pair, the 8 waves); slots alternate
     __device__ __forceinline__ float row_sum(float x, int slot) {
         x = pair_sum(x);
         float* red = (float*)(lds + OFF_RED);
-        if (lh == 0) red[(slot * 4 + wave) * RB + lr] = x;
+        if (lh == 0) red[(slot * NWV + wave) * RB + lr] = x;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_mem();
-        return red[(slot * 4 + 0) * RB + lr] + red[(slot * 4 + 1) * RB + lr] + red[(slot * 4 + 2) * RB + lr] +
-               red[(slot * 4 + 3) * RB + lr];
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) t += red[(slot * NWV + w) * RB + lr];
+        return t;
     }
 
     // in-place LayerNorm (nn.LayerNorm: biased variance) with weight / bias at parameter offsets
-    __device__ __forceinline__ void layernorm(float (&v)[32], int w_off, int b_off, float eps) {
+    __device__ __forceinline__ void layernorm(float (&v)[VPL], int w_off, int b_off, float eps) {
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) s += v[i];
+        for (int i = 0; i < VPL; ++i) s += v[i];
         const float mean = row_sum(s, 0) * (1.f / CE);
         float q = 0.f;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
+        for (int i = 0; i < VPL; ++i) {
             const float d = v[i] - mean;
             q += d * d;
         }
@@ -204,61 +205,52 @@ struct Eng {
         const float* pw = prm() + w_off;
         const float* pb = prm() + b_off;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int c = col(nt, r);
-                v[nt * 16 + r] = (v[nt * 16 + r] - mean) * rstd * pw[c] + pb[c];
-            }
+        for (int r = 0; r < VPL; ++r) {
+            const int c = col(r);
+            v[r] = (v[r] - mean) * rstd * pw[c] + pb[c];
+        }
     }
 
-    // this lane's 32 values of its row into an operand image [32][256] (16-B chunks XOR row & 15)
-    __device__ __forceinline__ void put_act(char* act, const float (&v)[32]) {
+    // this lane's values of its row into an operand image [32][256] (16-B chunks XOR row & 15)
+    __device__ __forceinline__ void put_act(char* act, const float (&v)[VPL]) {
         typedef T t4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int c0 = col(nt, 4 * g);
-                const t4 x = {(T)v[nt * 16 + 4 * g], (T)v[nt * 16 + 4 * g + 1], (T)v[nt * 16 + 4 * g + 2],
-                              (T)v[nt * 16 + 4 * g + 3]};
-                *(t4*)(act + lr * (CE * 2) + (((c0 >> 3) ^ (lr & 15)) << 4) + (c0 & 7) * 2) = x;
-            }
+        for (int g = 0; g < 4; ++g) {
+            const int c0 = col(4 * g);
+            const t4 x = {(T)v[4 * g], (T)v[4 * g + 1], (T)v[4 * g + 2], (T)v[4 * g + 3]};
+            *(t4*)(act + lr * (CE * 2) + (((c0 >> 3) ^ (lr & 15)) << 4) + (c0 & 7) * 2) = x;
+        }
     }
 };
 
-// this lane's 32 fp32 values of `row` (columns of Eng::col) from a [rows][256] fp32 matrix
-__device__ __forceinline__ void load_row32(const float* M, int row, int wave, int lh, float (&v)[32]) {
+// this lane's VPL fp32 values of `row` (columns of Eng::col) from a [rows][256] fp32 matrix
+__device__ __forceinline__ void load_row(const float* M, int row, int wave, int lh, float (&v)[VPL]) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const f32x4 x = *(const f32x4*)(M + (int64_t)row * CE + wave * 64 + nt * 32 + 8 * g + 4 * lh);
-            v[nt * 16 + 4 * g] = x[0];
-            v[nt * 16 + 4 * g + 1] = x[1];
-            v[nt * 16 + 4 * g + 2] = x[2];
-            v[nt * 16 + 4 * g + 3] = x[3];
-        }
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 x = *(const f32x4*)(M + (int64_t)row * CE + wave * 32 + 8 * g + 4 * lh);
+        v[4 * g] = x[0];
+        v[4 * g + 1] = x[1];
+        v[4 * g + 2] = x[2];
+        v[4 * g + 3] = x[3];
+    }
 }
 
-__device__ __forceinline__ void store_row32(float* M, int row, int wave, int lh, const float (&v)[32]) {
+__device__ __forceinline__ void store_row(float* M, int row, int wave, int lh, const float (&v)[VPL]) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            *(f32x4*)(M + (int64_t)row * CE + wave * 64 + nt * 32 + 8 * g + 4 * lh) =
-                f32x4{v[nt * 16 + 4 * g], v[nt * 16 + 4 * g + 1], v[nt * 16 + 4 * g + 2], v[nt * 16 + 4 * g + 3]};
+    for (int g = 0; g < 4; ++g)
+        *(f32x4*)(M + (int64_t)row * CE + wave * 32 + 8 * g + 4 * lh) =
+            f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
 }
 
 // The B1 -> B2 partials workspace is private to the chains, so it is kept in
-// the lanes' own order: per (plane, row block, wave, 16-byte group j = nt*4+g)
-// one contiguous 1 KB slab, lane-major.  Every wave instruction then moves 1 KB
+// the lanes' own order: per (plane, row block, wave, 16-byte group j) one
+// contiguous 1 KB slab, lane-major.  Every wave instruction then moves 1 KB
 // of consecutive bytes (8 cache lines) instead of 32-byte pieces of 32 rows
 // (32 lines), which is what bounded chain B2 (~9 us for one workgroup).
-__device__ __forceinline__ void load_tile32(const float* M, int rb, int wave, int lane, float (&v)[32]) {
-    const float* p = M + (int64_t)rb * RB * CE + wave * 2048 + lane * 4;
+__device__ __forceinline__ void load_tile(const float* M, int rb, int wave, int lane, float (&v)[VPL]) {
+    const float* p = M + (int64_t)rb * RB * CE + wave * (VPL * 64) + lane * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < VPL / 4; ++j) {
         const f32x4 x = *(const f32x4*)(p + j * 256);
         v[4 * j] = x[0];
         v[4 * j + 1] = x[1];
@@ -267,10 +259,11 @@ __device__ __forceinline__ void load_tile32(const float* M, int rb, int wave, in
     }
 }
 
-__device__ __forceinline__ void store_tile32(float* M, int rb, int wave, int lane, const float (&v)[32]) {
-    float* p = M + (int64_t)rb * RB * CE + wave * 2048 + lane * 4;
+__device__ __forceinline__ void store_tile(float* M, int rb, int wave, int lane, const float (&v)[VPL]) {
+    float* p = M + (int64_t)rb * RB * CE + wave * (VPL * 64) + lane * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) *(f32x4*)(p + j * 256) = f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+    for (int j = 0; j < VPL / 4; ++j)
+        *(f32x4*)(p + j * 256) = f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
 }
 
 // diagnostics build (CMT_CHAIN_STAMP=1): shader-clock stamps of wave 0 at the
@@ -339,41 +332,41 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
     const int64_t plane = (int64_t)((a.rows + RB - 1) / RB) * RB * CE;   // one partial in tile order
 
     // ---- prologue: every ordinary load and the first LDS-DMAs, then one full wait
-    float res[32], qp[32], oold[32];
+    float res[VPL], qp[VPL], oold[VPL];
     if (kind == 2) {
         // the FFN output + residual: sum of the four B1 partials
-        float t[32];
-        load_tile32(ws, rb, e.wave, e.lane, res);
+        float t[VPL];
+        load_tile(ws, rb, e.wave, e.lane, res);
 #pragma unroll
         for (int p = 1; p < 4; ++p) {
-            load_tile32(ws + p * plane, rb, e.wave, e.lane, t);
+            load_tile(ws + p * plane, rb, e.wave, e.lane, t);
 #pragma unroll
-            for (int i = 0; i < 32; ++i) res[i] += t[i];
+            for (int i = 0; i < VPL; ++i) res[i] += t[i];
         }
     } else if (a.R) {
-        load_row32(a.R, row, e.wave, e.lh, res);
+        load_row(a.R, row, e.wave, e.lh, res);
     } else {
 #pragma unroll
-        for (int i = 0; i < 32; ++i) res[i] = 0.f;
+        for (int i = 0; i < VPL; ++i) res[i] = 0.f;
     }
     const bool need_p = kind == 0 || (kind == 2 && has_next && g < 2);
     if (need_p) {
-        load_row32(a.P, row, e.wave, e.lh, qp);
+        load_row(a.P, row, e.wave, e.lh, qp);
     } else {
 #pragma unroll
-        for (int i = 0; i < 32; ++i) qp[i] = 0.f;
+        for (int i = 0; i < VPL; ++i) qp[i] = 0.f;
     }
     const bool max_into = kind == 2 && g == 0 && (a.out_flags & CMT_LN_MAX_INTO);
     if (max_into) {
-        load_row32(a.OUT, row, e.wave, e.lh, oold);
+        load_row(a.OUT, row, e.wave, e.lh, oold);
     } else {
 #pragma unroll
-        for (int i = 0; i < 32; ++i) oold[i] = 0.f;
+        for (int i = 0; i < VPL; ++i) oold[i] = 0.f;
     }
     if (kind != 2) {
         // attention output rows -> actA (32 rows x 32 chunks, swizzled)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < ACT_BYTES / 16 / NTC; ++i) {
             const int piece = e.tid + NTC * i;
             const int r = piece >> 5;
             const int lc = (piece & 31) ^ (r & 15);
@@ -388,18 +381,19 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
                                          16, 0, 0);
 #pragma unroll
     for (int s = 0; s < NSTG - 1; ++s) e.issue();
-    typename Eng<T>::frag wr[SUB_STAGES][2][2];
+    typename Eng<T>::frag wr[SUB_STAGES][2];
     if (kind == 2 && has_next) e.load_wregs((const T*)a.Wn, g, wr);
     if (kind == 0) e.load_wregs((const T*)a.W1, 0, wr);
     if (kind == 1) e.load_wregs((const T*)a.W2, g, wr);
     // first use of the ordinary loads: everything issued so far has landed after this
-    asm volatile("" ::"v"(res[0]), "v"(res[31]), "v"(qp[0]), "v"(qp[31]), "v"(oold[0]), "v"(oold[31]));
+    asm volatile("" ::"v"(res[0]), "v"(res[VPL - 1]), "v"(qp[0]), "v"(qp[VPL - 1]), "v"(oold[0]),
+                 "v"(oold[VPL - 1]));
     rc_wait<0>();
     barrier_mem();
     mark();   // 0: prologue landed
 
-    f32x16 acc[2];
-    float v[32];
+    f32x16 acc;
+    float v[VPL];
     const float eps = a.eps;
     if (kind == 0) {
         // ---------------- chain A
@@ -408,15 +402,13 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
         {
             const float* bo = e.prm();
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
+            for (int r = 0; r < VPL; ++r) v[r] = acc[r] + bo[e.col(r)] + res[r];
         }
         e.layernorm(v, 256, 512, eps);                                 // norms[0]
         mark();   // 2
-        float y[32];
+        float y[VPL];
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
+        for (int i = 0; i < VPL; ++i) {
             y[i] = v[i];
             v[i] += qp[i];
         }
@@ -424,26 +416,21 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
         e.sub_gemm_regs(actB, wr, acc);                                // cross-attn Q projection
         mark();   // 3
         const float* bq = e.prm() + 768;
-        t4 qo[8];
+        t4 qo[4];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const int c0 = e.col(nt, 4 * gg);
-                qo[nt * 4 + gg] = t4{(T)(acc[nt][4 * gg] + bq[c0]), (T)(acc[nt][4 * gg + 1] + bq[c0 + 1]),
-                                     (T)(acc[nt][4 * gg + 2] + bq[c0 + 2]), (T)(acc[nt][4 * gg + 3] + bq[c0 + 3])};
-            }
+        for (int gg = 0; gg < 4; ++gg) {
+            const int c0 = e.col(4 * gg);
+            qo[gg] = t4{(T)(acc[4 * gg] + bq[c0]), (T)(acc[4 * gg + 1] + bq[c0 + 1]), (T)(acc[4 * gg + 2] + bq[c0 + 2]),
+                        (T)(acc[4 * gg + 3] + bq[c0 + 3])};
+        }
         if (row_ok) {
-            store_row32(a.Y, row, e.wave, e.lh, y);
+            store_row(a.Y, row, e.wave, e.lh, y);
             const int b = row / a.Nq, rr = row - b * a.Nq;
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int gg = 0; gg < 4; ++gg) {
-                    const int c0 = e.col(nt, 4 * gg);
-                    *(t4*)((T*)a.Q + (((int64_t)b * 8 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
-                        qo[nt * 4 + gg];
-                }
+            for (int gg = 0; gg < 4; ++gg) {
+                const int c0 = e.col(4 * gg);
+                *(t4*)((T*)a.Q + (((int64_t)b * 8 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) = qo[gg];
+            }
         }
         mark();   // 4: stores issued
         flush();
@@ -457,9 +444,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
         {
             const float* bo = e.prm();
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[nt * 16 + r] = acc[nt][r] + bo[e.col(nt, r)] + res[nt * 16 + r];
+            for (int r = 0; r < VPL; ++r) v[r] = acc[r] + bo[e.col(r)] + res[r];
         }
         e.layernorm(v, 256, 512, eps);                                 // norms[1] -> o (FFN residual)
         e.put_act(actB, v);                                            // lowp(o): fc1 operand
@@ -468,25 +453,21 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
         mark();   // 3
         {
             const float* b1 = e.prm() + 768 + 256 * g;
-            float h[32];
+            float h[VPL];
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) h[nt * 16 + r] = fmaxf(acc[nt][r] + b1[e.col(nt, r)], 0.f);
+            for (int r = 0; r < VPL; ++r) h[r] = fmaxf(acc[r] + b1[e.col(r)], 0.f);
             e.put_act(actA, h);                                        // hidden quarter g = fc2 K block g
         }
         e.sub_gemm_regs(actA, wr, acc);                                // fc2 partial over K block g
         mark();   // 4
         const float* b2 = e.prm() + 1792;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float x = acc[nt][r];
-                if (g == 0) x += b2[e.col(nt, r)] + v[nt * 16 + r];
-                v[nt * 16 + r] = x;
-            }
-        store_tile32(ws + g * plane, rb, e.wave, e.lane, v);     // whole row block (clamped rows too)
+        for (int r = 0; r < VPL; ++r) {
+            float x = acc[r];
+            if (g == 0) x += b2[e.col(r)] + v[r];
+            v[r] = x;
+        }
+        store_tile(ws + g * plane, rb, e.wave, e.lane, v);             // whole row block (clamped rows too)
         mark();   // 5
         flush();
         return;
@@ -494,65 +475,57 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
 
     // ---------------- chain B2: norms[2] (+ post_norm), next layer's in_proj block g
 #pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = res[i];
+    for (int i = 0; i < VPL; ++i) v[i] = res[i];
     e.layernorm(v, 2048, 2304, eps);                                   // norms[2] -> next query
     mark();   // 1
-    float y[32];
+    float y[VPL];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) y[i] = v[i];
+    for (int i = 0; i < VPL; ++i) y[i] = v[i];
     if (g == 0) {
         e.layernorm(v, 2560, 2816, eps);                               // post_norm -> layer output
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
+        for (int i = 0; i < VPL; ++i) {
             float x = v[i];
             if (a.out_flags & CMT_LN_NAN_TO_NUM) x = nan_to_num(x);
             if (max_into) x = fmaxf(x, oold[i]);
             v[i] = x;
         }
     }
-    t4 qo[8];
+    t4 qo[4];
     if (has_next) {
-        float u[32];
+        float u[VPL];
 #pragma unroll
-        for (int i = 0; i < 32; ++i) u[i] = y[i] + qp[i];              // qp = 0 for the V block
+        for (int i = 0; i < VPL; ++i) u[i] = y[i] + qp[i];             // qp = 0 for the V block
         e.put_act(actA, u);                                            // lowp(y + pos) (Q|K) / lowp(y) (V)
         mark();   // 2
         e.sub_gemm_regs(actA, wr, acc);
         mark();   // 3
         const float* bqkv = e.prm() + 3072 + g * CE;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const int c0 = e.col(nt, 4 * gg);
-                qo[nt * 4 + gg] = t4{(T)(acc[nt][4 * gg] + bqkv[c0]), (T)(acc[nt][4 * gg + 1] + bqkv[c0 + 1]),
-                                     (T)(acc[nt][4 * gg + 2] + bqkv[c0 + 2]), (T)(acc[nt][4 * gg + 3] + bqkv[c0 + 3])};
-            }
+        for (int gg = 0; gg < 4; ++gg) {
+            const int c0 = e.col(4 * gg);
+            qo[gg] = t4{(T)(acc[4 * gg] + bqkv[c0]), (T)(acc[4 * gg + 1] + bqkv[c0 + 1]),
+                        (T)(acc[4 * gg + 2] + bqkv[c0 + 2]), (T)(acc[4 * gg + 3] + bqkv[c0 + 3])};
+        }
     }
     if (row_ok) {
         if (g == 0) {
-            store_row32(a.Y, row, e.wave, e.lh, y);
-            store_row32(a.OUT, row, e.wave, e.lh, v);
+            store_row(a.Y, row, e.wave, e.lh, y);
+            store_row(a.OUT, row, e.wave, e.lh, v);
             if (a.OUT16) {
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                    for (int gg = 0; gg < 4; ++gg)
-                        *(t4*)((T*)a.OUT16 + (int64_t)row * CE + e.col(nt, 4 * gg)) =
-                            t4{(T)v[nt * 16 + 4 * gg], (T)v[nt * 16 + 4 * gg + 1], (T)v[nt * 16 + 4 * gg + 2],
-                               (T)v[nt * 16 + 4 * gg + 3]};
+                for (int gg = 0; gg < 4; ++gg)
+                    *(t4*)((T*)a.OUT16 + (int64_t)row * CE + e.col(4 * gg)) =
+                        t4{(T)v[4 * gg], (T)v[4 * gg + 1], (T)v[4 * gg + 2], (T)v[4 * gg + 3]};
             }
         }
         if (has_next) {
             const int b = row / a.Nq, rr = row - b * a.Nq;
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int gg = 0; gg < 4; ++gg) {
-                    const int c0 = g * CE + e.col(nt, 4 * gg);
-                    *(t4*)((T*)a.Q + (((int64_t)b * 24 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) =
-                        qo[nt * 4 + gg];
-                }
+            for (int gg = 0; gg < 4; ++gg) {
+                const int c0 = g * CE + e.col(4 * gg);
+                *(t4*)((T*)a.Q + (((int64_t)b * 24 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) = qo[gg];
+            }
         }
     }
     mark();   // 4: stores issued
