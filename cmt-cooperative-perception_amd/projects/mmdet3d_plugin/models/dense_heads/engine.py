@@ -222,6 +222,22 @@ class HeadEngineMixin:
         pos = torch.empty((B * Nk, C), dtype=mdt, device=dev)
         R = mem if lowp else None
         cams = self._cams(metas, dev) if use_img else None
+        dec = self.transformer.decoder
+        Nq = self.num_query
+        state = None
+        side = self._side_stream(dev) if dec.chain_prologue_ok(prec) else None
+        if side is not None:
+            # the query side (query embedding + layer 0 up to the cross-attention core) reads
+            # nothing of the memory side: a second stream runs it beside shared_conv, the
+            # BEV / RV encodings and the K/V projection; run_rows joins it before the first
+            # cross-attention.  Its buffers are allocated here, on the main stream.
+            main = torch.cuda.current_stream()
+            state = dec.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
+                dec.lowp_layer0(state, qpos, B=B, Nq=Nq, prec=prec)
+            qpos.record_stream(main)
         if use_bev:
             self._shared_conv_into(x, mem, Nk, pk, prec)
             self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
@@ -229,12 +245,21 @@ class HeadEngineMixin:
             native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C, rows_per_batch=Nk,
                                 row_offset=HW)
             self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R, cams=cams)
-        qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
-        Nq = self.num_query
-        self.transformer.decoder.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
-                                          prec=prec, kv_operands=(mem, pos) if lowp else None,
-                                          out16=out16 if lowp else None)
+        if side is None:
+            qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
+        dec.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
+                     kv_operands=(mem, pos) if lowp else None, out16=out16 if lowp else None, state=state)
         return out
+
+    def _side_stream(self, dev):
+        """The head's second HIP stream on ``dev`` (CMT_SIDE_STREAM=0: none)."""
+        import os
+        if dev.type != "cuda" or os.environ.get("CMT_SIDE_STREAM", "1") == "0":
+            return None
+        pool = self.__dict__.setdefault("_side_streams", {})
+        if dev not in pool:
+            pool[dev] = torch.cuda.Stream(device=dev)
+        return pool[dev]
 
     # ------------------------------------------------------------------ task heads
     def _task_outputs(self, outs_dec, B, prec, outs16=None):

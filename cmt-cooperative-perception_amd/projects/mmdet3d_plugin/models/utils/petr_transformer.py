@@ -414,7 +414,7 @@ class PETRTransformerDecoder(nn.Module):
         return self._pack.get("decoder", params, prec.name, build)
 
     def run_rows(self, mem, pos, qpos, *, B, Nk, Nq, out=None, post_flags=native.LN_NAN_TO_NUM, prec=None,
-                 tgt0=None, kv_operands=None, out16=None):
+                 tgt0=None, kv_operands=None, out16=None, state=None):
         """Fused decoder.  mem/pos: [B*Nk, C] fp32 batch-major rows, qpos:
         [B*Nq, C] fp32.  Writes the post-normed layer outputs to
         out [L, B*Nq, C] (fp32) with ``post_flags`` (nan_to_num / max-into).
@@ -427,7 +427,7 @@ class PETRTransformerDecoder(nn.Module):
         prec = get_precision(prec)
         if prec.gemm != torch.float32:
             return self._run_rows_lowp(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
-                                       tgt0=tgt0, kv_operands=kv_operands, out16=out16)
+                                       tgt0=tgt0, kv_operands=kv_operands, out16=out16, state=state)
         pk = self.packed(prec)
         L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
         dev = mem.device
@@ -486,13 +486,75 @@ class PETRTransformerDecoder(nn.Module):
                              ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         return out
 
-    def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands, out16=None):
+    def chain_prologue_ok(self, prec):
+        """The lowp chain path, whose layer-0 self-attention block depends only
+        on the query embedding and can run beside the memory-side work."""
+        prec = get_precision(prec)
+        return (prec.gemm != torch.float32 and self.fused_supported() and self._chain_ok()
+                and os.environ.get("CMT_CHAIN", "1") != "0")
+
+    def lowp_state(self, *, B, Nk, Nq, prec, device):
+        """Working buffers of one lowp chain-path decoder run (allocated on the
+        current stream; lowp_layer0 may then run on another one)."""
+        prec = get_precision(prec)
+        pk = self.packed(prec)
+        C, H = self.embed_dims, self.embed_dims // 32
+        lp, f32, rows = prec.gemm, torch.float32, B * Nq
+        FF = pk["layers"][0]["f1_w"].shape[0]
+        ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
+                       native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
+        return dict(
+            tgt=torch.empty((rows, C), dtype=f32, device=device),
+            tl=torch.empty((rows, C), dtype=lp, device=device),          # lowp(tgt)
+            tp=torch.empty((rows, C), dtype=lp, device=device),          # lowp(tgt + qpos)
+            qkv=torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=device),
+            qc=torch.empty((B * C * Nq,), dtype=prec.attn, device=device),
+            ob=torch.empty((rows, C), dtype=lp, device=device),          # attention output (out-proj operand)
+            t1n=torch.empty((rows, C), dtype=f32, device=device),
+            hf=torch.empty((rows, FF), dtype=lp, device=device),
+            ws=torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=device),
+            cws=torch.empty(native.chain_ws_numel(rows), dtype=torch.float32, device=device),
+            layer0_done=False, stream=None)
+
+    def lowp_layer0(self, st, qpos, *, B, Nq, prec):
+        """Layer 0 up to the cross-attention core on the chain path: the zero
+        target's operands (add_cast), the self-attention in_proj, the
+        self-attention core and chain A (out_proj + norms[0] + cross Q
+        projection).  None of it reads the memory side, so the head runs it on
+        a second stream beside shared_conv / the encodings / the K/V projection
+        (the stream it runs on is recorded and joined before the first
+        cross-attention)."""
+        prec = get_precision(prec)
+        pk = self.packed(prec)
+        ch = self._chain_pack(prec)
+        C, H, rows = self.embed_dims, self.embed_dims // 32, B * Nq
+        l0 = pk["layers"][0]
+        native.add_cast(None, rows=rows, C=C, Yl=st["tl"], Yp=st["tp"], P=qpos)
+        native.gemm(st["tl"], l0["sa_w"], st["qkv"], M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
+                    A2=st["tp"], lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
+        self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
+        native.chain(0, st["ob"], qpos, ch["A"][0], l0["sa_ow"], l0["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
+                     eps=self.post_norm.eps, R=None, Q=st["qc"])
+        st["layer0_done"] = True
+        st["stream"] = torch.cuda.current_stream()
+
+    def _self_attn(self, st, *, B, H, Nq, C):
+        qkv = st["qkv"]
+        native.attention(qkv, qkv, qkv, st["ob"], B=B, H=H, Nq=Nq, Nk=Nq,
+                         q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
+                         v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
+                         o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0), workspace=st["ws"], fold_scale=True)
+
+    def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands, out16=None,
+                       state=None):
         """run_rows under an f16/bf16 policy: every GEMM operand is produced in
         the compute dtype by the kernel before it (LayerNorm writes lowp(y) and
         lowp(y + query_pos) beside the fp32 residual stream, attention writes
         its output in the compute dtype, FFN fc1 writes its activation in it),
         so every GEMM stages A and W by LDS-DMA.  The residual stream, the
-        LayerNorm statistics and the decoder outputs stay fp32."""
+        LayerNorm statistics and the decoder outputs stay fp32.  ``state``
+        (chain path, tgt0 None): buffers from lowp_state whose layer 0 up to
+        the cross-attention core may already be queued (lowp_layer0)."""
         pk = self.packed(prec)
         L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
         lp = prec.gemm
@@ -525,6 +587,16 @@ class PETRTransformerDecoder(nn.Module):
         # The chains never read the layer-0 target (chain A's residual is None), so there
         # it is only an output buffer and the first operands come from add_cast's zeros.
         use_chain = self._chain_ok() and os.environ.get("CMT_CHAIN", "1") != "0"
+        if use_chain and tgt0 is None:
+            st = state if state is not None else self.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
+            if not st["layer0_done"]:
+                self.lowp_layer0(st, qpos, B=B, Nq=Nq, prec=prec)
+            elif st["stream"] is not None and st["stream"] != torch.cuda.current_stream():
+                torch.cuda.current_stream().wait_stream(st["stream"])   # join the layer-0 side stream
+            return self._chain_layers(st, qpos, kv, kmax2, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
+                                      prec=prec, out16=out16)
+        if state is not None:
+            raise ValueError("run_rows: a lowp_state applies to the chain path with a zero target only")
         if tgt0 is not None:
             tgt = tgt0.clone()
         elif use_chain:
@@ -629,4 +701,35 @@ class PETRTransformerDecoder(nn.Module):
                                     W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         if out16 is not None:
             native.cast(out, out16)
+        return out
+
+    def _chain_layers(self, st, qpos, kv, kmax2, *, B, Nk, Nq, out, post_flags, prec, out16):
+        """Chain path from layer 0's cross-attention core on (layer 0's self
+        block already queued by lowp_layer0): per layer the cross-attention
+        core, chain B1, chain B2 (which also runs the next layer's in_proj),
+        then the next layer's self-attention core and chain A."""
+        pk = self.packed(prec)
+        ch = self._chain_pack(prec)
+        L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
+        rows = B * Nq
+        eps = self.post_norm.eps
+        tgt, qkv, qc, ob, t1n, ws, cws = (st[k] for k in ("tgt", "qkv", "qc", "ob", "t1n", "ws", "cws"))
+        for l, lw in enumerate(pk["layers"]):
+            if l > 0:
+                self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
+                native.chain(0, ob, qpos, ch["A"][l], lw["sa_ow"], lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
+                             R=tgt, Q=qc)
+            with timed("cross_attn"):
+                native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
+                                 q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
+                                 v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
+                                 v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0),
+                                 workspace=ws, round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2,
+                                 kmax_ld=L * H, kmax_plane0=l * H)
+            nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
+            native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
+                         R=t1n, W2=lw["f2_wp"], WS=cws)
+            native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
+                         Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
+                         Q=qkv if nxt is not None else None, WS=cws, OUT16=out16)
         return out
