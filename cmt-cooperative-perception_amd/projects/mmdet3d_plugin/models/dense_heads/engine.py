@@ -122,20 +122,34 @@ class HeadEngineMixin:
             pool[key] = torch.empty(t.shape, dtype=t.dtype).pin_memory()
         return t.to(dev)
 
-    def _bev_pos_into(self, pos, B, Nk, H, W, pk, R=None):
-        """bev_pos_embed (cmt_head.py:324-337, 489) into the pos rows of every
-        batch element; with R (the memory rows in the compute dtype) the
-        output is lowp(memory + pos) -- the K-projection operand."""
+    def _bev_pos_hidden(self, H, W, pk):
+        """First half of bev_pos_embed (cmt_head.py:324-337, 489): pos2embed of
+        the BEV grid and bev_embedding[0] + ReLU -- input-independent."""
         C = self.hidden_dim
         cfg = self.train_cfg if self.train_cfg else self.test_cfg
         x_size = cfg["grid_size"][1] // self.downsample_scale
         y_size = cfg["grid_size"][0] // self.downsample_scale
         if x_size * y_size != H * W:
             raise ValueError(f"BEV map {H}x{W} does not match grid_size/downsample ({x_size}x{y_size})")
-        pe_dt = pk["bev"][0].dtype
-        pe = torch.empty((H * W, 2 * C), dtype=pe_dt, device=pos.device)
+        w0, b0, _, _ = pk["bev"]
+        pe = torch.empty((H * W, 2 * C), dtype=w0.dtype, device=w0.device)
         native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
-        self._mlp(pe, pk["bev"], pos, batch=B, a_bstride=0, c_bstride=Nk * C, M=H * W, R=R)
+        hdt = pe.dtype if pe.dtype == w0.dtype else torch.float32
+        return native.linear(pe, w0, b0, relu=True, out_dtype=hdt)
+
+    def _bev_pos_out(self, hid, pos, B, Nk, pk, R=None):
+        """Second half: bev_embedding[2] into the pos rows of every batch
+        element; with R (the memory rows in the compute dtype) the output is
+        lowp(memory + pos) -- the K-projection operand."""
+        _, _, w2, b2 = pk["bev"]
+        C, M = self.hidden_dim, hid.shape[0]
+        native.gemm(hid, w2, pos, M=M, N=w2.shape[0], K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
+                    bias=b2, batch=B, a_bstride=0, c_bstride=Nk * C, R=R, ldr=C if R is not None else 0,
+                    r_bstride=Nk * C if R is not None else 0)
+
+    def _bev_pos_into(self, pos, B, Nk, H, W, pk, R=None):
+        """bev_pos_embed (cmt_head.py:324-337, 489) into the pos rows (both halves)."""
+        self._bev_pos_out(self._bev_pos_hidden(H, W, pk), pos, B, Nk, pk, R=R)
 
     def _cams(self, metas, dev):
         """(lidar2img, inv(lidar2img)) of every camera as [B, V, 4, 4] fp32 device
@@ -144,24 +158,35 @@ class HeadEngineMixin:
         both = self._h2d(np.stack([l2i, i2l]), dev, "cams")
         return both[0], both[1]
 
-    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None, cams=None):
-        C = self.hidden_dim
+    def _rv_pe_hidden(self, x_img, metas, B, pk, cams=None):
+        """First half of _rv_pe + rv_embedding (cmt_head.py:417-433, 297-301):
+        the frustum coordinates and rv_embedding[0] + ReLU -- they read only
+        the camera matrices and the feature-map shape."""
         BV, _, h, w = x_img.shape
-        V = BV // B
         pad_h, pad_w, _ = metas[0]["pad_shape"][0]
-        i2l = (cams if cams is not None else self._cams(metas, pos.device))[1]
+        dev = x_img.device
+        i2l = (cams if cams is not None else self._cams(metas, dev))[1]
         D = self.depth_num
-        w0, b0, w2, b2 = pk["rv"]
+        w0, b0, _, _ = pk["rv"]
         cdt = w0.dtype if (3 * D) % 64 == 0 else torch.float32
-        coords = torch.empty((BV * h * w, 3 * D), dtype=cdt, device=pos.device)
+        coords = torch.empty((BV * h * w, 3 * D), dtype=cdt, device=dev)
         native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w, D=D, pad_h=float(pad_h), pad_w=float(pad_w),
                             depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
         hdt = cdt if cdt == w0.dtype else torch.float32
-        hid = native.linear(coords, w0, b0, relu=True, out_dtype=hdt)       # [BV*h*w, 4C]
-        native.gemm(hid, w2, pos, M=V * h * w, N=C, K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
-                    bias=b2, batch=B, a_bstride=V * h * w * hid.shape[1], c_bstride=Nk * C, c_offset=offset * C,
+        return native.linear(coords, w0, b0, relu=True, out_dtype=hdt)       # [BV*h*w, 4C]
+
+    def _rv_pe_out(self, hid, pos, B, Nk, offset, pk, R=None):
+        """Second half: rv_embedding[2] into the camera pos rows (+ R as in _bev_pos_out)."""
+        C = self.hidden_dim
+        _, _, w2, b2 = pk["rv"]
+        M = hid.shape[0] // B   # V * h * w rows per batch element
+        native.gemm(hid, w2, pos, M=M, N=C, K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
+                    bias=b2, batch=B, a_bstride=M * hid.shape[1], c_bstride=Nk * C, c_offset=offset * C,
                     R=R, ldr=C if R is not None else 0, r_bstride=Nk * C if R is not None else 0,
                     r_offset=offset * C)
+
+    def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None, cams=None):
+        self._rv_pe_out(self._rv_pe_hidden(x_img, metas, B, pk, cams=cams), pos, B, Nk, offset, pk, R=R)
 
     def _query_pos(self, B, metas, with_rv, pk, cams=None):
         C = self.hidden_dim
@@ -227,24 +252,46 @@ class HeadEngineMixin:
         state = None
         side = self._side_stream(dev) if dec.chain_prologue_ok(prec) else None
         if side is not None:
-            # the query side (query embedding + layer 0 up to the cross-attention core) reads
-            # nothing of the memory side: a second stream runs it beside shared_conv, the
-            # BEV / RV encodings and the K/V projection; run_rows joins it before the first
-            # cross-attention.  Its buffers are allocated here, on the main stream.
+            # A second stream runs everything that does not read the conv output: the
+            # input-independent first halves of the BEV / RV position MLPs and the camera
+            # memory rows (joined by an event before their second GEMMs, which add the
+            # memory rows), then the query embedding and layer 0 up to the
+            # cross-attention core (joined by run_rows before the first cross-attention).
+            # Buffers that outlive the side stream's work are allocated here, on the main
+            # stream, or recorded on it.
             main = torch.cuda.current_stream()
             state = dec.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
             side.wait_stream(main)
+            ready = torch.cuda.Event()
+            hb = hr = None
             with torch.cuda.stream(side):
+                if use_bev:
+                    hb = self._bev_pos_hidden(H, W, pk)
+                if use_img:
+                    native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C,
+                                        rows_per_batch=Nk, row_offset=HW)
+                    hr = self._rv_pe_hidden(x_img, metas, B, pk, cams=cams)
+                ready.record(side)
                 qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
                 dec.lowp_layer0(state, qpos, B=B, Nq=Nq, prec=prec)
-            qpos.record_stream(main)
-        if use_bev:
-            self._shared_conv_into(x, mem, Nk, pk, prec)
-            self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
-        if use_img:
-            native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C, rows_per_batch=Nk,
-                                row_offset=HW)
-            self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R, cams=cams)
+            for t in (qpos, hb, hr):
+                if t is not None:
+                    t.record_stream(main)
+            if use_bev:
+                self._shared_conv_into(x, mem, Nk, pk, prec)
+            main.wait_event(ready)
+            if use_bev:
+                self._bev_pos_out(hb, pos, B, Nk, pk, R=R)
+            if use_img:
+                self._rv_pe_out(hr, pos, B, Nk, HW, pk, R=R)
+        else:
+            if use_bev:
+                self._shared_conv_into(x, mem, Nk, pk, prec)
+                self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
+            if use_img:
+                native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C,
+                                    rows_per_batch=Nk, row_offset=HW)
+                self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R, cams=cams)
         if side is None:
             qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
         dec.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
