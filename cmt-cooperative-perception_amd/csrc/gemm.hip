@@ -1001,7 +1001,19 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
         CMT_REQUIRE(a.ldc % 4 == 0 && (a.R == nullptr || a.ldr % 4 == 0) && a.bias_bstride % 4 == 0,
                     "cmt_gemm: ldc/ldr/bias_bstride must be multiples of 4");
         const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
-        if (a.N % 128 == 0 && big_tiles >= 480) return launch_dma<128, 128, 2>(a, s);
+        if (a.N % 128 == 0 && big_tiles >= 480) {
+            // diagnostics: CMT_GEMM_S128 = LDS stages of the 128 x 128 tile (2, 3 or 4)
+            const char* ov = getenv("CMT_GEMM_S128");
+            const int st = (ov && ov[0] >= '2' && ov[0] <= '4') ? ov[0] - '0' : 2;
+            if (st == 4) return launch_dma<128, 128, 4>(a, s);
+            if (st == 3) return launch_dma<128, 128, 3>(a, s);
+            return launch_dma<128, 128, 2>(a, s);
+        }
+        // long-K problems one 128x128 grid would not fill (the RV embedding's second GEMM,
+        // M = 24 000, N = 256, K = 1024): 128 x 64 tiles read 3/4 of the 64 x 64 tiles' operand
+        // bytes per output and still give ~3 workgroups per CU
+        const int64_t mid_tiles = (int64_t)(a.N / 64) * cdiv(a.M, 128) * a.batch;
+        if (kdiv >= 512 && a.a_mode == CMT_A_ROWS && mid_tiles >= 480) return launch_dma<128, 64, 3>(a, s);
         return launch_dma<64, 64, 4>(a, s);
     }
     // Tile choice: 128x128 when the grid still fills the chip, else 64x64.

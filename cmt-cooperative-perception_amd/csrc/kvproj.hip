@@ -44,12 +44,12 @@ template <typename T> using frag_of = typename mfma_traits<T>::frag;
 // One head plane of one 64-token half: 32 MFMAs on the fragment set wf (the
 // freed slots refill with plane `nxt`, two planes ahead), then round, stage
 // [token][32] in the wave's LDS slice, key-norm max, and 16-B stores.
-template <typename T, bool MAXQ>
+template <typename T, bool MAXQ, int DIAG, bool AF_LDS>
 __device__ __forceinline__ void kv_plane(const cmt_gemm_args& a, char* stg, const float* bw, const T* Wl,
                                          typename mfma_traits<T>::frag (&wf)[KP_KS],
-                                         const typename mfma_traits<T>::frag (&af)[2][KP_KS], int j, int nxt,
-                                         int plane, int mg, const uint32_t (&soff)[4], __amdgpu_buffer_rsrc_t crsrc,
-                                         __amdgpu_buffer_rsrc_t prsrc, int lane) {
+                                         const typename mfma_traits<T>::frag (&af)[2][KP_KS], const char* atile,
+                                         int j, int nxt, int plane, int mg, const uint32_t (&soff)[4],
+                                         __amdgpu_buffer_rsrc_t crsrc, __amdgpu_buffer_rsrc_t prsrc, int lane) {
     typedef T t4 __attribute__((ext_vector_type(4)));
     const int lr = lane & 31, lh = lane >> 5;
     const T* Wn = Wl + (int64_t)nxt * (KP_KS * 512);
@@ -67,9 +67,20 @@ __device__ __forceinline__ void kv_plane(const cmt_gemm_args& a, char* stg, cons
     }
 #pragma unroll
     for (int ks = 0; ks < KP_KS; ++ks) {
-        acc[0] = mfma_traits<T>::mma(wf[ks], af[0][ks], acc[0]);
-        acc[1] = mfma_traits<T>::mma(wf[ks], af[1][ks], acc[1]);
-        wf[ks] = *(const frag_of<T>*)(Wn + ks * 512);   // plane `nxt` into the freed slot
+        if constexpr (AF_LDS) {
+            // B fragments of the half's two 32-token tiles straight from the LDS A tile
+            // (atile = row lr of the half; rows 32 apart share the XOR pattern lr & 15)
+            const int sw = ((2 * ks + (lane >> 5)) ^ (lane & 15)) << 4;
+            const frag_of<T> a0 = *(const frag_of<T>*)(atile + sw);
+            const frag_of<T> a1 = *(const frag_of<T>*)(atile + 32 * (KP_K * 2) + sw);
+            acc[0] = mfma_traits<T>::mma(wf[ks], a0, acc[0]);
+            acc[1] = mfma_traits<T>::mma(wf[ks], a1, acc[1]);
+        } else {
+            acc[0] = mfma_traits<T>::mma(wf[ks], af[0][ks], acc[0]);
+            acc[1] = mfma_traits<T>::mma(wf[ks], af[1][ks], acc[1]);
+        }
+        if constexpr ((DIAG & 2) == 0)
+            wf[ks] = *(const frag_of<T>*)(Wn + ks * 512);   // plane `nxt` into the freed slot
     }
     float pm = 0.f;
 #pragma unroll
@@ -100,6 +111,16 @@ __device__ __forceinline__ void kv_plane(const cmt_gemm_args& a, char* stg, cons
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pm), prsrc, po, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr ((DIAG & 1) != 0) {   // diagnostics: no output stores (the LDS staging reads stay)
+        f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int tok = 16 * i + (lane >> 2), ch = lane & 3;
+            acc4 += *(const f32x4*)(stg + tok * 64 + (((ch ^ (tok >> 1)) & 3) << 4));
+        }
+        asm volatile("" ::"v"(acc4));
+        return;
+    }
     const uint32_t pl = (uint32_t)((int64_t)plane * a.rows_per_batch * 64);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -118,7 +139,7 @@ __device__ __forceinline__ void kv_plane(const cmt_gemm_args& a, char* stg, cons
 // fetched TWO planes ahead into two alternating sets: a load issued after a
 // plane's stores completes only after those stores do (one counter, in
 // order), so one plane of distance exposed the HBM store latency every plane.
-template <typename T, bool MAXQ>
+template <typename T, bool MAXQ, int DIAG, bool AF_LDS>
 __device__ __forceinline__ void kv_sweep(const cmt_gemm_args& a, const char* lds, char* stg, const float* bw,
                                          const T* Wl, typename mfma_traits<T>::frag (&wa)[KP_KS],
                                          typename mfma_traits<T>::frag (&wb)[KP_KS], int nplanes, int plane0,
@@ -134,12 +155,15 @@ __device__ __forceinline__ void kv_sweep(const cmt_gemm_args& a, const char* lds
     for (int half = 0; half < 2; ++half) {
         // B fragments of this half's 64 tokens: [token tile][k-step]
         frag af[2][KP_KS];
+        const char* atile = lds + (64 * half + lr) * (KP_K * 2);
+        if constexpr (!AF_LDS) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int ks = 0; ks < KP_KS; ++ks)
-                af[t][ks] = *(const frag*)(lds + (64 * half + 32 * t + lr) * (KP_K * 2) +
-                                           (((2 * ks + lh) ^ (lr & 15)) << 4));
+                for (int ks = 0; ks < KP_KS; ++ks)
+                    af[t][ks] = *(const frag*)(lds + (64 * half + 32 * t + lr) * (KP_K * 2) +
+                                               (((2 * ks + lh) ^ (lr & 15)) << 4));
+        }
         // byte offsets of this lane's 4 store rows (tokens 16 i + lane / 4, chunk lane & 3), plane 0
         uint32_t soff[4];
 #pragma unroll
@@ -150,19 +174,141 @@ __device__ __forceinline__ void kv_sweep(const cmt_gemm_args& a, const char* lds
             soff[i] = m < a.M ? (uint32_t)((row * 32 + 8 * (lane & 3)) * 2) : 0xffffffffu;
         }
         const int mg = m0 + 64 * half;                   // this half's 64-row key-norm group
+        if constexpr (AF_LDS) {
+            // two waves per SIMD: one W set, refilled with the next plane (wrapping to the
+            // next half's first) while this one's MFMAs run; the partner wave hides the rest
+            for (int j = 0; j < nplanes; ++j) {
+                const int n1 = j + 1 < nplanes ? j + 1 : 0;
+                kv_plane<T, MAXQ, DIAG, AF_LDS>(a, stg, bw, Wl, wa, af, atile, j, n1, plane0 + j, mg, soff, crsrc,
+                                                prsrc, lane);
+            }
+            continue;
+        }
         for (int j = 0; j < nplanes; j += 2) {
             const int n0 = j + 2 < nplanes ? j + 2 : j + 2 - nplanes;   // wraps to the next half's first two
-            kv_plane<T, MAXQ>(a, stg, bw, Wl, wa, af, j, n0, plane0 + j, mg, soff, crsrc, prsrc, lane);
-            kv_plane<T, MAXQ>(a, stg, bw, Wl, wb, af, j + 1, n0 + 1, plane0 + j + 1, mg, soff, crsrc, prsrc, lane);
+            kv_plane<T, MAXQ, DIAG, AF_LDS>(a, stg, bw, Wl, wa, af, atile, j, n0, plane0 + j, mg, soff, crsrc, prsrc,
+                                            lane);
+            kv_plane<T, MAXQ, DIAG, AF_LDS>(a, stg, bw, Wl, wb, af, atile, j + 1, n0 + 1, plane0 + j + 1, mg, soff,
+                                            crsrc, prsrc, lane);
         }
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(KP_NT, 1) void kvproj_kernel(cmt_gemm_args a, int parts) {
+// Whole 128-token tile per W fetch (8-wave form): the plane's W fragments
+// serve all four 32-token tiles, so each workgroup fetches its columns' W
+// once instead of once per 64-token half (768 KB instead of 1.5 MB per
+// workgroup -- the per-CU L2 stream that bounded the two-half sweep).  A
+// fragments come from the LDS tile per k-step (one ds_read_b128 per MFMA);
+// the plane leaves through an 8 KB per-wave staging slice.
+template <typename T, bool MAXQ>
+__device__ __forceinline__ void kv_plane_full(const cmt_gemm_args& a, char* stg, const float* bw, const T* Wl,
+                                              typename mfma_traits<T>::frag (&wf)[KP_KS], const char* arow, int j,
+                                              int nxt, int plane, int m0, const uint32_t (&soff)[8],
+                                              __amdgpu_buffer_rsrc_t crsrc, __amdgpu_buffer_rsrc_t prsrc, int lane) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    const int lr = lane & 31, lh = lane >> 5;
+    const T* Wn = Wl + (int64_t)nxt * (KP_KS * 512);
+    f32x16 acc[4];
+    {
+        f32x16 b16;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 b4 = *(const f32x4*)(bw + 32 * j + 8 * g + 4 * lh);
+            b16[4 * g] = b4[0]; b16[4 * g + 1] = b4[1]; b16[4 * g + 2] = b4[2]; b16[4 * g + 3] = b4[3];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = b16;
+    }
+#pragma unroll
+    for (int ks = 0; ks < KP_KS; ++ks) {
+        const int sw = ((2 * ks + lh) ^ (lr & 15)) << 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const frag_of<T> at = *(const frag_of<T>*)(arow + t * 32 * (KP_K * 2) + sw);
+            acc[t] = mfma_traits<T>::mma(wf[ks], at, acc[t]);
+        }
+        wf[ks] = *(const frag_of<T>*)(Wn + ks * 512);   // plane `nxt` into the freed slot
+    }
+    float pm[2] = {0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int tok = 32 * t + lr;
+        float ss = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const t4 v = t4{(T)acc[t][4 * g], (T)acc[t][4 * g + 1], (T)acc[t][4 * g + 2], (T)acc[t][4 * g + 3]};
+            const int c0 = 8 * g + 4 * lh;
+            *(t4*)(stg + tok * 64 + ((((c0 >> 3) ^ (tok >> 1)) & 3) << 4) + (c0 & 7) * 2) = v;
+            if (MAXQ) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
+            }
+        }
+        if (MAXQ) {
+            ss = pair_sum(m0 + tok < a.M ? ss : 0.f);
+            pm[t >> 1] = (t & 1) ? fmaxf(pm[t >> 1], ss) : ss;
+        }
+    }
+    if (MAXQ) {
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) {
+            float x = pm[gq];
+#pragma unroll
+            for (int off = 1; off < 32; off <<= 1) x = fmaxf(x, __shfl_xor(x, off));
+            const int pm_planes = a.plane_max_cols >> 5;
+            const int mg = m0 + 64 * gq;
+            const uint32_t po = (lane == 0 && mg < a.M) ? (uint32_t)((((int64_t)(mg >> 6)) * pm_planes + plane) * 4)
+                                                         : 0xffffffffu;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), prsrc, po, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t pl = (uint32_t)((int64_t)plane * a.rows_per_batch * 64);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int tok = 16 * i + (lane >> 2), ch = lane & 3;
+        const f32x4 v = *(const f32x4*)(stg + tok * 64 + (((ch ^ (tok >> 1)) & 3) << 4));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), crsrc,
+                                              soff[i] == 0xffffffffu ? soff[i] : soff[i] + pl, 0, 2);
+    }
+}
+
+template <typename T, bool MAXQ>
+__device__ __forceinline__ void kv_sweep_full(const cmt_gemm_args& a, const char* lds, char* stg, const float* bw,
+                                              const T* Wl, typename mfma_traits<T>::frag (&wa)[KP_KS], int nplanes,
+                                              int plane0, int m0, int lane) {
+    const int lr = lane & 31;
+    const uint32_t cbytes = (uint32_t)((int64_t)a.M * a.N * 2);
+    const auto crsrc = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, cbytes, 0x00020000);
+    const uint32_t pmbytes = MAXQ ? (uint32_t)(((a.M + 63) / 64) * (a.plane_max_cols >> 5) * 4) : 0u;
+    const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(MAXQ ? (void*)a.plane_max2 : a.C, 0, pmbytes, 0x00020000);
+    const int rpb = a.rows_per_batch;
+    uint32_t soff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = m0 + 16 * i + (lane >> 2);
+        const int bb = m / rpb;
+        const int64_t row = (int64_t)bb * (a.N >> 5) * rpb + (m - bb * rpb);
+        soff[i] = m < a.M ? (uint32_t)((row * 32 + 8 * (lane & 3)) * 2) : 0xffffffffu;
+    }
+    const char* arow = lds + lr * (KP_K * 2);
+    for (int j = 0; j < nplanes; ++j) {
+        const int n1 = j + 1 < nplanes ? j + 1 : j;   // the last plane re-fetches itself (cached, unused)
+        kv_plane_full<T, MAXQ>(a, stg, bw, Wl, wa, arow, j, n1, plane0 + j, m0, soff, crsrc, prsrc, lane);
+    }
+}
+
+// NW = 4: one wave per SIMD, each wave holds its half's A fragments in
+// registers.  NW = 8: two waves per SIMD (one's epilogue -- rounding, LDS
+// staging, key-norm max, stores -- runs beside the other's MFMAs), A fragments
+// read from the LDS tile per k-step so a wave fits in 256 registers.
+template <typename T, int DIAG = 0, int NW = 4, bool FULL = false>
+__global__ __launch_bounds__(64 * NW, 1) void kvproj_kernel(cmt_gemm_args a, int parts) {
     typedef typename mfma_traits<T>::frag frag;
-    // 64 KB A tile | 4 x 4 KB per-wave store staging | the part's bias (<= 8 KB)
-    __shared__ __attribute__((aligned(16))) char lds[KP_BM * KP_K * 2 + 4 * 4096 + KP_MAXB * 4];
+    constexpr int NTH = 64 * NW;
+    constexpr int STG = FULL ? 8192 : 4096;   // per-wave store staging bytes
+    // 64 KB A tile | NW x STG per-wave store staging | the part's bias (<= 8 KB)
+    __shared__ __attribute__((aligned(16))) char lds[KP_BM * KP_K * 2 + NW * STG + KP_MAXB * 4];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -179,8 +325,8 @@ __global__ __launch_bounds__(KP_NT, 1) void kvproj_kernel(cmt_gemm_args a, int p
 
     // ---- A tile -> LDS (16-B chunks XOR-swizzled by row & 15)
 #pragma unroll
-    for (int i = 0; i < KP_BM * KP_K * 2 / 16 / KP_NT; ++i) {
-        const int piece = tid + KP_NT * i;
+    for (int i = 0; i < KP_BM * KP_K * 2 / 16 / NTH; ++i) {
+        const int piece = tid + NTH * i;
         const int r = piece >> 5;
         const int lc = (piece & 31) ^ (r & 15);
         const int src = min(m0 + r, a.M - 1);
@@ -190,37 +336,42 @@ __global__ __launch_bounds__(KP_NT, 1) void kvproj_kernel(cmt_gemm_args a, int p
     // the part's bias -> LDS: the epilogue reads it with no vmcnt wait (a global
     // bias load there would drain the W prefetch and the stores before it, which
     // count on the same in-order counter)
-    float* bsm = (float*)(lds + KP_BM * KP_K * 2 + 4 * 4096);
-    for (int piece = tid; piece < (ncols >> 2); piece += KP_NT) {
+    float* bsm = (float*)(lds + KP_BM * KP_K * 2 + NW * STG);
+    for (int piece = tid; piece < (ncols >> 2); piece += NTH) {
         if (a.bias)
             __builtin_amdgcn_global_load_lds((kp_gaddr_t)(a.bias + n_part + 4 * piece), (kp_laddr_t)(bsm + 4 * piece),
                                              16, 0, 0);
         else
             *(f32x4*)(bsm + 4 * piece) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const int planes_w = ncols / 32 / 4;                // head planes per wave
+    const int planes_w = ncols / 32 / NW;               // head planes per wave (even)
     const int plane0 = (n_part >> 5) + wave * planes_w;
     const T* W = (const T*)a.W;
     // W in the fragment-packed layout (cmt_hip.h cmt_kv_proj): plane p, k-step ks
     // is 1 KB contiguous, lane-major -- every W load instruction touches 8 lines
     const T* Wl = W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
-    frag wa[KP_KS], wb[KP_KS];   // planes 0 and 1 (two planes of prefetch distance)
+    frag wa[KP_KS], wb[KP_KS];   // planes 0 and 1 (two planes of prefetch distance; NW = 8: plane 0 only)
 #pragma unroll
     for (int ks = 0; ks < KP_KS; ++ks) {
         wa[ks] = *(const frag*)(Wl + ks * 512);
-        wb[ks] = *(const frag*)(Wl + KP_KS * 512 + ks * 512);
+        if constexpr (NW == 4) wb[ks] = *(const frag*)(Wl + KP_KS * 512 + ks * 512);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_mem();
 
-    char* stg = lds + KP_BM * KP_K * 2 + wave * 4096;   // [64 tokens][32] 16-bit
+    char* stg = lds + KP_BM * KP_K * 2 + wave * STG;    // [64 or 128 tokens][32] 16-bit
     const float* bw = bsm + 32 * (plane0 - (n_part >> 5));
 
     // output stores: rows >= M (and non-writer lanes of the key-norm max) get an
     // out-of-range offset and the buffer range check drops them -- no branches
     const bool maxq = a.plane_max2 != nullptr && n_part < a.plane_max_cols;
-    if (maxq) kv_sweep<T, true>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
-    else kv_sweep<T, false>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
+    if constexpr (FULL) {
+        if (maxq) kv_sweep_full<T, true>(a, lds, stg, bw, Wl, wa, planes_w, plane0, m0, lane);
+        else kv_sweep_full<T, false>(a, lds, stg, bw, Wl, wa, planes_w, plane0, m0, lane);
+    } else {
+        if (maxq) kv_sweep<T, true, DIAG, (NW > 4)>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
+        else kv_sweep<T, false, DIAG, (NW > 4)>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
+    }
 }
 
 }  // namespace
@@ -246,7 +397,29 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                                     (uintptr_t)a.bias) % 16 == 0, "cmt_kv_proj: 16-byte aligned operands");
     hipStream_t s = (hipStream_t)stream;
     const unsigned grid = (unsigned)(cdiv(a.M, KP_BM) * parts);
-    if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t><<<grid, KP_NT, 0, s>>>(a, parts);
+    // diagnostics (CMT_KVPROJ_DIAG, bf16): 1 = no output stores, 2 = no W re-fetch, 3 = neither
+    const char* dg = getenv("CMT_KVPROJ_DIAG");
+    const int diag = (dg && dg[0] >= '1' && dg[0] <= '3') ? dg[0] - '0' : 0;
+    // 8-wave form when every wave gets an even number of head planes (CMT_KVPROJ_NW=4 forces the 4-wave form)
+    const char* nw = getenv("CMT_KVPROJ_NW");
+    const bool w8 = !(nw && nw[0] == '4') && (a.N / parts / 32) % 16 == 0;
+    // 8-wave form: whole 128-token tile per W fetch unless CMT_KVPROJ_FULL=0 (two 64-token halves)
+    const char* fu = getenv("CMT_KVPROJ_FULL");
+    const bool full = !(fu && fu[0] == '0');
+    if (w8 && diag == 0) {
+        if (full) {
+            if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t, 0, 8, true><<<grid, 512, 0, s>>>(a, parts);
+            else kvproj_kernel<f16_t, 0, 8, true><<<grid, 512, 0, s>>>(a, parts);
+        } else {
+            if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t, 0, 8><<<grid, 512, 0, s>>>(a, parts);
+            else kvproj_kernel<f16_t, 0, 8><<<grid, 512, 0, s>>>(a, parts);
+        }
+        return cmt_check_launch("cmt_kv_proj");
+    }
+    if (a.w_dtype == CMT_BF16 && diag == 1) kvproj_kernel<bf16_t, 1><<<grid, KP_NT, 0, s>>>(a, parts);
+    else if (a.w_dtype == CMT_BF16 && diag == 2) kvproj_kernel<bf16_t, 2><<<grid, KP_NT, 0, s>>>(a, parts);
+    else if (a.w_dtype == CMT_BF16 && diag == 3) kvproj_kernel<bf16_t, 3><<<grid, KP_NT, 0, s>>>(a, parts);
+    else if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t><<<grid, KP_NT, 0, s>>>(a, parts);
     else kvproj_kernel<f16_t><<<grid, KP_NT, 0, s>>>(a, parts);
     return cmt_check_launch("cmt_kv_proj");
 }

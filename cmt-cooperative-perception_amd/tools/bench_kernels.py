@@ -141,6 +141,14 @@ def main():
         gemm_case("out proj (+res)", 900, 256, 256, bf, a_f32=False, R=True)
         gemm_case("ffn fc1 (relu)", 900, 1024, 256, bf, a_f32=False, relu=True, out_dt=bf)
         gemm_case("ffn fc2 (+res)", 900, 256, 1024, bf, a_f32=False, R=True)
+    if args.only in ("", "enc"):
+        # the encoding GEMMs of the fusion frame (compute-dtype A, LDS-DMA path)
+        gemm_case("rv fc1 (relu)", 24000, 1024, 192, bf, a_f32=False, relu=True, out_dt=bf)
+        gemm_case("rv fc2 (+R)", 24000, 256, 1024, bf, a_f32=False, R=True, out_dt=bf)
+        gemm_case("rv query fc1 (relu)", 5400, 1024, 192, bf, a_f32=False, relu=True, out_dt=bf)
+        gemm_case("rv query fc2", 5400, 256, 1024, bf, a_f32=False)
+        gemm_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, bf, a_f32=False, conv=(180, 180, 512), relu=True,
+                  out_dt=bf)
     if args.only in ("", "gemm", "kv"):
         dev = torch.device("cuda")
         A = torch.randn(32400, 256, device=dev).to(bf)
