@@ -264,6 +264,30 @@ def test_gemm_dma_conv3x3_big(N, dev):
     assert err < 1e-2 + ref.abs().max().item() * 2 ** -8, err
 
 
+def test_gemm_conv3x3_8wave_batched(N, dev):
+    """The 8-wave 256x128 conv kernel (bf16 in/out): two images written into a
+    larger per-batch row block (the fusion memory's gap), M not a multiple of
+    256, every row outside the conv's untouched."""
+    g = torch.Generator().manual_seed(17)
+    B, Cin, H, W, Cout = 2, 64, 19, 23, 256
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / 24
+    b = torch.randn(Cout, generator=g)
+    xin = torch.empty(B * H * W, Cin, dtype=torch.bfloat16, device=dev)
+    N.nchw_to_rows(x.to(dev), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).bfloat16().to(dev).contiguous()
+    Nk = H * W + 7
+    out = torch.full((B * Nk, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    N.gemm(xin, wp, out, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout, bias=b.to(dev), relu=True,
+           a_mode=N.A_CONV3X3, conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin, c_bstride=Nk * Cout)
+    ref = torch.relu(torch.nn.functional.conv2d(_rt(x, torch.bfloat16), _rt(w, torch.bfloat16), b.double(),
+                                                padding=1)).flatten(2).permute(0, 2, 1)
+    got = out.view(B, Nk, Cout)[:, :H * W].cpu().double()
+    err = (got - ref).abs().max().item()
+    assert err < 1e-2 + ref.abs().max().item() * 2 ** -8, err
+    assert torch.isnan(out.view(B, Nk, Cout)[:, H * W:].float()).all(), "conv wrote outside its rows"
+
+
 def _attn_ref(q, k, v, scale):
     s = (q.double() @ k.double().transpose(-1, -2)) * scale
     return torch.softmax(s, -1) @ v.double()
