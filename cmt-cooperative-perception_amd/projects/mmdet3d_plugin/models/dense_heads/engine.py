@@ -314,36 +314,53 @@ class HeadEngineMixin:
         fp32; ``outs16`` (optional) the same in the compute dtype, read by the
         first grouped conv's GEMM directly (LDS-DMA path) instead of
         converting fp32 on load -- the same bf16/f16 rounding either way."""
+        plan = self._task_plan(outs_dec, B, prec, outs16)
+        self._task_run(plan, 0, outs_dec.shape[0])
+        return plan["ret"]
+
+    def _task_plan(self, outs_dec, B, prec, outs16=None):
+        """Output buffers of the task heads (allocated on the current stream)
+        and the per-task packed weights; _task_run fills layers [l0, l1)."""
         L = outs_dec.shape[0]
         Nq = self.num_query
-        C = self.hidden_dim
         ref = self.reference_points.weight.detach()
-        refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
-        ret = []
+        tasks, ret = [], []
         for task in self.task_heads:
             tp = task.packed(prec)
-            nh, k = len(tp["names"]), tp["k"]
-            width = nh * 64
+            width = len(tp["names"]) * 64
             H1 = torch.empty((L, B * Nq, width), dtype=torch.float32, device=outs_dec.device)
             A = outs16 if outs16 is not None and outs16.dtype == tp["w1"].dtype else outs_dec
-            native.gemm(A, tp["w1"], H1, M=B * Nq, N=width, K=k * C, lda=C, ldw=k * C, ldc=width, batch=L,
-                        a_bstride=B * Nq * C, w_bstride=width * k * C, c_bstride=B * Nq * width,
-                        a_mode=native.A_CONV1D3 if k == 3 else native.A_ROWS, seg_len=Nq)
             OUT = torch.empty((L, B, Nq, tp["out_total"]), dtype=torch.float32, device=outs_dec.device)
-            # box_epilogue = False (diagnostics / parity at the logit level): center and height
-            # come out as the raw task-head logits, before + inverse_sigmoid(ref) and sigmoid
-            epi = getattr(self, "box_epilogue", True)
-            native.task_head_tail(H1, tp["gw"], tp["gb"], tp["w2"], tp["b2"], refB, OUT, L=L, B=B, Nq=Nq,
-                                  nheads=nh, hc=64, head_out=tp["head_out"], k=k,
-                                  center_col=tp["center_col"] if epi else -1,
-                                  height_col=tp["height_col"] if epi else -1, pc_range=self.pc_range)
+            tasks.append((tp, A, H1, OUT))
             outs = {}
             start = 0
             for name, n in zip(tp["names"], tp["head_out"]):
                 outs[name] = OUT[..., start:start + n]
                 start += n
             ret.append(outs)
-        return ret
+        refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
+        return dict(tasks=tasks, ret=ret, refB=refB, B=B)
+
+    def _task_run(self, plan, l0, l1):
+        """Task heads of decoder layers [l0, l1): the grouped conv as one GEMM
+        batched over the layers, then GroupLayerNorm1d + ReLU, conv #2 and the
+        box epilogue (cmt_head.py:136-203, 501-513)."""
+        B, Nq, C, n = plan["B"], self.num_query, self.hidden_dim, l1 - l0
+        for tp, A, H1, OUT in plan["tasks"]:
+            nh, k = len(tp["names"]), tp["k"]
+            width = nh * 64
+            # the grouped conv's groups are the decoder layers: weights of groups [l0, l1)
+            native.gemm(A[l0:l1], tp["w1"][l0:l1], H1[l0:l1], M=B * Nq, N=width, K=k * C, lda=C, ldw=k * C, ldc=width,
+                        batch=n, a_bstride=B * Nq * C, w_bstride=width * k * C, c_bstride=B * Nq * width,
+                        a_mode=native.A_CONV1D3 if k == 3 else native.A_ROWS, seg_len=Nq)
+            # box_epilogue = False (diagnostics / parity at the logit level): center and height
+            # come out as the raw task-head logits, before + inverse_sigmoid(ref) and sigmoid
+            epi = getattr(self, "box_epilogue", True)
+            native.task_head_tail(H1[l0:l1], tp["gw"][l0:l1], tp["gb"][l0:l1], tp["w2"][l0:l1], tp["b2"][l0:l1],
+                                  plan["refB"], OUT[l0:l1], L=n,
+                                  B=B, Nq=Nq, nheads=nh, hc=64, head_out=tp["head_out"], k=k,
+                                  center_col=tp["center_col"] if epi else -1,
+                                  height_col=tp["height_col"] if epi else -1, pc_range=self.pc_range)
 
     def _check_eval(self):
         if self.training:

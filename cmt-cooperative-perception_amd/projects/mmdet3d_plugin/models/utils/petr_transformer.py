@@ -497,7 +497,11 @@ class PETRTransformerDecoder(nn.Module):
         """Working buffers of one lowp chain-path decoder run (allocated on the
         current stream; lowp_layer0 may then run on another one)."""
         prec = get_precision(prec)
+        # every packed weight the run reads is built HERE, on the current stream: a pack first
+        # built inside lowp_layer0 on the second stream would be read by the main stream's
+        # K/V projection with nothing ordering the two
         pk = self.packed(prec)
+        self._chain_pack(prec)
         C, H = self.embed_dims, self.embed_dims // 32
         lp, f32, rows = prec.gemm, torch.float32, B * Nq
         FF = pk["layers"][0]["f1_w"].shape[0]

@@ -226,3 +226,42 @@ def test_fusion_head_graph_replay_matches_eager(dev):
         a, b = eager[0][0][k], static[0][0][k]
         assert torch.equal(a, b), (k, (a - b).abs().max().item())
     set_precision("ref")
+
+
+@pytest.mark.parametrize("warm", ["ref", "none"])
+def test_second_stream_matches_single_stream(dev, warm, monkeypatch):
+    """The two-stream schedule (query side + layer 0 self block and the encoder
+    MLP halves on a second stream) gives bit-identical outputs to the
+    single-stream schedule, including on the first low-precision forward of a
+    head (weight packs built inside that forward must be built on the main
+    stream: a pack first built on the second stream was read by the main
+    stream's K/V projection unordered) and with the allocator's cached memory
+    poisoned beforehand (work that never ran leaves NaN, not equal values)."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=3, num_query=96, num_layers=3,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=31).to(dev)
+    xi = S.synthetic_img(6, 8, 20, seed=32).to(dev)
+    metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=33)
+
+    def run(side):
+        monkeypatch.setenv("CMT_SIDE_STREAM", side)
+        torch.empty(64 << 20, dtype=torch.uint8, device=dev).fill_(0xFF)   # NaN-poison the allocator's cache
+        with torch.no_grad():
+            out = head([x], [xi], metas)[0][0]
+        torch.cuda.synchronize()
+        return {k: v.clone() for k, v in out.items()}
+
+    if warm == "ref":
+        set_precision("ref")
+        run("1")
+    set_precision("bf16")
+    try:
+        two = run("1")
+        one = run("0")
+    finally:
+        set_precision("ref")
+    for k in KEYS:
+        assert torch.isfinite(one[k]).all(), k
+        assert torch.equal(one[k], two[k]), (k, (one[k] - two[k]).abs().max().item())
