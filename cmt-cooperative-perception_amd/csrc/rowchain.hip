@@ -277,7 +277,9 @@ __device__ __forceinline__ unsigned long long rc_stamp() {
 }
 constexpr int kChainStamps = 8;
 
-template <typename T, bool STAMP = false>
+// KIND is compile-time: each chain kind gets its own register allocation (chain A's two
+// register-streamed weight sets would otherwise be live in every kind's code)
+template <typename T, int KIND, bool STAMP = false>
 __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigned long long* stamps) {
     unsigned long long t0 = 0, ts[kChainStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
     int ns = 0;
@@ -304,16 +306,17 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
     e.lr = e.lane & 31;
     e.lh = e.lane >> 5;
     e.issued = e.consumed = 0;
-    const int kind = a.kind;
+    constexpr int kind = KIND;
     const bool has_next = a.Wn != nullptr;
     // workgroup -> (row block, part g)
     const int parts = kind == 0 ? 1 : kind == 1 ? 4 : (has_next ? 3 : 1);
     const int rb = blockIdx.x / parts, g = blockIdx.x - rb * parts;
     const T* Wo = (const T*)a.Wo;
+    const bool wo_regs = kind == 0 && a.wo_frag;   // chain A with fragment-major Wo: no LDS weight ring
     if (kind == 0) {
         e.w0 = Wo; e.ld0 = CE;
         e.w1 = nullptr; e.ld1 = CE;        // the Q projection streams into registers (fragment-major W1)
-        e.nstages = SUB_STAGES;
+        e.nstages = wo_regs ? 0 : SUB_STAGES;
     } else if (kind == 1) {
         e.w0 = Wo; e.ld0 = CE;
         e.w1 = (const T*)a.W1 + (int64_t)g * CE * CE; e.ld1 = CE;       // fc1 rows [256g, 256g + 256)
@@ -382,6 +385,10 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
 #pragma unroll
     for (int s = 0; s < NSTG - 1; ++s) e.issue();
     typename Eng<T>::frag wr[SUB_STAGES][2];
+    typename Eng<T>::frag wr0[kind == 0 ? SUB_STAGES : 1][2];
+    if constexpr (kind == 0) {
+        if (wo_regs) e.load_wregs(Wo, 0, wr0);
+    }
     if (kind == 2 && has_next) e.load_wregs((const T*)a.Wn, g, wr);
     if (kind == 0) e.load_wregs((const T*)a.W1, 0, wr);
     if (kind == 1) e.load_wregs((const T*)a.W2, g, wr);
@@ -397,7 +404,10 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
     const float eps = a.eps;
     if (kind == 0) {
         // ---------------- chain A
-        e.sub_gemm(actA, acc, true);                                   // out_proj
+        if constexpr (kind == 0) {
+            if (wo_regs) e.sub_gemm_regs(actA, wr0, acc);              // out_proj (register weights)
+            else e.sub_gemm(actA, acc, true);                          // out_proj (LDS weight ring)
+        }
         mark();   // 1
         {
             const float* bo = e.prm();
@@ -587,14 +597,21 @@ extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
     unsigned long long* st = chain_stamp_buffer(grid);
+#define CHAIN_LAUNCH(T, STAMPED, BUF)                                                  \
+    do {                                                                               \
+        if (a.kind == 0) chain_kernel<T, 0, STAMPED><<<grid, NTC, 0, s>>>(a, BUF);     \
+        else if (a.kind == 1) chain_kernel<T, 1, STAMPED><<<grid, NTC, 0, s>>>(a, BUF); \
+        else chain_kernel<T, 2, STAMPED><<<grid, NTC, 0, s>>>(a, BUF);                 \
+    } while (0)
     if (st) {
-        if (a.dtype == CMT_BF16) chain_kernel<bf16_t, true><<<grid, NTC, 0, s>>>(a, st);
-        else chain_kernel<f16_t, true><<<grid, NTC, 0, s>>>(a, st);
+        if (a.dtype == CMT_BF16) CHAIN_LAUNCH(bf16_t, true, st);
+        else CHAIN_LAUNCH(f16_t, true, st);
         const int rc = cmt_check_launch("cmt_chain");
         if (rc == 0) chain_stamp_report(a.kind, grid, st, s);
         return rc;
     }
-    if (a.dtype == CMT_BF16) chain_kernel<bf16_t><<<grid, NTC, 0, s>>>(a, nullptr);
-    else chain_kernel<f16_t><<<grid, NTC, 0, s>>>(a, nullptr);
+    if (a.dtype == CMT_BF16) CHAIN_LAUNCH(bf16_t, false, nullptr);
+    else CHAIN_LAUNCH(f16_t, false, nullptr);
+#undef CHAIN_LAUNCH
     return cmt_check_launch("cmt_chain");
 }

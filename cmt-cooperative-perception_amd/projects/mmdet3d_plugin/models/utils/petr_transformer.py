@@ -38,6 +38,11 @@ __all__ = ["FFN", "MultiheadAttention", "PETRMultiheadFlashAttention", "PETRMult
            "PETRTransformerDecoderLayer", "PETRTransformerDecoder"]
 
 
+def _wo(lw):
+    """Chain A's out_proj weights: fragment-major when packed (registers), else row-major (LDS ring)."""
+    return lw["sa_owp"] if lw.get("sa_owp") is not None else lw["sa_ow"]
+
+
 def _rows(x):
     """[N, B, C] -> contiguous fp32 [N*B, C]."""
     return x.reshape(-1, x.shape[-1]).contiguous().float()
@@ -388,6 +393,10 @@ class PETRTransformerDecoder(nn.Module):
                     sa_wp=(native.pack_chain_wn(to_dtype(sa.in_proj_weight, g))
                            if g != torch.float32 and tuple(sa.in_proj_weight.shape) == (768, 256) else None),
                     sa_ow=to_dtype(sa.out_proj.weight, g), sa_ob=sa.out_proj.bias.detach().contiguous(),
+                    # chain A's copy of the self-attn out_proj weights, fragment-major (cmt_hip.h wo_frag)
+                    sa_owp=(native.pack_chain_wn(to_dtype(sa.out_proj.weight, g))
+                            if g != torch.float32 and C == 256 and os.environ.get("CMT_CHAIN_A_WOREGS", "1") != "0"
+                            else None),
                     ca_wq=to_dtype(ca.in_proj_weight[:C], g),
                     ca_wqp=(native.pack_chain_wn(to_dtype(ca.in_proj_weight[:C], g))
                             if g != torch.float32 and C == 256 else None),
@@ -537,7 +546,7 @@ class PETRTransformerDecoder(nn.Module):
         native.gemm(st["tl"], l0["sa_w"], st["qkv"], M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
                     A2=st["tp"], lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
         self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
-        native.chain(0, st["ob"], qpos, ch["A"][0], l0["sa_ow"], l0["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
+        native.chain(0, st["ob"], qpos, ch["A"][0], _wo(l0), l0["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
                      eps=self.post_norm.eps, R=None, Q=st["qc"])
         st["layer0_done"] = True
         st["stream"] = torch.cuda.current_stream()
@@ -721,7 +730,7 @@ class PETRTransformerDecoder(nn.Module):
         for l, lw in enumerate(pk["layers"]):
             if l > 0:
                 self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
-                native.chain(0, ob, qpos, ch["A"][l], lw["sa_ow"], lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
+                native.chain(0, ob, qpos, ch["A"][l], _wo(lw), lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
                              R=tgt, Q=qc)
             with timed("cross_attn"):
                 native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,

@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -64,7 +64,7 @@ class ChainArgs(ctypes.Structure):
                 ("X", _vp), ("R", _vp), ("P", _vp), ("prm", _vp),
                 ("Wo", _vp), ("W1", _vp), ("W2", _vp), ("Wn", _vp),
                 ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp), ("WS", _vp),
-                ("OUT16", _vp)]
+                ("OUT16", _vp), ("wo_frag", _int)]
 
 
 class LnArgs(ctypes.Structure):
@@ -470,6 +470,10 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
         raise RuntimeError("cmt_chain: chain B1's W2 must be fragment-major (pack_chain_fc2)")
     if kind == 0 and (W1 is None or W1.dim() != 1 or W1.numel() != 256 * 256):
         raise RuntimeError("cmt_chain: chain A's W1 must be fragment-major (pack_chain_wn)")
+    # chain A's Wo: row-major [256, 256] (LDS weight ring) or fragment-major 1-D (pack_chain_wn: registers)
+    wo_frag = int(kind == 0 and Wo is not None and Wo.dim() == 1)
+    if wo_frag and Wo.numel() != 256 * 256:
+        raise RuntimeError("cmt_chain: a fragment-major Wo must be pack_chain_wn of [256, 256]")
     if OUT16 is not None and (OUT is None or OUT16.dtype not in (torch.float16, torch.bfloat16)):
         raise RuntimeError("cmt_chain: OUT16 must be a 16-bit copy target beside OUT")
     if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:
@@ -493,6 +497,7 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     a.Q = ptr(Q)
     a.WS = ptr(WS)
     a.OUT16 = None if OUT16 is None else OUT16.data_ptr() + 2 * out_offset
+    a.wo_frag = wo_frag
     _check(lib().cmt_chain(ctypes.byref(a), _stream()), "cmt_chain")
 
 

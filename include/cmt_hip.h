@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 9
+#define CMT_ABI_VERSION 10
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -260,6 +260,8 @@ typedef struct cmt_chain_args {
     void* Q;                   /* head-split projection output (A; B2 with Wn) */
     float* WS;                 /* B1 / B2: partials workspace, 4 * ceil(rows/32) * 32 * 256 fp32 (private order) */
     void* OUT16;               /* B2 (optional): the layer output again in dtype (the task-head GEMM operand) */
+    int wo_frag;               /* A: 1 = Wo is FRAGMENT-MAJOR (the Wn layout, g = 0) and streams into registers
+                                  with W1 (no LDS weight ring); 0 = row-major Wo through the ring (ABI 10) */
 } cmt_chain_args;
 int cmt_chain(const cmt_chain_args* args, void* stream);
 /* bytes of the B1 -> B2 partials workspace WS for `rows` query rows */

@@ -564,6 +564,13 @@ def test_chain_a(N, dev, dt, B, Nq, with_r):
     assert (Y.cpu().double() - y).abs().max().item() < 2e-3
     rel = (Q.cpu().double() - qref).abs().max().item() / qref.abs().max().item()
     assert rel < 1.5e-2, rel
+    # fragment-major Wo (wo_frag: register-streamed out_proj, no LDS weight ring): the same
+    # MFMA k-order, so bit-identical outputs
+    Y2 = torch.empty_like(Y)
+    Q2 = torch.empty_like(Q)
+    N.chain(0, X.to(dev), P.to(dev), prm.to(dev), N.pack_chain_wn(Wo.to(dev)), N.pack_chain_wn(Wq.to(dev)), Y2,
+            rows=rows, Nq=Nq, eps=1e-5, R=R.to(dev) if R is not None else None, Q=Q2)
+    assert torch.equal(Y, Y2) and torch.equal(Q, Q2)
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
