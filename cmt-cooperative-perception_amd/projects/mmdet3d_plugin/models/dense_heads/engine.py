@@ -24,6 +24,8 @@ The reference computes the BEV positional encoding, the coordinate encodings
 and every layer's K/V projection again on each forward; so does this engine
 (no output caching across frames).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -300,7 +302,6 @@ class HeadEngineMixin:
 
     def _side_stream(self, dev):
         """The head's second HIP stream on ``dev`` (CMT_SIDE_STREAM=0: none)."""
-        import os
         if dev.type != "cuda" or os.environ.get("CMT_SIDE_STREAM", "1") == "0":
             return None
         pool = self.__dict__.setdefault("_side_streams", {})

@@ -149,6 +149,7 @@ def main():
         gemm_case("rv query fc2", 5400, 256, 1024, bf, a_f32=False)
         gemm_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, bf, a_f32=False, conv=(180, 180, 512), relu=True,
                   out_dt=bf)
+        gemm_case("shared_conv shape, plain rows", 32400, 256, 4608, bf, a_f32=False, relu=True, out_dt=bf)
     if args.only in ("", "gemm", "kv"):
         dev = torch.device("cuda")
         A = torch.randn(32400, 256, device=dev).to(bf)
