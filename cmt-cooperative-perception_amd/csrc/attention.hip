@@ -1190,6 +1190,287 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Paired-tile form of attn_pb_kernel: every ping-pong window covers TWO 64-key
+// tiles (M: 8 QK^T + 16 PV / row-sum MFMAs; V: 64 exp2 + 32 packs), so the
+// per-window costs -- the barrier hand-off, the segment-start VALU penalty,
+// the LDS fragment reads' latency (MI355X_MICROARCH.md 'Two waves per SIMD'
+// items 6-7) -- are paid once per 128 keys instead of once per 64.  The K/V
+// ring grows to PB2_RING slots: half A issues tiles 2j+6 and 2j+7 at the start
+// of its M(j), into the slots of pair j-3, which half B (one segment behind)
+// last read in its V(j-2).  Same per-score math and the same tile order of the
+// PV / row-sum accumulation as attn_pb_kernel (bit-identical on the offset-free
+// path); on the online-max fallback one offset update covers both tiles of a
+// pair.  A leftover odd tile and the ragged last tile run after the loop with
+// every wave at once.  Row sums on the MFMA pipe only (RSUM 0).
+// ---------------------------------------------------------------------------
+constexpr int PB2_RING = 10;
+
+// tiles (two LDS-DMA pieces each) still allowed in flight behind the ones needed now, 0..4
+__device__ __forceinline__ void pb2_wait(int tiles) {
+    if (tiles >= 4) pp_wait_n<8>();
+    else if (tiles == 3) pp_wait_n<6>();
+    else if (tiles == 2) pp_wait_n<4>();
+    else if (tiles == 1) pp_wait_n<2>();
+    else pp_wait_n<0>();
+}
+
+// V segment of a pair: P = exp2(s) (offset-free) or exp2(s - m) with ONE online-max update for both tiles
+template <typename T>
+__device__ __forceinline__ void pb2_vseg(f32x16 (&s0)[2], f32x16 (&s1)[2], typename mfma_traits<T>::frag (&pf0)[2][2],
+                                         typename mfma_traits<T>::frag (&pf1)[2][2], f32x16& o, f32x16& lsum,
+                                         float& m_run, bool fast, bool first) {
+    if (!fast) {
+        float m0 = vmax(s0[0][0], s0[0][1]), m1 = vmax(s0[1][0], s0[1][1]);
+        float m2 = vmax(s1[0][0], s1[0][1]), m3 = vmax(s1[1][0], s1[1][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            m0 = vmax3(m0, s0[0][r], s0[0][r + 1]);
+            m1 = vmax3(m1, s0[1][r], s0[1][r + 1]);
+            m2 = vmax3(m2, s1[0][r], s1[0][r + 1]);
+            m3 = vmax3(m3, s1[1][r], s1[1][r + 1]);
+        }
+        const float mt = pair_max(vmax(vmax(m0, m1), vmax(m2, m3)));
+        if (first) {
+            m_run = mt;
+        } else if (__any(mt > m_run + kDeferMax)) {
+            const float mn = vmax(m_run, mt);
+            const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+            o *= alpha;
+            lsum *= alpha;
+            m_run = mn;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            s0[0][r] -= m_run;
+            s0[1][r] -= m_run;
+            s1[0][r] -= m_run;
+            s1[1][r] -= m_run;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        pf0[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s0[0][r]);
+        pf0[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s0[1][r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        pf1[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s1[0][r]);
+        pf1[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s1[1][r]);
+    }
+}
+
+template <typename T, int OCC>
+__global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
+    __shared__ __attribute__((aligned(16))) T ring[PB2_RING * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool hb = wave >= 4;          // wave-uniform: second half runs one segment behind
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+
+    // XCD-aware block order (as attn_pb_kernel)
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int qb = wg % p.nqb;
+    const int rest = wg / p.nqb;
+    const int BH = p.B * p.H;
+    const int bh = rest % BH;
+    const int split = rest / BH;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+
+    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+    const float c = p.c;
+
+    const int ntiles = (p.Nk + KT - 1) / KT;
+    const int t_begin = split * p.tiles_per_split;
+    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
+    const bool tail = (p.Nk % KT) != 0 && t_end == ntiles && t_begin < t_end;   // ragged last tile here
+    const int nt = max(0, t_end - t_begin - (tail ? 1 : 0));                    // full tiles
+    const int np = nt >> 1;                                                      // full tile pairs
+
+    const int crow = lane >> 2, cch = lane & 3;
+    const int prow = (wave & 3) * 16 + crow;
+    const T* ksrc = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+    const T* vsrc = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
+    const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
+    T* const my_k = ring + (wave & 3) * 16 * D;
+    int issued = 0;   // tiles issued (half A)
+    auto issue_upto = [&](int n) {   // tiles [issued, min(n, nt)) into their ring slots
+        const int e = min(n, nt);
+        while (issued < e) {
+            T* dst = my_k + (issued % PB2_RING) * STAGE;
+            dma16(ksrc, dst);
+            dma16(vsrc, dst + KT * D);
+            ksrc += kstep;
+            vsrc += vstep;
+            ++issued;
+        }
+    };
+
+    const char* const rb = (const char*)ring;
+    constexpr int STAGE_B = STAGE * (int)sizeof(T), KV_B = KT * D * (int)sizeof(T);
+    const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
+    f32x16 s0[2], s1[2];
+    frag pf0[2][2], pf1[2][2], kf0[2][2], kf1[2][2], vf0[2][2], vf1[2][2];
+    // the first three pairs' LDS-DMA before the Q / max-|k| loads
+    if (!hb) issue_upto(PB2_RING - 4);
+
+    // ---- Q^T fragments with the folded scale (s is in exp2 units)
+    const int q = qb * (8 * QW) + wave * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    frag qf[2];
+    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
+
+    // ---- fast path iff |q| max|k| <= kBoundMax for every query of the wave
+    bool fast;
+    {
+        const float km = kmax_reduce(p, b, h, split, lane);
+        float qq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
+        qq = pair_sum(qq);
+        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
+        fast = __all(bound <= kBoundMax);
+    }
+
+    f32x16 o, lsum;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o[r] = 0.f;
+        lsum[r] = 0.f;
+    }
+    float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tiles
+
+    auto slot_b = [&](int t) { return rb + (t % PB2_RING) * STAGE_B; };
+    if (hb) pp_barrier();   // half B: one segment behind
+    if (np > 0) {
+        if (!hb) pb2_wait(issued - 2);                 // tiles 0, 1 landed
+        pp_barrier();
+        if (!hb) issue_upto(8);
+        {
+            const PpLane l = pp_launder(lane_ofs);
+            pp_load_k<T>(slot_b(0), l, kf0);
+            pp_load_k<T>(slot_b(1), l, kf1);
+        }
+        pb_mseg<T, true, false, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_mseg<T, true, false, 0>(kf1, vf1, qf, pf1, s1, o, lsum);
+        if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
+        pp_barrier();
+        pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fast, true);
+        {
+            const PpLane l = pp_launder(lane_ofs);
+            pp_load_k<T>(slot_b(2), l, kf0);   // stale (unused) when np == 1
+            pp_load_k<T>(slot_b(3), l, kf1);
+            pp_load_v<T>(slot_b(0) + KV_B, l, vf0);
+            pp_load_v<T>(slot_b(1) + KV_B, l, vf1);
+        }
+        for (int j = 1; j < np; ++j) {
+            pp_barrier();
+            if (!hb) issue_upto(2 * j + 8);
+            pb_mseg<T, true, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);   // QK^T tile 2j, PV tile 2j-2
+            pb_mseg<T, true, true, 0>(kf1, vf1, qf, pf1, s1, o, lsum);   // QK^T tile 2j+1, PV tile 2j-1
+            if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
+            pp_barrier();
+            pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fast, false);
+            const PpLane l = pp_launder(lane_ofs);
+            pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
+            pp_load_k<T>(slot_b(2 * j + 3), l, kf1);
+            pp_load_v<T>(slot_b(2 * j) + KV_B, l, vf0);
+            pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
+        }
+        pp_barrier();
+        pb_mseg<T, false, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_mseg<T, false, true, 0>(kf1, vf1, qf, pf1, s1, o, lsum);
+    }
+    if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
+
+    if (nt & 1) {
+        // leftover full tile (odd count): every wave at once
+        if (!hb) {
+            issue_upto(nt);
+            pp_wait_n<0>();
+        }
+        pp_barrier();
+        const PpLane l = pp_launder(lane_ofs);
+        pp_load_k<T>(slot_b(nt - 1), l, kf0);
+        pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
+        pb_mseg<T, true, false, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_vseg<T, 0>(s0, pf0, o, lsum, m_run, fast, np == 0);
+        pb_mseg<T, false, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+    }
+
+    if (tail) {
+        // ragged last tile: masked, every wave at once
+        pp_barrier();
+        if (!hb) {
+            const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked below
+            const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+            const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
+            dma16(ks, my_k);
+            dma16(vs, my_k + KT * D);
+            pp_wait_n<0>();
+        }
+        pp_barrier();
+        const PpLane l = pp_launder(lane_ofs);
+        pp_load_k<T>(rb, l, kf0);
+        pp_load_v<T>(rb + KV_B, l, vf0);
+        pb_mseg<T, true, false, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        const int key0 = (ntiles - 1) * KT;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s0[kb][r] = -__builtin_inff();
+        pb_vseg<T, 0>(s0, pf0, o, lsum, m_run, fast, nt == 0);
+        pb_mseg<T, false, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+    }
+
+    // ---- write (as attn_pb_kernel)
+    const float l_tot = lsum[0];
+    if (q >= p.Nq) return;
+    if (p.splits == 1) {
+        const float inv = 1.f / l_tot;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+            if (p.round_out) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+            }
+            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
+        }
+    } else {
+        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
+        float* dst = p.Op + row * D;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
+        }
+        if (lh == 0) {
+            p.Mp[row] = m_run;   // exp2 units (0 on the fast path)
+            p.Lp[row] = l_tot;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Exact-f32 variant (v_mfma_f32_32x32x2_f32): same tiling and online softmax;
 // used where the reference computes attention in fp32 (nn.MultiheadAttention
 // self-attention).  K image rows padded to 36 floats (conflict-free
@@ -1433,6 +1714,12 @@ bool use_pp(const cmt_attn_args& a) {
     return a.dtype != CMT_F32 && sh.waves == 8 && sh.sub == 1;
 }
 
+// the paired-tile form of the pb kernel (128 keys per ping-pong window); CMT_ATTN_PB2=0: one tile per window
+bool use_pb2() {
+    const char* ov = getenv("CMT_ATTN_PB2");   // read per call: the tests toggle it in one process
+    return !(ov && ov[0] == '0');
+}
+
 // the bf16 long-key path with max-|k| partials and the folded scale
 bool use_pb(const cmt_attn_args& a) {
     static const char* ov = getenv("CMT_ATTN_PB");
@@ -1633,6 +1920,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     } while (0)
             if (p.stamp && stamp_mode() == 2) attn_pb_kernel<bf16_t, 0, 1, 2><<<nwg, 512, 0, s>>>(p);
             else if (p.stamp) attn_pb_kernel<bf16_t, 0, 1, 1><<<nwg, 512, 0, s>>>(p);
+            else if (rs == 0 && use_pb2()) attn_pb2_kernel<bf16_t, 1><<<nwg, 512, 0, s>>>(p);
             else if (pp_occ() == 2) PB_LAUNCH(2);
             else PB_LAUNCH(1);
 #undef PB_LAUNCH

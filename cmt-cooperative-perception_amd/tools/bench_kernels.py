@@ -83,8 +83,11 @@ def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0, fold=False):
           f"{tf:8.1f} TF/s", flush=True)
 
 
-def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
-    """Row-block chain A (kind 0), B1 (1) or B2 (2) at the decoder's query shape."""
+def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False, cold=False, wo_frag=False):
+    """Row-block chain A (kind 0), B1 (1) or B2 (2) at the decoder's query shape.
+    cold: a 64 MB streaming read between launches (evicts the weights from L2,
+    as the cross-attention's K/V stream does in the frame); its own time is
+    measured alone and subtracted."""
     dev = torch.device("cuda")
     C, F = 256, 1024
     X = torch.randn(rows, C, device=dev).to(dt)
@@ -99,7 +102,8 @@ def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
     Q = torch.empty(rows * 3 * C, dtype=dt, device=dev)
     if kind == 0:
         W1p = N.pack_chain_wn(W1[:256].contiguous())
-        fn = lambda: N.chain(0, X, P, prm, Wo, W1p, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, Q=Q)
+        Wa = N.pack_chain_wn(Wo) if wo_frag else Wo
+        fn = lambda: N.chain(0, X, P, prm, Wa, W1p, Y, rows=rows, Nq=Nq, eps=1e-5, R=R, Q=Q)
         fl = 2 * rows * C * C * 2
     elif kind == 1:
         W2p = N.pack_chain_fc2(W2)
@@ -109,8 +113,15 @@ def chain_case(kind, rows=900, Nq=900, dt=torch.bfloat16, last=False):
         fn = lambda: N.chain(2, None, None if last else P, prm, None, None, Y, rows=rows, Nq=Nq, eps=1e-5,
                              Wn=Wn, OUT=OUT, Q=None if last else Q, WS=WS)
         fl = 2 * rows * C * C * (0 if last else 3)
-    us = timeit(fn)
-    print(f"chain {['A ', 'B1', 'B2'][kind]}{' last' if last else '     '} rows={rows:5d} {us:9.2f} us "
+    if cold:
+        junk = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        flush = lambda: junk.view(torch.float32).sum()  # noqa: E731
+        t_flush = timeit(flush)
+        us = timeit(lambda: (flush(), fn())) - t_flush
+    else:
+        us = timeit(fn)
+    tag = (" cold" if cold else "") + (" wo_frag" if wo_frag else "")
+    print(f"chain {['A ', 'B1', 'B2'][kind]}{' last' if last else '     '}{tag} rows={rows:5d} {us:9.2f} us "
           f"{fl / (us * 1e-6) / 1e12:8.1f} TF/s", flush=True)
 
 
@@ -165,6 +176,9 @@ def main():
     if args.only in ("", "chain"):
         for kind, last in ((0, False), (1, False), (2, False), (2, True)):
             chain_case(kind, last=last)
+            chain_case(kind, last=last, cold=True)
+        chain_case(0, wo_frag=True)
+        chain_case(0, wo_frag=True, cold=True)
         chain_case(1, rows=1800)
     if args.only in ("", "attn"):
         for s in (0, 8, 16):

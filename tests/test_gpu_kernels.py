@@ -229,6 +229,43 @@ def test_attention_bounded_max(N, dev, B, Nq, Nk, splits, scale_q):
         assert err < 2e-2, (fold, err)
 
 
+@pytest.mark.parametrize("B,Nq,Nk,splits,scale_q", [(1, 900, 56400, 0, 1.0), (2, 300, 4097, 3, 1.0),
+                                                    (1, 257, 8192, 1, 1.0), (1, 900, 4160, 5, 1.0),
+                                                    (1, 900, 32400, 0, 12.0)])
+def test_attention_pb2_matches_pb(N, dev, monkeypatch, B, Nq, Nk, splits, scale_q):
+    """Paired-tile pb kernel (128 keys per ping-pong window) against the one-tile
+    pb kernel on the same inputs: bit-identical on the offset-free path (same
+    per-score math, same tile order of the PV / row-sum accumulation), with odd
+    full-tile counts per split, a ragged last tile and 1-5 splits; with large |q|
+    (online-max fallback, one offset update per pair) within 1e-2 of it."""
+    H = 8
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(Nk + Nq)
+    q = (torch.randn(B, H, Nq, 32, generator=g) * scale_q).to(dt).to(dev)
+    k = torch.randn(B, H, Nk, 32, generator=g).to(dt)
+    v = torch.randn(B, H, Nk, 32, generator=g).to(dt).to(dev)
+    ss = (k.double().permute(0, 2, 1, 3).reshape(B * Nk, H, 32) ** 2).sum(-1)
+    nb = -(-B * Nk // 64)
+    km = torch.cat([ss, torch.zeros(nb * 64 - B * Nk, H, dtype=ss.dtype)], 0).view(nb, 64, H).amax(1)
+    kmax2 = km.float().contiguous().to(dev)
+    k = k.to(dev)
+    outs = []
+    for pb2 in ("1", "0"):
+        monkeypatch.setenv("CMT_ATTN_PB2", pb2)
+        O = torch.empty(B, Nq, H * 32, device=dev)
+        N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk,
+                    q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                    v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
+                    kv_splits=splits, fold_scale=True, kmax2=kmax2, kmax_ld=H, kmax_plane0=0)
+        torch.cuda.synchronize()
+        outs.append(O.cpu())
+    assert torch.isfinite(outs[0]).all()
+    if scale_q == 1.0:
+        assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
+    else:
+        assert (outs[0] - outs[1]).abs().max().item() < 1e-2
+
+
 def test_gemm_dma_conv1d3_lowp(N, dev):
     g = torch.Generator().manual_seed(12)
     L, B, Nq, C, O = 3, 2, 37, 256, 128
