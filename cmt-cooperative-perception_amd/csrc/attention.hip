@@ -856,6 +856,33 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pp_kernel(AttnKParams p) {
 // ---------------------------------------------------------------------------
 template <int RSUM> struct pb_lsum { typedef float type; };
 template <> struct pb_lsum<0> { typedef f32x16 type; };
+template <> struct pb_lsum<3> { typedef f32x4 type; };
+
+// RSUM 3: row sums on v_mfma_f32_16x16x32 (16 cycles, half the 32x32x16 ones-MFMA).  The P^T
+// fragment (32x32x16 B layout: lane L = query L%32, keys 8*(L/32)..+8) read as a 16x16x32 B
+// operand puts query L%32 at column L%16 in k-group L/16, so queries q < 16 sit in k-groups 0, 2
+// and q >= 16 in k-groups 1, 3.  Selector rows: A[0][k] = 1 on groups 0, 2, A[1][k] = 1 on 1, 3;
+// D[0][n] accumulates query n, D[1][n] query n + 16 (lane n, registers 0 and 1).
+__device__ __forceinline__ bf16x8 rs16_selector(int lane) {
+    const int m = lane & 15, g = lane >> 4;
+    const bf16_t v = (bf16_t)((m == 0 && (g & 1) == 0) || (m == 1 && (g & 1) == 1) ? 1.f : 0.f);
+    bf16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = v;
+    return a;
+}
+// query lr's row sum from the RSUM 3 accumulator
+__device__ __forceinline__ float rs16_total(const f32x4& l, int lane) {
+    const int src = lane & 15;
+    const float a0 = __shfl(l[0], src), a1 = __shfl(l[1], src);
+    return (lane & 31) < 16 ? a0 : a1;
+}
+// online-max rescale of the RSUM 3 accumulator (alpha is per query = per lane L%32)
+__device__ __forceinline__ void rs16_scale(f32x4& l, float alpha, int lane) {
+    const float hi = __shfl(alpha, (lane & 15) + 16);
+    l[0] *= alpha;
+    l[1] *= hi;
+}
 
 template <typename T, bool QK, bool PV, int RSUM>
 __device__ __forceinline__ void pb_mseg(const typename mfma_traits<T>::frag (&kf)[2][2],
@@ -884,6 +911,8 @@ __device__ __forceinline__ void pb_mseg(const typename mfma_traits<T>::frag (&kf
                     for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
                     lsum = mfma_traits<T>::mma(ones, pf[kb][ss], lsum);
                 }
+                if constexpr (RSUM == 3)
+                    lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rs16_selector(lane_id()), pf[kb][ss], lsum, 0, 0, 0);
             }
     }
 }
@@ -907,7 +936,8 @@ __device__ __forceinline__ void pb_vseg(f32x16 (&s)[2], typename mfma_traits<T>:
             const float mn = vmax(m_run, mt);
             const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
             o *= alpha;
-            lsum *= alpha;
+            if constexpr (RSUM == 3) rs16_scale(lsum, alpha, lane_id());
+            else lsum *= alpha;
             m_run = mn;
         }
 #pragma unroll
@@ -1215,10 +1245,10 @@ __device__ __forceinline__ void pb2_wait(int tiles) {
 }
 
 // V segment of a pair: P = exp2(s) (offset-free) or exp2(s - m) with ONE online-max update for both tiles
-template <typename T>
+template <typename T, int RSUM>
 __device__ __forceinline__ void pb2_vseg(f32x16 (&s0)[2], f32x16 (&s1)[2], typename mfma_traits<T>::frag (&pf0)[2][2],
-                                         typename mfma_traits<T>::frag (&pf1)[2][2], f32x16& o, f32x16& lsum,
-                                         float& m_run, bool fast, bool first) {
+                                         typename mfma_traits<T>::frag (&pf1)[2][2], f32x16& o,
+                                         typename pb_lsum<RSUM>::type& lsum, float& m_run, bool fast, bool first) {
     if (!fast) {
         float m0 = vmax(s0[0][0], s0[0][1]), m1 = vmax(s0[1][0], s0[1][1]);
         float m2 = vmax(s1[0][0], s1[0][1]), m3 = vmax(s1[1][0], s1[1][1]);
@@ -1236,7 +1266,8 @@ __device__ __forceinline__ void pb2_vseg(f32x16 (&s0)[2], f32x16 (&s1)[2], typen
             const float mn = vmax(m_run, mt);
             const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
             o *= alpha;
-            lsum *= alpha;
+            if constexpr (RSUM == 3) rs16_scale(lsum, alpha, lane_id());
+            else lsum *= alpha;
             m_run = mn;
         }
 #pragma unroll
@@ -1259,7 +1290,7 @@ __device__ __forceinline__ void pb2_vseg(f32x16 (&s0)[2], f32x16 (&s1)[2], typen
     }
 }
 
-template <typename T, int OCC>
+template <typename T, int OCC, int RSUM>
 __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
     constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
@@ -1349,12 +1380,12 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         fast = __all(bound <= kBoundMax);
     }
 
-    f32x16 o, lsum;
+    static_assert(RSUM == 0 || RSUM == 3, "pb2: row sums on the MFMA pipe");
+    typedef typename pb_lsum<RSUM>::type LT;
+    f32x16 o;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        o[r] = 0.f;
-        lsum[r] = 0.f;
-    }
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    LT lsum = LT{};
     float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tiles
 
     auto slot_b = [&](int t) { return rb + (t % PB2_RING) * STAGE_B; };
@@ -1368,11 +1399,11 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
             pp_load_k<T>(slot_b(0), l, kf0);
             pp_load_k<T>(slot_b(1), l, kf1);
         }
-        pb_mseg<T, true, false, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
-        pb_mseg<T, true, false, 0>(kf1, vf1, qf, pf1, s1, o, lsum);
+        pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_mseg<T, true, false, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
         if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
         pp_barrier();
-        pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fast, true);
+        pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, true);
         {
             const PpLane l = pp_launder(lane_ofs);
             pp_load_k<T>(slot_b(2), l, kf0);   // stale (unused) when np == 1
@@ -1383,11 +1414,11 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         for (int j = 1; j < np; ++j) {
             pp_barrier();
             if (!hb) issue_upto(2 * j + 8);
-            pb_mseg<T, true, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);   // QK^T tile 2j, PV tile 2j-2
-            pb_mseg<T, true, true, 0>(kf1, vf1, qf, pf1, s1, o, lsum);   // QK^T tile 2j+1, PV tile 2j-1
+            pb_mseg<T, true, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);   // QK^T tile 2j, PV tile 2j-2
+            pb_mseg<T, true, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);   // QK^T tile 2j+1, PV tile 2j-1
             if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
             pp_barrier();
-            pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fast, false);
+            pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, false);
             const PpLane l = pp_launder(lane_ofs);
             pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
             pp_load_k<T>(slot_b(2 * j + 3), l, kf1);
@@ -1395,8 +1426,8 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
             pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
         }
         pp_barrier();
-        pb_mseg<T, false, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
-        pb_mseg<T, false, true, 0>(kf1, vf1, qf, pf1, s1, o, lsum);
+        pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_mseg<T, false, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
     }
     if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
 
@@ -1410,9 +1441,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         const PpLane l = pp_launder(lane_ofs);
         pp_load_k<T>(slot_b(nt - 1), l, kf0);
         pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
-        pb_mseg<T, true, false, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
-        pb_vseg<T, 0>(s0, pf0, o, lsum, m_run, fast, np == 0);
-        pb_mseg<T, false, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, np == 0);
+        pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
     }
 
     if (tail) {
@@ -1430,19 +1461,21 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         const PpLane l = pp_launder(lane_ofs);
         pp_load_k<T>(rb, l, kf0);
         pp_load_v<T>(rb + KV_B, l, vf0);
-        pb_mseg<T, true, false, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
         const int key0 = (ntiles - 1) * KT;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s0[kb][r] = -__builtin_inff();
-        pb_vseg<T, 0>(s0, pf0, o, lsum, m_run, fast, nt == 0);
-        pb_mseg<T, false, true, 0>(kf0, vf0, qf, pf0, s0, o, lsum);
+        pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, nt == 0);
+        pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
     }
 
     // ---- write (as attn_pb_kernel)
-    const float l_tot = lsum[0];
+    float l_tot;
+    if constexpr (RSUM == 3) l_tot = rs16_total(lsum, lane);
+    else l_tot = lsum[0];
     if (q >= p.Nq) return;
     if (p.splits == 1) {
         const float inv = 1.f / l_tot;
@@ -1720,6 +1753,12 @@ bool use_pb2() {
     return !(ov && ov[0] == '0');
 }
 
+// pb2 row sums on the 16x16x32 MFMA (RSUM 3); CMT_ATTN_RS16=0: the 32x32x16 ones-MFMA
+bool pb2_rs16() {
+    const char* ov = getenv("CMT_ATTN_RS16");   // read per call: the tests toggle it in one process
+    return !(ov && ov[0] == '0');
+}
+
 // the bf16 long-key path with max-|k| partials and the folded scale
 bool use_pb(const cmt_attn_args& a) {
     static const char* ov = getenv("CMT_ATTN_PB");
@@ -1920,7 +1959,8 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     } while (0)
             if (p.stamp && stamp_mode() == 2) attn_pb_kernel<bf16_t, 0, 1, 2><<<nwg, 512, 0, s>>>(p);
             else if (p.stamp) attn_pb_kernel<bf16_t, 0, 1, 1><<<nwg, 512, 0, s>>>(p);
-            else if (rs == 0 && use_pb2()) attn_pb2_kernel<bf16_t, 1><<<nwg, 512, 0, s>>>(p);
+            else if (rs == 0 && use_pb2() && pb2_rs16()) attn_pb2_kernel<bf16_t, 1, 3><<<nwg, 512, 0, s>>>(p);
+            else if (rs == 0 && use_pb2()) attn_pb2_kernel<bf16_t, 1, 0><<<nwg, 512, 0, s>>>(p);
             else if (pp_occ() == 2) PB_LAUNCH(2);
             else PB_LAUNCH(1);
 #undef PB_LAUNCH

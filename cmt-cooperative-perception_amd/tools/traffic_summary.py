@@ -50,8 +50,10 @@ def main():
         w = statistics.median(write.get(k, [0])) * 1024
         res["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "launches": len(fetch.get(k, []))}
     if match is None:
-        # the bounded bf16 core (attn_pb_kernel) or the ping-pong core (attn_pp_kernel), + its split combine
-        core = "attn_pb_kernel" if any("attn_pb_kernel" in k for k in res["kernels"]) else "attn_pp_kernel"
+        # the bounded bf16 core (attn_pb2_kernel paired-tile / attn_pb_kernel) or the ping-pong core
+        # (attn_pp_kernel), + its split combine
+        core = next((c for c in ("attn_pb2_kernel", "attn_pb_kernel")
+                     if any(c in k for k in res["kernels"])), "attn_pp_kernel")
         match = res["match"] = [core, "attn_combine_kernel<8>"]
     parts = {}
     for m in match:

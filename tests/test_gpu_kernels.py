@@ -237,7 +237,8 @@ def test_attention_pb2_matches_pb(N, dev, monkeypatch, B, Nq, Nk, splits, scale_
     pb kernel on the same inputs: bit-identical on the offset-free path (same
     per-score math, same tile order of the PV / row-sum accumulation), with odd
     full-tile counts per split, a ragged last tile and 1-5 splits; with large |q|
-    (online-max fallback, one offset update per pair) within 1e-2 of it."""
+    (online-max fallback, one offset update per pair) within 1e-2 of it.  The
+    16x16x32 row-sum form (CMT_ATTN_RS16, the default) against the 32x32x16 one."""
     H = 8
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(Nk + Nq)
@@ -250,8 +251,9 @@ def test_attention_pb2_matches_pb(N, dev, monkeypatch, B, Nq, Nk, splits, scale_
     kmax2 = km.float().contiguous().to(dev)
     k = k.to(dev)
     outs = []
-    for pb2 in ("1", "0"):
+    for pb2, rs16 in (("1", "0"), ("0", "0"), ("1", "1")):
         monkeypatch.setenv("CMT_ATTN_PB2", pb2)
+        monkeypatch.setenv("CMT_ATTN_RS16", rs16)
         O = torch.empty(B, Nq, H * 32, device=dev)
         N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk,
                     q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
@@ -259,11 +261,15 @@ def test_attention_pb2_matches_pb(N, dev, monkeypatch, B, Nq, Nk, splits, scale_
                     kv_splits=splits, fold_scale=True, kmax2=kmax2, kmax_ld=H, kmax_plane0=0)
         torch.cuda.synchronize()
         outs.append(O.cpu())
-    assert torch.isfinite(outs[0]).all()
+    assert torch.isfinite(outs[0]).all() and torch.isfinite(outs[2]).all()
     if scale_q == 1.0:
         assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
     else:
         assert (outs[0] - outs[1]).abs().max().item() < 1e-2
+    # row sums on the 16x16x32 MFMA: same products, another f32 summation order
+    rel = ((outs[2] - outs[0]).abs() / (outs[0].abs() + 1e-3)).max().item()
+    print(f"pb2 16x16x32 row sums vs 32x32x16: max rel {rel:.2e}")
+    assert rel < 1e-4, rel
 
 
 def test_gemm_dma_conv1d3_lowp(N, dev):
