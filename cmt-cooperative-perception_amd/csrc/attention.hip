@@ -440,6 +440,136 @@ __global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : (NWAVES == 8 ? 2 : 2)) 
 }
 
 // ---------------------------------------------------------------------------
+// Short key ranges (the decoder's self-attention, Nk = Nq = 900): one
+// workgroup = KW waves on the SAME 32 queries of one (batch, head); wave w
+// takes key tiles w, w + KW, ... through a private two-slot LDS ring (LDS-DMA,
+// 8 pieces per tile, counted waits, no workgroup barrier in the loop), and the
+// KW partial (O, row sum, offset) triples merge through LDS at the end.  No
+// split partials in HBM and no combine launch: a 900 x 900 problem is 29 x H
+// workgroups of KW waves, each wave ~ntiles / KW tiles deep.
+// ---------------------------------------------------------------------------
+constexpr int KWR = 2;      // ring slots per wave
+constexpr int KWO = 36;     // merge image row stride (floats): 16-byte aligned rows
+
+template <typename T, bool FOLD, int KW>
+__global__ __launch_bounds__(KW * 64) void attn_kw_kernel(AttnKParams p) {
+    typedef typename mfma_traits<T>::frag frag;
+    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
+    __shared__ __attribute__((aligned(16))) T ring[KW * KWR * STAGE];
+    __shared__ float xm[KW][QW], xl[KW][QW];
+    static_assert(KWR * STAGE * (int)sizeof(T) >= QW * KWO * (int)sizeof(float), "merge image fits a wave's ring");
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    const int bh = blockIdx.y;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+    const float c = p.c;
+
+    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+
+    const int ntiles = (p.Nk + KT - 1) / KT;
+    const int my_n = wave < ntiles ? (ntiles - 1 - wave) / KW + 1 : 0;   // tiles wave, wave + KW, ...
+    const bool ragged = (p.Nk % KT) != 0;
+    T* const myring = ring + wave * KWR * STAGE;
+
+    const int crow = lane >> 2, cch = lane & 3;
+    auto issue = [&](int slot, int t) {   // the whole 64-key tile t by this wave: 4 K + 4 V pieces
+        T* st = myring + slot * STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = i * 16 + crow;
+            const int key = min(t * KT + row, p.Nk - 1);   // ragged tail: clamped, masked in compute
+            dma16(Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((row >> 2) & 3)), st + i * 16 * D);
+            dma16(Vb + (int64_t)key * p.v_rs + 8 * cch, st + KT * D + i * 16 * D);
+        }
+    };
+    if (my_n > 0) issue(0, wave);
+    if (my_n > 1) issue(1, wave + KW);
+
+    const int q = blockIdx.x * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    frag qf[2];
+    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+    if (FOLD) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
+    }
+
+    f32x16 o, lsum, negm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o[r] = 0.f;
+        lsum[r] = 0.f;
+        negm[r] = 0.f;
+    }
+    float m_run = 0.f;
+    for (int i = 0; i < my_n; ++i) {
+        // tile i landed (the Q loads above are older: in-order completion covers them)
+        if (i + 1 < my_n) wait_vm_lgkm<8>();
+        else wait_vm_lgkm<0>();
+        const T* Kt = myring + (i & 1) * STAGE;
+        const T* Vt = Kt + KT * D;
+        const int t = wave + i * KW;
+        if (ragged && t == ntiles - 1)
+            attn_tile_lowp<T, true, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, i == 0, c, t * KT, p.Nk, lane);
+        else
+            attn_tile_lowp<T, false, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, i == 0, c, t * KT, p.Nk, lane);
+        if (i + 2 < my_n) {
+            wait_vm_lgkm<0>();   // the slot's ds_reads are done (lgkmcnt) before the DMA overwrites it
+            issue(i & 1, wave + (i + 2) * KW);
+        }
+    }
+
+    // ---- merge the KW partials through LDS (each wave's own ring region holds its O^T image)
+    wait_vm_lgkm<0>();
+    float* xo = (float*)myring;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+        *(f32x4*)(xo + lr * KWO + 8 * g + 4 * lh) = v;
+    }
+    if (lh == 0) {
+        xm[wave][lr] = my_n > 0 ? (FOLD ? m_run : m_run * c) : -__builtin_inff();   // exp2 units
+        xl[wave][lr] = lsum[0];
+    }
+    barrier_mem();
+    if (tid < QW * 8) {
+        const int mq = tid >> 3, d0 = 4 * (tid & 7);
+        const int qo = blockIdx.x * QW + mq;
+        if (qo < p.Nq) {
+            float M = xm[0][mq];
+#pragma unroll
+            for (int w = 1; w < KW; ++w) M = vmax(M, xm[w][mq]);
+            float L = 0.f;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int w = 0; w < KW; ++w) {
+                const float sc = __builtin_amdgcn_exp2f(xm[w][mq] - M);   // -inf -> 0 (waves without tiles)
+                L += xl[w][mq] * sc;
+                const f32x4 v = *(const f32x4*)((const float*)(ring + w * KWR * STAGE) + mq * KWO + d0);
+                acc += v * sc;
+            }
+            const float inv = 1.f / L;
+            f32x4 v = acc * inv;
+            if (p.round_out) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
+            }
+            store_o4(p, b, qo, h * D + d0, v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Ping-pong kernel for long key ranges (the cross-attention shape), f16/bf16.
 //
 // 8 waves = two halves of 4 (wave w sits on SIMD w % 4, so every SIMD holds
@@ -1849,8 +1979,20 @@ void stamp_report(const AttnKParams& p, unsigned nwg, hipStream_t s) {
             loop / nw, tot / nw, t1 - t0, e_max - t0);
 }
 
+// short key ranges (self-attention): the in-workgroup key split (attn_kw_kernel) with KW waves;
+// CMT_ATTN_KW=0 selects the split-partials + combine path, 4 / 8 the wave count (default 8)
+int kw_waves(const cmt_attn_args& a) {
+    const char* ov = getenv("CMT_ATTN_KW");   // read per call: the tests toggle it in one process
+    if (ov && ov[0] == '0') return 0;
+    if (a.dtype == CMT_F32 || a.kv_splits > 0 || use_pp(a)) return 0;
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    if (ntiles > 64) return 0;
+    return (ov && ov[0] == '4') ? 4 : 8;
+}
+
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
+    if (kw_waves(a) > 0) return 1;
     const int ntiles = (a.Nk + KT - 1) / KT;
     const LowpShape sh = lowp_shape(a);
     const int nw = a.dtype == CMT_F32 ? NW : sh.waves;
@@ -1944,8 +2086,24 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
             else attn_fwd_kernel<T, 4, false, 1><<<grid, 256, 0, s>>>(p);                                \
         }                                                                                                \
     } while (0)
+    const int kw = kw_waves(a);
     if (a.dtype == CMT_F32) {
         attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
+    } else if (kw > 0) {
+        const dim3 g2(cdiv(a.Nq, QW), a.B * a.H);
+#define KW_LAUNCH(T)                                                                                     \
+    do {                                                                                                 \
+        if (kw == 4) {                                                                                   \
+            if (fold) attn_kw_kernel<T, true, 4><<<g2, 256, 0, s>>>(p);                                  \
+            else attn_kw_kernel<T, false, 4><<<g2, 256, 0, s>>>(p);                                      \
+        } else {                                                                                         \
+            if (fold) attn_kw_kernel<T, true, 8><<<g2, 512, 0, s>>>(p);                                  \
+            else attn_kw_kernel<T, false, 8><<<g2, 512, 0, s>>>(p);                                      \
+        }                                                                                                \
+    } while (0)
+        if (a.dtype == CMT_F16) KW_LAUNCH(f16_t);
+        else KW_LAUNCH(bf16_t);
+#undef KW_LAUNCH
     } else if (use_pp(a)) {
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
         if (use_pb(a)) {

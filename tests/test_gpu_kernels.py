@@ -358,6 +358,48 @@ def test_attention(N, dev, dt, B, H, Nq, Nk, splits, fold):
     assert err < tol, err
 
 
+@pytest.mark.parametrize("kw", ["4", "8"])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,H,Nq,Nk,mode", [(1, 8, 900, 900, "rand"), (2, 3, 70, 65, "rand"), (1, 1, 5, 1, "rand"),
+                                            (1, 2, 40, 4096, "rand"), (1, 1, 33, 700, "spike"),
+                                            (1, 2, 70, 200, "negative")])
+def test_attention_key_split_workgroup(N, dev, monkeypatch, kw, dt, B, H, Nq, Nk, mode):
+    """Short key ranges (self-attention): KW waves of one workgroup split the
+    keys of the same 32 queries and merge (O, row sum, offset) through LDS.
+    Fewer tiles than waves (waves without keys), a ragged last tile, 64 tiles,
+    a late spike (the merge's max comes from a later wave than the first), all
+    scores ~ -200 exp2 units (no underflow in the merge); both scale folds;
+    against float64 and against the split-partials + combine path."""
+    g = torch.Generator().manual_seed(Nk * 7 + Nq)
+    if mode == "negative":
+        q = (5 + 0.1 * torch.randn(B, H, Nq, 32, generator=g)).to(dt)
+        k = (-5 + 0.1 * torch.randn(B, H, Nk, 32, generator=g)).to(dt)
+    else:
+        q = (torch.randn(B, H, Nq, 32, generator=g) * 1.5).to(dt)
+        k = (torch.randn(B, H, Nk, 32, generator=g) * (0.1 if mode == "spike" else 1.5)).to(dt)
+    if mode == "spike":
+        k[0, 0, 650] = q[0, 0, 5] * 4            # query 5's max sits in the last (ragged) tile
+    v = torch.randn(B, H, Nk, 32, generator=g).to(dt)
+    ref = _attn_ref(q, k, v, 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
+    qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
+    for fold in (False, True):
+        outs = []
+        for sel in (kw, "0"):
+            monkeypatch.setenv("CMT_ATTN_KW", sel)
+            O = torch.full((B, Nq, H * 32), float("nan"), device=dev)
+            N.attention(qd, kd, vd, O, B=B, H=H, Nq=Nq, Nk=Nk,
+                        q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                        v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32),
+                        scale=1 / math.sqrt(32), fold_scale=fold)
+            torch.cuda.synchronize()
+            outs.append(O.cpu().double())
+        assert torch.isfinite(outs[0]).all()
+        err = (outs[0] - ref).abs().max().item()
+        tol = {torch.float16: 3e-3, torch.bfloat16: 2e-2}[dt] * (10 if mode == "negative" else 1)
+        assert err < tol, (fold, err)
+        assert (outs[0] - outs[1]).abs().max().item() < tol
+
+
 def test_attention_spike_rescale(N, dev):
     """Force the online-softmax running max to jump late (rule 26)."""
     B, H, Nq, Nk = 1, 1, 64, 2048
