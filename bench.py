@@ -347,6 +347,9 @@ def main():
                 "matrices, random-init weights of the head)",
         "config": {"workload": w["desc"], "global_batch": world, "seq_len": sum(nks), "num_query": nq,
                    "parallelism": f"dp{world}", "graph": not args.no_graph,
+                   # pos2embed(BEV grid) + bev_embedding[0] is a function of the weights only: built
+                   # once per weight version like the packed weights (CMT_BEV_POS_CACHE=0: per frame)
+                   "bev_pos_hidden_cached": os.environ.get("CMT_BEV_POS_CACHE", "1") != "0",
                    "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nq=nq, nk=nk) for nk in nks) / 1e9, 2)},
         "roofline": {"kernel": "cmt_attn_fwd (cross-attention core + split combine)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

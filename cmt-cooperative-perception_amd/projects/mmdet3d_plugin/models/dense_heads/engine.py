@@ -134,10 +134,23 @@ class HeadEngineMixin:
         if x_size * y_size != H * W:
             raise ValueError(f"BEV map {H}x{W} does not match grid_size/downsample ({x_size}x{y_size})")
         w0, b0, _, _ = pk["bev"]
-        pe = torch.empty((H * W, 2 * C), dtype=w0.dtype, device=w0.device)
-        native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
-        hdt = pe.dtype if pe.dtype == w0.dtype else torch.float32
-        return native.linear(pe, w0, b0, relu=True, out_dtype=hdt)
+
+        def build():
+            pe = torch.empty((H * W, 2 * C), dtype=w0.dtype, device=w0.device)
+            native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
+            hdt = pe.dtype if pe.dtype == w0.dtype else torch.float32
+            return native.linear(pe, w0, b0, relu=True, out_dtype=hdt)
+        # A function of the weights and the grid only: kept like a weight pack (rebuilt when
+        # bev_embedding[0] changes, Tensor._version / storage tracked) unless CMT_BEV_POS_CACHE=0.
+        # Never built inside a graph capture (its buffer must outlive the graph).
+        if os.environ.get("CMT_BEV_POS_CACHE", "1") == "0":
+            return build()
+        key = (H, W, x_size, y_size, str(w0.dtype))
+        name = f"bev_hidden_{H}x{W}_{w0.dtype}"
+        src = [self.bev_embedding[0].weight, self.bev_embedding[0].bias]   # the parameters themselves
+        if torch.cuda.is_current_stream_capturing() and not self._pack.has(name, src, key):
+            return build()
+        return self._pack.get(name, src, key, build)
 
     def _bev_pos_out(self, hid, pos, B, Nk, pk, R=None):
         """Second half: bev_embedding[2] into the pos rows of every batch

@@ -26,6 +26,10 @@ class PackCache:
         self._store[name] = (k, val)
         return val
 
+    def has(self, name, tensors, extra):
+        hit = self._store.get(name)
+        return hit is not None and hit[0] == _key(tensors, extra)
+
     def clear(self):
         self._store.clear()
 

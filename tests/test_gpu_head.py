@@ -265,3 +265,42 @@ def test_second_stream_matches_single_stream(dev, warm, monkeypatch):
     for k in KEYS:
         assert torch.isfinite(one[k]).all(), k
         assert torch.equal(one[k], two[k]), (k, (one[k] - two[k]).abs().max().item())
+
+
+def test_bev_pos_hidden_cache(dev, monkeypatch):
+    """The input-independent first half of the BEV position MLP (pos2embed of
+    the grid + bev_embedding[0] + ReLU) is kept like a weight pack: a forward
+    that reuses it equals one that recomputes it (CMT_BEV_POS_CACHE=0)
+    bit-exactly, and an in-place change of bev_embedding[0] (an optimizer step)
+    rebuilds it."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=5, num_query=64, num_layers=2,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=41).to(dev)
+    xi = S.synthetic_img(6, 8, 20, seed=42).to(dev)
+    metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=43)
+
+    def run(cache):
+        monkeypatch.setenv("CMT_BEV_POS_CACHE", cache)
+        with torch.no_grad():
+            out = head([x], [xi], metas)[0][0]
+        torch.cuda.synchronize()
+        return {k: v.clone() for k, v in out.items()}
+
+    set_precision("bf16")
+    try:
+        run("1")                      # builds the cached hidden rows
+        cached = run("1")             # reuses them
+        fresh = run("0")
+        for k in KEYS:
+            assert torch.equal(cached[k], fresh[k]), k
+        with torch.no_grad():
+            head.bev_embedding[0].weight.mul_(1.5)
+        changed = run("1")
+        fresh2 = run("0")
+    finally:
+        set_precision("ref")
+    for k in KEYS:
+        assert torch.equal(changed[k], fresh2[k]), k
+    assert not torch.equal(changed["cls_logits"], cached["cls_logits"])
