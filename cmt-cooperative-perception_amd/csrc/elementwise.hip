@@ -203,10 +203,11 @@ __global__ void rv_pe_coords_kernel(int BV, int H, int W, int D, float pad_h, fl
 }
 
 // _rv_query_embed geometry (cmt_head.py:446-463): one thread per (b, v, q, depth).
+template <typename TO>
 __global__ void rv_query_coords_kernel(const float* __restrict__ ref, int B, int V, int Nq, int D,
                                        float pad_h, float pad_w, float dstep,
                                        const float* __restrict__ l2i, const float* __restrict__ i2l,
-                                       PcRange pc, float* out, float* mask) {
+                                       PcRange pc, TO* out, float* mask) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)B * V * Nq * D;
     if (idx >= total) return;
@@ -240,14 +241,14 @@ __global__ void rv_query_coords_kernel(const float* __restrict__ ref, int B, int
     const float d = 1.f + (float)k * dstep / (float)D;
     const float c4[4] = {px * d, py * d, pz * d, 1.f};
     const float* M = i2l + bv * 16;
-    float* o = out + bvq * (3 * D) + 3 * k;
+    TO* o = out + bvq * (3 * D) + 3 * k;
 #pragma unroll
     for (int rr = 0; rr < 3; ++rr) {
         float a = M[rr * 4 + 0] * c4[0];
         a = fmaf(M[rr * 4 + 1], c4[1], a);
         a = fmaf(M[rr * 4 + 2], c4[2], a);
         a = fmaf(M[rr * 4 + 3], c4[3], a);
-        o[rr] = (a - pc.v[rr]) / (pc.v[3 + rr] - pc.v[rr]);
+        o[rr] = (TO)((a - pc.v[rr]) / (pc.v[3 + rr] - pc.v[rr]));   // RNE, as cmt_cast
     }
 }
 
@@ -266,6 +267,29 @@ __global__ void masked_view_sum_kernel(const float* __restrict__ X, const float*
         s += X[bvq * C + c] * mask[bvq];
     }
     Y[idx] += s;
+}
+
+// Y[b,q,:] = base[q,:] + sum_v X[b,v,q,:] * mask[b,v,q]  (base NULL: Y += ...), and, when
+// given, the decoder's first operands Yp = lowp(Y) (= lowp(0 + query_pos)) and Yl = lowp(0).
+template <typename TL>
+__global__ void masked_view_sum_ex_kernel(const float* __restrict__ X, const float* __restrict__ mask, int B, int V,
+                                          int Nq, int C, const float* __restrict__ base, float* Y, TL* Yl, TL* Yp) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)B * Nq * C;
+    if (idx >= total) return;
+    const int c = (int)(idx % C);
+    const int64_t bq = idx / C;
+    const int q = (int)(bq % Nq);
+    const int b = (int)(bq / Nq);
+    float s = 0.f;
+    for (int v = 0; v < V; ++v) {
+        const int64_t bvq = ((int64_t)b * V + v) * Nq + q;
+        s += X[bvq * C + c] * mask[bvq];
+    }
+    const float y = (base ? base[(int64_t)q * C + c] : Y[idx]) + s;
+    Y[idx] = y;
+    if (Yp) Yp[idx] = (TL)y;
+    if (Yl) Yl[idx] = (TL)0.f;
 }
 
 // ---------------------------------------------------------------------------
@@ -597,9 +621,32 @@ extern "C" int cmt_rv_query_coords(const float* ref, int B, int V, int Nq, int D
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
     const int64_t total = (int64_t)B * V * Nq * D;
-    rv_query_coords_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(
+    rv_query_coords_kernel<float><<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(
         ref, B, V, Nq, D, pad_h, pad_w, pc.v[3] - 1.f, l2i, i2l, pc, out, mask);
     return cmt_check_launch("cmt_rv_query_coords");
+}
+
+extern "C" int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, int D, float pad_h, float pad_w,
+                                      const float* l2i, const float* i2l, const float* pc_range6, void* out,
+                                      int odtype, float* mask, void* stream) {
+    CMT_REQUIRE(ref && l2i && i2l && pc_range6 && out && mask && B > 0 && V > 0 && Nq > 0 && D > 0,
+                "cmt_rv_query_coords_ex: bad arguments");
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_rv_query_coords_ex: bad odtype");
+    PcRange pc;
+    for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
+    const int64_t total = (int64_t)B * V * Nq * D;
+    hipStream_t s = (hipStream_t)stream;
+    if (odtype == CMT_F32)
+        rv_query_coords_kernel<float><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
+                                                                          pc.v[3] - 1.f, l2i, i2l, pc, (float*)out, mask);
+    else if (odtype == CMT_F16)
+        rv_query_coords_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
+                                                                          pc.v[3] - 1.f, l2i, i2l, pc, (f16_t*)out, mask);
+    else
+        rv_query_coords_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
+                                                                           pc.v[3] - 1.f, l2i, i2l, pc, (bf16_t*)out,
+                                                                           mask);
+    return cmt_check_launch("cmt_rv_query_coords_ex");
 }
 
 extern "C" int cmt_masked_view_sum(const float* X, const float* mask, int B, int V, int Nq, int C, float* Y,
@@ -608,6 +655,22 @@ extern "C" int cmt_masked_view_sum(const float* X, const float* mask, int B, int
     const int64_t total = (int64_t)B * Nq * C;
     masked_view_sum_kernel<<<nblocks(total, 256), 256, 0, (hipStream_t)stream>>>(X, mask, B, V, Nq, C, Y);
     return cmt_check_launch("cmt_masked_view_sum");
+}
+
+extern "C" int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int Nq, int C,
+                                      const float* base, float* Y, void* Yl, void* Yp, int lowp_dtype, void* stream) {
+    CMT_REQUIRE(X && mask && Y && B > 0 && V > 0 && Nq > 0 && C > 0, "cmt_masked_view_sum_ex: bad arguments");
+    CMT_REQUIRE((!Yl && !Yp) || lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16,
+                "cmt_masked_view_sum_ex: lowp_dtype must be f16 or bf16");
+    const int64_t total = (int64_t)B * Nq * C;
+    hipStream_t s = (hipStream_t)stream;
+    if (lowp_dtype == CMT_F16)
+        masked_view_sum_ex_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
+                                                                             (f16_t*)Yl, (f16_t*)Yp);
+    else
+        masked_view_sum_ex_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
+                                                                              (bf16_t*)Yl, (bf16_t*)Yp);
+    return cmt_check_launch("cmt_masked_view_sum_ex");
 }
 
 extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype, int64_t ldy,

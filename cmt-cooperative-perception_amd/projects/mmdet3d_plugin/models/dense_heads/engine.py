@@ -203,35 +203,65 @@ class HeadEngineMixin:
     def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None, cams=None):
         self._rv_pe_out(self._rv_pe_hidden(x_img, metas, B, pk, cams=cams), pos, B, Nk, offset, pk, R=R)
 
-    def _query_pos(self, B, metas, with_rv, pk, cams=None):
+    def _query_bev_pos(self, pk):
+        """bev_embedding(pos2embed(sigmoid(inverse_sigmoid(reference_points))))
+        (cmt_head.py:469-473): [Nq, C] fp32, a function of the weights only --
+        kept like a weight pack (reference_points and bev_embedding tracked),
+        never built inside a graph capture; CMT_BEV_POS_CACHE=0 recomputes it."""
+        C = self.hidden_dim
+        ref = self.reference_points.weight.detach().contiguous()
+        Nq = ref.shape[0]
+
+        def build():
+            pe = torch.empty((Nq, 2 * C), dtype=pk["bev"][0].dtype, device=ref.device)
+            native.pos2embed(ref, pe, n=Nq, F=C, mode=1, pos_stride=3)
+            qb = torch.empty((Nq, C), dtype=torch.float32, device=ref.device)
+            self._mlp(pe, pk["bev"], qb, M=Nq)
+            return qb
+        if os.environ.get("CMT_BEV_POS_CACHE", "1") == "0":
+            return build()
+        be = self.bev_embedding
+        src = [self.reference_points.weight, be[0].weight, be[0].bias, be[2].weight, be[2].bias]
+        key = str(pk["bev"][0].dtype)
+        name = f"query_bev_pos_{key}"
+        if torch.cuda.is_current_stream_capturing() and not self._pack.has(name, src, key):
+            return build()
+        return self._pack.get(name, src, key, build)
+
+    def _query_pos(self, B, metas, with_rv, pk, cams=None, first_ops=None):
+        """query_embed (+ _rv_query_embed) -> [B*Nq, C] fp32.  ``first_ops``
+        (tl, tp) f16/bf16 [B*Nq, C]: with the RV term the final sum also writes
+        the decoder's first operands lowp(0) and lowp(0 + query_pos) (the
+        add_cast of layer 0); returns (qpos, written)."""
         C = self.hidden_dim
         ref = self.reference_points.weight.detach().contiguous()
         Nq = ref.shape[0]
         dev = ref.device
-        pe = torch.empty((Nq, 2 * C), dtype=pk["bev"][0].dtype, device=dev)
-        native.pos2embed(ref, pe, n=Nq, F=C, mode=1, pos_stride=3)
+        qb = self._query_bev_pos(pk)
+        if not with_rv:
+            return qb.repeat(B, 1), False
         qpos = torch.empty((B * Nq, C), dtype=torch.float32, device=dev)
-        self._mlp(pe, pk["bev"], qpos, batch=B, a_bstride=0, c_bstride=Nq * C, M=Nq)
-        if with_rv:
-            V = len(metas[0]["lidar2img"])
-            pad_h, pad_w, _ = metas[0]["pad_shape"][0]
-            l2i, i2l = cams if cams is not None else self._cams(metas, dev)
-            refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
-            D = self.depth_num
-            coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)   # kernel writes fp32
-            mask = torch.empty((B * V * Nq,), dtype=torch.float32, device=dev)
+        V = len(metas[0]["lidar2img"])
+        pad_h, pad_w, _ = metas[0]["pad_shape"][0]
+        l2i, i2l = cams if cams is not None else self._cams(metas, dev)
+        refB = ref.unsqueeze(0).expand(B, Nq, 3).contiguous()
+        D = self.depth_num
+        mask = torch.empty((B * V * Nq,), dtype=torch.float32, device=dev)
+        w0 = pk["rv"][0]
+        if w0.dtype != torch.float32 and (3 * D) % 64 == 0:
+            # compute-dtype operand written by the geometry kernel (the same RNE rounding the
+            # GEMM would apply on load): both MLP GEMMs then run on the LDS-DMA path
+            coords = torch.empty((B * V * Nq, 3 * D), dtype=w0.dtype, device=dev)
+            native.rv_query_coords_lowp(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
+                                        pad_w=float(pad_w), pc_range=self.pc_range)
+        else:
+            coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)
             native.rv_query_coords(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
                                    pad_w=float(pad_w), pc_range=self.pc_range)
-            w0 = pk["rv"][0]
-            if w0.dtype != torch.float32 and (3 * D) % 64 == 0:
-                # compute-dtype operand (the same RNE rounding the GEMM would apply on load):
-                # both MLP GEMMs then run on the LDS-DMA path
-                c16 = torch.empty(coords.shape, dtype=w0.dtype, device=dev)
-                native.cast(coords, c16)
-                coords = c16
-            r = self._mlp(coords, pk["rv"])
-            native.masked_view_sum(r, mask, qpos, B=B, V=V, Nq=Nq, C=C)
-        return qpos
+        r = self._mlp(coords, pk["rv"])
+        tl, tp = first_ops if first_ops is not None else (None, None)
+        native.masked_view_sum(r, mask, qpos, B=B, V=V, Nq=Nq, C=C, base=qb, Yl=tl, Yp=tp)
+        return qpos, first_ops is not None
 
     # ------------------------------------------------------------------ per agent
     def _decode_agent(self, x, x_img, metas, B, out, post_flags, variant, prec, out16=None):
@@ -287,8 +317,9 @@ class HeadEngineMixin:
                                         rows_per_batch=Nk, row_offset=HW)
                     hr = self._rv_pe_hidden(x_img, metas, B, pk, cams=cams)
                 ready.record(side)
-                qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
-                dec.lowp_layer0(state, qpos, B=B, Nq=Nq, prec=prec)
+                qpos, firsts = self._query_pos(B, metas, use_img, pk, cams=cams,
+                                               first_ops=(state["tl"], state["tp"]))
+                dec.lowp_layer0(state, qpos, B=B, Nq=Nq, prec=prec, first_ops_ready=firsts)
             for t in (qpos, hb, hr):
                 if t is not None:
                     t.record_stream(main)
@@ -308,7 +339,7 @@ class HeadEngineMixin:
                                     rows_per_batch=Nk, row_offset=HW)
                 self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R, cams=cams)
         if side is None:
-            qpos = self._query_pos(B, metas, use_img, pk, cams=cams)
+            qpos, _ = self._query_pos(B, metas, use_img, pk, cams=cams)
         dec.run_rows(mem, pos, qpos, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
                      kv_operands=(mem, pos) if lowp else None, out16=out16 if lowp else None, state=state)
         return out

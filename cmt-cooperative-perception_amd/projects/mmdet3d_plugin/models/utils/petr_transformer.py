@@ -529,7 +529,7 @@ class PETRTransformerDecoder(nn.Module):
             cws=torch.empty(native.chain_ws_numel(rows), dtype=torch.float32, device=device),
             layer0_done=False, stream=None)
 
-    def lowp_layer0(self, st, qpos, *, B, Nq, prec):
+    def lowp_layer0(self, st, qpos, *, B, Nq, prec, first_ops_ready=False):
         """Layer 0 up to the cross-attention core on the chain path: the zero
         target's operands (add_cast), the self-attention in_proj, the
         self-attention core and chain A (out_proj + norms[0] + cross Q
@@ -542,7 +542,8 @@ class PETRTransformerDecoder(nn.Module):
         ch = self._chain_pack(prec)
         C, H, rows = self.embed_dims, self.embed_dims // 32, B * Nq
         l0 = pk["layers"][0]
-        native.add_cast(None, rows=rows, C=C, Yl=st["tl"], Yp=st["tp"], P=qpos)
+        if not first_ops_ready:   # else written by the query embedding's last kernel (masked_view_sum_ex)
+            native.add_cast(None, rows=rows, C=C, Yl=st["tl"], Yp=st["tp"], P=qpos)
         native.gemm(st["tl"], l0["sa_w"], st["qkv"], M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
                     A2=st["tp"], lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
         self._self_attn(st, B=B, H=H, Nq=Nq, C=C)

@@ -25,7 +25,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -160,6 +160,9 @@ def _load():
         "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _int, _vp], _int),
         "cmt_rv_query_coords": ([_vp, _int, _int, _int, _int, _flt, _flt, _vp, _vp, P(_flt), _vp, _vp, _vp], _int),
         "cmt_masked_view_sum": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp], _int),
+        "cmt_rv_query_coords_ex": ([_vp, _int, _int, _int, _int, _flt, _flt, _vp, _vp, P(_flt), _vp, _int, _vp, _vp],
+                                   _int),
+        "cmt_masked_view_sum_ex": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _int, _vp], _int),
         "cmt_nchw_to_rows": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp], _int),
         "cmt_cast": ([_vp, _int, _vp, _int, _i64, _vp], _int),
         "cmt_task_head_tail": ([_vp, _int, _int, _int, _int, _int, _vp, _vp, _vp, _vp, P(_int), _int, _int, _vp,
@@ -527,9 +530,24 @@ def rv_query_coords(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w, pc_r
                                      _p(out), _p(mask), _stream()), "cmt_rv_query_coords")
 
 
-def masked_view_sum(X, mask, Y, *, B, V, Nq, C):
-    _dev(X, mask, Y)
-    _check(lib().cmt_masked_view_sum(_p(X), _p(mask), B, V, Nq, C, _p(Y), _stream()), "cmt_masked_view_sum")
+def masked_view_sum(X, mask, Y, *, B, V, Nq, C, base=None, Yl=None, Yp=None):
+    """Y += sum_v X * mask; with ``base`` [Nq, C]: Y = base + sum; Yp / Yl (f16/bf16):
+    lowp(Y) and lowp(0) -- the decoder's first operands."""
+    _dev(X, mask, Y, base, Yl, Yp)
+    if base is None and Yl is None and Yp is None:
+        _check(lib().cmt_masked_view_sum(_p(X), _p(mask), B, V, Nq, C, _p(Y), _stream()), "cmt_masked_view_sum")
+        return
+    low = Yp if Yp is not None else Yl
+    _check(lib().cmt_masked_view_sum_ex(_p(X), _p(mask), B, V, Nq, C, _p(base), _p(Y), _p(Yl), _p(Yp),
+                                        DT[low.dtype] if low is not None else 0, _stream()),
+           "cmt_masked_view_sum_ex")
+
+
+def rv_query_coords_lowp(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w, pc_range):
+    """cmt_rv_query_coords with the coordinates written in out's dtype (RNE)."""
+    _dev(ref, l2i, i2l, out, mask)
+    _check(lib().cmt_rv_query_coords_ex(_p(ref), B, V, Nq, D, pad_h, pad_w, _p(l2i), _p(i2l), _farr(pc_range, 6),
+                                        _p(out), DT[out.dtype], _p(mask), _stream()), "cmt_rv_query_coords_ex")
 
 
 def nchw_to_rows(X, Y, *, nb, nv, C, HW, ldy, rows_per_batch, row_offset=0):

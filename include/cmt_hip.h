@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 10
+#define CMT_ABI_VERSION 11
 
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2 };
 
@@ -288,6 +288,12 @@ int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype
  *   l2i / i2l [B,V,4,4] fp32 -> out [B,V,Nq,3*D], mask [B,V,Nq] fp32 {0,1}.
  * cmt_masked_view_sum: (rv * mask).sum(dim=1) (cmt_head.py:466) added into Y:
  *   Y[b,q,:] += sum_v X[b,v,q,:] * mask[b,v,q].
+ * cmt_rv_query_coords_ex (ABI 11): cmt_rv_query_coords with out in odtype
+ *   (f16/bf16 rounded RNE: the operand of the rv_embedding GEMM without a cast pass).
+ * cmt_masked_view_sum_ex (ABI 11): Y[b,q,:] = base[q,:] + sum_v ... (base [Nq,C]
+ *   fp32, the BEV half of query_pos shared by every batch element; NULL: Y += ...),
+ *   and optionally the decoder's first operands Yp = lowp(Y) = lowp(0 + query_pos)
+ *   and Yl = lowp(0) (the zero target, cmt_transformer.py:114) in lowp_dtype.
  * ------------------------------------------------------------------------ */
 int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F, int mode,
                   int grid_h, int grid_w, void* out, int odtype, int64_t ldo, void* stream);
@@ -298,6 +304,11 @@ int cmt_rv_query_coords(const float* ref, int B, int V, int Nq, int D, float pad
                         float* out, float* mask, void* stream);
 int cmt_masked_view_sum(const float* X, const float* mask, int B, int V, int Nq, int C,
                         float* Y, void* stream);
+int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, int D, float pad_h, float pad_w,
+                           const float* l2i, const float* i2l, const float* pc_range6,
+                           void* out, int odtype, float* mask, void* stream);
+int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int Nq, int C,
+                           const float* base, float* Y, void* Yl, void* Yp, int lowp_dtype, void* stream);
 
 /* ------------------------------------------------------------------------
  * Layout / dtype plumbing.
