@@ -105,26 +105,6 @@ __global__ __launch_bounds__(256) void add_cast_kernel(const float* __restrict__
     }
 }
 
-// Y[b, i, :] = lowp(A[i, :] + (bias + R[b, i, :])) -- the epilogue of a GEMM with bias and
-// residual (gemm.hip: acc += bias + r) applied to a precomputed accumulator A shared by every
-// batch element (the BEV position MLP's bev_embedding[2] product, a function of the weights).
-template <typename T>
-__global__ __launch_bounds__(256) void acc_bias_res_kernel(const float* __restrict__ A, const float* __restrict__ bias,
-                                                           const T* __restrict__ R, T* Y, int64_t n4, int C4,
-                                                           int64_t bstride) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n4) return;
-    const int b = blockIdx.y;
-    typedef T t4 __attribute__((ext_vector_type(4)));
-    const f32x4 a = ((const f32x4*)A)[i];
-    const f32x4 bv = ((const f32x4*)bias)[i % C4];
-    const t4 r = *(const t4*)(R + b * bstride + 4 * i);
-    f32x4 y;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = a[j] + (bv[j] + (float)r[j]);
-    *(t4*)(Y + b * bstride + 4 * i) = t4{(T)y[0], (T)y[1], (T)y[2], (T)y[3]};
-}
-
 // ---------------------------------------------------------------------------
 // pos2embed (cmt_head.py:40-50), optionally fused with coords_bev (324-337) or
 // with sigmoid(inverse_sigmoid(.)) of the query reference points (470).
@@ -589,22 +569,6 @@ extern "C" int cmt_add_cast(const float* X, const float* P, int rows, int C, int
     else
         add_cast_kernel<bf16_t><<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, (bf16_t*)Yl, (bf16_t*)Yp);
     return cmt_check_launch("cmt_add_cast");
-}
-
-extern "C" int cmt_acc_bias_res(const float* A, const float* bias, const void* R, void* Y, int dtype, int rows, int C,
-                                int B, int64_t bstride, void* stream) {
-    CMT_REQUIRE(A && bias && R && Y && rows >= 0 && B > 0 && C % 4 == 0 && bstride % 4 == 0,
-                "cmt_acc_bias_res: bad arguments");
-    CMT_REQUIRE(dtype == CMT_F16 || dtype == CMT_BF16, "cmt_acc_bias_res: dtype must be f16 or bf16");
-    const int64_t n4 = (int64_t)rows * C / 4;
-    if (n4 == 0) return 0;
-    const dim3 grid(nblocks(n4, 256), B);
-    hipStream_t s = (hipStream_t)stream;
-    if (dtype == CMT_F16)
-        acc_bias_res_kernel<f16_t><<<grid, 256, 0, s>>>(A, bias, (const f16_t*)R, (f16_t*)Y, n4, C / 4, bstride);
-    else
-        acc_bias_res_kernel<bf16_t><<<grid, 256, 0, s>>>(A, bias, (const bf16_t*)R, (bf16_t*)Y, n4, C / 4, bstride);
-    return cmt_check_launch("cmt_acc_bias_res");
 }
 
 extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F, int mode, int grid_h,

@@ -158,27 +158,6 @@ class HeadEngineMixin:
         lowp(memory + pos) -- the K-projection operand."""
         _, _, w2, b2 = pk["bev"]
         C, M = self.hidden_dim, hid.shape[0]
-        if (R is not None and R.dtype == pos.dtype and os.environ.get("CMT_BEV_POS_CACHE", "1") != "0"
-                and os.environ.get("CMT_BEV_ACC_CACHE", "1") != "0"):
-            # hid is the cached weight-only hidden layer, so its bev_embedding[2] product is a
-            # function of the weights too: kept (fp32, before the bias) and only the GEMM's
-            # epilogue -- acc + (bias + memory row), rounded -- runs per frame (bit-identical)
-            be = self.bev_embedding
-            src = [be[0].weight, be[0].bias, be[2].weight]
-            key = (M, str(w2.dtype), hid.data_ptr())
-            name = f"bev_pos_acc_{M}_{w2.dtype}"
-
-            def build():
-                acc = torch.empty((M, C), dtype=torch.float32, device=hid.device)
-                native.gemm(hid, w2, acc, M=M, N=w2.shape[0], K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1],
-                            ldc=C)
-                return acc
-            if torch.cuda.is_current_stream_capturing() and not self._pack.has(name, src, key):
-                acc = build()
-            else:
-                acc = self._pack.get(name, src, key, build)
-            native.acc_bias_res(acc, b2, R, pos, rows=M, C=C, B=B, bstride=Nk * C)
-            return
         native.gemm(hid, w2, pos, M=M, N=w2.shape[0], K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
                     bias=b2, batch=B, a_bstride=0, c_bstride=Nk * C, R=R, ldr=C if R is not None else 0,
                     r_bstride=Nk * C if R is not None else 0)

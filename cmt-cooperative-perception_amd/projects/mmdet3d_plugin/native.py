@@ -163,7 +163,6 @@ def _load():
         "cmt_rv_query_coords_ex": ([_vp, _int, _int, _int, _int, _flt, _flt, _vp, _vp, P(_flt), _vp, _int, _vp, _vp],
                                    _int),
         "cmt_masked_view_sum_ex": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _int, _vp], _int),
-        "cmt_acc_bias_res": ([_vp, _vp, _vp, _vp, _int, _int, _int, _int, _i64, _vp], _int),
         "cmt_nchw_to_rows": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp], _int),
         "cmt_cast": ([_vp, _int, _vp, _int, _i64, _vp], _int),
         "cmt_task_head_tail": ([_vp, _int, _int, _int, _int, _int, _vp, _vp, _vp, _vp, P(_int), _int, _int, _vp,
@@ -542,16 +541,6 @@ def masked_view_sum(X, mask, Y, *, B, V, Nq, C, base=None, Yl=None, Yp=None):
     _check(lib().cmt_masked_view_sum_ex(_p(X), _p(mask), B, V, Nq, C, _p(base), _p(Y), _p(Yl), _p(Yp),
                                         DT[low.dtype] if low is not None else 0, _stream()),
            "cmt_masked_view_sum_ex")
-
-
-def acc_bias_res(A, bias, R, Y, *, rows, C, B, bstride):
-    """Y[b, i] = lowp(A[i] + (bias + R[b, i])) for i < rows (rows of C), batch stride bstride
-    elements in R and Y -- cmt_gemm's bias + residual epilogue on a precomputed product."""
-    _dev(A, bias, R, Y)
-    if A.dtype != torch.float32 or bias.dtype != torch.float32 or R.dtype != Y.dtype:
-        raise RuntimeError("acc_bias_res: A / bias fp32, R and Y one 16-bit dtype")
-    _check(lib().cmt_acc_bias_res(_p(A), _p(bias), _p(R), _p(Y), DT[Y.dtype], rows, C, B, bstride, _stream()),
-           "cmt_acc_bias_res")
 
 
 def rv_query_coords_lowp(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w, pc_range):

@@ -309,12 +309,6 @@ int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, int D, float 
                            void* out, int odtype, float* mask, void* stream);
 int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int Nq, int C,
                            const float* base, float* Y, void* Yl, void* Yp, int lowp_dtype, void* stream);
-/* cmt_acc_bias_res (ABI 11): Y[b*bstride + i*C + c] = dtype(A[i*C + c] + (bias[c] + R[b*bstride + i*C + c]))
- * for i < rows, b < B -- the bias + residual epilogue of cmt_gemm (bit-identical) applied to a
- * precomputed fp32 product shared by the batch: bev_embedding[2](hidden) is a function of the
- * weights (cmt_head.py:324-337, 489), only the memory rows R change per frame. */
-int cmt_acc_bias_res(const float* A, const float* bias, const void* R, void* Y, int dtype, int rows, int C,
-                     int B, int64_t bstride, void* stream);
 
 /* ------------------------------------------------------------------------
  * Layout / dtype plumbing.

@@ -272,7 +272,7 @@ def test_bev_pos_hidden_cache(dev, monkeypatch):
     the grid + bev_embedding[0] + ReLU) is kept like a weight pack: a forward
     that reuses it equals one that recomputes it (CMT_BEV_POS_CACHE=0)
     bit-exactly, and an in-place change of bev_embedding[0] (an optimizer step)
-    rebuilds it (bev_embedding[0] and [2], whose product is kept as well)."""
+    rebuilds it."""
     from projects.mmdet3d_plugin import set_precision
     from projects.mmdet3d_plugin import synthetic as S
     head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=5, num_query=64, num_layers=2,
@@ -299,14 +299,8 @@ def test_bev_pos_hidden_cache(dev, monkeypatch):
             head.bev_embedding[0].weight.mul_(1.5)
         changed = run("1")
         fresh2 = run("0")
-        with torch.no_grad():
-            head.bev_embedding[2].weight.mul_(0.5)     # the cached bev_embedding[2] product too
-        changed2 = run("1")
-        fresh3 = run("0")
     finally:
         set_precision("ref")
     for k in KEYS:
         assert torch.equal(changed[k], fresh2[k]), k
-        assert torch.equal(changed2[k], fresh3[k]), k
     assert not torch.equal(changed["cls_logits"], cached["cls_logits"])
-    assert not torch.equal(changed2["cls_logits"], changed["cls_logits"])
