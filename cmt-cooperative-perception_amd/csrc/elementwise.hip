@@ -5,6 +5,8 @@
 // needed, 16-byte vector accesses where the layout allows.
 #include "cmt_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -174,6 +176,57 @@ __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict_
 // _rv_pe geometry (cmt_head.py:417-432): one thread per (bv, h, w, depth).
 // ---------------------------------------------------------------------------
 struct PcRange { float v[6]; };
+
+template <typename OT>
+__global__ void rv_pe_coords_kernel8(int BV, int H, int W, int D, float pad_h, float pad_w, float dstep,
+                                     const float* __restrict__ i2l, PcRange pc, OT* out) {
+    // one thread = 8 consecutive depth samples of one image token: 24 outputs, written as whole
+    // 16-byte (16-bit outputs) or 32-byte (fp32) pieces; 32-bit index math
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dg = D >> 3;
+    const int total = BV * H * W * dg;
+    if (idx >= total) return;
+    const int k0 = (idx % dg) * 8;
+    const int tok = idx / dg;
+    const int w = tok % W;
+    const int h = (tok / W) % H;
+    const int bv = tok / (W * H);
+    const float u = (float)w * pad_w / (float)W;
+    const float v = (float)h * pad_h / (float)H;
+    const float* M = i2l + bv * 16;
+    float m[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) m[i] = M[i];
+    float res[24];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float d = 1.f + (float)(k0 + j) * dstep / (float)D;
+        const float c[4] = {u * d, v * d, d, 1.f};
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            float a = m[r * 4 + 0] * c[0];
+            a = fmaf(m[r * 4 + 1], c[1], a);
+            a = fmaf(m[r * 4 + 2], c[2], a);
+            a = fmaf(m[r * 4 + 3], c[3], a);
+            res[3 * j + r] = (a - pc.v[r]) / (pc.v[3 + r] - pc.v[r]);
+        }
+    }
+    OT* o = out + (int64_t)tok * (3 * D) + 3 * k0;   // 24 consecutive outputs
+    if constexpr (sizeof(OT) == 2) {
+        typedef OT o8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            o8 pk;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pk[e] = (OT)res[8 * q + e];
+            *(o8*)(o + 8 * q) = pk;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+            *(f32x4*)(o + 4 * q) = f32x4{res[4 * q], res[4 * q + 1], res[4 * q + 2], res[4 * q + 3]};
+    }
+}
 
 template <typename OT>
 __global__ void rv_pe_coords_kernel(int BV, int H, int W, int D, float pad_h, float pad_w, float dstep,
@@ -599,8 +652,23 @@ extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float 
     CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_rv_pe_coords: bad odtype");
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
-    const int64_t total = (int64_t)BV * h * w * D;
     hipStream_t s = (hipStream_t)stream;
+    const char* vec = getenv("CMT_RVPE_VEC");   // diagnostics: 0 = the one-thread-per-depth kernel
+    if (!(vec && vec[0] == '0') && D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) &&
+        (uintptr_t)out % 16 == 0) {
+        const int64_t t8 = (int64_t)BV * h * w * (D / 8);
+        if (odtype == CMT_F32)
+            rv_pe_coords_kernel8<float><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
+                                                                         i2l, pc, (float*)out);
+        else if (odtype == CMT_F16)
+            rv_pe_coords_kernel8<f16_t><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
+                                                                         i2l, pc, (f16_t*)out);
+        else
+            rv_pe_coords_kernel8<bf16_t><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w,
+                                                                          depth_max - 1.f, i2l, pc, (bf16_t*)out);
+        return cmt_check_launch("cmt_rv_pe_coords");
+    }
+    const int64_t total = (int64_t)BV * h * w * D;
     if (odtype == CMT_F32)
         rv_pe_coords_kernel<float><<<nblocks(total, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
                                                                        i2l, pc, (float*)out);

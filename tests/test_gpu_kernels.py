@@ -724,3 +724,23 @@ def test_nchw_to_rows_layouts(N, dev, dt, nb, nv, C, HW, off):
     got = y.view(nb, rpb, C).cpu()
     assert torch.equal(got[:, off:off + nv * HW], ref)
     assert torch.isnan(got[:, :off].float()).all() and torch.isnan(got[:, off + nv * HW:].float()).all()
+
+
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16, torch.float16])
+def test_rv_pe_coords_vector_path_bitexact(N, dev, odt):
+    """The 8-depths-per-thread rv_pe_coords kernel (16/32-byte stores) equals the
+    one-thread-per-depth kernel bit for bit (forced by a misaligned output view);
+    the formula itself is held to the oracle by the head parity tests."""
+    g = torch.Generator().manual_seed(7)
+    BV, h, w, D = 6, 8, 20, 64
+    l2i = torch.randn(BV, 4, 4, generator=g, dtype=torch.float64) + 4 * torch.eye(4, dtype=torch.float64)
+    i2l = torch.linalg.inv(l2i).float().to(dev)
+    pcr = [-54.0, -54.0, -5.0, 54.0, 54.0, 3.0]
+    n = BV * h * w * 3 * D
+    a = torch.empty(n, dtype=odt, device=dev)
+    N.rv_pe_coords(i2l, a, BV=BV, h=h, w=w, D=D, pad_h=128.0, pad_w=320.0, depth_max=pcr[3], pc_range=pcr)
+    buf = torch.empty(n + 8, dtype=odt, device=dev)
+    b = buf[1:n + 1]                                        # 2- or 4-byte offset: the generic kernel
+    N.rv_pe_coords(i2l, b, BV=BV, h=h, w=w, D=D, pad_h=128.0, pad_w=320.0, depth_max=pcr[3], pc_range=pcr)
+    torch.cuda.synchronize()
+    assert torch.equal(a.cpu(), b.cpu())
