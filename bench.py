@@ -83,19 +83,20 @@ WORKLOADS = {
 }
 
 
-def make_workload(name, seed, device=None):
+def make_workload(name, seed, device=None, batch=1):
     """(head, head cfg, forward closure, per-agent memory lengths, oracle closure)
-    for one synthetic frame of ``name``; tensors on ``device`` (CPU if None)."""
+    for one synthetic frame of ``name`` (``batch`` frames per forward); tensors on
+    ``device`` (CPU if None)."""
     w = WORKLOADS[name]
     head, cfg, _ = S.build_synthetic_head(w["cfg"], seed=0, num_query=w["nq"], device=device)
-    inputs, nks, metas = [], [], [dict()]
+    inputs, nks, metas = [], [], [dict() for _ in range(batch)]
     for i, (prefix, yaws) in enumerate(w["agents"]):
-        x = S.synthetic_bev(1, 180, 180, seed=seed + 1 + 10 * i, device=device)
+        x = S.synthetic_bev(batch, 180, 180, seed=seed + 1 + 10 * i, device=device)
         xi = None
         if yaws is not None:
-            xi = S.synthetic_img(len(yaws), 40, 100, seed=seed + 2 + 10 * i, device=device)
-            m = S.synthetic_metas(1, yaws=yaws, prefix=prefix, seed=seed + 3 + 10 * i)[0]
-            metas[0].update(m)
+            xi = S.synthetic_img(batch * len(yaws), 40, 100, seed=seed + 2 + 10 * i, device=device)
+            for b, m in enumerate(S.synthetic_metas(batch, yaws=yaws, prefix=prefix, seed=seed + 3 + 10 * i)):
+                metas[b].update(m)
         inputs.append((prefix, x, xi))
         nks.append(180 * 180 + (0 if yaws is None else len(yaws) * 40 * 100))
     if len(inputs) == 1:
@@ -239,6 +240,9 @@ def main():
     ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "ref"],
                     help="compute policy of the headline value (default: the workload's, bf16 / fp16 for stress4)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-batch2", action="store_true", help="skip the two-frames-per-forward throughput key")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="frames per head forward (the headline is 1: one frame per GPU per step)")
     ap.add_argument("--no-ref", action="store_true", help="skip the 'ref'-policy frames/s key")
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -280,11 +284,12 @@ def main():
             dist.destroy_process_group()
         return
 
-    head, cfg, step, nks, _ = make_workload(args.workload, seed=dp.frame_seed(0, env), device=dev)
+    head, cfg, step, nks, _ = make_workload(args.workload, seed=dp.frame_seed(0, env), device=dev, batch=args.batch)
     with torch.no_grad():
         run = capture(step).replay if not args.no_graph else step
         elapsed, value = dp.timed_frames(run, steps=args.steps, warmup=args.warmup, env=env,
                                          sync=torch.cuda.synchronize, device=dev)
+        value *= args.batch   # frames per forward
 
         # --- dominant kernel: cross-attention, HIP events on its launch stream
         with region_timer() as rt:
@@ -292,6 +297,21 @@ def main():
                 step()
         attn_ms_all = rt.durations_ms("cross_attn")
         attn_ms = sum(attn_ms_all) / len(attn_ms_all)
+
+        # --- throughput with two frames per head forward (the headline stays one frame per GPU
+        # per step): the latency-bound query-side kernels (row-block chains, self-attention,
+        # small GEMMs) process both frames' rows in one launch
+        batch2 = None
+        if args.batch == 1 and not args.no_batch2:
+            _, _, step2, _, _ = make_workload(args.workload, seed=dp.frame_seed(0, env) + 101, device=dev, batch=2)
+            run2 = capture(step2).replay if not args.no_graph else step2
+            st2 = max(10, args.steps // 2)
+            e2, v2 = dp.timed_frames(run2, steps=st2, warmup=max(3, args.warmup // 2), env=env,
+                                     sync=torch.cuda.synchronize, device=dev)
+            batch2 = {"value": round(2 * v2, 3), "unit": "frames/s", "frames_per_forward": 2, "steps": st2,
+                      "ms_per_step": round(e2 / st2 * 1e3, 4)}
+            del run2, step2
+            torch.cuda.empty_cache()
 
         # --- the reference-numerics policy on the same frame (fp32 GEMMs, fp16 cross core)
         ref_policy = None
@@ -325,7 +345,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     # mean algorithmic FLOPs of one cross-attention launch (agents may differ in Nk)
     nq = w["nq"]
-    flop_launch = sum(cross_attn_flops(nq=nq, nk=nk) for nk in nks) / len(nks)
+    flop_launch = args.batch * sum(cross_attn_flops(nq=nq, nk=nk) for nk in nks) / len(nks)
     achieved = flop_launch / (attn_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS.get(prec, PEAK_TFLOPS["bf16"])
     traffic, traffic_src = (None, None)
@@ -345,7 +365,8 @@ def main():
         "dtype": {"bf16": "bf16", "fp16": "fp16", "ref": "fp32+fp16attn"}[prec],
         "data": "synthetic (seeded BEV features relu(N(0,1)), image feats N(0,1), nuScenes/TUMTraf-like camera "
                 "matrices, random-init weights of the head)",
-        "config": {"workload": w["desc"], "global_batch": world, "seq_len": sum(nks), "num_query": nq,
+        "config": {"workload": w["desc"] + ("" if args.batch == 1 else f" -- {args.batch} frames per forward"),
+                   "global_batch": world * args.batch, "seq_len": sum(nks), "num_query": nq,
                    "parallelism": f"dp{world}", "graph": not args.no_graph,
                    # pos2embed(BEV grid) + bev_embedding[0] is a function of the weights only: built
                    # once per weight version like the packed weights (CMT_BEV_POS_CACHE=0: per frame)
@@ -356,6 +377,7 @@ def main():
                      "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": round(attn_ms, 5), "flop_per_launch": flop_launch},
         "ref_policy": ref_policy,
+        "batch2": batch2,
         "voxel_scatter_mean_ms": round(vox_ms, 4),
         "cpu_baseline": None,
     }

@@ -304,3 +304,30 @@ def test_bev_pos_hidden_cache(dev, monkeypatch):
     for k in KEYS:
         assert torch.equal(changed[k], fresh2[k]), k
     assert not torch.equal(changed["cls_logits"], cached["cls_logits"])
+
+
+def test_fusion_batch2_equals_two_single_frames(dev):
+    """Two frames in one forward (bench.py's `batch2` key) give each frame
+    exactly its single-frame outputs (bf16 bench policy, chain path, side
+    stream): every kernel is per-row / per-(batch, head), so batching changes
+    only how many rows a launch covers."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=9, num_query=96, num_layers=2,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(2, 32, 32, seed=51).to(dev)
+    xi = S.synthetic_img(12, 8, 20, seed=52).to(dev)
+    metas = S.synthetic_metas(2, pad_shape=(128, 320, 3), seed=53)
+    set_precision("bf16")
+    try:
+        with torch.no_grad():
+            both = {k: v.clone() for k, v in head([x], [xi], metas)[0][0].items()}
+            one = [{k: v.clone() for k, v in head([x[b:b + 1]], [xi[6 * b:6 * b + 6]], metas[b:b + 1])[0][0].items()}
+                   for b in range(2)]
+        torch.cuda.synchronize()
+    finally:
+        set_precision("ref")
+    for k in KEYS:   # [layers, B, Nq, ...]
+        for b in range(2):
+            got, want = both[k][:, b], one[b][k][:, 0]
+            assert torch.equal(got, want), (k, b, (got - want).abs().max().item())
