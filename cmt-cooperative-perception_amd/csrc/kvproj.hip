@@ -379,7 +379,12 @@ __global__ __launch_bounds__(64 * NW, 1) void kvproj_kernel(cmt_gemm_args a, int
 extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_kv_proj: null args");
     const cmt_gemm_args& a = *ap;
-    const int parts = a.A2 ? 2 : 1;
+    // column parts per 128-token tile: 2 (K half | V half) or, CMT_KVPROJ_PARTS=4, quarters --
+    // twice the workgroups (1764 instead of 882 at the fusion shape: a fuller last round on 256
+    // CUs) for twice the A-tile reads
+    const char* pv = getenv("CMT_KVPROJ_PARTS");
+    const int pmul = (pv && pv[0] == '4' && a.A2 && (a.N / 4 / 32) % 8 == 0) ? 2 : 1;
+    const int parts = (a.A2 ? 2 : 1) * pmul;
     CMT_REQUIRE(a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16, "cmt_kv_proj: w_dtype must be f16 or bf16");
     CMT_REQUIRE(a.a_dtype == a.w_dtype && a.c_dtype == a.w_dtype, "cmt_kv_proj: A and C in the compute dtype");
     CMT_REQUIRE(a.A && a.W && a.C && a.M > 0 && a.K == KP_K && a.batch == 1, "cmt_kv_proj: needs A/W/C, K = 256");
@@ -402,10 +407,12 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
     const int diag = (dg && dg[0] >= '1' && dg[0] <= '3') ? dg[0] - '0' : 0;
     // 8-wave form when every wave gets an even number of head planes (CMT_KVPROJ_NW=4 forces the 4-wave form)
     const char* nw = getenv("CMT_KVPROJ_NW");
-    const bool w8 = !(nw && nw[0] == '4') && (a.N / parts / 32) % 16 == 0;
     // 8-wave form: whole 128-token tile per W fetch unless CMT_KVPROJ_FULL=0 (two 64-token halves)
     const char* fu = getenv("CMT_KVPROJ_FULL");
     const bool full = !(fu && fu[0] == '0');
+    // the two-half sweep needs an even plane count per wave, the full sweep any count
+    const bool w8 = !(nw && nw[0] == '4') && (a.N / parts / 32) % (full ? 8 : 16) == 0;
+    CMT_REQUIRE(pmul == 1 || (w8 && full && diag == 0), "cmt_kv_proj: CMT_KVPROJ_PARTS=4 needs the 8-wave full sweep");
     if (w8 && diag == 0) {
         if (full) {
             if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t, 0, 8, true><<<grid, 512, 0, s>>>(a, parts);

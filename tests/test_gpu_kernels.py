@@ -166,13 +166,16 @@ def test_gemm_plane_max2(N, dev, dt, B, S, big):
     assert torch.allclose(pm.cpu().double(), ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("parts", ["2", "4"])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100)])
-def test_kvproj_select_plane_max(N, dev, dt, B, S):
+def test_kvproj_select_plane_max(N, dev, monkeypatch, dt, B, S, parts):
     """All-layer K/V projection shape (N = 3072, K = 256, A2 select on the K half,
     head-split output, K-half key-norm maxima) through cmt_kv_proj, the
     A-stationary kernel on fragment-packed W (kvproj.hip); ragged M, row tiles
-    straddling the batch boundary, a grid smaller than one 128-row tile pair."""
+    straddling the batch boundary, a grid smaller than one 128-row tile pair;
+    column halves or quarters per row tile (CMT_KVPROJ_PARTS)."""
+    monkeypatch.setenv("CMT_KVPROJ_PARTS", parts)
     g = torch.Generator().manual_seed(S * 7 + B)
     K, Nc = 256, 3072
     M, cols = B * S, Nc // 2
