@@ -503,34 +503,32 @@ struct DmaTile {
             bsrc[i] = Wb + (int64_t)(n0 + row) * a.ldw + (ch ^ ((row >> 1) & 7)) * 8;
         }
 
-        // 3x3 implicit conv: the stages arrive in increasing k order, and a tap spans conv_c / 64
-        // stages, so each row's gathered offset is recomputed once per tap (9 times per tile),
-        // not per stage (no integer division by conv_c in the k loop)
+        // implicit convs (3x3, 1D k = 3): the stages arrive in increasing k order and a tap spans
+        // (tap width) / 64 stages, so each row's gathered offset is recomputed once per tap
+        // (9 or 3 times per tile), not per stage (no integer division in the k loop)
         int ctap = -1, ccin = 0;
         int64_t toff[APER];
         auto issue = [&](int buf, int kt) {
             char* sb = smem + buf * STAGE;
             const int k0 = kt * KS;
-            if constexpr (AMODE == CMT_A_CONV3X3) {
-                if (ctap < 0 || (ccin += KS) == a.conv_c) {
-                    ctap = ctap < 0 ? k0 / a.conv_c : ctap + 1;
-                    ccin = k0 - ctap * a.conv_c;
+            if constexpr (AMODE != CMT_A_ROWS) {
+                // the same per-tap cache for the 1D k = 3 conv (taps of K / 3 columns)
+                const int tapw = AMODE == CMT_A_CONV3X3 ? a.conv_c : a.K / 3;
+                if (ctap < 0 || (ccin += KS) == tapw) {
+                    ctap = ctap < 0 ? k0 / tapw : ctap + 1;
+                    ccin = k0 - ctap * tapw;
 #pragma unroll
                     for (int i = 0; i < APER; ++i)
-                        toff[i] = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), ctap * a.conv_c);
+                        toff[i] = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), ctap * tapw);
                 }
             }
 #pragma unroll
             for (int i = 0; i < APER; ++i) {
                 const void* src;
-                if (AMODE == CMT_A_ROWS) {
+                if (AMODE == CMT_A_ROWS)
                     src = asrc[i] + k0;
-                } else if (AMODE == CMT_A_CONV3X3) {
+                else
                     src = toff[i] < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + toff[i] + ccin + acs[i]);
-                } else {
-                    const int64_t off = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), k0);
-                    src = off < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + off + acs[i]);
-                }
                 glds16(src, sb + (4 * i + wave) * 1024);
             }
 #pragma unroll
