@@ -62,6 +62,7 @@ struct AttnKParams {
     int sync_all;                   // diagnostics: drain every LDS-DMA before each tile (flag bit 1 << 8)
     int prio;                       // static wave priority of the ping-pong halves (pb kernel): 0 none, 1 half B, 2 half A
     unsigned long long* stamp;      // diagnostics build only (CMT_ATTN_STAMP): per-wave segment cycle sums
+    int keep_dead;                  // diagnostics (CMT_ATTN_SKIPDEAD=0): padded waves compute anyway
 };
 
 // In-kernel segment stamp (diagnostic build of attn_pb_kernel only): shader
@@ -1446,6 +1447,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
     const int b = bh / p.H;
     const int h = bh - b * p.H;
 
+    // a wave whose 32 queries all lie past Nq (the padding of the last query block) keeps the
+    // workgroup's barriers and LDS-DMA duties but skips its MFMAs, exponentials and fragment reads
+    const bool live = p.keep_dead || qb * (8 * QW) + wave * QW < p.Nq;
     const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
     const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
     const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
@@ -1526,38 +1530,38 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         if (!hb) issue_upto(8);
         {
             const PpLane l = pp_launder(lane_ofs);
-            pp_load_k<T>(slot_b(0), l, kf0);
-            pp_load_k<T>(slot_b(1), l, kf1);
+            if (live) pp_load_k<T>(slot_b(0), l, kf0);
+            if (live) pp_load_k<T>(slot_b(1), l, kf1);
         }
-        pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        pb_mseg<T, true, false, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
+        if (live) pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        if (live) pb_mseg<T, true, false, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
         if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
         pp_barrier();
-        pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, true);
+        if (live) pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, true);
         {
             const PpLane l = pp_launder(lane_ofs);
-            pp_load_k<T>(slot_b(2), l, kf0);   // stale (unused) when np == 1
-            pp_load_k<T>(slot_b(3), l, kf1);
-            pp_load_v<T>(slot_b(0) + KV_B, l, vf0);
-            pp_load_v<T>(slot_b(1) + KV_B, l, vf1);
+            if (live) pp_load_k<T>(slot_b(2), l, kf0);   // stale (unused) when np == 1
+            if (live) pp_load_k<T>(slot_b(3), l, kf1);
+            if (live) pp_load_v<T>(slot_b(0) + KV_B, l, vf0);
+            if (live) pp_load_v<T>(slot_b(1) + KV_B, l, vf1);
         }
         for (int j = 1; j < np; ++j) {
             pp_barrier();
             if (!hb) issue_upto(2 * j + 8);
-            pb_mseg<T, true, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);   // QK^T tile 2j, PV tile 2j-2
-            pb_mseg<T, true, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);   // QK^T tile 2j+1, PV tile 2j-1
+            if (live) pb_mseg<T, true, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);   // QK^T tile 2j, PV tile 2j-2
+            if (live) pb_mseg<T, true, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);   // QK^T tile 2j+1, PV tile 2j-1
             if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
             pp_barrier();
-            pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, false);
+            if (live) pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, false);
             const PpLane l = pp_launder(lane_ofs);
-            pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
-            pp_load_k<T>(slot_b(2 * j + 3), l, kf1);
-            pp_load_v<T>(slot_b(2 * j) + KV_B, l, vf0);
-            pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
+            if (live) pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
+            if (live) pp_load_k<T>(slot_b(2 * j + 3), l, kf1);
+            if (live) pp_load_v<T>(slot_b(2 * j) + KV_B, l, vf0);
+            if (live) pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
         }
         pp_barrier();
-        pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        pb_mseg<T, false, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
+        if (live) pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        if (live) pb_mseg<T, false, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
     }
     if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
 
@@ -1569,11 +1573,11 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         }
         pp_barrier();
         const PpLane l = pp_launder(lane_ofs);
-        pp_load_k<T>(slot_b(nt - 1), l, kf0);
-        pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
-        pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, np == 0);
-        pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        if (live) pp_load_k<T>(slot_b(nt - 1), l, kf0);
+        if (live) pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
+        if (live) pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        if (live) pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, np == 0);
+        if (live) pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
     }
 
     if (tail) {
@@ -1589,17 +1593,17 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
         }
         pp_barrier();
         const PpLane l = pp_launder(lane_ofs);
-        pp_load_k<T>(rb, l, kf0);
-        pp_load_v<T>(rb + KV_B, l, vf0);
-        pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        if (live) pp_load_k<T>(rb, l, kf0);
+        if (live) pp_load_v<T>(rb + KV_B, l, vf0);
+        if (live) pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
         const int key0 = (ntiles - 1) * KT;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s0[kb][r] = -__builtin_inff();
-        pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, nt == 0);
-        pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+        if (live) pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, nt == 0);
+        if (live) pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
     }
 
     // ---- write (as attn_pb_kernel)
@@ -2059,6 +2063,10 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         p.prio = (pv && pv[0] >= '0' && pv[0] <= '2') ? pv[0] - '0' : 0;
     }
     p.stamp = nullptr;
+    {
+        const char* sd = getenv("CMT_ATTN_SKIPDEAD");
+        p.keep_dead = (sd && sd[0] == '0') ? 1 : 0;
+    }
     p.Op = p.Mp = p.Lp = nullptr;
     if (splits > 1) {
         const int64_t need = cmt_attn_workspace_bytes(&a);
