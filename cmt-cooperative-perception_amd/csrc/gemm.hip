@@ -1023,11 +1023,16 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
             if (st == 3) return launch_dma<128, 128, 3>(a, s);
             return launch_dma<128, 128, 2>(a, s);
         }
-        // long-K problems one 128x128 grid would not fill (the RV embedding's second GEMM,
-        // M = 24 000, N = 256, K = 1024): 128 x 64 tiles read 3/4 of the 64 x 64 tiles' operand
-        // bytes per output and still give ~3 workgroups per CU
+        // long-K problems a 128x128 grid fills less than twice over (the RV embedding's second
+        // GEMM, M = 24 000, N = 256, K = 1024: 376 tiles): still 128 x 128 with 2 stages when N
+        // allows (26.7 us vs 30.0 us on 128 x 64 x 3 stages, 36.3 on 128 x 128 x 3), else
+        // 128 x 64 tiles (3/4 of the 64 x 64 tiles' operand bytes per output)
         const int64_t mid_tiles = (int64_t)(a.N / 64) * cdiv(a.M, 128) * a.batch;
-        if (kdiv >= 512 && a.a_mode == CMT_A_ROWS && mid_tiles >= 480) return launch_dma<128, 64, 3>(a, s);
+        if (kdiv >= 512 && a.a_mode == CMT_A_ROWS && mid_tiles >= 480) {
+            const char* mid = getenv("CMT_GEMM_MID");   // diagnostics: 0 = the 128 x 64 tiles
+            if (a.N % 128 == 0 && !(mid && mid[0] == '0')) return launch_dma<128, 128, 2>(a, s);
+            return launch_dma<128, 64, 3>(a, s);
+        }
         return launch_dma<64, 64, 4>(a, s);
     }
     // Tile choice: 128x128 when the grid still fills the chip, else 64x64.
