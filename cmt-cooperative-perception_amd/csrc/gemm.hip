@@ -17,6 +17,8 @@
 // padded to 36 floats (conflict-free ds_read_b128).
 #include "cmt_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int BK = 32;
@@ -1015,7 +1017,13 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
         CMT_REQUIRE(a.ldc % 4 == 0 && (a.R == nullptr || a.ldr % 4 == 0) && a.bias_bstride % 4 == 0,
                     "cmt_gemm: ldc/ldr/bias_bstride must be multiples of 4");
         const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
-        if (a.N % 128 == 0 && big_tiles >= 480) {
+        // 128 x 128 tiles from ~1.9 workgroups per CU up.  CMT_GEMM_BIG_MIN (diagnostics) moves the
+        // threshold: at 300 the RV query MLP's fc1 (344 tiles) runs 9.9 instead of 12.4 us alone,
+        // but the frame is slower (919 vs 927 frames/s): it runs on the side stream beside the
+        // conv, where the bigger tiles' LDS does not fit
+        static const char* bmin = getenv("CMT_GEMM_BIG_MIN");
+        const int64_t big_min = bmin && bmin[0] ? atoi(bmin) : 480;
+        if (a.N % 128 == 0 && big_tiles >= big_min) {
             // diagnostics: CMT_GEMM_S128 = LDS stages of the 128 x 128 tile (2, 3 or 4)
             const char* ov = getenv("CMT_GEMM_S128");
             const int st = (ov && ov[0] >= '2' && ov[0] <= '4') ? ov[0] - '0' : 2;
