@@ -7,16 +7,20 @@ camera+LiDAR nuScenes-shape synthetic frame -- BEV [1, 512, 180, 180] plus
 6 views x [256, 40, 100] pre-extracted image features (32 400 + 24 000 =
 56 400 memory tokens), 900 queries, 6-layer decoder, the whole CmtHead forward
 per step: shared_conv, BEV / RV / query coordinate encodings, decoder, task
-heads, box epilogue; bf16 compute (fp32 accumulate, fp32 residual stream).
+heads, box epilogue, at the reference's numerics ('ref' policy: every fp32
+GEMM of the reference as a three-pass split-bf16 MFMA product, ~2^-16 relative
+per product; fp32 self-attention; fp16 flash cross-attention core with fp16 P
+and output, flash-attn 0.2.2).
 The ~30k-point voxel scatter-mean is timed separately.
 Inputs and weights are resident in HBM before the timed region; one step = one
-frame per rank, captured as a HIP graph.  The reference-numerics policy
-('ref': fp32 GEMMs, fp16 cross-attention core) is timed on the same frame and
-reported beside the headline as ``ref_policy``.
+frame per rank, captured as a HIP graph.  The bf16 speed policy (bf16 GEMM operands, bf16
+attention core: ~2.5 % of each output's scale from the fp32 reference, outside
+north_star's 1e-3) is timed on the same frame and reported beside the headline
+as ``bf16_policy``.
 
 Other workloads (--workload): lidar (configs[1], 32 400 tokens), coop
 (configs[3] forward: vehicle 36 400 + infrastructure 44 400 tokens), stress4
-(configs[4]: 4 agents x 48 400 tokens, 1500 queries, fp16).
+(configs[4]: 4 agents x 48 400 tokens, 1500 queries, fp16 policy).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 With --gpus N > 1 and no torch.distributed environment, this process starts
@@ -46,6 +50,9 @@ from projects.mmdet3d_plugin.mmcv_custom.ops.voxel import SPConvVoxelization  # 
 from projects.mmdet3d_plugin.profiling import region_timer  # noqa: E402
 
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}   # dense MFMA, MI355X_MICROARCH.md (no sparsity)
+DTYPE_LABEL = {"bf16": "bf16", "fp16": "fp16",
+               "ref": "fp32 (GEMMs as 3-pass split-bf16 MFMA) + fp16 flash attention core: reference numerics",
+               "exact": "fp32 (exact-f32 MFMA GEMMs) + fp16 flash attention core: reference numerics"}
 C, NQ, NK, L, H = 256, 900, 32400, 6, 8
 METRIC = "decoder frames/sec at 900 queries x (BEV+6-cam) tokens; 1/2/4/8 MI355X"
 STRESS_YAWS = (0.0, 90.0, 180.0, -90.0)
@@ -63,15 +70,15 @@ def decoder_frame_flops(nq=NQ, nk=NK, c=C, layers=L, ffn=1024):
 
 WORKLOADS = {
     # cfg: head config; agents: (meta prefix, camera yaws or None); nq: queries; precision: compute policy
-    "fusion": dict(cfg="cmt_fusion_nus", agents=[("", S.NUS_YAWS)], nq=900, precision="bf16", head="CmtHead",
+    "fusion": dict(cfg="cmt_fusion_nus", agents=[("", S.NUS_YAWS)], nq=900, precision="ref", head="CmtHead",
                    desc="CMT camera+LiDAR nuScenes-shape (BASELINE configs[2]): BEV 512x180x180 + 6 views x "
                         "256x40x100 image feats (56400 tokens), 900 queries, 6-layer decoder, CmtHead forward "
                         "(shared_conv + BEV/RV/query encodings + decoder + task heads), batch 1 frame per GPU"),
-    "lidar": dict(cfg="cmt_lidar_nus", agents=[("", None)], nq=900, precision="bf16", head="CmtLidarHead",
+    "lidar": dict(cfg="cmt_lidar_nus", agents=[("", None)], nq=900, precision="ref", head="CmtLidarHead",
                   desc="CMT-L (LiDAR-only) nuScenes-shape (BASELINE configs[1]): BEV 512x180x180 (32400 tokens), "
                        "900 queries, 6-layer decoder, CmtLidarHead forward, batch 1 frame per GPU"),
     "coop": dict(cfg="cmtcoop_fusion_tumtraf", agents=[("vehicle_", S.VEHICLE_YAWS), ("infrastructure_", S.INFRA_YAWS)],
-                 nq=900, precision="bf16", head="CmtHeadCoop",
+                 nq=900, precision="ref", head="CmtHeadCoop",
                  desc="CMTCoop TUMTraf-shape forward (BASELINE configs[3] forward leg): vehicle BEV 180x180 + 1 cam, "
                       "infrastructure BEV 180x180 + 3 cams (36400 + 44400 tokens), 900 queries, 6-layer decoder per "
                       "agent, max fusion, CmtHeadCoop forward, batch 1 frame per GPU"),
@@ -237,13 +244,13 @@ def main():
     ap.add_argument("--workload", default="fusion", choices=sorted(WORKLOADS),
                     help="fusion = BASELINE configs[2] (the headline line); lidar / coop / stress4 = configs[1] / "
                          "[3] forward / [4]")
-    ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "ref"],
-                    help="compute policy of the headline value (default: the workload's, bf16 / fp16 for stress4)")
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "ref", "exact"],
+                    help="compute policy of the headline value (default: the workload's: ref, fp16 for stress4)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-batch2", action="store_true", help="skip the two-frames-per-forward throughput key")
     ap.add_argument("--batch", type=int, default=1,
                     help="frames per head forward (the headline is 1: one frame per GPU per step)")
-    ap.add_argument("--no-ref", action="store_true", help="skip the 'ref'-policy frames/s key")
+    ap.add_argument("--no-ref", action="store_true", help="skip the bf16-policy frames/s side key")
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="profiling runs: do not read the committed PMC summary")
@@ -313,16 +320,18 @@ def main():
             del run2, step2
             torch.cuda.empty_cache()
 
-        # --- the reference-numerics policy on the same frame (fp32 GEMMs, fp16 cross core)
-        ref_policy = None
-        if not args.no_ref and prec != "ref":
-            set_precision("ref")
-            run_ref = capture(step).replay if not args.no_graph else step
-            e_ref, v_ref = dp.timed_frames(run_ref, steps=max(5, args.steps // 5), warmup=2, env=env,
-                                           sync=torch.cuda.synchronize, device=dev)
-            ref_policy = {"value": round(v_ref, 3), "unit": "frames/s", "steps": max(5, args.steps // 5),
-                          "ms_per_step": round(e_ref / max(5, args.steps // 5) * 1e3, 4),
-                          "dtype": "fp32 GEMMs + fp16 cross-attention core (reference numerics)"}
+        # --- the bf16 speed policy on the same frame (bf16 operands everywhere; NOT held to
+        # north_star's 1e-3 -- reported beside the headline, never as it)
+        side = None
+        if not args.no_ref and prec == "ref":
+            set_precision("bf16")
+            run_b = capture(step).replay if not args.no_graph else step
+            st_b = max(10, args.steps // 2)
+            e_b, v_b = dp.timed_frames(run_b, steps=st_b, warmup=3, env=env, sync=torch.cuda.synchronize, device=dev)
+            side = {"value": round(v_b, 3), "unit": "frames/s", "steps": st_b, "ms_per_step": round(e_b / st_b * 1e3, 4),
+                    "dtype": "bf16 GEMM and attention operands (fp32 accumulate): ~2.5 % of scale from the "
+                             "reference, outside north_star's 1e-3"}
+            del run_b
             set_precision(prec)
 
         # --- voxel scatter-mean of ~30k points (timed separately)
@@ -362,7 +371,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"bf16": "bf16", "fp16": "fp16", "ref": "fp32+fp16attn"}[prec],
+        "dtype": DTYPE_LABEL[prec],
         "data": "synthetic (seeded BEV features relu(N(0,1)), image feats N(0,1), nuScenes/TUMTraf-like camera "
                 "matrices, random-init weights of the head)",
         "config": {"workload": w["desc"] + ("" if args.batch == 1 else f" -- {args.batch} frames per forward"),
@@ -376,7 +385,7 @@ def main():
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": round(attn_ms, 5), "flop_per_launch": flop_launch},
-        "ref_policy": ref_policy,
+        "bf16_policy": side,
         "batch2": batch2,
         "voxel_scatter_mean_ms": round(vox_ms, 4),
         "cpu_baseline": None,

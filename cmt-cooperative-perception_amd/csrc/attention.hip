@@ -59,27 +59,15 @@ struct AttnKParams {
     int splits;
     int tiles_per_split;
     int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
-    int sync_all;                   // diagnostics: drain every LDS-DMA before each tile (flag bit 1 << 8)
-    int prio;                       // static wave priority of the ping-pong halves (pb kernel): 0 none, 1 half B, 2 half A
-    unsigned long long* stamp;      // diagnostics build only (CMT_ATTN_STAMP): per-wave segment cycle sums
-    int keep_dead;                  // diagnostics (CMT_ATTN_SKIPDEAD=0): padded waves compute anyway
 };
 
-// In-kernel segment stamp (diagnostic build of attn_pb_kernel only): shader
-// clock, with the lgkmcnt(0) the s_memtime result needs inside the statement.
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-constexpr int kStampSlots = 16;
-
-// Final normalised output: 4 consecutive head dims of one query row.
+// Final normalised output: 4 consecutive head dims of one query row.  A
+// CMT_BF16P row holds the H*32 hi values, then the H*32 lo values.
 __device__ __forceinline__ void store_o4(const AttnKParams& p, int b, int q, int d0, f32x4 v) {
     const int64_t idx = (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + d0;
-    if (p.o_dtype == CMT_F32) {
+    if (p.o_dtype == CMT_BF16P) {
+        store_pair4((bf16_t*)p.O + idx - d0, p.H * D, d0, v);
+    } else if (p.o_dtype == CMT_F32) {
         *(f32x4*)((float*)p.O + idx) = v;
     } else if (p.o_dtype == CMT_F16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -380,7 +368,7 @@ __global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : (NWAVES == 8 ? 2 : 2)) 
         if (i < nt) issue(i, t_begin + i);
     for (int i = 0; i < nt; ++i) {
         const int issued = min(nt, RING - 1 + i);
-        const int inflight = p.sync_all ? 0 : issued - i - 1;  // tiles allowed to stay in flight
+        const int inflight = issued - i - 1;  // tiles allowed to stay in flight
         if (inflight >= 2) wait_vm_lgkm<2 * PERT>();
         else if (inflight == 1) wait_vm_lgkm<PERT>();
         else wait_vm_lgkm<0>();
@@ -570,33 +558,89 @@ __global__ __launch_bounds__(KW * 64) void attn_kw_kernel(AttnKParams p) {
     }
 }
 
+// Wave-wide max of the max-|k|^2 partials (each covers kmax_rows key rows)
+// over the key range of this workgroup's split of batch b, head h: the bound
+// only has to hold for the keys this workgroup scores (the split combine
+// merges per-split offsets).  16 independent loads per lane in flight; the
+// first form reduced all Nk / kmax_rows partials of the head in every wave
+// (2048 waves x 882 scattered loads at the fusion shape, ~4 us of prologue).
+__device__ __forceinline__ float kmax_reduce(const AttnKParams& p, int b, int h, int split, int lane) {
+    const int key0 = split * p.tiles_per_split * KT;
+    const int key1 = min(p.Nk, key0 + p.tiles_per_split * KT);
+    if (key0 >= key1) return 0.f;
+    const int64_t r0 = (int64_t)b * p.Nk;
+    const int e0 = (int)((r0 + key0) / p.kmax_rows), e1 = (int)((r0 + key1 - 1) / p.kmax_rows);
+    const float* src = p.kmax2 + p.kmax_plane0 + h;
+    float km = 0.f;
+    for (int base = e0 + lane; base <= e1; base += 64 * 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int e = base + 64 * j;
+            v[j] = e <= e1 ? src[(int64_t)e * p.kmax_ld] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) km = fmaxf(km, v[j]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
+    return km;
+}
+
+template <int N>
+__device__ __forceinline__ void pp_wait_n() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
 // ---------------------------------------------------------------------------
-// Ping-pong kernel for long key ranges (the cross-attention shape), f16/bf16.
+// Long-key kernel (the cross-attention shape: Nk >= 4096, Nq > 128), f16/bf16,
+// 8 waves, two 64-key tiles per ping-pong window.
 //
-// 8 waves = two halves of 4 (wave w sits on SIMD w % 4, so every SIMD holds
-// one wave of each half).  A wave's work per 64-key tile is split into a
-// matrix segment M(i) = {QK^T of tile i, PV + row sums of tile i-1} and a
-// vector segment V(i) = {softmax of tile i's scores}.  Every segment ends at a
-// workgroup barrier.  Both halves run the same straight-line program, but half
-// B passes one extra barrier first (and half A one at the end), so between two
-// barriers one wave of each SIMD issues MFMAs while its partner issues the
-// exponentials (MI355X_MICROARCH.md 'Two waves per SIMD'):
-//     window 2i   : A: M(i)     B: V(i-1)
-//     window 2i+1 : A: V(i)     B: M(i)
-// Half A stages the K/V tiles (LDS-DMA, two 1-KB pieces per wave and tile):
-// tile t's K is read in windows 2t, 2t+1 and its V in 2t+2, 2t+3, so its slot
-// is refilled at window 2t+4 with tile t + PPR, first read 2(PPR-2) windows
-// later.  Only full 64-key tiles run through the ping-pong loop; a ragged last
-// tile is masked and processed by all waves after it.
+// Bounded offsets (with the K projection's max-|k| partials): the scores of
+// query q over this split's keys are <= bound_q = |q| max|k| (Cauchy-Schwarz),
+// so the softmax needs no running max:
+//  * bf16: when every bound of the wave is <= kBoundMax (60 exp2 units), P =
+//    exp2(s) lies in [2^-60, 2^60] -- a normal bf16 / f32 number whose
+//    relative rounding does not depend on its magnitude -- and the QK^T MFMAs
+//    start from zero: no max tree, no subtraction, no rescale.
+//  * f16 (flash-attn 0.2.2's P precision): the offset is bound_q - 15, fed in
+//    as the QK^T accumulator's initial value, so P = exp2(s - bound_q + 15)
+//    <= 2^15 can never overflow f16.  A loose bound only lowers P; the row
+//    total then tells whether the P of this row kept full f16 precision
+//    (l >= 2^-6, kF16MinSum: the absolute f16 spacing 2^-24 is then far below
+//    the result's own rounding).  A workgroup with a row below it runs its
+//    split again with the online maximum for the waves concerned (the slow
+//    path below) -- never taken on the decoder's data, measured by
+//    test_gpu_kernels.py's loose-bound cases.
+// Without partials, or a bf16 bound above kBoundMax, a wave tracks an online
+// running max as ONE register per lane, subtracted on the VALU (exact lazy
+// rescale, deferred by kDeferMax so P <= 2^8).
 //
-// Bounded-max mode (bf16 with the optional max-|k| partials): the softmax
-// offset of a query is fixed at bound = |q| * max_k |k| >= every score
-// (Cauchy-Schwarz), so V(i) is only exp2 + convert -- no running max, no
-// rescale.  O = sum(P V) / sum(P) is invariant to the offset; P <= 1 and
-// s - bound >= -2 * kBoundMax keeps P a normal bf16.  Waves with a larger
-// bound (or f16, or no partials) track the running max online as above.
+// Q carries the folded scale c = scale * log2(e) (s in exp2 units).  QS: q * c
+// is kept as hi + lo in T (both QK^T MFMA passes), the product of the stored
+// q and c to ~2^-22 -- the scores of the unfolded kernel (flash-attn computes
+// q k in fp32 and scales after); without QS it is rounded once to T (the
+// CMT_ATTN_FOLD_SCALE permission of the f16 / bf16 speed policies).
+//
+// Schedule: 8 waves = two halves of 4 (wave w on SIMD w % 4, so every SIMD
+// holds one wave of each half).  A wave's work per window (tiles 2j, 2j+1) is
+// a matrix segment M(j) = {QK^T of the pair j, PV + row sums of pair j-1} and
+// a vector segment V(j) = {exponentials of pair j}; every segment ends at a
+// workgroup barrier, and half B runs one segment behind half A, so one wave
+// of each SIMD issues MFMAs while its partner issues exponentials
+// (MI355X_MICROARCH.md 'Two waves per SIMD').  Half A stages the K/V tiles by
+// LDS-DMA into a PB2_RING-slot ring: tiles 2j+6, 2j+7 at the start of M(j),
+// into the slots of pair j-3, which half B last read in V(j-2).  A leftover
+// odd tile and the ragged last tile run after the loop with every wave at
+// once.  Row sums on v_mfma_f32_16x16x32 with a selector A operand: the P^T
+// fragment (32x32x16 B layout: lane L = query L%32, keys 8*(L/32)..+8) read as
+// a 16x16x32 B operand puts query L%32 at column L%16 in k-group L/16, so
+// queries q < 16 sit in k-groups 0, 2 and q >= 16 in k-groups 1, 3; selector
+// rows 0 / 1 pick them (D[0][n] = query n, D[1][n] = query n + 16).
 // ---------------------------------------------------------------------------
-constexpr int PPR = 6;   // K/V ring slots (8 KB per tile)
+constexpr int PB2_RING = 10;
+constexpr float kF16Top = 15.f;
+constexpr float kF16MinSum = 0.015625f;
 
 __device__ __forceinline__ void pp_barrier() {
     __builtin_amdgcn_sched_barrier(0);
@@ -658,376 +702,55 @@ __device__ __forceinline__ void pp_load_v(const char* Vt, const PpLane& l, typen
         }
 }
 
-// M segment on prefetched fragments: QK^T (accumulator init -m_run) into s
-// (QK = true), then O += V^T P^T and the row sums of the previous tile's P
-// (PV = true) -- MFMAs only.
-template <typename T, bool QK, bool PV>
-__device__ __forceinline__ void pp_mseg(const typename mfma_traits<T>::frag (&kf)[2][2],
-                                        const typename mfma_traits<T>::frag (&vf)[2][2],
-                                        const typename mfma_traits<T>::frag (&qf)[2], const f32x16& negm,
-                                        const typename mfma_traits<T>::frag (&pf)[2][2], f32x16 (&s)[2], f32x16& o,
-                                        f32x16& lsum) {
-    typedef typename mfma_traits<T>::frag frag;
-    if (QK) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            s[kb] = mfma_traits<T>::mma(kf[kb][0], qf[0], negm);
-            s[kb] = mfma_traits<T>::mma(kf[kb][1], qf[1], s[kb]);
-        }
-    }
-    if (PV) {
-        frag ones;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                o = mfma_traits<T>::mma(vf[kb][ss], pf[kb][ss], o);
-                lsum = mfma_traits<T>::mma(ones, pf[kb][ss], lsum);
-            }
-    }
-}
-
-// V segment: softmax of one full tile's scores (s' = s - m_run from the MFMA) into P.
-template <typename T, bool FOLD>
-__device__ __forceinline__ void pp_vseg(f32x16 (&s)[2], typename mfma_traits<T>::frag (&pf)[2][2], f32x16& o,
-                                        f32x16& lsum, f32x16& negm, float& m_run, bool online, bool first, float c) {
-    const float u = FOLD ? 1.f : c;   // s' units -> exp2 units
-    if (online) {
-        float m0 = vmax(s[0][0], s[0][1]), m1 = vmax(s[1][0], s[1][1]);
-#pragma unroll
-        for (int r = 2; r < 16; r += 2) {
-            m0 = vmax3(m0, s[0][r], s[0][r + 1]);
-            m1 = vmax3(m1, s[1][r], s[1][r + 1]);
-        }
-        const float mt = pair_max(vmax(m0, m1));
-        if (first || __any(mt > (FOLD ? kDeferMax : kDeferMax / c))) {
-            const float d = first ? mt : vmax(mt, 0.f);
-            // first tile: O and the sums are still 0 and -d may be huge (exp2 overflow -> 0*inf)
-            const float alpha = first ? 1.f : __builtin_amdgcn_exp2f(-d * u);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                o[r] *= alpha;
-                lsum[r] *= alpha;
-                s[0][r] -= d;
-                s[1][r] -= d;
-            }
-            m_run += d;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) negm[r] = -m_run;
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[0][r] : s[0][r] * u);
-        pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(FOLD ? s[1][r] : s[1][r] * u);
-    }
-}
-
-// Wave-wide max of the max-|k|^2 partials (each covers kmax_rows key rows)
-// over the key range of this workgroup's split of batch b, head h: the bound
-// only has to hold for the keys this workgroup scores (the split combine
-// merges per-split offsets).  16 independent loads per lane in flight; the
-// first form reduced all Nk / kmax_rows partials of the head in every wave
-// (2048 waves x 882 scattered loads at the fusion shape, ~4 us of prologue).
-__device__ __forceinline__ float kmax_reduce(const AttnKParams& p, int b, int h, int split, int lane) {
-    const int key0 = split * p.tiles_per_split * KT;
-    const int key1 = min(p.Nk, key0 + p.tiles_per_split * KT);
-    if (key0 >= key1) return 0.f;
-    const int64_t r0 = (int64_t)b * p.Nk;
-    const int e0 = (int)((r0 + key0) / p.kmax_rows), e1 = (int)((r0 + key1 - 1) / p.kmax_rows);
-    const float* src = p.kmax2 + p.kmax_plane0 + h;
-    float km = 0.f;
-    for (int base = e0 + lane; base <= e1; base += 64 * 16) {
-        float v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int e = base + 64 * j;
-            v[j] = e <= e1 ? src[(int64_t)e * p.kmax_ld] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) km = fmaxf(km, v[j]);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) km = fmaxf(km, __shfl_xor(km, off));
-    return km;
-}
-
-template <int N>
-__device__ __forceinline__ void pp_wait_n() {
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
-}
-
-// tiles still allowed in flight (two LDS-DMA pieces each) behind the one needed now
-__device__ __forceinline__ void pp_wait(int tiles) {
-    static_assert(PPR - 3 == 3, "wait ladder below covers 0..3 tiles");
-    if (tiles >= 3) pp_wait_n<6>();
-    else if (tiles == 2) pp_wait_n<4>();
-    else if (tiles == 1) pp_wait_n<2>();
-    else pp_wait_n<0>();
-}
-
-// OCC = workgroups per CU the register budget is sized for (1: <= 256 VGPRs,
-// 2: <= 128 VGPRs, 4 waves per SIMD)
-template <typename T, bool FOLD, int OCC>
-__global__ __launch_bounds__(512, 2 * OCC) void attn_pp_kernel(AttnKParams p) {
-    typedef typename mfma_traits<T>::frag frag;
-    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
-    __shared__ __attribute__((aligned(16))) T ring[PPR * STAGE];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool hb = wave >= 4;          // wave-uniform: second half runs one segment behind
-    const int lr = lane & 31;
-    const int lh = lane >> 5;
-
-    // XCD-aware block order: the query blocks of one (b, h, split) -- which
-    // stream the same K/V -- are consecutive logical blocks on one XCD (L2).
-    const int nwg = gridDim.x;
-    const int orig = blockIdx.x;
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int qb = wg % p.nqb;
-    const int rest = wg / p.nqb;
-    const int BH = p.B * p.H;
-    const int bh = rest % BH;
-    const int split = rest / BH;
-    const int b = bh / p.H;
-    const int h = bh - b * p.H;
-
-    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
-    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
-    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
-    const float c = p.c;
-
-    // ---- Q^T fragments (B operand), ordinary loads: all before the first LDS-DMA
-    const int q = qb * (8 * QW) + wave * QW + lr;
-    const int qc = q < p.Nq ? q : p.Nq - 1;
-    frag qf[2];
-    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-    if (FOLD) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
-    }
-
-    f32x16 o, lsum, negm;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        o[r] = 0.f;
-        lsum[r] = 0.f;
-        negm[r] = 0.f;
-    }
-    float m_run = 0.f;   // online: placeholder until the first tile sets it
-    bool online = true;
-    if (p.kmax2 != nullptr) {
-        // max |k|^2 over this split's key rows
-        const float km = kmax_reduce(p, b, h, split, lane);
-        float qq = 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
-        qq = pair_sum(qq);
-        // >= max_k q.k in the MFMA's units (the margin covers fp32 accumulation)
-        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
-        const float u = FOLD ? 1.f : c;
-        if (__all(bound * u <= kBoundMax)) {
-            online = false;
-            m_run = bound;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) negm[r] = -bound;
-        }
-    }
-
-    const int ntiles = (p.Nk + KT - 1) / KT;
-    const int t_begin = split * p.tiles_per_split;
-    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
-    const bool tail = (p.Nk % KT) != 0 && t_end == ntiles && t_begin < t_end;   // ragged last tile here
-    const int nt = max(0, t_end - t_begin - (tail ? 1 : 0));                    // full tiles
-
-    // half A's two 1-KB pieces of every tile: K and V rows (wave & 3) * 16 .. +15
-    // of the tile, issued in tile order from running source pointers (full
-    // tiles only: no clamp), into compile-time ring slots
-    const int crow = lane >> 2, cch = lane & 3;
-    const int prow = (wave & 3) * 16 + crow;
-    const T* ksrc = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
-    const T* vsrc = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
-    const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
-    T* const my_k = ring + (wave & 3) * 16 * D;      // this wave's piece of slot 0 (K), + KT*D for V
-    auto issue_next = [&](int slot) {
-        dma16(ksrc, my_k + slot * STAGE);
-        dma16(vsrc, my_k + slot * STAGE + KT * D);
-        ksrc += kstep;
-        vsrc += vstep;
-    };
-
-    const char* const rb = (const char*)ring;
-    constexpr int STAGE_B = STAGE * (int)sizeof(T), KV_B = KT * D * (int)sizeof(T);
-    const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
-    f32x16 s[2];
-    frag pf[2][2], kf[2][2], vf[2][2];
-    if (!hb) {
-#pragma unroll
-        for (int i = 0; i < PPR - 2; ++i)
-            if (i < nt) issue_next(i);
-    } else {
-        pp_barrier();   // half B: one segment behind
-    }
-    // Tile t is complete for every wave from window 2t-1 on (half A waits
-    // before that barrier): the V segment of tile t-1 prefetches K(t) and
-    // V(t-1) into registers, so each M segment is MFMAs only.
-    if (nt > 0) {
-        // M(0): QK^T of tile 0
-        if (!hb) pp_wait(min(nt - 1, PPR - 3));
-        pp_barrier();
-        if (!hb && PPR - 2 < nt) issue_next(PPR - 2);
-        pp_load_k<T>(rb, lane_ofs, kf);
-        pp_mseg<T, true, false>(kf, vf, qf, negm, pf, s, o, lsum);
-        // V(0)
-        if (!hb && nt > 1) pp_wait(min(nt - 1, PPR - 2) - 1);
-        pp_barrier();
-        pp_vseg<T, FOLD>(s, pf, o, lsum, negm, m_run, online, true, c);
-        {
-            const PpLane l = lane_ofs;
-            pp_load_k<T>(rb + 1 * STAGE_B, l, kf);   // stale (unused) when nt == 1
-            pp_load_v<T>(rb + KV_B, l, vf);
-        }
-        // slots as wave-uniform counters: K of tile i+1, V of tile i, DMA target of tile i+PPR-2
-        int kslot = 1, vslot = 0, islot = PPR - 1;
-        for (int i = 1; i < nt; ++i) {
-            // M(i): QK^T of tile i, PV of tile i-1
-            pp_barrier();
-            if (!hb && i + PPR - 2 < nt) issue_next(islot);
-            pp_mseg<T, true, true>(kf, vf, qf, negm, pf, s, o, lsum);
-            // V(i): softmax of tile i; prefetch K(i+1) (stale after the last tile) and V(i)
-            if (!hb && i + 1 < nt) pp_wait(min(nt - 1, i + PPR - 2) - (i + 1));
-            pp_barrier();
-            pp_vseg<T, FOLD>(s, pf, o, lsum, negm, m_run, online, false, c);
-            kslot = kslot == PPR - 1 ? 0 : kslot + 1;
-            vslot = vslot == PPR - 1 ? 0 : vslot + 1;
-            islot = islot == PPR - 1 ? 0 : islot + 1;
-            const PpLane l = lane_ofs;
-            pp_load_k<T>(rb + kslot * STAGE_B, l, kf);
-            pp_load_v<T>(rb + vslot * STAGE_B + KV_B, l, vf);
-        }
-        // last M: PV of tile nt-1
-        pp_barrier();
-        pp_mseg<T, false, true>(kf, vf, qf, negm, pf, s, o, lsum);
-    }
-    if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
-
-    if (tail) {
-        // ragged last tile: masked, every wave at once (slots are free: all waves passed the last barrier)
-        pp_barrier();
-        if (!hb) {
-            const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked in compute
-            const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
-            const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
-            dma16(ks, my_k);
-            dma16(vs, my_k + KT * D);
-            pp_wait_n<0>();
-        }
-        pp_barrier();
-        attn_tile_lowp<T, true, FOLD>(ring, ring + KT * D, qf, o, lsum, negm, m_run, nt == 0, c, (ntiles - 1) * KT,
-                                      p.Nk, lane);
-    }
-
-    // ---- write ---------------------------------------------------------------
-    const float l_tot = lsum[0];
-    if (q >= p.Nq) return;
-    if (p.splits == 1) {
-        const float inv = 1.f / l_tot;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-            if (p.round_out) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
-            }
-            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
-        }
-    } else {
-        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
-        float* dst = p.Op + row * D;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
-        }
-        if (lh == 0) {
-            p.Mp[row] = FOLD ? m_run : m_run * c;   // exp2 units for the combine
-            p.Lp[row] = l_tot;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Offset-free ping-pong kernel: the bf16 long-key cross-attention with the
-// max-|k| partials (bounded mode).  Same ping-pong windows, LDS-DMA ring and
-// prefetched fragments as attn_pp_kernel; what differs:
-//  * no softmax offset on the fast path.  When every query of the wave has
-//    |q| max|k| <= kBoundMax (exp2 units; Q carries the folded scale), every
-//    score satisfies |s| <= 60, so P = exp2(s) lies in [2^-60, 2^60] -- a
-//    normal bf16 / f32 number whose relative rounding does not depend on its
-//    magnitude -- and O = sum(P V) / sum(P) needs no offset (it cancels).  The
-//    QK^T MFMAs start from a zero accumulator: no -m register block, no VALU
-//    subtraction, no max tree, no rescale.
-//  * a wave whose bound is larger tracks an online running max as ONE
-//    register per lane, subtracted on the VALU (exact lazy rescale, deferred
-//    by kDeferMax) -- the slow path, never taken on the decoder's data.
-//  * row sums: RSUM 0 on the MFMA pipe (ones . P^T), RSUM 1 as f32 VALU adds
-//    of P before rounding, RSUM 2 as v_dot2 of the rounded bf16 P; for 1 and 2
-//    each lane sums its own 32 keys of the tile (one register) and the lane
-//    pair is added once at the end.
-// ---------------------------------------------------------------------------
-template <int RSUM> struct pb_lsum { typedef float type; };
-template <> struct pb_lsum<0> { typedef f32x16 type; };
-template <> struct pb_lsum<3> { typedef f32x4 type; };
-
-// RSUM 3: row sums on v_mfma_f32_16x16x32 (16 cycles, half the 32x32x16 ones-MFMA).  The P^T
-// fragment (32x32x16 B layout: lane L = query L%32, keys 8*(L/32)..+8) read as a 16x16x32 B
-// operand puts query L%32 at column L%16 in k-group L/16, so queries q < 16 sit in k-groups 0, 2
-// and q >= 16 in k-groups 1, 3.  Selector rows: A[0][k] = 1 on groups 0, 2, A[1][k] = 1 on 1, 3;
-// D[0][n] accumulates query n, D[1][n] query n + 16 (lane n, registers 0 and 1).
-__device__ __forceinline__ bf16x8 rs16_selector(int lane) {
+// row-sum selector (see above) and the 16x16x32 row-sum MFMA in T
+template <typename T>
+__device__ __forceinline__ typename mfma_traits<T>::frag rs16_selector(int lane) {
     const int m = lane & 15, g = lane >> 4;
-    const bf16_t v = (bf16_t)((m == 0 && (g & 1) == 0) || (m == 1 && (g & 1) == 1) ? 1.f : 0.f);
-    bf16x8 a;
+    const T v = (T)((m == 0 && (g & 1) == 0) || (m == 1 && (g & 1) == 1) ? 1.f : 0.f);
+    typename mfma_traits<T>::frag a;
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = v;
     return a;
 }
-// query lr's row sum from the RSUM 3 accumulator
+template <typename T>
+__device__ __forceinline__ f32x4 rs16_mma(const typename mfma_traits<T>::frag& pf, f32x4 l, int lane) {
+    if constexpr (std::is_same<T, bf16_t>::value)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(rs16_selector<T>(lane), pf, l, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(rs16_selector<T>(lane), pf, l, 0, 0, 0);
+}
+// query lr's row sum from the row-sum accumulator
 __device__ __forceinline__ float rs16_total(const f32x4& l, int lane) {
     const int src = lane & 15;
     const float a0 = __shfl(l[0], src), a1 = __shfl(l[1], src);
     return (lane & 31) < 16 ? a0 : a1;
 }
-// online-max rescale of the RSUM 3 accumulator (alpha is per query = per lane L%32)
+// online-max rescale of the row-sum accumulator (alpha is per query = per lane L%32)
 __device__ __forceinline__ void rs16_scale(f32x4& l, float alpha, int lane) {
     const float hi = __shfl(alpha, (lane & 15) + 16);
     l[0] *= alpha;
     l[1] *= hi;
 }
 
-template <typename T, bool QK, bool PV, int RSUM>
+// M segment of one tile on prefetched fragments: S^T = K Q^T into s (QK;
+// accumulator init sinit; QS adds the lo half of Q), then O^T += V^T P^T and
+// the row sums of the previous tile's P (PV) -- MFMAs only.
+template <typename T, bool QK, bool PV, bool QS>
 __device__ __forceinline__ void pb_mseg(const typename mfma_traits<T>::frag (&kf)[2][2],
                                         const typename mfma_traits<T>::frag (&vf)[2][2],
                                         const typename mfma_traits<T>::frag (&qf)[2],
+                                        const typename mfma_traits<T>::frag (&ql)[2], const f32x16& sinit,
                                         const typename mfma_traits<T>::frag (&pf)[2][2], f32x16 (&s)[2], f32x16& o,
-                                        typename pb_lsum<RSUM>::type& lsum) {
-    typedef typename mfma_traits<T>::frag frag;
+                                        f32x4& lsum) {
     if (QK) {
-        const f32x16 zero = {};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-            s[kb] = mfma_traits<T>::mma(kf[kb][0], qf[0], zero);
+            s[kb] = mfma_traits<T>::mma(kf[kb][0], qf[0], sinit);
             s[kb] = mfma_traits<T>::mma(kf[kb][1], qf[1], s[kb]);
+            if constexpr (QS) {
+                s[kb] = mfma_traits<T>::mma(kf[kb][0], ql[0], s[kb]);
+                s[kb] = mfma_traits<T>::mma(kf[kb][1], ql[1], s[kb]);
+            }
         }
     }
     if (PV) {
@@ -1036,378 +759,64 @@ __device__ __forceinline__ void pb_mseg(const typename mfma_traits<T>::frag (&kf
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 o = mfma_traits<T>::mma(vf[kb][ss], pf[kb][ss], o);
-                if constexpr (RSUM == 0) {
-                    frag ones;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) ones[j] = (T)1.f;
-                    lsum = mfma_traits<T>::mma(ones, pf[kb][ss], lsum);
-                }
-                if constexpr (RSUM == 3)
-                    lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rs16_selector(lane_id()), pf[kb][ss], lsum, 0, 0, 0);
+                lsum = rs16_mma<T>(pf[kb][ss], lsum, lane_id());
             }
     }
 }
 
-// V segment: P = exp2(s) (fast) or exp2(s - m) with the online max (fallback);
-// row sums for RSUM 1 / 2.  ``first``: the wave's first tile (sets m).
-template <typename T, int RSUM>
-__device__ __forceinline__ void pb_vseg(f32x16 (&s)[2], typename mfma_traits<T>::frag (&pf)[2][2], f32x16& o,
-                                        typename pb_lsum<RSUM>::type& lsum, float& m_run, bool fast, bool first) {
-    if (!fast) {
-        float m0 = vmax(s[0][0], s[0][1]), m1 = vmax(s[1][0], s[1][1]);
+// online-max step over the scores of NT tiles (slow path): raise m_run when a
+// score exceeds it by more than kDeferMax (always on the first tiles), rescale
+// O and the row sums, subtract m_run from the scores
+template <int NTL>
+__device__ __forceinline__ void pb_online(f32x16* const (&s)[NTL], f32x16& o, f32x4& lsum, float& m_run, bool first) {
+    float m = -__builtin_inff();
 #pragma unroll
-        for (int r = 2; r < 16; r += 2) {
-            m0 = vmax3(m0, s[0][r], s[0][r + 1]);
-            m1 = vmax3(m1, s[1][r], s[1][r + 1]);
-        }
-        const float mt = pair_max(vmax(m0, m1));
-        if (first) {
-            m_run = mt;
-        } else if (__any(mt > m_run + kDeferMax)) {
-            const float mn = vmax(m_run, mt);
-            const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
-            o *= alpha;
-            if constexpr (RSUM == 3) rs16_scale(lsum, alpha, lane_id());
-            else lsum *= alpha;
-            m_run = mn;
-        }
+    for (int t = 0; t < NTL; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            s[0][r] -= m_run;
-            s[1][r] -= m_run;
-        }
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) m = vmax3(m, s[t][kb][r], s[t][kb][r + 1]);
+    const float mt = pair_max(m);
+    if (first) {
+        m_run = mt;
+    } else if (__any(mt > m_run + kDeferMax)) {
+        const float mn = vmax(m_run, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+        o *= alpha;
+        rs16_scale(lsum, alpha, lane_id());
+        m_run = mn;
     }
-    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[t][kb][r] -= m_run;
+}
+
+// V segment of one tile: P = exp2(s) into the fragments (fast) or after the online step
+template <typename T>
+__device__ __forceinline__ void pb_vseg(f32x16 (&s)[2], typename mfma_traits<T>::frag (&pf)[2][2], f32x16& o,
+                                        f32x4& lsum, float& m_run, bool fast, bool first) {
+    if (!fast) {
+        f32x16* const ss[1] = {s};
+        pb_online<1>(ss, o, lsum, m_run, first);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const float e0 = __builtin_amdgcn_exp2f(s[0][r]);
-        const float e1 = __builtin_amdgcn_exp2f(s[1][r]);
-        pf[0][r >> 3][r & 7] = (T)e0;
-        pf[1][r >> 3][r & 7] = (T)e1;
-        if constexpr (RSUM == 1) {
-            a0 += e0;
-            a1 += e1;
-        }
-    }
-    if constexpr (RSUM == 1) lsum += a0 + a1;
-    if constexpr (RSUM == 2) {
-        typedef T t2 __attribute__((ext_vector_type(2)));
-        const t2 one2 = {(T)1.f, (T)1.f};
-        float acc = lsum;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const t2 pr = {pf[kb][ss][2 * j], pf[kb][ss][2 * j + 1]};
-                    if constexpr (std::is_same<T, bf16_t>::value)
-                        acc = __builtin_amdgcn_fdot2_f32_bf16(pr, one2, acc, false);
-                    else
-                        acc = __builtin_amdgcn_fdot2(pr, one2, acc, false);
-                }
-        lsum = acc;
+        pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[0][r]);
+        pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[1][r]);
     }
 }
 
-template <typename T, int RSUM, int OCC, int STAMP = 0>
-__global__ __launch_bounds__(512, 2 * OCC) void attn_pb_kernel(AttnKParams p) {
-    typedef typename mfma_traits<T>::frag frag;
-    typedef typename pb_lsum<RSUM>::type LT;
-    unsigned long long t_entry = 0;
-    if constexpr (STAMP != 0) t_entry = stamp_now();
-    unsigned long long r_entry = 0;
-    if constexpr (STAMP == 2) r_entry = __builtin_amdgcn_s_memrealtime();
-    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
-    __shared__ __attribute__((aligned(16))) T ring[PPR * STAGE];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool hb = wave >= 4;          // wave-uniform: second half runs one segment behind
-    const int lr = lane & 31;
-    const int lh = lane >> 5;
-
-    // XCD-aware block order (as attn_pp_kernel)
-    const int nwg = gridDim.x;
-    const int orig = blockIdx.x;
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int qb = wg % p.nqb;
-    const int rest = wg / p.nqb;
-    const int BH = p.B * p.H;
-    const int bh = rest % BH;
-    const int split = rest / BH;
-    const int b = bh / p.H;
-    const int h = bh - b * p.H;
-
-    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
-    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
-    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
-    const float c = p.c;
-
-    const int ntiles = (p.Nk + KT - 1) / KT;
-    const int t_begin = split * p.tiles_per_split;
-    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
-    const bool tail = (p.Nk % KT) != 0 && t_end == ntiles && t_begin < t_end;   // ragged last tile here
-    const int nt = max(0, t_end - t_begin - (tail ? 1 : 0));                    // full tiles
-
-    const int crow = lane >> 2, cch = lane & 3;
-    const int prow = (wave & 3) * 16 + crow;
-    const T* ksrc = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
-    const T* vsrc = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
-    const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
-    T* const my_k = ring + (wave & 3) * 16 * D;
-    auto issue_next = [&](int slot) {
-        dma16(ksrc, my_k + slot * STAGE);
-        dma16(vsrc, my_k + slot * STAGE + KT * D);
-        ksrc += kstep;
-        vsrc += vstep;
-    };
-
-    const char* const rb = (const char*)ring;
-    constexpr int STAGE_B = STAGE * (int)sizeof(T), KV_B = KT * D * (int)sizeof(T);
-    const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
-    f32x16 s[2];
-    frag pf[2][2], kf[2][2], vf[2][2];
-    // the first tiles' LDS-DMA goes out before the Q / max-|k| loads: their
-    // latencies overlap (the compiler's waits for Q also cover these earlier
-    // pieces; pp_wait below then sees only LDS-DMA in flight)
-    if (!hb) {
-#pragma unroll
-        for (int i = 0; i < PPR - 2; ++i)
-            if (i < nt) issue_next(i);
-    }
-
-    // ---- Q^T fragments with the folded scale (s is in exp2 units)
-    const int q = qb * (8 * QW) + wave * QW + lr;
-    const int qc = q < p.Nq ? q : p.Nq - 1;
-    frag qf[2];
-    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
-
-    // ---- fast path iff |q| max|k| <= kBoundMax for every query of the wave
-    bool fast;
-    {
-        const float km = kmax_reduce(p, b, h, split, lane);
-        float qq = 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
-        qq = pair_sum(qq);
-        // km is the max squared norm of the UNSCALED keys; q already carries c
-        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
-        fast = __all(bound <= kBoundMax);
-    }
-
-    f32x16 o;
-    LT lsum;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    lsum = LT{};
-    float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tile
-
-    unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};   // STAMP 1: prologue points
-    if constexpr (STAMP == 1) tp[0] = stamp_now();
-    // static priority of one half for the whole loop (MI355X_MICROARCH.md 'Two waves per SIMD'
-    // item 4: the second-dispatched half loses every VALU arbitration at equal priority)
-    if ((p.prio == 1 && hb) || (p.prio == 2 && !hb)) __builtin_amdgcn_s_setprio(1);
-    if (hb) pp_barrier();   // half B: one segment behind
-    if (nt > 0) {
-        if (!hb) pp_wait(min(nt - 1, PPR - 3));
-        if constexpr (STAMP == 1) tp[1] = stamp_now();
-        pp_barrier();
-        if constexpr (STAMP == 1) tp[2] = stamp_now();
-        if (!hb && PPR - 2 < nt) issue_next(PPR - 2);
-        pp_load_k<T>(rb, lane_ofs, kf);
-        pb_mseg<T, true, false, RSUM>(kf, vf, qf, pf, s, o, lsum);
-        if (!hb && nt > 1) pp_wait(min(nt - 1, PPR - 2) - 1);
-        if constexpr (STAMP == 1) tp[3] = stamp_now();
-        pp_barrier();
-        if constexpr (STAMP == 1) tp[4] = stamp_now();
-        pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, true);
-        {
-            const PpLane l = lane_ofs;
-            pp_load_k<T>(rb + 1 * STAGE_B, l, kf);   // stale (unused) when nt == 1
-            pp_load_v<T>(rb + KV_B, l, vf);
-        }
-        int kslot = 1, vslot = 0, islot = PPR - 1;
-        // STAMP: [0] barrier 1 + DMA issue, [1] M segment issue, [2] DMA wait + barrier 2,
-        // [3] V segment, [4] fragment loads, [5] iterations, [6] whole loop
-        unsigned long long st[7] = {0, 0, 0, 0, 0, 0, 0};
-        unsigned long long tl0 = 0;
-        if constexpr (STAMP == 1) tl0 = stamp_now();
-        for (int i = 1; i < nt; ++i) {
-            unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-            if constexpr (STAMP == 1) t0 = stamp_now();
-            pp_barrier();
-            if (!hb && i + PPR - 2 < nt) issue_next(islot);
-            if constexpr (STAMP == 1) t1 = stamp_now();
-            pb_mseg<T, true, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
-            if constexpr (STAMP == 1) t2 = stamp_now();
-            if (!hb && i + 1 < nt) pp_wait(min(nt - 1, i + PPR - 2) - (i + 1));
-            pp_barrier();
-            if constexpr (STAMP == 1) t3 = stamp_now();
-            kslot = kslot == PPR - 1 ? 0 : kslot + 1;
-            vslot = vslot == PPR - 1 ? 0 : vslot + 1;
-            islot = islot == PPR - 1 ? 0 : islot + 1;
-            const PpLane l = lane_ofs;
-            pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, false);
-            if constexpr (STAMP == 1) t4 = stamp_now();
-            pp_load_k<T>(rb + kslot * STAGE_B, l, kf);
-            pp_load_v<T>(rb + vslot * STAGE_B + KV_B, l, vf);
-            if constexpr (STAMP == 1) {
-                const unsigned long long t5 = stamp_now();
-                st[0] += t1 - t0; st[1] += t2 - t1; st[2] += t3 - t2; st[3] += t4 - t3; st[4] += t5 - t4;
-                st[5] += 1;
-            }
-        }
-        if constexpr (STAMP == 1) {
-            st[6] = stamp_now() - tl0;
-            if (lane == 0) {
-                unsigned long long* dst = p.stamp + ((int64_t)orig * 8 + wave) * kStampSlots;
-#pragma unroll
-                for (int j = 0; j < 7; ++j) dst[j] = st[j];
-                dst[7] = tl0 - t_entry;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) dst[10 + j] = tp[j] - t_entry;
-            }
-        }
-        pp_barrier();
-        pb_mseg<T, false, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
-    }
-    if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
-
-    if (tail) {
-        // ragged last tile: masked, every wave at once
-        pp_barrier();
-        if (!hb) {
-            const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked below
-            const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
-            const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
-            dma16(ks, my_k);
-            dma16(vs, my_k + KT * D);
-            pp_wait_n<0>();
-        }
-        pp_barrier();
-        const PpLane l = lane_ofs;
-        pp_load_k<T>(rb, l, kf);
-        pp_load_v<T>(rb + KV_B, l, vf);
-        pb_mseg<T, true, false, RSUM>(kf, vf, qf, pf, s, o, lsum);
-        const int key0 = (ntiles - 1) * KT;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s[kb][r] = -__builtin_inff();
-        pb_vseg<T, RSUM>(s, pf, o, lsum, m_run, fast, nt == 0);
-        pb_mseg<T, false, true, RSUM>(kf, vf, qf, pf, s, o, lsum);
-    }
-
-    // ---- write ---------------------------------------------------------------
-    float l_tot;
-    if constexpr (RSUM == 0) l_tot = lsum[0];
-    else l_tot = pair_sum(lsum);
-    if constexpr (STAMP != 0) {
-        const unsigned long long t_end = stamp_now();
-        unsigned long long r_end = 0;
-        if constexpr (STAMP == 2) r_end = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            unsigned long long* dst = p.stamp + ((int64_t)orig * 8 + wave) * kStampSlots;
-            dst[8] = t_end - t_entry;
-            dst[9] = STAMP == 2 ? r_end - r_entry : t_entry;
-        }
-    }
-    if (q >= p.Nq) return;
-    if (p.splits == 1) {
-        const float inv = 1.f / l_tot;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-            if (p.round_out) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
-            }
-            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
-        }
-    } else {
-        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
-        float* dst = p.Op + row * D;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
-        }
-        if (lh == 0) {
-            p.Mp[row] = m_run;   // exp2 units (0 on the fast path)
-            p.Lp[row] = l_tot;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Paired-tile form of attn_pb_kernel: every ping-pong window covers TWO 64-key
-// tiles (M: 8 QK^T + 16 PV / row-sum MFMAs; V: 64 exp2 + 32 packs), so the
-// per-window costs -- the barrier hand-off, the segment-start VALU penalty,
-// the LDS fragment reads' latency (MI355X_MICROARCH.md 'Two waves per SIMD'
-// items 6-7) -- are paid once per 128 keys instead of once per 64.  The K/V
-// ring grows to PB2_RING slots: half A issues tiles 2j+6 and 2j+7 at the start
-// of its M(j), into the slots of pair j-3, which half B (one segment behind)
-// last read in its V(j-2).  Same per-score math and the same tile order of the
-// PV / row-sum accumulation as attn_pb_kernel (bit-identical on the offset-free
-// path); on the online-max fallback one offset update covers both tiles of a
-// pair.  A leftover odd tile and the ragged last tile run after the loop with
-// every wave at once.  Row sums on the MFMA pipe only (RSUM 0).
-// ---------------------------------------------------------------------------
-constexpr int PB2_RING = 10;
-
-// tiles (two LDS-DMA pieces each) still allowed in flight behind the ones needed now, 0..4
-__device__ __forceinline__ void pb2_wait(int tiles) {
-    if (tiles >= 4) pp_wait_n<8>();
-    else if (tiles == 3) pp_wait_n<6>();
-    else if (tiles == 2) pp_wait_n<4>();
-    else if (tiles == 1) pp_wait_n<2>();
-    else pp_wait_n<0>();
-}
-
-// V segment of a pair: P = exp2(s) (offset-free) or exp2(s - m) with ONE online-max update for both tiles
-template <typename T, int RSUM>
+// V segment of a pair, ONE online-max update for both tiles on the slow path
+template <typename T>
 __device__ __forceinline__ void pb2_vseg(f32x16 (&s0)[2], f32x16 (&s1)[2], typename mfma_traits<T>::frag (&pf0)[2][2],
-                                         typename mfma_traits<T>::frag (&pf1)[2][2], f32x16& o,
-                                         typename pb_lsum<RSUM>::type& lsum, float& m_run, bool fast, bool first) {
+                                         typename mfma_traits<T>::frag (&pf1)[2][2], f32x16& o, f32x4& lsum,
+                                         float& m_run, bool fast, bool first) {
     if (!fast) {
-        float m0 = vmax(s0[0][0], s0[0][1]), m1 = vmax(s0[1][0], s0[1][1]);
-        float m2 = vmax(s1[0][0], s1[0][1]), m3 = vmax(s1[1][0], s1[1][1]);
-#pragma unroll
-        for (int r = 2; r < 16; r += 2) {
-            m0 = vmax3(m0, s0[0][r], s0[0][r + 1]);
-            m1 = vmax3(m1, s0[1][r], s0[1][r + 1]);
-            m2 = vmax3(m2, s1[0][r], s1[0][r + 1]);
-            m3 = vmax3(m3, s1[1][r], s1[1][r + 1]);
-        }
-        const float mt = pair_max(vmax(vmax(m0, m1), vmax(m2, m3)));
-        if (first) {
-            m_run = mt;
-        } else if (__any(mt > m_run + kDeferMax)) {
-            const float mn = vmax(m_run, mt);
-            const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
-            o *= alpha;
-            if constexpr (RSUM == 3) rs16_scale(lsum, alpha, lane_id());
-            else lsum *= alpha;
-            m_run = mn;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            s0[0][r] -= m_run;
-            s0[1][r] -= m_run;
-            s1[0][r] -= m_run;
-            s1[1][r] -= m_run;
-        }
+        f32x16* const ss[2] = {s0, s1};
+        pb_online<2>(ss, o, lsum, m_run, first);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1421,11 +830,22 @@ __device__ __forceinline__ void pb2_vseg(f32x16 (&s0)[2], f32x16 (&s1)[2], typen
     }
 }
 
-template <typename T, int OCC, int RSUM>
-__global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
+// tiles (two LDS-DMA pieces each) still allowed in flight behind the ones needed now, 0..4
+__device__ __forceinline__ void pb2_wait(int tiles) {
+    if (tiles >= 4) pp_wait_n<8>();
+    else if (tiles == 3) pp_wait_n<6>();
+    else if (tiles == 2) pp_wait_n<4>();
+    else if (tiles == 1) pp_wait_n<2>();
+    else pp_wait_n<0>();
+}
+
+template <typename T, bool QS>
+__global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
+    constexpr bool F16 = std::is_same<T, f16_t>::value;
     constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
     __shared__ __attribute__((aligned(16))) T ring[PB2_RING * STAGE];
+    __shared__ int redo;                // f16: some row of the workgroup needs the online-max pass
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1433,8 +853,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
     const bool hb = wave >= 4;          // wave-uniform: second half runs one segment behind
     const int lr = lane & 31;
     const int lh = lane >> 5;
+    if (tid == 0) redo = 0;
 
-    // XCD-aware block order (as attn_pb_kernel)
+    // XCD-aware block order: consecutive query blocks of one (b, h, split) on one XCD (shared K/V in its L2)
     const int nwg = gridDim.x;
     const int orig = blockIdx.x;
     const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -1449,7 +870,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
 
     // a wave whose 32 queries all lie past Nq (the padding of the last query block) keeps the
     // workgroup's barriers and LDS-DMA duties but skips its MFMAs, exponentials and fragment reads
-    const bool live = p.keep_dead || qb * (8 * QW) + wave * QW < p.Nq;
+    const bool live = qb * (8 * QW) + wave * QW < p.Nq;
     const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
     const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
     const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
@@ -1464,8 +885,10 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
 
     const int crow = lane >> 2, cch = lane & 3;
     const int prow = (wave & 3) * 16 + crow;
-    const T* ksrc = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
-    const T* vsrc = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
+    const T* const ksrc0 = Kb + (int64_t)(t_begin * KT + prow) * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+    const T* const vsrc0 = Vb + (int64_t)(t_begin * KT + prow) * p.v_rs + 8 * cch;
+    const T* ksrc = ksrc0;
+    const T* vsrc = vsrc0;
     const int64_t kstep = (int64_t)KT * p.k_rs, vstep = (int64_t)KT * p.v_rs;
     T* const my_k = ring + (wave & 3) * 16 * D;
     int issued = 0;   // tiles issued (half A)
@@ -1492,124 +915,162 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
     // ---- Q^T fragments with the folded scale (s is in exp2 units)
     const int q = qb * (8 * QW) + wave * QW + lr;
     const int qc = q < p.Nq ? q : p.Nq - 1;
-    frag qf[2];
-    qf[0] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-    qf[1] = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[i][j] = (T)((float)qf[i][j] * c);
-
-    // ---- fast path iff |q| max|k| <= kBoundMax for every query of the wave
-    bool fast;
+    frag qf[2], ql[2];
+    float qq = 0.f;
     {
+        const frag r0 = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
+        const frag r1 = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x0 = (float)r0[j] * c, x1 = (float)r1[j] * c;
+            qf[0][j] = (T)x0;
+            qf[1][j] = (T)x1;
+            ql[0][j] = (T)(x0 - (float)qf[0][j]);
+            ql[1][j] = (T)(x1 - (float)qf[1][j]);
+            const float e0 = QS ? x0 : (float)qf[0][j], e1 = QS ? x1 : (float)qf[1][j];
+            qq += e0 * e0 + e1 * e1;
+        }
+    }
+
+    // ---- offset mode: bounded (fast) iff partials are given (bf16: and every bound <= kBoundMax)
+    bool fast = false;
+    float off = 0.f;   // f16 fast path: the fixed offset bound - kF16Top
+    if (p.kmax2 != nullptr) {
         const float km = kmax_reduce(p, b, h, split, lane);
-        float qq = 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qq += (float)qf[i][j] * (float)qf[i][j];
-        qq = pair_sum(qq);
-        const float bound = sqrtf(qq * km) * 1.001f + 1e-6f;
-        fast = __all(bound <= kBoundMax);
+        const float bound = sqrtf(pair_sum(qq) * km) * 1.001f + 1e-6f;
+        if constexpr (F16) {
+            fast = true;
+            off = bound - kF16Top;
+        } else {
+            fast = __all(bound <= kBoundMax);
+        }
     }
+    f32x16 sinit;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sinit[r] = F16 && fast ? -off : 0.f;
 
-    static_assert(RSUM == 0 || RSUM == 3, "pb2: row sums on the MFMA pipe");
-    typedef typename pb_lsum<RSUM>::type LT;
     f32x16 o;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    LT lsum = LT{};
-    float m_run = 0.f;   // fast path: the offset stays 0; fallback: set by the first tiles
+    f32x4 lsum;
+    float m_run = 0.f;   // slow path: set by the first tiles
 
-    auto slot_b = [&](int t) { return rb + (t % PB2_RING) * STAGE_B; };
-    if (hb) pp_barrier();   // half B: one segment behind
-    if (np > 0) {
-        if (!hb) pb2_wait(issued - 2);                 // tiles 0, 1 landed
-        pp_barrier();
-        if (!hb) issue_upto(8);
-        {
-            const PpLane l = pp_launder(lane_ofs);
-            if (live) pp_load_k<T>(slot_b(0), l, kf0);
-            if (live) pp_load_k<T>(slot_b(1), l, kf1);
+    // One pass over the split's keys.  fastw: bounded offsets (else online max); livew: this wave
+    // computes (else it only keeps the barriers and, in half A, the LDS-DMA) and restarts O / l.
+    auto run = [&](bool fastw, bool livew) {
+        if (livew) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[r] = 0.f;
+            lsum = f32x4{0.f, 0.f, 0.f, 0.f};
+            m_run = 0.f;
         }
-        if (live) pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        if (live) pb_mseg<T, true, false, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
-        if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
-        pp_barrier();
-        if (live) pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, true);
-        {
-            const PpLane l = pp_launder(lane_ofs);
-            if (live) pp_load_k<T>(slot_b(2), l, kf0);   // stale (unused) when np == 1
-            if (live) pp_load_k<T>(slot_b(3), l, kf1);
-            if (live) pp_load_v<T>(slot_b(0) + KV_B, l, vf0);
-            if (live) pp_load_v<T>(slot_b(1) + KV_B, l, vf1);
-        }
-        for (int j = 1; j < np; ++j) {
+        auto slot_b = [&](int t) { return rb + (t % PB2_RING) * STAGE_B; };
+        if (hb) pp_barrier();   // half B: one segment behind
+        if (np > 0) {
+            if (!hb) pb2_wait(issued - 2);                 // tiles 0, 1 landed
             pp_barrier();
-            if (!hb) issue_upto(2 * j + 8);
-            if (live) pb_mseg<T, true, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);   // QK^T tile 2j, PV tile 2j-2
-            if (live) pb_mseg<T, true, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);   // QK^T tile 2j+1, PV tile 2j-1
-            if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
+            if (!hb) issue_upto(8);
+            {
+                const PpLane l = pp_launder(lane_ofs);
+                if (livew) pp_load_k<T>(slot_b(0), l, kf0);
+                if (livew) pp_load_k<T>(slot_b(1), l, kf1);
+            }
+            if (livew) pb_mseg<T, true, false, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
+            if (livew) pb_mseg<T, true, false, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
+            if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
             pp_barrier();
-            if (live) pb2_vseg<T, RSUM>(s0, s1, pf0, pf1, o, lsum, m_run, fast, false);
+            if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, true);
+            {
+                const PpLane l = pp_launder(lane_ofs);
+                if (livew) pp_load_k<T>(slot_b(2), l, kf0);   // stale (unused) when np == 1
+                if (livew) pp_load_k<T>(slot_b(3), l, kf1);
+                if (livew) pp_load_v<T>(slot_b(0) + KV_B, l, vf0);
+                if (livew) pp_load_v<T>(slot_b(1) + KV_B, l, vf1);
+            }
+            for (int j = 1; j < np; ++j) {
+                pp_barrier();
+                if (!hb) issue_upto(2 * j + 8);
+                if (livew) pb_mseg<T, true, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);   // QK^T 2j, PV 2j-2
+                if (livew) pb_mseg<T, true, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);   // QK^T 2j+1, PV 2j-1
+                if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
+                pp_barrier();
+                if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, false);
+                const PpLane l = pp_launder(lane_ofs);
+                if (livew) pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
+                if (livew) pp_load_k<T>(slot_b(2 * j + 3), l, kf1);
+                if (livew) pp_load_v<T>(slot_b(2 * j) + KV_B, l, vf0);
+                if (livew) pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
+            }
+            pp_barrier();
+            if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
+            if (livew) pb_mseg<T, false, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
+        }
+        if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
+
+        if (nt & 1) {
+            // leftover full tile (odd count): every wave at once
+            if (!hb) {
+                issue_upto(nt);
+                pp_wait_n<0>();
+            }
+            pp_barrier();
             const PpLane l = pp_launder(lane_ofs);
-            if (live) pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
-            if (live) pp_load_k<T>(slot_b(2 * j + 3), l, kf1);
-            if (live) pp_load_v<T>(slot_b(2 * j) + KV_B, l, vf0);
-            if (live) pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
+            if (livew) pp_load_k<T>(slot_b(nt - 1), l, kf0);
+            if (livew) pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
+            if (livew) pb_mseg<T, true, false, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
+            if (livew) pb_vseg<T>(s0, pf0, o, lsum, m_run, fastw, np == 0);
+            if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
         }
-        pp_barrier();
-        if (live) pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        if (live) pb_mseg<T, false, true, RSUM>(kf1, vf1, qf, pf1, s1, o, lsum);
-    }
-    if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
 
-    if (nt & 1) {
-        // leftover full tile (odd count): every wave at once
-        if (!hb) {
-            issue_upto(nt);
-            pp_wait_n<0>();
-        }
-        pp_barrier();
-        const PpLane l = pp_launder(lane_ofs);
-        if (live) pp_load_k<T>(slot_b(nt - 1), l, kf0);
-        if (live) pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
-        if (live) pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        if (live) pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, np == 0);
-        if (live) pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-    }
-
-    if (tail) {
-        // ragged last tile: masked, every wave at once
-        pp_barrier();
-        if (!hb) {
-            const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked below
-            const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
-            const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
-            dma16(ks, my_k);
-            dma16(vs, my_k + KT * D);
-            pp_wait_n<0>();
-        }
-        pp_barrier();
-        const PpLane l = pp_launder(lane_ofs);
-        if (live) pp_load_k<T>(rb, l, kf0);
-        if (live) pp_load_v<T>(rb + KV_B, l, vf0);
-        if (live) pb_mseg<T, true, false, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
-        const int key0 = (ntiles - 1) * KT;
+        if (tail) {
+            // ragged last tile: masked, every wave at once
+            pp_barrier();
+            if (!hb) {
+                const int key = min((ntiles - 1) * KT + prow, p.Nk - 1);   // clamped, masked below
+                const T* ks = Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((prow >> 2) & 3));
+                const T* vs = Vb + (int64_t)key * p.v_rs + 8 * cch;
+                dma16(ks, my_k);
+                dma16(vs, my_k + KT * D);
+                pp_wait_n<0>();
+            }
+            pp_barrier();
+            const PpLane l = pp_launder(lane_ofs);
+            if (livew) pp_load_k<T>(rb, l, kf0);
+            if (livew) pp_load_v<T>(rb + KV_B, l, vf0);
+            if (livew) pb_mseg<T, true, false, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
+            const int key0 = (ntiles - 1) * KT;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+            for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s0[kb][r] = -__builtin_inff();
-        if (live) pb_vseg<T, RSUM>(s0, pf0, o, lsum, m_run, fast, nt == 0);
-        if (live) pb_mseg<T, false, true, RSUM>(kf0, vf0, qf, pf0, s0, o, lsum);
+                for (int r = 0; r < 16; ++r)
+                    if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s0[kb][r] = -__builtin_inff();
+            if (livew) pb_vseg<T>(s0, pf0, o, lsum, m_run, fastw, nt == 0);
+            if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
+        }
+    };
+    run(fast, live);
+    float l_tot = rs16_total(lsum, lane);
+
+    if constexpr (F16) {
+        // a loose bound left some row's P too small for full f16 precision: those waves run the
+        // split again with the online max (every wave keeps the barriers and DMA duties)
+        const bool bad = fast && live && __any(!(l_tot >= kF16MinSum));
+        if (bad && lane == 0) redo = 1;
+        barrier_mem();   // every wave is past its last ring read and its vote is visible
+        if (redo) {
+            ksrc = ksrc0;
+            vsrc = vsrc0;
+            issued = 0;
+            if (!hb) issue_upto(PB2_RING - 4);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sinit[r] = 0.f;
+            run(false, bad);
+            if (bad) {
+                fast = false;
+                l_tot = rs16_total(lsum, lane);
+            }
+        }
     }
 
-    // ---- write (as attn_pb_kernel)
-    float l_tot;
-    if constexpr (RSUM == 3) l_tot = rs16_total(lsum, lane);
-    else l_tot = lsum[0];
+    // ---- write
     if (q >= p.Nq) return;
     if (p.splits == 1) {
         const float inv = 1.f / l_tot;
@@ -1631,7 +1092,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void attn_pb2_kernel(AttnKParams p) {
             *(f32x4*)(dst + 8 * g + 4 * lh) = v;
         }
         if (lh == 0) {
-            p.Mp[row] = m_run;   // exp2 units (0 on the fast path)
+            p.Mp[row] = fast ? off : m_run;   // exp2 units: the offset P was taken against
             p.Lp[row] = l_tot;
         }
     }
@@ -1842,172 +1303,29 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     store_o4(p, b, q, h * D + d4, r);
 }
 
-// Launch shape of the f16/bf16 kernel: waves per workgroup x query
-// sub-blocks per wave.  Long key ranges: 8 waves x 1 (256 queries share each
-// staged K/V tile, 2 waves per SIMD); short ones (self-attention): 4 x 1.
-// The 4 x 2 shape (two chains per wave) needs ~370 registers, and hipcc then
-// parks the accumulators in AGPRs and copies them back for every VALU use
-// (measured 125 us vs 79 us at the CMT-L cross-attention shape).
-struct LowpShape { int waves, sub; };
-LowpShape lowp_shape(const cmt_attn_args& a) {
-    // diagnostics: CMT_ATTN_SHAPE="waves,sub" (4|8, 1|2) overrides the choice
-    static const char* ov = getenv("CMT_ATTN_SHAPE");
-    if (ov && ov[0]) {
-        int w = 4, sb = 1;
-        if (sscanf(ov, "%d,%d", &w, &sb) == 2 && (w == 4 || w == 8) && (sb == 1 || sb == 2) && !(w == 8 && sb == 2))
-            return {w, sb};
-    }
-    if (a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128) return {8, 1};
-    return {4, 1};
-}
+// Path choice.  Long key ranges (the cross-attention shape) take the 8-wave
+// ping-pong kernel attn_pb2_kernel; short ones with at most 64 key tiles (the
+// self-attention) the in-workgroup key split attn_kw_kernel; anything else the
+// 4-wave single-phase attn_fwd_kernel with split partials.  f32 always takes
+// the exact-f32 kernel.
+bool use_long(const cmt_attn_args& a) { return a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128; }
 
-// The ping-pong kernel takes the 8 x 1 shape (long key ranges); CMT_ATTN_PP=0
-// selects the single-phase 8 x 1 kernel instead (diagnostics / A-B timing).
-// offset-free bounded kernel (attn_pb_kernel): workgroups per CU it is built
-// for (CMT_ATTN_OCC) and its row-sum form (CMT_ATTN_RSUM); diagnostics knobs
-int pp_occ() {
-    static const char* ov = getenv("CMT_ATTN_OCC");
-    return (ov && ov[0] == '2') ? 2 : 1;
-}
-int pb_rsum() {
-    static const char* ov = getenv("CMT_ATTN_RSUM");
-    return (ov && ov[0] >= '0' && ov[0] <= '2') ? ov[0] - '0' : 0;
-}
-
-bool use_pp(const cmt_attn_args& a) {
-    static const char* ov = getenv("CMT_ATTN_PP");
-    if (ov && ov[0] == '0') return false;
-    const LowpShape sh = lowp_shape(a);
-    return a.dtype != CMT_F32 && sh.waves == 8 && sh.sub == 1;
-}
-
-// the paired-tile form of the pb kernel (128 keys per ping-pong window); CMT_ATTN_PB2=0: one tile per window
-bool use_pb2() {
-    const char* ov = getenv("CMT_ATTN_PB2");   // read per call: the tests toggle it in one process
-    return !(ov && ov[0] == '0');
-}
-
-// pb2 row sums on the 16x16x32 MFMA (RSUM 3); CMT_ATTN_RS16=0: the 32x32x16 ones-MFMA
-bool pb2_rs16() {
-    const char* ov = getenv("CMT_ATTN_RS16");   // read per call: the tests toggle it in one process
-    return !(ov && ov[0] == '0');
-}
-
-// the bf16 long-key path with max-|k| partials and the folded scale
-bool use_pb(const cmt_attn_args& a) {
-    static const char* ov = getenv("CMT_ATTN_PB");
-    if (ov && ov[0] == '0') return false;
-    return use_pp(a) && a.dtype == CMT_BF16 && a.kmax2 != nullptr && (a.flags & CMT_ATTN_FOLD_SCALE);
-}
-
-// diagnostics: CMT_ATTN_STAMP=1 runs the stamped build of attn_pb_kernel and
-// prints its per-segment cycle shares (per wave and tile iteration) to stderr;
-// its run time is not the real kernel's (every stamp drains lgkmcnt)
-// CMT_ATTN_STAMP=2: entry / exit stamps only (shader clock and the 100 MHz
-// real-time counter: the effective clock of the real loop)
-int stamp_mode() {
-    static const char* ov = getenv("CMT_ATTN_STAMP");
-    return (ov && (ov[0] == '1' || ov[0] == '2')) ? ov[0] - '0' : 0;
-}
-
-unsigned long long* stamp_buffer(unsigned nwg) {
-    if (stamp_mode() == 0) return nullptr;
-    static unsigned long long* buf = nullptr;
-    static size_t cap = 0;
-    const size_t need = (size_t)nwg * 8 * kStampSlots * sizeof(unsigned long long);
-    if (need > cap) {
-        if (buf) (void)hipFree(buf);
-        if (hipMalloc(&buf, need) != hipSuccess) return nullptr;
-        cap = need;
-    }
-    (void)hipMemset(buf, 0, need);
-    return buf;
-}
-
-void stamp_report(const AttnKParams& p, unsigned nwg, hipStream_t s) {
-    const size_t n = (size_t)nwg * 8 * kStampSlots;
-    std::vector<unsigned long long> h(n);
-    if (hipStreamSynchronize(s) != hipSuccess ||
-        hipMemcpy(h.data(), p.stamp, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-        return;
-    if (stamp_mode() == 2) {
-        double tk = 0, rt = 0, nw = 0;
-        for (unsigned w = 0; w < nwg; ++w)
-            for (int v = 0; v < 8; ++v) {
-                const unsigned long long* x = &h[((size_t)w * 8 + v) * kStampSlots];
-                if (x[8] == 0) continue;   // waves the kernel does not have (4-wave workgroups)
-                tk += (double)x[8];
-                rt += (double)x[9];
-                nw += 1;
-            }
-        nw = nw > 0 ? nw : 1;
-        fprintf(stderr, "stamp light: wave entry->stores %.0f ticks, %.2f us real time, %.0f MHz\n", tk / nw,
-                rt / nw / 100.0, tk / (rt / 100.0));
-        return;
-    }
-    static const char* names[5] = {"bar1+dma", "mseg", "wait+bar2", "vseg", "loads"};
-    for (int half = 0; half < 2; ++half) {
-        double sum[7] = {0, 0, 0, 0, 0, 0, 0};
-        for (unsigned w = 0; w < nwg; ++w)
-            for (int v = 4 * half; v < 4 * half + 4; ++v)
-                for (int j = 0; j < 7; ++j) sum[j] += (double)h[((size_t)w * 8 + v) * kStampSlots + j];
-        const double it = sum[5] > 0 ? sum[5] : 1.0;
-        fprintf(stderr, "stamp half %c:", half ? 'B' : 'A');
-        for (int j = 0; j < 5; ++j) fprintf(stderr, " %s %.0f", names[j], sum[j] / it);
-        fprintf(stderr, " | loop/iter %.0f (iters/wave %.1f)\n", sum[6] / it, it / (4.0 * nwg));
-    }
-    // whole-wave spans: prologue (entry -> loop), loop, entry -> before the stores; start skew
-    double pro = 0, loop = 0, tot = 0;
-    unsigned long long t0 = ~0ull, t1 = 0, e_max = 0;
-    for (unsigned w = 0; w < nwg; ++w)
-        for (int v = 0; v < 8; ++v) {
-            const unsigned long long* x = &h[((size_t)w * 8 + v) * kStampSlots];
-            pro += (double)x[7];
-            loop += (double)x[6];
-            tot += (double)x[8];
-            t0 = x[9] < t0 ? x[9] : t0;
-            t1 = x[9] > t1 ? x[9] : t1;
-            e_max = x[9] + x[8] > e_max ? x[9] + x[8] : e_max;
-        }
-    const double nw = 8.0 * nwg;
-    for (int half = 0; half < 2; ++half) {
-        double tps[5] = {0, 0, 0, 0, 0};
-        for (unsigned w = 0; w < nwg; ++w)
-            for (int v = 4 * half; v < 4 * half + 4; ++v)
-                for (int j = 0; j < 5; ++j) tps[j] += (double)h[((size_t)w * 8 + v) * kStampSlots + 10 + j];
-        fprintf(stderr, "stamp prologue half %c (since entry): Q+bound %.0f | wait %.0f | bar %.0f | M0+wait %.0f | bar %.0f\n",
-                half ? 'B' : 'A', tps[0] / (nw / 2), tps[1] / (nw / 2), tps[2] / (nw / 2), tps[3] / (nw / 2),
-                tps[4] / (nw / 2));
-    }
-    fprintf(stderr, "stamp waves: prologue %.0f loop %.0f to-store %.0f | start skew %llu span %llu ticks\n", pro / nw,
-            loop / nw, tot / nw, t1 - t0, e_max - t0);
-}
-
-// short key ranges (self-attention): the in-workgroup key split (attn_kw_kernel) with KW waves;
-// CMT_ATTN_KW=0 selects the split-partials + combine path, 4 / 8 the wave count (default 8)
-int kw_waves(const cmt_attn_args& a) {
-    const char* ov = getenv("CMT_ATTN_KW");   // read per call: the tests toggle it in one process
-    if (ov && ov[0] == '0') return 0;
-    if (a.dtype == CMT_F32 || a.kv_splits > 0 || use_pp(a)) return 0;
-    const int ntiles = (a.Nk + KT - 1) / KT;
-    if (ntiles > 64) return 0;
-    return (ov && ov[0] == '4') ? 4 : 8;
+bool use_kw(const cmt_attn_args& a) {
+    if (a.dtype == CMT_F32 || a.kv_splits > 0 || use_long(a)) return false;
+    return (a.Nk + KT - 1) / KT <= 64;
 }
 
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
-    if (kw_waves(a) > 0) return 1;
+    if (use_kw(a)) return 1;
     const int ntiles = (a.Nk + KT - 1) / KT;
-    const LowpShape sh = lowp_shape(a);
-    const int nw = a.dtype == CMT_F32 ? NW : sh.waves;
-    const int qrows = a.dtype == CMT_F32 ? QB : sh.waves * sh.sub * QW;
-    const int base = cdiv(a.Nq, qrows) * a.B * a.H;
+    const int nw = a.dtype == CMT_F32 ? NW : (use_long(a) ? 8 : 4);
+    const int base = cdiv(a.Nq, nw * QW) * a.B * a.H;
     int s = 1;
     // aim for >= 2048 waves (two per SIMD) while keeping >= 8 tiles per split;
-    // short key ranges (self-attention) split down to 2 tiles per split
+    // short key ranges split down to 2 tiles per split
     const int min_tiles = ntiles >= 64 ? 8 : 2;
-    const int64_t target = use_pb(a) ? 2048 * pp_occ() : 2048;
-    while ((int64_t)base * s * nw < target && ntiles / (2 * s) >= min_tiles) s *= 2;
+    while ((int64_t)base * s * nw < 2048 && ntiles / (2 * s) >= min_tiles) s *= 2;
     return s;
 }
 
@@ -2031,7 +1349,8 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     CMT_REQUIRE(a.dtype != CMT_F32 || ((a.q_rstride | a.k_rstride | a.v_rstride) % 4 == 0),
                 "cmt_attn_fwd: f32 rows must be 16-byte aligned");
     CMT_REQUIRE(a.o_rstride % 4 == 0 && a.o_bstride % 4 == 0, "cmt_attn_fwd: O strides must be multiples of 4");
-    CMT_REQUIRE(a.o_dtype == CMT_F32 || a.o_dtype == CMT_F16 || a.o_dtype == CMT_BF16, "cmt_attn_fwd: bad o_dtype");
+    CMT_REQUIRE(a.o_dtype == CMT_F32 || a.o_dtype == CMT_F16 || a.o_dtype == CMT_BF16 || a.o_dtype == CMT_BF16P,
+                "cmt_attn_fwd: bad o_dtype");
     CMT_REQUIRE(a.q_rstride % 8 == 0 && a.k_rstride % 8 == 0 && a.v_rstride % 8 == 0 && a.q_hstride % 8 == 0 &&
                 a.k_hstride % 8 == 0 && a.v_hstride % 8 == 0 && a.q_bstride % 8 == 0 && a.k_bstride % 8 == 0 &&
                 a.v_bstride % 8 == 0, "cmt_attn_fwd: Q/K/V strides must be multiples of 8 elements");
@@ -2045,8 +1364,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     AttnKParams p;
     p.B = a.B; p.H = a.H; p.Nq = a.Nq; p.Nk = a.Nk;
     p.nqb = cdiv(a.Nq, 8 * QW);
-    // bounded-max mode needs bf16 P (f16's range cannot hold exp2(-2 * bound))
-    p.kmax2 = a.dtype == CMT_BF16 ? a.kmax2 : nullptr;
+    p.kmax2 = a.kmax2;
     p.kmax_ld = a.kmax_ld; p.kmax_plane0 = a.kmax_plane0; p.kmax_rows = a.kmax_rows;
     p.Q = a.Q; p.q_bs = a.q_bstride; p.q_hs = a.q_hstride; p.q_rs = a.q_rstride;
     p.K = a.K; p.k_bs = a.k_bstride; p.k_hs = a.k_hstride; p.k_rs = a.k_rstride;
@@ -2056,17 +1374,6 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     p.splits = splits;
     p.tiles_per_split = cdiv(ntiles, splits);
     p.round_out = (a.flags & CMT_ATTN_ROUND_OUTPUT) && a.dtype != CMT_F32 ? a.dtype : 0;
-    p.sync_all = (a.flags >> 8) & 1;
-    {
-        // CMT_ATTN_PRIO: static priority of the pb kernel's halves (0 none, 1 half B, 2 half A)
-        const char* pv = getenv("CMT_ATTN_PRIO");
-        p.prio = (pv && pv[0] >= '0' && pv[0] <= '2') ? pv[0] - '0' : 0;
-    }
-    p.stamp = nullptr;
-    {
-        const char* sd = getenv("CMT_ATTN_SKIPDEAD");
-        p.keep_dead = (sd && sd[0] == '0') ? 1 : 0;
-    }
     p.Op = p.Mp = p.Lp = nullptr;
     if (splits > 1) {
         const int64_t need = cmt_attn_workspace_bytes(&a);
@@ -2078,73 +1385,39 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
         p.Lp = p.Mp + rows;
     }
     hipStream_t s = (hipStream_t)stream;
-    const LowpShape sh = lowp_shape(a);
-    dim3 grid(cdiv(a.Nq, a.dtype == CMT_F32 ? QB : sh.waves * sh.sub * QW), a.B * a.H, splits);
     const bool fold = (a.flags & CMT_ATTN_FOLD_SCALE) != 0;
-#define ATTN_LAUNCH(T)                                                                                   \
-    do {                                                                                                 \
-        if (sh.sub == 2) {                                                                               \
-            if (fold) attn_fwd_kernel<T, 4, true, 2><<<grid, 256, 0, s>>>(p);                            \
-            else attn_fwd_kernel<T, 4, false, 2><<<grid, 256, 0, s>>>(p);                                \
-        } else if (sh.waves == 8) {                                                                      \
-            if (fold) attn_fwd_kernel<T, 8, true, 1><<<grid, 512, 0, s>>>(p);                            \
-            else attn_fwd_kernel<T, 8, false, 1><<<grid, 512, 0, s>>>(p);                                \
-        } else {                                                                                         \
-            if (fold) attn_fwd_kernel<T, 4, true, 1><<<grid, 256, 0, s>>>(p);                            \
-            else attn_fwd_kernel<T, 4, false, 1><<<grid, 256, 0, s>>>(p);                                \
-        }                                                                                                \
-    } while (0)
-    const int kw = kw_waves(a);
     if (a.dtype == CMT_F32) {
-        attn_fwd_f32_kernel<<<grid, 256, 0, s>>>(p);
-    } else if (kw > 0) {
+        attn_fwd_f32_kernel<<<dim3(cdiv(a.Nq, QB), a.B * a.H, splits), 256, 0, s>>>(p);
+    } else if (use_kw(a)) {
         const dim3 g2(cdiv(a.Nq, QW), a.B * a.H);
-#define KW_LAUNCH(T)                                                                                     \
-    do {                                                                                                 \
-        if (kw == 4) {                                                                                   \
-            if (fold) attn_kw_kernel<T, true, 4><<<g2, 256, 0, s>>>(p);                                  \
-            else attn_kw_kernel<T, false, 4><<<g2, 256, 0, s>>>(p);                                      \
-        } else {                                                                                         \
-            if (fold) attn_kw_kernel<T, true, 8><<<g2, 512, 0, s>>>(p);                                  \
-            else attn_kw_kernel<T, false, 8><<<g2, 512, 0, s>>>(p);                                      \
-        }                                                                                                \
-    } while (0)
-        if (a.dtype == CMT_F16) KW_LAUNCH(f16_t);
-        else KW_LAUNCH(bf16_t);
-#undef KW_LAUNCH
-    } else if (use_pp(a)) {
-        const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
-        if (use_pb(a)) {
-            const int rs = pb_rsum();
-            p.stamp = stamp_buffer(nwg);
-#define PB_LAUNCH(OCC)                                                                                    \
-    do {                                                                                                  \
-        if (rs == 1) attn_pb_kernel<bf16_t, 1, OCC><<<nwg, 512, 0, s>>>(p);                                \
-        else if (rs == 2) attn_pb_kernel<bf16_t, 2, OCC><<<nwg, 512, 0, s>>>(p);                           \
-        else attn_pb_kernel<bf16_t, 0, OCC><<<nwg, 512, 0, s>>>(p);                                        \
-    } while (0)
-            if (p.stamp && stamp_mode() == 2) attn_pb_kernel<bf16_t, 0, 1, 2><<<nwg, 512, 0, s>>>(p);
-            else if (p.stamp) attn_pb_kernel<bf16_t, 0, 1, 1><<<nwg, 512, 0, s>>>(p);
-            else if (rs == 0 && use_pb2() && pb2_rs16()) attn_pb2_kernel<bf16_t, 1, 3><<<nwg, 512, 0, s>>>(p);
-            else if (rs == 0 && use_pb2()) attn_pb2_kernel<bf16_t, 1, 0><<<nwg, 512, 0, s>>>(p);
-            else if (pp_occ() == 2) PB_LAUNCH(2);
-            else PB_LAUNCH(1);
-#undef PB_LAUNCH
-        } else if (a.dtype == CMT_F16) {
-            if (fold) attn_pp_kernel<f16_t, true, 1><<<nwg, 512, 0, s>>>(p);
-            else attn_pp_kernel<f16_t, false, 1><<<nwg, 512, 0, s>>>(p);
+        if (a.dtype == CMT_F16) {
+            if (fold) attn_kw_kernel<f16_t, true, 8><<<g2, 512, 0, s>>>(p);
+            else attn_kw_kernel<f16_t, false, 8><<<g2, 512, 0, s>>>(p);
         } else {
-            if (fold) attn_pp_kernel<bf16_t, true, 1><<<nwg, 512, 0, s>>>(p);
-            else attn_pp_kernel<bf16_t, false, 1><<<nwg, 512, 0, s>>>(p);
+            if (fold) attn_kw_kernel<bf16_t, true, 8><<<g2, 512, 0, s>>>(p);
+            else attn_kw_kernel<bf16_t, false, 8><<<g2, 512, 0, s>>>(p);
         }
-    } else if (a.dtype == CMT_F16) {
-        ATTN_LAUNCH(f16_t);
+    } else if (use_long(a)) {
+        // the scale is folded into Q either way; without the FOLD permission q * c is kept as hi + lo
+        const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
+        if (a.dtype == CMT_F16) {
+            if (fold) attn_pb2_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
+            else attn_pb2_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);
+        } else {
+            if (fold) attn_pb2_kernel<bf16_t, false><<<nwg, 512, 0, s>>>(p);
+            else attn_pb2_kernel<bf16_t, true><<<nwg, 512, 0, s>>>(p);
+        }
     } else {
-        ATTN_LAUNCH(bf16_t);
+        const dim3 grid(cdiv(a.Nq, 4 * QW), a.B * a.H, splits);
+        if (a.dtype == CMT_F16) {
+            if (fold) attn_fwd_kernel<f16_t, 4, true, 1><<<grid, 256, 0, s>>>(p);
+            else attn_fwd_kernel<f16_t, 4, false, 1><<<grid, 256, 0, s>>>(p);
+        } else {
+            if (fold) attn_fwd_kernel<bf16_t, 4, true, 1><<<grid, 256, 0, s>>>(p);
+            else attn_fwd_kernel<bf16_t, 4, false, 1><<<grid, 256, 0, s>>>(p);
+        }
     }
-#undef ATTN_LAUNCH
     int rc = cmt_check_launch("cmt_attn_fwd");
-    if (rc == 0 && p.stamp) stamp_report(p, (unsigned)p.nqb * a.B * a.H * splits, s);
     if (rc || splits == 1) return rc;
     const int64_t total = (int64_t)a.B * a.H * a.Nq * 8;
     const unsigned nb = (unsigned)cdiv64(total, 256);

@@ -73,8 +73,12 @@ __device__ __forceinline__ float pair_sum(float x) {
 // (global_load_lds) writes are invisible to the compiler, so ds_reads of a
 // freshly DMA'd buffer must not be scheduled above the s_barrier that orders
 // them after the other waves' counted vmcnt waits (the bare builtin does not
-// prevent that hoisting).
-__device__ __forceinline__ void barrier_mem() { asm volatile("s_barrier" ::: "memory"); }
+// prevent that hoisting).  gfx950 has back-off barriers, so the compiler puts
+// no wait before an s_barrier it cannot see: the lgkmcnt(0) here makes this
+// wave's own ds_writes visible to the waves past the barrier (without it a
+// tile staged through LDS was occasionally read before a 16-byte piece of it
+// landed -- a 4 x 8 block of wrong outputs in ~1 of 10^6 GEMM tiles).
+__device__ __forceinline__ void barrier_mem() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Non-finite sanitiser with torch.nan_to_num defaults.
 __device__ __forceinline__ float nan_to_num(float x) {
@@ -82,6 +86,42 @@ __device__ __forceinline__ float nan_to_num(float x) {
     if (x == __builtin_inff()) return 3.4028234663852886e38f;
     if (x == -__builtin_inff()) return -3.4028234663852886e38f;
     return x;
+}
+
+// CMT_BF16P split of one fp32 value (cmt_hip.h): x = hi + lo, both bf16 (RNE).
+__device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
+    hi = (bf16_t)x;
+    lo = (bf16_t)(x - (float)hi);
+}
+// Store v as element c of a CMT_BF16P row (hi at row[c], lo at row[C + c]).
+__device__ __forceinline__ void store_pair(bf16_t* row, int C, int c, float v) {
+    bf16_t h, l;
+    split_bf16(v, h, l);
+    row[c] = h;
+    row[C + c] = l;
+}
+// 4 consecutive elements c..c+3 of a CMT_BF16P row (8-byte stores).
+__device__ __forceinline__ void store_pair4(bf16_t* row, int C, int c, f32x4 v) {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    b4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h[j] = (bf16_t)v[j];
+        l[j] = (bf16_t)(v[j] - (float)h[j]);
+    }
+    *(b4*)(row + c) = h;
+    *(b4*)(row + C + c) = l;
+}
+// 8 consecutive elements c..c+7 (16-byte stores).
+__device__ __forceinline__ void store_pair8(bf16_t* row, int C, int c, const float* v) {
+    bf16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        h[j] = (bf16_t)v[j];
+        l[j] = (bf16_t)(v[j] - (float)h[j]);
+    }
+    *(bf16x8*)(row + c) = h;
+    *(bf16x8*)(row + C + c) = l;
 }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -28,7 +28,7 @@ __device__ __forceinline__ void store_dt(void* p, int64_t idx, int dt, float v) 
 // the same registers: a second LN of the result (post_norm), and the next
 // GEMMs' operands in the compute dtype (lowp(y), lowp(y + P)).
 // ---------------------------------------------------------------------------
-template <int VPT, typename LT>
+template <int VPT, typename LT, bool PAIR = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -70,8 +70,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
         if (a.flags & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
         if (a.flags & CMT_LN_MAX_INTO) o = fmaxf(o, yold[i]);
         if (a.Y) a.Y[(int64_t)row * a.ldy + c] = o;
-        if (a.Yl) ((LT*)a.Yl)[(int64_t)row * a.ldyl + c] = (LT)o;
-        if (a.Yp) ((LT*)a.Yp)[(int64_t)row * a.ldyp + c] = (LT)(o + pv[i]);
+        if constexpr (PAIR) {   // CMT_BF16P rows [hi(C) | lo(C)]
+            if (a.Yl) store_pair((bf16_t*)a.Yl + (int64_t)row * a.ldyl, C, c, o);
+            if (a.Yp) store_pair((bf16_t*)a.Yp + (int64_t)row * a.ldyp, C, c, o + pv[i]);
+        } else {
+            if (a.Yl) ((LT*)a.Yl)[(int64_t)row * a.ldyl + c] = (LT)o;
+            if (a.Yp) ((LT*)a.Yp)[(int64_t)row * a.ldyp + c] = (LT)(o + pv[i]);
+        }
     }
     if (a.Y2 == nullptr) return;
     s = 0.f;
@@ -91,6 +96,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
         if (a.flags2 & CMT_LN_MAX_INTO) o = fmaxf(o, y2old[i]);
         y2[c] = o;
     }
+}
+
+// CMT_BF16P form: one thread per 4 values of a row of width C (rows [hi(C) | lo(C)])
+__global__ __launch_bounds__(256) void add_cast_pair_kernel(const float* __restrict__ X, const float* __restrict__ P,
+                                                            int64_t n4, int C, bf16_t* Yl, bf16_t* Yp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const int64_t row = i / (C / 4);
+    const int c = (int)(i - row * (C / 4)) * 4;
+    const f32x4 x = X ? ((const f32x4*)X)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (Yl) store_pair4(Yl + row * 2 * C, C, c, x);
+    if (Yp) store_pair4(Yp + row * 2 * C, C, c, x + ((const f32x4*)P)[i]);
 }
 
 template <typename LT>
@@ -120,7 +137,7 @@ __device__ __forceinline__ float inv_sigmoid_dev(float x) {
 }
 __device__ __forceinline__ float sigmoid_dev(float x) { return 1.f / (1.f + expf(-x)); }
 
-template <typename OT>
+template <typename OT, bool PAIR = false>
 __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict__ pos, int64_t pos_stride, int n,
                                                         int F, int mode, int x_size, int y_size, OT* out,
                                                         int64_t ldo) {
@@ -163,7 +180,9 @@ __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict_
         o[2 * t + 1] = __cosf(v);
     }
     OT* dst = out + (int64_t)i * ldo + f0;
-    if constexpr (sizeof(OT) == 4) {
+    if constexpr (PAIR) {
+        store_pair8((bf16_t*)out + (int64_t)i * ldo, 2 * F, f0, o);
+    } else if constexpr (sizeof(OT) == 4) {
         *(f32x4*)dst = f32x4{o[0], o[1], o[2], o[3]};
         *(f32x4*)(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
     } else {
@@ -177,7 +196,7 @@ __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------
 struct PcRange { float v[6]; };
 
-template <typename OT>
+template <typename OT, bool PAIR = false>
 __global__ void rv_pe_coords_kernel8(int BV, int H, int W, int D, float pad_h, float pad_w, float dstep,
                                      const float* __restrict__ i2l, PcRange pc, OT* out) {
     // one thread = 8 consecutive depth samples of one image token: 24 outputs, written as whole
@@ -212,7 +231,11 @@ __global__ void rv_pe_coords_kernel8(int BV, int H, int W, int D, float pad_h, f
         }
     }
     OT* o = out + (int64_t)tok * (3 * D) + 3 * k0;   // 24 consecutive outputs
-    if constexpr (sizeof(OT) == 2) {
+    if constexpr (PAIR) {
+        bf16_t* prow = (bf16_t*)out + (int64_t)tok * (6 * D);   // [hi(3D) | lo(3D)]
+#pragma unroll
+        for (int q = 0; q < 3; ++q) store_pair8(prow, 3 * D, 3 * k0 + 8 * q, res + 8 * q);
+    } else if constexpr (sizeof(OT) == 2) {
         typedef OT o8 __attribute__((ext_vector_type(8)));
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
@@ -256,7 +279,7 @@ __global__ void rv_pe_coords_kernel(int BV, int H, int W, int D, float pad_h, fl
 }
 
 // _rv_query_embed geometry (cmt_head.py:446-463): one thread per (b, v, q, depth).
-template <typename TO>
+template <typename TO, bool PAIR = false>
 __global__ void rv_query_coords_kernel(const float* __restrict__ ref, int B, int V, int Nq, int D,
                                        float pad_h, float pad_w, float dstep,
                                        const float* __restrict__ l2i, const float* __restrict__ i2l,
@@ -301,7 +324,9 @@ __global__ void rv_query_coords_kernel(const float* __restrict__ ref, int B, int
         a = fmaf(M[rr * 4 + 1], c4[1], a);
         a = fmaf(M[rr * 4 + 2], c4[2], a);
         a = fmaf(M[rr * 4 + 3], c4[3], a);
-        o[rr] = (TO)((a - pc.v[rr]) / (pc.v[3 + rr] - pc.v[rr]));   // RNE, as cmt_cast
+        const float v = (a - pc.v[rr]) / (pc.v[3 + rr] - pc.v[rr]);
+        if constexpr (PAIR) store_pair((bf16_t*)out + bvq * (6 * D), 3 * D, 3 * k + rr, v);   // [hi(3D) | lo(3D)]
+        else o[rr] = (TO)v;   // RNE, as cmt_cast
     }
 }
 
@@ -324,7 +349,7 @@ __global__ void masked_view_sum_kernel(const float* __restrict__ X, const float*
 
 // Y[b,q,:] = base[q,:] + sum_v X[b,v,q,:] * mask[b,v,q]  (base NULL: Y += ...), and, when
 // given, the decoder's first operands Yp = lowp(Y) (= lowp(0 + query_pos)) and Yl = lowp(0).
-template <typename TL>
+template <typename TL, bool PAIR = false>
 __global__ void masked_view_sum_ex_kernel(const float* __restrict__ X, const float* __restrict__ mask, int B, int V,
                                           int Nq, int C, const float* __restrict__ base, float* Y, TL* Yl, TL* Yp) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -341,8 +366,13 @@ __global__ void masked_view_sum_ex_kernel(const float* __restrict__ X, const flo
     }
     const float y = (base ? base[(int64_t)q * C + c] : Y[idx]) + s;
     Y[idx] = y;
-    if (Yp) Yp[idx] = (TL)y;
-    if (Yl) Yl[idx] = (TL)0.f;
+    if constexpr (PAIR) {   // rows [hi(C) | lo(C)]
+        if (Yp) store_pair((bf16_t*)Yp + bq * 2 * C, C, c, y);
+        if (Yl) store_pair((bf16_t*)Yl + bq * 2 * C, C, c, 0.f);
+    } else {
+        if (Yp) Yp[idx] = (TL)y;
+        if (Yl) Yl[idx] = (TL)0.f;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -379,7 +409,7 @@ __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restri
 // layout pass to ~3.3 TB/s.  LDS tile [64 c][65]: bank (c + p) % 64, so both
 // the pixel-major scalar writes (16 pixel quads x 4 channels per wave) and the
 // transposed reads (8 channel groups x 8 pixels per wave) are conflict-free.
-template <typename TO>
+template <typename TO, bool PAIR = false>
 __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __restrict__ X, int nv, int C, int HW,
                                                                TO* Y, int64_t ldy, int64_t rows_per_batch,
                                                                int64_t row_offset) {
@@ -417,13 +447,25 @@ __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __re
         for (int j = 0; j < VW; ++j) o[j] = tile[cg + j][pi];
         const int64_t row = (int64_t)bo * rows_per_batch + row_offset + (int64_t)v * HW + p;
         TO* dst = Y + row * ldy + c0 + cg;
-        if constexpr (VW == 4) {
+        if constexpr (PAIR) {
+            store_pair8((bf16_t*)Y + row * ldy, C, c0 + cg, o);   // rows [hi(C) | lo(C)]
+        } else if constexpr (VW == 4) {
             *(f32x4*)dst = f32x4{o[0], o[1], o[2], o[3]};
         } else {
             typedef TO o8 __attribute__((ext_vector_type(8)));
             *(o8*)dst = o8{(TO)o[0], (TO)o[1], (TO)o[2], (TO)o[3], (TO)o[4], (TO)o[5], (TO)o[6], (TO)o[7]};
         }
     }
+}
+
+// fp32 rows (leading dimension ldx) -> CMT_BF16P rows [hi(C) | lo(C)], 4 values per thread
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ X, int64_t ldx, int64_t n4, int C,
+                                                         bf16_t* Y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const int64_t row = i / (C / 4);
+    const int c = (int)(i - row * (C / 4)) * 4;
+    store_pair4(Y + row * 2 * C, C, c, *(const f32x4*)(X + row * ldx + c));
 }
 
 template <typename TI, typename TO>
@@ -580,14 +622,15 @@ extern "C" int cmt_layernorm_ex(const cmt_ln_args* ap, void* stream) {
     CMT_REQUIRE(a.C % 64 == 0 && a.C >= 64 && a.C <= 1024, "cmt_layernorm: C must be a multiple of 64 in [64, 1024]");
     CMT_REQUIRE(a.Y2 == nullptr || (a.W2 && a.B2), "cmt_layernorm: second LN needs W2/B2");
     CMT_REQUIRE(a.Yp == nullptr || a.P != nullptr, "cmt_layernorm: Yp needs P");
-    CMT_REQUIRE((a.Yl == nullptr && a.Yp == nullptr) || a.lowp_dtype == CMT_F16 || a.lowp_dtype == CMT_BF16,
-                "cmt_layernorm: lowp_dtype must be f16 or bf16");
+    CMT_REQUIRE((a.Yl == nullptr && a.Yp == nullptr) || a.lowp_dtype == CMT_F16 || a.lowp_dtype == CMT_BF16 ||
+                    a.lowp_dtype == CMT_BF16P, "cmt_layernorm: lowp_dtype must be f16, bf16 or bf16 pair");
     if (a.rows == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     dim3 grid(cdiv(a.rows, 4));
 #define LN_CASE(V)                                                                              \
     case V:                                                                                     \
         if (a.lowp_dtype == CMT_F16) layernorm_kernel<V, f16_t><<<grid, 256, 0, s>>>(a);        \
+        else if (a.lowp_dtype == CMT_BF16P) layernorm_kernel<V, bf16_t, true><<<grid, 256, 0, s>>>(a); \
         else layernorm_kernel<V, bf16_t><<<grid, 256, 0, s>>>(a);                               \
         break;
     switch (a.C / 64) {
@@ -613,11 +656,14 @@ extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const
 extern "C" int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,
                             void* stream) {
     CMT_REQUIRE(rows >= 0 && C % 4 == 0 && (Yp == nullptr || P), "cmt_add_cast: bad arguments");
-    CMT_REQUIRE(lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16, "cmt_add_cast: lowp_dtype must be f16 or bf16");
+    CMT_REQUIRE(lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16 || lowp_dtype == CMT_BF16P,
+                "cmt_add_cast: lowp_dtype must be f16, bf16 or bf16 pair");
     const int64_t n4 = (int64_t)rows * C / 4;
     if (n4 == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    if (lowp_dtype == CMT_F16)
+    if (lowp_dtype == CMT_BF16P)
+        add_cast_pair_kernel<<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, C, (bf16_t*)Yl, (bf16_t*)Yp);
+    else if (lowp_dtype == CMT_F16)
         add_cast_kernel<f16_t><<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, (f16_t*)Yl, (f16_t*)Yp);
     else
         add_cast_kernel<bf16_t><<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, (bf16_t*)Yl, (bf16_t*)Yp);
@@ -629,7 +675,8 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
     CMT_REQUIRE(out && n >= 0 && F > 0 && F % 4 == 0 && ldo % 8 == 0, "cmt_pos2embed: bad arguments");
     CMT_REQUIRE(pos != nullptr || (grid_h > 0 && grid_w > 0 && n == grid_h * grid_w),
                 "cmt_pos2embed: grid mode needs n == grid_h*grid_w");
-    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_pos2embed: bad odtype");
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_BF16P,
+                "cmt_pos2embed: bad odtype");
     if (n == 0) return 0;
     const int64_t total = (int64_t)n * (2 * F / 8);
     CMT_REQUIRE(total < ((int64_t)1 << 31), "cmt_pos2embed: n * F too large for one launch");
@@ -640,6 +687,9 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
     else if (odtype == CMT_F16)
         pos2embed_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
                                                                     (f16_t*)out, ldo);
+    else if (odtype == CMT_BF16P)
+        pos2embed_kernel<bf16_t, true><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h,
+                                                                           grid_w, (bf16_t*)out, ldo);
     else
         pos2embed_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
                                                                      (bf16_t*)out, ldo);
@@ -649,12 +699,15 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
 extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float pad_w, float depth_max,
                                 const float* i2l, const float* pc_range6, void* out, int odtype, void* stream) {
     CMT_REQUIRE(i2l && pc_range6 && out && BV > 0 && h > 0 && w > 0 && D > 0, "cmt_rv_pe_coords: bad arguments");
-    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_rv_pe_coords: bad odtype");
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_BF16P,
+                "cmt_rv_pe_coords: bad odtype");
+    CMT_REQUIRE(odtype != CMT_BF16P || (D % 8 == 0 && (uintptr_t)out % 16 == 0),
+                "cmt_rv_pe_coords: the bf16-pair output needs D % 8 == 0 and a 16-byte aligned out");
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
     hipStream_t s = (hipStream_t)stream;
     const char* vec = getenv("CMT_RVPE_VEC");   // diagnostics: 0 = the one-thread-per-depth kernel
-    if (!(vec && vec[0] == '0') && D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) &&
+    if ((odtype == CMT_BF16P || !(vec && vec[0] == '0')) && D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) &&
         (uintptr_t)out % 16 == 0) {
         const int64_t t8 = (int64_t)BV * h * w * (D / 8);
         if (odtype == CMT_F32)
@@ -663,6 +716,10 @@ extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float 
         else if (odtype == CMT_F16)
             rv_pe_coords_kernel8<f16_t><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
                                                                          i2l, pc, (f16_t*)out);
+        else if (odtype == CMT_BF16P)
+            rv_pe_coords_kernel8<bf16_t, true><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w,
+                                                                                depth_max - 1.f, i2l, pc,
+                                                                                (bf16_t*)out);
         else
             rv_pe_coords_kernel8<bf16_t><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w,
                                                                           depth_max - 1.f, i2l, pc, (bf16_t*)out);
@@ -699,7 +756,8 @@ extern "C" int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, in
                                       int odtype, float* mask, void* stream) {
     CMT_REQUIRE(ref && l2i && i2l && pc_range6 && out && mask && B > 0 && V > 0 && Nq > 0 && D > 0,
                 "cmt_rv_query_coords_ex: bad arguments");
-    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16, "cmt_rv_query_coords_ex: bad odtype");
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_BF16P,
+                "cmt_rv_query_coords_ex: bad odtype");
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
     const int64_t total = (int64_t)B * V * Nq * D;
@@ -710,6 +768,10 @@ extern "C" int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, in
     else if (odtype == CMT_F16)
         rv_query_coords_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
                                                                           pc.v[3] - 1.f, l2i, i2l, pc, (f16_t*)out, mask);
+    else if (odtype == CMT_BF16P)
+        rv_query_coords_kernel<bf16_t, true><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
+                                                                                 pc.v[3] - 1.f, l2i, i2l, pc,
+                                                                                 (bf16_t*)out, mask);
     else
         rv_query_coords_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
                                                                            pc.v[3] - 1.f, l2i, i2l, pc, (bf16_t*)out,
@@ -728,11 +790,14 @@ extern "C" int cmt_masked_view_sum(const float* X, const float* mask, int B, int
 extern "C" int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int Nq, int C,
                                       const float* base, float* Y, void* Yl, void* Yp, int lowp_dtype, void* stream) {
     CMT_REQUIRE(X && mask && Y && B > 0 && V > 0 && Nq > 0 && C > 0, "cmt_masked_view_sum_ex: bad arguments");
-    CMT_REQUIRE((!Yl && !Yp) || lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16,
-                "cmt_masked_view_sum_ex: lowp_dtype must be f16 or bf16");
+    CMT_REQUIRE((!Yl && !Yp) || lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16 || lowp_dtype == CMT_BF16P,
+                "cmt_masked_view_sum_ex: lowp_dtype must be f16, bf16 or bf16 pair");
     const int64_t total = (int64_t)B * Nq * C;
     hipStream_t s = (hipStream_t)stream;
-    if (lowp_dtype == CMT_F16)
+    if (lowp_dtype == CMT_BF16P)
+        masked_view_sum_ex_kernel<bf16_t, true><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
+                                                                                    (bf16_t*)Yl, (bf16_t*)Yp);
+    else if (lowp_dtype == CMT_F16)
         masked_view_sum_ex_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
                                                                              (f16_t*)Yl, (f16_t*)Yp);
     else
@@ -747,6 +812,13 @@ extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, v
     dim3 grid(cdiv(HW, 64), cdiv(C, 64), nb * nv);
     hipStream_t s = (hipStream_t)stream;
     const int esz = ydtype == CMT_F32 ? 4 : 2;
+    if (ydtype == CMT_BF16P) {
+        CMT_REQUIRE(HW % 4 == 0 && C % 64 == 0 && ldy == 2 * C && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0,
+                    "cmt_nchw_to_rows: bf16-pair rows need HW % 4 == 0, C % 64 == 0, ldy == 2C, 16-byte alignment");
+        nchw_to_rows_vec_kernel<bf16_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
+                                                                   row_offset);
+        return cmt_check_launch("cmt_nchw_to_rows");
+    }
     if (HW % 4 == 0 && C % 64 == 0 && (ldy * esz) % 16 == 0 && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0 &&
         (ydtype == CMT_F32 || ydtype == CMT_F16 || ydtype == CMT_BF16)) {
         if (ydtype == CMT_F32)
@@ -769,6 +841,15 @@ extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, v
     else
         return cmt_fail(CMT_EINVAL, "cmt_nchw_to_rows: bad ydtype");
     return cmt_check_launch("cmt_nchw_to_rows");
+}
+
+extern "C" int cmt_split_rows(const float* X, int64_t ldx, int64_t rows, int C, void* Y, void* stream) {
+    CMT_REQUIRE(X && Y && rows >= 0 && C > 0 && C % 4 == 0 && ldx % 4 == 0 && (uintptr_t)X % 16 == 0 &&
+                    (uintptr_t)Y % 8 == 0, "cmt_split_rows: bad arguments");
+    const int64_t n4 = rows * (C / 4);
+    if (n4 == 0) return 0;
+    split_rows_kernel<<<nblocks(n4, 256), 256, 0, (hipStream_t)stream>>>(X, ldx, n4, C, (bf16_t*)Y);
+    return cmt_check_launch("cmt_split_rows");
 }
 
 extern "C" int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* stream) {

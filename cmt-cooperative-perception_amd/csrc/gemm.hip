@@ -446,8 +446,16 @@ __device__ __forceinline__ void store4(void* C, int64_t idx, int dt, f32x4 v) {
     }
 }
 
-__device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt) {
+// lo_off: element distance of a CMT_BF16P row's lo half (its logical width)
+__device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt, int lo_off = 0) {
     if (dt == CMT_F32) return *(const f32x4*)((const float*)p + idx);
+    if (dt == CMT_BF16P) {
+        typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+        const b4 h = *(const b4*)((const bf16_t*)p + idx);
+        const b4 l = *(const b4*)((const bf16_t*)p + idx + lo_off);
+        return f32x4{(float)h[0] + (float)l[0], (float)h[1] + (float)l[1], (float)h[2] + (float)l[2],
+                     (float)h[3] + (float)l[3]};
+    }
     if (dt == CMT_F16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 h = *(const h4*)((const f16_t*)p + idx);
@@ -461,7 +469,13 @@ __device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt) {
 // Main loop of the LDS-DMA GEMM for one BM x BN output tile (4 waves in a
 // WM x (4/WM) grid; each wave owns (BM/WM) x (BN*WM/4) as TM x TN 32x32 MFMA
 // tiles).  Accumulators are in the swapped C^T layout: lane = output row.
-template <typename CT, int BM, int BN, int S, int AMODE, int WM>
+//
+// X3 (A and W both CMT_BF16P, cmt_hip.h): the k loop runs over three
+// segments of the logical K -- (A_hi, W_hi), (A_lo, W_hi), (A_hi, W_lo) --
+// so the split-bf16 product is the plain bf16 pipeline over 3K with a column
+// offset per operand and segment: the A row's lo half starts at its logical
+// width (K for rows, the channel count for the implicit convs), W's at K.
+template <typename CT, int BM, int BN, int S, int AMODE, int WM, bool X3 = false>
 struct DmaTile {
     static constexpr int KS = 64;                          // k per stage: one 128-byte LDS row per tile row
     static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
@@ -507,34 +521,55 @@ struct DmaTile {
 
         // implicit convs (3x3, 1D k = 3): the stages arrive in increasing k order and a tap spans
         // (tap width) / 64 stages, so each row's gathered offset is recomputed once per tap
-        // (9 or 3 times per tile), not per stage (no integer division in the k loop)
-        int ctap = -1, ccin = 0;
+        // (9 or 3 times per tile and X3 segment), not per stage (no integer division in the k loop)
+        const int tapw = AMODE == CMT_A_CONV3X3 ? a.conv_c : (AMODE == CMT_A_CONV1D3 ? a.K / 3 : a.K);
+        const int ntaps = AMODE == CMT_A_CONV3X3 ? 9 : (AMODE == CMT_A_CONV1D3 ? 3 : 1);
+        int cseg = 0, ctap = -1, ccin = 0;
         int64_t toff[APER];
         auto issue = [&](int buf, int kt) {
             char* sb = smem + buf * STAGE;
-            const int k0 = kt * KS;
+            int ka, kw;   // A / W column of this stage's first k
             if constexpr (AMODE != CMT_A_ROWS) {
                 // the same per-tap cache for the 1D k = 3 conv (taps of K / 3 columns)
-                const int tapw = AMODE == CMT_A_CONV3X3 ? a.conv_c : a.K / 3;
-                if (ctap < 0 || (ccin += KS) == tapw) {
-                    ctap = ctap < 0 ? k0 / tapw : ctap + 1;
+                if (ctap < 0) {
+                    const int k0 = kt * KS;
+                    ctap = k0 / tapw;
                     ccin = k0 - ctap * tapw;
 #pragma unroll
                     for (int i = 0; i < APER; ++i)
                         toff[i] = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), ctap * tapw);
+                } else if ((ccin += KS) == tapw) {
+                    ccin = 0;
+                    if (++ctap == ntaps) {   // X3: next segment, taps from 0 again
+                        ctap = 0;
+                        ++cseg;
+                    }
+#pragma unroll
+                    for (int i = 0; i < APER; ++i)
+                        toff[i] = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), ctap * tapw);
+                }
+                ka = ccin + (X3 && cseg == 1 ? tapw : 0);
+                kw = ctap * tapw + ccin + (X3 && cseg == 2 ? a.K : 0);
+            } else {
+                const int k0 = kt * KS;
+                if constexpr (X3) {
+                    ka = k0 >= 2 * a.K ? k0 - 2 * a.K : k0;   // hi | lo | hi
+                    kw = k0 >= a.K ? k0 - a.K : k0;           // hi | hi | lo
+                } else {
+                    ka = kw = k0;
                 }
             }
 #pragma unroll
             for (int i = 0; i < APER; ++i) {
                 const void* src;
                 if (AMODE == CMT_A_ROWS)
-                    src = asrc[i] + k0;
+                    src = asrc[i] + ka;
                 else
-                    src = toff[i] < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + toff[i] + ccin + acs[i]);
+                    src = toff[i] < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + toff[i] + ka + acs[i]);
                 glds16(src, sb + (4 * i + wave) * 1024);
             }
 #pragma unroll
-            for (int i = 0; i < BPER; ++i) glds16(bsrc[i] + k0, sb + A_BYTES + (4 * i + wave) * 1024);
+            for (int i = 0; i < BPER; ++i) glds16(bsrc[i] + kw, sb + A_BYTES + (4 * i + wave) * 1024);
         };
 
 #pragma unroll
@@ -544,7 +579,7 @@ struct DmaTile {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-        const int nk = a.K / KS;
+        const int nk = (X3 ? 3 : 1) * a.K / KS;
 #pragma unroll
         for (int s = 0; s < S; ++s)
             if (s < nk) issue(s, s);
@@ -596,9 +631,9 @@ __device__ __forceinline__ void xcd_tile(int tiles_m, int tiles_n, int batch, in
     nt = rem - mt * tiles_n;
 }
 
-template <typename CT, int BM, int BN, int S, int AMODE>
+template <typename CT, int BM, int BN, int S, int AMODE, bool X3 = false>
 __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
-    typedef DmaTile<CT, BM, BN, S, AMODE, 2> Tile;
+    typedef DmaTile<CT, BM, BN, S, AMODE, 2, X3> Tile;
     constexpr int TM = Tile::TM, TN = Tile::TN;
     __shared__ __attribute__((aligned(16))) char smem[Tile::SMEM];
     int z, mt, nt;
@@ -636,7 +671,7 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int n = n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;
-                    const f32x4 r = load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype);
+                    const f32x4 r = load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype, a.N);
                     // bias + relu come first; keep R apart only when relu is on
                     if (a.relu) {
 #pragma unroll
@@ -665,110 +700,120 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     // written to LDS (16-byte chunks XOR-swizzled by row) and read back so
     // every wave instruction stores 1 KB of contiguous memory (head-split:
     // 16 rows x 64 B of one head; rows: whole row segments).
-    barrier_mem();                                       // every wave is done with the staging ring
-    const int cpr = BN * esz / 16;                       // 16-byte chunks per tile row (power of two)
-    const int cpe = 16 / esz;                            // elements per chunk
+    // A CMT_BF16P C (row mode) is staged and stored twice: the hi halves, then
+    // the lo halves N columns further (cmt_hip.h).
+    const int npass = a.c_dtype == CMT_BF16P ? 2 : 1;
+    for (int pass = 0; pass < npass; ++pass) {
+        barrier_mem();                                       // every wave is done with the staging ring
+        const int cpr = BN * esz / 16;                       // 16-byte chunks per tile row (power of two)
+        const int cpe = 16 / esz;                            // elements per chunk
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-        const int row = wm * (BM / 2) + tm * 32 + lr;
+        for (int tm = 0; tm < TM; ++tm) {
+            const int row = wm * (BM / 2) + tm * 32 + lr;
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
+            for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int c0 = wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;     // first of 4 columns
-                const int ch = c0 / cpe;
-                char* dst = smem + row * (BN * esz) + ((ch ^ (row & (cpr - 1))) << 4) + (c0 % cpe) * esz;
-                const f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
-                                 acc[tm][tn][4 * g + 3]};
-                store4<CT>(dst, 0, a.c_dtype, v);
-            }
-    }
-    barrier_mem();
-    const bool headsplit = a.c_mode != CMT_C_ROWS;
-    const int lcpr = esz == 4 ? __builtin_ctz(BN / 4) : __builtin_ctz(BN / 8);   // log2 chunks per row
-    const int lcph = esz == 4 ? 3 : 2;                   // log2 chunks per 32-column head slice
-    constexpr int LBM = __builtin_ctz(BM);
-    // batch of the tile's first row; a tile spans at most two batches when rows_per_batch >= BM
-    const int rpb = headsplit ? a.rows_per_batch : 1;
-    const int b0 = headsplit ? m0 / rpb : 0;
-    const int rr0 = m0 - b0 * rpb;
-    // head-plane max of squared row norms (cmt_gemm_args.plane_max2, 16-bit C):
-    // with 4 chunks per 32-column head row one iteration of the loop below
-    // covers one head plane x 64 rows -- one entry
-    if (headsplit && a.plane_max2 != nullptr && esz == 2) {
-        constexpr int PITERS = BM * BN / 8 / NT;         // 16-byte chunks of the 16-bit tile per thread
-        float* red = (float*)(smem + BM * BN * 2);       // [iteration][wave], after the staged tile
+                for (int g = 0; g < 4; ++g) {
+                    const int c0 = wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;     // first of 4 columns
+                    const int ch = c0 / cpe;
+                    char* dst = smem + row * (BN * esz) + ((ch ^ (row & (cpr - 1))) << 4) + (c0 % cpe) * esz;
+                    f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
+                               acc[tm][tn][4 * g + 3]};
+                    if (pass) {
 #pragma unroll
-        for (int it = 0; it < PITERS; ++it) {
-            const int q = threadIdx.x + it * NT;
-            const int h = q >> (LBM + 2);
-            const int rem = q & ((BM << 2) - 1);
-            const int row = rem >> 2;
-            const int c = (h << 2) + (rem & 3);
-            const f32x4 v = *(const f32x4*)(smem + row * (BN * 2) + ((c ^ (row & ((1 << lcpr) - 1))) << 4));
-            float ss = 0.f;
-            if (m0 + row < a.M && n0 + c * 8 < a.plane_max_cols) {
-                if (a.c_dtype == CMT_BF16) {
-                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                    const u32x4 w = __builtin_bit_cast(u32x4, v);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float lo = __uint_as_float(w[j] << 16), hi = __uint_as_float(w[j] & 0xffff0000u);
-                        ss += lo * lo + hi * hi;
+                        for (int j = 0; j < 4; ++j) v[j] -= (float)(bf16_t)v[j];   // lo = bf16(x - hi)
                     }
-                } else {
-                    const f16x8 hv = __builtin_bit_cast(f16x8, v);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) ss += (float)hv[j] * (float)hv[j];
+                    store4<CT>(dst, 0, a.c_dtype == CMT_BF16P ? CMT_BF16 : a.c_dtype, v);
                 }
-            }
-            ss += __shfl_xor(ss, 1);                     // the 4 chunks of one head row
-            ss += __shfl_xor(ss, 2);
-#pragma unroll
-            for (int off = 4; off < 64; off <<= 1) ss = fmaxf(ss, __shfl_xor(ss, off));
-            if ((threadIdx.x & 63) == 0) red[it * 4 + (threadIdx.x >> 6)] = ss;
         }
         barrier_mem();
-        if ((int)threadIdx.x < PITERS) {
-            const int itx = threadIdx.x;
-            const float mx = fmaxf(fmaxf(red[itx * 4], red[itx * 4 + 1]), fmaxf(red[itx * 4 + 2], red[itx * 4 + 3]));
-            const int q0 = itx * NT;
-            const int plane = (n0 >> 5) + (q0 >> (LBM + 2));
-            const int row0 = (q0 & ((BM << 2) - 1)) >> 2;
-            if (plane * 32 < a.plane_max_cols)
-                a.plane_max2[(int64_t)((m0 + row0) >> 6) * (a.plane_max_cols >> 5) + plane] = mx;
-        }
-    }
-#pragma unroll 4
-    for (int q = threadIdx.x; q < (BM << lcpr); q += NT) {
-        int row, c;
-        if (headsplit) {                                 // head-major, then row, then chunk: contiguous in memory
-            const int h = q >> (LBM + lcph);
-            const int rem = q & ((BM << lcph) - 1);
-            row = rem >> lcph;
-            c = (h << lcph) + (rem & ((1 << lcph) - 1));
-        } else {
-            row = q >> lcpr;
-            c = q & ((1 << lcpr) - 1);
-        }
-        const int m = m0 + row;
-        if (m >= a.M) continue;
-        const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & ((1 << lcpr) - 1))) << 4));
-        const int n = n0 + c * cpe;
-        int64_t idx;
-        if (headsplit) {
-            int bb = b0, rr = rr0 + row;
-            if (rpb >= BM) {
-                if (rr >= rpb) { rr -= rpb; ++bb; }
-            } else {
-                bb = m / rpb;
-                rr = m - bb * rpb;
+        const bool headsplit = a.c_mode != CMT_C_ROWS;
+        const int lcpr = esz == 4 ? __builtin_ctz(BN / 4) : __builtin_ctz(BN / 8);   // log2 chunks per row
+        const int lcph = esz == 4 ? 3 : 2;                   // log2 chunks per 32-column head slice
+        constexpr int LBM = __builtin_ctz(BM);
+        // batch of the tile's first row; a tile spans at most two batches when rows_per_batch >= BM
+        const int rpb = headsplit ? a.rows_per_batch : 1;
+        const int b0 = headsplit ? m0 / rpb : 0;
+        const int rr0 = m0 - b0 * rpb;
+        // head-plane max of squared row norms (cmt_gemm_args.plane_max2, 16-bit C):
+        // with 4 chunks per 32-column head row one iteration of the loop below
+        // covers one head plane x 64 rows -- one entry
+        if (headsplit && a.plane_max2 != nullptr && esz == 2) {
+            constexpr int PITERS = BM * BN / 8 / NT;         // 16-byte chunks of the 16-bit tile per thread
+            float* red = (float*)(smem + BM * BN * 2);       // [iteration][wave], after the staged tile
+#pragma unroll
+            for (int it = 0; it < PITERS; ++it) {
+                const int q = threadIdx.x + it * NT;
+                const int h = q >> (LBM + 2);
+                const int rem = q & ((BM << 2) - 1);
+                const int row = rem >> 2;
+                const int c = (h << 2) + (rem & 3);
+                const f32x4 v = *(const f32x4*)(smem + row * (BN * 2) + ((c ^ (row & ((1 << lcpr) - 1))) << 4));
+                float ss = 0.f;
+                if (m0 + row < a.M && n0 + c * 8 < a.plane_max_cols) {
+                    if (a.c_dtype == CMT_BF16) {
+                        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 w = __builtin_bit_cast(u32x4, v);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float lo = __uint_as_float(w[j] << 16), hi = __uint_as_float(w[j] & 0xffff0000u);
+                            ss += lo * lo + hi * hi;
+                        }
+                    } else {
+                        const f16x8 hv = __builtin_bit_cast(f16x8, v);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) ss += (float)hv[j] * (float)hv[j];
+                    }
+                }
+                ss += __shfl_xor(ss, 1);                     // the 4 chunks of one head row
+                ss += __shfl_xor(ss, 2);
+#pragma unroll
+                for (int off = 4; off < 64; off <<= 1) ss = fmaxf(ss, __shfl_xor(ss, off));
+                if ((threadIdx.x & 63) == 0) red[it * 4 + (threadIdx.x >> 6)] = ss;
             }
-            idx = (((int64_t)bb * (a.N >> 5) + (n >> 5)) * rpb + rr) * 32 + (n & 31);
-        } else {
-            idx = (int64_t)m * a.ldc + n;
+            barrier_mem();
+            if ((int)threadIdx.x < PITERS) {
+                const int itx = threadIdx.x;
+                const float mx = fmaxf(fmaxf(red[itx * 4], red[itx * 4 + 1]), fmaxf(red[itx * 4 + 2], red[itx * 4 + 3]));
+                const int q0 = itx * NT;
+                const int plane = (n0 >> 5) + (q0 >> (LBM + 2));
+                const int row0 = (q0 & ((BM << 2) - 1)) >> 2;
+                if (plane * 32 < a.plane_max_cols)
+                    a.plane_max2[(int64_t)((m0 + row0) >> 6) * (a.plane_max_cols >> 5) + plane] = mx;
+            }
         }
-        *(f32x4*)(Cz + idx * esz) = v;                   // 16 bytes: 4 fp32 or 8 f16/bf16 values
+#pragma unroll 4
+        for (int q = threadIdx.x; q < (BM << lcpr); q += NT) {
+            int row, c;
+            if (headsplit) {                                 // head-major, then row, then chunk: contiguous in memory
+                const int h = q >> (LBM + lcph);
+                const int rem = q & ((BM << lcph) - 1);
+                row = rem >> lcph;
+                c = (h << lcph) + (rem & ((1 << lcph) - 1));
+            } else {
+                row = q >> lcpr;
+                c = q & ((1 << lcpr) - 1);
+            }
+            const int m = m0 + row;
+            if (m >= a.M) continue;
+            const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & ((1 << lcpr) - 1))) << 4));
+            const int n = n0 + c * cpe;
+            int64_t idx;
+            if (headsplit) {
+                int bb = b0, rr = rr0 + row;
+                if (rpb >= BM) {
+                    if (rr >= rpb) { rr -= rpb; ++bb; }
+                } else {
+                    bb = m / rpb;
+                    rr = m - bb * rpb;
+                }
+                idx = (((int64_t)bb * (a.N >> 5) + (n >> 5)) * rpb + rr) * 32 + (n & 31);
+            } else {
+                idx = (int64_t)m * a.ldc + n + (pass ? a.N : 0);
+            }
+            *(f32x4*)(Cz + idx * esz) = v;                   // 16 bytes: 4 fp32 or 8 f16/bf16 values
+        }
+
     }
 }
 
@@ -893,7 +938,8 @@ template <int BM, int BN, int S, int AMODE>
 int launch_dma_mode(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.M, BM), tn = a.N / BN;
     const int64_t nwg = (int64_t)tm * tn * a.batch;
-    if (a.w_dtype == CMT_BF16) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
+    if (a.w_dtype == CMT_BF16P) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE, true><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
+    else if (a.w_dtype == CMT_BF16) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     else gemm_dma_kernel<f16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     return cmt_check_launch("cmt_gemm");
 }
@@ -982,13 +1028,19 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
     CMT_REQUIRE(a.K % BK == 0, "cmt_gemm: K must be a multiple of 32");
     CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
-    CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16, "cmt_gemm: bad w_dtype");
+    CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_BF16P,
+                "cmt_gemm: bad w_dtype");
+    CMT_REQUIRE(a.w_dtype != CMT_BF16P || a.a_dtype == CMT_BF16P, "cmt_gemm: split-bf16 (CMT_BF16P) W needs CMT_BF16P A");
+    CMT_REQUIRE(a.c_dtype != CMT_BF16P || a.c_mode == CMT_C_ROWS, "cmt_gemm: a CMT_BF16P C must be row mode");
     CMT_REQUIRE(a.a_dtype == CMT_F32 || a.a_dtype == a.w_dtype, "cmt_gemm: A must be f32 or the compute dtype");
     CMT_REQUIRE(a.a_mode != CMT_A_CONV3X3 || a.a_dtype == a.w_dtype,
                 "cmt_gemm: the conv3x3 gather needs A in the compute dtype");
-    CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16, "cmt_gemm: bad c_dtype");
+    CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16 || a.c_dtype == CMT_BF16P,
+                "cmt_gemm: bad c_dtype");
     CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0, "cmt_gemm: lda/ldw must be multiples of 8 elements");
     CMT_REQUIRE(a.r_dtype == CMT_F32 || a.r_dtype == a.w_dtype, "cmt_gemm: R must be f32 or the compute dtype");
+    CMT_REQUIRE((a.c_dtype != CMT_BF16P && a.r_dtype != CMT_BF16P) || a.w_dtype == CMT_BF16P,
+                "cmt_gemm: CMT_BF16P C / R belong to the split-bf16 GEMM");
     CMT_REQUIRE(a.A2 == nullptr || (a.a_mode == CMT_A_ROWS && a.a2_cols % 128 == 0),
                 "cmt_gemm: A2 needs row mode and 128-aligned a2_cols");
     CMT_REQUIRE(a.A2 == nullptr || a.a2_mode == CMT_A2_SELECT || (a.a_dtype == CMT_F32 && a.lda2 % 4 == 0),

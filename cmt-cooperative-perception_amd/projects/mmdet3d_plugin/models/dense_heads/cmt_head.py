@@ -19,7 +19,7 @@ import torch.nn as nn
 
 from ... import native
 from ...registry import HEADS, build_bbox_coder, build_from_cfg, build_transformer
-from ...runtime import get_precision
+from ...runtime import get_precision, is_split, op_empty
 from ..utils.packing import PackCache, to_dtype
 from .engine import HeadEngineMixin
 from .train_engine import HeadTrainMixin
@@ -150,6 +150,8 @@ class SeparateTaskHead(nn.Module):
         width = len(tp["names"]) * 64
         k = tp["k"]
         X = x.reshape(L, B * Nq, C).contiguous().float()
+        if is_split(tp["w1"]):
+            X = native.split_rows(X.view(L * B * Nq, C)).view(L, B * Nq, 2, C)
         H1 = torch.empty((L, B * Nq, width), dtype=torch.float32, device=x.device)
         native.gemm(X, tp["w1"], H1, M=B * Nq, N=width, K=k * C, lda=C, ldw=k * C, ldc=width, batch=L,
                     a_bstride=B * Nq * C, w_bstride=width * k * C, c_bstride=B * Nq * width,
@@ -322,7 +324,7 @@ class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
                            device=self.reference_points.weight.device)
         outs16 = None
         if prec.gemm != torch.float32:
-            outs16 = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=prec.gemm, device=outs.device)
+            outs16 = op_empty(B * self.num_query, self.hidden_dim, prec.gemm, outs.device, lead=(L,))
         self._h2d_seq = 0    # staging-buffer slot of each camera-matrix upload in this forward (engine._h2d)
         for i, (x, x_img, metas) in enumerate(agents):
             flags = native.LN_NAN_TO_NUM | (native.LN_MAX_INTO if i > 0 else 0)

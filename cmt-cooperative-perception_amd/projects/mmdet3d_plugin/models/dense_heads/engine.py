@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from ... import native
-from ...runtime import get_precision
+from ...runtime import get_precision, op_empty
 from ..utils.packing import to_dtype
 
 __all__ = ["HeadEngineMixin"]
@@ -84,8 +84,8 @@ class HeadEngineMixin:
         if out is None:
             return native.linear(h, w2, b2)
         M = M if M is not None else h.shape[0]
-        native.gemm(h, w2, out, M=M, N=w2.shape[0], K=w2.shape[1], lda=h.shape[1], ldw=w2.shape[1],
-                    ldc=out.shape[-1], bias=b2, batch=batch, a_bstride=a_bstride * h.shape[1] if batch > 1 else 0,
+        native.gemm(h, w2, out, M=M, N=w2.shape[0], K=w2.shape[-1], lda=h.shape[-1], ldw=w2.shape[-1],
+                    ldc=out.shape[-1], bias=b2, batch=batch, a_bstride=a_bstride * h.shape[-1] if batch > 1 else 0,
                     c_bstride=c_bstride, c_offset=c_offset, R=R, ldr=out.shape[-1] if R is not None else 0,
                     r_bstride=c_bstride if R is not None else 0, r_offset=r_offset)
         return out
@@ -93,8 +93,7 @@ class HeadEngineMixin:
     def _shared_conv_into(self, x, mem, Nk, pk, prec):
         B, Cin, H, W = x.shape
         Cout = pk["conv_w"].shape[0]
-        in_dt = prec.gemm if prec.gemm != torch.float32 else torch.float32
-        xin = torch.empty((B * H * W, Cin), dtype=in_dt, device=x.device)
+        xin = op_empty(B * H * W, Cin, prec.gemm, x.device)
         native.nchw_to_rows(x.contiguous().float(), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
         native.gemm(xin, pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,
                     bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B,
@@ -136,7 +135,7 @@ class HeadEngineMixin:
         w0, b0, _, _ = pk["bev"]
 
         def build():
-            pe = torch.empty((H * W, 2 * C), dtype=w0.dtype, device=w0.device)
+            pe = op_empty(H * W, 2 * C, w0.dtype, w0.device)
             native.pos2embed(None, pe, n=H * W, F=C, grid=(x_size, y_size))
             hdt = pe.dtype if pe.dtype == w0.dtype else torch.float32
             return native.linear(pe, w0, b0, relu=True, out_dtype=hdt)
@@ -158,7 +157,7 @@ class HeadEngineMixin:
         lowp(memory + pos) -- the K-projection operand."""
         _, _, w2, b2 = pk["bev"]
         C, M = self.hidden_dim, hid.shape[0]
-        native.gemm(hid, w2, pos, M=M, N=w2.shape[0], K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
+        native.gemm(hid, w2, pos, M=M, N=w2.shape[0], K=w2.shape[-1], lda=hid.shape[-1], ldw=w2.shape[-1], ldc=C,
                     bias=b2, batch=B, a_bstride=0, c_bstride=Nk * C, R=R, ldr=C if R is not None else 0,
                     r_bstride=Nk * C if R is not None else 0)
 
@@ -184,7 +183,7 @@ class HeadEngineMixin:
         D = self.depth_num
         w0, b0, _, _ = pk["rv"]
         cdt = w0.dtype if (3 * D) % 64 == 0 else torch.float32
-        coords = torch.empty((BV * h * w, 3 * D), dtype=cdt, device=dev)
+        coords = op_empty(BV * h * w, 3 * D, cdt, dev)
         native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w, D=D, pad_h=float(pad_h), pad_w=float(pad_w),
                             depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
         hdt = cdt if cdt == w0.dtype else torch.float32
@@ -195,8 +194,8 @@ class HeadEngineMixin:
         C = self.hidden_dim
         _, _, w2, b2 = pk["rv"]
         M = hid.shape[0] // B   # V * h * w rows per batch element
-        native.gemm(hid, w2, pos, M=M, N=C, K=w2.shape[1], lda=hid.shape[1], ldw=w2.shape[1], ldc=C,
-                    bias=b2, batch=B, a_bstride=M * hid.shape[1], c_bstride=Nk * C, c_offset=offset * C,
+        native.gemm(hid, w2, pos, M=M, N=C, K=w2.shape[-1], lda=hid.shape[-1], ldw=w2.shape[-1], ldc=C,
+                    bias=b2, batch=B, a_bstride=M * hid.shape[-1], c_bstride=Nk * C, c_offset=offset * C,
                     R=R, ldr=C if R is not None else 0, r_bstride=Nk * C if R is not None else 0,
                     r_offset=offset * C)
 
@@ -213,7 +212,7 @@ class HeadEngineMixin:
         Nq = ref.shape[0]
 
         def build():
-            pe = torch.empty((Nq, 2 * C), dtype=pk["bev"][0].dtype, device=ref.device)
+            pe = op_empty(Nq, 2 * C, pk["bev"][0].dtype, ref.device)
             native.pos2embed(ref, pe, n=Nq, F=C, mode=1, pos_stride=3)
             qb = torch.empty((Nq, C), dtype=torch.float32, device=ref.device)
             self._mlp(pe, pk["bev"], qb, M=Nq)
@@ -251,7 +250,7 @@ class HeadEngineMixin:
         if w0.dtype != torch.float32 and (3 * D) % 64 == 0:
             # compute-dtype operand written by the geometry kernel (the same RNE rounding the
             # GEMM would apply on load): both MLP GEMMs then run on the LDS-DMA path
-            coords = torch.empty((B * V * Nq, 3 * D), dtype=w0.dtype, device=dev)
+            coords = op_empty(B * V * Nq, 3 * D, w0.dtype, dev)
             native.rv_query_coords_lowp(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
                                         pad_w=float(pad_w), pc_range=self.pc_range)
         else:
@@ -288,8 +287,8 @@ class HeadEngineMixin:
         # GEMM operands lowp(memory) and lowp(memory + pos) are written
         # directly by the conv / layout epilogues and the pos-MLP epilogues.
         mdt = prec.gemm if lowp else torch.float32
-        mem = torch.empty((B * Nk, C), dtype=mdt, device=dev)
-        pos = torch.empty((B * Nk, C), dtype=mdt, device=dev)
+        mem = op_empty(B * Nk, C, mdt, dev)
+        pos = op_empty(B * Nk, C, mdt, dev)
         R = mem if lowp else None
         cams = self._cams(metas, dev) if use_img else None
         dec = self.transformer.decoder

@@ -16,7 +16,7 @@ import torch.nn as nn
 from torch.nn.init import constant_, xavier_uniform_
 
 from ... import native
-from ...runtime import get_precision
+from ...runtime import SPLIT, get_precision, is_split, op_empty
 from .packing import PackCache, to_dtype
 
 __all__ = ["FlashAttention", "FlashMHA", "project_attend_project"]
@@ -125,15 +125,26 @@ def project_attend_project(q, k, v, q_pos, k_pos, w_in, b_in, w_out, b_out, iden
     C = q.shape[1]
     D = C // H
     dev = q.device
+    split = is_split(w_in)
     proj = []
     for i, (x, pos, n) in enumerate(((q, q_pos, Nq), (k, k_pos, Nk), (v, None, Nk))):
         y = torch.empty((x.shape[0], C), dtype=adt, device=dev)
         w = w_in[i * C:(i + 1) * C]
-        native.gemm(x, w, y, M=x.shape[0], N=C, K=C, lda=x.stride(0), ldw=w.stride(0), ldc=C,
-                    bias=None if b_in is None else b_in[i * C:(i + 1) * C], A2=pos,
-                    lda2=pos.stride(0) if pos is not None else 0, a2_cols=C if pos is not None else 0)
+        if split:
+            # split-bf16 operand of x (+ pos): one native pass writes the pair rows
+            xs = op_empty(x.shape[0], C, SPLIT, dev)
+            if pos is not None:
+                native.add_cast(x.contiguous(), rows=x.shape[0], C=C, Yp=xs, P=pos.contiguous())
+            else:
+                native.split_rows(x, xs)
+            native.gemm(xs, w, y, M=x.shape[0], N=C, K=C, lda=C, ldw=C, ldc=C,
+                        bias=None if b_in is None else b_in[i * C:(i + 1) * C])
+        else:
+            native.gemm(x, w, y, M=x.shape[0], N=C, K=C, lda=x.stride(0), ldw=w.stride(0), ldc=C,
+                        bias=None if b_in is None else b_in[i * C:(i + 1) * C], A2=pos,
+                        lda2=pos.stride(0) if pos is not None else 0, a2_cols=C if pos is not None else 0)
         proj.append(y)
-    o = torch.empty((q.shape[0], C), dtype=torch.float32, device=dev)
+    o = op_empty(q.shape[0], C, SPLIT if split else torch.float32, dev)
 
     def strides(n):
         if layout == "batch_first":
@@ -145,6 +156,6 @@ def project_attend_project(q, k, v, q_pos, k_pos, w_in, b_in, w_out, b_out, iden
                      k_strides=strides(Nk), v_strides=strides(Nk), o_strides=(ob, orow), scale=1.0 / math.sqrt(D),
                      round_output=round_out)
     out = torch.empty((q.shape[0], C), dtype=torch.float32, device=dev)
-    native.gemm(o, w_out, out, M=o.shape[0], N=C, K=C, lda=C, ldw=w_out.stride(0), ldc=C, bias=b_out,
+    native.gemm(o, w_out, out, M=o.shape[0], N=C, K=C, lda=C, ldw=native.lstride(w_out), ldc=C, bias=b_out,
                 R=identity, ldr=identity.stride(0) if identity is not None else 0)
     return out

@@ -35,4 +35,11 @@ class PackCache:
 
 
 def to_dtype(t, dtype):
+    """Weights in a compute format: a torch dtype, or the split-bf16 pair
+    (runtime.SPLIT): [..., K] -> [..., 2, K] with hi = bf16(w), lo = bf16(w - hi)."""
+    if dtype == torch.uint16:
+        w = t.detach().float()
+        hi = w.bfloat16()
+        lo = (w - hi.float()).bfloat16()
+        return torch.stack([hi, lo], dim=-2).contiguous().view(torch.uint16)
     return t.detach().to(dtype).contiguous()

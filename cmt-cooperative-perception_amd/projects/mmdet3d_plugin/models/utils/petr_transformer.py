@@ -30,7 +30,7 @@ from ... import native
 from ...registry import (ATTENTION, FEEDFORWARD_NETWORK, TRANSFORMER_LAYER, TRANSFORMER_LAYER_SEQUENCE,
                          build_from_cfg)
 from ...profiling import timed
-from ...runtime import get_precision
+from ...runtime import SPLIT, get_precision, op_empty
 from .attention import FlashMHA, project_attend_project
 from .packing import PackCache, to_dtype
 
@@ -416,7 +416,7 @@ class PETRTransformerDecoder(nn.Module):
                     vb.append(ca.in_proj_bias[2 * C:])
             kv_w = to_dtype(torch.cat(kw + vw, 0), g)
             kv_b = torch.cat(kb + vb, 0).detach().contiguous() if kb else None
-            kv_wp = native.kv_pack(kv_w) if (C == 256 and kv_w.dtype != torch.float32) else None
+            kv_wp = native.kv_pack(kv_w) if (C == 256 and kv_w.dtype in (torch.float16, torch.bfloat16)) else None
             return dict(layers=layers, kv_w=kv_w, kv_wp=kv_wp, kv_b=kv_b,
                         post=(self.post_norm.weight.detach().contiguous(),
                               self.post_norm.bias.detach().contiguous(), self.post_norm.eps))
@@ -499,7 +499,7 @@ class PETRTransformerDecoder(nn.Module):
         """The lowp chain path, whose layer-0 self-attention block depends only
         on the query embedding and can run beside the memory-side work."""
         prec = get_precision(prec)
-        return (prec.gemm != torch.float32 and self.fused_supported() and self._chain_ok()
+        return (prec.gemm in (torch.float16, torch.bfloat16) and self.fused_supported() and self._chain_ok()
                 and os.environ.get("CMT_CHAIN", "1") != "0")
 
     def lowp_state(self, *, B, Nk, Nq, prec, device):
@@ -579,7 +579,7 @@ class PETRTransformerDecoder(nn.Module):
             out = torch.empty((L, rows, C), dtype=f32, device=dev)
         scale = 1.0 / math.sqrt(32.0)
         if kv_operands is None:
-            memb = torch.empty((B * Nk, C), dtype=lp, device=dev)
+            memb = op_empty(B * Nk, C, lp, dev)
             mposb = torch.empty_like(memb)
             native.add_cast(mem, rows=B * Nk, C=C, Yl=memb, Yp=mposb, P=pos)
         else:
@@ -589,7 +589,7 @@ class PETRTransformerDecoder(nn.Module):
         # bf16: the K columns' per-64-row max |k|^2 (epilogue by-product) bounds every score,
         # so the cross-attention kernel needs no running max (cmt_hip.h kmax2)
         kmax2 = None
-        if prec.attn == torch.bfloat16 and os.environ.get("CMT_ATTN_BOUND", "1") != "0":
+        if prec.attn in (torch.bfloat16, torch.float16):
             kmax2 = torch.empty((-(-B * Nk // native.PLANE_MAX_ROWS), L * H), dtype=f32, device=dev)
         if pk["kv_wp"] is not None and memb.dtype == pk["kv_wp"].dtype and os.environ.get("CMT_KVPROJ", "1") != "0":
             native.kv_proj(memb, pk["kv_wp"], kv, M=B * Nk, N=2 * L * C, bias=pk["kv_b"], A2=mposb,
@@ -600,7 +600,7 @@ class PETRTransformerDecoder(nn.Module):
         # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114).
         # The chains never read the layer-0 target (chain A's residual is None), so there
         # it is only an output buffer and the first operands come from add_cast's zeros.
-        use_chain = self._chain_ok() and os.environ.get("CMT_CHAIN", "1") != "0"
+        use_chain = self._chain_ok() and lp != SPLIT and os.environ.get("CMT_CHAIN", "1") != "0"
         if use_chain and tgt0 is None:
             st = state if state is not None else self.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
             if not st["layer0_done"]:
@@ -617,18 +617,18 @@ class PETRTransformerDecoder(nn.Module):
             tgt = torch.empty((rows, C), dtype=f32, device=dev)
         else:
             tgt = torch.zeros((rows, C), dtype=f32, device=dev)
-        tl = torch.empty((rows, C), dtype=lp, device=dev)          # lowp(tgt)
+        tl = op_empty(rows, C, lp, dev)                            # lowp(tgt)
         tp = torch.empty_like(tl)                                  # lowp(tgt + qpos)
         native.add_cast(tgt if (tgt0 is not None or not use_chain) else None, rows=rows, C=C, Yl=tl, Yp=tp,
                         P=qpos)
         qkv = torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=dev)
         qc = torch.empty((B * C * Nq,), dtype=prec.attn, device=dev)
-        ob = torch.empty((rows, C), dtype=lp, device=dev)          # attention output (out-proj operand)
+        ob = op_empty(rows, C, lp, dev)                            # attention output (out-proj operand)
         t1 = torch.empty((rows, C), dtype=f32, device=dev)
         t1n = torch.empty_like(t1)
         o = torch.empty_like(t1)
         FF = pk["layers"][0]["f1_w"].shape[0]
-        hf = torch.empty((rows, FF), dtype=lp, device=dev)
+        hf = op_empty(rows, FF, lp, dev)
         ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
                        native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
         ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
@@ -714,7 +714,10 @@ class PETRTransformerDecoder(nn.Module):
                 native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
                                     W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         if out16 is not None:
-            native.cast(out, out16)
+            if lp == SPLIT:
+                native.split_rows(out.view(-1, C), out16.view(-1, 2, C))
+            else:
+                native.cast(out, out16)
         return out
 
     def _chain_layers(self, st, qpos, kv, kmax2, *, B, Nk, Nq, out, post_flags, prec, out16):

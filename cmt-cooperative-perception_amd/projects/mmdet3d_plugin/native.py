@@ -11,7 +11,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "available", "gemm", "gemm_ln", "chain", "kv_proj", "kv_pack", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
+__all__ = ["lib", "available", "gemm", "split_rows", "width", "lstride", "BF16P", "gemm_ln", "chain", "kv_proj", "kv_pack", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
            "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
            "voxelize", "box_decode", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
@@ -19,13 +19,15 @@ __all__ = ["lib", "available", "gemm", "gemm_ln", "chain", "kv_proj", "kv_pack",
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 _DEFAULT_LIB = os.path.join(_PKG_ROOT, "lib", "libcmt_hip.so")
 
-F32, F16, BF16 = 0, 1, 2
-DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
+F32, F16, BF16, BF16P = 0, 1, 2, 3
+# torch.uint16 (runtime.SPLIT) carries the split-bf16 pair format CMT_BF16P: a
+# logical [..., C] operand stored as [..., 2, C] (hi values, then lo values)
+DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.uint16: BF16P}
 LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -165,6 +167,7 @@ def _load():
         "cmt_masked_view_sum_ex": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _int, _vp], _int),
         "cmt_nchw_to_rows": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp], _int),
         "cmt_cast": ([_vp, _int, _vp, _int, _i64, _vp], _int),
+        "cmt_split_rows": ([_vp, _i64, _i64, _int, _vp, _vp], _int),
         "cmt_task_head_tail": ([_vp, _int, _int, _int, _int, _int, _vp, _vp, _vp, _vp, P(_int), _int, _int, _vp,
                                 _int, _int, P(_flt), _vp, _vp], _int),
         "cmt_box_decode": ([_vp, _i64, _vp, _i64, _vp, _int, _int, _int, _int, _int, P(_flt), _flt, _int,
@@ -305,6 +308,24 @@ def kv_proj(A, Wp, C, *, M, N, bias=None, A2=None, headsplit_rows, plane_max2=No
     _check(lib().cmt_kv_proj(ctypes.byref(g), _stream()), "cmt_kv_proj")
 
 
+def _ps(t):
+    """Physical 16-bit words per logical element: 2 for a split-bf16 pair
+    tensor, else 1.  Strides and offsets of the wrappers below are LOGICAL
+    (elements of the [..., C] operand) and scaled by this; pair offsets must
+    be whole rows."""
+    return 2 if t is not None and t.dtype == torch.uint16 else 1
+
+
+def width(t):
+    """Logical row width of an operand tensor (pair tensors are [..., 2, C])."""
+    return t.shape[-1]
+
+
+def lstride(t):
+    """Logical row stride of a 2-D (or pair [rows, 2, C]) operand tensor."""
+    return t.stride(0) // _ps(t)
+
+
 def _gemm_args(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0,
                a2_cols=0, a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0,
                bias_bstride=0, r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0,
@@ -312,22 +333,23 @@ def _gemm_args(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None
     _dev(A, W, C, bias, R, A2)
     g = GemmArgs()
     g.M, g.N, g.K, g.batch = M, N, K, batch
-    g.A = A.data_ptr() + a_offset * A.element_size()
-    g.lda, g.a_bstride, g.a_dtype = lda, a_bstride, DT[A.dtype]
-    g.A2 = None if A2 is None else A2.data_ptr() + a2_offset * A2.element_size()
-    g.lda2, g.a2_cols = lda2, a2_cols
+    sa, sw, sr, sc, s2 = _ps(A), _ps(W), _ps(R), _ps(C), _ps(A2)
+    g.A = A.data_ptr() + a_offset * sa * A.element_size()
+    g.lda, g.a_bstride, g.a_dtype = lda * sa, a_bstride * sa, DT[A.dtype]
+    g.A2 = None if A2 is None else A2.data_ptr() + a2_offset * s2 * A2.element_size()
+    g.lda2, g.a2_cols = lda2 * s2, a2_cols
     g.a2_mode = A2_ADD if (A2 is None or A.dtype == torch.float32) else A2_SELECT
     g.a_mode = a_mode
     g.conv_h, g.conv_w, g.conv_c = conv
     g.seg_len = seg_len
-    g.W, g.ldw, g.w_bstride, g.w_dtype = W.data_ptr(), ldw, w_bstride, DT[W.dtype]
+    g.W, g.ldw, g.w_bstride, g.w_dtype = W.data_ptr(), ldw * sw, w_bstride * sw, DT[W.dtype]
     g.bias = None if bias is None else bias.data_ptr()
     g.bias_bstride = bias_bstride
-    g.R = None if R is None else R.data_ptr() + r_offset * R.element_size()
-    g.ldr, g.r_bstride = ldr, r_bstride
+    g.R = None if R is None else R.data_ptr() + r_offset * sr * R.element_size()
+    g.ldr, g.r_bstride = ldr * sr, r_bstride * sr
     g.r_dtype = F32 if R is None else DT[R.dtype]
-    g.C = None if C is None else C.data_ptr() + c_offset * C.element_size()
-    g.ldc, g.c_bstride, g.c_dtype = ldc, c_bstride, DT[C.dtype] if C is not None else F32
+    g.C = None if C is None else C.data_ptr() + c_offset * sc * C.element_size()
+    g.ldc, g.c_bstride, g.c_dtype = ldc * sc, c_bstride * sc, DT[C.dtype] if C is not None else F32
     g.c_mode = C_HEADSPLIT if headsplit_rows else C_ROWS
     g.rows_per_batch = headsplit_rows
     g.relu = int(bool(relu))
@@ -336,14 +358,27 @@ def _gemm_args(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None
 
 def linear(X, W, bias=None, *, relu=False, R=None, out=None, out_dtype=torch.float32, A2=None, a2_cols=0,
            headsplit_rows=0):
-    """Row-major linear layer: X [M, K] (f32 or compute dtype), W [N, K]."""
-    M, K = X.shape
+    """Row-major linear layer: X [M, K] (f32 or compute dtype; pair [M, 2, K]),
+    W [N, K] (pair [N, 2, K]).  A split-bf16 W with an fp32 X splits X first."""
+    if W.dtype == torch.uint16 and X.dtype == torch.float32:
+        X = split_rows(X)
+    M, K = X.shape[0], width(X)
     N = W.shape[0]
     if out is None:
-        out = torch.empty((M, N), device=X.device, dtype=out_dtype)
-    gemm(X, W, out, M=M, N=N, K=K, lda=X.stride(0), ldw=W.stride(0), ldc=N, bias=bias, relu=relu, R=R,
-         ldr=(R.stride(0) if R is not None else 0), A2=A2, lda2=(A2.stride(0) if A2 is not None else 0),
+        out = torch.empty((M, 2, N) if out_dtype == torch.uint16 else (M, N), device=X.device, dtype=out_dtype)
+    gemm(X, W, out, M=M, N=N, K=K, lda=lstride(X), ldw=lstride(W), ldc=N, bias=bias, relu=relu, R=R,
+         ldr=(lstride(R) if R is not None else 0), A2=A2, lda2=(lstride(A2) if A2 is not None else 0),
          a2_cols=a2_cols, headsplit_rows=headsplit_rows)
+    return out
+
+
+def split_rows(X, out=None):
+    """fp32 rows X [M, C] (any row stride) -> split-bf16 pair rows [M, 2, C] (cmt_split_rows)."""
+    _dev(X, out)
+    M, C = X.shape
+    if out is None:
+        out = torch.empty((M, 2, C), dtype=torch.uint16, device=X.device)
+    _check(lib().cmt_split_rows(_p(X), X.stride(0), M, C, _p(out), _stream()), "cmt_split_rows")
     return out
 
 
@@ -368,8 +403,9 @@ def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_st
     a.k_bstride, a.k_hstride, a.k_rstride = k_strides
     a.V = V.data_ptr() + v_offset * es
     a.v_bstride, a.v_hstride, a.v_rstride = v_strides
-    a.O = O.data_ptr() + o_offset * O.element_size()
-    a.o_bstride, a.o_rstride = o_strides
+    so = _ps(O)
+    a.O = O.data_ptr() + o_offset * so * O.element_size()
+    a.o_bstride, a.o_rstride = o_strides[0] * so, o_strides[1] * so
     a.o_dtype = DT[O.dtype]
     a.scale, a.kv_splits = scale, kv_splits
     a.flags = (1 if round_output else 0) | (2 if fold_scale else 0) | _diag_flags
@@ -419,8 +455,8 @@ def _ln_args(X, W, Bv, *, rows, C, ldx, eps=1e-5, Y=None, ldy=0, flags=0, W2=Non
     a.ldy2, a.flags2 = ldy2, flags2
     low = Yl if Yl is not None else Yp
     a.lowp_dtype = DT[low.dtype] if low is not None else BF16
-    a.Yl, a.ldyl = _p(Yl), C
-    a.Yp, a.ldyp, a.P, a.ldp = _p(Yp), C, _p(P), C
+    a.Yl, a.ldyl = _p(Yl), C * _ps(Yl)
+    a.Yp, a.ldyp, a.P, a.ldp = _p(Yp), C * _ps(Yp), _p(P), C
     return a
 
 
@@ -515,7 +551,7 @@ def add_cast(X, *, rows, C, Yl=None, Yp=None, P=None):
 def pos2embed(pos, out, *, n, F, mode=0, pos_stride=2, grid=(0, 0), ldo=None):
     _dev(pos, out)
     _check(lib().cmt_pos2embed(_p(pos), pos_stride, n, F, mode, grid[0], grid[1], _p(out), DT[out.dtype],
-                               ldo if ldo is not None else 2 * F, _stream()), "cmt_pos2embed")
+                               (ldo if ldo is not None else 2 * F) * _ps(out), _stream()), "cmt_pos2embed")
 
 
 def rv_pe_coords(i2l, out, *, BV, h, w, D, pad_h, pad_w, depth_max, pc_range):
@@ -552,7 +588,7 @@ def rv_query_coords_lowp(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w,
 
 def nchw_to_rows(X, Y, *, nb, nv, C, HW, ldy, rows_per_batch, row_offset=0):
     _dev(X, Y)
-    _check(lib().cmt_nchw_to_rows(_p(X), nb, nv, C, HW, _p(Y), DT[Y.dtype], ldy, rows_per_batch, row_offset,
+    _check(lib().cmt_nchw_to_rows(_p(X), nb, nv, C, HW, _p(Y), DT[Y.dtype], ldy * _ps(Y), rows_per_batch, row_offset,
                                   _stream()), "cmt_nchw_to_rows")
 
 

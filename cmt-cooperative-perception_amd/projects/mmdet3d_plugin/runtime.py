@@ -7,22 +7,45 @@ custom_fp16=dict(pts_bbox_head=False), e.g.
 configs/CMT_Nuscenes/lidar/cmt_lidar_voxel0075_cbgs.py:284-286).
 
 Policies (``set_precision`` / env ``CMT_PRECISION``):
-  'ref'  -- the reference's numerics: GEMMs on the exact-f32 MFMA
-            (v_mfma_f32_32x32x2_f32), self-attention core in exact f32
-            (nn.MultiheadAttention), cross-attention core in fp16 with fp32
-            accumulation and an fp16-rounded output (flash-attn 0.2.2).
-  'fp16' -- GEMMs and attention in fp16 MFMA (fp32 accumulate).
-  'bf16' -- GEMMs and attention in bf16 MFMA (fp32 accumulate).
-Activations between kernels stay fp32 in HBM in every policy; K/V/Q for the
-attention kernels are written by the projection epilogue in the attention
-dtype.
+  'ref'   -- the reference's numerics with fp32-accurate split-bf16 GEMMs:
+             every fp32 GEMM operand is carried as a bf16 pair (hi, lo)
+             (``SPLIT``, cmt_hip.h CMT_BF16P) and multiplied in three bf16
+             MFMA passes (hi*hi + lo*hi + hi*lo, fp32 accumulate: ~2^-16
+             relative per product, against TF32's 2^-11); self-attention core
+             in exact f32 (nn.MultiheadAttention); cross-attention core in
+             fp16 with fp32 accumulation, P rounded to fp16 and an fp16-rounded
+             output (flash-attn 0.2.2 under auto_fp16).
+  'exact' -- as 'ref' but the GEMMs on the exact-f32 MFMA
+             (v_mfma_f32_32x32x2_f32, 1/16 of the bf16 rate): the yardstick the
+             split GEMMs are checked against.
+  'fp16'  -- GEMMs and attention in fp16 MFMA (fp32 accumulate).
+  'bf16'  -- GEMMs and attention in bf16 MFMA (fp32 accumulate).
+The residual stream and LayerNorm statistics stay fp32 in every policy; the
+producer of each GEMM operand writes it in the policy's operand format, and
+K/V/Q for the attention kernels are written by the projection epilogue in the
+attention dtype.
 """
 import os
 from dataclasses import dataclass
 
 import torch
 
-__all__ = ["Precision", "get_precision", "set_precision", "PRECISIONS"]
+__all__ = ["Precision", "get_precision", "set_precision", "PRECISIONS", "SPLIT", "op_empty", "is_split"]
+
+# Storage dtype of a split-bf16 operand: 16-bit words, a tensor of logical shape
+# [..., C] stored as [..., 2, C] (the C bf16 hi values, then the C bf16 lo values).
+SPLIT = torch.uint16
+
+
+def is_split(t):
+    return t is not None and t.dtype == SPLIT
+
+
+def op_empty(rows, C, dtype, device, lead=()):
+    """An operand buffer of logical shape [*lead, rows, C] in ``dtype`` (SPLIT:
+    [*lead, rows, 2, C] 16-bit words)."""
+    shape = tuple(lead) + ((rows, 2, C) if dtype == SPLIT else (rows, C))
+    return torch.empty(shape, dtype=dtype, device=device)
 
 
 @dataclass(frozen=True)
@@ -35,7 +58,8 @@ class Precision:
 
 
 PRECISIONS = {
-    "ref": Precision("ref", torch.float32, torch.float16, torch.float32, True),
+    "ref": Precision("ref", SPLIT, torch.float16, torch.float32, True),
+    "exact": Precision("exact", torch.float32, torch.float16, torch.float32, True),
     "fp16": Precision("fp16", torch.float16, torch.float16, torch.float16, False),
     "bf16": Precision("bf16", torch.bfloat16, torch.bfloat16, torch.bfloat16, False),
 }

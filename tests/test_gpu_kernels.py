@@ -235,13 +235,12 @@ def test_attention_bounded_max(N, dev, B, Nq, Nk, splits, scale_q):
 @pytest.mark.parametrize("B,Nq,Nk,splits,scale_q", [(1, 900, 56400, 0, 1.0), (2, 300, 4097, 3, 1.0),
                                                     (1, 257, 8192, 1, 1.0), (1, 900, 4160, 5, 1.0),
                                                     (1, 900, 32400, 0, 12.0)])
-def test_attention_pb2_matches_pb(N, dev, monkeypatch, B, Nq, Nk, splits, scale_q):
-    """Paired-tile pb kernel (128 keys per ping-pong window) against the one-tile
-    pb kernel on the same inputs: bit-identical on the offset-free path (same
-    per-score math, same tile order of the PV / row-sum accumulation), with odd
-    full-tile counts per split, a ragged last tile and 1-5 splits; with large |q|
-    (online-max fallback, one offset update per pair) within 1e-2 of it.  The
-    16x16x32 row-sum form (CMT_ATTN_RS16, the default) against the 32x32x16 one."""
+def test_attention_pb2_bounded_matches_online(N, dev, B, Nq, Nk, splits, scale_q):
+    """bf16 long-key kernel (128 keys per ping-pong window): the offset-free
+    bounded path (K norm partials) against the online-max path (no partials)
+    on the same inputs, odd full-tile counts per split, a ragged last tile and
+    1-5 splits; with large |q| every wave of the bounded launch falls back to
+    the online max (bound > 60 exp2 units) and the two launches agree exactly."""
     H = 8
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(Nk + Nq)
@@ -254,25 +253,23 @@ def test_attention_pb2_matches_pb(N, dev, monkeypatch, B, Nq, Nk, splits, scale_
     kmax2 = km.float().contiguous().to(dev)
     k = k.to(dev)
     outs = []
-    for pb2, rs16 in (("1", "0"), ("0", "0"), ("1", "1")):
-        monkeypatch.setenv("CMT_ATTN_PB2", pb2)
-        monkeypatch.setenv("CMT_ATTN_RS16", rs16)
+    for km2 in (kmax2, None):
         O = torch.empty(B, Nq, H * 32, device=dev)
         N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk,
                     q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
                     v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
-                    kv_splits=splits, fold_scale=True, kmax2=kmax2, kmax_ld=H, kmax_plane0=0)
+                    kv_splits=splits, fold_scale=True, kmax2=km2, kmax_ld=H if km2 is not None else 0,
+                    kmax_plane0=0)
         torch.cuda.synchronize()
         outs.append(O.cpu())
-    assert torch.isfinite(outs[0]).all() and torch.isfinite(outs[2]).all()
+    assert torch.isfinite(outs[0]).all() and torch.isfinite(outs[1]).all()
     if scale_q == 1.0:
-        assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
+        # P at another offset: bf16 rounding of P differs, O agrees to bf16 precision
+        assert (outs[0] - outs[1]).abs().max().item() < 2e-2
     else:
-        assert (outs[0] - outs[1]).abs().max().item() < 1e-2
-    # row sums on the 16x16x32 MFMA: same products, another f32 summation order
-    rel = ((outs[2] - outs[0]).abs() / (outs[0].abs() + 1e-3)).max().item()
-    print(f"pb2 16x16x32 row sums vs 32x32x16: max rel {rel:.2e}")
-    assert rel < 1e-4, rel
+        assert torch.equal(outs[0], outs[1])
+    ref = _attn_ref(q.cpu(), k.cpu(), v.cpu(), 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
+    assert (outs[0].double() - ref).abs().max().item() < 2e-2
 
 
 def test_gemm_dma_conv1d3_lowp(N, dev):
@@ -361,12 +358,11 @@ def test_attention(N, dev, dt, B, H, Nq, Nk, splits, fold):
     assert err < tol, err
 
 
-@pytest.mark.parametrize("kw", ["4", "8"])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("B,H,Nq,Nk,mode", [(1, 8, 900, 900, "rand"), (2, 3, 70, 65, "rand"), (1, 1, 5, 1, "rand"),
                                             (1, 2, 40, 4096, "rand"), (1, 1, 33, 700, "spike"),
                                             (1, 2, 70, 200, "negative")])
-def test_attention_key_split_workgroup(N, dev, monkeypatch, kw, dt, B, H, Nq, Nk, mode):
+def test_attention_key_split_workgroup(N, dev, dt, B, H, Nq, Nk, mode):
     """Short key ranges (self-attention): KW waves of one workgroup split the
     keys of the same 32 queries and merge (O, row sum, offset) through LDS.
     Fewer tiles than waves (waves without keys), a ragged last tile, 64 tiles,
@@ -387,13 +383,12 @@ def test_attention_key_split_workgroup(N, dev, monkeypatch, kw, dt, B, H, Nq, Nk
     qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
     for fold in (False, True):
         outs = []
-        for sel in (kw, "0"):
-            monkeypatch.setenv("CMT_ATTN_KW", sel)
+        for splits in (0, 2):   # 0: the in-workgroup key split; 2: split partials + combine
             O = torch.full((B, Nq, H * 32), float("nan"), device=dev)
             N.attention(qd, kd, vd, O, B=B, H=H, Nq=Nq, Nk=Nk,
                         q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
                         v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32),
-                        scale=1 / math.sqrt(32), fold_scale=fold)
+                        scale=1 / math.sqrt(32), fold_scale=fold, kv_splits=splits)
             torch.cuda.synchronize()
             outs.append(O.cpu().double())
         assert torch.isfinite(outs[0]).all()

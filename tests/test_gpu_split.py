@@ -1,0 +1,274 @@
+"""Split-bf16 ('ref' policy) kernels against float64 PyTorch references.
+
+The reference computes every projection / MLP / conv of the head in fp32; the
+'ref' policy carries each fp32 operand as a bf16 pair x = hi + lo (cmt_hip.h
+CMT_BF16P) and multiplies in three bf16 MFMA passes.  These tests hold the
+split GEMM (row, implicit 3x3 conv, implicit k=3 conv1d modes; fp32, f16
+head-split and pair outputs; pair residual), every producer of pair operands
+and the f16 long-key cross-attention (flash-attn 0.2.2 numerics) to bounds
+that an fp32 GEMM meets and a bf16 one misses by two orders of magnitude.
+Every call goes through the C ABI."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+SPLIT = torch.uint16
+
+
+@pytest.fixture(scope="module")
+def N():
+    from projects.mmdet3d_plugin import native
+    native.lib()
+    return native
+
+
+def _pair(x):
+    """fp32 [..., C] -> [..., 2, C] uint16 (the host restatement of the split)."""
+    hi = x.float().bfloat16()
+    lo = (x.float() - hi.float()).bfloat16()
+    return torch.stack([hi, lo], -2).contiguous().view(SPLIT)
+
+
+def _same(a, b):
+    """Bit equality of two pair tensors (16-bit words compared as int16)."""
+    return torch.equal(a.cpu().view(torch.int16), b.cpu().view(torch.int16))
+
+
+def _unpair(p):
+    b = p.view(torch.bfloat16).double()
+    return b[..., 0, :] + b[..., 1, :]
+
+
+def _tol(ref, K):
+    # three bf16 passes: <= ~2^-16 relative per product; random-sign sums over K
+    return 4e-5 * ref.abs().max().item() + 1e-6
+
+
+@pytest.mark.parametrize("M,N_,K", [(900, 256, 256), (130, 768, 512), (2000, 3072, 256), (64, 1024, 192),
+                                    (24000, 256, 1024)])
+def test_gemm_split_rows(N, dev, M, N_, K):
+    g = torch.Generator().manual_seed(M + N_ + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N_, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N_, generator=g)
+    R = torch.randn(M, N_, generator=g)
+    ref = A.double() @ W.double().t() + b.double()
+    out = torch.empty(M, N_, device=dev)
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), out, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_, bias=b.to(dev))
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= _tol(ref, K), err
+    # relu + fp32 residual, pair output (the next GEMM's operand) and pair residual
+    ref2 = torch.relu(ref) + R.double()
+    outp = torch.empty(M, 2, N_, dtype=SPLIT, device=dev)
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), outp, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_, bias=b.to(dev),
+           relu=True, R=_pair(R).to(dev), ldr=N_)
+    err2 = (_unpair(outp.cpu()) - ref2).abs().max().item()
+    # the pair output itself keeps 16 significant bits
+    assert err2 <= _tol(ref2, K) + 2 ** -16 * ref2.abs().max().item(), err2
+    bf = (A.bfloat16().double() @ W.bfloat16().double().t() + b.double() - ref).abs().max().item()
+    print(f"split GEMM {M}x{N_}x{K}: max abs err {err:.2e} (bf16 operands: {bf:.2e})")
+    assert err * 30 < bf
+
+
+def test_gemm_split_headsplit_select(N, dev):
+    """Q|K columns from A2 (select), V columns from A, head-split f16 / f32 output
+    with the key-norm partials (the K/V projection contract)."""
+    g = torch.Generator().manual_seed(3)
+    B, S, C = 2, 300, 256
+    M, N_ = B * S, 4 * C
+    A = torch.randn(M, C, generator=g)
+    A2 = torch.randn(M, C, generator=g)
+    W = torch.randn(N_, C, generator=g) / 16
+    b = torch.randn(N_, generator=g)
+    sel = torch.cat([A2.double() @ W[:2 * C].double().t(), A.double() @ W[2 * C:].double().t()], 1) + b.double()
+    for odt in (torch.float16, torch.float32):
+        out = torch.empty(B * N_ * S, dtype=odt, device=dev)
+        pm = torch.empty(-(-M // 64) * (2 * C // 32), device=dev) if odt == torch.float16 else None
+        N.gemm(_pair(A).to(dev), _pair(W).to(dev), out, M=M, N=N_, K=C, lda=C, ldw=C, ldc=0, bias=b.to(dev),
+               A2=_pair(A2).to(dev), lda2=C, a2_cols=2 * C, headsplit_rows=S, plane_max2=pm,
+               plane_max_cols=2 * C if pm is not None else 0)
+        got = out.cpu().double().view(B, N_ // 32, S, 32).permute(0, 2, 1, 3).reshape(M, N_)
+        if odt == torch.float16:
+            # one f16 rounding of the fp32-accurate result
+            assert torch.equal(got.half(), sel.half().double()) or \
+                (got - sel).abs().max().item() <= 2 ** -10 * sel.abs().max().item()
+            ss = (got[:, :2 * C].view(M, 2 * C // 32, 32) ** 2).sum(-1)
+            nb = -(-M // 64)
+            pref = torch.cat([ss, torch.zeros(nb * 64 - M, ss.shape[1], dtype=ss.dtype)], 0).view(nb, 64, -1).amax(1)
+            assert torch.allclose(pm.cpu().double().view(nb, -1), pref, rtol=1e-5, atol=1e-6)
+        else:
+            assert (got - sel).abs().max().item() <= _tol(sel, C)
+
+
+def test_gemm_split_conv3x3(N, dev):
+    """Implicit 3x3 conv (shared_conv) on split operands: NCHW fp32 -> pair rows
+    (cmt_nchw_to_rows) -> conv + BN-folded bias + ReLU into pair memory rows."""
+    g = torch.Generator().manual_seed(13)
+    B, Cin, H, W, Cout = 2, 128, 29, 33, 256
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / 34
+    b = torch.randn(Cout, generator=g)
+    xin = torch.empty(B * H * W, 2, Cin, dtype=SPLIT, device=dev)
+    N.nchw_to_rows(x.to(dev), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+    assert _same(xin, _pair(x.permute(0, 2, 3, 1).reshape(-1, Cin)))
+    wp = _pair(w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)).to(dev)
+    Nk = H * W + 5
+    out = torch.empty(B * Nk, 2, Cout, dtype=SPLIT, device=dev)
+    N.gemm(xin, wp, out, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout, bias=b.to(dev), relu=True,
+           a_mode=N.A_CONV3X3, conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin, c_bstride=Nk * Cout)
+    ref = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=1))
+    ref = ref.flatten(2).permute(0, 2, 1)
+    got = _unpair(out.cpu()).view(B, Nk, Cout)[:, :H * W]
+    err = (got - ref).abs().max().item()
+    assert err <= _tol(ref, 9 * Cin) + 2 ** -16 * ref.abs().max().item(), err
+
+
+def test_gemm_split_conv1d3_grouped(N, dev):
+    """The task heads' grouped k = 3 Conv1d (batched over layers) on split operands."""
+    g = torch.Generator().manual_seed(12)
+    L, B, Nq, C, O = 3, 2, 37, 256, 128
+    x = torch.randn(L, B * Nq, C, generator=g)
+    w = torch.randn(L * O, C, 3, generator=g) / 30
+    wp = w.view(L, O, C, 3).permute(0, 1, 3, 2).reshape(L, O, 3 * C)
+    out = torch.empty(L, B * Nq, O, device=dev)
+    N.gemm(_pair(x).to(dev), _pair(wp).to(dev), out, M=B * Nq, N=O, K=3 * C, lda=C, ldw=3 * C, ldc=O, batch=L,
+           a_bstride=B * Nq * C, w_bstride=O * 3 * C, c_bstride=B * Nq * O, a_mode=N.A_CONV1D3, seg_len=Nq)
+    xin = x.view(L, B, Nq, C).permute(1, 0, 3, 2).reshape(B, L * C, Nq).double()
+    ref = torch.nn.functional.conv1d(xin, w.double(), padding=1, groups=L)
+    ref = ref.view(B, L, O, Nq).permute(1, 0, 3, 2).reshape(L, B * Nq, O)
+    assert (out.cpu().double() - ref).abs().max().item() <= _tol(ref, 3 * C)
+
+
+def test_split_producers(N, dev):
+    """Every kernel that writes a pair operand writes exactly the host split of
+    the fp32 value it writes in the fp32 policy."""
+    g = torch.Generator().manual_seed(9)
+    rows, C = 301, 256
+    x = torch.randn(rows, C, generator=g) * 2
+    w, b = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    P = torch.randn(rows, C, generator=g)
+    xd, Pd = x.to(dev), P.to(dev)
+    Y = torch.empty(rows, C, device=dev)
+    Yl = torch.empty(rows, 2, C, dtype=SPLIT, device=dev)
+    Yp = torch.empty_like(Yl)
+    N.layernorm_ex(xd, w.to(dev), b.to(dev), rows=rows, C=C, ldx=C, Y=Y, ldy=C, Yl=Yl, Yp=Yp, P=Pd)
+    y = Y.cpu()
+    assert _same(Yl, _pair(y))
+    assert _same(Yp, _pair(y + P))
+    Zl, Zp = torch.empty_like(Yl), torch.empty_like(Yp)
+    N.add_cast(Y, rows=rows, C=C, Yl=Zl, Yp=Zp, P=Pd)
+    assert _same(Zl, Yl) and _same(Zp, Yp)
+    assert _same(N.split_rows(xd), _pair(x))
+    # pos2embed (BEV grid and reference points)
+    pos = torch.rand(1000, 3, device=dev)
+    o32 = torch.empty(1000, 512, device=dev)
+    op = torch.empty(1000, 2, 512, dtype=SPLIT, device=dev)
+    for o in (o32, op):
+        N.pos2embed(pos, o, n=1000, F=256, mode=1, pos_stride=3)
+    assert _same(op, _pair(o32.cpu()))
+    # rv_pe coordinates
+    i2l = torch.randn(3, 4, 4, device=dev)
+    r32 = torch.empty(3 * 8 * 10, 192, device=dev)
+    rp = torch.empty(3 * 8 * 10, 2, 192, dtype=SPLIT, device=dev)
+    for o in (r32, rp):
+        N.rv_pe_coords(i2l, o, BV=3, h=8, w=10, D=64, pad_h=128.0, pad_w=320.0, depth_max=61.2,
+                       pc_range=[-61.2, -61.2, -10.0, 61.2, 61.2, 10.0])
+    assert _same(rp, _pair(r32.cpu()))
+    # rv query coordinates + masked view sum (with the decoder's first operands)
+    B, V, Nq, D = 1, 2, 50, 64
+    ref = torch.rand(B, Nq, 3, device=dev)
+    l2i = torch.randn(B, V, 4, 4, device=dev) * 100
+    i2lq = torch.randn(B, V, 4, 4, device=dev)
+    q32 = torch.empty(B * V * Nq, 3 * D, device=dev)
+    qp = torch.empty(B * V * Nq, 2, 3 * D, dtype=SPLIT, device=dev)
+    m32 = torch.empty(B * V * Nq, device=dev)
+    mp = torch.empty_like(m32)
+    N.rv_query_coords(ref, l2i, i2lq, q32, m32, B=B, V=V, Nq=Nq, D=D, pad_h=640.0, pad_w=1600.0,
+                      pc_range=[-54.0, -54.0, -5.0, 54.0, 54.0, 3.0])
+    N.rv_query_coords_lowp(ref, l2i, i2lq, qp, mp, B=B, V=V, Nq=Nq, D=D, pad_h=640.0, pad_w=1600.0,
+                           pc_range=[-54.0, -54.0, -5.0, 54.0, 54.0, 3.0])
+    assert _same(qp, _pair(q32.cpu())) and torch.equal(mp, m32)
+    X = torch.randn(B * V * Nq, C, device=dev)
+    base = torch.randn(Nq, C, device=dev)
+    Yq = torch.empty(B * Nq, C, device=dev)
+    Ql, Qp = torch.empty(B * Nq, 2, C, dtype=SPLIT, device=dev), torch.empty(B * Nq, 2, C, dtype=SPLIT, device=dev)
+    N.masked_view_sum(X, m32, Yq, B=B, V=V, Nq=Nq, C=C, base=base, Yl=Ql, Yp=Qp)
+    assert _same(Qp, _pair(Yq.cpu()))
+    assert (_unpair(Ql.cpu()) == 0).all()
+
+
+def _attn_ref16(q, k, v, scale):
+    """flash-attn 0.2.2's f16 core (oracle.flash_core_fp16): f16 q/k/v, f32
+    scores and row statistics, P rounded to f16, f16 output -- in float64."""
+    s = (q.double() @ k.double().transpose(-1, -2)) * scale
+    p = torch.exp(s - s.amax(-1, keepdim=True))
+    return ((p.half().double() @ v.double()) / p.sum(-1, keepdim=True)).half().double()
+
+
+def _kmax2(k, B, Nk, H):
+    ss = (k.double().permute(0, 2, 1, 3).reshape(B * Nk, H, 32) ** 2).sum(-1)
+    nb = -(-B * Nk // 64)
+    return torch.cat([ss, torch.zeros(nb * 64 - B * Nk, H, dtype=ss.dtype)], 0).view(nb, 64, H).amax(1).float()
+
+
+@pytest.mark.parametrize("B,Nq,Nk,splits,mode", [(1, 900, 56400, 0, "rand"), (2, 300, 4097, 3, "rand"),
+                                                 (1, 257, 8192, 1, "rand"), (1, 900, 32400, 0, "loose"),
+                                                 (1, 300, 8192, 1, "loose"), (1, 900, 4160, 5, "scaled")])
+def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
+    """f16 long-key kernel (the 'ref' policy's cross-attention): bounded offsets
+    from the K norm partials, the loose-bound redo (one key of huge norm
+    orthogonal to every query: its bound puts every P of the split below
+    f16's normal range, so the workgroup reruns that split on the online max),
+    the online max alone (no partials), and the scale fold with q kept as
+    hi + lo.  Held to the f16 core's own output rounding."""
+    H = 8
+    g = torch.Generator().manual_seed(Nk + Nq)
+    sq = 3.0 if mode == "scaled" else 1.0
+    q = (torch.randn(B, H, Nq, 32, generator=g) * sq).half()
+    k = torch.randn(B, H, Nk, 32, generator=g).half()
+    v = torch.randn(B, H, Nk, 32, generator=g).half()
+    if mode == "loose":
+        q[..., 0] = 0
+        k[:, :, Nk // 2] = 0
+        k[:, :, Nk // 2, 0] = 500.0
+    ref = _attn_ref16(q, k, v, 1 / math.sqrt(32)).permute(0, 2, 1, 3).reshape(B, Nq, H * 32)
+    km = _kmax2(k, B, Nk, H).to(dev)
+    qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
+    outs = {}
+    for name, kmax2, fold in (("bounded", km, False), ("online", None, False), ("fold", km, True)):
+        O = torch.full((B, Nq, H * 32), float("nan"), device=dev)
+        N.attention(qd, kd, vd, O, B=B, H=H, Nq=Nq, Nk=Nk,
+                    q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                    v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
+                    kv_splits=splits, round_output=True, fold_scale=fold, kmax2=kmax2, kmax_ld=H if kmax2 is not None
+                    else 0, kmax_plane0=0)
+        torch.cuda.synchronize()
+        got = O.cpu().double()
+        assert torch.isfinite(got).all(), name
+        outs[name] = got
+    ulp = 2 ** -10 * ref.abs().clamp(min=2 ** -4)
+    for name in ("bounded", "online"):
+        d = (outs[name] - ref).abs()
+        # one f16 output ulp either way (P rounding at another offset moves O across a rounding boundary)
+        assert (d <= 2 * ulp + 1e-4).all(), (name, d.max().item())
+    # the fold permission rounds q*c once to f16: a slightly larger deviation, still small
+    assert (outs["fold"] - ref).abs().max().item() < 2e-2
+
+
+def test_attention_pair_output(N, dev):
+    """Attention output written as the split-bf16 operand of the out-projection:
+    exactly the split of the f32 output (f16-rounded values are exact as hi + lo)."""
+    g = torch.Generator().manual_seed(21)
+    B, H, Nq, Nk = 1, 8, 300, 5000
+    q, k, v = (torch.randn(B, H, n, 32, generator=g).half().to(dev) for n in (Nq, Nk, Nk))
+    O32 = torch.empty(B, Nq, H * 32, device=dev)
+    Op = torch.empty(B * Nq, 2, H * 32, dtype=SPLIT, device=dev)
+    for O in (O32, Op):
+        N.attention(q, k, v, O, B=B, H=H, Nq=Nq, Nk=Nk,
+                    q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
+                    v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=32 ** -0.5,
+                    round_output=True)
+    assert _same(Op, _pair(O32.cpu().view(B * Nq, H * 32)))
+    assert torch.equal(_unpair(Op.cpu()), O32.cpu().double().view(B * Nq, H * 32))
