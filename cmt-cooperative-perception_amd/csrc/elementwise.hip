@@ -378,7 +378,7 @@ __global__ void masked_view_sum_ex_kernel(const float* __restrict__ X, const flo
 // ---------------------------------------------------------------------------
 // NCHW -> token rows (64x64 tile transpose through LDS).
 // ---------------------------------------------------------------------------
-template <typename TO>
+template <typename TO, bool PAIR = false>
 __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restrict__ X, int nv, int C, int HW,
                                                            TO* Y, int64_t ldy, int64_t rows_per_batch,
                                                            int64_t row_offset) {
@@ -398,7 +398,8 @@ __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restri
         const int p = p0 + i, c = c0 + tx;
         if (p < HW && c < C) {
             const int64_t row = (int64_t)bo * rows_per_batch + row_offset + (int64_t)v * HW + p;
-            Y[row * ldy + c] = (TO)tile[tx][i];
+            if constexpr (PAIR) store_pair((bf16_t*)Y + row * ldy, C, c, tile[tx][i]);
+            else Y[row * ldy + c] = (TO)tile[tx][i];
         }
     }
 }
@@ -813,9 +814,12 @@ extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, v
     hipStream_t s = (hipStream_t)stream;
     const int esz = ydtype == CMT_F32 ? 4 : 2;
     if (ydtype == CMT_BF16P) {
-        CMT_REQUIRE(HW % 4 == 0 && C % 64 == 0 && ldy == 2 * C && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0,
-                    "cmt_nchw_to_rows: bf16-pair rows need HW % 4 == 0, C % 64 == 0, ldy == 2C, 16-byte alignment");
-        nchw_to_rows_vec_kernel<bf16_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
+        CMT_REQUIRE(ldy == 2 * C, "cmt_nchw_to_rows: bf16-pair rows need ldy == 2C (hi row, then lo row)");
+        if (HW % 4 == 0 && C % 64 == 0 && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0)
+            nchw_to_rows_vec_kernel<bf16_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
+                                                                       row_offset);
+        else
+            nchw_to_rows_kernel<bf16_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
                                                                    row_offset);
         return cmt_check_launch("cmt_nchw_to_rows");
     }

@@ -53,6 +53,15 @@ class Boxes3D:
         return torch.cat([t[:, :2], t[:, 2:3] + t[:, 5:6] * 0.5], 1)
 
 
+def _gravity_boxes(g):
+    """GT boxes [n, 9] with gravity centres: LiDARInstance3DBoxes-like objects
+    (anything with ``gravity_center`` and ``tensor``, cmt_head.py:571-573) are
+    converted; plain tensors are taken as gravity-centre boxes already."""
+    if hasattr(g, "gravity_center") and hasattr(g, "tensor"):
+        return torch.cat([g.gravity_center, g.tensor[:, 3:]], 1)
+    return g
+
+
 def _normalize_bbox(b):
     """core/bbox/util.py:8-34."""
     return torch.cat([b[..., 0:3], b[..., 3:6].log(), b[..., 6:7].sin(), b[..., 6:7].cos(), b[..., 7:9]], -1)
@@ -160,8 +169,7 @@ class HeadTrainMixin:
         mems, poss = [], []
         if x is not None and self.shared_conv is not None:
             _, Cin, H, W = x.shape
-            xr = torch.empty((B * H * W, Cin), dtype=torch.float32, device=x.device)
-            native.nchw_to_rows(x.contiguous().float(), xr, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+            xr = ops.nchw_rows(x, B)
             conv = self.shared_conv.conv
             w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1)
             y = ops.bn_relu(ops.conv3x3(xr, w, (B, H, W, Cin)), self.shared_conv.bn)
@@ -174,10 +182,7 @@ class HeadTrainMixin:
         if x_img is not None:
             BV, _, h, w_ = x_img.shape
             V = BV // B
-            xi = torch.empty((B * V * h * w_, C), dtype=torch.float32, device=x_img.device)
-            native.nchw_to_rows(x_img.contiguous().float(), xi, nb=B, nv=V, C=C, HW=h * w_, ldy=C,
-                                rows_per_batch=V * h * w_)
-            mems.append(xi.view(B, V * h * w_, C))
+            mems.append(ops.nchw_rows(x_img, B).view(B, V * h * w_, C))
             pad_h, pad_w, _ = metas[0]["pad_shape"][0]
             i2l = torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
                                              for m in metas])).float().to(x_img.device)
@@ -265,14 +270,16 @@ class HeadTrainMixin:
         ref, mask_dict = self.prepare_for_dn_train(B, gt_boxes, gt_labels, rand_prob)
         rp = inverse_sigmoid(ref.clone()).sigmoid()
         qpos = self._mlp_t(_pos2embed(rp, C), self.bev_embedding)
-        dec = None
+        decs = []
         for x, x_img, metas in agents:
             q = qpos
             if x_img is not None and self.rv_embedding is not None:
                 q = q + self._rv_query_embed_t(rp, metas)
             mem, pos = self._memory_t(x, x_img, metas, B)
-            d = self._decoder_t(torch.zeros_like(q), q, mem, pos, mask_dict)
-            dec = d if dec is None else torch.maximum(dec, d)     # coop max fusion (cmt_head_coop.py:383-389)
+            decs.append(self._decoder_t(torch.zeros_like(q), q, mem, pos, mask_dict))
+        # coop max fusion as the reference writes it (cmt_head_coop.py:388-389): torch.max over the
+        # stacked agents routes each element's gradient to ONE agent (the max index), also on ties
+        dec = decs[0] if len(decs) == 1 else torch.max(torch.stack(decs), 0).values
         reference = inverse_sigmoid(ref.clone())
         preds = []
         flag = 0
@@ -308,21 +315,61 @@ class HeadTrainMixin:
                     match_cls_weight=float(asg.get("cls_cost", {}).get("weight", 2.0)),
                     match_reg_weight=float(asg.get("reg_cost", {}).get("weight", 0.25)), code_weights=cw)
 
-    def _targets(self, pb, pl, gtb, gtl, cfg, code_w):
-        """_get_targets_single + HungarianAssigner3D for one (sample, task)."""
-        Nq, ncls = pl.shape
-        dev = pl.device
+    def _assign_all(self, preds, gtb, gtl, cfg, code_w):
+        """HungarianAssigner3D (hungarian_assigner_3d.py:68-156) for every
+        (layer, task, sample): the [Nq, n_gt] cost matrices are built on the
+        device (cmt_match_cost), copied to the host in ONE transfer, solved by
+        scipy's linear_sum_assignment as the reference does, and the matched
+        (query, gt) index pairs go back in ONE transfer.  Returns
+        {(l, t, b): (rows, cols) device index tensors (None: no GT), n_pos}."""
+        L, B = preds[0]["center"].shape[:2]
+        dev = preds[0]["center"].device
+        jobs, costs = [], []
+        flag = 0
+        for t, d in enumerate(preds):
+            ncls = self.num_classes[t]
+            for l in range(L):
+                pb = torch.cat([d[k][l] for k in ("center", "height", "dim", "rot", "vel")], -1)    # [B, Nq, 10]
+                pl = d["cls_logits"][l]
+                for b in range(B):
+                    m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
+                    g_b, gl_b = gtb[b][m], gtl[b][m] - flag
+                    if g_b.shape[0] == 0:
+                        continue
+                    cost = T.match_cost(pl[b].detach().contiguous(), pb[b].detach().contiguous(),
+                                        _normalize_bbox(g_b).contiguous(), gl_b.int().contiguous(), code_w,
+                                        gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["match_cls_weight"],
+                                        reg_weight=cfg["match_reg_weight"])
+                    jobs.append(((l, t, b), cost.shape))
+                    costs.append(cost.reshape(-1))
+            flag += ncls
+        out = {}
+        if not jobs:
+            return out
+        host = torch.cat(costs).cpu().numpy()                     # the one device -> host copy
+        rows, cols, off = [], [], 0
+        for key, shape in jobs:
+            n = shape[0] * shape[1]
+            r, c = linear_sum_assignment(host[off:off + n].reshape(shape))
+            off += n
+            rows.append(r)
+            cols.append(c)
+        lens = [len(r) for r in rows]
+        both = torch.from_numpy(np.stack([np.concatenate(rows), np.concatenate(cols)]).astype(np.int64)).to(dev)
+        start = 0
+        for (key, _), n in zip(jobs, lens):
+            out[key] = (both[0, start:start + n], both[1, start:start + n])
+            start += n
+        return out
+
+    def _targets(self, Nq, ncls, gtb, gtl, match, dev):
+        """_get_targets_single for one (sample, task) from its assignment."""
         labels = torch.full((Nq,), ncls, dtype=torch.int32, device=dev)
         tgt = torch.zeros((Nq, 9), dtype=torch.float32, device=dev)
         bw = torch.zeros((Nq, 10), dtype=torch.float32, device=dev)
-        if gtb.shape[0] == 0:
+        if match is None:
             return labels, tgt, bw, 0, Nq
-        cost = T.match_cost(pl.detach().contiguous(), pb.detach().contiguous(), _normalize_bbox(gtb).contiguous(),
-                            gtl.int().contiguous(), code_w, gamma=cfg["gamma"], alpha=cfg["alpha"],
-                            cls_weight=cfg["match_cls_weight"], reg_weight=cfg["match_reg_weight"])
-        r, c = linear_sum_assignment(cost.cpu().numpy())          # host, as the reference (scipy)
-        r = torch.from_numpy(r).to(dev)
-        c = torch.from_numpy(c).to(dev)
+        r, c = match
         labels[r] = gtl[c].int()
         tgt[r] = gtb[c].float()
         bw[r] = 1.0
@@ -344,11 +391,21 @@ class HeadTrainMixin:
         cfg = self._loss_cfg()
         dev = preds[0]["center"].device
         code_w = torch.tensor(cfg["code_weights"], dtype=torch.float32, device=dev)
-        gtb = [(g.gravity_center if False else g).to(dev).float() if not isinstance(g, Boxes3D)
-               else torch.cat([g.gravity_center, g.tensor[:, 3:]], 1).to(dev).float() for g in gt_bboxes_3d]
+        gtb = [_gravity_boxes(g).to(dev).float() for g in gt_bboxes_3d]
         gtl = [l.to(dev).long() for l in gt_labels_3d]
         L, B = preds[0]["center"].shape[:2]
         eps = float(torch.finfo(torch.float32).eps)   # mmdet weight_reduce_loss avg_factor + eps
+        matches = self._assign_all(preds, gtb, gtl, cfg, code_w)
+        # reduce_mean of the DN target count (cmt_head_coop.py:686): the same for every layer and task, so
+        # one all-reduce per step -- issued on EVERY rank, also when its frames carry no GT (a rank that
+        # skipped it would pair the next collective, the gradient all-reduce, with this one)
+        md0 = next((d.get("dn_mask_dict") for d in preds if d.get("dn_mask_dict") is not None), None)
+        num_tgt = float(md0["known_indice"].numel()) if md0 is not None else 0.0
+        if dist.is_available() and dist.is_initialized():
+            nt_t = torch.tensor([num_tgt], device=dev)
+            dist.all_reduce(nt_t)
+            num_tgt = float(nt_t.item()) / dist.get_world_size()
+        num_tgt = max(num_tgt, 1.0)
         losses = {}
         for l in range(L):
             tot = {"loss_cls": 0.0, "loss_bbox": 0.0, "dn_loss_cls": 0.0, "dn_loss_bbox": 0.0}
@@ -360,7 +417,8 @@ class HeadTrainMixin:
                 labs, tgts, bws, npos, nneg = [], [], [], 0, 0
                 for b in range(B):
                     m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
-                    lab, tg, bw, p_, n_ = self._targets(pb[b], pl[b], gtb[b][m], gtl[b][m] - flag, cfg, code_w)
+                    lab, tg, bw, p_, n_ = self._targets(pl.shape[1], ncls, gtb[b][m], gtl[b][m] - flag,
+                                                        matches.get((l, t, b)), dev)
                     labs.append(lab); tgts.append(tg); bws.append(bw)
                     npos += p_; nneg += n_
                 nt, w = self._box_terms(torch.cat(tgts), torch.cat(bws), code_w)
@@ -373,7 +431,7 @@ class HeadTrainMixin:
                 tot["loss_bbox"] = tot["loss_bbox"] + torch.nan_to_num(out[1])
                 md = d.get("dn_mask_dict")
                 if md is not None and md["pad_size"] > 0:
-                    dout = self._dn_loss(d, l, md, ncls, cfg, code_w, eps)
+                    dout = self._dn_loss(d, l, md, ncls, cfg, code_w, eps, num_tgt)
                     tot["dn_loss_cls"] = tot["dn_loss_cls"] + dout[0]
                     tot["dn_loss_bbox"] = tot["dn_loss_bbox"] + dout[1]
                 flag += ncls
@@ -383,8 +441,9 @@ class HeadTrainMixin:
                     losses[key + k] = v
         return losses
 
-    def _dn_loss(self, d, l, md, ncls, cfg, code_w, eps):
-        """_dn_loss_single_task (cmt_head.py:760-806)."""
+    def _dn_loss(self, d, l, md, ncls, cfg, code_w, eps, nt):
+        """_dn_loss_single_task (cmt_head.py:760-806); ``nt``: the reduce_mean'd,
+        clamped DN target count of the step (loss())."""
         kl, kb = md["known_lbs_bboxes"]
         raw = md["known_labels_raw"]
         bid = md["batch_idx"][md["known_indice"]]
@@ -396,11 +455,6 @@ class HeadTrainMixin:
         any_task = bool(task_mask.any())
         rows = task_mask if any_task else torch.ones_like(task_mask)
         cls_avg = max(num_tgt * 3.14159 / 6 * self.split ** 3, 1)
-        nt_t = torch.tensor([float(num_tgt)], device=pl.device)
-        if dist.is_available() and dist.is_initialized():       # reduce_mean (cmt_head_coop.py:686)
-            dist.all_reduce(nt_t)
-            nt_t = nt_t / dist.get_world_size()
-        nt = max(float(nt_t.item()), 1.0)
         ntg, w = self._box_terms(kb[rows].float(), torch.ones((int(rows.sum()), 10), device=pl.device), code_w)
         # the classification term covers every DN row, the box term only the task's rows
         lw = torch.ones(pl.shape[0], dtype=torch.float32, device=pl.device)

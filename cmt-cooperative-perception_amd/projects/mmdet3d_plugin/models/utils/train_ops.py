@@ -12,7 +12,9 @@ Reference semantics (training step of CmtHead / CmtHeadCoop):
   LayerNorm       nn.LayerNorm (eps 1e-5) and GroupLayerNorm1d (cmt_head.py:53-94)
   BN + ReLU       shared_conv's BatchNorm2d (training statistics) + ReLU
   conv3x3         shared_conv's Conv2d (no bias): forward on cmt_gemm's exact-f32
-                  implicit-GEMM path, weight gradient = dY^T im2col(X)
+                  implicit-GEMM path, weight gradient = dY^T im2col(X), input
+                  gradient = the same implicit conv on the flipped weights
+  nchw_rows       the memory-row layout of the feature maps (gradient back to NCHW)
 """
 import math
 
@@ -21,7 +23,7 @@ import torch
 from ... import native
 from ... import native_train as T
 
-__all__ = ["linear", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "det_loss"]
+__all__ = ["linear", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss"]
 
 
 class _Linear(torch.autograd.Function):
@@ -107,6 +109,11 @@ class _BnRelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, running_mean, running_var, eps, momentum):
         y, mean, rstd = T.bn_relu_train_fwd(x, w, b, running_mean, running_var, eps=eps, momentum=momentum)
+        # the kernel updated the running statistics through their pointers: bump the versions so
+        # weight packs built from them (the BN fold of the inference engine) are rebuilt
+        for t in (running_mean, running_var):
+            if t is not None:
+                torch.autograd.graph.increment_version(t)
         ctx.save_for_backward(x, y, w, mean, rstd)
         return y
 
@@ -149,13 +156,45 @@ class _Conv3x3(torch.autograd.Function):
             dw = torch.zeros((Cout, 9 * Cin), dtype=torch.float32, device=x.device)
             T.gemm_ex(dy.contiguous(), (1, Cout), col, (1, 9 * Cin), dw, M=Cout, N_=9 * Cin, K=rows, ldc=9 * Cin,
                       beta=1.0, ksplit=max(ks, 2))
+        dx = None
         if ctx.needs_input_grad[0]:
-            raise NotImplementedError("shared_conv input gradient (the BEV backbone is out of scope)")
-        return None, dw, None
+            # dX = conv3x3(dY, W'), W'[cin][tap][cout] = W[cout][8 - tap][cin]: the transposed conv is the
+            # same implicit GEMM on the spatially flipped, transposed weights (zero padding included)
+            wt = w.view(Cout, 9, Cin).flip(1).permute(2, 1, 0).reshape(Cin, 9 * Cout).contiguous()
+            dx = torch.empty((B * H * W, Cin), dtype=torch.float32, device=x.device)
+            native.gemm(dy.contiguous(), wt, dx, M=H * W, N=Cin, K=9 * Cout, lda=Cout, ldw=9 * Cout, ldc=Cin,
+                        a_mode=native.A_CONV3X3, conv=(H, W, Cout), batch=B, a_bstride=H * W * Cout,
+                        c_bstride=H * W * Cin)
+        return dx, dw, None
 
 
 def conv3x3(x_rows, w_tap_major, geom):
     return _Conv3x3.apply(x_rows, w_tap_major, geom)
+
+
+class _NchwRows(torch.autograd.Function):
+    """Feature maps [B*V, C, H, W] -> memory rows [B*V*H*W, C] ("(bs v) c h w ->
+    bs (v h w) c", cmt_transformer.py:104-105) on the native layout kernel;
+    the backward is the transpose back, so the backbone / neck that produced
+    the maps receives its gradient as in the reference."""
+
+    @staticmethod
+    def forward(ctx, x, B):
+        BV, C, H, W = x.shape
+        y = torch.empty((BV * H * W, C), dtype=torch.float32, device=x.device)
+        native.nchw_to_rows(x.contiguous().float(), y, nb=B, nv=BV // B, C=C, HW=H * W, ldy=C,
+                            rows_per_batch=BV // B * H * W)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        BV, C, H, W = ctx.shape
+        return dy.view(BV, H * W, C).transpose(1, 2).reshape(BV, C, H, W), None
+
+
+def nchw_rows(x, B):
+    return _NchwRows.apply(x, B)
 
 
 class _DetLoss(torch.autograd.Function):

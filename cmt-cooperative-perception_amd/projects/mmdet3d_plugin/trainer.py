@@ -11,9 +11,10 @@ MI355X design: every trainable parameter of the head is re-pointed into ONE
 flat fp32 buffer and its .grad into ONE flat gradient buffer (autograd then
 accumulates straight into it), so the gradient exchange is a few large
 RCCL all-reduces over contiguous buckets (fewer, larger collectives: each
-xGMI ring step moves bucket/world bytes per link), the clip's global norm is
-one native sum-of-squares pass and the AdamW update one native launch over
-the whole buffer.  With world size 1 there is no collective at all.
+xGMI ring step moves bucket/world bytes per link) launched from
+post-accumulate-grad hooks while backward is still running, the clip's global
+norm is one native sum-of-squares pass and the AdamW update one native launch
+over the whole buffer.  With world size 1 there is no collective at all.
 """
 import torch
 import torch.distributed as dist
@@ -70,9 +71,77 @@ def allreduce_buckets(flat, bucket_bytes=25 << 20, group=None):
     return len(works)
 
 
+class _GradBuckets:
+    """Gradient all-reduce overlapped with backward (mmcv
+    MMDistributedDataParallel / torch DDP semantics, tools/train.py:282-289):
+    the flat gradient buffer is cut at parameter boundaries into buckets of
+    ~bucket_bytes in REVERSE parameter order (backward produces the last
+    layers' gradients first); a post-accumulate-grad hook counts each bucket's
+    parameters and, once a bucket is complete, launches the async all-reduces
+    of every complete bucket in bucket order -- the same launch sequence on
+    every rank whatever order autograd finishes them in, so the collectives
+    pair up.  finish() flushes buckets whose parameters got no gradient, waits
+    for all of them and scales by 1 / world."""
+
+    def __init__(self, fp, bucket_bytes, group):
+        self.fp, self.group = fp, group
+        self.world = dist.get_world_size(group)
+        self.buckets = []                      # (lo, hi, n_params), in launch order
+        self.of_param = [0] * len(fp.params)
+        lo = hi = None
+        members = 0
+        for i in reversed(range(len(fp.params))):
+            off, k = fp.slices[i]
+            if hi is None:
+                hi = off + k
+            lo = off
+            members += 1
+            self.of_param[i] = len(self.buckets)
+            if (hi - lo) * 4 >= bucket_bytes:
+                self.buckets.append((lo, hi, members))
+                lo = hi = None
+                members = 0
+        if hi is not None:
+            self.buckets.append((lo, hi, members))
+        self.handles = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(fp.params)]
+        self.reset()
+
+    def reset(self):
+        self.pending = [n for _, _, n in self.buckets]
+        self.next = 0
+        self.works = []
+
+    def _launch_ready(self, upto=None):
+        end = len(self.buckets) if upto is None else upto
+        while self.next < end and (upto is not None or self.pending[self.next] == 0):
+            lo, hi, _ = self.buckets[self.next]
+            self.works.append(dist.all_reduce(self.fp.grad[lo:hi], group=self.group, async_op=True))
+            self.next += 1
+
+    def _make_hook(self, i):
+        def hook(_param):
+            b = self.of_param[i]
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self._launch_ready()
+        return hook
+
+    def finish(self):
+        self._launch_ready(upto=len(self.buckets))
+        for w in self.works:
+            w.wait()
+        self.fp.grad.mul_(1.0 / self.world)
+        n = len(self.works)
+        self.reset()
+        return n
+
+
 class Trainer:
-    """One optimisation step: backward of the summed loss dict, bucketed
-    gradient all-reduce, clip_grad_norm_(max_norm), AdamW."""
+    """One optimisation step: backward of the summed loss dict with the
+    bucketed gradient all-reduce overlapped (world > 1), clip_grad_norm_
+    (max_norm), AdamW.  At construction, rank 0's parameters and buffers are
+    broadcast to every rank (as MMDistributedDataParallel does), so ranks
+    that started from different initialisations train the same model."""
 
     def __init__(self, module, lr=1e-4, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-8, max_norm=35.0,
                  bucket_mb=25, group=None):
@@ -85,6 +154,29 @@ class Trainer:
         self.exp_avg_sq = torch.zeros_like(self.fp.flat)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=self.fp.flat.device)
         self.step_count = 0
+        self.buckets = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast(self.fp.flat, src, group=group)
+            for b in module.buffers():
+                if b.dtype.is_floating_point or b.dtype in (torch.int64, torch.int32):
+                    dist.broadcast(b, src, group=group)
+            self._bump_versions()
+            self.buckets = _GradBuckets(self.fp, self.bucket_bytes, group)
+
+    def set_hyperparams(self, lr=None, betas=None):
+        """Per-step learning rate / momentum (the reference's cyclic lr and
+        momentum schedules are applied by the caller through this)."""
+        if lr is not None:
+            self.lr = float(lr)
+        if betas is not None:
+            self.betas = tuple(betas)
+
+    def _bump_versions(self):
+        # the native AdamW (and the broadcast) write the parameters through their pointers: bump
+        # Tensor._version so weight packs keyed on it (packing.PackCache) are rebuilt
+        for p in self.fp.params:
+            torch.autograd.graph.increment_version(p)
 
     def backward(self, losses):
         total = sum(losses.values()) if isinstance(losses, dict) else losses
@@ -94,7 +186,8 @@ class Trainer:
 
     def step(self, losses):
         total = self.backward(losses)
-        allreduce_buckets(self.fp.grad, self.bucket_bytes, self.group)
+        if self.buckets is not None:
+            self.buckets.finish()
         self.step_count += 1
         self.sumsq.zero_()
         if self.max_norm and self.max_norm > 0:
@@ -102,4 +195,5 @@ class Trainer:
         T.adamw_step(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, step=self.step_count, lr=self.lr,
                      beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=self.wd,
                      max_norm=self.max_norm or 0.0, sumsq_buf=self.sumsq)
+        self._bump_versions()
         return total.detach()

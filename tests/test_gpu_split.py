@@ -248,11 +248,13 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
         got = O.cpu().double()
         assert torch.isfinite(got).all(), name
         outs[name] = got
-    ulp = 2 ** -10 * ref.abs().clamp(min=2 ** -4)
+    # an f16 output ulp either way (P rounded at another offset moves O across a rounding boundary;
+    # 2^-9 |x| covers one ulp of the larger neighbour at a binade boundary), plus the f16 rounding of
+    # the dominant P itself when a few keys carry the row (scaled q): 2^-11 of the largest |v|
+    tol = 2 ** -9 * ref.abs().clamp(min=2 ** -4) + 2 ** -11 * v.double().abs().max().item()
     for name in ("bounded", "online"):
         d = (outs[name] - ref).abs()
-        # one f16 output ulp either way (P rounding at another offset moves O across a rounding boundary)
-        assert (d <= 2 * ulp + 1e-4).all(), (name, d.max().item())
+        assert (d <= tol).all(), (name, d.max().item())
     # the fold permission rounds q*c once to f16: a slightly larger deviation, still small
     assert (outs["fold"] - ref).abs().max().item() < 2e-2
 

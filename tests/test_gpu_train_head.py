@@ -27,10 +27,12 @@ def _gt(B, pc_range, ncls, n, seed):
     return boxes, labels
 
 
-def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5):
+def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5, coop=False):
     from oracle import cmt_oracle as O
     from oracle import cmt_train_oracle as TO
     from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.models.dense_heads.cmt_head_coop import (get_infrastructure_image_metas,
+                                                                          get_vehicle_image_metas)
     head, cfg, _ = S.build_synthetic_head(name, num_query=Nq, num_layers=L, grid_size=[128, 128, 40])
     oc = O.cfg_from_head_cfg(cfg)
     sd_cpu = {k: v.detach().double().clone() for k, v in head.state_dict().items()}
@@ -43,6 +45,20 @@ def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5):
     xi = S.synthetic_img(B * 2, 8, 20, seed=6) if variant == "fusion" else None
     metas = S.synthetic_metas(B, yaws=S.NUS_YAWS[:2], pad_shape=(128, 320, 3), seed=7) if variant == "fusion" \
         else [dict() for _ in range(B)]
+    if coop:
+        # CMTCoop (cmt_head_coop.py:205-275, 362-437): vehicle (BEV + 1 camera) and infrastructure
+        # (BEV + 2 cameras) decoders with the shared weights, max-fused before the task heads
+        xr = S.synthetic_bev(B, 16, 16, seed=15)
+        xi = S.synthetic_img(B * 1, 8, 20, seed=6)
+        xir = S.synthetic_img(B * 2, 8, 20, seed=16)
+        mv = S.synthetic_metas(B, yaws=S.VEHICLE_YAWS, prefix="vehicle_", pad_shape=(128, 320, 3), seed=7)
+        mi = S.synthetic_metas(B, yaws=S.INFRA_YAWS[:2], prefix="infrastructure_", pad_shape=(128, 320, 3), seed=17)
+        metas = [dict(a, **b) for a, b in zip(mv, mi)]
+        oracle_agents = [("vehicle_", x.double(), xi.double()), ("infrastructure_", xr.double(), xir.double())]
+        native_agents = [(x, xi, get_vehicle_image_metas(metas)), (xr, xir, get_infrastructure_image_metas(metas))]
+    else:
+        oracle_agents = [("", x.double(), None if xi is None else xi.double())]
+        native_agents = [(x, xi, metas)]
 
     # ---- oracle, float64
     params = {k: v.clone().requires_grad_() for k, v in sd_cpu.items() if not k.endswith(("running_mean", "running_var",
@@ -51,8 +67,7 @@ def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5):
     ref_p, pad, single_pad, _, md = TO.prepare_for_dn(sd64["reference_points.weight"], [b.double() for b in gtb], gtl,
                                                       Nq, head.scalar, head.bbox_noise_scale, head.bbox_noise_trans,
                                                       head.split, pcr, head.num_classes, rand_prob.double())
-    preds64 = TO.head_train_forward(oc, sd64, [("", x.double(), None if xi is None else xi.double())], metas,
-                                    variant, ref_p, pad, single_pad)
+    preds64 = TO.head_train_forward(oc, sd64, oracle_agents, metas, variant, ref_p, pad, single_pad)
     lc = head._loss_cfg()
     code_w = torch.tensor(lc["code_weights"], dtype=torch.float64)
     loss_cfg = dict(gamma=lc["gamma"], alpha=lc["alpha"], cls_weight=lc["cls_weight"], box_weight=lc["box_weight"],
@@ -65,8 +80,8 @@ def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5):
     head.to(dev).train()
     head.train_dropout = False
     head.train_cross_fp16 = fp16
-    preds = head.forward_train([(x.to(dev), None if xi is None else xi.to(dev), metas)], metas,
-                               [b.to(dev) for b in gtb], [l.to(dev) for l in gtl], rand_prob=rand_prob.to(dev))
+    preds = head.forward_train([(a.to(dev), None if ai is None else ai.to(dev), m) for a, ai, m in native_agents],
+                               metas, [b.to(dev) for b in gtb], [l.to(dev) for l in gtl], rand_prob=rand_prob.to(dev))
     losses = head.loss([b.to(dev) for b in gtb], [l.to(dev) for l in gtl], [[p] for p in preds])
     sum(losses.values()).backward()
     torch.cuda.synchronize()
@@ -89,7 +104,8 @@ def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5):
         e = (got.detach().cpu().double() - want).abs().max().item() / max(want.abs().max().item(), floor)
         if e > gerr:
             gerr, worst = e, k
-    parity_log.append(f"training step {name} ({variant}, Nq {Nq}+DN {pad}, L {L}, cross core "
+    parity_log.append(f"training step {name}{' two-agent' if coop else ''} ({variant}, Nq {Nq}+DN {pad}, L {L}, "
+                      f"cross core "
                       f"{'fp16' if fp16 else 'f32'}) vs float64 autograd: losses max rel {lerr:.1e}, "
                       f"param grads max rel {gerr:.1e} ({worst})")
     return lerr, gerr, worst
@@ -100,6 +116,81 @@ def test_training_step_grads_match_float64(dev, parity_log, name, variant):
     lerr, gerr, worst = _run(name, variant, dev, parity_log, fp16=False)
     assert lerr < 2e-4
     assert gerr < 5e-3, worst
+
+
+def test_coop_training_step_grads_match_float64(dev, parity_log):
+    """configs[3]'s workload: the two-agent CmtHeadCoop training step (forward_train,
+    loss, backward) against the float64 restatement with the reference's
+    torch.max(stack, 0) fusion, whose gradient goes to one agent per element."""
+    lerr, gerr, worst = _run("cmtcoop_fusion_tumtraf", "fusion", dev, parity_log, fp16=False, coop=True)
+    assert lerr < 2e-4
+    assert gerr < 5e-3, worst
+
+
+def test_coop_training_fullsize_steps(dev, parity_log):
+    """Full-size configs[3] training (TUMTraf shapes: two agents, BEV 180x180, 1 + 3
+    cameras of 40x100, 900 queries + DN groups from 20 GT boxes, 6 layers):
+    every gradient finite and the loss decreasing over AdamW steps on one batch."""
+    from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.models.dense_heads.cmt_head_coop import (get_infrastructure_image_metas,
+                                                                          get_vehicle_image_metas)
+    from projects.mmdet3d_plugin.trainer import Trainer
+    head, _, _ = S.build_synthetic_head("cmtcoop_fusion_tumtraf", seed=0, num_query=900, device=dev)
+    head.train()
+    head.train_dropout = False
+    mv = S.synthetic_metas(1, yaws=S.VEHICLE_YAWS, prefix="vehicle_", seed=49)
+    mi = S.synthetic_metas(1, yaws=S.INFRA_YAWS, prefix="infrastructure_", seed=50)
+    metas = [dict(mv[0], **mi[0])]
+    agents = [(S.synthetic_bev(1, 180, 180, seed=45, device=dev), S.synthetic_img(1, 40, 100, seed=47, device=dev),
+               get_vehicle_image_metas(metas)),
+              (S.synthetic_bev(1, 180, 180, seed=46, device=dev), S.synthetic_img(3, 40, 100, seed=48, device=dev),
+               get_infrastructure_image_metas(metas))]
+    gtb, gtl = S.synthetic_gt(1, list(head.pc_range), head.num_classes[0], n=20, seed=3, device=dev)
+    rp = torch.rand(900, 3, generator=torch.Generator().manual_seed(2)).to(dev) * 2 - 1
+    tr = Trainer(head, lr=2e-4)
+    vals = []
+    for _ in range(4):
+        groups = min(head.scalar, 900 // 20)
+        preds = head.forward_train(agents, metas, gtb, gtl, rand_prob=rp[:groups * 20])
+        vals.append(tr.step(head.loss(gtb, gtl, [[p] for p in preds])).item())
+        assert torch.isfinite(tr.fp.grad).all()
+    parity_log.append(f"full-size coop training (2 agents, Nq 900, L 6): loss {vals[0]:.4f} -> {vals[-1]:.4f} "
+                      f"over {len(vals)} AdamW steps")
+    assert vals[-1] < vals[0], vals
+
+
+def test_eval_after_train_step_sees_new_weights(dev):
+    """Native AdamW writes the flat parameter buffer through its pointer: the
+    eval engine's packed weights must be rebuilt (Tensor._version bump), so an
+    eval forward after a training step equals a freshly built head loaded with
+    the updated state_dict."""
+    from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.trainer import Trainer
+    head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=32, num_layers=1, grid_size=[128, 128, 40],
+                                        device=dev)
+    x = S.synthetic_bev(1, 16, 16, seed=9).to(dev)
+    head.eval()
+    with torch.no_grad():
+        before = head([x], None, [dict()])[0][0]["cls_logits"].clone()
+    head.train()
+    head.train_dropout = False
+    gtb, gtl = _gt(1, list(head.pc_range), head.num_classes[0], 4, seed=8)
+    gtb, gtl = [b.to(dev) for b in gtb], [l.to(dev) for l in gtl]
+    tr = Trainer(head, lr=1e-2)
+    preds = head.forward_train([(x, None, [dict()])], [dict()], gtb, gtl)
+    tr.step(head.loss(gtb, gtl, [[p] for p in preds]))
+    head.eval()
+    with torch.no_grad():
+        after = head([x], None, [dict()])[0][0]["cls_logits"].clone()
+    fresh, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=32, num_layers=1, grid_size=[128, 128, 40],
+                                         device=dev)
+    fresh.load_state_dict(head.state_dict())
+    fresh.eval()
+    with torch.no_grad():
+        want = fresh([x], None, [dict()])[0][0]["cls_logits"]
+    torch.cuda.synchronize()
+    assert not torch.equal(before, after)
+    assert torch.equal(after, want)
 
 
 def test_training_step_fp16_core_close(dev, parity_log):
