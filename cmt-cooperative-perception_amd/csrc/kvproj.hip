@@ -374,6 +374,139 @@ __global__ __launch_bounds__(64 * NW, 1) void kvproj_kernel(cmt_gemm_args a, int
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 form (CMT_BF16P A / W: the 'ref' policy's fp32-accurate K/V):
+// per k-step and 32-token tile three MFMAs W_hi A_hi + W_hi A_lo + W_lo A_hi.
+// The 128-token A tile is resident as its hi and lo planes (2 x 64 KB of
+// LDS).  W (hi and lo, L2-resident: 3 MB for all layers) streams into a
+// KV3_RING-deep register ring of k-steps, KV3_RING steps ahead across plane
+// boundaries -- a whole plane's hi + lo fragments (128 registers) beside the
+// accumulators and A fragments would not fit two waves per SIMD.  The bias
+// comes from scalar loads (no LDS left), and each lane stores its token's
+// 4-column pieces straight from the accumulators (8-byte stores; L2 merges
+// the two lane halves' pieces of a 64-byte head row) -- no staging buffer.
+// W_lo sits N * 256 elements after W_hi, both fragment-packed like
+// cmt_kv_proj's W.
+// ---------------------------------------------------------------------------
+constexpr int KV3_RING = 4;
+
+template <typename TC>
+__global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int parts) {
+    // A tile hi plane | lo plane, each [128 tokens][256] bf16 with 16-byte chunks XOR-swizzled by row & 15
+    __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rt = blockIdx.x / parts, part = blockIdx.x - rt * parts;
+    const int m0 = rt * KP_BM;
+    const int ncols = a.N / parts;
+    const int n_part = part * ncols;
+    const bool sel_a2 = a.A2 != nullptr && n_part < a.a2_cols;
+    const bf16_t* Ab = (const bf16_t*)(sel_a2 ? a.A2 : a.A);
+    const int64_t lda = sel_a2 ? a.lda2 : a.lda;   // bf16 elements per pair row (hi 256 | lo 256)
+#pragma unroll
+    for (int i = 0; i < 2 * KP_BM * KP_K * 2 / 16 / 512; ++i) {
+        const int piece = tid + 512 * i;
+        const int plane_lo = piece >= KP_BM * 32;                 // first half: hi plane, second: lo plane
+        const int pc = piece - plane_lo * KP_BM * 32;
+        const int r = pc >> 5;
+        const int lc = (pc & 31) ^ (r & 15);
+        const int src = min(m0 + r, a.M - 1);
+        __builtin_amdgcn_global_load_lds((kp_gaddr_t)(Ab + (int64_t)src * lda + plane_lo * KP_K + 8 * lc),
+                                         (kp_laddr_t)(lds + piece * 16), 16, 0, 0);
+    }
+    const int planes_w = ncols / 32 / 8;
+    const int plane0 = (n_part >> 5) + wave * planes_w;
+    const bf16_t* Wh = (const bf16_t*)a.W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
+    const bf16_t* Wl = Wh + (int64_t)a.N * KP_K;
+    bf16x8 rh[KV3_RING], rl[KV3_RING];
+#pragma unroll
+    for (int ks = 0; ks < KV3_RING; ++ks) {
+        rh[ks] = *(const bf16x8*)(Wh + ks * 512);
+        rl[ks] = *(const bf16x8*)(Wl + ks * 512);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_mem();
+    // head-split element offset of each tile's token row (plane 0)
+    const int rpb = a.rows_per_batch;
+    int64_t rbase[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int m = min(m0 + 32 * t + lr, a.M - 1);
+        const int bb = m / rpb;
+        rbase[t] = ((int64_t)bb * (a.N >> 5) * rpb + (m - bb * rpb)) * 32;
+    }
+    const char* lhi = lds;
+    const char* llo = lds + KP_BM * KP_K * 2;
+    const bool maxq = a.plane_max2 != nullptr && n_part < a.plane_max_cols;
+    const int pm_planes = a.plane_max_cols >> 5;
+    typedef TC t4 __attribute__((ext_vector_type(4)));
+    for (int j = 0; j < planes_w; ++j) {
+        const int plane = plane0 + j;
+        f32x16 acc[4];
+        {
+            const float* bp = a.bias + plane * 32;   // wave-uniform: scalar loads
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int c = (r & 3) + 8 * (r >> 2);
+                const float b = a.bias ? (lh ? bp[c + 4] : bp[c]) : 0.f;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[t][r] = b;
+            }
+        }
+        // the ring's next loads: the rest of this plane, then the next plane's first steps
+        const int jn = j + 1 < planes_w ? j + 1 : j;   // past the last plane: re-fetch it (cached, unused)
+#pragma unroll
+        for (int ks = 0; ks < KP_KS; ++ks) {
+            const int sw = ((2 * ks + lh) ^ (lr & 15)) << 4;
+            const int slot = ks % KV3_RING;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const bf16x8 ah = *(const bf16x8*)(lhi + (t * 32 + lr) * (KP_K * 2) + sw);
+                const bf16x8 al = *(const bf16x8*)(llo + (t * 32 + lr) * (KP_K * 2) + sw);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rh[slot], ah, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rh[slot], al, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rl[slot], ah, acc[t], 0, 0, 0);
+            }
+            const int kn = ks + KV3_RING;
+            const int64_t woff = kn < KP_KS ? (int64_t)j * (KP_KS * 512) + kn * 512
+                                            : (int64_t)jn * (KP_KS * 512) + (kn - KP_KS) * 512;
+            rh[slot] = *(const bf16x8*)(Wh + woff);
+            rl[slot] = *(const bf16x8*)(Wl + woff);
+            // each k-step's LDS fragment reads stay beside its MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        TC* C = (TC*)a.C + (int64_t)plane * rpb * 32;
+        float pm[2] = {0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int m = m0 + 32 * t + lr;
+            float ss = 0.f;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const t4 v = t4{(TC)acc[t][4 * g], (TC)acc[t][4 * g + 1], (TC)acc[t][4 * g + 2],
+                                (TC)acc[t][4 * g + 3]};
+                if (m < a.M) *(t4*)(C + rbase[t] + 8 * g + 4 * lh) = v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
+            }
+            ss = pair_sum(m < a.M ? ss : 0.f);
+            pm[t >> 1] = (t & 1) ? fmaxf(pm[t >> 1], ss) : ss;
+        }
+        if (maxq) {
+#pragma unroll
+            for (int gq = 0; gq < 2; ++gq) {
+                float x = pm[gq];
+#pragma unroll
+                for (int off = 1; off < 32; off <<= 1) x = fmaxf(x, __shfl_xor(x, off));
+                const int mg = m0 + 64 * gq;
+                if (lane == 0 && mg < a.M) a.plane_max2[(int64_t)(mg >> 6) * pm_planes + plane] = x;
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
@@ -385,6 +518,29 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
     const char* pv = getenv("CMT_KVPROJ_PARTS");
     const int pmul = (pv && pv[0] == '4' && a.A2 && (a.N / 4 / 32) % 8 == 0) ? 2 : 1;
     const int parts = (a.A2 ? 2 : 1) * pmul;
+    if (a.w_dtype == CMT_BF16P) {
+        // split-bf16 (fp32-accurate) form: pair A / A2 rows, W_hi then W_lo fragment-packed, f16 / bf16 C
+        CMT_REQUIRE(a.a_dtype == CMT_BF16P && (a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16),
+                    "cmt_kv_proj: split W needs pair A and an f16 / bf16 C");
+        CMT_REQUIRE(a.A && a.W && a.C && a.M > 0 && a.K == KP_K && a.batch == 1 && a.a_mode == CMT_A_ROWS &&
+                        a.c_mode == CMT_C_HEADSPLIT && a.R == nullptr && !a.relu && a.rows_per_batch > 0 &&
+                        a.M % a.rows_per_batch == 0,
+                    "cmt_kv_proj: row A, K = 256, head-split C, no residual / relu, batch 1");
+        const int parts3 = a.A2 ? 2 : 1;
+        CMT_REQUIRE(a.N % (256 * parts3) == 0, "cmt_kv_proj: N must be a multiple of 256 per column part");
+        CMT_REQUIRE(a.A2 == nullptr || (a.a2_mode == CMT_A2_SELECT && a.a2_cols * 2 == a.N),
+                    "cmt_kv_proj: A2 selects the first half of the columns");
+        CMT_REQUIRE(a.plane_max2 == nullptr || (a.plane_max_cols % (a.N / parts3) == 0 && a.plane_max_cols <= a.N),
+                    "cmt_kv_proj: plane_max_cols must be a multiple of the column part (N / parts) <= N");
+        CMT_REQUIRE(a.lda % 8 == 0 && (a.A2 == nullptr || a.lda2 % 8 == 0) &&
+                        ((uintptr_t)a.A | (uintptr_t)a.W | (uintptr_t)a.C | (uintptr_t)a.A2) % 16 == 0,
+                    "cmt_kv_proj: 16-byte aligned operands");
+        const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts3);
+        hipStream_t s3 = (hipStream_t)stream;
+        if (a.c_dtype == CMT_F16) kvproj_x3_kernel<f16_t><<<g3, 512, 0, s3>>>(a, parts3);
+        else kvproj_x3_kernel<bf16_t><<<g3, 512, 0, s3>>>(a, parts3);
+        return cmt_check_launch("cmt_kv_proj");
+    }
     CMT_REQUIRE(a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16, "cmt_kv_proj: w_dtype must be f16 or bf16");
     CMT_REQUIRE(a.a_dtype == a.w_dtype && a.c_dtype == a.w_dtype, "cmt_kv_proj: A and C in the compute dtype");
     CMT_REQUIRE(a.A && a.W && a.C && a.M > 0 && a.K == KP_K && a.batch == 1, "cmt_kv_proj: needs A/W/C, K = 256");

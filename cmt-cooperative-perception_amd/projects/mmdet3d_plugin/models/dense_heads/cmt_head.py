@@ -8,12 +8,14 @@ Reference: projects/mmdet3d_plugin/models/dense_heads/cmt_head.py
   CmtLidarHead 1002-1085.
 Outputs: ``forward`` returns the multi_apply layout -- a tuple over tasks of a
 list over feature levels (one) of dicts {center, height, dim, rot, vel,
-cls_logits}, each [L, B, Nq, k] fp32 (cmt_head.py:549-554).
-Training-mode forward (DN queries, losses) is not implemented natively yet.
+cls_logits}, each [L, B, Nq, k] fp32 (cmt_head.py:549-554).  In training mode
+forward_single runs forward_train (DN queries, native training kernels,
+train_engine.py) and ``loss`` the Hungarian-matched focal / L1 / DN losses.
 """
 import copy
 import math
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -21,7 +23,7 @@ from ... import native
 from ...registry import HEADS, build_bbox_coder, build_from_cfg, build_transformer
 from ...runtime import get_precision, is_split, op_empty
 from ..utils.packing import PackCache, to_dtype
-from .engine import HeadEngineMixin
+from .engine import HeadEngineMixin, _inv_lidar2img
 from .train_engine import HeadTrainMixin
 
 __all__ = ["pos2embed", "GroupLayerNorm1d", "SeparateTaskHead", "ConvModule", "CmtHead", "CmtLidarHead",
@@ -314,10 +316,14 @@ class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
         batch_y = (batch_y + 0.5) / y_size
         return torch.cat([batch_x[None], batch_y[None]], dim=0).view(2, -1).transpose(1, 0)
 
-    def _forward_agents(self, agents, img_metas, B):
+    def _forward_agents(self, agents, img_metas, B, meta_fns=None):
         """Run the decoder for each (x, x_img, metas) agent, max-fusing into one
-        [L, B*Nq, C] buffer, then the task heads."""
+        [L, B*Nq, C] buffer, then the task heads.  ``meta_fns[i]`` maps the
+        frame's img_metas to agent i's metas (identity by default); the ones of
+        the agents with cameras are kept for stage_metas."""
         self._check_eval()
+        fns = meta_fns if meta_fns is not None else [lambda m: m] * len(agents)
+        self._meta_plan = [fn for (_, x_img, _), fn in zip(agents, fns) if x_img is not None and self.variant != "lidar"]
         prec = get_precision()
         L = self.transformer.decoder.num_layers
         outs = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=torch.float32,
@@ -340,6 +346,27 @@ class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
         if self.training:
             return self.forward_train([(x, x_img, img_metas)], img_metas, *gt_from_metas(img_metas))
         return self._forward_agents([(x, x_img, img_metas)], img_metas, B)
+
+    def stage_metas(self, img_metas):
+        """Write a new frame's camera matrices (lidar2img and its fp64 host
+        inverse, cmt_head.py:428, 441-444) into the pinned staging buffers a
+        captured forward reads, so ``graph.replay()`` computes the frame with
+        THESE metas (the graph's copy nodes re-read the buffers).  Call it after
+        the previous replay has consumed its buffers (e.g. after synchronising
+        that replay's stream) and before the next one.  The agents and camera
+        counts must be those of the captured forward."""
+        plan = getattr(self, "_meta_plan", None)
+        pool = self.__dict__.get("_pinned_meta")
+        if plan is None or pool is None:
+            raise RuntimeError("stage_metas needs one eager forward (and the graph capture) first")
+        for seq, fn in enumerate(plan):
+            l2i, i2l = _inv_lidar2img(fn(img_metas))
+            t = torch.from_numpy(np.ascontiguousarray(np.stack([l2i, i2l]))).float()
+            key = ("cams", tuple(t.shape), seq)
+            if key not in pool:
+                raise RuntimeError(f"stage_metas: camera layout {tuple(t.shape)} of agent {seq} differs from the "
+                                   "captured forward's")
+            pool[key].copy_(t)
 
     def forward(self, pts_feats, img_feats=None, img_metas=None):
         """list([bs, c, h, w]) per level -> multi_apply layout (cmt_head.py:549-554)."""

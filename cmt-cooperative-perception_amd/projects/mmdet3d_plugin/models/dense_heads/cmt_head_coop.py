@@ -45,16 +45,18 @@ class CmtHeadCoop(CmtHead):
 
     def forward_single(self, x_vehicle, x_infrastructure, x_img_vehicle, x_img_infrastructure, img_metas):
         B = len(img_metas)
-        agents = []
-        if x_vehicle is not None or x_img_vehicle is not None:
-            agents.append((x_vehicle, x_img_vehicle, self._agent_metas(img_metas, "vehicle_")))
-        if x_infrastructure is not None or x_img_infrastructure is not None:
-            agents.append((x_infrastructure, x_img_infrastructure, self._agent_metas(img_metas, "infrastructure_")))
+        agents, fns = [], []
+        for x, xi, prefix in ((x_vehicle, x_img_vehicle, "vehicle_"),
+                              (x_infrastructure, x_img_infrastructure, "infrastructure_")):
+            if x is not None or xi is not None:
+                fn = (lambda m, p=prefix: self._agent_metas(m, p))
+                agents.append((x, xi, fn(img_metas)))
+                fns.append(fn)
         if not agents:
             raise ValueError("CmtHeadCoop needs at least one agent's features")
         if self.training:   # cmt_head_coop.py:205-275 training branch (DN queries, shared GT)
             return self.forward_train(agents, img_metas, *gt_from_metas(img_metas))
-        return self._forward_agents(agents, img_metas, B)
+        return self._forward_agents(agents, img_metas, B, meta_fns=fns)
 
     def _agent_metas(self, img_metas, prefix):
         if self.variant == "lidar":
@@ -79,11 +81,14 @@ class CmtHeadCoop(CmtHead):
         B = len(img_metas)
         prefixes = [p for p, _, _ in agents]
         if set(prefixes) <= {"vehicle_", "infrastructure_"}:
-            metas = [self._agent_metas(img_metas, p) for p in prefixes]
+            fns = [(lambda m, p=p: self._agent_metas(m, p)) for p in prefixes]
         else:
-            metas = [[self._select_metas(m, p, prefixes) for m in img_metas] if self.variant != "lidar" else img_metas
-                     for p in prefixes]
-        return self._forward_agents([(x, xi, m) for (_, x, xi), m in zip(agents, metas)], img_metas, B)
+            fns = [(lambda m, p=p: [self._select_metas(mm, p, prefixes) for mm in m] if self.variant != "lidar"
+                    else m) for p in prefixes]
+        triples = [(x, xi, fn(img_metas)) for (_, x, xi), fn in zip(agents, fns)]
+        if self.training:
+            return self.forward_train(triples, img_metas, *gt_from_metas(img_metas))
+        return self._forward_agents(triples, img_metas, B, meta_fns=fns)
 
     @staticmethod
     def _select_metas(meta, prefix, prefixes):

@@ -408,6 +408,5 @@ class HeadEngineMixin:
 
     def _check_eval(self):
         if self.training:
-            raise NotImplementedError(
-                "training-mode forward (DN query groups, losses, Hungarian assignment) is not implemented on the "
-                "native path yet (SURVEY.md 8(f) next #2); call .eval()")
+            raise RuntimeError("the fused inference path was reached in training mode: training goes through "
+                               "forward_train (forward / forward_single / forward_agents route there)")

@@ -195,35 +195,12 @@ class HeadTrainMixin:
 
     def _decoder_t(self, tgt, qpos, mem, pos, mask_dict):
         """PETRTransformerDecoder with the training op walk (post-norm,
-        petr_transformer.py:324-487; mmcv BaseTransformerLayer)."""
-        dec = self.transformer.decoder
-        B, Nq, C = tgt.shape
-        H = dec.layers[0].attentions[0].num_heads
-        pad = mask_dict["pad_size"] if mask_dict else 0
-        grp = mask_dict["single_pad"] if mask_dict else 0
-        memk = mem + pos
-        outs = []
-        seed0 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if self.train_dropout else 0
-        for li, lay in enumerate(dec.layers):
-            sa, ca, ffn, nm = lay.attentions[0].attn, lay.attentions[1].attn, lay.ffns[0], lay.norms
-            wq, wk, wv = sa.in_proj_weight.chunk(3)
-            bq, bk, bv = sa.in_proj_bias.chunk(3)
-            qi = tgt + qpos
-            o = ops.attention(ops.linear(qi, wq, bq), ops.linear(qi, wk, bk), ops.linear(tgt, wv, bv), H, dn_pad=pad,
-                              dn_group=grp, dropout_p=sa.dropout if self.train_dropout else 0.0, seed=seed0 + li)
-            tgt = ops.layer_norm(tgt + self._drop(ops.linear(o, sa.out_proj.weight, sa.out_proj.bias)),
-                                 nm[0].weight, nm[0].bias, nm[0].eps)
-            wq, wk, wv = ca.in_proj_weight.chunk(3)
-            bq, bk, bv = ca.in_proj_bias.chunk(3) if ca.in_proj_bias is not None else (None, None, None)
-            o = ops.attention(ops.linear(tgt + qpos, wq, bq), ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H,
-                              fp16=self.train_cross_fp16)
-            tgt = ops.layer_norm(tgt + self._drop(ops.linear(o, ca.out_proj.weight, ca.out_proj.bias)),
-                                 nm[1].weight, nm[1].bias, nm[1].eps)
-            l1, l2 = ffn.layers[0][0], ffn.layers[1]
-            h = torch.relu(ops.linear(tgt, l1.weight, l1.bias))
-            tgt = ops.layer_norm(tgt + ops.linear(h, l2.weight, l2.bias), nm[2].weight, nm[2].bias, nm[2].eps)
-            outs.append(ops.layer_norm(tgt, dec.post_norm.weight, dec.post_norm.bias, dec.post_norm.eps))
-        return torch.nan_to_num(torch.stack(outs))          # [L, B, Nq, C]
+        petr_transformer.py:324-487; mmcv BaseTransformerLayer): the decoder's
+        own train_rows, with this head's DN padding and dropout switches."""
+        return self.transformer.decoder.train_rows(
+            tgt, qpos, mem, pos, pad=mask_dict["pad_size"] if mask_dict else 0,
+            group=mask_dict["single_pad"] if mask_dict else 0, dropout=self.train_dropout,
+            cross_fp16=self.train_cross_fp16)
 
     def _task_head_t(self, task, x, reference):
         """SeparateTaskHead (cmt_head.py:136-203) + box epilogue (501-513).

@@ -38,7 +38,9 @@ class FlashAttention(nn.Module):
         if key_padding_mask is not None:
             raise NotImplementedError("key_padding_mask path is dead in CMT configs (petr_transformer.py:316)")
         if self.training and self.dropout_p > 0:
-            raise NotImplementedError("attention dropout (training) is not implemented on the native path")
+            raise NotImplementedError("FlashAttention attention_dropout > 0: CMT keeps flash-attn's default 0 "
+                                      "(attention.py:36); the training core takes dropout only for the "
+                                      "self-attention (train_ops.attention dropout_p)")
         B, T, H, D = q.shape
         S = kv.shape[1]
         if D != 32:

@@ -25,6 +25,7 @@ import warnings
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from ... import native
 from ...registry import (ATTENTION, FEEDFORWARD_NETWORK, TRANSFORMER_LAYER, TRANSFORMER_LAYER_SEQUENCE,
@@ -46,6 +47,71 @@ def _wo(lw):
 def _rows(x):
     """[N, B, C] -> contiguous fp32 [N*B, C]."""
     return x.reshape(-1, x.shape[-1]).contiguous().float()
+
+
+def _grad_mode(module):
+    """Training forward on the differentiable native ops (train_ops) instead of
+    the fused inference kernels."""
+    return module.training and torch.is_grad_enabled()
+
+
+def dn_mask_params(mask):
+    """(pad_size, single_pad) of the DN self-attention mask of prepare_for_dn
+    (cmt_head.py:386-398: True = hidden; the matching queries never see the DN
+    queries, DN group i sees only itself among the DN queries) -- the structure
+    the native kernels apply from these two numbers.  Any other mask raises."""
+    m = mask.bool()
+    if m.dim() != 2 or m.shape[0] != m.shape[1]:
+        raise NotImplementedError("only [T, T] DN self-attention masks are supported natively")
+    T = m.shape[0]
+    pad = int(m[-1].sum().item())
+    if pad == 0:
+        if bool(m.any()):
+            raise NotImplementedError("only the DN query mask of prepare_for_dn is supported natively")
+        return 0, 0
+    single = int((~m[0]).sum().item()) - (T - pad)
+    if single <= 0 or pad % single:
+        raise NotImplementedError("only the DN query mask of prepare_for_dn is supported natively")
+    idx = torch.arange(T, device=m.device)
+    q, k = idx[:, None], idx[None, :]
+    want = (k < pad) & ((q >= pad) | (k // single != q // single))
+    if not torch.equal(want, m):
+        raise NotImplementedError("only the DN query mask of prepare_for_dn is supported natively")
+    return pad, single
+
+
+def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cross_fp16=True, seed=0):
+    """One PETRTransformerDecoderLayer in training (petr_transformer.py:374-487,
+    mmcv BaseTransformerLayer post-norm walk) on the differentiable native ops:
+    rows batch-first [B, N, C]; memk = memory + key_pos.  The self-attention
+    core applies the DN mask (pad, group) and attn_drop, both attentions the
+    dropout_layer after their out-projection (mmcv's deprecated ``dropout``
+    kwarg sets both, 0.1 in every config); the cross core emulates flash-attn's
+    fp16 inputs when cross_fp16."""
+    from . import train_ops as ops
+    sa, ca, ffn, nm = lay.attentions[0], lay.attentions[1], lay.ffns[0], lay.norms
+    H = sa.num_heads
+
+    def drop(x, p):
+        return F.dropout(x, p, True) if dropout and p > 0 else x
+    w = sa.attn
+    wq, wk, wv = w.in_proj_weight.chunk(3)
+    bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
+    qi = tgt + qpos
+    o = ops.attention(ops.linear(qi, wq, bq), ops.linear(qi, wk, bk), ops.linear(tgt, wv, bv), H, dn_pad=pad,
+                      dn_group=group, dropout_p=sa.attn_drop_p if dropout else 0.0, seed=seed)
+    tgt = ops.layer_norm(tgt + drop(ops.linear(o, w.out_proj.weight, w.out_proj.bias), sa.drop_prob),
+                         nm[0].weight, nm[0].bias, nm[0].eps)
+    w = ca.attn
+    wq, wk, wv = w.in_proj_weight.chunk(3)
+    bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
+    o = ops.attention(ops.linear(tgt + qpos, wq, bq), ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H,
+                      fp16=cross_fp16)
+    tgt = ops.layer_norm(tgt + drop(ops.linear(o, w.out_proj.weight, w.out_proj.bias), ca.drop_prob),
+                         nm[1].weight, nm[1].bias, nm[1].eps)
+    l1, l2 = ffn.layers[0][0], ffn.layers[1]
+    h = torch.relu(ops.linear(tgt, l1.weight, l1.bias))
+    return ops.layer_norm(tgt + ops.linear(h, l2.weight, l2.bias), nm[2].weight, nm[2].bias, nm[2].eps)
 
 
 @FEEDFORWARD_NETWORK.register_module()
@@ -81,6 +147,15 @@ class FFN(nn.Module):
                               lambda: [to_dtype(l.weight, prec.gemm) for l in lins])
 
     def forward(self, x, identity=None):
+        if _grad_mode(self):
+            from . import train_ops as ops
+            h = x
+            lins = [m[0] for m in self.layers[:-2]] + [self.layers[-2]]
+            for i, lin in enumerate(lins):
+                h = ops.linear(h, lin.weight, lin.bias)
+                if i < len(lins) - 1:
+                    h = F.dropout(torch.relu(h), self.layers[i][2].p, True)
+            return (identity if identity is not None else x) + F.dropout(h, self.layers[-1].p, True)
         prec = get_precision()
         ws = self.packed(prec)
         shape = x.shape
@@ -104,10 +179,13 @@ class _MHABase(nn.Module):
     def _weights(self):
         raise NotImplementedError
 
+    drop_prob = 0.0     # dropout_layer after the out-projection (training)
+    attn_drop_p = 0.0   # attention-probability dropout of the core (training; nn.MultiheadAttention only)
+
     def forward(self, query, key=None, value=None, identity=None, query_pos=None, key_pos=None, attn_mask=None,
                 key_padding_mask=None, **kwargs):
-        if attn_mask is not None:
-            raise NotImplementedError("attention masks (training-time DN queries) are not implemented natively yet")
+        if attn_mask is not None or _grad_mode(self):
+            return self._forward_t(query, key, value, identity, query_pos, key_pos, attn_mask)
         if key_padding_mask is not None and bool(key_padding_mask.any()):
             raise NotImplementedError("non-trivial key_padding_mask is not used by CMT configs")
         if key is None:
@@ -139,6 +217,34 @@ class _MHABase(nn.Module):
         return out.transpose(0, 1) if self.batch_first else out
 
 
+    def _forward_t(self, query, key, value, identity, query_pos, key_pos, attn_mask):
+        """Training (or DN-masked) forward on the differentiable native ops: the
+        DN mask goes to the attention kernel as (pad, group) (dn_mask_params)."""
+        from . import train_ops as ops
+        key = query if key is None else key
+        value = key if value is None else value
+        identity = query if identity is None else identity
+        if key_pos is None and query_pos is not None and query_pos.shape == key.shape:
+            key_pos = query_pos
+        pad, grp = dn_mask_params(attn_mask) if attn_mask is not None else (0, 0)
+        bf = self.batch_first
+        t = (lambda x: x) if bf else (lambda x: None if x is None else x.transpose(0, 1))
+        q, k, v, idn, qp, kp = (t(x) for x in (query, key, value, identity, query_pos, key_pos))
+        qi = q + qp if qp is not None else q
+        ki = k + kp if kp is not None else k
+        w = self.attn
+        wq, wk, wv = w.in_proj_weight.chunk(3)
+        bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
+        training = self.training
+        o = ops.attention(ops.linear(qi, wq, bq), ops.linear(ki, wk, bk), ops.linear(v, wv, bv), self.num_heads,
+                          dn_pad=pad, dn_group=grp, fp16=self.fp16_core,
+                          dropout_p=self.attn_drop_p if training else 0.0,
+                          seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training and self.attn_drop_p else 0)
+        y = ops.linear(o, w.out_proj.weight, w.out_proj.bias)
+        out = idn + (F.dropout(y, self.drop_prob, True) if training and self.drop_prob > 0 else y)
+        return out if bf else out.transpose(0, 1)
+
+
 @ATTENTION.register_module()
 class MultiheadAttention(_MHABase):
     """mmcv 1.6.2 MultiheadAttention wrapper around ``nn.MultiheadAttention``
@@ -150,8 +256,12 @@ class MultiheadAttention(_MHABase):
     def __init__(self, embed_dims, num_heads, attn_drop=0.0, proj_drop=0.0,
                  dropout_layer=dict(type="Dropout", drop_prob=0.0), init_cfg=None, batch_first=False, **kwargs):
         super().__init__()
-        if "dropout" in kwargs:
+        if "dropout" in kwargs:   # mmcv 1.6.2: the deprecated kwarg sets attn_drop AND dropout_layer's drop_prob
             attn_drop = kwargs.pop("dropout")
+            self.drop_prob = float(attn_drop)
+        else:
+            self.drop_prob = float((dropout_layer or {}).get("drop_prob", 0.0))
+        self.attn_drop_p = float(attn_drop)
         self.embed_dims = embed_dims
         self.num_heads = num_heads
         self.batch_first = batch_first
@@ -177,9 +287,12 @@ class PETRMultiheadFlashAttention(_MHABase):
     def __init__(self, embed_dims, num_heads, attn_drop=0.0, proj_drop=0.0,
                  dropout_layer=dict(type="Dropout", drop_prob=0.0), init_cfg=None, batch_first=True, **kwargs):
         super().__init__()
-        if "dropout" in kwargs:
+        if "dropout" in kwargs:   # petr_transformer.py:211-218: attn_drop (FlashMHA's `bias`) and dropout_layer
             attn_drop = kwargs["dropout"]
-            kwargs.pop("dropout")
+            self.drop_prob = float(kwargs.pop("dropout"))
+        else:
+            self.drop_prob = float((dropout_layer or {}).get("drop_prob", 0.0))
+        self.attn_drop_p = 0.0   # FlashAttention's attention_dropout keeps its default 0 (attention.py:36)
         self.embed_dims = embed_dims
         self.num_heads = num_heads
         self.batch_first = False   # forward() receives sequence-first tensors (mmcv layer convention)
@@ -239,6 +352,9 @@ class PETRTransformerDecoderLayer(nn.Module):
 
     def _norm(self, i, x):
         n = self.norms[i]
+        if _grad_mode(self):
+            from . import train_ops as ops
+            return ops.layer_norm(x, n.weight, n.bias, n.eps)
         rows = _rows(x)
         y = torch.empty_like(rows)
         native.layernorm(rows, n.weight, n.bias, y, rows=rows.shape[0], C=rows.shape[1], ldx=rows.shape[1],
@@ -247,9 +363,10 @@ class PETRTransformerDecoderLayer(nn.Module):
 
     def forward(self, query, key=None, value=None, query_pos=None, key_pos=None, attn_masks=None,
                 query_key_padding_mask=None, key_padding_mask=None, **kwargs):
-        """mmcv BaseTransformerLayer.forward op walk (post-norm)."""
-        if self.training and self.use_checkpoint:
-            raise NotImplementedError("training (with_cp) is not implemented on the native path yet")
+        """mmcv BaseTransformerLayer.forward op walk (post-norm).  In training
+        every op runs on the differentiable native ops (with_cp, the
+        reference's gradient checkpointing, only trades memory for recompute:
+        the step's values and gradients are the same without it)."""
         num_attn = 2
         if attn_masks is None or isinstance(attn_masks, torch.Tensor):
             attn_masks = [attn_masks for _ in range(num_attn)]
@@ -300,9 +417,11 @@ class PETRTransformerDecoder(nn.Module):
                 query_key_padding_mask=None, key_padding_mask=None, reg_branch=None, **kwargs):
         """Sequence-first API (query [Nq,B,C], key [Nk,B,C]) ->
         [L, Nq, B, C] (return_intermediate) or [1, Nq, B, C]."""
-        if attn_masks is not None and any(m is not None for m in (attn_masks if isinstance(attn_masks, list)
-                                                                 else [attn_masks])):
-            raise NotImplementedError("attention masks (training-time DN queries) are not implemented natively yet")
+        masked = attn_masks is not None and any(m is not None for m in (attn_masks if isinstance(attn_masks, list)
+                                                                       else [attn_masks]))
+        if masked or _grad_mode(self):
+            # training-time DN queries / gradients: the layer walk on the differentiable native ops
+            return self._forward_layers(query, key, value, query_pos, key_pos, attn_masks)
         if value is not None and value is not key and not torch.equal(value, key):
             # the fused path assumes value == key (true for every CMT transformer)
             return self._forward_layers(query, key, value, query_pos, key_pos)
@@ -318,17 +437,36 @@ class PETRTransformerDecoder(nn.Module):
         out = out.view(self.num_layers, B, Nq, C).transpose(1, 2)
         return out if self.return_intermediate else out[-1:]
 
-    def _forward_layers(self, query, key, value, query_pos, key_pos):
+    def _forward_layers(self, query, key, value, query_pos, key_pos, attn_masks=None):
         inter = []
         for layer in self.layers:
-            query = layer(query, key, value, query_pos=query_pos, key_pos=key_pos)
+            query = layer(query, key, value, query_pos=query_pos, key_pos=key_pos, attn_masks=attn_masks)
             if self.return_intermediate:
                 inter.append(self._post(query) if self.post_norm is not None else query)
         if not self.return_intermediate:
             return (self._post(query) if self.post_norm is not None else query)[None]
         return torch.stack(inter)
 
+    def train_rows(self, tgt, qpos, mem, pos, *, pad=0, group=0, dropout=True, cross_fp16=True):
+        """The decoder in training on batch-first rows (tgt / qpos [B, Nq, C],
+        mem / pos [B, Nk, C]): every layer (train_layer) and its post_norm
+        (petr_transformer.py:347-371), nan_to_num (cmt_head.py:499) ->
+        [L, B, Nq, C], differentiable in every input and parameter."""
+        from . import train_ops as ops
+        memk = mem + pos
+        outs = []
+        seed0 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
+        for li, lay in enumerate(self.layers):
+            tgt = train_layer(lay, tgt, qpos, memk, mem, pad=pad, group=group, dropout=dropout,
+                              cross_fp16=cross_fp16, seed=seed0 + li)
+            outs.append(ops.layer_norm(tgt, self.post_norm.weight, self.post_norm.bias, self.post_norm.eps))
+        return torch.nan_to_num(torch.stack(outs))
+
     def _post(self, x):
+        if _grad_mode(self):
+            from . import train_ops as ops
+            n = self.post_norm
+            return ops.layer_norm(x, n.weight, n.bias, n.eps)
         rows = _rows(x)
         y = torch.empty_like(rows)
         n = self.post_norm
@@ -387,26 +525,26 @@ class PETRTransformerDecoder(nn.Module):
                 sa = lay.attentions[0].attn
                 ca = lay.attentions[1].attn
                 ffn = lay.ffns[0]
+                chain = g in (torch.float16, torch.bfloat16)   # the row-block chains' fragment-major copies
                 layers.append(dict(
                     sa_w=to_dtype(sa.in_proj_weight, g), sa_b=sa.in_proj_bias.detach().contiguous(),
                     # chain B2's copy of the in_proj weights, fragment-major (cmt_hip.h cmt_chain_args.Wn)
                     sa_wp=(native.pack_chain_wn(to_dtype(sa.in_proj_weight, g))
-                           if g != torch.float32 and tuple(sa.in_proj_weight.shape) == (768, 256) else None),
+                           if chain and tuple(sa.in_proj_weight.shape) == (768, 256) else None),
                     sa_ow=to_dtype(sa.out_proj.weight, g), sa_ob=sa.out_proj.bias.detach().contiguous(),
                     # chain A's copy of the self-attn out_proj weights, fragment-major (cmt_hip.h wo_frag)
                     sa_owp=(native.pack_chain_wn(to_dtype(sa.out_proj.weight, g))
-                            if g != torch.float32 and C == 256 and os.environ.get("CMT_CHAIN_A_WOREGS", "1") != "0"
-                            else None),
+                            if chain and C == 256 else None),
                     ca_wq=to_dtype(ca.in_proj_weight[:C], g),
                     ca_wqp=(native.pack_chain_wn(to_dtype(ca.in_proj_weight[:C], g))
-                            if g != torch.float32 and C == 256 else None),
+                            if chain and C == 256 else None),
                     ca_bq=ca.in_proj_bias[:C].detach().contiguous() if ca.in_proj_bias is not None else None,
                     ca_ow=to_dtype(ca.out_proj.weight, g),
                     ca_ob=ca.out_proj.bias.detach().contiguous() if ca.out_proj.bias is not None else None,
                     f1_w=to_dtype(ffn.layers[0][0].weight, g), f1_b=ffn.layers[0][0].bias.detach().contiguous(),
                     f2_w=to_dtype(ffn.layers[1].weight, g), f2_b=ffn.layers[1].bias.detach().contiguous(),
                     f2_wp=(native.pack_chain_fc2(to_dtype(ffn.layers[1].weight, g))
-                           if g != torch.float32 and tuple(ffn.layers[1].weight.shape) == (256, 1024) else None),
+                           if chain and tuple(ffn.layers[1].weight.shape) == (256, 1024) else None),
                     norms=[(n.weight.detach().contiguous(), n.bias.detach().contiguous(), n.eps)
                            for n in lay.norms]))
                 kw.append(ca.in_proj_weight[C:2 * C])
@@ -416,7 +554,14 @@ class PETRTransformerDecoder(nn.Module):
                     vb.append(ca.in_proj_bias[2 * C:])
             kv_w = to_dtype(torch.cat(kw + vw, 0), g)
             kv_b = torch.cat(kb + vb, 0).detach().contiguous() if kb else None
-            kv_wp = native.kv_pack(kv_w) if (C == 256 and kv_w.dtype in (torch.float16, torch.bfloat16)) else None
+            kv_wp = None
+            if C == 256 and kv_w.dtype in (torch.float16, torch.bfloat16):
+                kv_wp = native.kv_pack(kv_w)
+            elif C == 256 and kv_w.dtype == SPLIT:
+                # split pairs: the fragment-packed hi halves, then the lo halves (cmt_kv_proj's split form)
+                b = kv_w.view(torch.bfloat16)
+                kv_wp = torch.cat([native.kv_pack(b[:, 0].contiguous()),
+                                   native.kv_pack(b[:, 1].contiguous())]).view(SPLIT)
             return dict(layers=layers, kv_w=kv_w, kv_wp=kv_wp, kv_b=kv_b,
                         post=(self.post_norm.weight.detach().contiguous(),
                               self.post_norm.bias.detach().contiguous(), self.post_norm.eps))

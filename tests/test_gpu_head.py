@@ -228,6 +228,65 @@ def test_fusion_head_graph_replay_matches_eager(dev):
     set_precision("ref")
 
 
+@pytest.mark.parametrize("prec,coop", [("bf16", False), ("ref", False), ("ref", True)])
+def test_graph_replay_with_new_metas(dev, prec, coop):
+    """Capture a forward with the cameras of frame A, stage frame B's cameras
+    into the pinned buffers (head.stage_metas: lidar2img and its fp64 host
+    inverse, cmt_head.py:428, 441-444), replay: bit-identical to the eager
+    forward on frame B -- and different from A's (the cameras are not frozen
+    into the graph)."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    name = "cmtcoop_fusion_tumtraf" if coop else "cmt_fusion_nus"
+    head, cfg, _ = S.build_synthetic_head(name, seed=0, num_query=64, num_layers=2, grid_size=[256, 256, 40],
+                                          device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=21).to(dev)
+    if coop:
+        xr = S.synthetic_bev(1, 32, 32, seed=24).to(dev)
+        iv, ir = S.synthetic_img(1, 8, 20, seed=22).to(dev), S.synthetic_img(3, 8, 20, seed=25).to(dev)
+
+        def metas_of(seed):
+            mv = S.synthetic_metas(1, yaws=S.VEHICLE_YAWS, prefix="vehicle_", pad_shape=(128, 320, 3), seed=seed)
+            mi = S.synthetic_metas(1, yaws=S.INFRA_YAWS, prefix="infrastructure_", pad_shape=(128, 320, 3),
+                                   seed=seed + 1)
+            return [dict(mv[0], **mi[0])]
+        fwd = lambda m: head([x], [xr], [iv], [ir], m)   # noqa: E731
+    else:
+        xi = S.synthetic_img(6, 8, 20, seed=22).to(dev)
+
+        def metas_of(seed):
+            return S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=seed)
+        fwd = lambda m: head([x], [xi], m)   # noqa: E731
+    ma, mb = metas_of(23), metas_of(40)
+    set_precision(prec)
+    try:
+        with torch.no_grad():
+            eager_b = fwd(mb)
+            eager_a = fwd(ma)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fwd(ma)
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g):
+                    static = fwd(ma)
+            torch.cuda.current_stream().wait_stream(s)
+            g.replay()
+            torch.cuda.synchronize()
+            rep_a = {k: static[0][0][k].clone() for k in KEYS}
+            head.stage_metas(mb)
+            g.replay()
+            torch.cuda.synchronize()
+    finally:
+        set_precision("ref")
+    for k in KEYS:
+        assert torch.equal(rep_a[k], eager_a[0][0][k]), k
+        assert torch.equal(static[0][0][k], eager_b[0][0][k]), (k, (static[0][0][k] - eager_b[0][0][k]).abs().max())
+    assert not torch.equal(eager_a[0][0]["cls_logits"], eager_b[0][0]["cls_logits"])
+
+
 @pytest.mark.parametrize("warm", ["ref", "none"])
 def test_second_stream_matches_single_stream(dev, warm, monkeypatch):
     """The two-stream schedule (query side + layer 0 self block and the encoder

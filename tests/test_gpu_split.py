@@ -274,3 +274,32 @@ def test_attention_pair_output(N, dev):
                     round_output=True)
     assert _same(Op, _pair(O32.cpu().view(B * Nq, H * 32)))
     assert torch.equal(_unpair(Op.cpu()), O32.cpu().double().view(B * Nq, H * 32))
+
+
+@pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100)])
+def test_kvproj_split(N, dev, B, S):
+    """cmt_kv_proj's split-bf16 form (K columns from lowp(mem + pos), V columns
+    from lowp(mem); all layers in one launch) against float64, with the key-norm
+    partials of the K planes; ragged last row tile."""
+    g = torch.Generator().manual_seed(B * S)
+    C, L = 256, 2
+    M, N_ = B * S, 2 * L * C
+    A = torch.randn(M, C, generator=g)
+    A2 = torch.randn(M, C, generator=g)
+    W = torch.randn(N_, C, generator=g) / 16
+    b = torch.randn(N_, generator=g)
+    ref = torch.cat([A2.double() @ W[:N_ // 2].double().t(), A.double() @ W[N_ // 2:].double().t()], 1) + b.double()
+    Wp = _pair(W)
+    wb = Wp.view(torch.bfloat16)
+    packed = torch.cat([N.kv_pack(wb[:, 0].contiguous()), N.kv_pack(wb[:, 1].contiguous())]).view(SPLIT).to(dev)
+    out = torch.empty(B * N_ * S, dtype=torch.float16, device=dev)
+    pm = torch.empty(-(-M // 64) * (N_ // 2 // 32), device=dev)
+    N.kv_proj(_pair(A).to(dev), packed, out, M=M, N=N_, bias=b.to(dev), A2=_pair(A2).to(dev), headsplit_rows=S,
+              plane_max2=pm, plane_max_cols=N_ // 2)
+    got = out.cpu().double().view(B, N_ // 32, S, 32).permute(0, 2, 1, 3).reshape(M, N_)
+    # one f16 rounding of the fp32-accurate product
+    assert ((got - ref).abs() <= 2 ** -11 * ref.abs() + 1e-4).all(), (got - ref).abs().max().item()
+    ss = (got[:, :N_ // 2].view(M, N_ // 64, 32) ** 2).sum(-1)
+    nb = -(-M // 64)
+    pref = torch.cat([ss, torch.zeros(nb * 64 - M, ss.shape[1], dtype=ss.dtype)], 0).view(nb, 64, -1).amax(1)
+    assert torch.allclose(pm.cpu().double().view(nb, -1), pref, rtol=1e-5, atol=1e-6)

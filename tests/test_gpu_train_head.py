@@ -217,3 +217,54 @@ def test_trainer_step_reduces_loss(dev):
         preds = head.forward_train([(x, None, [dict()])], [dict()], gtb, gtl, rand_prob=rp)
         vals.append(tr.step(head.loss(gtb, gtl, [[p] for p in preds])).item())
     assert vals[-1] < vals[0], vals
+
+
+def test_transformer_forward_with_dn_mask_training(dev, parity_log):
+    """Transformer-level drop-in for training: CmtLidarTransformer.forward(...,
+    attn_masks=[dn_mask, None]) in training mode (cmt_transformer.py:166-204,
+    the DN mask of prepare_for_dn, cmt_head.py:386-398) runs the decoder on the
+    native differentiable ops; outputs and the gradients of every decoder
+    parameter match the float64 restatement (dropout off, f32 cross core).
+    A mask that is not a DN mask raises."""
+    from oracle import cmt_train_oracle as TO
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=32, num_layers=2, grid_size=[128, 128, 40])
+    tr = head.transformer
+    for m in tr.modules():
+        if hasattr(m, "drop_prob"):
+            m.drop_prob, m.attn_drop_p = 0.0, 0.0
+    tr.train_cross_fp16 = False
+    sd64 = {k[len("transformer."):]: v.detach().double().clone().requires_grad_()
+            for k, v in head.state_dict().items() if k.startswith("transformer.decoder")}
+    g = torch.Generator().manual_seed(11)
+    B, C, Nq, single, groups = 1, 256, 32, 4, 3
+    pad = single * groups
+    x = torch.relu(torch.randn(B, C, 16, 16, generator=g))
+    qe = torch.randn(B, pad + Nq, C, generator=g)
+    pe = torch.randn(256, C, generator=g)
+    mask = TO.dn_attn_mask(pad, single, groups, Nq)
+    cot = torch.randn(2, B, pad + Nq, C, generator=g)
+    # float64 restatement (sequence-first)
+    mem = x.double().flatten(2).permute(2, 0, 1)
+    ref = TO._decoder_train(torch.zeros(pad + Nq, B, C, dtype=torch.float64), mem,
+                            qe.double().transpose(0, 1), pe.double().unsqueeze(1).repeat(1, B, 1), sd64,
+                            "decoder", 2, 8, mask)                          # [L, Nq, B, C]
+    ref = torch.nan_to_num(ref).transpose(1, 2)
+    (ref * cot.double()).sum().backward()
+    tr.to(dev).train()
+    out, _ = tr(x.to(dev), torch.zeros(B, 16, 16, device=dev), qe.to(dev), pe.to(dev),
+                attn_masks=[mask.to(dev), None])
+    (out * cot.to(dev)).sum().backward()
+    torch.cuda.synchronize()
+    oerr = (out.detach().cpu().double() - ref.detach()).abs().max().item()
+    named = dict(tr.named_parameters())
+    floor = 1e-3 * max(p.grad.abs().max().item() for p in sd64.values() if p.grad is not None)
+    gerr = max((named[k].grad.cpu().double() - p.grad).abs().max().item() / max(p.grad.abs().max().item(), floor)
+               for k, p in sd64.items() if p.grad is not None)
+    parity_log.append(f"CmtLidarTransformer training forward with the DN mask (pad {pad}, 2 layers) vs float64: "
+                      f"outputs max abs {oerr:.1e}, decoder param grads max rel {gerr:.1e}")
+    assert oerr < 1e-4 and gerr < 5e-3
+    bad = mask.clone()
+    bad[0, -1] = True
+    with pytest.raises(NotImplementedError):
+        tr(x.to(dev), None, qe.to(dev), pe.to(dev), attn_masks=[bad.to(dev), None])
