@@ -8,7 +8,7 @@ camera+LiDAR nuScenes-shape synthetic frame -- BEV [1, 512, 180, 180] plus
 56 400 memory tokens), 900 queries, 6-layer decoder, the whole CmtHead forward
 per step: shared_conv, BEV / RV / query coordinate encodings, decoder, task
 heads, box epilogue, at the reference's numerics ('ref' policy: every fp32
-GEMM of the reference as a three-pass split-bf16 MFMA product, ~2^-16 relative
+GEMM of the reference as a three-pass split-f16 MFMA product, ~2^-21 relative
 per product; fp32 self-attention; fp16 flash cross-attention core with fp16 P
 and output, flash-attn 0.2.2).
 The ~30k-point voxel scatter-mean is timed separately.
@@ -51,7 +51,7 @@ from projects.mmdet3d_plugin.profiling import region_timer  # noqa: E402
 
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}   # dense MFMA, MI355X_MICROARCH.md (no sparsity)
 DTYPE_LABEL = {"bf16": "bf16", "fp16": "fp16",
-               "ref": "fp32 (GEMMs as 3-pass split-bf16 MFMA) + fp16 flash attention core: reference numerics",
+               "ref": "fp32 (GEMMs as 3-pass split-f16 MFMA) + fp16 flash attention core: reference numerics",
                "exact": "fp32 (exact-f32 MFMA GEMMs) + fp16 flash attention core: reference numerics"}
 C, NQ, NK, L, H = 256, 900, 32400, 6, 8
 METRIC = "decoder frames/sec at 900 queries x (BEV+6-cam) tokens; 1/2/4/8 MI355X"

@@ -62,11 +62,11 @@ struct AttnKParams {
 };
 
 // Final normalised output: 4 consecutive head dims of one query row.  A
-// CMT_BF16P row holds the H*32 hi values, then the H*32 lo values.
+// CMT_F16P row holds the H*32 hi values, then the H*32 lo values.
 __device__ __forceinline__ void store_o4(const AttnKParams& p, int b, int q, int d0, f32x4 v) {
     const int64_t idx = (int64_t)b * p.o_bs + (int64_t)q * p.o_rs + d0;
-    if (p.o_dtype == CMT_BF16P) {
-        store_pair4((bf16_t*)p.O + idx - d0, p.H * D, d0, v);
+    if (p.o_dtype == CMT_F16P) {
+        store_pair4((pair_t*)p.O + idx - d0, p.H * D, d0, v);
     } else if (p.o_dtype == CMT_F32) {
         *(f32x4*)((float*)p.O + idx) = v;
     } else if (p.o_dtype == CMT_F16) {
@@ -1349,7 +1349,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     CMT_REQUIRE(a.dtype != CMT_F32 || ((a.q_rstride | a.k_rstride | a.v_rstride) % 4 == 0),
                 "cmt_attn_fwd: f32 rows must be 16-byte aligned");
     CMT_REQUIRE(a.o_rstride % 4 == 0 && a.o_bstride % 4 == 0, "cmt_attn_fwd: O strides must be multiples of 4");
-    CMT_REQUIRE(a.o_dtype == CMT_F32 || a.o_dtype == CMT_F16 || a.o_dtype == CMT_BF16 || a.o_dtype == CMT_BF16P,
+    CMT_REQUIRE(a.o_dtype == CMT_F32 || a.o_dtype == CMT_F16 || a.o_dtype == CMT_BF16 || a.o_dtype == CMT_F16P,
                 "cmt_attn_fwd: bad o_dtype");
     CMT_REQUIRE(a.q_rstride % 8 == 0 && a.k_rstride % 8 == 0 && a.v_rstride % 8 == 0 && a.q_hstride % 8 == 0 &&
                 a.k_hstride % 8 == 0 && a.v_hstride % 8 == 0 && a.q_bstride % 8 == 0 && a.k_bstride % 8 == 0 &&

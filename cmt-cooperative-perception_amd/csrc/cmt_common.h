@@ -88,40 +88,42 @@ __device__ __forceinline__ float nan_to_num(float x) {
     return x;
 }
 
-// CMT_BF16P split of one fp32 value (cmt_hip.h): x = hi + lo, both bf16 (RNE).
-__device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
-    hi = (bf16_t)x;
-    lo = (bf16_t)(x - (float)hi);
+// CMT_F16P split of one fp32 value (cmt_hip.h): x = hi + lo, both f16 (RNE).
+typedef f16_t pair_t;
+typedef f16x8 pair8_t;
+__device__ __forceinline__ void split_pair(float x, pair_t& hi, pair_t& lo) {
+    hi = (pair_t)x;
+    lo = (pair_t)(x - (float)hi);
 }
-// Store v as element c of a CMT_BF16P row (hi at row[c], lo at row[C + c]).
-__device__ __forceinline__ void store_pair(bf16_t* row, int C, int c, float v) {
-    bf16_t h, l;
-    split_bf16(v, h, l);
+// Store v as element c of a CMT_F16P row (hi at row[c], lo at row[C + c]).
+__device__ __forceinline__ void store_pair(pair_t* row, int C, int c, float v) {
+    pair_t h, l;
+    split_pair(v, h, l);
     row[c] = h;
     row[C + c] = l;
 }
-// 4 consecutive elements c..c+3 of a CMT_BF16P row (8-byte stores).
-__device__ __forceinline__ void store_pair4(bf16_t* row, int C, int c, f32x4 v) {
-    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-    b4 h, l;
+// 4 consecutive elements c..c+3 of a CMT_F16P row (8-byte stores).
+__device__ __forceinline__ void store_pair4(pair_t* row, int C, int c, f32x4 v) {
+    typedef pair_t p4 __attribute__((ext_vector_type(4)));
+    p4 h, l;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        h[j] = (bf16_t)v[j];
-        l[j] = (bf16_t)(v[j] - (float)h[j]);
+        h[j] = (pair_t)v[j];
+        l[j] = (pair_t)(v[j] - (float)h[j]);
     }
-    *(b4*)(row + c) = h;
-    *(b4*)(row + C + c) = l;
+    *(p4*)(row + c) = h;
+    *(p4*)(row + C + c) = l;
 }
 // 8 consecutive elements c..c+7 (16-byte stores).
-__device__ __forceinline__ void store_pair8(bf16_t* row, int C, int c, const float* v) {
-    bf16x8 h, l;
+__device__ __forceinline__ void store_pair8(pair_t* row, int C, int c, const float* v) {
+    pair8_t h, l;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        h[j] = (bf16_t)v[j];
-        l[j] = (bf16_t)(v[j] - (float)h[j]);
+        h[j] = (pair_t)v[j];
+        l[j] = (pair_t)(v[j] - (float)h[j]);
     }
-    *(bf16x8*)(row + c) = h;
-    *(bf16x8*)(row + C + c) = l;
+    *(pair8_t*)(row + c) = h;
+    *(pair8_t*)(row + C + c) = l;
 }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -70,9 +70,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
         if (a.flags & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
         if (a.flags & CMT_LN_MAX_INTO) o = fmaxf(o, yold[i]);
         if (a.Y) a.Y[(int64_t)row * a.ldy + c] = o;
-        if constexpr (PAIR) {   // CMT_BF16P rows [hi(C) | lo(C)]
-            if (a.Yl) store_pair((bf16_t*)a.Yl + (int64_t)row * a.ldyl, C, c, o);
-            if (a.Yp) store_pair((bf16_t*)a.Yp + (int64_t)row * a.ldyp, C, c, o + pv[i]);
+        if constexpr (PAIR) {   // CMT_F16P rows [hi(C) | lo(C)]
+            if (a.Yl) store_pair((pair_t*)a.Yl + (int64_t)row * a.ldyl, C, c, o);
+            if (a.Yp) store_pair((pair_t*)a.Yp + (int64_t)row * a.ldyp, C, c, o + pv[i]);
         } else {
             if (a.Yl) ((LT*)a.Yl)[(int64_t)row * a.ldyl + c] = (LT)o;
             if (a.Yp) ((LT*)a.Yp)[(int64_t)row * a.ldyp + c] = (LT)(o + pv[i]);
@@ -98,9 +98,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
     }
 }
 
-// CMT_BF16P form: one thread per 4 values of a row of width C (rows [hi(C) | lo(C)])
+// CMT_F16P form: one thread per 4 values of a row of width C (rows [hi(C) | lo(C)])
 __global__ __launch_bounds__(256) void add_cast_pair_kernel(const float* __restrict__ X, const float* __restrict__ P,
-                                                            int64_t n4, int C, bf16_t* Yl, bf16_t* Yp) {
+                                                            int64_t n4, int C, pair_t* Yl, pair_t* Yp) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const int64_t row = i / (C / 4);
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void pos2embed_kernel(const float* __restrict_
     }
     OT* dst = out + (int64_t)i * ldo + f0;
     if constexpr (PAIR) {
-        store_pair8((bf16_t*)out + (int64_t)i * ldo, 2 * F, f0, o);
+        store_pair8((pair_t*)out + (int64_t)i * ldo, 2 * F, f0, o);
     } else if constexpr (sizeof(OT) == 4) {
         *(f32x4*)dst = f32x4{o[0], o[1], o[2], o[3]};
         *(f32x4*)(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
@@ -232,7 +232,7 @@ __global__ void rv_pe_coords_kernel8(int BV, int H, int W, int D, float pad_h, f
     }
     OT* o = out + (int64_t)tok * (3 * D) + 3 * k0;   // 24 consecutive outputs
     if constexpr (PAIR) {
-        bf16_t* prow = (bf16_t*)out + (int64_t)tok * (6 * D);   // [hi(3D) | lo(3D)]
+        pair_t* prow = (pair_t*)out + (int64_t)tok * (6 * D);   // [hi(3D) | lo(3D)]
 #pragma unroll
         for (int q = 0; q < 3; ++q) store_pair8(prow, 3 * D, 3 * k0 + 8 * q, res + 8 * q);
     } else if constexpr (sizeof(OT) == 2) {
@@ -325,7 +325,7 @@ __global__ void rv_query_coords_kernel(const float* __restrict__ ref, int B, int
         a = fmaf(M[rr * 4 + 2], c4[2], a);
         a = fmaf(M[rr * 4 + 3], c4[3], a);
         const float v = (a - pc.v[rr]) / (pc.v[3 + rr] - pc.v[rr]);
-        if constexpr (PAIR) store_pair((bf16_t*)out + bvq * (6 * D), 3 * D, 3 * k + rr, v);   // [hi(3D) | lo(3D)]
+        if constexpr (PAIR) store_pair((pair_t*)out + bvq * (6 * D), 3 * D, 3 * k + rr, v);   // [hi(3D) | lo(3D)]
         else o[rr] = (TO)v;   // RNE, as cmt_cast
     }
 }
@@ -367,8 +367,8 @@ __global__ void masked_view_sum_ex_kernel(const float* __restrict__ X, const flo
     const float y = (base ? base[(int64_t)q * C + c] : Y[idx]) + s;
     Y[idx] = y;
     if constexpr (PAIR) {   // rows [hi(C) | lo(C)]
-        if (Yp) store_pair((bf16_t*)Yp + bq * 2 * C, C, c, y);
-        if (Yl) store_pair((bf16_t*)Yl + bq * 2 * C, C, c, 0.f);
+        if (Yp) store_pair((pair_t*)Yp + bq * 2 * C, C, c, y);
+        if (Yl) store_pair((pair_t*)Yl + bq * 2 * C, C, c, 0.f);
     } else {
         if (Yp) Yp[idx] = (TL)y;
         if (Yl) Yl[idx] = (TL)0.f;
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restri
         const int p = p0 + i, c = c0 + tx;
         if (p < HW && c < C) {
             const int64_t row = (int64_t)bo * rows_per_batch + row_offset + (int64_t)v * HW + p;
-            if constexpr (PAIR) store_pair((bf16_t*)Y + row * ldy, C, c, tile[tx][i]);
+            if constexpr (PAIR) store_pair((pair_t*)Y + row * ldy, C, c, tile[tx][i]);
             else Y[row * ldy + c] = (TO)tile[tx][i];
         }
     }
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __re
         const int64_t row = (int64_t)bo * rows_per_batch + row_offset + (int64_t)v * HW + p;
         TO* dst = Y + row * ldy + c0 + cg;
         if constexpr (PAIR) {
-            store_pair8((bf16_t*)Y + row * ldy, C, c0 + cg, o);   // rows [hi(C) | lo(C)]
+            store_pair8((pair_t*)Y + row * ldy, C, c0 + cg, o);   // rows [hi(C) | lo(C)]
         } else if constexpr (VW == 4) {
             *(f32x4*)dst = f32x4{o[0], o[1], o[2], o[3]};
         } else {
@@ -459,9 +459,9 @@ __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __re
     }
 }
 
-// fp32 rows (leading dimension ldx) -> CMT_BF16P rows [hi(C) | lo(C)], 4 values per thread
+// fp32 rows (leading dimension ldx) -> CMT_F16P rows [hi(C) | lo(C)], 4 values per thread
 __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ X, int64_t ldx, int64_t n4, int C,
-                                                         bf16_t* Y) {
+                                                         pair_t* Y) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const int64_t row = i / (C / 4);
@@ -624,14 +624,14 @@ extern "C" int cmt_layernorm_ex(const cmt_ln_args* ap, void* stream) {
     CMT_REQUIRE(a.Y2 == nullptr || (a.W2 && a.B2), "cmt_layernorm: second LN needs W2/B2");
     CMT_REQUIRE(a.Yp == nullptr || a.P != nullptr, "cmt_layernorm: Yp needs P");
     CMT_REQUIRE((a.Yl == nullptr && a.Yp == nullptr) || a.lowp_dtype == CMT_F16 || a.lowp_dtype == CMT_BF16 ||
-                    a.lowp_dtype == CMT_BF16P, "cmt_layernorm: lowp_dtype must be f16, bf16 or bf16 pair");
+                    a.lowp_dtype == CMT_F16P, "cmt_layernorm: lowp_dtype must be f16, bf16 or f16 pair");
     if (a.rows == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     dim3 grid(cdiv(a.rows, 4));
 #define LN_CASE(V)                                                                              \
     case V:                                                                                     \
         if (a.lowp_dtype == CMT_F16) layernorm_kernel<V, f16_t><<<grid, 256, 0, s>>>(a);        \
-        else if (a.lowp_dtype == CMT_BF16P) layernorm_kernel<V, bf16_t, true><<<grid, 256, 0, s>>>(a); \
+        else if (a.lowp_dtype == CMT_F16P) layernorm_kernel<V, pair_t, true><<<grid, 256, 0, s>>>(a); \
         else layernorm_kernel<V, bf16_t><<<grid, 256, 0, s>>>(a);                               \
         break;
     switch (a.C / 64) {
@@ -657,13 +657,13 @@ extern "C" int cmt_layernorm(const float* X, int64_t ldx, int rows, int C, const
 extern "C" int cmt_add_cast(const float* X, const float* P, int rows, int C, int lowp_dtype, void* Yl, void* Yp,
                             void* stream) {
     CMT_REQUIRE(rows >= 0 && C % 4 == 0 && (Yp == nullptr || P), "cmt_add_cast: bad arguments");
-    CMT_REQUIRE(lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16 || lowp_dtype == CMT_BF16P,
-                "cmt_add_cast: lowp_dtype must be f16, bf16 or bf16 pair");
+    CMT_REQUIRE(lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16 || lowp_dtype == CMT_F16P,
+                "cmt_add_cast: lowp_dtype must be f16, bf16 or f16 pair");
     const int64_t n4 = (int64_t)rows * C / 4;
     if (n4 == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    if (lowp_dtype == CMT_BF16P)
-        add_cast_pair_kernel<<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, C, (bf16_t*)Yl, (bf16_t*)Yp);
+    if (lowp_dtype == CMT_F16P)
+        add_cast_pair_kernel<<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, C, (pair_t*)Yl, (pair_t*)Yp);
     else if (lowp_dtype == CMT_F16)
         add_cast_kernel<f16_t><<<nblocks(n4, 256), 256, 0, s>>>(X, P, n4, (f16_t*)Yl, (f16_t*)Yp);
     else
@@ -676,7 +676,7 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
     CMT_REQUIRE(out && n >= 0 && F > 0 && F % 4 == 0 && ldo % 8 == 0, "cmt_pos2embed: bad arguments");
     CMT_REQUIRE(pos != nullptr || (grid_h > 0 && grid_w > 0 && n == grid_h * grid_w),
                 "cmt_pos2embed: grid mode needs n == grid_h*grid_w");
-    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_BF16P,
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_F16P,
                 "cmt_pos2embed: bad odtype");
     if (n == 0) return 0;
     const int64_t total = (int64_t)n * (2 * F / 8);
@@ -688,9 +688,9 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
     else if (odtype == CMT_F16)
         pos2embed_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
                                                                     (f16_t*)out, ldo);
-    else if (odtype == CMT_BF16P)
-        pos2embed_kernel<bf16_t, true><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h,
-                                                                           grid_w, (bf16_t*)out, ldo);
+    else if (odtype == CMT_F16P)
+        pos2embed_kernel<pair_t, true><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h,
+                                                                           grid_w, (pair_t*)out, ldo);
     else
         pos2embed_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(pos, pos_stride, n, F, mode, grid_h, grid_w,
                                                                      (bf16_t*)out, ldo);
@@ -700,15 +700,15 @@ extern "C" int cmt_pos2embed(const float* pos, int64_t pos_stride, int n, int F,
 extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float pad_w, float depth_max,
                                 const float* i2l, const float* pc_range6, void* out, int odtype, void* stream) {
     CMT_REQUIRE(i2l && pc_range6 && out && BV > 0 && h > 0 && w > 0 && D > 0, "cmt_rv_pe_coords: bad arguments");
-    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_BF16P,
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_F16P,
                 "cmt_rv_pe_coords: bad odtype");
-    CMT_REQUIRE(odtype != CMT_BF16P || (D % 8 == 0 && (uintptr_t)out % 16 == 0),
-                "cmt_rv_pe_coords: the bf16-pair output needs D % 8 == 0 and a 16-byte aligned out");
+    CMT_REQUIRE(odtype != CMT_F16P || (D % 8 == 0 && (uintptr_t)out % 16 == 0),
+                "cmt_rv_pe_coords: the f16-pair output needs D % 8 == 0 and a 16-byte aligned out");
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
     hipStream_t s = (hipStream_t)stream;
     const char* vec = getenv("CMT_RVPE_VEC");   // diagnostics: 0 = the one-thread-per-depth kernel
-    if ((odtype == CMT_BF16P || !(vec && vec[0] == '0')) && D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) &&
+    if ((odtype == CMT_F16P || !(vec && vec[0] == '0')) && D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) &&
         (uintptr_t)out % 16 == 0) {
         const int64_t t8 = (int64_t)BV * h * w * (D / 8);
         if (odtype == CMT_F32)
@@ -717,10 +717,10 @@ extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float 
         else if (odtype == CMT_F16)
             rv_pe_coords_kernel8<f16_t><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,
                                                                          i2l, pc, (f16_t*)out);
-        else if (odtype == CMT_BF16P)
-            rv_pe_coords_kernel8<bf16_t, true><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w,
+        else if (odtype == CMT_F16P)
+            rv_pe_coords_kernel8<pair_t, true><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w,
                                                                                 depth_max - 1.f, i2l, pc,
-                                                                                (bf16_t*)out);
+                                                                                (pair_t*)out);
         else
             rv_pe_coords_kernel8<bf16_t><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w,
                                                                           depth_max - 1.f, i2l, pc, (bf16_t*)out);
@@ -757,7 +757,7 @@ extern "C" int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, in
                                       int odtype, float* mask, void* stream) {
     CMT_REQUIRE(ref && l2i && i2l && pc_range6 && out && mask && B > 0 && V > 0 && Nq > 0 && D > 0,
                 "cmt_rv_query_coords_ex: bad arguments");
-    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_BF16P,
+    CMT_REQUIRE(odtype == CMT_F32 || odtype == CMT_F16 || odtype == CMT_BF16 || odtype == CMT_F16P,
                 "cmt_rv_query_coords_ex: bad odtype");
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
@@ -769,10 +769,10 @@ extern "C" int cmt_rv_query_coords_ex(const float* ref, int B, int V, int Nq, in
     else if (odtype == CMT_F16)
         rv_query_coords_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
                                                                           pc.v[3] - 1.f, l2i, i2l, pc, (f16_t*)out, mask);
-    else if (odtype == CMT_BF16P)
-        rv_query_coords_kernel<bf16_t, true><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
+    else if (odtype == CMT_F16P)
+        rv_query_coords_kernel<pair_t, true><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
                                                                                  pc.v[3] - 1.f, l2i, i2l, pc,
-                                                                                 (bf16_t*)out, mask);
+                                                                                 (pair_t*)out, mask);
     else
         rv_query_coords_kernel<bf16_t><<<nblocks(total, 256), 256, 0, s>>>(ref, B, V, Nq, D, pad_h, pad_w,
                                                                            pc.v[3] - 1.f, l2i, i2l, pc, (bf16_t*)out,
@@ -791,13 +791,13 @@ extern "C" int cmt_masked_view_sum(const float* X, const float* mask, int B, int
 extern "C" int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int Nq, int C,
                                       const float* base, float* Y, void* Yl, void* Yp, int lowp_dtype, void* stream) {
     CMT_REQUIRE(X && mask && Y && B > 0 && V > 0 && Nq > 0 && C > 0, "cmt_masked_view_sum_ex: bad arguments");
-    CMT_REQUIRE((!Yl && !Yp) || lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16 || lowp_dtype == CMT_BF16P,
-                "cmt_masked_view_sum_ex: lowp_dtype must be f16, bf16 or bf16 pair");
+    CMT_REQUIRE((!Yl && !Yp) || lowp_dtype == CMT_F16 || lowp_dtype == CMT_BF16 || lowp_dtype == CMT_F16P,
+                "cmt_masked_view_sum_ex: lowp_dtype must be f16, bf16 or f16 pair");
     const int64_t total = (int64_t)B * Nq * C;
     hipStream_t s = (hipStream_t)stream;
-    if (lowp_dtype == CMT_BF16P)
-        masked_view_sum_ex_kernel<bf16_t, true><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
-                                                                                    (bf16_t*)Yl, (bf16_t*)Yp);
+    if (lowp_dtype == CMT_F16P)
+        masked_view_sum_ex_kernel<pair_t, true><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
+                                                                                    (pair_t*)Yl, (pair_t*)Yp);
     else if (lowp_dtype == CMT_F16)
         masked_view_sum_ex_kernel<f16_t><<<nblocks(total, 256), 256, 0, s>>>(X, mask, B, V, Nq, C, base, Y,
                                                                              (f16_t*)Yl, (f16_t*)Yp);
@@ -813,13 +813,13 @@ extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, v
     dim3 grid(cdiv(HW, 64), cdiv(C, 64), nb * nv);
     hipStream_t s = (hipStream_t)stream;
     const int esz = ydtype == CMT_F32 ? 4 : 2;
-    if (ydtype == CMT_BF16P) {
-        CMT_REQUIRE(ldy == 2 * C, "cmt_nchw_to_rows: bf16-pair rows need ldy == 2C (hi row, then lo row)");
+    if (ydtype == CMT_F16P) {
+        CMT_REQUIRE(ldy == 2 * C, "cmt_nchw_to_rows: f16-pair rows need ldy == 2C (hi row, then lo row)");
         if (HW % 4 == 0 && C % 64 == 0 && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0)
-            nchw_to_rows_vec_kernel<bf16_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
+            nchw_to_rows_vec_kernel<pair_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (pair_t*)Y, ldy, rows_per_batch,
                                                                        row_offset);
         else
-            nchw_to_rows_kernel<bf16_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
+            nchw_to_rows_kernel<pair_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (pair_t*)Y, ldy, rows_per_batch,
                                                                    row_offset);
         return cmt_check_launch("cmt_nchw_to_rows");
     }
@@ -852,7 +852,7 @@ extern "C" int cmt_split_rows(const float* X, int64_t ldx, int64_t rows, int C, 
                     (uintptr_t)Y % 8 == 0, "cmt_split_rows: bad arguments");
     const int64_t n4 = rows * (C / 4);
     if (n4 == 0) return 0;
-    split_rows_kernel<<<nblocks(n4, 256), 256, 0, (hipStream_t)stream>>>(X, ldx, n4, C, (bf16_t*)Y);
+    split_rows_kernel<<<nblocks(n4, 256), 256, 0, (hipStream_t)stream>>>(X, ldx, n4, C, (pair_t*)Y);
     return cmt_check_launch("cmt_split_rows");
 }
 

@@ -446,13 +446,13 @@ __device__ __forceinline__ void store4(void* C, int64_t idx, int dt, f32x4 v) {
     }
 }
 
-// lo_off: element distance of a CMT_BF16P row's lo half (its logical width)
+// lo_off: element distance of a CMT_F16P row's lo half (its logical width)
 __device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt, int lo_off = 0) {
     if (dt == CMT_F32) return *(const f32x4*)((const float*)p + idx);
-    if (dt == CMT_BF16P) {
-        typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-        const b4 h = *(const b4*)((const bf16_t*)p + idx);
-        const b4 l = *(const b4*)((const bf16_t*)p + idx + lo_off);
+    if (dt == CMT_F16P) {
+        typedef pair_t b4 __attribute__((ext_vector_type(4)));
+        const b4 h = *(const b4*)((const pair_t*)p + idx);
+        const b4 l = *(const b4*)((const pair_t*)p + idx + lo_off);
         return f32x4{(float)h[0] + (float)l[0], (float)h[1] + (float)l[1], (float)h[2] + (float)l[2],
                      (float)h[3] + (float)l[3]};
     }
@@ -470,9 +470,9 @@ __device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt, int l
 // WM x (4/WM) grid; each wave owns (BM/WM) x (BN*WM/4) as TM x TN 32x32 MFMA
 // tiles).  Accumulators are in the swapped C^T layout: lane = output row.
 //
-// X3 (A and W both CMT_BF16P, cmt_hip.h): the k loop runs over three
+// X3 (A and W both CMT_F16P, cmt_hip.h): the k loop runs over three
 // segments of the logical K -- (A_hi, W_hi), (A_lo, W_hi), (A_hi, W_lo) --
-// so the split-bf16 product is the plain bf16 pipeline over 3K with a column
+// so the split product is the plain f16 pipeline over 3K with a column
 // offset per operand and segment: the A row's lo half starts at its logical
 // width (K for rows, the channel count for the implicit convs), W's at K.
 template <typename CT, int BM, int BN, int S, int AMODE, int WM, bool X3 = false>
@@ -700,9 +700,9 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     // written to LDS (16-byte chunks XOR-swizzled by row) and read back so
     // every wave instruction stores 1 KB of contiguous memory (head-split:
     // 16 rows x 64 B of one head; rows: whole row segments).
-    // A CMT_BF16P C (row mode) is staged and stored twice: the hi halves, then
+    // A CMT_F16P C (row mode) is staged and stored twice: the hi halves, then
     // the lo halves N columns further (cmt_hip.h).
-    const int npass = a.c_dtype == CMT_BF16P ? 2 : 1;
+    const int npass = a.c_dtype == CMT_F16P ? 2 : 1;
     for (int pass = 0; pass < npass; ++pass) {
         barrier_mem();                                       // every wave is done with the staging ring
         const int cpr = BN * esz / 16;                       // 16-byte chunks per tile row (power of two)
@@ -721,9 +721,9 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
                                acc[tm][tn][4 * g + 3]};
                     if (pass) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] -= (float)(bf16_t)v[j];   // lo = bf16(x - hi)
+                        for (int j = 0; j < 4; ++j) v[j] -= (float)(pair_t)v[j];   // lo = f16(x - hi)
                     }
-                    store4<CT>(dst, 0, a.c_dtype == CMT_BF16P ? CMT_BF16 : a.c_dtype, v);
+                    store4<CT>(dst, 0, a.c_dtype == CMT_F16P ? CMT_F16 : a.c_dtype, v);
                 }
         }
         barrier_mem();
@@ -938,7 +938,7 @@ template <int BM, int BN, int S, int AMODE>
 int launch_dma_mode(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.M, BM), tn = a.N / BN;
     const int64_t nwg = (int64_t)tm * tn * a.batch;
-    if (a.w_dtype == CMT_BF16P) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE, true><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
+    if (a.w_dtype == CMT_F16P) gemm_dma_kernel<pair_t, BM, BN, S, AMODE, true><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     else if (a.w_dtype == CMT_BF16) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     else gemm_dma_kernel<f16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     return cmt_check_launch("cmt_gemm");
@@ -1028,19 +1028,19 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
     CMT_REQUIRE(a.K % BK == 0, "cmt_gemm: K must be a multiple of 32");
     CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
-    CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_BF16P,
+    CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16P,
                 "cmt_gemm: bad w_dtype");
-    CMT_REQUIRE(a.w_dtype != CMT_BF16P || a.a_dtype == CMT_BF16P, "cmt_gemm: split-bf16 (CMT_BF16P) W needs CMT_BF16P A");
-    CMT_REQUIRE(a.c_dtype != CMT_BF16P || a.c_mode == CMT_C_ROWS, "cmt_gemm: a CMT_BF16P C must be row mode");
+    CMT_REQUIRE(a.w_dtype != CMT_F16P || a.a_dtype == CMT_F16P, "cmt_gemm: split (CMT_F16P) W needs CMT_F16P A");
+    CMT_REQUIRE(a.c_dtype != CMT_F16P || a.c_mode == CMT_C_ROWS, "cmt_gemm: a CMT_F16P C must be row mode");
     CMT_REQUIRE(a.a_dtype == CMT_F32 || a.a_dtype == a.w_dtype, "cmt_gemm: A must be f32 or the compute dtype");
     CMT_REQUIRE(a.a_mode != CMT_A_CONV3X3 || a.a_dtype == a.w_dtype,
                 "cmt_gemm: the conv3x3 gather needs A in the compute dtype");
-    CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16 || a.c_dtype == CMT_BF16P,
+    CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16 || a.c_dtype == CMT_F16P,
                 "cmt_gemm: bad c_dtype");
     CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0, "cmt_gemm: lda/ldw must be multiples of 8 elements");
     CMT_REQUIRE(a.r_dtype == CMT_F32 || a.r_dtype == a.w_dtype, "cmt_gemm: R must be f32 or the compute dtype");
-    CMT_REQUIRE((a.c_dtype != CMT_BF16P && a.r_dtype != CMT_BF16P) || a.w_dtype == CMT_BF16P,
-                "cmt_gemm: CMT_BF16P C / R belong to the split-bf16 GEMM");
+    CMT_REQUIRE((a.c_dtype != CMT_F16P && a.r_dtype != CMT_F16P) || a.w_dtype == CMT_F16P,
+                "cmt_gemm: CMT_F16P C / R belong to the split GEMM");
     CMT_REQUIRE(a.A2 == nullptr || (a.a_mode == CMT_A_ROWS && a.a2_cols % 128 == 0),
                 "cmt_gemm: A2 needs row mode and 128-aligned a2_cols");
     CMT_REQUIRE(a.A2 == nullptr || a.a2_mode == CMT_A2_SELECT || (a.a_dtype == CMT_F32 && a.lda2 % 4 == 0),

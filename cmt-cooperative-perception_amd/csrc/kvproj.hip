@@ -375,8 +375,8 @@ __global__ __launch_bounds__(64 * NW, 1) void kvproj_kernel(cmt_gemm_args a, int
 }
 
 // ---------------------------------------------------------------------------
-// Split-bf16 form (CMT_BF16P A / W: the 'ref' policy's fp32-accurate K/V):
-// per k-step and 32-token tile three MFMAs W_hi A_hi + W_hi A_lo + W_lo A_hi.
+// Split form (CMT_F16P A / W: the 'ref' policy's fp32-accurate K/V):
+// per k-step and 32-token tile three f16 MFMAs W_hi A_hi + W_hi A_lo + W_lo A_hi.
 // The 128-token A tile is resident as its hi and lo planes (2 x 64 KB of
 // LDS).  W (hi and lo, L2-resident: 3 MB for all layers) streams into a
 // KV3_RING-deep register ring of k-steps, KV3_RING steps ahead across plane
@@ -392,7 +392,7 @@ constexpr int KV3_RING = 4;
 
 template <typename TC>
 __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int parts) {
-    // A tile hi plane | lo plane, each [128 tokens][256] bf16 with 16-byte chunks XOR-swizzled by row & 15
+    // A tile hi plane | lo plane, each [128 tokens][256] f16 with 16-byte chunks XOR-swizzled by row & 15
     __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -403,8 +403,8 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     const int ncols = a.N / parts;
     const int n_part = part * ncols;
     const bool sel_a2 = a.A2 != nullptr && n_part < a.a2_cols;
-    const bf16_t* Ab = (const bf16_t*)(sel_a2 ? a.A2 : a.A);
-    const int64_t lda = sel_a2 ? a.lda2 : a.lda;   // bf16 elements per pair row (hi 256 | lo 256)
+    const pair_t* Ab = (const pair_t*)(sel_a2 ? a.A2 : a.A);
+    const int64_t lda = sel_a2 ? a.lda2 : a.lda;   // 16-bit elements per pair row (hi 256 | lo 256)
 #pragma unroll
     for (int i = 0; i < 2 * KP_BM * KP_K * 2 / 16 / 512; ++i) {
         const int piece = tid + 512 * i;
@@ -418,13 +418,13 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     }
     const int planes_w = ncols / 32 / 8;
     const int plane0 = (n_part >> 5) + wave * planes_w;
-    const bf16_t* Wh = (const bf16_t*)a.W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
-    const bf16_t* Wl = Wh + (int64_t)a.N * KP_K;
-    bf16x8 rh[KV3_RING], rl[KV3_RING];
+    const pair_t* Wh = (const pair_t*)a.W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
+    const pair_t* Wl = Wh + (int64_t)a.N * KP_K;
+    pair8_t rh[KV3_RING], rl[KV3_RING];
 #pragma unroll
     for (int ks = 0; ks < KV3_RING; ++ks) {
-        rh[ks] = *(const bf16x8*)(Wh + ks * 512);
-        rl[ks] = *(const bf16x8*)(Wl + ks * 512);
+        rh[ks] = *(const pair8_t*)(Wh + ks * 512);
+        rl[ks] = *(const pair8_t*)(Wl + ks * 512);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_mem();
@@ -463,17 +463,17 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
             const int slot = ks % KV3_RING;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const bf16x8 ah = *(const bf16x8*)(lhi + (t * 32 + lr) * (KP_K * 2) + sw);
-                const bf16x8 al = *(const bf16x8*)(llo + (t * 32 + lr) * (KP_K * 2) + sw);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rh[slot], ah, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rh[slot], al, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rl[slot], ah, acc[t], 0, 0, 0);
+                const pair8_t ah = *(const pair8_t*)(lhi + (t * 32 + lr) * (KP_K * 2) + sw);
+                const pair8_t al = *(const pair8_t*)(llo + (t * 32 + lr) * (KP_K * 2) + sw);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], ah, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], al, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], ah, acc[t], 0, 0, 0);
             }
             const int kn = ks + KV3_RING;
             const int64_t woff = kn < KP_KS ? (int64_t)j * (KP_KS * 512) + kn * 512
                                             : (int64_t)jn * (KP_KS * 512) + (kn - KP_KS) * 512;
-            rh[slot] = *(const bf16x8*)(Wh + woff);
-            rl[slot] = *(const bf16x8*)(Wl + woff);
+            rh[slot] = *(const pair8_t*)(Wh + woff);
+            rl[slot] = *(const pair8_t*)(Wl + woff);
             // each k-step's LDS fragment reads stay beside its MFMAs
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -518,9 +518,9 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
     const char* pv = getenv("CMT_KVPROJ_PARTS");
     const int pmul = (pv && pv[0] == '4' && a.A2 && (a.N / 4 / 32) % 8 == 0) ? 2 : 1;
     const int parts = (a.A2 ? 2 : 1) * pmul;
-    if (a.w_dtype == CMT_BF16P) {
-        // split-bf16 (fp32-accurate) form: pair A / A2 rows, W_hi then W_lo fragment-packed, f16 / bf16 C
-        CMT_REQUIRE(a.a_dtype == CMT_BF16P && (a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16),
+    if (a.w_dtype == CMT_F16P) {
+        // split (fp32-accurate) form: f16 pair A / A2 rows, W_hi then W_lo fragment-packed, f16 / bf16 C
+        CMT_REQUIRE(a.a_dtype == CMT_F16P && (a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16),
                     "cmt_kv_proj: split W needs pair A and an f16 / bf16 C");
         CMT_REQUIRE(a.A && a.W && a.C && a.M > 0 && a.K == KP_K && a.batch == 1 && a.a_mode == CMT_A_ROWS &&
                         a.c_mode == CMT_C_HEADSPLIT && a.R == nullptr && !a.relu && a.rows_per_batch > 0 &&

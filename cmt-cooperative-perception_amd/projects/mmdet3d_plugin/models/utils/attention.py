@@ -133,7 +133,7 @@ def project_attend_project(q, k, v, q_pos, k_pos, w_in, b_in, w_out, b_out, iden
         y = torch.empty((x.shape[0], C), dtype=adt, device=dev)
         w = w_in[i * C:(i + 1) * C]
         if split:
-            # split-bf16 operand of x (+ pos): one native pass writes the pair rows
+            # split f16 operand of x (+ pos): one native pass writes the pair rows
             xs = op_empty(x.shape[0], C, SPLIT, dev)
             if pos is not None:
                 native.add_cast(x.contiguous(), rows=x.shape[0], C=C, Yp=xs, P=pos.contiguous())

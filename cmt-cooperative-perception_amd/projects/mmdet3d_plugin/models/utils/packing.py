@@ -35,11 +35,14 @@ class PackCache:
 
 
 def to_dtype(t, dtype):
-    """Weights in a compute format: a torch dtype, or the split-bf16 pair
-    (runtime.SPLIT): [..., K] -> [..., 2, K] with hi = bf16(w), lo = bf16(w - hi)."""
+    """Weights in a compute format: a torch dtype, or the split f16 pair
+    (runtime.SPLIT, cmt_hip.h CMT_F16P): [..., K] -> [..., 2, K] with
+    hi = f16(w), lo = f16(w - hi)."""
     if dtype == torch.uint16:
         w = t.detach().float()
-        hi = w.bfloat16()
-        lo = (w - hi.float()).bfloat16()
+        if w.numel() and w.abs().max().item() >= 65504.0:
+            raise ValueError("weights beyond the f16 range cannot take the split f16 pair format")
+        hi = w.half()
+        lo = (w - hi.float()).half()
         return torch.stack([hi, lo], dim=-2).contiguous().view(torch.uint16)
     return t.detach().to(dtype).contiguous()

@@ -559,7 +559,7 @@ class PETRTransformerDecoder(nn.Module):
                 kv_wp = native.kv_pack(kv_w)
             elif C == 256 and kv_w.dtype == SPLIT:
                 # split pairs: the fragment-packed hi halves, then the lo halves (cmt_kv_proj's split form)
-                b = kv_w.view(torch.bfloat16)
+                b = kv_w.view(torch.float16)
                 kv_wp = torch.cat([native.kv_pack(b[:, 0].contiguous()),
                                    native.kv_pack(b[:, 1].contiguous())]).view(SPLIT)
             return dict(layers=layers, kv_w=kv_w, kv_wp=kv_wp, kv_b=kv_b,
@@ -800,7 +800,7 @@ class PETRTransformerDecoder(nn.Module):
                                      q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
                                      v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
                                      v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
-                                     round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2,
+                                     round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2,
                                      kmax_ld=L * H, kmax_plane0=l * H)
                 nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
                 native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
@@ -835,7 +835,7 @@ class PETRTransformerDecoder(nn.Module):
                                  q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
                                  v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
                                  v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
-                                 round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2, kmax_ld=L * H,
+                                 round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2, kmax_ld=L * H,
                                  kmax_plane0=l * H)
             w1, b1, e1 = lw["norms"][1]
             if fuse_ln:
@@ -886,7 +886,7 @@ class PETRTransformerDecoder(nn.Module):
                                  q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
                                  v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
                                  v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0),
-                                 workspace=ws, round_output=prec.round_cross_out, fold_scale=True, kmax2=kmax2,
+                                 workspace=ws, round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2,
                                  kmax_ld=L * H, kmax_plane0=l * H)
             nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
             native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,

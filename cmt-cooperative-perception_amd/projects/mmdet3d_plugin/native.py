@@ -11,7 +11,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "available", "gemm", "split_rows", "width", "lstride", "BF16P", "gemm_ln", "chain", "kv_proj", "kv_pack", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
+__all__ = ["lib", "available", "gemm", "split_rows", "width", "lstride", "F16P", "gemm_ln", "chain", "kv_proj", "kv_pack", "attention", "layernorm", "layernorm_ex", "add_cast", "pos2embed",
            "rv_pe_coords",
            "rv_query_coords", "masked_view_sum", "nchw_to_rows", "cast", "task_head_tail",
            "voxelize", "box_decode", "DT", "dtype_code", "LN_NAN_TO_NUM", "LN_MAX_INTO"]
@@ -19,10 +19,10 @@ __all__ = ["lib", "available", "gemm", "split_rows", "width", "lstride", "BF16P"
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 _DEFAULT_LIB = os.path.join(_PKG_ROOT, "lib", "libcmt_hip.so")
 
-F32, F16, BF16, BF16P = 0, 1, 2, 3
-# torch.uint16 (runtime.SPLIT) carries the split-bf16 pair format CMT_BF16P: a
-# logical [..., C] operand stored as [..., 2, C] (hi values, then lo values)
-DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.uint16: BF16P}
+F32, F16, BF16, F16P = 0, 1, 2, 3
+# torch.uint16 (runtime.SPLIT) carries the split pair format CMT_F16P: a logical
+# [..., C] operand stored as [..., 2, C] (f16 hi values, then f16 lo values)
+DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.uint16: F16P}
 LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
@@ -309,7 +309,7 @@ def kv_proj(A, Wp, C, *, M, N, bias=None, A2=None, headsplit_rows, plane_max2=No
 
 
 def _ps(t):
-    """Physical 16-bit words per logical element: 2 for a split-bf16 pair
+    """Physical 16-bit words per logical element: 2 for a split f16 pair
     tensor, else 1.  Strides and offsets of the wrappers below are LOGICAL
     (elements of the [..., C] operand) and scaled by this; pair offsets must
     be whole rows."""
@@ -359,7 +359,7 @@ def _gemm_args(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None
 def linear(X, W, bias=None, *, relu=False, R=None, out=None, out_dtype=torch.float32, A2=None, a2_cols=0,
            headsplit_rows=0):
     """Row-major linear layer: X [M, K] (f32 or compute dtype; pair [M, 2, K]),
-    W [N, K] (pair [N, 2, K]).  A split-bf16 W with an fp32 X splits X first."""
+    W [N, K] (pair [N, 2, K]).  A split W with an fp32 X splits X first."""
     if W.dtype == torch.uint16 and X.dtype == torch.float32:
         X = split_rows(X)
     M, K = X.shape[0], width(X)
@@ -373,7 +373,7 @@ def linear(X, W, bias=None, *, relu=False, R=None, out=None, out_dtype=torch.flo
 
 
 def split_rows(X, out=None):
-    """fp32 rows X [M, C] (any row stride) -> split-bf16 pair rows [M, 2, C] (cmt_split_rows)."""
+    """fp32 rows X [M, C] (any row stride) -> split f16 pair rows [M, 2, C] (cmt_split_rows)."""
     _dev(X, out)
     M, C = X.shape
     if out is None:

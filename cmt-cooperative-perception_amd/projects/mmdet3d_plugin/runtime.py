@@ -7,11 +7,11 @@ custom_fp16=dict(pts_bbox_head=False), e.g.
 configs/CMT_Nuscenes/lidar/cmt_lidar_voxel0075_cbgs.py:284-286).
 
 Policies (``set_precision`` / env ``CMT_PRECISION``):
-  'ref'   -- the reference's numerics with fp32-accurate split-bf16 GEMMs:
-             every fp32 GEMM operand is carried as a bf16 pair (hi, lo)
-             (``SPLIT``, cmt_hip.h CMT_BF16P) and multiplied in three bf16
-             MFMA passes (hi*hi + lo*hi + hi*lo, fp32 accumulate: ~2^-16
-             relative per product, against TF32's 2^-11); self-attention core
+  'ref'   -- the reference's numerics with fp32-accurate split GEMMs: every
+             fp32 GEMM operand is carried as an f16 pair (hi, lo) (``SPLIT``,
+             cmt_hip.h CMT_F16P) and multiplied in three f16 MFMA passes
+             (hi*hi + lo*hi + hi*lo, fp32 accumulate: ~2^-21 relative per
+             product, against TF32's 2^-11); self-attention core
              in exact f32 (nn.MultiheadAttention); cross-attention core in
              fp16 with fp32 accumulation, P rounded to fp16 and an fp16-rounded
              output (flash-attn 0.2.2 under auto_fp16).
@@ -32,8 +32,8 @@ import torch
 
 __all__ = ["Precision", "get_precision", "set_precision", "PRECISIONS", "SPLIT", "op_empty", "is_split"]
 
-# Storage dtype of a split-bf16 operand: 16-bit words, a tensor of logical shape
-# [..., C] stored as [..., 2, C] (the C bf16 hi values, then the C bf16 lo values).
+# Storage dtype of a split operand: 16-bit words, a tensor of logical shape
+# [..., C] stored as [..., 2, C] (the C f16 hi values, then the C f16 lo values).
 SPLIT = torch.uint16
 
 
@@ -55,13 +55,15 @@ class Precision:
     attn: torch.dtype          # cross-attention core dtype
     self_attn: torch.dtype     # self-attention core dtype
     round_cross_out: bool      # round the cross-attention output to ``attn``
+    fold_q: bool = False       # fold scale*log2(e) into the low-precision cross-attention Q
+                               # (one more rounding of Q; off where Q must stay the reference's)
 
 
 PRECISIONS = {
     "ref": Precision("ref", SPLIT, torch.float16, torch.float32, True),
     "exact": Precision("exact", torch.float32, torch.float16, torch.float32, True),
-    "fp16": Precision("fp16", torch.float16, torch.float16, torch.float16, False),
-    "bf16": Precision("bf16", torch.bfloat16, torch.bfloat16, torch.bfloat16, False),
+    "fp16": Precision("fp16", torch.float16, torch.float16, torch.float16, False, True),
+    "bf16": Precision("bf16", torch.bfloat16, torch.bfloat16, torch.bfloat16, False, True),
 }
 
 _current = PRECISIONS[os.environ.get("CMT_PRECISION", "ref")]

@@ -1,4 +1,4 @@
-"""Diagnostics: error pattern of the split-bf16 GEMM over shapes (GPU)."""
+"""Diagnostics: error pattern of the split f16 GEMM over shapes (GPU)."""
 import math
 import sys
 import os

@@ -32,17 +32,19 @@ extern "C" {
 
 #define CMT_ABI_VERSION 12
 
-/* CMT_BF16P (ABI 12), "bf16 pair": an fp32 operand split into two bf16
- * halves, x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (16 significant
- * bits, relative error <= 2^-17).  A row of logical width C is stored as
- * C hi values followed by C lo values ([rows][2C] bf16, leading dimensions in
- * bf16 elements).  A GEMM whose A and W are both CMT_BF16P computes
- * A_hi W_hi + A_lo W_hi + A_hi W_lo with fp32 accumulation (three bf16 MFMA
- * passes, the dropped A_lo W_lo term is ~2^-16 of a product): the fp32
- * GEMMs of the reference at 3/16 of the bf16 rate instead of the exact-f32
- * MFMA's 1/16.  Producers (LayerNorm, layout, geometry, GEMM epilogues,
- * attention outputs) write this format directly. */
-enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2, CMT_BF16P = 3 };
+/* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
+ * x = hi + lo with hi = f16(x), lo = f16(x - hi) (22 significant bits: relative
+ * error <= 2^-22 for |x| in f16's normal range, absolute <= 2^-25 below it;
+ * |x| must stay below 65504).  A row of logical width C is stored as C hi
+ * values followed by C lo values ([rows][2C] 16-bit words, leading dimensions
+ * in 16-bit elements).  A GEMM whose A and W are both CMT_F16P computes
+ * A_hi W_hi + A_lo W_hi + A_hi W_lo with fp32 accumulation (three f16 MFMA
+ * passes; the dropped A_lo W_lo term is ~2^-22 of a product): the fp32 GEMMs
+ * of the reference at 3/16 of the f16 rate instead of the exact-f32 MFMA's
+ * 1/16, 16x tighter than a bf16 pair would be (2^-16) at the same rate.
+ * Producers (LayerNorm, layout, geometry, GEMM epilogues, attention outputs)
+ * write this format directly. */
+enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2, CMT_F16P = 3 };
 
 enum cmt_status {
     CMT_OK = 0,
@@ -331,8 +333,8 @@ int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int 
 int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype,
                      int64_t ldy, int64_t rows_per_batch, int64_t row_offset, void* stream);
 int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* stream);
-/* cmt_split_rows (ABI 12): fp32 rows X[r * ldx + c] -> CMT_BF16P rows Y [rows][2C]
- * (the split-bf16 GEMM operand of an fp32 tensor, e.g. the module-level API's inputs). */
+/* cmt_split_rows (ABI 12): fp32 rows X[r * ldx + c] -> CMT_F16P rows Y [rows][2C]
+ * (the split f16 GEMM operand of an fp32 tensor, e.g. the module-level API's inputs). */
 int cmt_split_rows(const float* X, int64_t ldx, int64_t rows, int C, void* Y, void* stream);
 
 /* ------------------------------------------------------------------------

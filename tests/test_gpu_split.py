@@ -1,12 +1,12 @@
-"""Split-bf16 ('ref' policy) kernels against float64 PyTorch references.
+"""Split-f16 ('ref' policy) kernels against float64 PyTorch references.
 
 The reference computes every projection / MLP / conv of the head in fp32; the
-'ref' policy carries each fp32 operand as a bf16 pair x = hi + lo (cmt_hip.h
-CMT_BF16P) and multiplies in three bf16 MFMA passes.  These tests hold the
+'ref' policy carries each fp32 operand as an f16 pair x = hi + lo (cmt_hip.h
+CMT_F16P) and multiplies in three f16 MFMA passes.  These tests hold the
 split GEMM (row, implicit 3x3 conv, implicit k=3 conv1d modes; fp32, f16
 head-split and pair outputs; pair residual), every producer of pair operands
 and the f16 long-key cross-attention (flash-attn 0.2.2 numerics) to bounds
-that an fp32 GEMM meets and a bf16 one misses by two orders of magnitude.
+that an fp32 GEMM meets and a bf16 one misses by three orders of magnitude.
 Every call goes through the C ABI."""
 import math
 
@@ -25,9 +25,9 @@ def N():
 
 
 def _pair(x):
-    """fp32 [..., C] -> [..., 2, C] uint16 (the host restatement of the split)."""
-    hi = x.float().bfloat16()
-    lo = (x.float() - hi.float()).bfloat16()
+    """fp32 [..., C] -> [..., 2, C] uint16 (the host restatement of the f16 split)."""
+    hi = x.float().half()
+    lo = (x.float() - hi.float()).half()
     return torch.stack([hi, lo], -2).contiguous().view(SPLIT)
 
 
@@ -37,13 +37,13 @@ def _same(a, b):
 
 
 def _unpair(p):
-    b = p.view(torch.bfloat16).double()
+    b = p.view(torch.float16).double()
     return b[..., 0, :] + b[..., 1, :]
 
 
 def _tol(ref, K):
-    # three bf16 passes: <= ~2^-16 relative per product; random-sign sums over K
-    return 4e-5 * ref.abs().max().item() + 1e-6
+    # three f16 passes: <= ~2^-21 relative per product (2^-25 absolute below f16's normal range)
+    return 3e-6 * ref.abs().max().item() + 1e-6
 
 
 @pytest.mark.parametrize("M,N_,K", [(900, 256, 256), (130, 768, 512), (2000, 3072, 256), (64, 1024, 192),
@@ -65,11 +65,11 @@ def test_gemm_split_rows(N, dev, M, N_, K):
     N.gemm(_pair(A).to(dev), _pair(W).to(dev), outp, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_, bias=b.to(dev),
            relu=True, R=_pair(R).to(dev), ldr=N_)
     err2 = (_unpair(outp.cpu()) - ref2).abs().max().item()
-    # the pair output itself keeps 16 significant bits
-    assert err2 <= _tol(ref2, K) + 2 ** -16 * ref2.abs().max().item(), err2
+    # the pair output itself keeps 22 significant bits
+    assert err2 <= _tol(ref2, K) + 2 ** -21 * ref2.abs().max().item(), err2
     bf = (A.bfloat16().double() @ W.bfloat16().double().t() + b.double() - ref).abs().max().item()
     print(f"split GEMM {M}x{N_}x{K}: max abs err {err:.2e} (bf16 operands: {bf:.2e})")
-    assert err * 30 < bf
+    assert err * 300 < bf
 
 
 def test_gemm_split_headsplit_select(N, dev):
@@ -122,7 +122,7 @@ def test_gemm_split_conv3x3(N, dev):
     ref = ref.flatten(2).permute(0, 2, 1)
     got = _unpair(out.cpu()).view(B, Nk, Cout)[:, :H * W]
     err = (got - ref).abs().max().item()
-    assert err <= _tol(ref, 9 * Cin) + 2 ** -16 * ref.abs().max().item(), err
+    assert err <= _tol(ref, 9 * Cin) + 2 ** -21 * ref.abs().max().item(), err
 
 
 def test_gemm_split_conv1d3_grouped(N, dev):
@@ -260,7 +260,7 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
 
 
 def test_attention_pair_output(N, dev):
-    """Attention output written as the split-bf16 operand of the out-projection:
+    """Attention output written as the split f16 operand of the out-projection:
     exactly the split of the f32 output (f16-rounded values are exact as hi + lo)."""
     g = torch.Generator().manual_seed(21)
     B, H, Nq, Nk = 1, 8, 300, 5000
@@ -278,7 +278,7 @@ def test_attention_pair_output(N, dev):
 
 @pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100)])
 def test_kvproj_split(N, dev, B, S):
-    """cmt_kv_proj's split-bf16 form (K columns from lowp(mem + pos), V columns
+    """cmt_kv_proj's split f16 form (K columns from lowp(mem + pos), V columns
     from lowp(mem); all layers in one launch) against float64, with the key-norm
     partials of the K planes; ragged last row tile."""
     g = torch.Generator().manual_seed(B * S)
@@ -290,7 +290,7 @@ def test_kvproj_split(N, dev, B, S):
     b = torch.randn(N_, generator=g)
     ref = torch.cat([A2.double() @ W[:N_ // 2].double().t(), A.double() @ W[N_ // 2:].double().t()], 1) + b.double()
     Wp = _pair(W)
-    wb = Wp.view(torch.bfloat16)
+    wb = Wp.view(torch.float16)
     packed = torch.cat([N.kv_pack(wb[:, 0].contiguous()), N.kv_pack(wb[:, 1].contiguous())]).view(SPLIT).to(dev)
     out = torch.empty(B * N_ * S, dtype=torch.float16, device=dev)
     pm = torch.empty(-(-M // 64) * (N_ // 2 // 32), device=dev)
