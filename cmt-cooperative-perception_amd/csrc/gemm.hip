@@ -470,17 +470,20 @@ __device__ __forceinline__ f32x4 load4(const void* p, int64_t idx, int dt, int l
 // WM x (4/WM) grid; each wave owns (BM/WM) x (BN*WM/4) as TM x TN 32x32 MFMA
 // tiles).  Accumulators are in the swapped C^T layout: lane = output row.
 //
-// X3 (A and W both CMT_F16P, cmt_hip.h): the k loop runs over three
-// segments of the logical K -- (A_hi, W_hi), (A_lo, W_hi), (A_hi, W_lo) --
-// so the split product is the plain f16 pipeline over 3K with a column
-// offset per operand and segment: the A row's lo half starts at its logical
-// width (K for rows, the channel count for the implicit convs), W's at K.
+// X3 (A and W both CMT_F16P, cmt_hip.h): every stage carries four tiles --
+// A_hi, A_lo, W_hi, W_lo of the same 64 k -- and each k step runs the three
+// products A_hi W_hi + A_lo W_hi + A_hi W_lo on them, so one staged byte feeds
+// 3/2 MFMAs instead of one (a stage per product re-streams A_hi and W_hi) and
+// the k loop is K / 64 steps long, not 3K / 64.  The A row's lo half starts at
+// its logical width (K for rows, the channel count for the implicit convs),
+// W's at K.
 template <typename CT, int BM, int BN, int S, int AMODE, int WM, bool X3 = false>
 struct DmaTile {
     static constexpr int KS = 64;                          // k per stage: one 128-byte LDS row per tile row
-    static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+    static constexpr int NPL = X3 ? 2 : 1;                 // planes per operand (hi, lo)
+    static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = NPL * (A_BYTES + B_BYTES);
     static constexpr int APER = BM / 32, BPER = BN / 32;   // 256 lanes x 16 B = 32 rows per block-wide copy
-    static constexpr int PER = APER + BPER;                // glds per thread per stage
+    static constexpr int PER = NPL * (APER + BPER);        // glds per thread per stage
     static constexpr int WN = 4 / WM;
     static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     static constexpr int SMEM = S * STAGE;
@@ -521,10 +524,12 @@ struct DmaTile {
 
         // implicit convs (3x3, 1D k = 3): the stages arrive in increasing k order and a tap spans
         // (tap width) / 64 stages, so each row's gathered offset is recomputed once per tap
-        // (9 or 3 times per tile and X3 segment), not per stage (no integer division in the k loop)
+        // (9 or 3 times per tile), not per stage (no integer division in the k loop)
         const int tapw = AMODE == CMT_A_CONV3X3 ? a.conv_c : (AMODE == CMT_A_CONV1D3 ? a.K / 3 : a.K);
         const int ntaps = AMODE == CMT_A_CONV3X3 ? 9 : (AMODE == CMT_A_CONV1D3 ? 3 : 1);
-        int cseg = 0, ctap = -1, ccin = 0;
+        (void)ntaps;
+        const int a_lo = AMODE == CMT_A_ROWS ? a.K : tapw;    // element offset of an A row's lo half
+        int ctap = -1, ccin = 0;
         int64_t toff[APER];
         auto issue = [&](int buf, int kt) {
             char* sb = smem + buf * STAGE;
@@ -540,36 +545,33 @@ struct DmaTile {
                         toff[i] = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), ctap * tapw);
                 } else if ((ccin += KS) == tapw) {
                     ccin = 0;
-                    if (++ctap == ntaps) {   // X3: next segment, taps from 0 again
-                        ctap = 0;
-                        ++cseg;
-                    }
+                    ++ctap;
 #pragma unroll
                     for (int i = 0; i < APER; ++i)
                         toff[i] = a_offset<AMODE>(a, ri[i], m0 + (4 * i + wave) * 8 + (lane >> 3), ctap * tapw);
                 }
-                ka = ccin + (X3 && cseg == 1 ? tapw : 0);
-                kw = ctap * tapw + ccin + (X3 && cseg == 2 ? a.K : 0);
+                ka = ccin;
+                kw = ctap * tapw + ccin;
             } else {
-                const int k0 = kt * KS;
-                if constexpr (X3) {
-                    ka = k0 >= 2 * a.K ? k0 - 2 * a.K : k0;   // hi | lo | hi
-                    kw = k0 >= a.K ? k0 - a.K : k0;           // hi | hi | lo
-                } else {
-                    ka = kw = k0;
-                }
+                ka = kw = kt * KS;
             }
 #pragma unroll
             for (int i = 0; i < APER; ++i) {
-                const void* src;
+                const CT* src;
                 if (AMODE == CMT_A_ROWS)
                     src = asrc[i] + ka;
                 else
-                    src = toff[i] < 0 ? (const void*)g_zero_page : (const void*)((const CT*)Ab + toff[i] + ka + acs[i]);
-                glds16(src, sb + (4 * i + wave) * 1024);
+                    src = toff[i] < 0 ? nullptr : (const CT*)Ab + toff[i] + ka + acs[i];
+                glds16(src ? (const void*)src : (const void*)g_zero_page, sb + (4 * i + wave) * 1024);
+                if constexpr (X3)
+                    glds16(src ? (const void*)(src + a_lo) : (const void*)g_zero_page,
+                           sb + A_BYTES + (4 * i + wave) * 1024);
             }
 #pragma unroll
-            for (int i = 0; i < BPER; ++i) glds16(bsrc[i] + kw, sb + A_BYTES + (4 * i + wave) * 1024);
+            for (int i = 0; i < BPER; ++i) {
+                glds16(bsrc[i] + kw, sb + NPL * A_BYTES + (4 * i + wave) * 1024);
+                if constexpr (X3) glds16(bsrc[i] + kw + a.K, sb + NPL * A_BYTES + B_BYTES + (4 * i + wave) * 1024);
+            }
         };
 
 #pragma unroll
@@ -579,7 +581,7 @@ struct DmaTile {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-        const int nk = (X3 ? 3 : 1) * a.K / KS;
+        const int nk = a.K / KS;
 #pragma unroll
         for (int s = 0; s < S; ++s)
             if (s < nk) issue(s, s);
@@ -593,7 +595,7 @@ struct DmaTile {
             // every wave is past its reads of stage kt-1: refill that buffer
             if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
             const char* As = smem + (kt % S) * STAGE;
-            const char* Bs = As + A_BYTES;
+            const char* Bs = As + NPL * A_BYTES;
 #pragma unroll
             for (int ks = 0; ks < KS / 16; ++ks) {
                 frag af[TM], bfr[TN];
@@ -607,6 +609,28 @@ struct DmaTile {
                 for (int tn = 0; tn < TN; ++tn) {
                     const int r = wn * (BN / WN) + tn * 32 + lr;
                     bfr[tn] = *(const frag*)(Bs + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+                }
+                if constexpr (X3) {
+                    frag al[TM], bl[TN];
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm) {
+                        const int r = wm * (BM / WM) + tm * 32 + lr;
+                        al[tm] = *(const frag*)(As + A_BYTES + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+                    }
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) {
+                        const int r = wn * (BN / WN) + tn * 32 + lr;
+                        bl[tn] = *(const frag*)(Bs + B_BYTES + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+                    }
+                    // the two small products first, then the hi product, per accumulator
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<CT>::mma(bfr[tn], al[tm], acc[tm][tn]);
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<CT>::mma(bl[tn], af[tm], acc[tm][tn]);
                 }
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
@@ -938,7 +962,9 @@ template <int BM, int BN, int S, int AMODE>
 int launch_dma_mode(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.M, BM), tn = a.N / BN;
     const int64_t nwg = (int64_t)tm * tn * a.batch;
-    if (a.w_dtype == CMT_F16P) gemm_dma_kernel<pair_t, BM, BN, S, AMODE, true><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
+    // the pair stages carry four tiles: 128 x 128 keeps 2 of them (128 KB), the others 3 or 2
+    constexpr int SP = BM * BN >= 128 * 128 ? 2 : (BM * BN >= 128 * 64 ? 2 : 3);
+    if (a.w_dtype == CMT_F16P) gemm_dma_kernel<pair_t, BM, BN, SP, AMODE, true><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     else if (a.w_dtype == CMT_BF16) gemm_dma_kernel<bf16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     else gemm_dma_kernel<f16_t, BM, BN, S, AMODE><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
     return cmt_check_launch("cmt_gemm");
