@@ -38,6 +38,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
     const float* x = a.X + (int64_t)row * a.ldx;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) v[i] = x[lane + 64 * i];
+    for (int q = 1; q < a.nparts; ++q) {   // split-K partial products (cmt_gemm k_splits)
+        const float* xq = x + q * a.part_stride;
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) v[i] += xq[lane + 64 * i];
+    }
     float pv[VPT];
     if (a.Yp) {
         const float* pr = a.P + (int64_t)row * a.ldp;

@@ -489,8 +489,9 @@ struct DmaTile {
     static constexpr int SMEM = S * STAGE;
     static_assert(TM >= 1 && TN >= 1 && APER >= 1, "tile too small");
 
+    // k steps kt0 .. kt0 + nk - 1 (of 64) of the logical K; nk < 0: all of them
     static __device__ __forceinline__ void run(const cmt_gemm_args& a, char* smem, int m0, int n0, int z,
-                                               f32x16 (&acc)[TM][TN]) {
+                                               f32x16 (&acc)[TM][TN], int kt0 = 0, int nk = -1) {
         typedef typename mfma_traits<CT>::frag frag;
         const int tid = threadIdx.x;
         const int lane = tid & 63;
@@ -581,10 +582,10 @@ struct DmaTile {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-        const int nk = a.K / KS;
+        if (nk < 0) nk = a.K / KS;
 #pragma unroll
         for (int s = 0; s < S; ++s)
-            if (s < nk) issue(s, s);
+            if (s < nk) issue(s, kt0 + s);
 
         const int lr = lane & 31;
         const int lh = lane >> 5;
@@ -593,7 +594,7 @@ struct DmaTile {
             wait_tiles<PER, S>(last - kt);
             barrier_mem();
             // every wave is past its reads of stage kt-1: refill that buffer
-            if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
+            if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt0 + kt + S - 1);
             const char* As = smem + (kt % S) * STAGE;
             const char* Bs = As + NPL * A_BYTES;
 #pragma unroll
@@ -661,10 +662,15 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     constexpr int TM = Tile::TM, TN = Tile::TN;
     __shared__ __attribute__((aligned(16))) char smem[Tile::SMEM];
     int z, mt, nt;
-    xcd_tile(tiles_m, tiles_n, a.batch, z, mt, nt);
+    // split-K (batch 1): grid z enumerates the K parts
+    const int ksp = a.k_splits > 1 ? a.k_splits : 1;
+    xcd_tile(tiles_m, tiles_n, a.batch * ksp, z, mt, nt);
     const int m0 = mt * BM, n0 = nt * BN;
     f32x16 acc[TM][TN];
-    Tile::run(a, smem, m0, n0, z, acc);
+    const int part = ksp > 1 ? z : 0;
+    if (ksp > 1) z = 0;
+    const int nkp = a.K / Tile::KS / ksp;
+    Tile::run(a, smem, m0, n0, z, acc, part * nkp, nkp);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -675,9 +681,10 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     // Every bias / residual load is issued before the first store: vmcnt counts
     // stores too on CDNA4, so a load waited for after a store would drain it.
     const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
-    char* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
-    const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
-    const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
+    char* Cz = (char*)a.C + ((int64_t)z * a.c_bstride + part * a.c_split_stride) * esz;
+    const float* biasz = a.bias && part == 0 ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
+    const char* Rz = a.R && part == 0 ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2)
+                                      : nullptr;
     f32x4 bv[TN][4];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
@@ -961,7 +968,7 @@ __global__ __launch_bounds__(NT) void gemm_ln_kernel(cmt_gemm_args a, cmt_ln_arg
 template <int BM, int BN, int S, int AMODE>
 int launch_dma_mode(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.M, BM), tn = a.N / BN;
-    const int64_t nwg = (int64_t)tm * tn * a.batch;
+    const int64_t nwg = (int64_t)tm * tn * a.batch * (a.k_splits > 1 ? a.k_splits : 1);
     // the pair stages carry four tiles: 128 x 128 keeps 2 of them (128 KB), the others 3 or 2
     constexpr int SP = BM * BN >= 128 * 128 ? 2 : (BM * BN >= 128 * 64 ? 2 : 3);
     if (a.w_dtype == CMT_F16P) gemm_dma_kernel<pair_t, BM, BN, SP, AMODE, true><<<(unsigned)nwg, NT, 0, s>>>(a, tm, tn);
@@ -1057,6 +1064,13 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16P,
                 "cmt_gemm: bad w_dtype");
     CMT_REQUIRE(a.w_dtype != CMT_F16P || a.a_dtype == CMT_F16P, "cmt_gemm: split (CMT_F16P) W needs CMT_F16P A");
+    CMT_REQUIRE(a.k_splits <= 1 ||
+                    (a.w_dtype != CMT_F32 && a.a_dtype == a.w_dtype && a.a_mode == CMT_A_ROWS &&
+                     a.c_mode == CMT_C_ROWS && a.c_dtype == CMT_F32 && a.batch == 1 && !a.relu &&
+                     a.plane_max2 == nullptr && a.k_splits <= 64 && (a.K / 64) % a.k_splits == 0 &&
+                     a.c_split_stride >= (int64_t)(a.M - 1) * a.ldc + a.N),
+                "cmt_gemm: split-K needs compute-dtype row A, fp32 row C, batch 1, no relu / plane_max2, "
+                "K / 64 divisible by k_splits and non-overlapping parts");
     CMT_REQUIRE(a.c_dtype != CMT_F16P || a.c_mode == CMT_C_ROWS, "cmt_gemm: a CMT_F16P C must be row mode");
     CMT_REQUIRE(a.a_dtype == CMT_F32 || a.a_dtype == a.w_dtype, "cmt_gemm: A must be f32 or the compute dtype");
     CMT_REQUIRE(a.a_mode != CMT_A_CONV3X3 || a.a_dtype == a.w_dtype,

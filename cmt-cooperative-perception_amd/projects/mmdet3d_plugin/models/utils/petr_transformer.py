@@ -769,9 +769,13 @@ class PETRTransformerDecoder(nn.Module):
         qkv = torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=dev)
         qc = torch.empty((B * C * Nq,), dtype=prec.attn, device=dev)
         ob = op_empty(rows, C, lp, dev)                            # attention output (out-proj operand)
-        t1 = torch.empty((rows, C), dtype=f32, device=dev)
-        t1n = torch.empty_like(t1)
-        o = torch.empty_like(t1)
+        # the N = C out-projection / fc2 GEMMs of the split policy run split-K into KSP fp32
+        # partial blocks of t1 (their 64 x 64 tile grid alone covers under a quarter of the
+        # CUs); the LayerNorm after each sums the blocks
+        KSP = 4 if lp == SPLIT and not use_chain else 1
+        t1 = torch.empty((KSP, rows, C), dtype=f32, device=dev)
+        t1n = torch.empty((rows, C), dtype=f32, device=dev)
+        o = torch.empty_like(t1n)
         FF = pk["layers"][0]["f1_w"].shape[0]
         hf = op_empty(rows, FF, lp, dev)
         ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
@@ -825,8 +829,9 @@ class PETRTransformerDecoder(nn.Module):
                                ln_b=b0, eps=e0, Y=t1n, Yp=tp, P=qpos)
             else:
                 native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt,
-                            ldr=C)
-                native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos)
+                            ldr=C, k_splits=KSP)
+                native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos,
+                                    nparts=KSP)
             # --- cross attention: q = lowp(x + qpos); K/V from the hoisted GEMM
             native.gemm(tp, lw["ca_wq"], qc, M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
                         headsplit_rows=Nq)
@@ -843,8 +848,8 @@ class PETRTransformerDecoder(nn.Module):
                                ln_b=b1, eps=e1, Y=o, Yl=tl)
             else:
                 native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n,
-                            ldr=C)
-                native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl)
+                            ldr=C, k_splits=KSP)
+                native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl, nparts=KSP)
             # --- FFN (fc1 activation written in the compute dtype)
             native.gemm(tl, lw["f1_w"], hf, M=rows, N=FF, K=C, lda=C, ldw=C, ldc=FF, bias=lw["f1_b"], relu=True)
             # --- fc2 + residual + norms.2 -> next query (fp32 + both lowp operands), + post_norm -> out[l]
@@ -855,9 +860,10 @@ class PETRTransformerDecoder(nn.Module):
                                flags2=post_flags, y2_offset=l * rows * C)
             else:
                 native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o,
-                            ldr=C)
+                            ldr=C, k_splits=KSP)
                 native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
-                                    W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
+                                    W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C,
+                                    nparts=KSP)
         if out16 is not None:
             if lp == SPLIT:
                 native.split_rows(out.view(-1, C), out16.view(-1, 2, C))

@@ -27,7 +27,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -46,7 +46,8 @@ class GemmArgs(ctypes.Structure):
                 ("R", _vp), ("ldr", _i64), ("r_bstride", _i64), ("r_dtype", _int),
                 ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int),
                 ("c_mode", _int), ("rows_per_batch", _int), ("relu", _int),
-                ("plane_max2", _vp), ("plane_max_cols", _int)]
+                ("plane_max2", _vp), ("plane_max_cols", _int),
+                ("k_splits", _int), ("c_split_stride", _i64)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -76,7 +77,8 @@ class LnArgs(ctypes.Structure):
                 ("W2", _vp), ("B2", _vp), ("Y2", _vp), ("ldy2", _i64), ("flags2", _int),
                 ("lowp_dtype", _int),
                 ("Yl", _vp), ("ldyl", _i64),
-                ("Yp", _vp), ("ldyp", _i64), ("P", _vp), ("ldp", _i64)]
+                ("Yp", _vp), ("ldyp", _i64), ("P", _vp), ("ldp", _i64),
+                ("nparts", _int), ("part_stride", _i64)]
 
 
 class GemmExArgs(ctypes.Structure):
@@ -265,12 +267,16 @@ def _farr(vals, n):
 def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0, a2_cols=0,
          a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0, bias_bstride=0,
          r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0,
-         plane_max2=None, plane_max_cols=0):
+         plane_max2=None, plane_max_cols=0, k_splits=0):
     """C = act(A W^T + bias) + R with the fused prologue/epilogue of cmt_gemm.
     Offsets are in elements of the respective tensor.  A2 of A's dtype selects
     (replaces A for output columns < a2_cols); an fp32 A2 beside fp32 A is
     added on load.  plane_max2 (fp32 [ceil(M/64), plane_max_cols/32], head-split
-    16-bit C only) receives the per-64-row max squared row norm of each head plane."""
+    16-bit C only) receives the per-64-row max squared row norm of each head plane.
+    k_splits >= 2: C holds k_splits fp32 partial blocks of M * ldc elements whose sum
+    is the output (bias and R in the first); a layernorm_ex(nparts=k_splits) reduces them."""
+    if k_splits > 1 and C.numel() < k_splits * M * ldc:
+        raise RuntimeError("gemm: a split-K C needs k_splits blocks of M * ldc elements")
     g = _gemm_args(A, W, C, M=M, N=N, K=K, lda=lda, ldw=ldw, ldc=ldc, bias=bias, relu=relu, R=R, ldr=ldr, A2=A2,
                    lda2=lda2, a2_cols=a2_cols, a_mode=a_mode, conv=conv, seg_len=seg_len, batch=batch,
                    a_bstride=a_bstride, w_bstride=w_bstride, bias_bstride=bias_bstride, r_bstride=r_bstride,
@@ -281,6 +287,8 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
         if plane_max2.dtype != torch.float32 or plane_max2.numel() < -(-M // PLANE_MAX_ROWS) * (plane_max_cols // 32):
             raise RuntimeError("plane_max2 must be fp32 with ceil(M/64) * plane_max_cols/32 entries")
         g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
+    if k_splits > 1:
+        g.k_splits, g.c_split_stride = k_splits, M * ldc
     _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
 
 
@@ -435,11 +443,16 @@ def layernorm(X, W, Bv, Y, *, rows, C, ldx, ldy, eps=1e-5, flags=0, W2=None, B2=
 
 
 def layernorm_ex(X, W, Bv, *, rows, C, ldx, eps=1e-5, Y=None, ldy=0, flags=0, W2=None, B2=None, Y2=None, ldy2=0,
-                 flags2=0, Yl=None, Yp=None, P=None, y2_offset=0):
+                 flags2=0, Yl=None, Yp=None, P=None, y2_offset=0, nparts=1):
     """LayerNorm with optional second LN (Y2) and compute-dtype copies
-    Yl = lowp(y), Yp = lowp(y + P) (rows of width C, contiguous)."""
+    Yl = lowp(y), Yp = lowp(y + P) (rows of width C, contiguous).  nparts >= 2:
+    the input is the sum of nparts blocks X + p * rows * ldx (a split-K gemm's C)."""
     a = _ln_args(X, W, Bv, rows=rows, C=C, ldx=ldx, eps=eps, Y=Y, ldy=ldy, flags=flags, W2=W2, B2=B2, Y2=Y2,
                  ldy2=ldy2, flags2=flags2, Yl=Yl, Yp=Yp, P=P, y2_offset=y2_offset)
+    if nparts > 1:
+        if X.numel() < nparts * rows * ldx:
+            raise RuntimeError("layernorm_ex: X holds fewer than nparts blocks of rows * ldx")
+        a.nparts, a.part_stride = nparts, rows * ldx
     _check(lib().cmt_layernorm_ex(ctypes.byref(a), _stream()), "cmt_layernorm_ex")
 
 

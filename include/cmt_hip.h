@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 12
+#define CMT_ABI_VERSION 13
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi) (22 significant bits: relative
@@ -119,6 +119,13 @@ typedef struct cmt_gemm_args {
      * (of the stored, rounded values), for n < plane_max_cols; every entry is written
      * (rows >= M count as 0).  Feeds cmt_attn_args.kmax2. */
     float* plane_max2; int plane_max_cols;
+    /* optional split-K (ABI 13): k_splits >= 2 splits the logical K into k_splits equal
+     * parts (K / k_splits % 64 == 0) run by separate workgroups; part s writes its partial
+     * product to C + s * c_split_stride (fp32, row mode, batch 1, no relu), bias and R
+     * are added by part 0 only, so the sum of the parts is the GEMM's output.  For the
+     * decoder's 900-row GEMMs, whose tile grid alone covers a quarter of the CUs; the
+     * LayerNorm after them sums the parts (cmt_ln_args.nparts).  0 or 1: no split. */
+    int k_splits; int64_t c_split_stride;
 } cmt_gemm_args;
 
 int cmt_gemm(const cmt_gemm_args* args, void* stream);
@@ -212,6 +219,9 @@ typedef struct cmt_ln_args {
     int lowp_dtype;
     void* Yl; int64_t ldyl;
     void* Yp; int64_t ldyp; const float* P; int64_t ldp;
+    /* ABI 13: the LayerNorm input is the sum of nparts (>= 1; 0 = 1) row blocks
+     * X + p * part_stride -- the partial products of a split-K cmt_gemm */
+    int nparts; int64_t part_stride;
 } cmt_ln_args;
 int cmt_layernorm_ex(const cmt_ln_args* args, void* stream);
 

@@ -72,6 +72,38 @@ def test_gemm_split_rows(N, dev, M, N_, K):
     assert err * 300 < bf
 
 
+@pytest.mark.parametrize("K,ks", [(256, 4), (1024, 4), (512, 2)])
+def test_gemm_split_k_into_layernorm(N, dev, K, ks):
+    """Split-K pair GEMM (the decoder's out-projections / fc2 at 900 rows): ks fp32
+    partial blocks, bias + residual in the first, summed by layernorm_ex(nparts)."""
+    g = torch.Generator().manual_seed(K + ks)
+    M, C = 900, 256
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(C, K, generator=g) / math.sqrt(K)
+    b = torch.randn(C, generator=g)
+    R = torch.randn(M, C, generator=g)
+    lw, lb = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    t = A.double() @ W.double().t() + b.double() + R.double()
+    part = torch.full((ks, M, C), float("nan"), device=dev)
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), part, M=M, N=C, K=K, lda=K, ldw=K, ldc=C, bias=b.to(dev),
+           R=R.to(dev), ldr=C, k_splits=ks)
+    got = part.cpu().double().sum(0)
+    assert (got - t).abs().max().item() <= _tol(t, K), (got - t).abs().max().item()
+    # part 0 carries bias + R, the others only their K slice
+    kk = K // ks
+    p1 = A[:, kk:2 * kk].double() @ W[:, kk:2 * kk].double().t()
+    assert (part[1].cpu().double() - p1).abs().max().item() <= _tol(p1, kk)
+    y = torch.empty(M, C, device=dev)
+    yl = torch.empty(M, 2, C, dtype=SPLIT, device=dev)
+    N.layernorm_ex(part, lw.to(dev), lb.to(dev), rows=M, C=C, ldx=C, eps=1e-5, Y=y, ldy=C, Yl=yl, nparts=ks)
+    ref = torch.nn.functional.layer_norm(t, (C,), lw.double(), lb.double(), 1e-5)
+    assert (y.cpu().double() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+    assert _same(yl, _pair(y.cpu()))
+    with pytest.raises(RuntimeError):   # relu does not distribute over the parts
+        N.gemm(_pair(A).to(dev), _pair(W).to(dev), part, M=M, N=C, K=K, lda=K, ldw=K, ldc=C, relu=True,
+               k_splits=ks)
+
+
 def test_gemm_split_headsplit_select(N, dev):
     """Q|K columns from A2 (select), V columns from A, head-split f16 / f32 output
     with the key-norm partials (the K/V projection contract)."""
