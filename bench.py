@@ -48,6 +48,7 @@ from projects.mmdet3d_plugin import dp, native, set_precision  # noqa: E402
 from projects.mmdet3d_plugin import synthetic as S  # noqa: E402
 from projects.mmdet3d_plugin.mmcv_custom.ops.voxel import SPConvVoxelization  # noqa: E402
 from projects.mmdet3d_plugin.profiling import region_timer  # noqa: E402
+from projects.mmdet3d_plugin.runtime import OPTIONS  # noqa: E402
 
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}   # dense MFMA, MI355X_MICROARCH.md (no sparsity)
 DTYPE_LABEL = {"bf16": "bf16", "fp16": "fp16",
@@ -379,7 +380,7 @@ def main():
                    "parallelism": f"dp{world}", "graph": not args.no_graph,
                    # pos2embed(BEV grid) + bev_embedding[0] is a function of the weights only: built
                    # once per weight version like the packed weights (CMT_BEV_POS_CACHE=0: per frame)
-                   "bev_pos_hidden_cached": os.environ.get("CMT_BEV_POS_CACHE", "1") != "0",
+                   "bev_pos_hidden_cached": OPTIONS.bev_pos_cache,
                    "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nq=nq, nk=nk) for nk in nks) / 1e9, 2)},
         "roofline": {"kernel": "cmt_attn_fwd (cross-attention core + split combine)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

@@ -712,9 +712,8 @@ extern "C" int cmt_rv_pe_coords(int BV, int h, int w, int D, float pad_h, float 
     PcRange pc;
     for (int i = 0; i < 6; ++i) pc.v[i] = pc_range6[i];
     hipStream_t s = (hipStream_t)stream;
-    const char* vec = getenv("CMT_RVPE_VEC");   // diagnostics: 0 = the one-thread-per-depth kernel
-    if ((odtype == CMT_F16P || !(vec && vec[0] == '0')) && D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) &&
-        (uintptr_t)out % 16 == 0) {
+    // eight depths per thread when D and the output allow it, else one thread per depth
+    if (D % 8 == 0 && (int64_t)BV * h * w * (D / 8) < ((int64_t)1 << 31) && (uintptr_t)out % 16 == 0) {
         const int64_t t8 = (int64_t)BV * h * w * (D / 8);
         if (odtype == CMT_F32)
             rv_pe_coords_kernel8<float><<<nblocks(t8, 256), 256, 0, s>>>(BV, h, w, D, pad_h, pad_w, depth_max - 1.f,

@@ -1109,28 +1109,17 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
         CMT_REQUIRE(a.ldc % 4 == 0 && (a.R == nullptr || a.ldr % 4 == 0) && a.bias_bstride % 4 == 0,
                     "cmt_gemm: ldc/ldr/bias_bstride must be multiples of 4");
         const int64_t big_tiles = (int64_t)(a.N / 128) * cdiv(a.M, 128) * a.batch;
-        // 128 x 128 tiles from ~1.9 workgroups per CU up.  CMT_GEMM_BIG_MIN (diagnostics) moves the
-        // threshold: at 300 the RV query MLP's fc1 (344 tiles) runs 9.9 instead of 12.4 us alone,
-        // but the frame is slower (919 vs 927 frames/s): it runs on the side stream beside the
-        // conv, where the bigger tiles' LDS does not fit
-        static const char* bmin = getenv("CMT_GEMM_BIG_MIN");
-        const int64_t big_min = bmin && bmin[0] ? atoi(bmin) : 480;
-        if (a.N % 128 == 0 && big_tiles >= big_min) {
-            // diagnostics: CMT_GEMM_S128 = LDS stages of the 128 x 128 tile (2, 3 or 4)
-            const char* ov = getenv("CMT_GEMM_S128");
-            const int st = (ov && ov[0] >= '2' && ov[0] <= '4') ? ov[0] - '0' : 2;
-            if (st == 4) return launch_dma<128, 128, 4>(a, s);
-            if (st == 3) return launch_dma<128, 128, 3>(a, s);
-            return launch_dma<128, 128, 2>(a, s);
-        }
+        // 128 x 128 tiles from ~1.9 workgroups per CU up (480 tiles: a lower threshold made the RV
+        // query MLP's fc1 faster alone -- 9.9 vs 12.4 us at 344 tiles -- but the bf16 frame slower,
+        // 919 vs 927 frames/s, beside the conv on the second stream), 2 LDS stages
+        if (a.N % 128 == 0 && big_tiles >= 480) return launch_dma<128, 128, 2>(a, s);
         // long-K problems a 128x128 grid fills less than twice over (the RV embedding's second
         // GEMM, M = 24 000, N = 256, K = 1024: 376 tiles): still 128 x 128 with 2 stages when N
         // allows (26.7 us vs 30.0 us on 128 x 64 x 3 stages, 36.3 on 128 x 128 x 3), else
         // 128 x 64 tiles (3/4 of the 64 x 64 tiles' operand bytes per output)
         const int64_t mid_tiles = (int64_t)(a.N / 64) * cdiv(a.M, 128) * a.batch;
         if (kdiv >= 512 && a.a_mode == CMT_A_ROWS && mid_tiles >= 480) {
-            const char* mid = getenv("CMT_GEMM_MID");   // diagnostics: 0 = the 128 x 64 tiles
-            if (a.N % 128 == 0 && !(mid && mid[0] == '0')) return launch_dma<128, 128, 2>(a, s);
+            if (a.N % 128 == 0) return launch_dma<128, 128, 2>(a, s);
             return launch_dma<128, 64, 3>(a, s);
         }
         return launch_dma<64, 64, 4>(a, s);

@@ -32,7 +32,6 @@ namespace {
 
 constexpr int KP_BM = 128;            // token rows per workgroup
 constexpr int KP_K = 256;             // reduction depth (embed dims)
-constexpr int KP_NT = 256;            // 4 waves
 constexpr int KP_KS = KP_K / 16;      // MFMA k-steps
 constexpr int KP_MAXB = 2048;         // bias floats per column part held in LDS
 
@@ -40,159 +39,6 @@ typedef const __attribute__((address_space(1))) void* kp_gaddr_t;
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* kp_laddr_t;
 template <typename T> using frag_of = typename mfma_traits<T>::frag;
-
-// One head plane of one 64-token half: 32 MFMAs on the fragment set wf (the
-// freed slots refill with plane `nxt`, two planes ahead), then round, stage
-// [token][32] in the wave's LDS slice, key-norm max, and 16-B stores.
-template <typename T, bool MAXQ, int DIAG, bool AF_LDS>
-__device__ __forceinline__ void kv_plane(const cmt_gemm_args& a, char* stg, const float* bw, const T* Wl,
-                                         typename mfma_traits<T>::frag (&wf)[KP_KS],
-                                         const typename mfma_traits<T>::frag (&af)[2][KP_KS], const char* atile,
-                                         int j, int nxt, int plane, int mg, const uint32_t (&soff)[4],
-                                         __amdgpu_buffer_rsrc_t crsrc, __amdgpu_buffer_rsrc_t prsrc, int lane) {
-    typedef T t4 __attribute__((ext_vector_type(4)));
-    const int lr = lane & 31, lh = lane >> 5;
-    const T* Wn = Wl + (int64_t)nxt * (KP_KS * 512);
-    f32x16 acc[2];
-    {
-        // accumulators start at the bias (columns (r & 3) + 8 (r >> 2) + 4 lh)
-        f32x16 b16;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const f32x4 b4 = *(const f32x4*)(bw + 32 * j + 8 * g + 4 * lh);
-            b16[4 * g] = b4[0]; b16[4 * g + 1] = b4[1]; b16[4 * g + 2] = b4[2]; b16[4 * g + 3] = b4[3];
-        }
-        acc[0] = b16;
-        acc[1] = b16;
-    }
-#pragma unroll
-    for (int ks = 0; ks < KP_KS; ++ks) {
-        if constexpr (AF_LDS) {
-            // B fragments of the half's two 32-token tiles straight from the LDS A tile
-            // (atile = row lr of the half; rows 32 apart share the XOR pattern lr & 15)
-            const int sw = ((2 * ks + (lane >> 5)) ^ (lane & 15)) << 4;
-            const frag_of<T> a0 = *(const frag_of<T>*)(atile + sw);
-            const frag_of<T> a1 = *(const frag_of<T>*)(atile + 32 * (KP_K * 2) + sw);
-            acc[0] = mfma_traits<T>::mma(wf[ks], a0, acc[0]);
-            acc[1] = mfma_traits<T>::mma(wf[ks], a1, acc[1]);
-        } else {
-            acc[0] = mfma_traits<T>::mma(wf[ks], af[0][ks], acc[0]);
-            acc[1] = mfma_traits<T>::mma(wf[ks], af[1][ks], acc[1]);
-        }
-        if constexpr ((DIAG & 2) == 0)
-            wf[ks] = *(const frag_of<T>*)(Wn + ks * 512);   // plane `nxt` into the freed slot
-    }
-    float pm = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int tok = 32 * t + lr;
-        float ss = 0.f;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const t4 v = t4{(T)acc[t][4 * g], (T)acc[t][4 * g + 1], (T)acc[t][4 * g + 2], (T)acc[t][4 * g + 3]};
-            const int c0 = 8 * g + 4 * lh;
-            *(t4*)(stg + tok * 64 + ((((c0 >> 3) ^ (tok >> 1)) & 3) << 4) + (c0 & 7) * 2) = v;
-            if (MAXQ) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
-            }
-        }
-        if (MAXQ) {
-            ss = pair_sum(mg + tok < a.M ? ss : 0.f);
-            pm = t ? fmaxf(pm, ss) : ss;
-        }
-    }
-    if (MAXQ) {
-#pragma unroll
-        for (int off = 1; off < 32; off <<= 1) pm = fmaxf(pm, __shfl_xor(pm, off));
-        const int pm_planes = a.plane_max_cols >> 5;
-        const uint32_t po = (lane == 0 && mg < a.M) ? (uint32_t)((((int64_t)(mg >> 6)) * pm_planes + plane) * 4)
-                                                     : 0xffffffffu;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pm), prsrc, po, 0, 0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr ((DIAG & 1) != 0) {   // diagnostics: no output stores (the LDS staging reads stay)
-        f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int tok = 16 * i + (lane >> 2), ch = lane & 3;
-            acc4 += *(const f32x4*)(stg + tok * 64 + (((ch ^ (tok >> 1)) & 3) << 4));
-        }
-        asm volatile("" ::"v"(acc4));
-        return;
-    }
-    const uint32_t pl = (uint32_t)((int64_t)plane * a.rows_per_batch * 64);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int tok = 16 * i + (lane >> 2), ch = lane & 3;
-        const f32x4 v = *(const f32x4*)(stg + tok * 64 + (((ch ^ (tok >> 1)) & 3) << 4));
-        // streamed once (non-temporal): keeps W resident in L2
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), crsrc,
-                                              soff[i] == 0xffffffffu ? soff[i] : soff[i] + pl, 0, 2);
-    }
-}
-
-// The two 64-token halves x this wave's planes (an even count); MAXQ = this
-// part's planes all feed the key-norm maxima.  Every global access in the loop
-// is unconditional (stores masked by the buffer range check, not branches), so
-// the compiler counts the in-order vm counter exactly.  W fragments are
-// fetched TWO planes ahead into two alternating sets: a load issued after a
-// plane's stores completes only after those stores do (one counter, in
-// order), so one plane of distance exposed the HBM store latency every plane.
-template <typename T, bool MAXQ, int DIAG, bool AF_LDS>
-__device__ __forceinline__ void kv_sweep(const cmt_gemm_args& a, const char* lds, char* stg, const float* bw,
-                                         const T* Wl, typename mfma_traits<T>::frag (&wa)[KP_KS],
-                                         typename mfma_traits<T>::frag (&wb)[KP_KS], int nplanes, int plane0,
-                                         int m0, int lane) {
-    typedef typename mfma_traits<T>::frag frag;
-    const int lr = lane & 31, lh = lane >> 5;
-    const uint32_t cbytes = (uint32_t)((int64_t)a.M * a.N * 2);
-    const auto crsrc = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, cbytes, 0x00020000);
-    const uint32_t pmbytes = MAXQ ? (uint32_t)(((a.M + 63) / 64) * (a.plane_max_cols >> 5) * 4) : 0u;
-    const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(MAXQ ? (void*)a.plane_max2 : a.C, 0, pmbytes, 0x00020000);
-    const int rpb = a.rows_per_batch;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        // B fragments of this half's 64 tokens: [token tile][k-step]
-        frag af[2][KP_KS];
-        const char* atile = lds + (64 * half + lr) * (KP_K * 2);
-        if constexpr (!AF_LDS) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int ks = 0; ks < KP_KS; ++ks)
-                    af[t][ks] = *(const frag*)(lds + (64 * half + 32 * t + lr) * (KP_K * 2) +
-                                               (((2 * ks + lh) ^ (lr & 15)) << 4));
-        }
-        // byte offsets of this lane's 4 store rows (tokens 16 i + lane / 4, chunk lane & 3), plane 0
-        uint32_t soff[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = m0 + 64 * half + 16 * i + (lane >> 2);
-            const int bb = m / rpb;
-            const int64_t row = (int64_t)bb * (a.N >> 5) * rpb + (m - bb * rpb);
-            soff[i] = m < a.M ? (uint32_t)((row * 32 + 8 * (lane & 3)) * 2) : 0xffffffffu;
-        }
-        const int mg = m0 + 64 * half;                   // this half's 64-row key-norm group
-        if constexpr (AF_LDS) {
-            // two waves per SIMD: one W set, refilled with the next plane (wrapping to the
-            // next half's first) while this one's MFMAs run; the partner wave hides the rest
-            for (int j = 0; j < nplanes; ++j) {
-                const int n1 = j + 1 < nplanes ? j + 1 : 0;
-                kv_plane<T, MAXQ, DIAG, AF_LDS>(a, stg, bw, Wl, wa, af, atile, j, n1, plane0 + j, mg, soff, crsrc,
-                                                prsrc, lane);
-            }
-            continue;
-        }
-        for (int j = 0; j < nplanes; j += 2) {
-            const int n0 = j + 2 < nplanes ? j + 2 : j + 2 - nplanes;   // wraps to the next half's first two
-            kv_plane<T, MAXQ, DIAG, AF_LDS>(a, stg, bw, Wl, wa, af, atile, j, n0, plane0 + j, mg, soff, crsrc, prsrc,
-                                            lane);
-            kv_plane<T, MAXQ, DIAG, AF_LDS>(a, stg, bw, Wl, wb, af, atile, j + 1, n0 + 1, plane0 + j + 1, mg, soff,
-                                            crsrc, prsrc, lane);
-        }
-    }
-}
 
 // Whole 128-token tile per W fetch (8-wave form): the plane's W fragments
 // serve all four 32-token tiles, so each workgroup fetches its columns' W
@@ -298,15 +144,14 @@ __device__ __forceinline__ void kv_sweep_full(const cmt_gemm_args& a, const char
     }
 }
 
-// NW = 4: one wave per SIMD, each wave holds its half's A fragments in
-// registers.  NW = 8: two waves per SIMD (one's epilogue -- rounding, LDS
-// staging, key-norm max, stores -- runs beside the other's MFMAs), A fragments
-// read from the LDS tile per k-step so a wave fits in 256 registers.
-template <typename T, int DIAG = 0, int NW = 4, bool FULL = false>
-__global__ __launch_bounds__(64 * NW, 1) void kvproj_kernel(cmt_gemm_args a, int parts) {
+// 8 waves, two per SIMD (one's epilogue -- rounding, LDS staging, key-norm max,
+// stores -- runs beside the other's MFMAs); A fragments are read from the LDS
+// tile per k-step so a wave fits in 256 registers.
+template <typename T>
+__global__ __launch_bounds__(512, 1) void kvproj_kernel(cmt_gemm_args a, int parts) {
     typedef typename mfma_traits<T>::frag frag;
-    constexpr int NTH = 64 * NW;
-    constexpr int STG = FULL ? 8192 : 4096;   // per-wave store staging bytes
+    constexpr int NW = 8, NTH = 64 * NW;
+    constexpr int STG = 8192;   // per-wave store staging bytes
     // 64 KB A tile | NW x STG per-wave store staging | the part's bias (<= 8 KB)
     __shared__ __attribute__((aligned(16))) char lds[KP_BM * KP_K * 2 + NW * STG + KP_MAXB * 4];
 
@@ -344,34 +189,26 @@ __global__ __launch_bounds__(64 * NW, 1) void kvproj_kernel(cmt_gemm_args a, int
         else
             *(f32x4*)(bsm + 4 * piece) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const int planes_w = ncols / 32 / NW;               // head planes per wave (even)
+    const int planes_w = ncols / 32 / NW;               // head planes per wave
     const int plane0 = (n_part >> 5) + wave * planes_w;
     const T* W = (const T*)a.W;
     // W in the fragment-packed layout (cmt_hip.h cmt_kv_proj): plane p, k-step ks
     // is 1 KB contiguous, lane-major -- every W load instruction touches 8 lines
     const T* Wl = W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
-    frag wa[KP_KS], wb[KP_KS];   // planes 0 and 1 (two planes of prefetch distance; NW = 8: plane 0 only)
+    frag wa[KP_KS];   // the current plane; each slot refills with the next plane once used
 #pragma unroll
-    for (int ks = 0; ks < KP_KS; ++ks) {
-        wa[ks] = *(const frag*)(Wl + ks * 512);
-        if constexpr (NW == 4) wb[ks] = *(const frag*)(Wl + KP_KS * 512 + ks * 512);
-    }
+    for (int ks = 0; ks < KP_KS; ++ks) wa[ks] = *(const frag*)(Wl + ks * 512);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_mem();
 
-    char* stg = lds + KP_BM * KP_K * 2 + wave * STG;    // [64 or 128 tokens][32] 16-bit
+    char* stg = lds + KP_BM * KP_K * 2 + wave * STG;    // [128 tokens][32] 16-bit
     const float* bw = bsm + 32 * (plane0 - (n_part >> 5));
 
     // output stores: rows >= M (and non-writer lanes of the key-norm max) get an
     // out-of-range offset and the buffer range check drops them -- no branches
     const bool maxq = a.plane_max2 != nullptr && n_part < a.plane_max_cols;
-    if constexpr (FULL) {
-        if (maxq) kv_sweep_full<T, true>(a, lds, stg, bw, Wl, wa, planes_w, plane0, m0, lane);
-        else kv_sweep_full<T, false>(a, lds, stg, bw, Wl, wa, planes_w, plane0, m0, lane);
-    } else {
-        if (maxq) kv_sweep<T, true, DIAG, (NW > 4)>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
-        else kv_sweep<T, false, DIAG, (NW > 4)>(a, lds, stg, bw, Wl, wa, wb, planes_w, plane0, m0, lane);
-    }
+    if (maxq) kv_sweep_full<T, true>(a, lds, stg, bw, Wl, wa, planes_w, plane0, m0, lane);
+    else kv_sweep_full<T, false>(a, lds, stg, bw, Wl, wa, planes_w, plane0, m0, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -512,12 +349,8 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
 extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_kv_proj: null args");
     const cmt_gemm_args& a = *ap;
-    // column parts per 128-token tile: 2 (K half | V half) or, CMT_KVPROJ_PARTS=4, quarters --
-    // twice the workgroups (1764 instead of 882 at the fusion shape: a fuller last round on 256
-    // CUs) for twice the A-tile reads
-    const char* pv = getenv("CMT_KVPROJ_PARTS");
-    const int pmul = (pv && pv[0] == '4' && a.A2 && (a.N / 4 / 32) % 8 == 0) ? 2 : 1;
-    const int parts = (a.A2 ? 2 : 1) * pmul;
+    // column parts per 128-token tile: the K half (A2 = lowp(mem + pos)) and the V half (A)
+    const int parts = a.A2 ? 2 : 1;
     if (a.w_dtype == CMT_F16P) {
         // split (fp32-accurate) form: f16 pair A / A2 rows, W_hi then W_lo fragment-packed, f16 / bf16 C
         CMT_REQUIRE(a.a_dtype == CMT_F16P && (a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16),
@@ -526,19 +359,18 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                         a.c_mode == CMT_C_HEADSPLIT && a.R == nullptr && !a.relu && a.rows_per_batch > 0 &&
                         a.M % a.rows_per_batch == 0,
                     "cmt_kv_proj: row A, K = 256, head-split C, no residual / relu, batch 1");
-        const int parts3 = a.A2 ? 2 : 1;
-        CMT_REQUIRE(a.N % (256 * parts3) == 0, "cmt_kv_proj: N must be a multiple of 256 per column part");
+        CMT_REQUIRE(a.N % (256 * parts) == 0, "cmt_kv_proj: N must be a multiple of 256 per column part");
         CMT_REQUIRE(a.A2 == nullptr || (a.a2_mode == CMT_A2_SELECT && a.a2_cols * 2 == a.N),
                     "cmt_kv_proj: A2 selects the first half of the columns");
-        CMT_REQUIRE(a.plane_max2 == nullptr || (a.plane_max_cols % (a.N / parts3) == 0 && a.plane_max_cols <= a.N),
+        CMT_REQUIRE(a.plane_max2 == nullptr || (a.plane_max_cols % (a.N / parts) == 0 && a.plane_max_cols <= a.N),
                     "cmt_kv_proj: plane_max_cols must be a multiple of the column part (N / parts) <= N");
         CMT_REQUIRE(a.lda % 8 == 0 && (a.A2 == nullptr || a.lda2 % 8 == 0) &&
                         ((uintptr_t)a.A | (uintptr_t)a.W | (uintptr_t)a.C | (uintptr_t)a.A2) % 16 == 0,
                     "cmt_kv_proj: 16-byte aligned operands");
-        const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts3);
+        const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts);
         hipStream_t s3 = (hipStream_t)stream;
-        if (a.c_dtype == CMT_F16) kvproj_x3_kernel<f16_t><<<g3, 512, 0, s3>>>(a, parts3);
-        else kvproj_x3_kernel<bf16_t><<<g3, 512, 0, s3>>>(a, parts3);
+        if (a.c_dtype == CMT_F16) kvproj_x3_kernel<f16_t><<<g3, 512, 0, s3>>>(a, parts);
+        else kvproj_x3_kernel<bf16_t><<<g3, 512, 0, s3>>>(a, parts);
         return cmt_check_launch("cmt_kv_proj");
     }
     CMT_REQUIRE(a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16, "cmt_kv_proj: w_dtype must be f16 or bf16");
@@ -558,31 +390,7 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                                     (uintptr_t)a.bias) % 16 == 0, "cmt_kv_proj: 16-byte aligned operands");
     hipStream_t s = (hipStream_t)stream;
     const unsigned grid = (unsigned)(cdiv(a.M, KP_BM) * parts);
-    // diagnostics (CMT_KVPROJ_DIAG, bf16): 1 = no output stores, 2 = no W re-fetch, 3 = neither
-    const char* dg = getenv("CMT_KVPROJ_DIAG");
-    const int diag = (dg && dg[0] >= '1' && dg[0] <= '3') ? dg[0] - '0' : 0;
-    // 8-wave form when every wave gets an even number of head planes (CMT_KVPROJ_NW=4 forces the 4-wave form)
-    const char* nw = getenv("CMT_KVPROJ_NW");
-    // 8-wave form: whole 128-token tile per W fetch unless CMT_KVPROJ_FULL=0 (two 64-token halves)
-    const char* fu = getenv("CMT_KVPROJ_FULL");
-    const bool full = !(fu && fu[0] == '0');
-    // the two-half sweep needs an even plane count per wave, the full sweep any count
-    const bool w8 = !(nw && nw[0] == '4') && (a.N / parts / 32) % (full ? 8 : 16) == 0;
-    CMT_REQUIRE(pmul == 1 || (w8 && full && diag == 0), "cmt_kv_proj: CMT_KVPROJ_PARTS=4 needs the 8-wave full sweep");
-    if (w8 && diag == 0) {
-        if (full) {
-            if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t, 0, 8, true><<<grid, 512, 0, s>>>(a, parts);
-            else kvproj_kernel<f16_t, 0, 8, true><<<grid, 512, 0, s>>>(a, parts);
-        } else {
-            if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t, 0, 8><<<grid, 512, 0, s>>>(a, parts);
-            else kvproj_kernel<f16_t, 0, 8><<<grid, 512, 0, s>>>(a, parts);
-        }
-        return cmt_check_launch("cmt_kv_proj");
-    }
-    if (a.w_dtype == CMT_BF16 && diag == 1) kvproj_kernel<bf16_t, 1><<<grid, KP_NT, 0, s>>>(a, parts);
-    else if (a.w_dtype == CMT_BF16 && diag == 2) kvproj_kernel<bf16_t, 2><<<grid, KP_NT, 0, s>>>(a, parts);
-    else if (a.w_dtype == CMT_BF16 && diag == 3) kvproj_kernel<bf16_t, 3><<<grid, KP_NT, 0, s>>>(a, parts);
-    else if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t><<<grid, KP_NT, 0, s>>>(a, parts);
-    else kvproj_kernel<f16_t><<<grid, KP_NT, 0, s>>>(a, parts);
+    if (a.w_dtype == CMT_BF16) kvproj_kernel<bf16_t><<<grid, 512, 0, s>>>(a, parts);
+    else kvproj_kernel<f16_t><<<grid, 512, 0, s>>>(a, parts);
     return cmt_check_launch("cmt_kv_proj");
 }

@@ -37,7 +37,6 @@
 
 #include <cstdio>
 #include <cstdlib>
-#include <vector>
 
 namespace {
 
@@ -266,36 +265,10 @@ __device__ __forceinline__ void store_tile(float* M, int rb, int wave, int lane,
         *(f32x4*)(p + j * 256) = f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
 }
 
-// diagnostics build (CMT_CHAIN_STAMP=1): shader-clock stamps of wave 0 at the
-// phase boundaries, written to a buffer no other code reads
-__device__ __forceinline__ unsigned long long rc_stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-constexpr int kChainStamps = 8;
-
 // KIND is compile-time: each chain kind gets its own register allocation (chain A's two
 // register-streamed weight sets would otherwise be live in every kind's code)
-template <typename T, int KIND, bool STAMP = false>
-__global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigned long long* stamps) {
-    unsigned long long t0 = 0, ts[kChainStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int ns = 0;
-    if constexpr (STAMP) t0 = rc_stamp();
-    auto mark = [&]() {
-        if constexpr (STAMP) {
-            if (ns < kChainStamps) ts[ns] = rc_stamp() - t0;
-            ++ns;
-        }
-    };
-    auto flush = [&]() {
-        if constexpr (STAMP) {
-            if (threadIdx.x == 0)
-                for (int j = 0; j < kChainStamps; ++j) stamps[(int64_t)blockIdx.x * kChainStamps + j] = ts[j];
-        }
-    };
+template <typename T, int KIND>
+__global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
     typedef T t4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) char lds[LDS_TOTAL];
     Eng<T> e;
@@ -397,7 +370,6 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
                  "v"(oold[VPL - 1]));
     rc_wait<0>();
     barrier_mem();
-    mark();   // 0: prologue landed
 
     f32x16 acc;
     float v[VPL];
@@ -408,14 +380,12 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
             if (wo_regs) e.sub_gemm_regs(actA, wr0, acc);              // out_proj (register weights)
             else e.sub_gemm(actA, acc, true);                          // out_proj (LDS weight ring)
         }
-        mark();   // 1
         {
             const float* bo = e.prm();
 #pragma unroll
             for (int r = 0; r < VPL; ++r) v[r] = acc[r] + bo[e.col(r)] + res[r];
         }
         e.layernorm(v, 256, 512, eps);                                 // norms[0]
-        mark();   // 2
         float y[VPL];
 #pragma unroll
         for (int i = 0; i < VPL; ++i) {
@@ -424,7 +394,6 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
         }
         e.put_act(actB, v);                                            // lowp(y + query_pos)
         e.sub_gemm_regs(actB, wr, acc);                                // cross-attn Q projection
-        mark();   // 3
         const float* bq = e.prm() + 768;
         t4 qo[4];
 #pragma unroll
@@ -442,15 +411,12 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
                 *(t4*)((T*)a.Q + (((int64_t)b * 8 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) = qo[gg];
             }
         }
-        mark();   // 4: stores issued
-        flush();
         return;
     }
 
     if (kind == 1) {
         // ---------------- chain B1: out_proj + norms[1], then FFN quarter g
         e.sub_gemm(actA, acc, true);                                   // out_proj
-        mark();   // 1
         {
             const float* bo = e.prm();
 #pragma unroll
@@ -458,9 +424,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
         }
         e.layernorm(v, 256, 512, eps);                                 // norms[1] -> o (FFN residual)
         e.put_act(actB, v);                                            // lowp(o): fc1 operand
-        mark();   // 2
         e.sub_gemm(actB, acc, true);                                   // fc1 rows [256g, 256g + 256)
-        mark();   // 3
         {
             const float* b1 = e.prm() + 768 + 256 * g;
             float h[VPL];
@@ -469,7 +433,6 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
             e.put_act(actA, h);                                        // hidden quarter g = fc2 K block g
         }
         e.sub_gemm_regs(actA, wr, acc);                                // fc2 partial over K block g
-        mark();   // 4
         const float* b2 = e.prm() + 1792;
 #pragma unroll
         for (int r = 0; r < VPL; ++r) {
@@ -478,8 +441,6 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
             v[r] = x;
         }
         store_tile(ws + g * plane, rb, e.wave, e.lane, v);             // whole row block (clamped rows too)
-        mark();   // 5
-        flush();
         return;
     }
 
@@ -487,7 +448,6 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
 #pragma unroll
     for (int i = 0; i < VPL; ++i) v[i] = res[i];
     e.layernorm(v, 2048, 2304, eps);                                   // norms[2] -> next query
-    mark();   // 1
     float y[VPL];
 #pragma unroll
     for (int i = 0; i < VPL; ++i) y[i] = v[i];
@@ -507,9 +467,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
 #pragma unroll
         for (int i = 0; i < VPL; ++i) u[i] = y[i] + qp[i];             // qp = 0 for the V block
         e.put_act(actA, u);                                            // lowp(y + pos) (Q|K) / lowp(y) (V)
-        mark();   // 2
         e.sub_gemm_regs(actA, wr, acc);
-        mark();   // 3
         const float* bqkv = e.prm() + 3072 + g * CE;
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
@@ -538,38 +496,6 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a, unsigne
             }
         }
     }
-    mark();   // 4: stores issued
-    flush();
-}
-
-// CMT_CHAIN_STAMP=1: run the stamped build and print the mean phase times (shader clock,
-// since entry, wave 0) per chain kind to stderr
-unsigned long long* chain_stamp_buffer(unsigned grid) {
-    static const char* ov = getenv("CMT_CHAIN_STAMP");
-    if (!(ov && ov[0] == '1')) return nullptr;
-    static unsigned long long* buf = nullptr;
-    static size_t cap = 0;
-    const size_t need = (size_t)grid * kChainStamps * sizeof(unsigned long long);
-    if (need > cap) {
-        if (buf) (void)hipFree(buf);
-        if (hipMalloc(&buf, need) != hipSuccess) return nullptr;
-        cap = need;
-    }
-    (void)hipMemset(buf, 0, need);
-    return buf;
-}
-
-void chain_stamp_report(int kind, unsigned grid, const unsigned long long* dbuf, hipStream_t s) {
-    std::vector<unsigned long long> h((size_t)grid * kChainStamps);
-    if (hipStreamSynchronize(s) != hipSuccess ||
-        hipMemcpy(h.data(), dbuf, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-        return;
-    double m[kChainStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (unsigned w = 0; w < grid; ++w)
-        for (int j = 0; j < kChainStamps; ++j) m[j] += (double)h[(size_t)w * kChainStamps + j] / grid;
-    fprintf(stderr, "chain stamp kind %d (%u workgroups):", kind, grid);
-    for (int j = 0; j < kChainStamps && m[j] > 0; ++j) fprintf(stderr, " %.0f", m[j]);
-    fprintf(stderr, "\n");
 }
 
 }  // namespace
@@ -596,22 +522,14 @@ extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
-    unsigned long long* st = chain_stamp_buffer(grid);
-#define CHAIN_LAUNCH(T, STAMPED, BUF)                                                  \
-    do {                                                                               \
-        if (a.kind == 0) chain_kernel<T, 0, STAMPED><<<grid, NTC, 0, s>>>(a, BUF);     \
-        else if (a.kind == 1) chain_kernel<T, 1, STAMPED><<<grid, NTC, 0, s>>>(a, BUF); \
-        else chain_kernel<T, 2, STAMPED><<<grid, NTC, 0, s>>>(a, BUF);                 \
+#define CHAIN_LAUNCH(T)                                                    \
+    do {                                                                   \
+        if (a.kind == 0) chain_kernel<T, 0><<<grid, NTC, 0, s>>>(a);       \
+        else if (a.kind == 1) chain_kernel<T, 1><<<grid, NTC, 0, s>>>(a);  \
+        else chain_kernel<T, 2><<<grid, NTC, 0, s>>>(a);                   \
     } while (0)
-    if (st) {
-        if (a.dtype == CMT_BF16) CHAIN_LAUNCH(bf16_t, true, st);
-        else CHAIN_LAUNCH(f16_t, true, st);
-        const int rc = cmt_check_launch("cmt_chain");
-        if (rc == 0) chain_stamp_report(a.kind, grid, st, s);
-        return rc;
-    }
-    if (a.dtype == CMT_BF16) CHAIN_LAUNCH(bf16_t, false, nullptr);
-    else CHAIN_LAUNCH(f16_t, false, nullptr);
+    if (a.dtype == CMT_BF16) CHAIN_LAUNCH(bf16_t);
+    else CHAIN_LAUNCH(f16_t);
 #undef CHAIN_LAUNCH
     return cmt_check_launch("cmt_chain");
 }

@@ -24,13 +24,12 @@ The reference computes the BEV positional encoding, the coordinate encodings
 and every layer's K/V projection again on each forward; so does this engine
 (no output caching across frames).
 """
-import os
 
 import numpy as np
 import torch
 
 from ... import native
-from ...runtime import get_precision, op_empty
+from ...runtime import OPTIONS, get_precision, op_empty
 from ..utils.packing import to_dtype
 
 __all__ = ["HeadEngineMixin"]
@@ -142,7 +141,7 @@ class HeadEngineMixin:
         # A function of the weights and the grid only: kept like a weight pack (rebuilt when
         # bev_embedding[0] changes, Tensor._version / storage tracked) unless CMT_BEV_POS_CACHE=0.
         # Never built inside a graph capture (its buffer must outlive the graph).
-        if os.environ.get("CMT_BEV_POS_CACHE", "1") == "0":
+        if not OPTIONS.bev_pos_cache:
             return build()
         key = (H, W, x_size, y_size, str(w0.dtype))
         name = f"bev_hidden_{H}x{W}_{w0.dtype}"
@@ -217,7 +216,7 @@ class HeadEngineMixin:
             qb = torch.empty((Nq, C), dtype=torch.float32, device=ref.device)
             self._mlp(pe, pk["bev"], qb, M=Nq)
             return qb
-        if os.environ.get("CMT_BEV_POS_CACHE", "1") == "0":
+        if not OPTIONS.bev_pos_cache:
             return build()
         be = self.bev_embedding
         src = [self.reference_points.weight, be[0].weight, be[0].bias, be[2].weight, be[2].bias]
@@ -345,7 +344,7 @@ class HeadEngineMixin:
 
     def _side_stream(self, dev):
         """The head's second HIP stream on ``dev`` (CMT_SIDE_STREAM=0: none)."""
-        if dev.type != "cuda" or os.environ.get("CMT_SIDE_STREAM", "1") == "0":
+        if dev.type != "cuda" or not OPTIONS.side_stream:
             return None
         pool = self.__dict__.setdefault("_side_streams", {})
         if dev not in pool:

@@ -20,7 +20,6 @@ Two execution paths:
 """
 import copy
 import math
-import os
 import warnings
 
 import torch
@@ -31,7 +30,7 @@ from ... import native
 from ...registry import (ATTENTION, FEEDFORWARD_NETWORK, TRANSFORMER_LAYER, TRANSFORMER_LAYER_SEQUENCE,
                          build_from_cfg)
 from ...profiling import timed
-from ...runtime import SPLIT, get_precision, op_empty
+from ...runtime import OPTIONS, SPLIT, get_precision, op_empty
 from .attention import FlashMHA, project_attend_project
 from .packing import PackCache, to_dtype
 
@@ -645,7 +644,7 @@ class PETRTransformerDecoder(nn.Module):
         on the query embedding and can run beside the memory-side work."""
         prec = get_precision(prec)
         return (prec.gemm in (torch.float16, torch.bfloat16) and self.fused_supported() and self._chain_ok()
-                and os.environ.get("CMT_CHAIN", "1") != "0")
+                and OPTIONS.chain)
 
     def lowp_state(self, *, B, Nk, Nq, prec, device):
         """Working buffers of one lowp chain-path decoder run (allocated on the
@@ -736,7 +735,7 @@ class PETRTransformerDecoder(nn.Module):
         kmax2 = None
         if prec.attn in (torch.bfloat16, torch.float16):
             kmax2 = torch.empty((-(-B * Nk // native.PLANE_MAX_ROWS), L * H), dtype=f32, device=dev)
-        if pk["kv_wp"] is not None and memb.dtype == pk["kv_wp"].dtype and os.environ.get("CMT_KVPROJ", "1") != "0":
+        if pk["kv_wp"] is not None and memb.dtype == pk["kv_wp"].dtype:
             native.kv_proj(memb, pk["kv_wp"], kv, M=B * Nk, N=2 * L * C, bias=pk["kv_b"], A2=mposb,
                            headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
         else:
@@ -745,7 +744,7 @@ class PETRTransformerDecoder(nn.Module):
         # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114).
         # The chains never read the layer-0 target (chain A's residual is None), so there
         # it is only an output buffer and the first operands come from add_cast's zeros.
-        use_chain = self._chain_ok() and lp != SPLIT and os.environ.get("CMT_CHAIN", "1") != "0"
+        use_chain = self._chain_ok() and lp != SPLIT and OPTIONS.chain
         if use_chain and tgt0 is None:
             st = state if state is not None else self.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
             if not st["layer0_done"]:
@@ -813,8 +812,6 @@ class PETRTransformerDecoder(nn.Module):
                              Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
                              Q=qkv if nxt is not None else None, WS=cws, OUT16=out16)
             return out
-        # out-projection / fc2 GEMMs fused with their residual + LayerNorm (cmt_gemm_ln)
-        fuse_ln = C == 256 and os.environ.get("CMT_GEMM_LN", "0") == "1"
         for l, lw in enumerate(pk["layers"]):
             # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
             native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
@@ -824,14 +821,9 @@ class PETRTransformerDecoder(nn.Module):
                              v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
                              o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
             w0, b0, e0 = lw["norms"][0]
-            if fuse_ln:
-                native.gemm_ln(ob, lw["sa_ow"], M=rows, K=C, lda=C, ldw=C, bias=lw["sa_ob"], R=tgt, ldr=C, ln_w=w0,
-                               ln_b=b0, eps=e0, Y=t1n, Yp=tp, P=qpos)
-            else:
-                native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt,
-                            ldr=C, k_splits=KSP)
-                native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos,
-                                    nparts=KSP)
+            native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt,
+                        ldr=C, k_splits=KSP)
+            native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos, nparts=KSP)
             # --- cross attention: q = lowp(x + qpos); K/V from the hoisted GEMM
             native.gemm(tp, lw["ca_wq"], qc, M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
                         headsplit_rows=Nq)
@@ -843,27 +835,18 @@ class PETRTransformerDecoder(nn.Module):
                                  round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2, kmax_ld=L * H,
                                  kmax_plane0=l * H)
             w1, b1, e1 = lw["norms"][1]
-            if fuse_ln:
-                native.gemm_ln(ob, lw["ca_ow"], M=rows, K=C, lda=C, ldw=C, bias=lw["ca_ob"], R=t1n, ldr=C, ln_w=w1,
-                               ln_b=b1, eps=e1, Y=o, Yl=tl)
-            else:
-                native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n,
-                            ldr=C, k_splits=KSP)
-                native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl, nparts=KSP)
+            native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n,
+                        ldr=C, k_splits=KSP)
+            native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl, nparts=KSP)
             # --- FFN (fc1 activation written in the compute dtype)
             native.gemm(tl, lw["f1_w"], hf, M=rows, N=FF, K=C, lda=C, ldw=C, ldc=FF, bias=lw["f1_b"], relu=True)
             # --- fc2 + residual + norms.2 -> next query (fp32 + both lowp operands), + post_norm -> out[l]
             w2, b2, e2 = lw["norms"][2]
-            if fuse_ln:
-                native.gemm_ln(hf, lw["f2_w"], M=rows, K=FF, lda=FF, ldw=FF, bias=lw["f2_b"], R=o, ldr=C, ln_w=w2,
-                               ln_b=b2, eps=e2, Y=tgt, Yl=tl, Yp=tp, P=qpos, W2=pw, B2=pb, Y2=out,
-                               flags2=post_flags, y2_offset=l * rows * C)
-            else:
-                native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o,
-                            ldr=C, k_splits=KSP)
-                native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
-                                    W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C,
-                                    nparts=KSP)
+            native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o,
+                        ldr=C, k_splits=KSP)
+            native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
+                                W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C,
+                                nparts=KSP)
         if out16 is not None:
             if lp == SPLIT:
                 native.split_rows(out.view(-1, C), out16.view(-1, 2, C))

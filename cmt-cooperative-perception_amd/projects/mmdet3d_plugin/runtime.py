@@ -25,12 +25,14 @@ producer of each GEMM operand writes it in the policy's operand format, and
 K/V/Q for the attention kernels are written by the projection epilogue in the
 attention dtype.
 """
+import contextlib
 import os
 from dataclasses import dataclass
 
 import torch
 
-__all__ = ["Precision", "get_precision", "set_precision", "PRECISIONS", "SPLIT", "op_empty", "is_split"]
+__all__ = ["Precision", "get_precision", "set_precision", "PRECISIONS", "SPLIT", "op_empty", "is_split",
+           "Options", "OPTIONS", "options"]
 
 # Storage dtype of a split operand: 16-bit words, a tensor of logical shape
 # [..., C] stored as [..., 2, C] (the C f16 hi values, then the C f16 lo values).
@@ -81,3 +83,37 @@ def set_precision(name):
     global _current
     _current = PRECISIONS[name] if isinstance(name, str) else name
     return _current
+
+
+@dataclass
+class Options:
+    """Path selections of the head, read ONCE from the environment when this
+    module is imported (``options()`` overrides them for a block of code).
+    Each selects between two paths that produce the same outputs and that the
+    GPU tests run both of."""
+    side_stream: bool      # CMT_SIDE_STREAM=0: everything on the caller's stream
+    chain: bool            # CMT_CHAIN=0: f16/bf16 decoder as separate GEMM / LayerNorm launches
+    bev_pos_cache: bool    # CMT_BEV_POS_CACHE=0: rebuild the BEV position-MLP hidden rows per call
+
+
+def _env_on(name):
+    return os.environ.get(name, "1") != "0"
+
+
+OPTIONS = Options(side_stream=_env_on("CMT_SIDE_STREAM"), chain=_env_on("CMT_CHAIN"),
+                  bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"))
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """Temporarily override fields of OPTIONS: ``with options(side_stream=False): ...``."""
+    old = {k: getattr(OPTIONS, k) for k in kw}
+    for k, v in kw.items():
+        if not hasattr(OPTIONS, k):
+            raise AttributeError(f"unknown option {k}")
+        setattr(OPTIONS, k, bool(v))
+    try:
+        yield OPTIONS
+    finally:
+        for k, v in old.items():
+            setattr(OPTIONS, k, v)

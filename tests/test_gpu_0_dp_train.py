@@ -68,7 +68,10 @@ def _worker(rank, world, port, q):
                               for i, p in enumerate(tr.fp.params)]
         tr.backward(loss())
         nb = tr.buckets.finish()
-        q.put((rank, w0, local, tr.fp.grad.detach().cpu().clone(), nb, len(tr.buckets.buckets)))
+        # numpy arrays travel by value (a torch CPU tensor would travel as a shared-memory fd that
+        # the parent can only open while this process is still alive)
+        q.put((rank, w0.numpy(), local.numpy(), tr.fp.grad.detach().cpu().numpy().copy(), nb,
+               len(tr.buckets.buckets)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -87,6 +90,7 @@ def test_head_dp_step_world2_gloo():
     for p in ps:
         p.join(timeout=120)
         assert p.exitcode == 0
+    res = [tuple(torch.from_numpy(x) if hasattr(x, "dtype") else x for x in r) for r in res]
     (_, w0a, la, ra, nb, nbk), (_, w0b, lb, rb, _, _) = res
     assert torch.equal(w0a, w0b), "rank 0's parameters were not broadcast"
     assert nb == nbk and nbk > 1, (nb, nbk)

@@ -26,6 +26,8 @@ center/height normalised by the point-cloud range extent
 import pytest
 import torch
 
+from projects.mmdet3d_plugin.runtime import options
+
 pytestmark = pytest.mark.gpu
 
 KEYS = ("center", "height", "dim", "rot", "vel", "cls_logits")
@@ -288,7 +290,7 @@ def test_graph_replay_with_new_metas(dev, prec, coop):
 
 
 @pytest.mark.parametrize("warm", ["ref", "none"])
-def test_second_stream_matches_single_stream(dev, warm, monkeypatch):
+def test_second_stream_matches_single_stream(dev, warm):
     """The two-stream schedule (query side + layer 0 self block and the encoder
     MLP halves on a second stream) gives bit-identical outputs to the
     single-stream schedule, including on the first low-precision forward of a
@@ -305,9 +307,8 @@ def test_second_stream_matches_single_stream(dev, warm, monkeypatch):
     metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=33)
 
     def run(side):
-        monkeypatch.setenv("CMT_SIDE_STREAM", side)
         torch.empty(64 << 20, dtype=torch.uint8, device=dev).fill_(0xFF)   # NaN-poison the allocator's cache
-        with torch.no_grad():
+        with torch.no_grad(), options(side_stream=side == "1"):
             out = head([x], [xi], metas)[0][0]
         torch.cuda.synchronize()
         return {k: v.clone() for k, v in out.items()}
@@ -326,7 +327,37 @@ def test_second_stream_matches_single_stream(dev, warm, monkeypatch):
         assert torch.equal(one[k], two[k]), (k, (one[k] - two[k]).abs().max().item())
 
 
-def test_bev_pos_hidden_cache(dev, monkeypatch):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_chain_path_matches_separate_launches(dev, prec):
+    """OPTIONS.chain (CMT_CHAIN): the row-block chain decoder (rowchain.hip)
+    and the decoder as separate GEMM / LayerNorm launches compute the same
+    f16/bf16 policy -- the same operands rounded at the same points, summed in
+    other orders -- so the logits agree to the policy's own rounding scale."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=7, num_query=96, num_layers=3,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=51).to(dev)
+    xi = S.synthetic_img(6, 8, 20, seed=52).to(dev)
+    metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=53)
+    outs = {}
+    set_precision(prec)
+    try:
+        for chain in (True, False):
+            with torch.no_grad(), options(chain=chain):
+                o = head([x], [xi], metas)[0][0]
+            torch.cuda.synchronize()
+            outs[chain] = {k: v.float().clone() for k, v in o.items()}
+    finally:
+        set_precision("ref")
+    for k in KEYS:
+        a, b = outs[True][k], outs[False][k]
+        assert torch.isfinite(a).all() and torch.isfinite(b).all(), k
+        scale = b.abs().max().item() + 1e-6
+        assert (a - b).abs().max().item() <= 2e-2 * scale, (k, (a - b).abs().max().item(), scale)
+
+
+def test_bev_pos_hidden_cache(dev):
     """The input-independent first half of the BEV position MLP (pos2embed of
     the grid + bev_embedding[0] + ReLU) is kept like a weight pack: a forward
     that reuses it equals one that recomputes it (CMT_BEV_POS_CACHE=0)
@@ -341,8 +372,7 @@ def test_bev_pos_hidden_cache(dev, monkeypatch):
     metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=43)
 
     def run(cache):
-        monkeypatch.setenv("CMT_BEV_POS_CACHE", cache)
-        with torch.no_grad():
+        with torch.no_grad(), options(bev_pos_cache=cache == "1"):
             out = head([x], [xi], metas)[0][0]
         torch.cuda.synchronize()
         return {k: v.clone() for k, v in out.items()}

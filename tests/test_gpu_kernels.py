@@ -166,30 +166,29 @@ def test_gemm_plane_max2(N, dev, dt, B, S, big):
     assert torch.allclose(pm.cpu().double(), ref, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("parts", ["2", "4"])
+@pytest.mark.parametrize("with_a2", [True, False])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100)])
-def test_kvproj_select_plane_max(N, dev, monkeypatch, dt, B, S, parts):
+def test_kvproj_select_plane_max(N, dev, dt, B, S, with_a2):
     """All-layer K/V projection shape (N = 3072, K = 256, A2 select on the K half,
     head-split output, K-half key-norm maxima) through cmt_kv_proj, the
     A-stationary kernel on fragment-packed W (kvproj.hip); ragged M, row tiles
     straddling the batch boundary, a grid smaller than one 128-row tile pair;
-    column halves or quarters per row tile (CMT_KVPROJ_PARTS)."""
-    monkeypatch.setenv("CMT_KVPROJ_PARTS", parts)
+    without A2 a single column part (N = 1536) reads A only."""
     g = torch.Generator().manual_seed(S * 7 + B)
-    K, Nc = 256, 3072
-    M, cols = B * S, Nc // 2
+    K, Nc = 256, 3072 if with_a2 else 1536
+    M, cols = B * S, Nc // 2 if with_a2 else Nc
     A = torch.randn(M, K, generator=g).to(dt)
-    A2 = torch.randn(M, K, generator=g).to(dt)
+    A2 = torch.randn(M, K, generator=g).to(dt) if with_a2 else A
     W = (torch.randn(Nc, K, generator=g) / 16).to(dt)
     bias = torch.randn(Nc, generator=g) * 0.1
     Y = torch.empty(M * Nc, dtype=dt, device=dev)
     nb = -(-M // 64)
     pm = torch.full((nb, cols // 32), -1.0, device=dev)
-    N.kv_proj(A.to(dev), N.kv_pack(W.to(dev)), Y, M=M, N=Nc, bias=bias.to(dev), A2=A2.to(dev), headsplit_rows=S,
-              plane_max2=pm, plane_max_cols=cols)
+    N.kv_proj(A.to(dev), N.kv_pack(W.to(dev)), Y, M=M, N=Nc, bias=bias.to(dev),
+              A2=A2.to(dev) if with_a2 else None, headsplit_rows=S, plane_max2=pm, plane_max_cols=cols)
     d = lambda t: t.double()
-    ref = torch.cat([d(A2) @ d(W[:cols]).T, d(A) @ d(W[cols:]).T], 1) + d(bias)
+    ref = torch.cat([d(A2) @ d(W[:Nc // 2]).T, d(A) @ d(W[Nc // 2:]).T], 1) + d(bias)
     y = Y.cpu().view(B, Nc // 32, S, 32).permute(0, 2, 1, 3).reshape(M, Nc).double()
     rel = (y - ref).abs().max().item() / ref.abs().max().item()
     assert rel < 1e-2, rel

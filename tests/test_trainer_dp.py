@@ -35,7 +35,10 @@ def _worker(rank, world, port, q):
     model(x).pow(2).sum().backward()
     local = fp.grad.clone()
     nb = allreduce_buckets(fp.grad, bucket_bytes=4096)
-    q.put((rank, local, fp.grad.clone(), nb, [p.grad.data_ptr() for p in fp.params], fp.grad.data_ptr()))
+    # numpy arrays travel by value (torch CPU tensors travel as shared-memory fds that the
+    # parent can open only while this process lives)
+    q.put((rank, local.numpy(), fp.grad.numpy().copy(), nb, [p.grad.data_ptr() for p in fp.params],
+           fp.grad.data_ptr()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -53,6 +56,7 @@ def test_bucketed_allreduce_matches_single_process_sum():
         p.join(timeout=60)
         assert p.exitcode == 0
     (_, l0, r0, nb, ptrs, base), (_, l1, r1, _, _, _) = res
+    l0, r0, l1, r1 = (torch.from_numpy(t) for t in (l0, r0, l1, r1))
     assert nb > 1                                              # several buckets
     assert torch.allclose(r0, (l0 + l1) / 2, atol=1e-6) and torch.equal(r0, r1)
     assert ptrs[0] == base                                      # grads are views of the flat buffer
