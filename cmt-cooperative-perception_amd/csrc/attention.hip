@@ -558,6 +558,222 @@ __global__ __launch_bounds__(KW * 64) void attn_kw_kernel(AttnKParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split-f16 self-attention (dtype CMT_F16P: the 'ref' policy's fp32-accurate
+// nn.MultiheadAttention core).  Q / K / V rows are f16 pairs in the head-split
+// layout cmt_gemm writes for a pair C: 64 16-bit elements per (head, row) --
+// the 32 hi values, then the 32 lo values.  The workgroup structure is
+// attn_kw_kernel's (KW waves on the same 32 queries, wave w takes key tiles
+// w, w + KW, ... through a private two-slot LDS-DMA ring, partials merged
+// through LDS), with 32-key tiles (a pair tile is twice a 16-bit tile's bytes).
+// Every product is three f16 MFMAs on the pairs -- hi*hi + lo*hi + hi*lo,
+// ~2^-21 relative -- with fp32 accumulation:
+//   S^T = K Q^T with Q * scale * log2(e) re-split in the prologue (the
+//         reference scales q before its matmul, torch MultiheadAttention)
+//   P = exp2(S - m) in fp32 (online max, deferred rescale), split into a pair
+//   O^T += V^T P^T (pair V^T by transposed LDS reads of both halves)
+// Row sums in fp32 on the VALU.
+// ---------------------------------------------------------------------------
+constexpr int KTP = 32;     // keys per pair tile
+constexpr int PRW = 64;     // 16-bit elements per pair row (hi 32 | lo 32)
+
+__device__ __forceinline__ void split8(const f32x4 (&x)[2], f16x8& hi, f16x8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = x[j >> 2][j & 3];
+        hi[j] = (f16_t)v;
+        lo[j] = (f16_t)(v - (float)hi[j]);
+    }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void attn_tile_pair(const f16_t* __restrict__ Kt, const f16_t* __restrict__ Vt,
+                                               const f16x8 (&qh)[2], const f16x8 (&ql)[2], f32x16& o, float& l_run,
+                                               f32x16& negm, float& m_run, bool first, int key0, int Nk, int lane) {
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    // K rows: 128 B, 16-byte chunks XOR-swizzled by row & 7 (chunks 0-3 hi, 4-7 lo)
+    const int sw = lr & 7;
+    const f16_t* kr = Kt + lr * PRW;
+    const f16x8 kh0 = *(const f16x8*)(kr + 8 * ((lh) ^ sw));
+    const f16x8 kh1 = *(const f16x8*)(kr + 8 * ((2 + lh) ^ sw));
+    const f16x8 kl0 = *(const f16x8*)(kr + 8 * ((4 + lh) ^ sw));
+    const f16x8 kl1 = *(const f16x8*)(kr + 8 * ((6 + lh) ^ sw));
+    f32x16 s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl0, qh[0], negm, 0, 0, 0);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh0, ql[0], s, 0, 0, 0);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl1, qh[1], s, 0, 0, 0);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh1, ql[1], s, 0, 0, 0);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh0, qh[0], s, 0, 0, 0);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh1, qh[1], s, 0, 0, 0);
+    if (MASK) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (key >= Nk) s[r] = -__builtin_inff();
+        }
+    }
+    float mt = vmax(s[0], s[1]);
+#pragma unroll
+    for (int r = 2; r < 16; r += 2) mt = vmax3(mt, s[r], s[r + 1]);
+    mt = pair_max(mt);
+    if (first || __any(mt > kDeferMax)) {
+        const float d = first ? mt : vmax(mt, 0.f);
+        const float alpha = first ? 1.f : __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            o[r] *= alpha;
+            s[r] -= d;
+        }
+        l_run *= alpha;
+        m_run += d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+    }
+    f16x8 ph[2], pl[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(s[r]);
+        l_run += pv;
+        const f16_t h = (f16_t)pv;
+        ph[r >> 3][r & 7] = h;
+        pl[r >> 3][r & 7] = (f16_t)(pv - (float)h);
+    }
+    // V^T fragments by transposed LDS reads (attn_tile_lowp's key order), both halves
+    const int dgrp = 16 * ((lane >> 4) & 1);
+    const int tq = (lane & 15) >> 2;
+    const int tp = lane & 3;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+        const int r0 = 16 * ss + 4 * lh + tq;
+        f16x8 vf[2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const f16_t* base0 = &Vt[r0 * PRW + 32 * half + dgrp + 4 * tp];
+            const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)base0);
+            const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)(base0 + 8 * PRW));
+            s16x8 vv;
+            vv[0] = a0[0]; vv[1] = a0[1]; vv[2] = a0[2]; vv[3] = a0[3];
+            vv[4] = a1[0]; vv[5] = a1[1]; vv[6] = a1[2]; vv[7] = a1[3];
+            vf[half] = __builtin_bit_cast(f16x8, vv);
+        }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[1], ph[ss], o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[0], pl[ss], o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[0], ph[ss], o, 0, 0, 0);
+    }
+}
+
+template <int KW>
+__global__ __launch_bounds__(KW * 64) void attn_kw_pair_kernel(AttnKParams p) {
+    constexpr int STAGE = 2 * KTP * PRW;   // 16-bit elements: K tile then V tile (8 KB)
+    __shared__ __attribute__((aligned(16))) f16_t ring[KW * KWR * STAGE];
+    __shared__ float xm[KW][QW], xl[KW][QW];
+    static_assert(KWR * STAGE * 2 >= QW * KWO * (int)sizeof(float), "merge image fits a wave's ring");
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31;
+    const int lh = lane >> 5;
+    const int bh = blockIdx.y;
+    const int b = bh / p.H;
+    const int h = bh - b * p.H;
+
+    const f16_t* Qb = (const f16_t*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
+    const f16_t* Kb = (const f16_t*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
+    const f16_t* Vb = (const f16_t*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
+
+    const int ntiles = (p.Nk + KTP - 1) / KTP;
+    const int my_n = wave < ntiles ? (ntiles - 1 - wave) / KW + 1 : 0;
+    const bool ragged = (p.Nk % KTP) != 0;
+    f16_t* const myring = ring + wave * KWR * STAGE;
+
+    // one 1 KB piece = 8 rows of 128 B; lane -> (row lane / 8, chunk lane & 7)
+    const int crow = lane >> 3, cch = lane & 7;
+    auto issue = [&](int slot, int t) {   // the whole 32-key tile t: 4 K + 4 V pieces
+        f16_t* st = myring + slot * STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = i * 8 + crow;
+            const int key = min(t * KTP + row, p.Nk - 1);   // ragged tail: clamped, masked in compute
+            dma16(Kb + (int64_t)key * p.k_rs + 8 * (cch ^ (row & 7)), st + i * 8 * PRW);
+            dma16(Vb + (int64_t)key * p.v_rs + 8 * cch, st + KTP * PRW + i * 8 * PRW);
+        }
+    };
+    if (my_n > 0) issue(0, wave);
+    if (my_n > 1) issue(1, wave + KW);
+
+    // Q^T fragments (B operand), q * c re-split: B[k = 8 lh + j][col = q] = Q[q][16 ks + 8 lh + j]
+    const int q = blockIdx.x * QW + lr;
+    const int qc = q < p.Nq ? q : p.Nq - 1;
+    f16x8 qh[2], ql[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const f16x8 hi = *(const f16x8*)(Qb + (int64_t)qc * p.q_rs + 16 * ks + 8 * lh);
+        const f16x8 lo = *(const f16x8*)(Qb + (int64_t)qc * p.q_rs + 32 + 16 * ks + 8 * lh);
+        f32x4 x[2];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j >> 2][j & 3] = ((float)hi[j] + (float)lo[j]) * p.c;
+        split8(x, qh[ks], ql[ks]);
+    }
+
+    f32x16 o, negm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o[r] = 0.f;
+        negm[r] = 0.f;
+    }
+    float m_run = 0.f, l_run = 0.f;
+    for (int i = 0; i < my_n; ++i) {
+        if (i + 1 < my_n) wait_vm_lgkm<8>();
+        else wait_vm_lgkm<0>();
+        const f16_t* Kt = myring + (i & 1) * STAGE;
+        const f16_t* Vt = Kt + KTP * PRW;
+        const int t = wave + i * KW;
+        if (ragged && t == ntiles - 1)
+            attn_tile_pair<true>(Kt, Vt, qh, ql, o, l_run, negm, m_run, i == 0, t * KTP, p.Nk, lane);
+        else
+            attn_tile_pair<false>(Kt, Vt, qh, ql, o, l_run, negm, m_run, i == 0, t * KTP, p.Nk, lane);
+        if (i + 2 < my_n) {
+            wait_vm_lgkm<0>();   // the slot's ds_reads are done before the DMA overwrites it
+            issue(i & 1, wave + (i + 2) * KW);
+        }
+    }
+    l_run = pair_sum(l_run);
+
+    // ---- merge the KW partials through LDS (each wave's own ring region holds its O^T image)
+    wait_vm_lgkm<0>();
+    float* xo = (float*)myring;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+        *(f32x4*)(xo + lr * KWO + 8 * g + 4 * lh) = v;
+    }
+    if (lh == 0) {
+        xm[wave][lr] = my_n > 0 ? m_run : -__builtin_inff();   // exp2 units
+        xl[wave][lr] = l_run;
+    }
+    barrier_mem();
+    if (tid < QW * 8) {
+        const int mq = tid >> 3, d0 = 4 * (tid & 7);
+        const int qo = blockIdx.x * QW + mq;
+        if (qo < p.Nq) {
+            float M = xm[0][mq];
+#pragma unroll
+            for (int w = 1; w < KW; ++w) M = vmax(M, xm[w][mq]);
+            float L = 0.f;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int w = 0; w < KW; ++w) {
+                const float sc = __builtin_amdgcn_exp2f(xm[w][mq] - M);   // -inf -> 0 (waves without tiles)
+                L += xl[w][mq] * sc;
+                const f32x4 v = *(const f32x4*)((const float*)(ring + w * KWR * STAGE) + mq * KWO + d0);
+                acc += v * sc;
+            }
+            store_o4(p, b, qo, h * D + d0, acc * (1.f / L));
+        }
+    }
+}
+
 // Wave-wide max of the max-|k|^2 partials (each covers kmax_rows key rows)
 // over the key range of this workgroup's split of batch b, head h: the bound
 // only has to hold for the keys this workgroup scores (the split combine
@@ -1308,9 +1524,12 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
 // self-attention) the in-workgroup key split attn_kw_kernel; anything else the
 // 4-wave single-phase attn_fwd_kernel with split partials.  f32 always takes
 // the exact-f32 kernel.
-bool use_long(const cmt_attn_args& a) { return a.dtype != CMT_F32 && a.Nk >= 4096 && a.Nq > 128; }
+bool use_long(const cmt_attn_args& a) {
+    return a.dtype != CMT_F32 && a.dtype != CMT_F16P && a.Nk >= 4096 && a.Nq > 128;
+}
 
 bool use_kw(const cmt_attn_args& a) {
+    if (a.dtype == CMT_F16P) return true;   // the split-f16 kernel has only the key-split form
     if (a.dtype == CMT_F32 || a.kv_splits > 0 || use_long(a)) return false;
     return (a.Nk + KT - 1) / KT <= 64;
 }
@@ -1343,8 +1562,13 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_attn_fwd: null args");
     const cmt_attn_args& a = *ap;
     CMT_REQUIRE(a.B > 0 && a.H > 0 && a.Nq > 0 && a.Nk > 0, "cmt_attn_fwd: empty problem");
-    CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16 || a.dtype == CMT_F32,
-                "cmt_attn_fwd: dtype must be f32, f16 or bf16");
+    CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16 || a.dtype == CMT_F32 || a.dtype == CMT_F16P,
+                "cmt_attn_fwd: dtype must be f32, f16, bf16 or f16 pair");
+    CMT_REQUIRE(a.dtype != CMT_F16P || (a.kv_splits <= 1 && a.kmax2 == nullptr && a.q_rstride >= 64 &&
+                                        a.k_rstride >= 64 && a.v_rstride >= 64 && a.Nk <= (1 << 20) &&
+                                        ((uintptr_t)a.Q | (uintptr_t)a.K | (uintptr_t)a.V) % 16 == 0),
+                "cmt_attn_fwd: f16-pair Q/K/V take pair rows (>= 64 16-bit elements: 32 hi, 32 lo), "
+                "no kv_splits / kmax2, 16-byte aligned");
     CMT_REQUIRE(a.Q && a.K && a.V && a.O, "cmt_attn_fwd: null pointer");
     CMT_REQUIRE(a.dtype != CMT_F32 || ((a.q_rstride | a.k_rstride | a.v_rstride) % 4 == 0),
                 "cmt_attn_fwd: f32 rows must be 16-byte aligned");
@@ -1386,6 +1610,10 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     }
     hipStream_t s = (hipStream_t)stream;
     const bool fold = (a.flags & CMT_ATTN_FOLD_SCALE) != 0;
+    if (a.dtype == CMT_F16P) {
+        attn_kw_pair_kernel<8><<<dim3(cdiv(a.Nq, QW), a.B * a.H), 512, 0, s>>>(p);
+        return cmt_check_launch("cmt_attn_fwd");
+    }
     if (a.dtype == CMT_F32) {
         attn_fwd_f32_kernel<<<dim3(cdiv(a.Nq, QB), a.B * a.H, splits), 256, 0, s>>>(p);
     } else if (use_kw(a)) {

@@ -731,8 +731,8 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     // written to LDS (16-byte chunks XOR-swizzled by row) and read back so
     // every wave instruction stores 1 KB of contiguous memory (head-split:
     // 16 rows x 64 B of one head; rows: whole row segments).
-    // A CMT_F16P C (row mode) is staged and stored twice: the hi halves, then
-    // the lo halves N columns further (cmt_hip.h).
+    // A CMT_F16P C is staged and stored twice: the hi halves, then the lo
+    // halves N columns further (rows) or 32 elements further (head split).
     const int npass = a.c_dtype == CMT_F16P ? 2 : 1;
     for (int pass = 0; pass < npass; ++pass) {
         barrier_mem();                                       // every wave is done with the staging ring
@@ -838,7 +838,10 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
                     bb = m / rpb;
                     rr = m - bb * rpb;
                 }
-                idx = (((int64_t)bb * (a.N >> 5) + (n >> 5)) * rpb + rr) * 32 + (n & 31);
+                // a CMT_F16P C: 64 elements per (head, row) -- the hi row, then the lo row
+                idx = a.c_dtype == CMT_F16P
+                          ? (((int64_t)bb * (a.N >> 5) + (n >> 5)) * rpb + rr) * 64 + (pass ? 32 : 0) + (n & 31)
+                          : (((int64_t)bb * (a.N >> 5) + (n >> 5)) * rpb + rr) * 32 + (n & 31);
             } else {
                 idx = (int64_t)m * a.ldc + n + (pass ? a.N : 0);
             }
@@ -1071,7 +1074,6 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
                      a.c_split_stride >= (int64_t)(a.M - 1) * a.ldc + a.N),
                 "cmt_gemm: split-K needs compute-dtype row A, fp32 row C, batch 1, no relu / plane_max2, "
                 "K / 64 divisible by k_splits and non-overlapping parts");
-    CMT_REQUIRE(a.c_dtype != CMT_F16P || a.c_mode == CMT_C_ROWS, "cmt_gemm: a CMT_F16P C must be row mode");
     CMT_REQUIRE(a.a_dtype == CMT_F32 || a.a_dtype == a.w_dtype, "cmt_gemm: A must be f32 or the compute dtype");
     CMT_REQUIRE(a.a_mode != CMT_A_CONV3X3 || a.a_dtype == a.w_dtype,
                 "cmt_gemm: the conv3x3 gather needs A in the compute dtype");

@@ -207,6 +207,8 @@ class _MHABase(nn.Module):
         prec = get_precision()
         w_in, b_in, w_out, b_out = self._weights(prec)
         adt, rnd = (prec.attn, prec.round_cross_out) if self.fp16_core else (prec.self_attn, False)
+        if adt == SPLIT:   # the split core takes head-split pair rows (fused decoder); rows here: exact f32
+            adt = torch.float32
         out = project_attend_project(_rows(query), _rows(key), _rows(value),
                                      _rows(query_pos) if query_pos is not None else None,
                                      _rows(key_pos) if key_pos is not None else None,
@@ -765,7 +767,10 @@ class PETRTransformerDecoder(nn.Module):
         tp = torch.empty_like(tl)                                  # lowp(tgt + qpos)
         native.add_cast(tgt if (tgt0 is not None or not use_chain) else None, rows=rows, C=C, Yl=tl, Yp=tp,
                         P=qpos)
-        qkv = torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=dev)
+        # self-attention Q|K|V head-split; a split self-attention core (the 'ref' policy) takes
+        # them as f16 pairs, 64 16-bit elements per (head, row): hi 32 | lo 32
+        sps = 2 if prec.self_attn == SPLIT else 1
+        qkv = torch.empty((B * 3 * C * Nq * sps,), dtype=prec.self_attn, device=dev)
         qc = torch.empty((B * C * Nq,), dtype=prec.attn, device=dev)
         ob = op_empty(rows, C, lp, dev)                            # attention output (out-proj operand)
         # the N = C out-projection / fc2 GEMMs of the split policy run split-K into KSP fp32
@@ -816,10 +821,10 @@ class PETRTransformerDecoder(nn.Module):
             # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
             native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
                         A2=tp, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
-            native.attention(qkv, qkv, qkv, ob, B=B, H=H, Nq=Nq, Nk=Nq,
-                             q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
-                             v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
-                             o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
+            hs = (3 * C * Nq * sps, 32 * sps * Nq, 32 * sps)
+            native.attention(qkv, qkv, qkv, ob, B=B, H=H, Nq=Nq, Nk=Nq, q_strides=hs, k_strides=hs, v_strides=hs,
+                             k_offset=C * Nq * sps, v_offset=2 * C * Nq * sps, o_strides=(Nq * C, C), scale=scale,
+                             workspace=ws, fold_scale=True)
             w0, b0, e0 = lw["norms"][0]
             native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt,
                         ldr=C, k_splits=KSP)

@@ -397,6 +397,8 @@ def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_st
               k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False,
               fold_scale=False, kmax2=None, kmax_ld=0, kmax_plane0=0, _diag_flags=0):
     """Strides are (batch, head, row) in elements; o_strides = (batch, row).
+    f16-pair Q/K/V (torch.uint16, the split self-attention): strides and offsets
+    count 16-bit elements, a pair row being 64 of them (32 hi, 32 lo).
     fold_scale lets the kernel fold scale*log2(e) into Q on load (one extra
     rounding of Q; the f16/bf16 policies only).  kmax2: the K projection's
     plane_max2 partials (see gemm) -- lets the bf16 long-key kernel fix each

@@ -62,7 +62,7 @@ class Precision:
 
 
 PRECISIONS = {
-    "ref": Precision("ref", SPLIT, torch.float16, torch.float32, True),
+    "ref": Precision("ref", SPLIT, torch.float16, SPLIT, True),
     "exact": Precision("exact", torch.float32, torch.float16, torch.float32, True),
     "fp16": Precision("fp16", torch.float16, torch.float16, torch.float16, False, True),
     "bf16": Precision("bf16", torch.bfloat16, torch.bfloat16, torch.bfloat16, False, True),

@@ -111,7 +111,8 @@ typedef struct cmt_gemm_args {
     const float* bias; int64_t bias_bstride;
     const void* R; int64_t ldr; int64_t r_bstride; int r_dtype;
     void* C; int64_t ldc; int64_t c_bstride; int c_dtype;
-    int c_mode;                /* cmt_gemm_cmode; HEADSPLIT: C[(b*(N/32)+n/32)*rows_per_batch + r][32] */
+    int c_mode;                /* cmt_gemm_cmode; HEADSPLIT: C[(b*(N/32)+n/32)*rows_per_batch + r][32]
+                                  (a CMT_F16P C: [..][64], the 32 hi values then the 32 lo values) */
     int rows_per_batch;
     int relu;
     /* optional (HEADSPLIT with a 16-bit C only): plane_max2[(m/64)*(plane_max_cols/32) + n/32]
@@ -153,8 +154,13 @@ int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
  * (head-split layout: rstride = 32; token-major [B,S,H*32]: rstride = H*32;
  * sequence-first [S,B,H*32]: rstride = B*H*32).  Row strides must keep
  * 16-byte alignment (multiples of 8 elements).
- * Output O (o_dtype: fp32, or f16/bf16 when it only feeds the out-projection
- * GEMM) has the heads concatenated per row (normalised).
+ * Output O (o_dtype: fp32, or f16/bf16/f16-pair when it only feeds the
+ * out-projection GEMM) has the heads concatenated per row (normalised).
+ * dtype CMT_F16P (ABI 13, the reference-numerics self-attention): Q/K/V rows
+ * are f16 pairs of 64 16-bit elements -- the 32 hi values, then the 32 lo
+ * values (cmt_gemm's head-split pair C: rstride = 64) -- every product runs
+ * as three f16 MFMAs (~2^-21 relative, fp32 softmax); strides count 16-bit
+ * elements; no kv_splits, kmax2 or output rounding.
  * Nk is split into kv_splits chunks processed by separate workgroups and
  * merged by a combine pass (workspace: cmt_attn_workspace_bytes).
  * ------------------------------------------------------------------------ */
@@ -167,12 +173,12 @@ enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2 };
 
 typedef struct cmt_attn_args {
     int B, H, Nq, Nk;
-    int dtype;                 /* CMT_F16 or CMT_BF16 (Q, K, V) */
+    int dtype;                 /* CMT_F32, CMT_F16, CMT_BF16 or CMT_F16P (Q, K, V) */
     const void* Q; int64_t q_bstride, q_hstride, q_rstride;
     const void* K; int64_t k_bstride, k_hstride, k_rstride;
     const void* V; int64_t v_bstride, v_hstride, v_rstride;
     void* O; int64_t o_bstride, o_rstride;   /* O[b*o_bstride + q*o_rstride + h*32 + d] */
-    int o_dtype;               /* CMT_F32 / CMT_F16 / CMT_BF16 */
+    int o_dtype;               /* CMT_F32 / CMT_F16 / CMT_BF16 / CMT_F16P (pair rows [hi H*32 | lo H*32]) */
     float scale;               /* softmax scale, usually 1/sqrt(32) */
     int kv_splits;             /* 0 = choose automatically */
     int flags;                 /* CMT_ATTN_ROUND_OUTPUT | CMT_ATTN_FOLD_SCALE */

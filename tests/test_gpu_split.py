@@ -104,6 +104,66 @@ def test_gemm_split_k_into_layernorm(N, dev, K, ks):
                k_splits=ks)
 
 
+def _pair_heads(x, B, S, H):
+    """fp32 [B*S, H*32] rows -> head-split f16 pairs [B][H][S][64] (hi 32 | lo 32) as uint16."""
+    hi = x.float().half()
+    lo = (x.float() - hi.float()).half()
+    t = torch.cat([hi.view(B, S, H, 32), lo.view(B, S, H, 32)], -1)       # [B, S, H, 64]
+    return t.permute(0, 2, 1, 3).contiguous().view(SPLIT)
+
+
+def test_gemm_split_headsplit_pair_output(N, dev):
+    """Pair C in head-split mode (the split self-attention's Q|K|V): 64 16-bit
+    elements per (head, row), hi 32 then lo 32; Q|K columns from A2 (select)."""
+    g = torch.Generator().manual_seed(17)
+    B, S, C = 2, 450, 256
+    M, N_ = B * S, 3 * C
+    A = torch.randn(M, C, generator=g)
+    A2 = torch.randn(M, C, generator=g)
+    W = torch.randn(N_, C, generator=g) / 16
+    b = torch.randn(N_, generator=g)
+    ref = torch.cat([A2.double() @ W[:2 * C].double().t(), A.double() @ W[2 * C:].double().t()], 1) + b.double()
+    out = torch.empty(B * N_ * S * 2, dtype=SPLIT, device=dev)
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), out, M=M, N=N_, K=C, lda=C, ldw=C, ldc=0, bias=b.to(dev),
+           A2=_pair(A2).to(dev), lda2=C, a2_cols=2 * C, headsplit_rows=S)
+    h = out.cpu().view(torch.float16).double().view(B, N_ // 32, S, 64)
+    got = (h[..., :32] + h[..., 32:]).permute(0, 2, 1, 3).reshape(M, N_)
+    assert (got - ref).abs().max().item() <= _tol(ref, C) + 2 ** -21 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("B,Nq,Nk,scale", [(1, 900, 900, 1.0), (2, 77, 301, 3.0), (1, 33, 5, 1.0)])
+def test_attention_pair_self(N, dev, B, Nq, Nk, scale):
+    """Split-f16 attention core (CMT_F16P Q/K/V, head-split pair rows): the
+    reference-numerics self-attention -- fp32 softmax(QK^T / sqrt(32)) V to
+    ~2^-20 relative, f32 and pair outputs; ragged key tiles."""
+    g = torch.Generator().manual_seed(Nq + Nk)
+    H, C = 8, 256
+    q = torch.randn(B * Nq, C, generator=g) * scale
+    k = torch.randn(B * Nk, C, generator=g) * scale
+    v = torch.randn(B * Nk, C, generator=g)
+    qp, kp, vp = _pair_heads(q, B, Nq, H).to(dev), _pair_heads(k, B, Nk, H).to(dev), _pair_heads(v, B, Nk, H).to(dev)
+    qd = q.double().view(B, Nq, H, 32).transpose(1, 2)
+    kd = k.double().view(B, Nk, H, 32).transpose(1, 2)
+    vd = v.double().view(B, Nk, H, 32).transpose(1, 2)
+    att = torch.softmax(qd @ kd.transpose(-1, -2) / math.sqrt(32), -1)
+    ref = (att @ vd).transpose(1, 2).reshape(B * Nq, C)
+    qs, ks = (H * Nq * 64, Nq * 64, 64), (H * Nk * 64, Nk * 64, 64)
+    o32 = torch.empty(B * Nq, C, device=dev)
+    N.attention(qp, kp, vp, o32, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=qs, k_strides=ks, v_strides=ks,
+                o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32))
+    err = (o32.cpu().double() - ref).abs().max().item()
+    tol = 4e-6 * ref.abs().max().item() + 1e-6
+    assert err <= tol, (err, tol)
+    op = torch.empty(B * Nq, 2, C, dtype=SPLIT, device=dev)
+    N.attention(qp, kp, vp, op, B=B, H=H, Nq=Nq, Nk=Nk, q_strides=qs, k_strides=ks, v_strides=ks,
+                o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32))
+    assert _same(op, _pair(o32.cpu()))
+    b16 = torch.softmax((qd.half().double() @ kd.half().double().transpose(-1, -2)) / math.sqrt(32), -1)
+    e16 = ((b16 @ vd.half().double()).transpose(1, 2).reshape(B * Nq, C) - ref).abs().max().item()
+    print(f"pair self-attention B{B} {Nq}x{Nk}: max abs err {err:.2e} (f16 operands: {e16:.2e})")
+    assert err * 100 < e16
+
+
 def test_gemm_split_headsplit_select(N, dev):
     """Q|K columns from A2 (select), V columns from A, head-split f16 / f32 output
     with the key-norm partials (the K/V projection contract)."""
