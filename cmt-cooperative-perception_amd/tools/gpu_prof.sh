@@ -12,3 +12,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-for
 cat "$OUT/bench.json"
 python3 cmt-cooperative-perception_amd/tools/trace_table.py "$OUT" 28 > "gpurun_out/${TAG}/table.txt"
 head -40 "gpurun_out/${TAG}/table.txt"
+cp "$OUT"/*kernel_stats.csv "gpurun_out/${TAG}/kernel_stats.csv" 2>/dev/null
+# the full trace is kept only when small enough for gpurun to copy back
+find "$OUT" -name "*kernel_trace.csv" -size +40M -delete
