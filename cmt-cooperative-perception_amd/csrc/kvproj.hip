@@ -40,6 +40,18 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* kp_laddr_t;
 template <typename T> using frag_of = typename mfma_traits<T>::frag;
 
+// Batch stride of the head-split C in 16-bit elements: c_bstride when given (one
+// layer's K/V planes written into a larger [B][planes][Nk][32] buffer), else the
+// launch's own N/32 planes per batch element.
+__host__ __device__ inline int64_t kv_c_bstride(const cmt_gemm_args& a) {
+    return a.c_bstride ? a.c_bstride : (int64_t)(a.N >> 5) * a.rows_per_batch * 32;
+}
+// Bytes from C to the end of the last plane the launch writes.
+__host__ __device__ inline int64_t kv_c_extent_bytes(const cmt_gemm_args& a) {
+    const int64_t nb = a.M / a.rows_per_batch;
+    return ((nb - 1) * kv_c_bstride(a) + (int64_t)(a.N >> 5) * a.rows_per_batch * 32) * 2;
+}
+
 // Whole 128-token tile per W fetch (8-wave form): the plane's W fragments
 // serve all four 32-token tiles, so each workgroup fetches its columns' W
 // once instead of once per 64-token half (768 KB instead of 1.5 MB per
@@ -124,18 +136,19 @@ __device__ __forceinline__ void kv_sweep_full(const cmt_gemm_args& a, const char
                                               const T* Wl, typename mfma_traits<T>::frag (&wa)[KP_KS], int nplanes,
                                               int plane0, int m0, int lane) {
     const int lr = lane & 31;
-    const uint32_t cbytes = (uint32_t)((int64_t)a.M * a.N * 2);
+    const uint32_t cbytes = (uint32_t)kv_c_extent_bytes(a);
     const auto crsrc = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, cbytes, 0x00020000);
     const uint32_t pmbytes = MAXQ ? (uint32_t)(((a.M + 63) / 64) * (a.plane_max_cols >> 5) * 4) : 0u;
     const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(MAXQ ? (void*)a.plane_max2 : a.C, 0, pmbytes, 0x00020000);
     const int rpb = a.rows_per_batch;
+    const int64_t cbs = kv_c_bstride(a);
     uint32_t soff[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int m = m0 + 16 * i + (lane >> 2);
         const int bb = m / rpb;
-        const int64_t row = (int64_t)bb * (a.N >> 5) * rpb + (m - bb * rpb);
-        soff[i] = m < a.M ? (uint32_t)((row * 32 + 8 * (lane & 3)) * 2) : 0xffffffffu;
+        const int64_t el = (int64_t)bb * cbs + (int64_t)(m - bb * rpb) * 32;
+        soff[i] = m < a.M ? (uint32_t)((el + 8 * (lane & 3)) * 2) : 0xffffffffu;
     }
     const char* arow = lds + lr * (KP_K * 2);
     for (int j = 0; j < nplanes; ++j) {
@@ -267,12 +280,13 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     barrier_mem();
     // head-split element offset of each tile's token row (plane 0)
     const int rpb = a.rows_per_batch;
+    const int64_t cbs = kv_c_bstride(a);
     int64_t rbase[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const int m = min(m0 + 32 * t + lr, a.M - 1);
         const int bb = m / rpb;
-        rbase[t] = ((int64_t)bb * (a.N >> 5) * rpb + (m - bb * rpb)) * 32;
+        rbase[t] = (int64_t)bb * cbs + (int64_t)(m - bb * rpb) * 32;
     }
     const char* lhi = lds;
     const char* llo = lds + KP_BM * KP_K * 2;
@@ -351,6 +365,10 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
     const cmt_gemm_args& a = *ap;
     // column parts per 128-token tile: the K half (A2 = lowp(mem + pos)) and the V half (A)
     const int parts = a.A2 ? 2 : 1;
+    CMT_REQUIRE(a.rows_per_batch > 0 && a.M % a.rows_per_batch == 0, "cmt_kv_proj: bad head-split rows");
+    CMT_REQUIRE(a.c_bstride == 0 || (a.c_bstride % 32 == 0 &&
+                                     a.c_bstride >= (int64_t)(a.N >> 5) * a.rows_per_batch * 32),
+                "cmt_kv_proj: c_bstride must hold the launch's N/32 planes of rows_per_batch rows");
     if (a.w_dtype == CMT_F16P) {
         // split (fp32-accurate) form: f16 pair A / A2 rows, W_hi then W_lo fragment-packed, f16 / bf16 C
         CMT_REQUIRE(a.a_dtype == CMT_F16P && (a.c_dtype == CMT_F16 || a.c_dtype == CMT_BF16),
@@ -385,7 +403,7 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                 "cmt_kv_proj: A2 selects the first half of the columns");
     CMT_REQUIRE(a.plane_max2 == nullptr || (a.plane_max_cols % (a.N / parts) == 0 && a.plane_max_cols <= a.N),
                 "cmt_kv_proj: plane_max_cols must be a multiple of the column part (N / parts) <= N");
-    CMT_REQUIRE((int64_t)a.M * a.N * 2 < ((int64_t)1 << 32) - 1, "cmt_kv_proj: C must be < 4 GiB (32-bit offsets)");
+    CMT_REQUIRE(kv_c_extent_bytes(a) < ((int64_t)1 << 32) - 1, "cmt_kv_proj: C must be < 4 GiB (32-bit offsets)");
     CMT_REQUIRE(a.lda % 8 == 0 && ((uintptr_t)a.A | (uintptr_t)a.W | (uintptr_t)a.C | (uintptr_t)a.A2 |
                                     (uintptr_t)a.bias) % 16 == 0, "cmt_kv_proj: 16-byte aligned operands");
     hipStream_t s = (hipStream_t)stream;

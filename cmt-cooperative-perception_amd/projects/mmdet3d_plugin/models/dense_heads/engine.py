@@ -293,7 +293,7 @@ class HeadEngineMixin:
         dec = self.transformer.decoder
         Nq = self.num_query
         state = None
-        side = self._side_stream(dev) if dec.chain_prologue_ok(prec) else None
+        side = self._side_stream(dev) if dec.prologue_ok(prec) else None
         if side is not None:
             # A second stream runs everything that does not read the conv output: the
             # input-independent first halves of the BEV / RV position MLPs and the camera

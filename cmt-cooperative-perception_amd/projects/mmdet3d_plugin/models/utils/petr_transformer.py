@@ -641,51 +641,70 @@ class PETRTransformerDecoder(nn.Module):
                              ldy2=C, flags2=post_flags, y2_offset=l * rows * C)
         return out
 
-    def chain_prologue_ok(self, prec):
-        """The lowp chain path, whose layer-0 self-attention block depends only
-        on the query embedding and can run beside the memory-side work."""
+    def _use_chain(self, prec):
+        """Row-block chains (f16 / bf16 policies; CMT_CHAIN=0: separate launches)."""
+        return self._chain_ok() and get_precision(prec).gemm != SPLIT and OPTIONS.chain
+
+    def prologue_ok(self, prec):
+        """Whether run_rows takes a lowp_state whose layer 0 up to the
+        cross-attention core (it reads only the query embedding) may be queued
+        beforehand on another stream, beside the memory-side work (every f16 /
+        bf16 / split policy of the fused decoder)."""
         prec = get_precision(prec)
-        return (prec.gemm in (torch.float16, torch.bfloat16) and self.fused_supported() and self._chain_ok()
-                and OPTIONS.chain)
+        return prec.gemm != torch.float32 and self.fused_supported()
 
     def lowp_state(self, *, B, Nk, Nq, prec, device):
-        """Working buffers of one lowp chain-path decoder run (allocated on the
-        current stream; lowp_layer0 may then run on another one)."""
+        """Working buffers of one lowp decoder run with a zero target
+        (allocated on the current stream; lowp_layer0 may then run on another
+        one)."""
         prec = get_precision(prec)
         # every packed weight the run reads is built HERE, on the current stream: a pack first
         # built inside lowp_layer0 on the second stream would be read by the main stream's
         # K/V projection with nothing ordering the two
         pk = self.packed(prec)
-        self._chain_pack(prec)
+        chain = self._use_chain(prec)
+        if chain:
+            self._chain_pack(prec)
         C, H = self.embed_dims, self.embed_dims // 32
         lp, f32, rows = prec.gemm, torch.float32, B * Nq
         FF = pk["layers"][0]["f1_w"].shape[0]
         ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
                        native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
-        return dict(
+        # self-attention Q|K|V head-split; a split self-attention core (the 'ref' policy) takes
+        # them as f16 pairs, 64 16-bit elements per (head, row): hi 32 | lo 32
+        sps = 2 if prec.self_attn == SPLIT else 1
+        st = dict(
+            chain=chain,
             tgt=torch.empty((rows, C), dtype=f32, device=device),
-            tl=torch.empty((rows, C), dtype=lp, device=device),          # lowp(tgt)
-            tp=torch.empty((rows, C), dtype=lp, device=device),          # lowp(tgt + qpos)
-            qkv=torch.empty((B * 3 * C * Nq,), dtype=prec.self_attn, device=device),
+            tl=op_empty(rows, C, lp, device),                            # lowp(tgt)
+            tp=op_empty(rows, C, lp, device),                            # lowp(tgt + qpos)
+            qkv=torch.empty((B * 3 * C * Nq * sps,), dtype=prec.self_attn, device=device),
             qc=torch.empty((B * C * Nq,), dtype=prec.attn, device=device),
-            ob=torch.empty((rows, C), dtype=lp, device=device),          # attention output (out-proj operand)
+            ob=op_empty(rows, C, lp, device),                            # attention output (out-proj operand)
             t1n=torch.empty((rows, C), dtype=f32, device=device),
-            hf=torch.empty((rows, FF), dtype=lp, device=device),
+            hf=op_empty(rows, FF, lp, device),
             ws=torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=device),
-            cws=torch.empty(native.chain_ws_numel(rows), dtype=torch.float32, device=device),
             layer0_done=False, stream=None)
+        if chain:
+            st["cws"] = torch.empty(native.chain_ws_numel(rows), dtype=f32, device=device)
+        else:
+            # the N = C out-projection / fc2 GEMMs of the split policy run split-K into KSP fp32
+            # partial blocks of t1 (their 64 x 64 tile grid alone covers under a quarter of the
+            # CUs); the LayerNorm after each sums the blocks
+            st["ksp"] = 4 if lp == SPLIT else 1
+            st["t1"] = torch.empty((st["ksp"], rows, C), dtype=f32, device=device)
+            st["o"] = torch.empty((rows, C), dtype=f32, device=device)
+        return st
 
     def lowp_layer0(self, st, qpos, *, B, Nq, prec, first_ops_ready=False):
-        """Layer 0 up to the cross-attention core on the chain path: the zero
-        target's operands (add_cast), the self-attention in_proj, the
-        self-attention core and chain A (out_proj + norms[0] + cross Q
-        projection).  None of it reads the memory side, so the head runs it on
-        a second stream beside shared_conv / the encodings / the K/V projection
-        (the stream it runs on is recorded and joined before the first
-        cross-attention)."""
+        """Layer 0 up to the cross-attention core: the zero target's operands
+        (add_cast), the self-attention in_proj and core, out_proj + norms[0]
+        and the cross-attention Q projection (chain A on the chain path).  None
+        of it reads the memory side, so the head runs it on a second stream
+        beside shared_conv / the encodings / the K/V projection (the stream it
+        runs on is recorded and joined before the first cross-attention)."""
         prec = get_precision(prec)
         pk = self.packed(prec)
-        ch = self._chain_pack(prec)
         C, H, rows = self.embed_dims, self.embed_dims // 32, B * Nq
         l0 = pk["layers"][0]
         if not first_ops_ready:   # else written by the query embedding's last kernel (masked_view_sum_ex)
@@ -693,27 +712,82 @@ class PETRTransformerDecoder(nn.Module):
         native.gemm(st["tl"], l0["sa_w"], st["qkv"], M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
                     A2=st["tp"], lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
         self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
-        native.chain(0, st["ob"], qpos, ch["A"][0], _wo(l0), l0["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
-                     eps=self.post_norm.eps, R=None, Q=st["qc"])
+        if st["chain"]:
+            ch = self._chain_pack(prec)
+            native.chain(0, st["ob"], qpos, ch["A"][0], _wo(l0), l0["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
+                         eps=self.post_norm.eps, R=None, Q=st["qc"])
+        else:
+            self._self_out_q(st, l0, qpos, None, rows=rows, Nq=Nq, C=C)   # layer 0: zero residual
         st["layer0_done"] = True
         st["stream"] = torch.cuda.current_stream()
 
     def _self_attn(self, st, *, B, H, Nq, C):
         qkv = st["qkv"]
-        native.attention(qkv, qkv, qkv, st["ob"], B=B, H=H, Nq=Nq, Nk=Nq,
-                         q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
-                         v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
-                         o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0), workspace=st["ws"], fold_scale=True)
+        sps = 2 if qkv.dtype == SPLIT else 1
+        hs = (3 * C * Nq * sps, 32 * sps * Nq, 32 * sps)
+        native.attention(qkv, qkv, qkv, st["ob"], B=B, H=H, Nq=Nq, Nk=Nq, q_strides=hs, k_strides=hs, v_strides=hs,
+                         k_offset=C * Nq * sps, v_offset=2 * C * Nq * sps, o_strides=(Nq * C, C),
+                         scale=1.0 / math.sqrt(32.0), workspace=st["ws"], fold_scale=True)
+
+    def _self_out_q(self, st, lw, qpos, R, *, rows, Nq, C):
+        """Separate-launch path: self-attn out_proj (+ residual R; None = zero
+        target), norms[0] -> t1n and lowp(t1n + qpos), cross-attention Q."""
+        t1, ksp = st["t1"], st["ksp"]
+        w0, b0, e0 = lw["norms"][0]
+        native.gemm(st["ob"], lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=R,
+                    ldr=C if R is not None else 0, k_splits=ksp)
+        native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=st["t1n"], ldy=C, Yp=st["tp"], P=qpos,
+                            nparts=ksp)
+        native.gemm(st["tp"], lw["ca_wq"], st["qc"], M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
+                    headsplit_rows=Nq)
+
+    def _project_kv(self, pk, memb, mposb, *, B, Nk, prec):
+        """Cross-attention K / V of every layer from lowp(mem) / lowp(mem + pos)
+        in one launch, into [B][K_0..K_L-1 | V_0..V_L-1][H][Nk][32].  Returns
+        (kv, one dict per layer: k / v element offsets and the key-norm maxima).
+
+        (One launch per layer on a second stream, each joined by an event
+        before its layer's cross-attention, was measured: the later layers'
+        launches took the whole chip ahead of layer 0's cross-attention instead
+        of filling the latency-bound query-side gaps, and a per-layer launch
+        re-stages the token tile for 2 of the 12 projections -- 68-71 us each
+        against 288 / 6; profiles/r3s_kv_per_layer.txt.)"""
+        L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
+        dev = memb.device
+        kv = torch.empty((B * 2 * L * C * Nk,), dtype=prec.attn, device=dev)
+        # f16 / bf16 K: the per-64-row max |k|^2 (epilogue by-product) bounds every score,
+        # so the cross-attention kernel needs no running max (cmt_hip.h kmax2)
+        kmax2 = None
+        if prec.attn in (torch.bfloat16, torch.float16):
+            kmax2 = torch.empty((-(-B * Nk // native.PLANE_MAX_ROWS), L * H), dtype=torch.float32, device=dev)
+        if pk["kv_wp"] is not None and memb.dtype == pk["kv_wp"].dtype:
+            native.kv_proj(memb, pk["kv_wp"], kv, M=B * Nk, N=2 * L * C, bias=pk["kv_b"], A2=mposb,
+                           headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
+        else:
+            native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
+                        A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
+        return kv, [dict(k=l * C * Nk, v=(L + l) * C * Nk, kmax=kmax2, ld=L * H, p0=l * H) for l in range(L)]
+
+    def _cross_attn(self, qc, kv, ent, ob, *, B, Nq, Nk, ws, prec):
+        """Cross-attention core of one layer."""
+        L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
+        with timed("cross_attn"):
+            native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
+                             q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
+                             v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=ent["k"], v_offset=ent["v"],
+                             o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0), workspace=ws,
+                             round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=ent["kmax"],
+                             kmax_ld=ent["ld"], kmax_plane0=ent["p0"])
 
     def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands, out16=None,
                        state=None):
-        """run_rows under an f16/bf16 policy: every GEMM operand is produced in
-        the compute dtype by the kernel before it (LayerNorm writes lowp(y) and
-        lowp(y + query_pos) beside the fp32 residual stream, attention writes
-        its output in the compute dtype, FFN fc1 writes its activation in it),
-        so every GEMM stages A and W by LDS-DMA.  The residual stream, the
+        """run_rows under an f16/bf16/split policy: every GEMM operand is
+        produced in the compute format by the kernel before it (LayerNorm
+        writes lowp(y) and lowp(y + query_pos) beside the fp32 residual stream,
+        attention writes its output in it, FFN fc1 writes its activation in
+        it), so every GEMM stages A and W by LDS-DMA.  The residual stream, the
         LayerNorm statistics and the decoder outputs stay fp32.  ``state``
-        (chain path, tgt0 None): buffers from lowp_state whose layer 0 up to
+        (zero target, tgt0 None): buffers from lowp_state whose layer 0 up to
         the cross-attention core may already be queued (lowp_layer0)."""
         pk = self.packed(prec)
         L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
@@ -723,135 +797,92 @@ class PETRTransformerDecoder(nn.Module):
         rows = B * Nq
         if out is None:
             out = torch.empty((L, rows, C), dtype=f32, device=dev)
-        scale = 1.0 / math.sqrt(32.0)
         if kv_operands is None:
             memb = op_empty(B * Nk, C, lp, dev)
             mposb = torch.empty_like(memb)
             native.add_cast(mem, rows=B * Nk, C=C, Yl=memb, Yp=mposb, P=pos)
         else:
             memb, mposb = kv_operands
-        # K/V of every layer in one GEMM: K columns read lowp(mem + pos), V columns lowp(mem)
-        kv = torch.empty((B * 2 * L * C * Nk,), dtype=prec.attn, device=dev)
-        # bf16: the K columns' per-64-row max |k|^2 (epilogue by-product) bounds every score,
-        # so the cross-attention kernel needs no running max (cmt_hip.h kmax2)
-        kmax2 = None
-        if prec.attn in (torch.bfloat16, torch.float16):
-            kmax2 = torch.empty((-(-B * Nk // native.PLANE_MAX_ROWS), L * H), dtype=f32, device=dev)
-        if pk["kv_wp"] is not None and memb.dtype == pk["kv_wp"].dtype:
-            native.kv_proj(memb, pk["kv_wp"], kv, M=B * Nk, N=2 * L * C, bias=pk["kv_b"], A2=mposb,
-                           headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
-        else:
-            native.gemm(memb, pk["kv_w"], kv, M=B * Nk, N=2 * L * C, K=C, lda=C, ldw=C, ldc=0, bias=pk["kv_b"],
-                        A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
-        # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114).
-        # The chains never read the layer-0 target (chain A's residual is None), so there
-        # it is only an output buffer and the first operands come from add_cast's zeros.
-        use_chain = self._chain_ok() and lp != SPLIT and OPTIONS.chain
-        if use_chain and tgt0 is None:
+        # K columns read lowp(mem + pos), V columns lowp(mem)
+        kv, kvl = self._project_kv(pk, memb, mposb, B=B, Nk=Nk, prec=prec)
+        use_chain = self._use_chain(prec)
+        if tgt0 is None:
+            # target = zeros_like(query_embed) in every CMT transformer (cmt_transformer.py:114):
+            # layer 0's residual is None and its first operands come from add_cast's zeros
             st = state if state is not None else self.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
             if not st["layer0_done"]:
                 self.lowp_layer0(st, qpos, B=B, Nq=Nq, prec=prec)
             elif st["stream"] is not None and st["stream"] != torch.cuda.current_stream():
                 torch.cuda.current_stream().wait_stream(st["stream"])   # join the layer-0 side stream
-            return self._chain_layers(st, qpos, kv, kmax2, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
-                                      prec=prec, out16=out16)
+            if use_chain:
+                return self._chain_layers(st, qpos, kv, kvl, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
+                                          prec=prec, out16=out16)
+            return self._sep_layers(st, qpos, kv, kvl, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags,
+                                    prec=prec, out16=out16, l0_done=True)
         if state is not None:
-            raise ValueError("run_rows: a lowp_state applies to the chain path with a zero target only")
-        if tgt0 is not None:
-            tgt = tgt0.clone()
-        elif use_chain:
-            tgt = torch.empty((rows, C), dtype=f32, device=dev)
-        else:
-            tgt = torch.zeros((rows, C), dtype=f32, device=dev)
-        tl = op_empty(rows, C, lp, dev)                            # lowp(tgt)
-        tp = torch.empty_like(tl)                                  # lowp(tgt + qpos)
-        native.add_cast(tgt if (tgt0 is not None or not use_chain) else None, rows=rows, C=C, Yl=tl, Yp=tp,
-                        P=qpos)
-        # self-attention Q|K|V head-split; a split self-attention core (the 'ref' policy) takes
-        # them as f16 pairs, 64 16-bit elements per (head, row): hi 32 | lo 32
-        sps = 2 if prec.self_attn == SPLIT else 1
-        qkv = torch.empty((B * 3 * C * Nq * sps,), dtype=prec.self_attn, device=dev)
-        qc = torch.empty((B * C * Nq,), dtype=prec.attn, device=dev)
-        ob = op_empty(rows, C, lp, dev)                            # attention output (out-proj operand)
-        # the N = C out-projection / fc2 GEMMs of the split policy run split-K into KSP fp32
-        # partial blocks of t1 (their 64 x 64 tile grid alone covers under a quarter of the
-        # CUs); the LayerNorm after each sums the blocks
-        KSP = 4 if lp == SPLIT and not use_chain else 1
-        t1 = torch.empty((KSP, rows, C), dtype=f32, device=dev)
-        t1n = torch.empty((rows, C), dtype=f32, device=dev)
-        o = torch.empty_like(t1n)
-        FF = pk["layers"][0]["f1_w"].shape[0]
-        hf = op_empty(rows, FF, lp, dev)
-        ws_bytes = max(native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nk),
-                       native.attn_workspace_bytes(B=B, H=H, Nq=Nq, Nk=Nq))
-        ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
-        pw, pb, _pe = pk["post"]
+            raise ValueError("run_rows: a lowp_state applies to a zero target only")
+        st = self.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
+        tgt = st["tgt"]
+        tgt.copy_(tgt0)
+        native.add_cast(tgt, rows=rows, C=C, Yl=st["tl"], Yp=st["tp"], P=qpos)
         if use_chain:
             # per layer: self-attn core, chain A (out_proj + norms[0] + cross Q proj),
             # cross-attn core, chain B1 (out_proj + norms[1] + FFN quarter -> fp32 partials),
             # chain B2 (partials -> norms[2] + post_norm + next layer's in_proj) -- see rowchain.hip
             ch = self._chain_pack(prec)
-            cws = torch.empty(native.chain_ws_numel(rows), dtype=torch.float32, device=dev)
             eps = self.post_norm.eps
             l0 = pk["layers"][0]
-            native.gemm(tl, l0["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=l0["sa_b"],
-                        A2=tp, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
+            native.gemm(st["tl"], l0["sa_w"], st["qkv"], M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0,
+                        bias=l0["sa_b"], A2=st["tp"], lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
             for l, lw in enumerate(pk["layers"]):
-                native.attention(qkv, qkv, qkv, ob, B=B, H=H, Nq=Nq, Nk=Nq,
-                                 q_strides=(3 * C * Nq, 32 * Nq, 32), k_strides=(3 * C * Nq, 32 * Nq, 32),
-                                 v_strides=(3 * C * Nq, 32 * Nq, 32), k_offset=C * Nq, v_offset=2 * C * Nq,
-                                 o_strides=(Nq * C, C), scale=scale, workspace=ws, fold_scale=True)
-                native.chain(0, ob, qpos, ch["A"][l], lw["sa_ow"], lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
-                             R=tgt if (l > 0 or tgt0 is not None) else None, Q=qc)
-                with timed("cross_attn"):
-                    native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
-                                     q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
-                                     v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
-                                     v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
-                                     round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2,
-                                     kmax_ld=L * H, kmax_plane0=l * H)
+                self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
+                native.chain(0, st["ob"], qpos, ch["A"][l], lw["sa_ow"], lw["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
+                             eps=eps, R=tgt, Q=st["qc"])
+                self._cross_attn(st["qc"], kv, kvl[l], st["ob"], B=B, Nq=Nq, Nk=Nk, ws=st["ws"], prec=prec)
                 nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
-                native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
-                             R=t1n, W2=lw["f2_wp"], WS=cws)
+                native.chain(1, st["ob"], None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
+                             R=st["t1n"], W2=lw["f2_wp"], WS=st["cws"])
                 native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                              Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
-                             Q=qkv if nxt is not None else None, WS=cws, OUT16=out16)
+                             Q=st["qkv"] if nxt is not None else None, WS=st["cws"], OUT16=out16)
             return out
+        return self._sep_layers(st, qpos, kv, kvl, B=B, Nk=Nk, Nq=Nq, out=out, post_flags=post_flags, prec=prec,
+                                out16=out16, l0_done=False)
+
+    def _sep_layers(self, st, qpos, kv, kvl, *, B, Nk, Nq, out, post_flags, prec, out16, l0_done):
+        """Separate-launch decoder layers (the split policy, or CMT_CHAIN=0).
+        ``l0_done``: layer 0 up to its cross-attention core already queued
+        (lowp_layer0, zero target)."""
+        pk = self.packed(prec)
+        L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
+        rows = B * Nq
+        lp = prec.gemm
+        tgt, tl, tp, qkv, ob, t1n, hf, t1, o, ws, ksp = (st[k] for k in ("tgt", "tl", "tp", "qkv", "ob", "t1n", "hf",
+                                                                         "t1", "o", "ws", "ksp"))
+        FF = hf.shape[-1]
+        pw, pb, _pe = pk["post"]
         for l, lw in enumerate(pk["layers"]):
-            # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
-            native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
-                        A2=tp, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
-            hs = (3 * C * Nq * sps, 32 * sps * Nq, 32 * sps)
-            native.attention(qkv, qkv, qkv, ob, B=B, H=H, Nq=Nq, Nk=Nq, q_strides=hs, k_strides=hs, v_strides=hs,
-                             k_offset=C * Nq * sps, v_offset=2 * C * Nq * sps, o_strides=(Nq * C, C), scale=scale,
-                             workspace=ws, fold_scale=True)
-            w0, b0, e0 = lw["norms"][0]
-            native.gemm(ob, lw["sa_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["sa_ob"], R=tgt,
-                        ldr=C, k_splits=KSP)
-            native.layernorm_ex(t1, w0, b0, rows=rows, C=C, ldx=C, eps=e0, Y=t1n, ldy=C, Yp=tp, P=qpos, nparts=KSP)
-            # --- cross attention: q = lowp(x + qpos); K/V from the hoisted GEMM
-            native.gemm(tp, lw["ca_wq"], qc, M=rows, N=C, K=C, lda=C, ldw=C, ldc=0, bias=lw["ca_bq"],
-                        headsplit_rows=Nq)
-            with timed("cross_attn"):
-                native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
-                                 q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
-                                 v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
-                                 v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=scale, workspace=ws,
-                                 round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2, kmax_ld=L * H,
-                                 kmax_plane0=l * H)
+            if l > 0 or not l0_done:
+                # --- self attention: Q|K columns read lowp(tgt + qpos), V columns lowp(tgt)
+                native.gemm(tl, lw["sa_w"], qkv, M=rows, N=3 * C, K=C, lda=C, ldw=C, ldc=0, bias=lw["sa_b"],
+                            A2=tp, lda2=C, a2_cols=2 * C, headsplit_rows=Nq)
+                self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
+                self._self_out_q(st, lw, qpos, tgt, rows=rows, Nq=Nq, C=C)
+            # --- cross attention: q = lowp(x + qpos); K/V from _project_kv
+            self._cross_attn(st["qc"], kv, kvl[l], ob, B=B, Nq=Nq, Nk=Nk, ws=ws, prec=prec)
             w1, b1, e1 = lw["norms"][1]
             native.gemm(ob, lw["ca_ow"], t1, M=rows, N=C, K=C, lda=C, ldw=C, ldc=C, bias=lw["ca_ob"], R=t1n,
-                        ldr=C, k_splits=KSP)
-            native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl, nparts=KSP)
+                        ldr=C, k_splits=ksp)
+            native.layernorm_ex(t1, w1, b1, rows=rows, C=C, ldx=C, eps=e1, Y=o, ldy=C, Yl=tl, nparts=ksp)
             # --- FFN (fc1 activation written in the compute dtype)
             native.gemm(tl, lw["f1_w"], hf, M=rows, N=FF, K=C, lda=C, ldw=C, ldc=FF, bias=lw["f1_b"], relu=True)
             # --- fc2 + residual + norms.2 -> next query (fp32 + both lowp operands), + post_norm -> out[l]
             w2, b2, e2 = lw["norms"][2]
             native.gemm(hf, lw["f2_w"], t1, M=rows, N=C, K=FF, lda=FF, ldw=FF, ldc=C, bias=lw["f2_b"], R=o,
-                        ldr=C, k_splits=KSP)
+                        ldr=C, k_splits=ksp)
             native.layernorm_ex(t1, w2, b2, rows=rows, C=C, ldx=C, eps=e2, Y=tgt, ldy=C, Yl=tl, Yp=tp, P=qpos,
                                 W2=pw, B2=pb, Y2=out, ldy2=C, flags2=post_flags, y2_offset=l * rows * C,
-                                nparts=KSP)
+                                nparts=ksp)
         if out16 is not None:
             if lp == SPLIT:
                 native.split_rows(out.view(-1, C), out16.view(-1, 2, C))
@@ -859,7 +890,7 @@ class PETRTransformerDecoder(nn.Module):
                 native.cast(out, out16)
         return out
 
-    def _chain_layers(self, st, qpos, kv, kmax2, *, B, Nk, Nq, out, post_flags, prec, out16):
+    def _chain_layers(self, st, qpos, kv, kvl, *, B, Nk, Nq, out, post_flags, prec, out16):
         """Chain path from layer 0's cross-attention core on (layer 0's self
         block already queued by lowp_layer0): per layer the cross-attention
         core, chain B1, chain B2 (which also runs the next layer's in_proj),
@@ -875,13 +906,7 @@ class PETRTransformerDecoder(nn.Module):
                 self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
                 native.chain(0, ob, qpos, ch["A"][l], _wo(lw), lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
                              R=tgt, Q=qc)
-            with timed("cross_attn"):
-                native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
-                                 q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
-                                 v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=l * C * Nk,
-                                 v_offset=(L + l) * C * Nk, o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0),
-                                 workspace=ws, round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=kmax2,
-                                 kmax_ld=L * H, kmax_plane0=l * H)
+            self._cross_attn(qc, kv, kvl[l], ob, B=B, Nq=Nq, Nk=Nk, ws=ws, prec=prec)
             nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
             native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
                          R=t1n, W2=lw["f2_wp"], WS=cws)

@@ -301,13 +301,18 @@ def kv_pack(W):
     return W.reshape(n // 32, 32, 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
 
 
-def kv_proj(A, Wp, C, *, M, N, bias=None, A2=None, headsplit_rows, plane_max2=None, plane_max_cols=0):
-    """All-layer cross-attention K/V projection (cmt_kv_proj): columns < N/2 read
-    A2 (lowp(mem + pos)) when given, the rest A (lowp(mem)); Wp from kv_pack;
-    head-split C; optional per-64-row key-norm maxima (as cmt_gemm)."""
+def kv_proj(A, Wp, C, *, M, N, bias=None, A2=None, headsplit_rows, plane_max2=None, plane_max_cols=0,
+            c_offset=0, c_bstride=0):
+    """Cross-attention K/V projection (cmt_kv_proj): columns < N/2 read A2
+    (lowp(mem + pos)) when given, the rest A (lowp(mem)); Wp from kv_pack;
+    head-split C starting ``c_offset`` elements in, batch stride ``c_bstride``
+    elements (0: the launch's own N/32 planes); optional per-64-row key-norm
+    maxima (as cmt_gemm)."""
     g = _gemm_args(A, Wp, C, M=M, N=N, K=256, lda=256, ldw=256, ldc=0, bias=bias, A2=A2,
                    lda2=256 if A2 is not None else 0, a2_cols=N // 2 if A2 is not None else 0,
-                   headsplit_rows=headsplit_rows)
+                   headsplit_rows=headsplit_rows, c_offset=c_offset, c_bstride=c_bstride)
+    if C.numel() < c_offset + (M // headsplit_rows - 1) * (c_bstride or N * headsplit_rows) + N * headsplit_rows:
+        raise RuntimeError("kv_proj: C is too small for the launch's planes")
     if plane_max2 is not None:
         _dev(plane_max2)
         if plane_max2.dtype != torch.float32 or plane_max2.numel() < -(-M // PLANE_MAX_ROWS) * (plane_max_cols // 32):

@@ -22,7 +22,8 @@ def short(name):
     return n[:90]
 
 
-starts = [i for i, r in enumerate(rows) if "gemm_dma_kernel" in r["Kernel_Name"] and "Li1EEEv" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "gemm_dma_kernel" in r["Kernel_Name"]
+          and ("Li1EEEv" in r["Kernel_Name"] or "Li1ELb" in r["Kernel_Name"])]
 if len(starts) < back + 1:
     sys.exit(f"only {len(starts)} frames in the trace")
 i0, i1 = starts[-back - 1], starts[-back]

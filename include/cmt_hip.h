@@ -139,7 +139,11 @@ int cmt_gemm(const cmt_gemm_args* args, void* stream);
  * in select mode on exactly the first N/2 columns, N % (256 * parts) == 0,
  * optional plane_max2.  W is in the FRAGMENT-PACKED layout
  *   Wp[((p * 16 + ks) * 64 + lane) * 8 + e] = W[32 p + (lane & 31)][16 ks + 8 (lane >> 5) + e]
- * (torch: W.view(N/32, 32, 16, 2, 8).permute(0, 2, 3, 1, 4)), ldw unused. */
+ * (torch: W.view(N/32, 32, 16, 2, 8).permute(0, 2, 3, 1, 4)), ldw unused.
+ * c_bstride (16-bit elements, 0: (N/32) * rows_per_batch * 32) is the batch
+ * stride of the head-split C, so one layer's K and V planes can be written into
+ * a larger [B][planes][Nk][32] buffer (one launch per layer, C pointing at the
+ * layer's first plane). */
 int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
 
 /* ------------------------------------------------------------------------

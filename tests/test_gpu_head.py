@@ -289,11 +289,13 @@ def test_graph_replay_with_new_metas(dev, prec, coop):
     assert not torch.equal(eager_a[0][0]["cls_logits"], eager_b[0][0]["cls_logits"])
 
 
-@pytest.mark.parametrize("warm", ["ref", "none"])
-def test_second_stream_matches_single_stream(dev, warm):
-    """The two-stream schedule (query side + layer 0 self block and the encoder
-    MLP halves on a second stream) gives bit-identical outputs to the
-    single-stream schedule, including on the first low-precision forward of a
+@pytest.mark.parametrize("prec,warm", [("bf16", "ref"), ("bf16", "none"), ("ref", "bf16"), ("ref", "none"),
+                                       ("fp16", "none")])
+def test_second_stream_matches_single_stream(dev, prec, warm):
+    """The two-stream schedule (query side + layer 0 up to the cross-attention
+    core and the encoder MLP halves on a second stream) gives bit-identical
+    outputs to the single-stream schedule, for the chain path (bf16 / fp16) and
+    the split policy's separate launches ('ref'), including on the first forward of a
     head (weight packs built inside that forward must be built on the main
     stream: a pack first built on the second stream was read by the main
     stream's K/V projection unordered) and with the allocator's cached memory
@@ -313,10 +315,10 @@ def test_second_stream_matches_single_stream(dev, warm):
         torch.cuda.synchronize()
         return {k: v.clone() for k, v in out.items()}
 
-    if warm == "ref":
-        set_precision("ref")
+    if warm != "none":
+        set_precision(warm)
         run("1")
-    set_precision("bf16")
+    set_precision(prec)
     try:
         two = run("1")
         one = run("0")

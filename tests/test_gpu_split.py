@@ -395,3 +395,49 @@ def test_kvproj_split(N, dev, B, S):
     nb = -(-M // 64)
     pref = torch.cat([ss, torch.zeros(nb * 64 - M, ss.shape[1], dtype=ss.dtype)], 0).view(nb, 64, -1).amax(1)
     assert torch.allclose(pm.cpu().double().view(nb, -1), pref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("form", ["split", "bf16"])
+@pytest.mark.parametrize("B,S", [(2, 4100), (1, 1000)])
+def test_kvproj_per_layer_equals_all_layers(N, dev, form, B, S):
+    """One cmt_kv_proj launch per layer (c_offset at the layer's K plane,
+    c_bstride = the whole [L][K|V][H] buffer per batch element, the decoder's
+    K/V-stream schedule) writes the same K/V values and key-norm maxima bit for
+    bit as the all-layer launch, into the per-layer layout [B][L][K|V][H][S][32]."""
+    g = torch.Generator().manual_seed(7 * B + S)
+    C, L, H = 256, 3, 8
+    M = B * S
+    A = torch.randn(M, C, generator=g)
+    A2 = torch.randn(M, C, generator=g)
+    Wk = [torch.randn(C, C, generator=g) / 16 for _ in range(L)]
+    Wv = [torch.randn(C, C, generator=g) / 16 for _ in range(L)]
+    bk = [torch.randn(C, generator=g) for _ in range(L)]
+    bv = [torch.randn(C, generator=g) for _ in range(L)]
+    if form == "split":
+        op = lambda x: _pair(x).to(dev)   # noqa: E731
+
+        def pack(w):
+            wb = _pair(w).view(torch.float16)
+            return torch.cat([N.kv_pack(wb[:, 0].contiguous()), N.kv_pack(wb[:, 1].contiguous())]).view(SPLIT).to(dev)
+        cdt = torch.float16
+    else:
+        op = lambda x: x.to(torch.bfloat16).to(dev)   # noqa: E731
+        pack = lambda w: N.kv_pack(w.to(torch.bfloat16)).to(dev)   # noqa: E731
+        cdt = torch.bfloat16
+    a, a2 = op(A), op(A2)
+    E = -(-M // 64)
+    full = torch.empty(B * 2 * L * C * S, dtype=cdt, device=dev)
+    pm_full = torch.empty(E, L * H, device=dev)
+    N.kv_proj(a, pack(torch.cat(Wk + Wv)), full, M=M, N=2 * L * C, bias=torch.cat(bk + bv).to(dev), A2=a2,
+              headsplit_rows=S, plane_max2=pm_full, plane_max_cols=L * C)
+    per = torch.full((B * 2 * L * C * S,), float("nan"), dtype=cdt, device=dev)
+    pm_per = torch.empty(L, E, H, device=dev)
+    for l in range(L):
+        N.kv_proj(a, pack(torch.cat([Wk[l], Wv[l]])), per, M=M, N=2 * C, bias=torch.cat([bk[l], bv[l]]).to(dev),
+                  A2=a2, headsplit_rows=S, plane_max2=pm_per[l], plane_max_cols=C, c_offset=2 * l * C * S,
+                  c_bstride=2 * L * C * S)
+    torch.cuda.synchronize()
+    f = full.cpu().view(torch.int16).view(B, 2, L, H, S, 32)        # [b][K|V][layer][head]
+    p = per.cpu().view(torch.int16).view(B, L, 2, H, S, 32)         # [b][layer][K|V][head]
+    assert torch.equal(f.permute(0, 2, 1, 3, 4, 5), p)
+    assert torch.equal(pm_full.cpu().view(E, L, H).permute(1, 0, 2), pm_per.cpu())
