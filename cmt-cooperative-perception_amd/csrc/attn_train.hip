@@ -376,6 +376,323 @@ __global__ __launch_bounds__(256) void train_dkv_kernel(AP p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// f16 MFMA forms of the three kernels for the flash-attn fp16 core
+// (fp16_inputs): q, k, v, dO, P and dS enter every product as f16 -- the
+// operands flash-attn 0.2.2's fp16 forward / backward multiply -- on
+// v_mfma_f32_32x32x16_f16 (16x the rate of the f32 MFMA), fp32 accumulate;
+// softmax statistics, dS = P (dP - delta) and every accumulator stay fp32.
+// Tiles of 64 keys (queries in the dK/dV kernel) are staged in LDS as f16,
+// row-major [row][32 d] (16-byte chunks XOR-swizzled by (row >> 2) & 3: the
+// 16-lane groups of ds_read_b128 hit distinct bank slots) and, where a tile is
+// the A operand of a product over its rows, transposed [32 d][64 rows].  A
+// product whose B operand is an accumulator tile (P^T, dS^T, P, dS) takes the
+// accumulator's own row order as its k order: register 8 ss + j of lane half
+// lh is row (j & 3) + 16 ss + 8 (j >> 2) + 4 lh, and the transposed A reads
+// the same rows as two 4-element runs.
+// MASK: the DN mask can hide keys; DROP: dropout (counter hash, as above); the
+// dropout scale 1 / (1 - p) multiplies O, dV and dP' once instead of each P.
+// ---------------------------------------------------------------------------
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+constexpr int RMB = 64;    // bytes per row-major LDS row (32 d)
+constexpr int TRB = 128;   // bytes per transposed LDS row (64 rows)
+
+__device__ __forceinline__ int rm_off(int row, int chunk) { return row * RMB + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// stage rows r0 .. r0+63 of X (fp32, row stride rs; rows >= nrows are zero) as f16
+// into the row-major image rm and / or the transposed image tr
+__device__ __forceinline__ void stage16(char* rm, char* tr, const float* X, int64_t rs, int r0, int nrows, int tid) {
+    const int r = tid >> 2, c = tid & 3;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
+    if (r0 + r < nrows) {
+        a = *(const f32x4*)(X + (int64_t)(r0 + r) * rs + 8 * c);
+        b = *(const f32x4*)(X + (int64_t)(r0 + r) * rs + 8 * c + 4);
+    }
+    h8_t hv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        hv[j] = (_Float16)a[j];
+        hv[4 + j] = (_Float16)b[j];
+    }
+    if (rm) *(h8_t*)(rm + rm_off(r, c)) = hv;
+    if (tr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *(_Float16*)(tr + (8 * c + j) * TRB + 2 * r) = hv[j];
+    }
+}
+
+// A fragment of rows rb*32 + (lane & 31) of a row-major image, d half kk
+__device__ __forceinline__ h8_t frag_rm(const char* rm, int rb, int kk, int lane) {
+    return *(const h8_t*)(rm + rm_off(rb * 32 + (lane & 31), 2 * kk + (lane >> 5)));
+}
+// A fragment of a transposed image: row d = lane & 31, the 8 rows of k half ss of block rb
+// in the accumulator order (two 4-element runs)
+__device__ __forceinline__ h8_t frag_tr(const char* tr, int rb, int ss, int lane) {
+    const char* base = tr + (lane & 31) * TRB + 2 * (rb * 32 + 16 * ss + 4 * (lane >> 5));
+    const h4_t lo = *(const h4_t*)base, hi = *(const h4_t*)(base + 16);
+    return h8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// B fragment from accumulator registers 8 ss .. 8 ss + 7 (rounded to f16)
+__device__ __forceinline__ h8_t frag_acc(const f32x16& x, int ss) {
+    h8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (_Float16)x[8 * ss + j];
+    return v;
+}
+// a lane's own row of 32 fp32 values as the two B fragments (d = 16 kk + 8 lh + j)
+__device__ __forceinline__ void own_row16(const float* row, int lh, h8_t (&f)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const f32x4 a = *(const f32x4*)(row + 16 * kk + 8 * lh), b = *(const f32x4*)(row + 16 * kk + 8 * lh + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f[kk][j] = (_Float16)a[j];
+            f[kk][4 + j] = (_Float16)b[j];
+        }
+    }
+}
+__device__ __forceinline__ f32x16 mma16(h8_t a, h8_t b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <bool MASK, bool DROP>
+__global__ __launch_bounds__(256) void train16_fwd_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) char Ks[KT * RMB];   // [key][d]
+    __shared__ __attribute__((aligned(16))) char Vt[D * TRB];    // [d][key]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H, split = blockIdx.z;
+    const float* Qb = a.Q + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
+    const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
+    const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const int qc = min(q, a.Nq - 1);
+    h8_t qf[2];
+    own_row16(Qb + (int64_t)qc * a.q_rs, lh, qf);
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int t0 = split * p.tiles_per_split, t1 = min(ntiles, t0 + p.tiles_per_split);
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    float m_run = -__builtin_inff(), l_run = 0.f;
+    for (int t = t0; t < t1; ++t) {
+        __syncthreads();
+        stage16(Ks, nullptr, Kb, a.k_rs, t * KT, a.Nk, tid);
+        stage16(nullptr, Vt, Vb, a.v_rs, t * KT, a.Nk, tid);
+        __syncthreads();
+        const bool edge = (t + 1) * KT > a.Nk;
+        f32x16 s[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) s[kb] = mma16(frag_rm(Ks, kb, kk, lane), qf[kk], s[kb]);   // S^T
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = t * KT + kb * 32 + key_of(r, lh);
+                const bool hide = (edge && k >= a.Nk) || (MASK && masked(a, q, k));
+                s[kb][r] = hide ? -__builtin_inff() : s[kb][r] * p.c;
+            }
+        }
+        float mt = -__builtin_inff();
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kb][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_run, mt);
+        const float m_use = m_new == -__builtin_inff() ? 0.f : m_new;   // fully masked so far
+        const float alpha = exp2f(m_run - m_use);
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = exp2f(s[kb][r] - m_use);
+                ls += e;
+                float pe = e;
+                if (DROP) {
+                    const int k = t * KT + kb * 32 + key_of(r, lh);
+                    pe = keep(p, bh, q, k) ? pe : 0.f;
+                }
+                s[kb][r] = pe;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) o = mma16(frag_tr(Vt, kb, ss, lane), frag_acc(s[kb], ss), o);   // O^T += V^T P^T
+    }
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    if (DROP) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= p.keep_scale;
+    }
+    if (q >= a.Nq) return;
+    if (a.kv_splits <= 1) {
+        const float inv = 1.f / l_tot;
+        float* Ob = a.O + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs + (int64_t)q * a.o_rs;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Ob[key_of(r, lh)] = r16(o[r] * inv);
+        if (lh == 0) a.LSE[(int64_t)bh * a.Nq + q] = m_run + log2f(l_tot);
+    } else {
+        float* ws = (float*)a.workspace;
+        const int64_t rows = (int64_t)a.B * a.H * a.Nq;
+        const int64_t row = (int64_t)split * rows + (int64_t)bh * a.Nq + q;
+        float* Op = ws + row * D;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Op[key_of(r, lh)] = o[r];
+        if (lh == 0) {
+            ws[(int64_t)a.kv_splits * rows * D + row] = m_run;
+            ws[(int64_t)a.kv_splits * rows * (D + 1) + row] = l_tot;
+        }
+    }
+}
+
+template <bool MASK, bool DROP>
+__global__ __launch_bounds__(256) void train16_dq_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) char Ks[KT * RMB];   // [key][d]
+    __shared__ __attribute__((aligned(16))) char Kt[D * TRB];    // [d][key]
+    __shared__ __attribute__((aligned(16))) char Vs[KT * RMB];   // [key][d]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H, split = blockIdx.z;
+    const float* Qb = a.Q + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
+    const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
+    const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
+    const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const int qc = min(q, a.Nq - 1);
+    h8_t qf[2], df[2];
+    own_row16(Qb + (int64_t)qc * a.q_rs, lh, qf);
+    own_row16(dOb + (int64_t)qc * a.o_rs, lh, df);
+    const float lse = a.LSE[(int64_t)bh * a.Nq + qc];
+    const float dl = a.delta[(int64_t)bh * a.Nq + qc];
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int t0 = split * p.tiles_per_split, t1 = min(ntiles, t0 + p.tiles_per_split);
+    f32x16 dq;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+    for (int t = t0; t < t1; ++t) {
+        __syncthreads();
+        stage16(Ks, Kt, Kb, a.k_rs, t * KT, a.Nk, tid);
+        stage16(Vs, nullptr, Vb, a.v_rs, t * KT, a.Nk, tid);
+        __syncthreads();
+        const bool edge = (t + 1) * KT > a.Nk;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                s = mma16(frag_rm(Ks, kb, kk, lane), qf[kk], s);      // S^T
+                dp = mma16(frag_rm(Vs, kb, kk, lane), df[kk], dp);    // dP^T = V dO^T
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = t * KT + kb * 32 + key_of(r, lh);
+                const bool hide = (edge && k >= a.Nk) || (MASK && masked(a, q, k));
+                const float pr = hide ? 0.f : exp2f(s[r] * p.c - lse);
+                float g = dp[r];
+                if (DROP) g = keep(p, bh, q, k) ? g * p.keep_scale : 0.f;
+                s[r] = pr * (g - dl);                                   // dS^T
+            }
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) dq = mma16(frag_tr(Kt, kb, ss, lane), frag_acc(s, ss), dq);   // dQ^T += K^T dS^T
+        }
+    }
+    if (q >= a.Nq) return;
+    float* dQb = a.dQ + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs + (int64_t)q * a.q_rs;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float v = dq[r] * a.scale;
+        if (a.kv_splits > 1) atomicAdd(dQb + key_of(r, lh), v);
+        else dQb[key_of(r, lh)] = v;
+    }
+}
+
+template <bool MASK, bool DROP>
+__global__ __launch_bounds__(256) void train16_dkv_kernel(AP p) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) char Qs[KT * RMB];   // [q][d]
+    __shared__ __attribute__((aligned(16))) char Qt[D * TRB];    // [d][q]
+    __shared__ __attribute__((aligned(16))) char Ds[KT * RMB];   // dO [q][d]
+    __shared__ __attribute__((aligned(16))) char Dt[D * TRB];    // dO [d][q]
+    __shared__ float Ls[KT], Dl[KT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+    const float* Qb = a.Q + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs;
+    const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
+    const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
+    const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
+    const int k = blockIdx.x * 128 + wave * 32 + lr;
+    const int kc = min(k, a.Nk - 1);
+    h8_t kf[2], vf[2];
+    own_row16(Kb + (int64_t)kc * a.k_rs, lh, kf);
+    own_row16(Vb + (int64_t)kc * a.v_rs, lh, vf);
+    f32x16 dk, dv;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
+    const int nqt = (a.Nq + KT - 1) / KT;
+    for (int t = 0; t < nqt; ++t) {
+        __syncthreads();
+        stage16(Qs, Qt, Qb, a.q_rs, t * KT, a.Nq, tid);
+        stage16(Ds, Dt, dOb, a.o_rs, t * KT, a.Nq, tid);
+        if (tid < KT) {
+            const int qq = min(t * KT + tid, a.Nq - 1);
+            Ls[tid] = a.LSE[(int64_t)bh * a.Nq + qq];
+            Dl[tid] = a.delta[(int64_t)bh * a.Nq + qq];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                s = mma16(frag_rm(Qs, qb, kk, lane), kf[kk], s);      // S = Q K^T (lane = key)
+                dp = mma16(frag_rm(Ds, qb, kk, lane), vf[kk], dp);    // dP = dO V^T
+            }
+            f32x16 pd;                                                 // P, dropped (dV operand; scale later)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int qi = qb * 32 + key_of(r, lh), qq = t * KT + qi;
+                const bool valid = qq < a.Nq && k < a.Nk && !(MASK && masked(a, qq, k));
+                const float pr = valid ? exp2f(s[r] * p.c - Ls[qi]) : 0.f;
+                float g = dp[r], pe = pr;
+                if (DROP) {
+                    const bool kp = keep(p, bh, qq, k);
+                    g = kp ? g * p.keep_scale : 0.f;
+                    pe = kp ? pe : 0.f;
+                }
+                pd[r] = pe;
+                s[r] = pr * (g - Dl[qi]);                              // dS
+            }
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                dv = mma16(frag_tr(Dt, qb, ss, lane), frag_acc(pd, ss), dv);   // dV^T += dO^T P
+                dk = mma16(frag_tr(Qt, qb, ss, lane), frag_acc(s, ss), dk);    // dK^T += Q^T dS
+            }
+        }
+    }
+    if (k >= a.Nk) return;
+    float* dKb = a.dK + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs + (int64_t)k * a.k_rs;
+    float* dVb = a.dV + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs + (int64_t)k * a.v_rs;
+    const float vs = DROP ? p.keep_scale : 1.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        dKb[key_of(r, lh)] = dk[r] * a.scale;
+        dVb[key_of(r, lh)] = dv[r] * vs;
+    }
+}
+
 AP make_ap(const cmt_attn_train_args& a, int splits) {
     AP p;
     p.a = a;
@@ -426,7 +743,16 @@ extern "C" int cmt_attn_train_fwd(const cmt_attn_train_args* ap, void* stream) {
         return cmt_fail(CMT_EWORKSPACE, "cmt_attn_train_fwd: workspace too small");
     AP p = make_ap(*ap, splits);
     hipStream_t s = (hipStream_t)stream;
-    train_fwd_kernel<<<dim3(cdiv(ap->Nq, 128), ap->B * ap->H, splits), 256, 0, s>>>(p);
+    const dim3 grid(cdiv(ap->Nq, 128), ap->B * ap->H, splits);
+    if (ap->fp16_inputs) {
+        const bool mask = ap->dn_pad > 0, drop = ap->dropout_p > 0.f;
+        if (mask && drop) train16_fwd_kernel<true, true><<<grid, 256, 0, s>>>(p);
+        else if (mask) train16_fwd_kernel<true, false><<<grid, 256, 0, s>>>(p);
+        else if (drop) train16_fwd_kernel<false, true><<<grid, 256, 0, s>>>(p);
+        else train16_fwd_kernel<false, false><<<grid, 256, 0, s>>>(p);
+    } else {
+        train_fwd_kernel<<<grid, 256, 0, s>>>(p);
+    }
     if (splits > 1) {
         const int64_t n = (int64_t)ap->B * ap->H * ap->Nq * D;
         train_combine_kernel<<<(unsigned)cdiv64(n, 256), 256, 0, s>>>(p);
@@ -453,7 +779,25 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
                 hipMemset2DAsync(ap->dQ + (int64_t)b * ap->q_bs + (int64_t)h * ap->q_hs, ap->q_rs * sizeof(float), 0,
                                  D * sizeof(float), ap->Nq, s);
     }
-    train_dq_kernel<<<dim3(cdiv(ap->Nq, 128), ap->B * ap->H, qs), 256, 0, s>>>(p);
-    train_dkv_kernel<<<dim3(cdiv(ap->Nk, 128), ap->B * ap->H), 256, 0, s>>>(p);
+    const dim3 gq(cdiv(ap->Nq, 128), ap->B * ap->H, qs), gk(cdiv(ap->Nk, 128), ap->B * ap->H);
+    if (ap->fp16_inputs) {
+        const bool mask = ap->dn_pad > 0, drop = ap->dropout_p > 0.f;
+        if (mask && drop) {
+            train16_dq_kernel<true, true><<<gq, 256, 0, s>>>(p);
+            train16_dkv_kernel<true, true><<<gk, 256, 0, s>>>(p);
+        } else if (mask) {
+            train16_dq_kernel<true, false><<<gq, 256, 0, s>>>(p);
+            train16_dkv_kernel<true, false><<<gk, 256, 0, s>>>(p);
+        } else if (drop) {
+            train16_dq_kernel<false, true><<<gq, 256, 0, s>>>(p);
+            train16_dkv_kernel<false, true><<<gk, 256, 0, s>>>(p);
+        } else {
+            train16_dq_kernel<false, false><<<gq, 256, 0, s>>>(p);
+            train16_dkv_kernel<false, false><<<gk, 256, 0, s>>>(p);
+        }
+    } else {
+        train_dq_kernel<<<gq, 256, 0, s>>>(p);
+        train_dkv_kernel<<<gk, 256, 0, s>>>(p);
+    }
     return cmt_check_launch("cmt_attn_train_bwd");
 }

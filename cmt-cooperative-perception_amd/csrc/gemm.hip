@@ -852,6 +852,247 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
 }
 
 // ---------------------------------------------------------------------------
+// Split (CMT_F16P) GEMM for the large problems of the 'ref' policy (shared_conv,
+// the BEV / RV position MLPs): BM x 128 tiles (BM 256 or 128), 8 waves, 32-deep
+// k stages in an S-slot LDS-DMA ring.
+//
+// Each stage carries A_hi, A_lo, W_hi, W_lo of 32 k (64-byte LDS rows; 16-byte
+// chunks XOR-swizzled by (row >> 2) & 3 on the source address, so the 16-lane
+// groups of ds_read_b128 hit 16 distinct bank slots) and each 16-k step runs the
+// three products W_hi A_lo + W_lo A_hi + W_hi A_hi in the order of the 128 x 128
+// DmaTile<..., X3> -- the same fp32 accumulation sequence, so the two kernels
+// give bit-identical outputs.  Against that tile (2 stages of 64 k, 4 waves, one
+// wave per SIMD) a BM = 256 tile stages 1.33x the MFMA work per byte and keeps
+// 2 stages in flight behind the one being read (the 64 KB fills of the 2-stage
+// ring were the pace: ~36 GB/s per CU against 88 for the MFMA rate).
+// Row-mode C only (fp32, f16 / bf16 or pair), bias / ReLU / residual, batch.
+// ---------------------------------------------------------------------------
+template <int BM, int AMODE>
+struct X3Tile {
+    static constexpr int BN = 128, KS = 32, ROWB = KS * 2, NTX = 512;
+    static constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
+    static constexpr int STAGE = 2 * (A_BYTES + B_BYTES);
+    static constexpr int S = BM == 256 ? 3 : 4;
+    static constexpr int SMEM = S * STAGE;
+    static constexpr int APER = A_BYTES / 1024 / 8, BPER = B_BYTES / 1024 / 8;   // wave copies per plane
+    static constexpr int PER = 2 * (APER + BPER);                               // glds per thread per stage
+    static constexpr int WMW = BM / 64, WNW = 8 / WMW;                          // wave grid
+    static constexpr int TM = 2, TN = BN / WNW / 32;
+    static_assert(APER >= 1 && BPER >= 1 && TN >= 1, "x3 tile");
+    static_assert(SMEM >= BM * BN * 4 && SMEM <= 160 * 1024, "x3 LDS");
+};
+
+template <int BM, int AMODE>
+__global__ __launch_bounds__(512) void gemm_x3_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
+    typedef X3Tile<BM, AMODE> T;
+    typedef pair8_t frag;
+    constexpr int BN = T::BN, KS = T::KS, S = T::S, TM = T::TM, TN = T::TN, PER = T::PER;
+    __shared__ __attribute__((aligned(16))) char smem[T::SMEM];
+    int z, mt, nt;
+    xcd_tile(tiles_m, tiles_n, a.batch, z, mt, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / T::WNW, wn = wave % T::WNW;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const pair_t* Ab = (const pair_t*)a.A + (int64_t)z * a.a_bstride;
+    const pair_t* Wb = (const pair_t*)a.W + (int64_t)z * a.w_bstride;
+    // copy i of this wave: tile rows (8 i + wave) * 16 + lane / 4, 16-byte chunk lane & 3
+    const int ch = lane & 3;
+    const pair_t* asrc[T::APER];
+    RowInfo ri[T::APER];
+    int acs[T::APER];
+#pragma unroll
+    for (int i = 0; i < T::APER; ++i) {
+        const int row = (8 * i + wave) * 16 + (lane >> 2);
+        acs[i] = (ch ^ ((row >> 2) & 3)) * 8;
+        const int m = m0 + row;
+        ri[i] = make_row_info<AMODE>(a, m);
+        asrc[i] = Ab + (int64_t)min(m, a.M - 1) * a.lda + acs[i];
+    }
+    const pair_t* bsrc[T::BPER];
+#pragma unroll
+    for (int i = 0; i < T::BPER; ++i) {
+        const int row = (8 * i + wave) * 16 + (lane >> 2);
+        bsrc[i] = Wb + (int64_t)(n0 + row) * a.ldw + (ch ^ ((row >> 2) & 3)) * 8;
+    }
+    const int tapw = AMODE == CMT_A_CONV3X3 ? a.conv_c : (AMODE == CMT_A_CONV1D3 ? a.K / 3 : a.K);
+    const int a_lo = AMODE == CMT_A_ROWS ? a.K : tapw;     // element offset of an A row's lo half
+    int ctap = -1, ccin = 0;
+    int64_t toff[T::APER];
+    auto issue = [&](int buf, int kt) {
+        char* sb = smem + buf * T::STAGE;
+        int ka, kw;
+        if constexpr (AMODE != CMT_A_ROWS) {
+            // a tap spans tapw / 32 stages: gathered row offsets once per tap
+            if (ctap < 0) {
+                const int k0 = kt * KS;
+                ctap = k0 / tapw;
+                ccin = k0 - ctap * tapw;
+#pragma unroll
+                for (int i = 0; i < T::APER; ++i)
+                    toff[i] = a_offset<AMODE>(a, ri[i], m0 + (8 * i + wave) * 16 + (lane >> 2), ctap * tapw);
+            } else if ((ccin += KS) == tapw) {
+                ccin = 0;
+                ++ctap;
+#pragma unroll
+                for (int i = 0; i < T::APER; ++i)
+                    toff[i] = a_offset<AMODE>(a, ri[i], m0 + (8 * i + wave) * 16 + (lane >> 2), ctap * tapw);
+            }
+            ka = ccin;
+            kw = ctap * tapw + ccin;
+        } else {
+            ka = kw = kt * KS;
+        }
+#pragma unroll
+        for (int i = 0; i < T::APER; ++i) {
+            const pair_t* src;
+            if (AMODE == CMT_A_ROWS) src = asrc[i] + ka;
+            else src = toff[i] < 0 ? nullptr : Ab + toff[i] + ka + acs[i];
+            glds16(src ? (const void*)src : (const void*)g_zero_page, sb + (8 * i + wave) * 1024);
+            glds16(src ? (const void*)(src + a_lo) : (const void*)g_zero_page, sb + T::A_BYTES + (8 * i + wave) * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < T::BPER; ++i) {
+            glds16(bsrc[i] + kw, sb + 2 * T::A_BYTES + (8 * i + wave) * 1024);
+            glds16(bsrc[i] + kw + a.K, sb + 2 * T::A_BYTES + T::B_BYTES + (8 * i + wave) * 1024);
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = a.K / KS;
+#pragma unroll
+    for (int st = 0; st < S; ++st)
+        if (st < nk) issue(st, st);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int last = min(nk - 1, kt == 0 ? S - 1 : kt + S - 2);
+        wait_tiles<PER, S>(last - kt);
+        barrier_mem();
+        // every wave is past its reads of stage kt-1: refill that slot
+        if (kt >= 1 && kt + S - 1 < nk) issue((kt - 1) % S, kt + S - 1);
+        const char* As = smem + (kt % S) * T::STAGE;
+        const char* Bs = As + 2 * T::A_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < KS / 16; ++ks) {
+            const int kc = 2 * ks + lh;
+            frag af[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                const int r = wm * 64 + tm * 32 + lr;
+                const int o = r * T::ROWB + ((kc ^ ((r >> 2) & 3)) << 4);
+                af[tm] = *(const frag*)(As + o);
+                al[tm] = *(const frag*)(As + T::A_BYTES + o);
+            }
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int r = wn * (BN / T::WNW) + tn * 32 + lr;
+                const int o = r * T::ROWB + ((kc ^ ((r >> 2) & 3)) << 4);
+                bh[tn] = *(const frag*)(Bs + o);
+                bl[tn] = *(const frag*)(Bs + T::B_BYTES + o);
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], al[tm], acc[tm][tn]);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bl[tn], af[tm], acc[tm][tn]);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], af[tm], acc[tm][tn]);
+        }
+    }
+
+    // ---- epilogue (as gemm_dma_kernel's, row-mode C): bias / relu / residual loads
+    // first, then the tile staged through LDS and stored as whole row segments
+    const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
+    char* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
+    const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
+    const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
+    f32x4 bv[TN][4];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * (BN / T::WNW) + tn * 32 + 8 * g + 4 * lh;
+            bv[tn][g] = biasz ? *(const f32x4*)(biasz + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int m = min(m0 + wm * 64 + tm * 32 + lr, a.M - 1);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * (BN / T::WNW) + tn * 32 + 8 * g + 4 * lh;
+                const f32x4 r = Rz ? load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype, a.N) : f32x4{0.f, 0.f, 0.f, 0.f};
+                if (a.relu) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[tm][tn][4 * g + j] = fmaxf(acc[tm][tn][4 * g + j] + bv[tn][g][j], 0.f) + r[j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                }
+            }
+    }
+    const int npass = a.c_dtype == CMT_F16P ? 2 : 1;
+    const int cpr = BN * esz / 16;                            // 16-byte chunks per tile row
+    const int cpe = 16 / esz;                                 // elements per chunk
+    const int lcpr = esz == 4 ? 5 : 4;                        // log2(cpr) for BN = 128
+    for (int pass = 0; pass < npass; ++pass) {
+        barrier_mem();                                        // every wave is done with the ring / last pass
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int row = wm * 64 + tm * 32 + lr;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c0 = wn * (BN / T::WNW) + tn * 32 + 8 * g + 4 * lh;
+                    const int c = c0 / cpe;
+                    char* dst = smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4) + (c0 % cpe) * esz;
+                    f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
+                               acc[tm][tn][4 * g + 3]};
+                    if (pass) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] -= (float)(pair_t)v[j];   // lo = f16(x - hi)
+                    }
+                    store4<pair_t>(dst, 0, a.c_dtype == CMT_F16P ? CMT_F16 : a.c_dtype, v);
+                }
+        }
+        barrier_mem();
+#pragma unroll 4
+        for (int q = tid; q < (BM << lcpr); q += T::NTX) {
+            const int row = q >> lcpr, c = q & (cpr - 1);
+            const int m = m0 + row;
+            if (m >= a.M) continue;
+            const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4));
+            const int64_t idx = (int64_t)m * a.ldc + n0 + c * cpe + (pass ? a.N : 0);
+            *(f32x4*)(Cz + idx * esz) = v;
+        }
+    }
+}
+
+template <int BM>
+int launch_x3(const cmt_gemm_args& a, hipStream_t s) {
+    const int tm = cdiv(a.M, BM), tn = a.N / 128;
+    const unsigned nwg = (unsigned)((int64_t)tm * tn * a.batch);
+    if (a.a_mode == CMT_A_CONV3X3) gemm_x3_kernel<BM, CMT_A_CONV3X3><<<nwg, 512, 0, s>>>(a, tm, tn);
+    else gemm_x3_kernel<BM, CMT_A_ROWS><<<nwg, 512, 0, s>>>(a, tm, tn);
+    return cmt_check_launch("cmt_gemm");
+}
+
+// ---------------------------------------------------------------------------
 // GEMM + residual + LayerNorm, fused (cmt_gemm_ln).  One workgroup owns 32
 // full output rows (BN = N = 256): waves 1 x 4, each wave 32 rows x 64
 // columns.  The epilogue adds bias and R, reduces each row's mean / variance
@@ -1057,6 +1298,13 @@ extern "C" int cmt_gemm_ln(const cmt_gemm_args* gp, const cmt_ln_args* lp, void*
     return cmt_check_launch("cmt_gemm_ln");
 }
 
+// the row-mode / 3x3-conv split GEMMs gemm_x3_kernel covers
+static bool x3_eligible(const cmt_gemm_args& a) {
+    const int kdiv = a.a_mode == CMT_A_CONV3X3 ? a.conv_c : a.K;
+    return (a.a_mode == CMT_A_ROWS || a.a_mode == CMT_A_CONV3X3) && a.A2 == nullptr && a.c_mode == CMT_C_ROWS &&
+           a.k_splits <= 1 && a.plane_max2 == nullptr && a.N % 128 == 0 && kdiv % 32 == 0 && a.K % 32 == 0;
+}
+
 extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm: null args");
     const cmt_gemm_args& a = *ap;
@@ -1104,6 +1352,14 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
                     a.plane_max_cols <= a.N,
                     "cmt_gemm: plane_max2 needs a head-split 16-bit C, compute-dtype A and plane_max_cols % 32 == 0");
     hipStream_t s = (hipStream_t)stream;
+    if (a.w_dtype == CMT_F16P && x3_eligible(a)) {
+        // split GEMMs whose 256-row grid covers most CUs (tools/bench_kernels.py --only split, against
+        // the 128 x 128 DMA tile: shared_conv 265 -> 249 us, RV fc1 76 -> 59, RV fc2 76 -> 64, BEV fc2
+        // 42 -> 34, RV query fc1 33 -> 20; 128 x 128 x3 tiles everywhere: 280, 65, 69, 37, 22);
+        // fusion frame 539 -> 559 frames/s alternating on one box
+        const int64_t t256 = (int64_t)(a.N / 128) * cdiv(a.M, 256) * a.batch;
+        if (t256 >= 160) return launch_x3<256>(a, s);
+    }
     if (a.w_dtype != CMT_F32 && a.a_dtype == a.w_dtype) {
         // LDS-DMA path: 64-deep k stages
         const int kdiv = a.a_mode == CMT_A_CONV3X3 ? a.conv_c : (a.a_mode == CMT_A_CONV1D3 ? a.K / 3 : a.K);

@@ -120,6 +120,138 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(cmt_gemm_ex_args a, int kc
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same general-stride GEMM on bf16 MFMA in three passes (cmt_gemm_bf16x3_ex):
+// every fp32 operand is split x = hi + lo, both bf16 (RNE) -- bf16 keeps the
+// fp32 exponent range, so the small gradients of a backward pass stay exact to
+// ~2^-17 where an f16 pair would flush them -- and each 16-deep k step runs
+// lo*hi + hi*lo + hi*hi on v_mfma_f32_32x32x16_bf16, fp32 accumulate: ~2^-16
+// relative per product (the dropped lo*lo term and the pair's representation),
+// at 3 x 32 cycles per 16 k against 8 x 64 for the f32 MFMA (5.3x the rate).
+// Tiles 64 x 64 x 32 as gemm_ex_kernel, staged through registers (any operand
+// stride) into bf16 LDS images [row][32 k] (64-byte rows, 16-byte chunks
+// XOR-swizzled by (row >> 2) & 3), hi and lo planes.
+// ---------------------------------------------------------------------------
+constexpr int X3RB = 64;   // bytes per staged row (32 k of bf16)
+
+__device__ __forceinline__ int x3_off(int row, int k) {
+    return row * X3RB + ((((k >> 3) ^ ((row >> 2) & 3))) << 4) + (k & 7) * 2;
+}
+__device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
+    hi = (bf16_t)x;
+    lo = (bf16_t)(x - (float)hi);
+}
+
+// stage a 64-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) as bf16 hi / lo images
+template <int MODE>
+__device__ __forceinline__ void stage_x3(char* __restrict__ hi, char* __restrict__ lo, const float* __restrict__ X,
+                                         int64_t s_r, int64_t s_k, int rows, int K, int r0, int k0, int tid) {
+    typedef bf16_t b4 __attribute__((ext_vector_type(4)));
+    if (MODE == OP_KC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int r = idx >> 3, c = (idx & 7) * 4;
+            const int gr = r0 + r, gk = k0 + c;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (gr < rows) {
+                const float* p = X + (int64_t)gr * s_r + gk;
+                if (gk + 3 < K) v = *(const f32x4*)p;
+                else
+                    for (int j = 0; j < 4; ++j) v[j] = gk + j < K ? p[j] : 0.f;
+            }
+            b4 h, l;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bf16_t hj, lj;
+                split_bf16(v[j], hj, lj);
+                h[j] = hj;
+                l[j] = lj;
+            }
+            *(b4*)(hi + x3_off(r, c)) = h;
+            *(b4*)(lo + x3_off(r, c)) = l;
+        }
+    } else if (MODE == OP_MC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int gr = r0 + r, gk = k0 + k;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (gk < K) {
+                const float* p = X + (int64_t)gk * s_k + gr;
+                if (gr + 3 < rows) v = *(const f32x4*)p;
+                else
+                    for (int j = 0; j < 4; ++j) v[j] = gr + j < rows ? p[j] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bf16_t h, l;
+                split_bf16(v[j], h, l);
+                *(bf16_t*)(hi + x3_off(r + j, k)) = h;
+                *(bf16_t*)(lo + x3_off(r + j, k)) = l;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int idx = tid + TNT * i;
+            const int r = idx >> 5, k = idx & 31;
+            const int gr = r0 + r, gk = k0 + k;
+            const float v = (gr < rows && gk < K) ? X[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
+            bf16_t h, l;
+            split_bf16(v, h, l);
+            *(bf16_t*)(hi + x3_off(r, k)) = h;
+            *(bf16_t*)(lo + x3_off(r, k)) = l;
+        }
+    }
+}
+
+template <int AM, int BM>
+__global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int kchunk) {
+    __shared__ __attribute__((aligned(16))) char As[2][64 * X3RB];   // hi, lo
+    __shared__ __attribute__((aligned(16))) char Bs[2][64 * X3RB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
+    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    const int z = blockIdx.z / a.ksplit, ks = blockIdx.z - z * a.ksplit;
+    const float* A = a.A + (int64_t)z * a.a_bs;
+    const float* B = a.B + (int64_t)z * a.b_bs;
+    const int kb = ks * kchunk, ke = min(a.K, kb + kchunk);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int ar = wm * 32 + lr, br = wn * 32 + lr;
+    for (int k0 = kb; k0 < ke; k0 += TBK) {
+        __syncthreads();
+        stage_x3<AM>(As[0], As[1], A, a.a_sm, a.a_sk, a.M, ke, m0, k0, tid);
+        stage_x3<BM>(Bs[0], Bs[1], B, a.b_sn, a.b_sk, a.N, ke, n0, k0, tid);
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int c = 16 * kk + 8 * lh;
+            const bf16x8 ah = *(const bf16x8*)(As[0] + x3_off(ar, c)), al = *(const bf16x8*)(As[1] + x3_off(ar, c));
+            const bf16x8 bh = *(const bf16x8*)(Bs[0] + x3_off(br, c)), bl = *(const bf16x8*)(Bs[1] + x3_off(br, c));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+        }
+    }
+    float* C = a.C + (int64_t)z * a.c_bs;
+    const int col = n0 + wn * 32 + lr;
+    if (col >= a.N) return;
+    const float bias = (a.bias && ks == 0) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= a.M) continue;
+        float* c = C + (int64_t)row * a.ldc + col;
+        const float v = a.alpha * acc[r] + bias;
+        if (a.ksplit > 1) atomicAdd(c, v);
+        else *c = a.beta != 0.f ? v + a.beta * *c : v;
+    }
+}
+
 int op_mode(int64_t s_row, int64_t s_k, const float* p) {
     const bool al = ((uintptr_t)p & 15) == 0;
     if (s_k == 1 && s_row % 4 == 0 && al) return OP_KC;
@@ -421,7 +553,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(cmt_adamw_args a) {
 
 }  // namespace
 
-extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) {
+namespace {
+int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm_f32_ex: null args");
     cmt_gemm_ex_args a = *ap;
     CMT_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.batch > 0, "cmt_gemm_f32_ex: empty problem");
@@ -433,15 +566,23 @@ extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) {
     a.ksplit = cdiv(a.K, kchunk);
     dim3 grid(cdiv(a.N, 64), cdiv(a.M, 64), a.batch * a.ksplit);
     hipStream_t s = (hipStream_t)stream;
-#define GX(AM, BM) gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk)
+#define GX(AM, BM)                                                       \
+    do {                                                                 \
+        if (x3) gemm_ex3_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk); \
+        else gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk);     \
+    } while (0)
     switch (am * 3 + bm) {
         case 0: GX(0, 0); break; case 1: GX(0, 1); break; case 2: GX(0, 2); break;
         case 3: GX(1, 0); break; case 4: GX(1, 1); break; case 5: GX(1, 2); break;
         case 6: GX(2, 0); break; case 7: GX(2, 1); break; default: GX(2, 2); break;
     }
 #undef GX
-    return cmt_check_launch("cmt_gemm_f32_ex");
+    return cmt_check_launch(x3 ? "cmt_gemm_bf16x3_ex" : "cmt_gemm_f32_ex");
 }
+}  // namespace
+
+extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, false); }
+extern "C" int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, true); }
 
 extern "C" int cmt_ln_train_fwd(const cmt_ln_train_args* ap, void* stream) {
     CMT_REQUIRE(ap && ap->rows > 0 && (ap->C == 64 || ap->C == 256), "cmt_ln_train_fwd: C must be 64 or 256");

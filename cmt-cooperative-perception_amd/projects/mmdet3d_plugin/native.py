@@ -191,6 +191,7 @@ def _load():
         "cmt_match_cost_args_size": ([], _i64),
         "cmt_adamw_args_size": ([], _i64),
         "cmt_gemm_f32_ex": ([P(GemmExArgs), _vp], _int),
+        "cmt_gemm_bf16x3_ex": ([P(GemmExArgs), _vp], _int),
         "cmt_attn_train_workspace_bytes": ([P(AttnTrainArgs)], _i64),
         "cmt_attn_train_fwd": ([P(AttnTrainArgs), _vp], _int),
         "cmt_attn_train_bwd": ([P(AttnTrainArgs), _vp], _int),

@@ -7,7 +7,7 @@ import torch
 
 from . import native as N
 
-__all__ = ["gemm_ex", "linear_fwd", "linear_bwd", "attn_train_fwd", "attn_train_bwd", "ln_train_fwd", "ln_train_bwd",
+__all__ = ["gemm_ex", "set_train_gemm", "linear_fwd", "linear_bwd", "attn_train_fwd", "attn_train_bwd", "ln_train_fwd", "ln_train_bwd",
            "bn_relu_train_fwd", "bn_relu_train_bwd", "im2col3x3", "det_loss", "match_cost", "sumsq", "adamw_step"]
 
 
@@ -22,10 +22,27 @@ def _f32(*ts):
             raise RuntimeError("training kernels take fp32 tensors")
 
 
+# Arithmetic of the training step's GEMMs: "bf16x3" (cmt_gemm_bf16x3_ex, three bf16 MFMA
+# passes on split operands, ~2^-16 relative per product) or "f32" (cmt_gemm_f32_ex, the
+# exact-f32 MFMA at 1/16 of the bf16 rate).  The reference's fp32 GEMMs ran as TF32
+# (~2^-11) under torch 1.9.1's defaults on its Ampere GPUs.
+_GEMM_ENTRY = {"bf16x3": "cmt_gemm_bf16x3_ex", "f32": "cmt_gemm_f32_ex"}
+_gemm_mode = "bf16x3"
+
+
+def set_train_gemm(mode):
+    """Select the training GEMM arithmetic ("bf16x3" or "f32"); returns the previous mode."""
+    global _gemm_mode
+    if mode not in _GEMM_ENTRY:
+        raise ValueError(f"train gemm mode must be one of {sorted(_GEMM_ENTRY)}")
+    old, _gemm_mode = _gemm_mode, mode
+    return old
+
+
 def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0, bias=None, batch=1, a_bs=0,
-            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0):
+            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0, mode=None):
     """C[z][m][n] = alpha sum_k A(m,k) B(n,k) (+bias) + beta C; strides in elements:
-    a_strides = (s_m, s_k), b_strides = (s_n, s_k)."""
+    a_strides = (s_m, s_k), b_strides = (s_n, s_k).  ``mode``: see set_train_gemm."""
     _f32(A, B, C, bias)
     g = N.GemmExArgs()
     g.M, g.N, g.K, g.batch, g.alpha, g.beta = M, N_, K, batch, alpha, beta
@@ -33,7 +50,8 @@ def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0
     g.B, (g.b_sn, g.b_sk), g.b_bs = B.data_ptr() + 4 * b_offset, b_strides, b_bs
     g.C, g.ldc, g.c_bs = C.data_ptr() + 4 * c_offset, ldc, c_bs
     g.bias, g.ksplit = _ptr(bias), ksplit
-    N._check(N.lib().cmt_gemm_f32_ex(ctypes.byref(g), N._stream()), "cmt_gemm_f32_ex")
+    entry = _GEMM_ENTRY[mode or _gemm_mode]
+    N._check(getattr(N.lib(), entry)(ctypes.byref(g), N._stream()), entry)
 
 
 def _ksplit(k, m, n):

@@ -64,6 +64,25 @@ def gemm_case(name, M, Nn, K, dt, a_f32=True, A2_cols=0, out_dt=torch.float32, h
     print(line, flush=True)
 
 
+def split_case(name, M, Nn, K, conv=None, relu=False, R=False, out="pair"):
+    """A split (f16-pair) GEMM of the 'ref' policy: A / W / C as [rows, 2, width] 16-bit pairs."""
+    dev = torch.device("cuda")
+    rows_a = M if conv is None else M
+    width = K if conv is None else conv[2]
+    A = torch.randint(0, 1 << 14, (rows_a, 2, width), dtype=torch.int16, device=dev).view(torch.uint16)
+    W = torch.randint(0, 1 << 14, (Nn, 2, K), dtype=torch.int16, device=dev).view(torch.uint16)
+    bias = torch.randn(Nn, device=dev)
+    C = (torch.empty(M, 2, Nn, dtype=torch.uint16, device=dev) if out == "pair"
+         else torch.empty(M, Nn, device=dev))
+    Rt = torch.empty(M, 2, Nn, dtype=torch.uint16, device=dev).fill_(0) if R else None
+    kw = dict(M=M, N=Nn, K=K, lda=width, ldw=K, ldc=Nn, bias=bias, relu=relu, R=Rt, ldr=Nn if R else 0)
+    if conv is not None:
+        kw.update(a_mode=N.A_CONV3X3, conv=conv)
+    us = timeit(lambda: N.gemm(A, W, C, **kw))
+    tf = 3 * 2.0 * M * Nn * K / (us * 1e-6) / 1e12
+    print(f"split {name:28s} M={M:6d} N={Nn:5d} K={K:5d} {us:9.2f} us {tf:8.1f} TF/s (3 f16 passes)", flush=True)
+
+
 def attn_case(name, Nq, Nk, dt, B=1, H=8, splits=0, fold=False):
     dev = torch.device("cuda")
     q = torch.randn(B * H * Nq * 32, device=dev).to(dt)
@@ -173,6 +192,13 @@ def main():
                                       plane_max2=pm, plane_max_cols=1536))
         print(f"kv_proj (A-stationary, packed W)  M= 32400 N= 3072 K=  256 {us:9.2f} us "
               f"{2 * 32400 * 3072 * 256 / (us * 1e-6) / 1e12:8.1f} TF/s", flush=True)
+    if args.only in ("", "split"):
+        split_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, conv=(180, 180, 512), relu=True)
+        split_case("rv fc1 (relu)", 24000, 1024, 192, relu=True)
+        split_case("rv fc2 (+R)", 24000, 256, 1024, R=True)
+        split_case("bev fc2 (+R)", 32400, 256, 256, R=True)
+        split_case("rv query fc1 (relu)", 5400, 1024, 192, relu=True)
+        split_case("rv query fc2", 5400, 256, 1024, out="f32")
     if args.only in ("", "chain"):
         for kind, last in ((0, False), (1, False), (2, False), (2, True)):
             chain_case(kind, last=last)

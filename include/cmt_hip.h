@@ -442,6 +442,12 @@ typedef struct cmt_gemm_ex_args {
     int ksplit;
 } cmt_gemm_ex_args;
 int cmt_gemm_f32_ex(const cmt_gemm_ex_args* args, void* stream);
+/* cmt_gemm_bf16x3_ex: the same contract, each fp32 operand split into a bf16
+ * pair (hi + lo, RNE) and multiplied in three bf16 MFMA passes (lo*hi + hi*lo +
+ * hi*hi, fp32 accumulate): ~2^-16 relative per product, fp32 exponent range --
+ * the training step's Linear forward / dX / dW (the reference's fp32 cuBLAS
+ * GEMMs, which torch 1.9.1 runs as TF32, ~2^-11, on Ampere by default). */
+int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* args, void* stream);
 
 /* Attention forward with row statistics, and its backward (attn_train.hip),
  * exact f32, head_dim 32.  Replaces, in the training step, the fp32

@@ -194,11 +194,14 @@ def test_gemm_split_headsplit_select(N, dev):
             assert (got - sel).abs().max().item() <= _tol(sel, C)
 
 
-def test_gemm_split_conv3x3(N, dev):
+@pytest.mark.parametrize("B,Cin,H,W", [(2, 128, 29, 33), (1, 64, 150, 140), (1, 64, 120, 130), (2, 64, 131, 127)])
+def test_gemm_split_conv3x3(N, dev, B, Cin, H, W):
     """Implicit 3x3 conv (shared_conv) on split operands: NCHW fp32 -> pair rows
-    (cmt_nchw_to_rows) -> conv + BN-folded bias + ReLU into pair memory rows."""
-    g = torch.Generator().manual_seed(13)
-    B, Cin, H, W, Cout = 2, 128, 29, 33, 256
+    (cmt_nchw_to_rows) -> conv + BN-folded bias + ReLU into pair memory rows.
+    Maps whose 256-row grid covers most CUs run on gemm_x3_kernel (1 or 2
+    images), the others on the 128 x 128 DMA tile."""
+    g = torch.Generator().manual_seed(13 + H)
+    Cout = 256
     x = torch.randn(B, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, 3, 3, generator=g) / 34
     b = torch.randn(Cout, generator=g)
@@ -215,6 +218,36 @@ def test_gemm_split_conv3x3(N, dev):
     got = _unpair(out.cpu()).view(B, Nk, Cout)[:, :H * W]
     err = (got - ref).abs().max().item()
     assert err <= _tol(ref, 9 * Cin) + 2 ** -21 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("M,N_,K,batch,rdt,cdt,relu", [(30000, 256, 512, 1, "pair", "pair", False),
+                                                      (12000, 256, 1024, 2, "pair", "pair", False),
+                                                      (24000, 1024, 192, 1, None, "pair", True),
+                                                      (20500, 384, 256, 1, "f32", "f32", True)])
+def test_gemm_split_x3_epilogues(N, dev, M, N_, K, batch, rdt, cdt, relu):
+    """gemm_x3_kernel (the large split GEMMs: BEV / RV position MLPs) with batch
+    strides, pair or fp32 residual, ReLU, pair or fp32 output and ragged row tiles,
+    against float64."""
+    g = torch.Generator().manual_seed(M + K)
+    A = torch.randn(batch, M, K, generator=g)
+    W = torch.randn(N_, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N_, generator=g)
+    R = torch.randn(batch, M, N_, generator=g) if rdt else None
+    ref = A.double() @ W.double().t() + b.double()
+    if relu:
+        ref = torch.relu(ref)
+    if R is not None:
+        ref = ref + R.double()
+    Rd = None if R is None else (_pair(R).to(dev) if rdt == "pair" else R.to(dev))
+    out = (torch.empty(batch, M, 2, N_, dtype=SPLIT, device=dev) if cdt == "pair"
+           else torch.empty(batch, M, N_, device=dev))
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), out, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_, bias=b.to(dev),
+           relu=relu, R=Rd, ldr=N_ if R is not None else 0, batch=batch, a_bstride=M * K, c_bstride=M * N_,
+           r_bstride=M * N_ if R is not None else 0)
+    got = _unpair(out.cpu()) if cdt == "pair" else out.cpu().double()
+    err = (got - ref).abs().max().item()
+    bound = _tol(ref, K) + (2 ** -21 * ref.abs().max().item() if cdt == "pair" else 0.0)
+    assert err <= bound, (err, bound)
 
 
 def test_gemm_split_conv1d3_grouped(N, dev):

@@ -27,7 +27,16 @@ def _gt(B, pc_range, ncls, n, seed):
     return boxes, labels
 
 
-def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5, coop=False):
+def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5, coop=False, gemm="f32"):
+    from projects.mmdet3d_plugin import native_train as NT
+    old = NT.set_train_gemm(gemm)
+    try:
+        return _run_mode(name, variant, dev, parity_log, fp16, B, Nq, L, ngt, coop, gemm)
+    finally:
+        NT.set_train_gemm(old)
+
+
+def _run_mode(name, variant, dev, parity_log, fp16, B, Nq, L, ngt, coop, gemm):
     from oracle import cmt_oracle as O
     from oracle import cmt_train_oracle as TO
     from projects.mmdet3d_plugin import synthetic as S
@@ -105,26 +114,35 @@ def _run(name, variant, dev, parity_log, fp16, B=1, Nq=32, L=2, ngt=5, coop=Fals
         if e > gerr:
             gerr, worst = e, k
     parity_log.append(f"training step {name}{' two-agent' if coop else ''} ({variant}, Nq {Nq}+DN {pad}, L {L}, "
-                      f"cross core "
-                      f"{'fp16' if fp16 else 'f32'}) vs float64 autograd: losses max rel {lerr:.1e}, "
+                      f"cross core {'fp16' if fp16 else 'f32'}, GEMMs {gemm}) vs float64 autograd: "
+                      f"losses max rel {lerr:.1e}, "
                       f"param grads max rel {gerr:.1e} ({worst})")
     return lerr, gerr, worst
 
 
+# Bounds: the exact-f32 GEMMs (cmt_gemm_f32_ex) are held to 2e-4 / 5e-3; the bf16x3 GEMMs of the
+# production step (~2^-16 per product, 10x the f32 error on the single-agent steps) to 2e-4 / 2e-2:
+# the two-agent step's max fusion and the Hungarian matching are discrete decisions that a
+# ~1e-5 forward difference can flip at a near tie, which moves whole gradient entries.
+GRAD_BOUND = {"f32": 5e-3, "bf16x3": 2e-2}
+
+
+@pytest.mark.parametrize("gemm", ["f32", "bf16x3"])
 @pytest.mark.parametrize("name,variant", [("cmt_fusion_nus", "fusion"), ("cmt_lidar_nus", "lidar")])
-def test_training_step_grads_match_float64(dev, parity_log, name, variant):
-    lerr, gerr, worst = _run(name, variant, dev, parity_log, fp16=False)
+def test_training_step_grads_match_float64(dev, parity_log, name, variant, gemm):
+    lerr, gerr, worst = _run(name, variant, dev, parity_log, fp16=False, gemm=gemm)
     assert lerr < 2e-4
-    assert gerr < 5e-3, worst
+    assert gerr < GRAD_BOUND[gemm], worst
 
 
-def test_coop_training_step_grads_match_float64(dev, parity_log):
+@pytest.mark.parametrize("gemm", ["f32", "bf16x3"])
+def test_coop_training_step_grads_match_float64(dev, parity_log, gemm):
     """configs[3]'s workload: the two-agent CmtHeadCoop training step (forward_train,
     loss, backward) against the float64 restatement with the reference's
     torch.max(stack, 0) fusion, whose gradient goes to one agent per element."""
-    lerr, gerr, worst = _run("cmtcoop_fusion_tumtraf", "fusion", dev, parity_log, fp16=False, coop=True)
+    lerr, gerr, worst = _run("cmtcoop_fusion_tumtraf", "fusion", dev, parity_log, fp16=False, coop=True, gemm=gemm)
     assert lerr < 2e-4
-    assert gerr < 5e-3, worst
+    assert gerr < GRAD_BOUND[gemm], worst
 
 
 def test_coop_training_fullsize_steps(dev, parity_log):

@@ -18,9 +18,14 @@ def _T():
     return T
 
 
+@pytest.mark.parametrize("mode", ["f32", "bf16x3"])
 @pytest.mark.parametrize("M,N,K,ta,tb", [(100, 70, 50, False, False), (256, 256, 900, True, True),
                                          (33, 257, 64, False, True), (64, 64, 4000, True, False)])
-def test_gemm_ex_transposes(dev, M, N, K, ta, tb):
+def test_gemm_ex_transposes(dev, M, N, K, ta, tb, mode):
+    """cmt_gemm_f32_ex (exact f32) and cmt_gemm_bf16x3_ex (three bf16 passes on split
+    operands) against float64, every transpose, split-K; the bf16x3 form also on
+    operands scaled by 2^-30 (gradient-sized values keep their relative accuracy:
+    bf16 pairs have the fp32 exponent range)."""
     T = _T()
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
@@ -31,13 +36,22 @@ def test_gemm_ex_transposes(dev, M, N, K, ta, tb):
     C = torch.empty(M, N, device=dev)
     a_str = (1, M) if ta else (K, 1)
     b_str = (1, N) if tb else (K, 1)
-    T.gemm_ex(Ad, a_str, Bd, b_str, C, M=M, N_=N, K=K, ldc=N, alpha=0.5, bias=bias.to(dev))
+    T.gemm_ex(Ad, a_str, Bd, b_str, C, M=M, N_=N, K=K, ldc=N, alpha=0.5, bias=bias.to(dev), mode=mode)
     C2 = torch.zeros(M, N, device=dev)
-    T.gemm_ex(Ad, a_str, Bd, b_str, C2, M=M, N_=N, K=K, ldc=N, alpha=0.5, beta=1.0, bias=bias.to(dev), ksplit=4)
+    T.gemm_ex(Ad, a_str, Bd, b_str, C2, M=M, N_=N, K=K, ldc=N, alpha=0.5, beta=1.0, bias=bias.to(dev), ksplit=4,
+              mode=mode)
     torch.cuda.synchronize()
-    tol = 1e-5 * math.sqrt(K) * 4
+    # f32: fp32 rounding; bf16x3: ~2^-16 of each product (|a b| ~ 1 here, a random walk over K)
+    tol = 1e-5 * math.sqrt(K) * 4 if mode == "f32" else 2 ** -15 * math.sqrt(K) * 4
     assert (C.cpu().double() - ref).abs().max().item() < tol
     assert (C2.cpu().double() - ref).abs().max().item() < tol
+    if mode == "bf16x3":
+        tiny = 2.0 ** -30
+        C3 = torch.empty(M, N, device=dev)
+        T.gemm_ex(Ad * tiny, a_str, Bd * tiny, b_str, C3, M=M, N_=N, K=K, ldc=N, alpha=0.5, mode=mode)
+        torch.cuda.synchronize()
+        ref3 = (ref - bias.double()) * tiny * tiny
+        assert (C3.cpu().double() - ref3).abs().max().item() < tol * tiny * tiny
 
 
 def _mix32(x):
@@ -68,7 +82,9 @@ def dn_mask(Nq, Nk, pad, grp):
 
 
 @pytest.mark.parametrize("B,Nq,Nk,pad,grp,fp16,p", [(1, 100, 1000, 0, 0, False, 0.0), (2, 70, 70, 30, 10, False, 0.0),
-                                                    (1, 140, 140, 40, 8, False, 0.25), (1, 96, 3000, 0, 0, True, 0.0)])
+                                                    (1, 140, 140, 40, 8, False, 0.25), (1, 96, 3000, 0, 0, True, 0.0),
+                                                    (2, 150, 1100, 50, 10, True, 0.25), (1, 200, 2049, 0, 0, True, 0.1),
+                                                    (1, 77, 300, 40, 8, True, 0.0)])
 def test_attention_train_fwd_bwd(dev, B, Nq, Nk, pad, grp, fp16, p):
     T = _T()
     H, C = 8, 256
