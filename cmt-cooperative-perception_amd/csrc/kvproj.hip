@@ -236,7 +236,10 @@ __global__ __launch_bounds__(512, 1) void kvproj_kernel(cmt_gemm_args a, int par
 // 4-column pieces straight from the accumulators (8-byte stores; L2 merges
 // the two lane halves' pieces of a 64-byte head row) -- no staging buffer.
 // W_lo sits N * 256 elements after W_hi, both fragment-packed like
-// cmt_kv_proj's W.
+// cmt_kv_proj's W.  The A fragments are read one k-step ahead into a second
+// register set (342.6 vs 347.2 us alone, 577.1 vs 576.1 frames/s in frame;
+// SQ counters before it: MFMA pipe busy 44 % of SIMD cycles, 61 % of wave
+// cycles issue-stalled -- profiles/r3_kvproj_sq_counters.json).
 // ---------------------------------------------------------------------------
 constexpr int KV3_RING = 4;
 
@@ -293,6 +296,19 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     const bool maxq = a.plane_max2 != nullptr && n_part < a.plane_max_cols;
     const int pm_planes = a.plane_max_cols >> 5;
     typedef TC t4 __attribute__((ext_vector_type(4)));
+    // A fragments software-pipelined one k-step ahead (two register sets): k-step ks's MFMAs
+    // run on the set read during k-step ks - 1 while the reads of ks + 1 are in flight; the
+    // tile is the same for every plane, so the last k-step of a plane reads k-step 0 again
+    pair8_t fa[2][4][2];
+    auto read_a = [&](int ks, pair8_t (&f)[4][2]) {
+        const int sw = ((2 * ks + lh) ^ (lr & 15)) << 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f[t][0] = *(const pair8_t*)(lhi + (t * 32 + lr) * (KP_K * 2) + sw);
+            f[t][1] = *(const pair8_t*)(llo + (t * 32 + lr) * (KP_K * 2) + sw);
+        }
+    };
+    read_a(0, fa[0]);
     for (int j = 0; j < planes_w; ++j) {
         const int plane = plane0 + j;
         f32x16 acc[4];
@@ -310,15 +326,14 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
         const int jn = j + 1 < planes_w ? j + 1 : j;   // past the last plane: re-fetch it (cached, unused)
 #pragma unroll
         for (int ks = 0; ks < KP_KS; ++ks) {
-            const int sw = ((2 * ks + lh) ^ (lr & 15)) << 4;
             const int slot = ks % KV3_RING;
+            read_a((ks + 1) % KP_KS, fa[(ks + 1) & 1]);
+            const pair8_t (&f)[4][2] = fa[ks & 1];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const pair8_t ah = *(const pair8_t*)(lhi + (t * 32 + lr) * (KP_K * 2) + sw);
-                const pair8_t al = *(const pair8_t*)(llo + (t * 32 + lr) * (KP_K * 2) + sw);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], ah, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], al, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], ah, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][0], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][1], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], f[t][0], acc[t], 0, 0, 0);
             }
             const int kn = ks + KV3_RING;
             const int64_t woff = kn < KP_KS ? (int64_t)j * (KP_KS * 512) + kn * 512
