@@ -23,7 +23,8 @@ def short(name):
 
 
 starts = [i for i, r in enumerate(rows) if "gemm_dma_kernel" in r["Kernel_Name"]
-          and ("Li1EEEv" in r["Kernel_Name"] or "Li1ELb" in r["Kernel_Name"])]
+          and ("Li1EEEv" in r["Kernel_Name"] or "Li1ELb" in r["Kernel_Name"])
+          or "gemm_x3_kernel<256, 1>" in r["Kernel_Name"]]
 if len(starts) < back + 1:
     sys.exit(f"only {len(starts)} frames in the trace")
 i0, i1 = starts[-back - 1], starts[-back]
