@@ -851,6 +851,83 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     }
 }
 
+// Epilogue of the 8-wave split tiles (gemm_x3_kernel, conv_halo_x3_kernel), row-mode C:
+// bias / relu / residual loads first, then the tile staged through LDS (the ring is
+// free) and stored as whole row segments (a CMT_F16P C in two passes, hi then lo).
+template <int BM, int TM, int TN, int WNW, int NTX>
+__device__ __forceinline__ void x3_epilogue(const cmt_gemm_args& a, f32x16 (&acc)[TM][TN], char* smem, int m0, int n0,
+                                            int z, int wm, int wn) {
+    constexpr int BN = 128;
+    const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
+    const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
+    char* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
+    const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
+    const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
+    f32x4 bv[TN][4];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * (BN / WNW) + tn * 32 + 8 * g + 4 * lh;
+            bv[tn][g] = biasz ? *(const f32x4*)(biasz + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int m = min(m0 + wm * 64 + tm * 32 + lr, a.M - 1);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * (BN / WNW) + tn * 32 + 8 * g + 4 * lh;
+                const f32x4 r = Rz ? load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype, a.N) : f32x4{0.f, 0.f, 0.f, 0.f};
+                if (a.relu) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[tm][tn][4 * g + j] = fmaxf(acc[tm][tn][4 * g + j] + bv[tn][g][j], 0.f) + r[j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                }
+            }
+    }
+    const int npass = a.c_dtype == CMT_F16P ? 2 : 1;
+    const int cpr = BN * esz / 16;                            // 16-byte chunks per tile row
+    const int cpe = 16 / esz;                                 // elements per chunk
+    const int lcpr = esz == 4 ? 5 : 4;                        // log2(cpr) for BN = 128
+    for (int pass = 0; pass < npass; ++pass) {
+        barrier_mem();                                        // every wave is done with the ring / last pass
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int row = wm * 64 + tm * 32 + lr;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c0 = wn * (BN / WNW) + tn * 32 + 8 * g + 4 * lh;
+                    const int c = c0 / cpe;
+                    char* dst = smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4) + (c0 % cpe) * esz;
+                    f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
+                               acc[tm][tn][4 * g + 3]};
+                    if (pass) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] -= (float)(pair_t)v[j];   // lo = f16(x - hi)
+                    }
+                    store4<pair_t>(dst, 0, a.c_dtype == CMT_F16P ? CMT_F16 : a.c_dtype, v);
+                }
+        }
+        barrier_mem();
+#pragma unroll 4
+        for (int q = tid; q < (BM << lcpr); q += NTX) {
+            const int row = q >> lcpr, c = q & (cpr - 1);
+            const int m = m0 + row;
+            if (m >= a.M) continue;
+            const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4));
+            const int64_t idx = (int64_t)m * a.ldc + n0 + c * cpe + (pass ? a.N : 0);
+            *(f32x4*)(Cz + idx * esz) = v;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Split (CMT_F16P) GEMM for the large problems of the 'ref' policy (shared_conv,
 // the BEV / RV position MLPs): BM x 128 tiles (BM 256 or 128), 8 waves, 32-deep
@@ -1012,75 +1089,7 @@ __global__ __launch_bounds__(512) void gemm_x3_kernel(cmt_gemm_args a, int tiles
         }
     }
 
-    // ---- epilogue (as gemm_dma_kernel's, row-mode C): bias / relu / residual loads
-    // first, then the tile staged through LDS and stored as whole row segments
-    const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
-    char* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
-    const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
-    const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
-    f32x4 bv[TN][4];
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = n0 + wn * (BN / T::WNW) + tn * 32 + 8 * g + 4 * lh;
-            bv[tn][g] = biasz ? *(const f32x4*)(biasz + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-        const int m = min(m0 + wm * 64 + tm * 32 + lr, a.M - 1);
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = n0 + wn * (BN / T::WNW) + tn * 32 + 8 * g + 4 * lh;
-                const f32x4 r = Rz ? load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype, a.N) : f32x4{0.f, 0.f, 0.f, 0.f};
-                if (a.relu) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[tm][tn][4 * g + j] = fmaxf(acc[tm][tn][4 * g + j] + bv[tn][g][j], 0.f) + r[j];
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
-                }
-            }
-    }
-    const int npass = a.c_dtype == CMT_F16P ? 2 : 1;
-    const int cpr = BN * esz / 16;                            // 16-byte chunks per tile row
-    const int cpe = 16 / esz;                                 // elements per chunk
-    const int lcpr = esz == 4 ? 5 : 4;                        // log2(cpr) for BN = 128
-    for (int pass = 0; pass < npass; ++pass) {
-        barrier_mem();                                        // every wave is done with the ring / last pass
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-            const int row = wm * 64 + tm * 32 + lr;
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int c0 = wn * (BN / T::WNW) + tn * 32 + 8 * g + 4 * lh;
-                    const int c = c0 / cpe;
-                    char* dst = smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4) + (c0 % cpe) * esz;
-                    f32x4 v = {acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
-                               acc[tm][tn][4 * g + 3]};
-                    if (pass) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] -= (float)(pair_t)v[j];   // lo = f16(x - hi)
-                    }
-                    store4<pair_t>(dst, 0, a.c_dtype == CMT_F16P ? CMT_F16 : a.c_dtype, v);
-                }
-        }
-        barrier_mem();
-#pragma unroll 4
-        for (int q = tid; q < (BM << lcpr); q += T::NTX) {
-            const int row = q >> lcpr, c = q & (cpr - 1);
-            const int m = m0 + row;
-            if (m >= a.M) continue;
-            const f32x4 v = *(const f32x4*)(smem + row * (BN * esz) + ((c ^ (row & (cpr - 1))) << 4));
-            const int64_t idx = (int64_t)m * a.ldc + n0 + c * cpe + (pass ? a.N : 0);
-            *(f32x4*)(Cz + idx * esz) = v;
-        }
-    }
+    x3_epilogue<BM, TM, TN, T::WNW, T::NTX>(a, acc, smem, m0, n0, z, wm, wn);
 }
 
 template <int BM>
@@ -1089,6 +1098,230 @@ int launch_x3(const cmt_gemm_args& a, hipStream_t s) {
     const unsigned nwg = (unsigned)((int64_t)tm * tn * a.batch);
     if (a.a_mode == CMT_A_CONV3X3) gemm_x3_kernel<BM, CMT_A_CONV3X3><<<nwg, 512, 0, s>>>(a, tm, tn);
     else gemm_x3_kernel<BM, CMT_A_ROWS><<<nwg, 512, 0, s>>>(a, tm, tn);
+    return cmt_check_launch("cmt_gemm");
+}
+
+// ---------------------------------------------------------------------------
+// shared_conv at the reference's numerics, straight from the NCHW fp32 map
+// (CMT_A_CONV3X3_NCHW, W CMT_F16P; cmt_head.py:280-287, 481).
+//
+// The 3x3 implicit GEMM re-stages every input pixel once per tap when the A
+// tile is gathered per (tap, channel chunk) (gemm_x3_kernel<CONV3X3>: 9 x 32 KB
+// of A per 32 channels of a 256-pixel tile).  Here a tile of BM = 256
+// consecutive pixels of one image reads, per chunk of 16 input channels, the
+// pixel HALO it needs for all nine taps -- pixels p0 - W - 1 .. p0 + 256 + W,
+// zero outside the image -- from the NCHW map (each channel's run is
+// contiguous: one coalesced scalar load per channel and lane), splits it into
+// f16 hi / lo in registers and writes it to LDS once as 64-byte pixel rows (hi
+// 16 | lo 16, 16-byte chunks XOR-swizzled by (row >> 2) & 3).  The nine taps'
+// A fragments are then ds_reads of that halo at a per-tap row shift (W x dy +
+// dx); a lane whose pixel sits on the left / right image edge zeroes its
+// fragment for dx = -1 / +1 (the row-wrapped neighbour is padding).  W is
+// staged per (chunk, tap) -- 128 rows x 64 bytes -- through an S-slot LDS-DMA
+// ring.  Per 16 channels the LDS fill is ~40 KB halo + 72 KB W against
+// 9 x 24 KB, and the NCHW -> pair-rows layout pass disappears.
+//
+// The halo loads of chunk c + 1 go out at tap 0 of chunk c (after that step's
+// W issue) into registers and are converted after tap 8; vmcnt completes in
+// issue order, so each W wait counts the halo loads issued after it (the
+// compiler's own wait for the halo registers trails 8 W stages).
+// 8 waves in a 4 x 2 grid of 64 x 64 sub-tiles, the three products per tap in
+// gemm_x3_kernel's order; epilogue x3_epilogue (bias, ReLU, pair / fp32 rows).
+// ---------------------------------------------------------------------------
+struct HaloConv {
+    static constexpr int BM = 256, BN = 128, CK = 16, NTX = 512;
+    static constexpr int WMAX = 240;                          // widest map row supported
+    static constexpr int NHMAX = BM + 2 * WMAX + 2;           // halo pixels per tile
+    static constexpr int ROWB = 64;                           // hi 16 | lo 16 f16 per row
+    static constexpr int HALO = (NHMAX * ROWB + 1023) / 1024 * 1024;
+    static constexpr int WSLOT = BN * ROWB;                   // one (chunk, tap) of W: 8 KB
+    static constexpr int S = 6;                               // W ring slots
+    static constexpr int SMEM = 2 * HALO + S * WSLOT;
+    static constexpr int UPT = (2 * NHMAX + NTX - 1) / NTX;   // (pixel, channel octet) units per thread
+    static constexpr int WNW = 2, TM = 2, TN = 2;
+    static_assert(SMEM <= 160 * 1024 && SMEM >= BM * BN * 4, "halo conv LDS");
+    static_assert(WSLOT == NTX * 16, "one 16-byte DMA per thread per W slot");
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
+    typedef HaloConv T;
+    typedef pair8_t frag;
+    constexpr int BM = T::BM, S = T::S, TM = T::TM, TN = T::TN, UPT = T::UPT;
+    constexpr int HLOADS = UPT * 8;                           // halo loads per thread per chunk
+    __shared__ __attribute__((aligned(16))) char smem[T::SMEM];
+    int z, mt, nt;
+    xcd_tile(tiles_m, tiles_n, a.batch, z, mt, nt);
+    const int m0 = mt * BM, n0 = nt * T::BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / T::WNW, wn = wave % T::WNW;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int Wd = a.conv_w, HW = a.conv_h * a.conv_w, Cin = a.conv_c;
+    const int NH = BM + 2 * Wd + 2;                           // halo pixels of this launch
+    const int hs = m0 - Wd - 1;                               // image pixel of halo row 0
+    const float* X = (const float*)a.A + (int64_t)z * a.a_bstride;
+    const pair_t* Wb = (const pair_t*)a.W;
+
+    // halo units of this thread: (halo row h, channel octet o); lanes walk consecutive rows
+    int u_src[UPT], u_lds[UPT];
+    bool u_ok[UPT], u_on[UPT];
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+        const int u = tid + i * T::NTX;
+        const int o = u >= NH ? 1 : 0;
+        const int h = u - o * NH;
+        const int p = hs + h;
+        u_on[i] = u < 2 * NH;                                 // a unit of this tile at all
+        u_ok[i] = u_on[i] && p >= 0 && p < HW;                // inside the image (else zeros)
+        u_src[i] = 8 * o * HW + p;
+        const int sw = (h >> 2) & 3;
+        u_lds[i] = h * T::ROWB + ((o ^ sw) << 4);             // hi chunk; the lo chunk is (2 + o) ^ sw
+    }
+    float hv[UPT][8];
+    auto load_halo = [&](int c) {
+        const float* Xc = X + (int64_t)c * T::CK * HW;
+#pragma unroll
+        for (int i = 0; i < UPT; ++i) {
+            // every wave issues all HLOADS loads (the vmcnt waits count them), with no
+            // condition on the loaded value (a select would wait for it): padding units
+            // read the zero page
+            const float* src = u_ok[i] ? Xc + u_src[i] : (const float*)g_zero_page;
+            const int es = u_ok[i] ? HW : 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hv[i][e] = src[e * es];
+        }
+    };
+    auto store_halo = [&](int buf) {
+        char* hb = smem + buf * T::HALO;
+        // pin the halo registers here: without this the split arithmetic below (no memory
+        // dependence) is hoisted right behind the loads and waits for them there
+#pragma unroll
+        for (int i = 0; i < UPT; ++i)
+            asm volatile("" : "+v"(hv[i][0]), "+v"(hv[i][1]), "+v"(hv[i][2]), "+v"(hv[i][3]), "+v"(hv[i][4]),
+                         "+v"(hv[i][5]), "+v"(hv[i][6]), "+v"(hv[i][7]));
+#pragma unroll
+        for (int i = 0; i < UPT; ++i) {
+            if (!u_on[i]) continue;
+            pair8_t hi, lo;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                hi[e] = (pair_t)hv[i][e];
+                lo[e] = (pair_t)(hv[i][e] - (float)hi[e]);
+            }
+            *(pair8_t*)(hb + u_lds[i]) = hi;
+            *(pair8_t*)(hb + (u_lds[i] ^ (2 << 4))) = lo;     // (2 + o) ^ sw == (o ^ sw) ^ 2
+        }
+    };
+
+    // W slot fill: LDS byte tid * 16 of the slot = row tid / 4, physical chunk tid % 4
+    const int wrow = tid >> 2, wlc = (tid & 3) ^ ((wrow >> 2) & 3);
+    const pair_t* wsrc = Wb + (int64_t)(n0 + wrow) * a.ldw + (wlc >> 1) * a.K + (wlc & 1) * 8;
+    const int nchunks = Cin / T::CK, G = nchunks * 9;
+    auto issue_w = [&](int g) {
+        const int c = g / 9, t = g - 9 * (g / 9);
+        glds16(wsrc + t * Cin + c * T::CK, smem + 2 * T::HALO + (g % S) * T::WSLOT + wave * 1024);
+    };
+
+    // per-lane fragment geometry: tile rows of the two 32-row sub-tiles, their edge flags
+    int arow[TM];
+    bool edl[TM], edr[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        arow[tm] = wm * 64 + tm * 32 + lr;
+        const int x = (m0 + arow[tm]) % Wd;
+        edl[tm] = x == 0;
+        edr[tm] = x == Wd - 1;
+    }
+    int woff[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+        const int r = wn * 64 + tn * 32 + lr;
+        woff[tn] = r * T::ROWB + ((lh ^ ((r >> 2) & 3)) << 4);
+    }
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // prologue: chunk 0's halo, W of steps 0 .. S-1
+    load_halo(0);
+    store_halo(0);
+#pragma unroll
+    for (int g = 0; g < S; ++g) issue_w(g);
+
+    // Every step issues exactly one W DMA (past the last step: a dummy refill of a slot no
+    // later step reads) and tap 0 of every chunk the next chunk's halo loads (the last
+    // chunk: its own again, converted into the idle buffer), so the issue stream is the
+    // same for every chunk and each wait below counts the ops issued after W(g) exactly;
+    // the compiler's own wait for the halo registers (after tap 8) then trails 8 W DMAs.
+    for (int c = 0; c < nchunks; ++c) {
+        const char* Hs = smem + (c & 1) * T::HALO;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int g = 9 * c + t;
+            // VMEM ops issued after W(g): S - 2 later W stages (S - 1 at step 0), plus the
+            // halo loads of tap 0 for taps 1 .. S - 1
+            if (t >= 1 && t <= S - 1) vm_wait<S - 2 + HLOADS>();
+            else if (t == 0 && c == 0) vm_wait<S - 1>();
+            else vm_wait<S - 2>();
+            barrier_mem();
+            if (g >= 1) issue_w(g + S - 1 < G ? g + S - 1 : g - 1);
+            if (t == 0) load_halo(c + 1 < nchunks ? c + 1 : c);
+
+            const char* Ws = smem + 2 * T::HALO + (g % S) * T::WSLOT;
+            const int tsh = (t / 3) * Wd + (t % 3);           // halo row of (pixel, tap) - tile row
+            frag af[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                const int hr = arow[tm] + tsh;
+                const int base = hr * T::ROWB, sw = (hr >> 2) & 3;
+                af[tm] = *(const frag*)(Hs + base + ((lh ^ sw) << 4));
+                al[tm] = *(const frag*)(Hs + base + (((2 + lh) ^ sw) << 4));
+                if ((t % 3 == 0 && edl[tm]) || (t % 3 == 2 && edr[tm])) {
+                    af[tm] = frag{};
+                    al[tm] = frag{};
+                }
+            }
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                bh[tn] = *(const frag*)(Ws + woff[tn]);
+                bl[tn] = *(const frag*)(Ws + (woff[tn] ^ (2 << 4)));
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], al[tm], acc[tm][tn]);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bl[tn], af[tm], acc[tm][tn]);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], af[tm], acc[tm][tn]);
+        }
+        // chunk c + 1's halo into the other buffer (its last readers, chunk c - 1's taps, are
+        // all past this chunk's first barrier); the next step's barrier publishes it
+        store_halo((c + 1) & 1);
+    }
+    // the dummy W refills and the last halo loads are still in flight: drain them before
+    // the epilogue reuses the LDS
+    vm_wait<0>();
+    x3_epilogue<BM, TM, TN, T::WNW, T::NTX>(a, acc, smem, m0, n0, z, wm, wn);
+}
+
+int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
+    const int tm = cdiv(a.conv_h * a.conv_w, HaloConv::BM), tn = a.N / HaloConv::BN;
+    const unsigned nwg = (unsigned)((int64_t)tm * tn * a.batch);
+    conv_halo_x3_kernel<<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
     return cmt_check_launch("cmt_gemm");
 }
 
@@ -1309,9 +1542,24 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm: null args");
     const cmt_gemm_args& a = *ap;
     CMT_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.batch > 0, "cmt_gemm: empty problem");
+    CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
+    if (a.a_mode == CMT_A_CONV3X3_NCHW) {
+        CMT_REQUIRE(a.a_dtype == CMT_F32 && a.w_dtype == CMT_F16P &&
+                        (a.c_dtype == CMT_F16P || a.c_dtype == CMT_F32) && a.c_mode == CMT_C_ROWS &&
+                        a.A2 == nullptr && a.k_splits <= 1 && a.plane_max2 == nullptr,
+                    "cmt_gemm: the NCHW conv3x3 takes fp32 A, CMT_F16P W, fp32 / CMT_F16P row C, no A2 / "
+                    "split-K / plane_max2");
+        CMT_REQUIRE(a.conv_c % 16 == 0 && a.K == 9 * a.conv_c && a.conv_h > 0 && a.conv_w > 0 &&
+                        a.conv_w <= HaloConv::WMAX && a.M == a.conv_h * a.conv_w && a.N % 128 == 0,
+                    "cmt_gemm: bad NCHW conv3x3 geometry (C_in % 16, K = 9 C_in, width <= 240, M = h * w, "
+                    "N % 128)");
+        CMT_REQUIRE(a.ldw % 8 == 0 && a.ldc % 8 == 0 && (a.R == nullptr || a.ldr % 4 == 0) && a.bias_bstride % 4 == 0 &&
+                        a.r_dtype != CMT_F16P,
+                    "cmt_gemm: NCHW conv3x3 strides (ldw, ldc % 8; ldr, bias_bstride % 4; fp32 / f16 R)");
+        return launch_conv_halo(a, (hipStream_t)stream);
+    }
     CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
     CMT_REQUIRE(a.K % BK == 0, "cmt_gemm: K must be a multiple of 32");
-    CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
     CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16P,
                 "cmt_gemm: bad w_dtype");
     CMT_REQUIRE(a.w_dtype != CMT_F16P || a.a_dtype == CMT_F16P, "cmt_gemm: split (CMT_F16P) W needs CMT_F16P A");

@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from ... import native
-from ...runtime import OPTIONS, get_precision, op_empty
+from ...runtime import OPTIONS, SPLIT, get_precision, op_empty
 from ..utils.packing import to_dtype
 
 __all__ = ["HeadEngineMixin"]
@@ -92,6 +92,14 @@ class HeadEngineMixin:
     def _shared_conv_into(self, x, mem, Nk, pk, prec):
         B, Cin, H, W = x.shape
         Cout = pk["conv_w"].shape[0]
+        if prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 240 and Cout % 128 == 0:
+            # reference numerics: the conv reads the NCHW fp32 map itself, splitting each input
+            # pixel into f16 hi / lo once per workgroup for all nine taps (cmt_hip.h
+            # CMT_A_CONV3X3_NCHW) -- no NCHW -> pair-rows pass
+            native.gemm(x.contiguous().float(), pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=H * W,
+                        ldw=9 * Cin, ldc=Cout, bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3_NCHW,
+                        conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W, c_bstride=Nk * Cout)
+            return
         xin = op_empty(B * H * W, Cin, prec.gemm, x.device)
         native.nchw_to_rows(x.contiguous().float(), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
         native.gemm(xin, pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,

@@ -24,10 +24,10 @@ F32, F16, BF16, F16P = 0, 1, 2, 3
 # [..., C] operand stored as [..., 2, C] (f16 hi values, then f16 lo values)
 DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.uint16: F16P}
 LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
-A_ROWS, A_CONV3X3, A_CONV1D3 = 0, 1, 2
+A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 13
+ABI_VERSION = 14
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p

@@ -94,6 +94,7 @@ class Options:
     side_stream: bool      # CMT_SIDE_STREAM=0: everything on the caller's stream
     chain: bool            # CMT_CHAIN=0: f16/bf16 decoder as separate GEMM / LayerNorm launches
     bev_pos_cache: bool    # CMT_BEV_POS_CACHE=0: rebuild the BEV position-MLP hidden rows per call
+    conv_halo: bool        # CMT_CONV_HALO=0: split shared_conv via NCHW->pair rows + per-tap gathered GEMM
 
 
 def _env_on(name):
@@ -101,7 +102,7 @@ def _env_on(name):
 
 
 OPTIONS = Options(side_stream=_env_on("CMT_SIDE_STREAM"), chain=_env_on("CMT_CHAIN"),
-                  bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"))
+                  bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"), conv_halo=_env_on("CMT_CONV_HALO"))
 
 
 @contextlib.contextmanager

@@ -64,7 +64,7 @@ def gemm_case(name, M, Nn, K, dt, a_f32=True, A2_cols=0, out_dt=torch.float32, h
     print(line, flush=True)
 
 
-def split_case(name, M, Nn, K, conv=None, relu=False, R=False, out="pair"):
+def split_case(name, M, Nn, K, conv=None, relu=False, R=False, out="pair", nchw=False):
     """A split (f16-pair) GEMM of the 'ref' policy: A / W / C as [rows, 2, width] 16-bit pairs."""
     dev = torch.device("cuda")
     rows_a = M if conv is None else M
@@ -78,6 +78,10 @@ def split_case(name, M, Nn, K, conv=None, relu=False, R=False, out="pair"):
     kw = dict(M=M, N=Nn, K=K, lda=width, ldw=K, ldc=Nn, bias=bias, relu=relu, R=Rt, ldr=Nn if R else 0)
     if conv is not None:
         kw.update(a_mode=N.A_CONV3X3, conv=conv)
+    if conv is not None and nchw:
+        # the NCHW fp32 map itself (CMT_A_CONV3X3_NCHW: halo split in the kernel)
+        A = torch.randn(conv[2], M, device=dev)
+        kw.update(a_mode=N.A_CONV3X3_NCHW, lda=M, a_bstride=conv[2] * M)
     us = timeit(lambda: N.gemm(A, W, C, **kw))
     tf = 3 * 2.0 * M * Nn * K / (us * 1e-6) / 1e12
     print(f"split {name:28s} M={M:6d} N={Nn:5d} K={K:5d} {us:9.2f} us {tf:8.1f} TF/s (3 f16 passes)", flush=True)
@@ -194,6 +198,7 @@ def main():
               f"{2 * 32400 * 3072 * 256 / (us * 1e-6) / 1e12:8.1f} TF/s", flush=True)
     if args.only in ("", "split"):
         split_case("shared_conv 3x3 (implicit)", 32400, 256, 4608, conv=(180, 180, 512), relu=True)
+        split_case("shared_conv 3x3 (NCHW halo)", 32400, 256, 4608, conv=(180, 180, 512), relu=True, nchw=True)
         split_case("rv fc1 (relu)", 24000, 1024, 192, relu=True)
         split_case("rv fc2 (+R)", 24000, 256, 1024, R=True)
         split_case("bev fc2 (+R)", 32400, 256, 256, R=True)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 13
+#define CMT_ABI_VERSION 14
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi) (22 significant bits: relative
@@ -95,7 +95,13 @@ int64_t cmt_adamw_args_size(void);
  * Requirements: N % 64 == 0, K % 32 == 0 (K % 64 for compute-dtype A),
  * 16-byte aligned A/W rows, ldc/ldr multiples of 4.
  * ------------------------------------------------------------------------ */
-enum cmt_gemm_amode { CMT_A_ROWS = 0, CMT_A_CONV3X3 = 1, CMT_A_CONV1D3 = 2 };
+/* CMT_A_CONV3X3_NCHW (ABI 14): the 3x3 / pad 1 conv straight from an fp32 NCHW map
+ * A[b * a_bstride + c * (conv_h * conv_w) + pixel] (lda unused), K = 9 * conv_c tap-major
+ * as CONV3X3, M = conv_h * conv_w per batch element; split (CMT_F16P) W only (the
+ * reference-numerics shared_conv: each input pixel is split into f16 hi / lo once per
+ * workgroup and serves all nine taps from LDS); conv_c % 16 == 0, conv_w <= 240,
+ * N % 128 == 0, fp32 or CMT_F16P row C. */
+enum cmt_gemm_amode { CMT_A_ROWS = 0, CMT_A_CONV3X3 = 1, CMT_A_CONV1D3 = 2, CMT_A_CONV3X3_NCHW = 3 };
 enum cmt_gemm_cmode { CMT_C_ROWS = 0, CMT_C_HEADSPLIT = 1 };
 enum cmt_gemm_a2mode { CMT_A2_ADD = 0, CMT_A2_SELECT = 1 };
 

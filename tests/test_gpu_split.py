@@ -220,6 +220,49 @@ def test_gemm_split_conv3x3(N, dev, B, Cin, H, W):
     assert err <= _tol(ref, 9 * Cin) + 2 ** -21 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("B,Cin,H,W,Cout,cdt", [(1, 512, 180, 180, 256, "pair"),    # configs[2] shared_conv
+                                                (2, 48, 37, 41, 128, "pair"),
+                                                (1, 16, 16, 16, 256, "f32"),        # one chunk, one tile
+                                                (1, 32, 9, 240, 384, "pair"),       # widest row
+                                                (3, 64, 1, 70, 128, "f32"),         # one image row
+                                                (1, 32, 300, 1, 128, "pair")])      # one image column
+def test_gemm_split_conv3x3_nchw(N, dev, B, Cin, H, W, Cout, cdt):
+    """shared_conv at the reference's numerics straight from the NCHW fp32 map
+    (CMT_A_CONV3X3_NCHW: per-workgroup pixel halo split once, nine taps from
+    LDS, image-edge zeroing) + BN-folded bias + ReLU, into batch-strided pair
+    memory rows or fp32 rows, against float64 conv2d."""
+    g = torch.Generator().manual_seed(7 + H + W)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    b = torch.randn(Cout, generator=g)
+    wp = _pair(w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)).to(dev)
+    Nk = H * W + 37
+    out = (torch.full((B * Nk, 2, Cout), 0x7e00, dtype=torch.int16, device=dev).view(SPLIT) if cdt == "pair"
+           else torch.full((B * Nk, Cout), float("nan"), device=dev))
+    N.gemm(x.to(dev), wp, out, M=H * W, N=Cout, K=9 * Cin, lda=H * W, ldw=9 * Cin, ldc=Cout, bias=b.to(dev),
+           relu=True, a_mode=N.A_CONV3X3_NCHW, conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W,
+           c_bstride=Nk * Cout)
+    ref = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=1))
+    ref = ref.flatten(2).permute(0, 2, 1)
+    o = _unpair(out.cpu()) if cdt == "pair" else out.cpu().double()
+    got = o.view(B, Nk, Cout)[:, :H * W]
+    err = (got - ref).abs().max().item()
+    tol = _tol(ref, 9 * Cin) + (2 ** -21 * ref.abs().max().item() if cdt == "pair" else 0)
+    print(f"NCHW split conv B{B} {Cin}->{Cout} {H}x{W}: max abs err {err:.2e} (bound {tol:.2e})")
+    assert err <= tol, err
+    # rows past each image's map are untouched
+    assert torch.isnan(o.view(B, Nk, Cout)[:, H * W:]).all()
+
+
+def test_gemm_split_conv3x3_nchw_rejects(N, dev):
+    x = torch.zeros(1, 16, 4, 241, device=dev)
+    wp = torch.zeros(128, 2, 144, dtype=SPLIT, device=dev)
+    out = torch.zeros(4 * 241, 2, 128, dtype=SPLIT, device=dev)
+    with pytest.raises(RuntimeError, match="width"):
+        N.gemm(x, wp, out, M=4 * 241, N=128, K=144, lda=4 * 241, ldw=144, ldc=128,
+               a_mode=N.A_CONV3X3_NCHW, conv=(4, 241, 16), a_bstride=16 * 4 * 241)
+
+
 @pytest.mark.parametrize("M,N_,K,batch,rdt,cdt,relu", [(30000, 256, 512, 1, "pair", "pair", False),
                                                       (12000, 256, 1024, 2, "pair", "pair", False),
                                                       (24000, 1024, 192, 1, None, "pair", True),
