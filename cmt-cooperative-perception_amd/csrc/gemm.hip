@@ -1117,8 +1117,9 @@ int launch_x3(const cmt_gemm_args& a, hipStream_t s) {
 // A fragments are then ds_reads of that halo at a per-tap row shift (W x dy +
 // dx); a lane whose pixel sits on the left / right image edge zeroes its
 // fragment for dx = -1 / +1 (the row-wrapped neighbour is padding).  W is
-// staged per (chunk, tap) -- 128 rows x 64 bytes -- through an S-slot LDS-DMA
-// ring.  Per 16 channels the LDS fill is ~40 KB halo + 72 KB W against
+// staged per (chunk, kernel row) -- 3 taps x 128 rows x 64 bytes -- through an
+// S-slot LDS-DMA ring (one barrier per three taps).  Per 16 channels the LDS
+// fill is ~40 KB halo + 72 KB W against
 // 9 x 24 KB, and the NCHW -> pair-rows layout pass disappears.
 //
 // The halo loads of chunk c + 1 go out at tap 0 of chunk c (after that step's
@@ -1130,17 +1131,18 @@ int launch_x3(const cmt_gemm_args& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 struct HaloConv {
     static constexpr int BM = 256, BN = 128, CK = 16, NTX = 512;
-    static constexpr int WMAX = 240;                          // widest map row supported
+    static constexpr int WMAX = 180;                          // widest map row supported (the 0.075 m BEV grid)
     static constexpr int NHMAX = BM + 2 * WMAX + 2;           // halo pixels per tile
     static constexpr int ROWB = 64;                           // hi 16 | lo 16 f16 per row
     static constexpr int HALO = (NHMAX * ROWB + 1023) / 1024 * 1024;
-    static constexpr int WSLOT = BN * ROWB;                   // one (chunk, tap) of W: 8 KB
-    static constexpr int S = 6;                               // W ring slots
+    static constexpr int WTAP = BN * ROWB;                    // one (chunk, tap) of W: 8 KB
+    static constexpr int WSLOT = 3 * WTAP;                    // one step = one kernel row (3 taps)
+    static constexpr int S = 3;                               // W ring slots
     static constexpr int SMEM = 2 * HALO + S * WSLOT;
     static constexpr int UPT = (2 * NHMAX + NTX - 1) / NTX;   // (pixel, channel octet) units per thread
     static constexpr int WNW = 2, TM = 2, TN = 2;
     static_assert(SMEM <= 160 * 1024 && SMEM >= BM * BN * 4, "halo conv LDS");
-    static_assert(WSLOT == NTX * 16, "one 16-byte DMA per thread per W slot");
+    static_assert(WTAP == NTX * 16, "one 16-byte DMA per thread per tap of a W slot");
 };
 
 template <int N>
@@ -1220,10 +1222,12 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
     // W slot fill: LDS byte tid * 16 of the slot = row tid / 4, physical chunk tid % 4
     const int wrow = tid >> 2, wlc = (tid & 3) ^ ((wrow >> 2) & 3);
     const pair_t* wsrc = Wb + (int64_t)(n0 + wrow) * a.ldw + (wlc >> 1) * a.K + (wlc & 1) * 8;
-    const int nchunks = Cin / T::CK, G = nchunks * 9;
-    auto issue_w = [&](int g) {
-        const int c = g / 9, t = g - 9 * (g / 9);
-        glds16(wsrc + t * Cin + c * T::CK, smem + 2 * T::HALO + (g % S) * T::WSLOT + wave * 1024);
+    const int nchunks = Cin / T::CK, G = nchunks * 3;
+    auto issue_w = [&](int g) {   // step g = (chunk g / 3, kernel row g % 3): its three taps
+        const int c = g / 3, dy = g - 3 * (g / 3);
+        char* slot = smem + 2 * T::HALO + (g % S) * T::WSLOT + wave * 1024;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) glds16(wsrc + (3 * dy + dx) * Cin + c * T::CK, slot + dx * T::WTAP);
     };
 
     // per-lane fragment geometry: tile rows of the two 32-row sub-tiles, their edge flags
@@ -1257,56 +1261,63 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
     for (int g = 0; g < S; ++g) issue_w(g);
 
-    // Every step issues exactly one W DMA (past the last step: a dummy refill of a slot no
-    // later step reads) and tap 0 of every chunk the next chunk's halo loads (the last
-    // chunk: its own again, converted into the idle buffer), so the issue stream is the
-    // same for every chunk and each wait below counts the ops issued after W(g) exactly;
-    // the compiler's own wait for the halo registers (after tap 8) then trails 8 W DMAs.
+    // Every step (one kernel row: three taps) issues exactly one W stage (past the last step:
+    // a dummy refill of a slot no later step reads) and the first step of every chunk the next
+    // chunk's halo loads (the last chunk: its own again, converted into the idle buffer), so
+    // the issue stream is the same for every chunk and each wait below counts the ops issued
+    // after W(g) exactly.
+    constexpr int WOPS = 3;                                   // DMAs per thread per W stage
     for (int c = 0; c < nchunks; ++c) {
         const char* Hs = smem + (c & 1) * T::HALO;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            const int g = 9 * c + t;
-            // VMEM ops issued after W(g): S - 2 later W stages (S - 1 at step 0), plus the
-            // halo loads of tap 0 for taps 1 .. S - 1
-            if (t >= 1 && t <= S - 1) vm_wait<S - 2 + HLOADS>();
-            else if (t == 0 && c == 0) vm_wait<S - 1>();
-            else vm_wait<S - 2>();
+        for (int dy = 0; dy < 3; ++dy) {
+            const int g = 3 * c + dy;
+            // VMEM ops issued after W(g): S - 2 later stages (S - 1 at step 0), plus the halo
+            // loads of the chunk's first step for its second and third
+            if (dy >= 1) vm_wait<(S - 2) * WOPS + HLOADS>();
+            else if (c == 0) vm_wait<(S - 1) * WOPS>();
+            else vm_wait<(S - 2) * WOPS>();
             barrier_mem();
             if (g >= 1) issue_w(g + S - 1 < G ? g + S - 1 : g - 1);
-            if (t == 0) load_halo(c + 1 < nchunks ? c + 1 : c);
+            if (dy == 0) load_halo(c + 1 < nchunks ? c + 1 : c);
 
             const char* Ws = smem + 2 * T::HALO + (g % S) * T::WSLOT;
-            const int tsh = (t / 3) * Wd + (t % 3);           // halo row of (pixel, tap) - tile row
-            frag af[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-                const int hr = arow[tm] + tsh;
-                const int base = hr * T::ROWB, sw = (hr >> 2) & 3;
-                af[tm] = *(const frag*)(Hs + base + ((lh ^ sw) << 4));
-                al[tm] = *(const frag*)(Hs + base + (((2 + lh) ^ sw) << 4));
-                if ((t % 3 == 0 && edl[tm]) || (t % 3 == 2 && edr[tm])) {
-                    af[tm] = frag{};
-                    al[tm] = frag{};
+            for (int dx = 0; dx < 3; ++dx) {
+                const int tsh = dy * Wd + dx;                 // halo row of (pixel, tap) - tile row
+                frag af[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const int hr = arow[tm] + tsh;
+                    const int base = hr * T::ROWB, sw = (hr >> 2) & 3;
+                    af[tm] = *(const frag*)(Hs + base + ((lh ^ sw) << 4));
+                    al[tm] = *(const frag*)(Hs + base + (((2 + lh) ^ sw) << 4));
+                    if ((dx == 0 && edl[tm]) || (dx == 2 && edr[tm])) {
+                        af[tm] = frag{};
+                        al[tm] = frag{};
+                    }
                 }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    bh[tn] = *(const frag*)(Ws + dx * T::WTAP + woff[tn]);
+                    bl[tn] = *(const frag*)(Ws + dx * T::WTAP + (woff[tn] ^ (2 << 4)));
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], al[tm], acc[tm][tn]);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = mfma_traits<pair_t>::mma(bl[tn], af[tm], acc[tm][tn]);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], af[tm], acc[tm][tn]);
             }
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                bh[tn] = *(const frag*)(Ws + woff[tn]);
-                bl[tn] = *(const frag*)(Ws + (woff[tn] ^ (2 << 4)));
-            }
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], al[tm], acc[tm][tn]);
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bl[tn], af[tm], acc[tm][tn]);
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], af[tm], acc[tm][tn]);
         }
         // chunk c + 1's halo into the other buffer (its last readers, chunk c - 1's taps, are
         // all past this chunk's first barrier); the next step's barrier publishes it
@@ -1551,7 +1562,7 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
                     "split-K / plane_max2");
         CMT_REQUIRE(a.conv_c % 16 == 0 && a.K == 9 * a.conv_c && a.conv_h > 0 && a.conv_w > 0 &&
                         a.conv_w <= HaloConv::WMAX && a.M == a.conv_h * a.conv_w && a.N % 128 == 0,
-                    "cmt_gemm: bad NCHW conv3x3 geometry (C_in % 16, K = 9 C_in, width <= 240, M = h * w, "
+                    "cmt_gemm: bad NCHW conv3x3 geometry (C_in % 16, K = 9 C_in, width <= 180, M = h * w, "
                     "N % 128)");
         CMT_REQUIRE(a.ldw % 8 == 0 && a.ldc % 8 == 0 && (a.R == nullptr || a.ldr % 4 == 0) && a.bias_bstride % 4 == 0 &&
                         a.r_dtype != CMT_F16P,

@@ -92,7 +92,7 @@ class HeadEngineMixin:
     def _shared_conv_into(self, x, mem, Nk, pk, prec):
         B, Cin, H, W = x.shape
         Cout = pk["conv_w"].shape[0]
-        if prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 240 and Cout % 128 == 0:
+        if prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 180 and Cout % 128 == 0:
             # reference numerics: the conv reads the NCHW fp32 map itself, splitting each input
             # pixel into f16 hi / lo once per workgroup for all nine taps (cmt_hip.h
             # CMT_A_CONV3X3_NCHW) -- no NCHW -> pair-rows pass

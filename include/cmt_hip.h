@@ -99,7 +99,7 @@ int64_t cmt_adamw_args_size(void);
  * A[b * a_bstride + c * (conv_h * conv_w) + pixel] (lda unused), K = 9 * conv_c tap-major
  * as CONV3X3, M = conv_h * conv_w per batch element; split (CMT_F16P) W only (the
  * reference-numerics shared_conv: each input pixel is split into f16 hi / lo once per
- * workgroup and serves all nine taps from LDS); conv_c % 16 == 0, conv_w <= 240,
+ * workgroup and serves all nine taps from LDS); conv_c % 16 == 0, conv_w <= 180,
  * N % 128 == 0, fp32 or CMT_F16P row C. */
 enum cmt_gemm_amode { CMT_A_ROWS = 0, CMT_A_CONV3X3 = 1, CMT_A_CONV1D3 = 2, CMT_A_CONV3X3_NCHW = 3 };
 enum cmt_gemm_cmode { CMT_C_ROWS = 0, CMT_C_HEADSPLIT = 1 };

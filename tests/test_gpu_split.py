@@ -223,7 +223,7 @@ def test_gemm_split_conv3x3(N, dev, B, Cin, H, W):
 @pytest.mark.parametrize("B,Cin,H,W,Cout,cdt", [(1, 512, 180, 180, 256, "pair"),    # configs[2] shared_conv
                                                 (2, 48, 37, 41, 128, "pair"),
                                                 (1, 16, 16, 16, 256, "f32"),        # one chunk, one tile
-                                                (1, 32, 9, 240, 384, "pair"),       # widest row
+                                                (1, 32, 9, 180, 384, "pair"),       # widest row
                                                 (3, 64, 1, 70, 128, "f32"),         # one image row
                                                 (1, 32, 300, 1, 128, "pair")])      # one image column
 def test_gemm_split_conv3x3_nchw(N, dev, B, Cin, H, W, Cout, cdt):
@@ -255,12 +255,12 @@ def test_gemm_split_conv3x3_nchw(N, dev, B, Cin, H, W, Cout, cdt):
 
 
 def test_gemm_split_conv3x3_nchw_rejects(N, dev):
-    x = torch.zeros(1, 16, 4, 241, device=dev)
+    x = torch.zeros(1, 16, 4, 181, device=dev)
     wp = torch.zeros(128, 2, 144, dtype=SPLIT, device=dev)
-    out = torch.zeros(4 * 241, 2, 128, dtype=SPLIT, device=dev)
+    out = torch.zeros(4 * 181, 2, 128, dtype=SPLIT, device=dev)
     with pytest.raises(RuntimeError, match="width"):
-        N.gemm(x, wp, out, M=4 * 241, N=128, K=144, lda=4 * 241, ldw=144, ldc=128,
-               a_mode=N.A_CONV3X3_NCHW, conv=(4, 241, 16), a_bstride=16 * 4 * 241)
+        N.gemm(x, wp, out, M=4 * 181, N=128, K=144, lda=4 * 181, ldw=144, ldc=128,
+               a_mode=N.A_CONV3X3_NCHW, conv=(4, 181, 16), a_bstride=16 * 4 * 181)
 
 
 @pytest.mark.parametrize("M,N_,K,batch,rdt,cdt,relu", [(30000, 256, 512, 1, "pair", "pair", False),
