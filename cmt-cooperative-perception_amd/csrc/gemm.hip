@@ -1344,9 +1344,9 @@ int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
 // the staging ring in the same LDS array), then writes what cmt_layernorm_ex
 // would: Y, lowp(y), lowp(y + P) and the second LN (post_norm) Y2.
 // ---------------------------------------------------------------------------
-template <typename CT, int S>
+template <typename CT, int S, bool X3 = false>
 __global__ __launch_bounds__(NT) void gemm_ln_kernel(cmt_gemm_args a, cmt_ln_args ln) {
-    typedef DmaTile<CT, 32, 256, S, CMT_A_ROWS, 1> Tile;
+    typedef DmaTile<CT, 32, 256, S, CMT_A_ROWS, 1, X3> Tile;
     static_assert(Tile::TM == 1 && Tile::TN == 2, "32 x 256 tile, 1 x 4 waves");
     __shared__ __attribute__((aligned(16))) char smem[Tile::SMEM + 2 * 4 * 32 * 4];
     float* red = (float*)(smem + Tile::SMEM);       // [2][4 waves][32 rows]
@@ -1447,8 +1447,13 @@ __global__ __launch_bounds__(NT) void gemm_ln_kernel(cmt_gemm_args a, cmt_ln_arg
             if (ln.flags & CMT_LN_MAX_INTO) o[j] = fmaxf(o[j], yo[t][j]);
         }
         if (ln.Y) *(f32x4*)(ln.Y + (int64_t)m * ln.ldy + n) = o;
-        if (ln.Yl) store4<CT>(ln.Yl, (int64_t)m * ln.ldyl + n, ln.lowp_dtype, o);
-        if (ln.Yp) store4<CT>(ln.Yp, (int64_t)m * ln.ldyp + n, ln.lowp_dtype, o + pv[t]);
+        if constexpr (X3) {   // CMT_F16P rows: hi at n, lo at C + n
+            if (ln.Yl) store_pair4((pair_t*)ln.Yl + (int64_t)m * ln.ldyl, C, n, o);
+            if (ln.Yp) store_pair4((pair_t*)ln.Yp + (int64_t)m * ln.ldyp, C, n, o + pv[t]);
+        } else {
+            if (ln.Yl) store4<CT>(ln.Yl, (int64_t)m * ln.ldyl + n, ln.lowp_dtype, o);
+            if (ln.Yp) store4<CT>(ln.Yp, (int64_t)m * ln.ldyp + n, ln.lowp_dtype, o + pv[t]);
+        }
         if (ln.Y2) *(f32x4*)(ln.Y2 + (int64_t)m * ln.ldy2 + n) = y2[t];
     }
 }
@@ -1523,8 +1528,9 @@ extern "C" int cmt_gemm_ln(const cmt_gemm_args* gp, const cmt_ln_args* lp, void*
     const cmt_ln_args& l = *lp;
     CMT_REQUIRE(a.M > 0 && a.N == 256 && l.C == 256 && a.K % 64 == 0 && a.batch == 1,
                 "cmt_gemm_ln: needs N == C == 256, K % 64 == 0, batch 1");
-    CMT_REQUIRE(a.A && a.W && (a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16) && a.a_dtype == a.w_dtype,
-                "cmt_gemm_ln: A and W in the f16/bf16 compute dtype");
+    CMT_REQUIRE(a.A && a.W && (a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16P) &&
+                    a.a_dtype == a.w_dtype, "cmt_gemm_ln: A and W in the f16/bf16 compute dtype or both CMT_F16P");
+    CMT_REQUIRE(a.w_dtype != CMT_F16P || a.R == nullptr || a.r_dtype == CMT_F32, "cmt_gemm_ln: split R must be fp32");
     CMT_REQUIRE(a.a_mode == CMT_A_ROWS && a.A2 == nullptr && a.c_mode == CMT_C_ROWS && !a.relu,
                 "cmt_gemm_ln: plain row GEMM (no A2, no head split, no relu)");
     CMT_REQUIRE(a.lda % 8 == 0 && a.ldw % 8 == 0 && (a.R == nullptr || a.ldr % 4 == 0) &&
@@ -1537,7 +1543,9 @@ extern "C" int cmt_gemm_ln(const cmt_gemm_args* gp, const cmt_ln_args* lp, void*
                 "cmt_gemm_ln: LN strides must be multiples of 4");
     hipStream_t s = (hipStream_t)stream;
     const unsigned grid = (unsigned)cdiv(a.M, 32);
-    if (a.w_dtype == CMT_BF16) gemm_ln_kernel<bf16_t, 3><<<grid, NT, 0, s>>>(a, l);
+    // split pairs: four tiles per stage (A_hi, A_lo, W_hi, W_lo: 72 KB), 2 stages
+    if (a.w_dtype == CMT_F16P) gemm_ln_kernel<pair_t, 2, true><<<grid, NT, 0, s>>>(a, l);
+    else if (a.w_dtype == CMT_BF16) gemm_ln_kernel<bf16_t, 3><<<grid, NT, 0, s>>>(a, l);
     else gemm_ln_kernel<f16_t, 3><<<grid, NT, 0, s>>>(a, l);
     return cmt_check_launch("cmt_gemm_ln");
 }

@@ -694,6 +694,9 @@ class PETRTransformerDecoder(nn.Module):
             st["ksp"] = 4 if lp == SPLIT else 1
             st["t1"] = torch.empty((st["ksp"], rows, C), dtype=f32, device=device)
             st["o"] = torch.empty((rows, C), dtype=f32, device=device)
+            # (cmt_gemm_ln on pairs -- out-projection + LayerNorm in one launch, 32 full rows per
+            # workgroup -- measured slower in the frame: 572 vs 590 frames/s alternating A/B; its
+            # 29 workgroups each stream the 256 KB of pair weights, profiles/r3f_fused_ln_ab.txt)
         return st
 
     def lowp_layer0(self, st, qpos, *, B, Nq, prec, first_ops_ready=False):

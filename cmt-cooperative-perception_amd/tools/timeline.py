@@ -3,7 +3,8 @@ start / end offsets from the frame's first kernel, duration, queue, grid, name,
 and the busy/idle picture (union of kernel intervals) -- shows what the second
 stream overlaps and where the critical path idles.
     python cmt-cooperative-perception_amd/tools/timeline.py gpurun_out/<tag>/trace [frame_index_from_end]
-A frame starts at the shared_conv launch (gemm_dma_kernel<...,1> = CONV3X3)."""
+A frame starts at the shared_conv launch (gemm_dma_kernel<...,1> / gemm_x3_kernel<256, 1> =
+CONV3X3, conv_halo_x3_kernel = CONV3X3_NCHW)."""
 import csv
 import glob
 import sys
@@ -24,7 +25,7 @@ def short(name):
 
 starts = [i for i, r in enumerate(rows) if "gemm_dma_kernel" in r["Kernel_Name"]
           and ("Li1EEEv" in r["Kernel_Name"] or "Li1ELb" in r["Kernel_Name"])
-          or "gemm_x3_kernel<256, 1>" in r["Kernel_Name"]]
+          or "gemm_x3_kernel<256, 1>" in r["Kernel_Name"] or "conv_halo_x3_kernel" in r["Kernel_Name"]]
 if len(starts) < back + 1:
     sys.exit(f"only {len(starts)} frames in the trace")
 i0, i1 = starts[-back - 1], starts[-back]

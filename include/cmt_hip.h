@@ -246,7 +246,8 @@ int cmt_layernorm_ex(const cmt_ln_args* args, void* stream);
  * petr_transformer.py:374-487 for the attention out-projections and FFN fc2):
  * t = A W^T + bias + R is never written; ln->X is ignored and every LN output
  * of ln (Y, Yl, Yp, Y2) is produced.  Needs N == ln->C == 256, compute-dtype
- * A/W, row mode, batch 1. */
+ * A/W, row mode, batch 1.  ABI 14: A and W both CMT_F16P (the reference-numerics
+ * out-projections + norms[0] / norms[1]: three f16 passes, fp32 R, pair Yl / Yp). */
 int cmt_gemm_ln(const cmt_gemm_args* gemm, const cmt_ln_args* ln, void* stream);
 
 /* ------------------------------------------------------------------------

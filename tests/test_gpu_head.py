@@ -359,6 +359,38 @@ def test_chain_path_matches_separate_launches(dev, prec):
         assert (a - b).abs().max().item() <= 2e-2 * scale, (k, (a - b).abs().max().item(), scale)
 
 
+@pytest.mark.parametrize("opt", ["conv_halo"])
+def test_ref_path_selections_agree(dev, opt):
+    """OPTIONS.conv_halo (CMT_CONV_HALO: shared_conv straight from the NCHW map
+    vs NCHW -> pair rows + the per-tap gathered GEMM) at the reference-numerics
+    policy: both forms are fp32-accurate, summed in
+    other orders; a ~2^-21 difference still flips the f16 rounding of a few K / V
+    elements of the fp16 flash core (2^-11 each), so the logits agree to ~1e-4,
+    inside north_star's 1e-3 (each path is also held to the oracle at full size)."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=9, num_query=96, num_layers=3,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=61).to(dev)
+    xi = S.synthetic_img(6, 8, 20, seed=62).to(dev)
+    metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=63)
+    outs = {}
+    set_precision("ref")
+    head.box_epilogue = False
+    try:
+        for on in (True, False):
+            with torch.no_grad(), options(**{opt: on}):
+                o = head([x], [xi], metas)[0][0]
+            torch.cuda.synchronize()
+            outs[on] = {k: v.float().clone() for k, v in o.items()}
+    finally:
+        head.box_epilogue = True
+    for k in KEYS:
+        a, b = outs[True][k], outs[False][k]
+        assert torch.isfinite(a).all() and torch.isfinite(b).all(), k
+        assert (a - b).abs().max().item() <= 5e-4, (k, (a - b).abs().max().item())
+
+
 def test_bev_pos_hidden_cache(dev):
     """The input-independent first half of the BEV position MLP (pos2embed of
     the grid + bev_embedding[0] + ReLU) is kept like a weight pack: a forward

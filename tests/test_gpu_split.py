@@ -104,6 +104,40 @@ def test_gemm_split_k_into_layernorm(N, dev, K, ks):
                k_splits=ks)
 
 
+@pytest.mark.parametrize("M,with_r", [(900, True), (900, False), (77, True)])
+def test_gemm_ln_split(N, dev, M, with_r):
+    """cmt_gemm_ln on f16 pairs (the split out-projection + norms[0] / norms[1]):
+    LN(A W^T + b + R) to fp32 accuracy, pair Yl = pair(y) and Yp = pair(y + P)
+    bit-exact against the split of the fp32 output."""
+    g = torch.Generator().manual_seed(M + with_r)
+    C = 256
+    A = torch.randn(M, C, generator=g)
+    W = torch.randn(C, C, generator=g) / 16
+    b = torch.randn(C, generator=g)
+    R = torch.randn(M, C, generator=g)
+    P = torch.randn(M, C, generator=g)
+    lw, lb = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    t = A.double() @ W.double().t() + b.double() + (R.double() if with_r else 0)
+    ref = torch.nn.functional.layer_norm(t, (C,), lw.double(), lb.double(), 1e-5)
+    y = torch.empty(M, C, device=dev)
+    yl = torch.empty(M, 2, C, dtype=SPLIT, device=dev)
+    yp = torch.empty(M, 2, C, dtype=SPLIT, device=dev)
+    N.gemm_ln(_pair(A).to(dev), _pair(W).to(dev), M=M, K=C, lda=C, ldw=C, bias=b.to(dev),
+              R=R.to(dev) if with_r else None, ldr=C if with_r else 0, ln_w=lw.to(dev), ln_b=lb.to(dev), eps=1e-5,
+              Y=y, Yl=yl, Yp=yp, P=P.to(dev))
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-5 * ref.abs().max().item(), err
+    assert _same(yl, _pair(y.cpu()))
+    assert _same(yp, _pair(y.cpu() + P))
+    # the same as the split-K GEMM + layernorm_ex it replaces, to fp32 rounding
+    part = torch.empty(4, M, C, device=dev)
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), part, M=M, N=C, K=C, lda=C, ldw=C, ldc=C, bias=b.to(dev),
+           R=R.to(dev) if with_r else None, ldr=C if with_r else 0, k_splits=4)
+    y2 = torch.empty(M, C, device=dev)
+    N.layernorm_ex(part, lw.to(dev), lb.to(dev), rows=M, C=C, ldx=C, eps=1e-5, Y=y2, ldy=C, nparts=4)
+    assert (y.cpu() - y2.cpu()).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
 def _pair_heads(x, B, S, H):
     """fp32 [B*S, H*32] rows -> head-split f16 pairs [B][H][S][64] (hi 32 | lo 32) as uint16."""
     hi = x.float().half()
