@@ -1561,6 +1561,7 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm: null args");
     const cmt_gemm_args& a = *ap;
     CMT_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.batch > 0, "cmt_gemm: empty problem");
+    CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
     CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
     if (a.a_mode == CMT_A_CONV3X3_NCHW) {
         CMT_REQUIRE(a.a_dtype == CMT_F32 && a.w_dtype == CMT_F16P &&
@@ -1577,7 +1578,6 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
                     "cmt_gemm: NCHW conv3x3 strides (ldw, ldc % 8; ldr, bias_bstride % 4; fp32 / f16 R)");
         return launch_conv_halo(a, (hipStream_t)stream);
     }
-    CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
     CMT_REQUIRE(a.K % BK == 0, "cmt_gemm: K must be a multiple of 32");
     CMT_REQUIRE(a.w_dtype == CMT_F32 || a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16P,
                 "cmt_gemm: bad w_dtype");
