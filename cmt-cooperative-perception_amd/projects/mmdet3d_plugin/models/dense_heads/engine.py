@@ -314,10 +314,15 @@ class HeadEngineMixin:
             state = dec.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
             side.wait_stream(main)
             ready = torch.cuda.Event()
+            bev_ready = torch.cuda.Event()
             hb = hr = None
             with torch.cuda.stream(side):
                 if use_bev:
                     hb = self._bev_pos_hidden(H, W, pk)
+                # the BEV position MLP's second GEMM waits only for its own hidden rows (usually a
+                # kept pack: no kernel), not for the RV encoder's first half -- whose kernels
+                # cannot start until shared_conv's workgroups leave the CUs
+                bev_ready.record(side)
                 if use_img:
                     native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C,
                                         rows_per_batch=Nk, row_offset=HW)
@@ -331,9 +336,9 @@ class HeadEngineMixin:
                     t.record_stream(main)
             if use_bev:
                 self._shared_conv_into(x, mem, Nk, pk, prec)
-            main.wait_event(ready)
-            if use_bev:
+                main.wait_event(bev_ready)
                 self._bev_pos_out(hb, pos, B, Nk, pk, R=R)
+            main.wait_event(ready)
             if use_img:
                 self._rv_pe_out(hr, pos, B, Nk, HW, pk, R=R)
         else:
