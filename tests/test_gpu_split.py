@@ -478,11 +478,12 @@ def test_attention_pair_output(N, dev):
     assert torch.equal(_unpair(Op.cpu()), O32.cpu().double().view(B * Nq, H * 32))
 
 
-@pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100)])
+@pytest.mark.parametrize("B,S", [(1, 32400), (2, 4100), (1, 100), (1, 56400)])
 def test_kvproj_split(N, dev, B, S):
     """cmt_kv_proj's split f16 form (K columns from lowp(mem + pos), V columns
     from lowp(mem); all layers in one launch) against float64, with the key-norm
-    partials of the K planes; ragged last row tile."""
+    partials of the K planes; ragged last row tile.  56 400 tokens (the fusion
+    frame: 441 token tiles) takes the doubled column parts (4 per tile)."""
     g = torch.Generator().manual_seed(B * S)
     C, L = 256, 2
     M, N_ = B * S, 2 * L * C
