@@ -894,6 +894,25 @@ __device__ __forceinline__ void x3_epilogue(const cmt_gemm_args& a, f32x16 (&acc
     const int cpr = BN * esz / 16;                            // 16-byte chunks per tile row
     const int cpe = 16 / esz;                                 // elements per chunk
     const int lcpr = esz == 4 ? 5 : 4;                        // log2(cpr) for BN = 128
+    // CONV3X3_NCHW with A2 (cmt_hip.h): a second output out + A2[m] at C + c_split_stride
+    const bool two = a.a_mode == CMT_A_CONV3X3_NCHW && a.A2 != nullptr;
+    for (int out = 0; out < (two ? 2 : 1); ++out) {
+    if (out == 1) {
+        Cz += a.c_split_stride * esz;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int m = min(m0 + wm * 64 + tm * 32 + lr, a.M - 1);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = n0 + wn * (BN / WNW) + tn * 32 + 8 * g + 4 * lh;
+                    const f32x4 pv = *(const f32x4*)((const float*)a.A2 + (int64_t)m * a.lda2 + n);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += pv[j];
+                }
+        }
+    }
     for (int pass = 0; pass < npass; ++pass) {
         barrier_mem();                                        // every wave is done with the ring / last pass
 #pragma unroll
@@ -925,6 +944,7 @@ __device__ __forceinline__ void x3_epilogue(const cmt_gemm_args& a, f32x16 (&acc
             const int64_t idx = (int64_t)m * a.ldc + n0 + c * cpe + (pass ? a.N : 0);
             *(f32x4*)(Cz + idx * esz) = v;
         }
+    }
     }
 }
 
@@ -1566,9 +1586,11 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     if (a.a_mode == CMT_A_CONV3X3_NCHW) {
         CMT_REQUIRE(a.a_dtype == CMT_F32 && a.w_dtype == CMT_F16P &&
                         (a.c_dtype == CMT_F16P || a.c_dtype == CMT_F32) && a.c_mode == CMT_C_ROWS &&
-                        a.A2 == nullptr && a.k_splits <= 1 && a.plane_max2 == nullptr,
-                    "cmt_gemm: the NCHW conv3x3 takes fp32 A, CMT_F16P W, fp32 / CMT_F16P row C, no A2 / "
+                        a.k_splits <= 1 && a.plane_max2 == nullptr,
+                    "cmt_gemm: the NCHW conv3x3 takes fp32 A, CMT_F16P W, fp32 / CMT_F16P row C, no "
                     "split-K / plane_max2");
+        CMT_REQUIRE(a.A2 == nullptr || (a.lda2 % 4 == 0 && ((uintptr_t)a.A2 & 15) == 0),
+                    "cmt_gemm: NCHW conv3x3 second-output rows A2: fp32, lda2 % 4 == 0, 16-byte aligned");
         CMT_REQUIRE(a.conv_c % 16 == 0 && a.K == 9 * a.conv_c && a.conv_h > 0 && a.conv_w > 0 &&
                         a.conv_w <= HaloConv::WMAX && a.M == a.conv_h * a.conv_w && a.N % 128 == 0,
                     "cmt_gemm: bad NCHW conv3x3 geometry (C_in % 16, K = 9 C_in, width <= 180, M = h * w, "

@@ -89,17 +89,27 @@ class HeadEngineMixin:
                     r_bstride=c_bstride if R is not None else 0, r_offset=r_offset)
         return out
 
-    def _shared_conv_into(self, x, mem, Nk, pk, prec):
+    def _conv_halo_ok(self, x, pk, prec):
+        _, Cin, _, W = x.shape
+        return (prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 180
+                and pk["conv_w"].shape[0] % 128 == 0)
+
+    def _shared_conv_into(self, x, mem, Nk, pk, prec, pos=None, P=None):
+        """shared_conv into the memory rows; with ``P`` (the weight-only BEV
+        position rows, fp32 [H*W, C]) the NCHW conv also writes lowp(memory + pos)
+        into ``pos`` -- the BEV position MLP's second GEMM is then not run."""
         B, Cin, H, W = x.shape
         Cout = pk["conv_w"].shape[0]
-        if prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 180 and Cout % 128 == 0:
+        if self._conv_halo_ok(x, pk, prec):
             # reference numerics: the conv reads the NCHW fp32 map itself, splitting each input
             # pixel into f16 hi / lo once per workgroup for all nine taps (cmt_hip.h
             # CMT_A_CONV3X3_NCHW) -- no NCHW -> pair-rows pass
             native.gemm(x.contiguous().float(), pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=H * W,
                         ldw=9 * Cin, ldc=Cout, bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3_NCHW,
-                        conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W, c_bstride=Nk * Cout)
+                        conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W, c_bstride=Nk * Cout,
+                        A2=P, lda2=Cout if P is not None else 0, c2=pos if P is not None else None)
             return
+        assert P is None
         xin = op_empty(B * H * W, Cin, prec.gemm, x.device)
         native.nchw_to_rows(x.contiguous().float(), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
         native.gemm(xin, pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,
@@ -154,6 +164,29 @@ class HeadEngineMixin:
         key = (H, W, x_size, y_size, str(w0.dtype))
         name = f"bev_hidden_{H}x{W}_{w0.dtype}"
         src = [self.bev_embedding[0].weight, self.bev_embedding[0].bias]   # the parameters themselves
+        if torch.cuda.is_current_stream_capturing() and not self._pack.has(name, src, key):
+            return build()
+        return self._pack.get(name, src, key, build)
+
+    def _bev_pos_rows(self, H, W, pk):
+        """The whole BEV position encoding bev_embedding(pos2embed(coords_bev))
+        (cmt_head.py:324-337, 489) as fp32 rows [H*W, C]: like the hidden rows, a
+        function of the weights and the grid only, kept like a weight pack
+        (bev_embedding tracked); the NCHW conv adds it to the memory rows in its
+        epilogue (``_shared_conv_into(P=...)``)."""
+        _, _, w2, b2 = pk["bev"]
+        C = self.hidden_dim
+
+        def build():
+            hid = self._bev_pos_hidden(H, W, pk)
+            rows = torch.empty((H * W, C), dtype=torch.float32, device=w2.device)
+            native.gemm(hid, w2, rows, M=H * W, N=C, K=w2.shape[-1], lda=hid.shape[-1], ldw=w2.shape[-1], ldc=C,
+                        bias=b2)
+            return rows
+        key = (H, W, str(w2.dtype))
+        name = f"bev_pos_rows_{H}x{W}_{w2.dtype}"
+        be = self.bev_embedding
+        src = [be[0].weight, be[0].bias, be[2].weight, be[2].bias]
         if torch.cuda.is_current_stream_capturing() and not self._pack.has(name, src, key):
             return build()
         return self._pack.get(name, src, key, build)
@@ -297,6 +330,9 @@ class HeadEngineMixin:
         mem = op_empty(B * Nk, C, mdt, dev)
         pos = op_empty(B * Nk, C, mdt, dev)
         R = mem if lowp else None
+        # reference numerics with the NCHW conv: lowp(memory + pos) of the BEV rows comes from the
+        # conv epilogue plus the kept BEV position rows (CMT_BEV_POS_CACHE=0: the MLP runs per call)
+        fuse_bev = use_bev and OPTIONS.bev_pos_cache and self._conv_halo_ok(x, pk, prec)
         cams = self._cams(metas, dev) if use_img else None
         dec = self.transformer.decoder
         Nq = self.num_query
@@ -312,12 +348,14 @@ class HeadEngineMixin:
             # stream, or recorded on it.
             main = torch.cuda.current_stream()
             state = dec.lowp_state(B=B, Nk=Nk, Nq=Nq, prec=prec, device=dev)
+            # the BEV position rows (weight-only, kept) folded into the conv epilogue
+            P = self._bev_pos_rows(H, W, pk) if fuse_bev else None
             side.wait_stream(main)
             ready = torch.cuda.Event()
             bev_ready = torch.cuda.Event()
             hb = hr = None
             with torch.cuda.stream(side):
-                if use_bev:
+                if use_bev and not fuse_bev:
                     hb = self._bev_pos_hidden(H, W, pk)
                 # the BEV position MLP's second GEMM waits only for its own hidden rows (usually a
                 # kept pack: no kernel), not for the RV encoder's first half -- whose kernels
@@ -334,7 +372,9 @@ class HeadEngineMixin:
             for t in (qpos, hb, hr):
                 if t is not None:
                     t.record_stream(main)
-            if use_bev:
+            if use_bev and fuse_bev:
+                self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=P)
+            elif use_bev:
                 self._shared_conv_into(x, mem, Nk, pk, prec)
                 main.wait_event(bev_ready)
                 self._bev_pos_out(hb, pos, B, Nk, pk, R=R)
@@ -342,7 +382,9 @@ class HeadEngineMixin:
             if use_img:
                 self._rv_pe_out(hr, pos, B, Nk, HW, pk, R=R)
         else:
-            if use_bev:
+            if use_bev and fuse_bev:
+                self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=self._bev_pos_rows(H, W, pk))
+            elif use_bev:
                 self._shared_conv_into(x, mem, Nk, pk, prec)
                 self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
             if use_img:

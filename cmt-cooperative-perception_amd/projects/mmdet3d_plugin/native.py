@@ -268,14 +268,15 @@ def _farr(vals, n):
 def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0, a2_cols=0,
          a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0, bias_bstride=0,
          r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0,
-         plane_max2=None, plane_max_cols=0, k_splits=0):
+         plane_max2=None, plane_max_cols=0, k_splits=0, c2=None):
     """C = act(A W^T + bias) + R with the fused prologue/epilogue of cmt_gemm.
     Offsets are in elements of the respective tensor.  A2 of A's dtype selects
     (replaces A for output columns < a2_cols); an fp32 A2 beside fp32 A is
     added on load.  plane_max2 (fp32 [ceil(M/64), plane_max_cols/32], head-split
     16-bit C only) receives the per-64-row max squared row norm of each head plane.
     k_splits >= 2: C holds k_splits fp32 partial blocks of M * ldc elements whose sum
-    is the output (bias and R in the first); a layernorm_ex(nparts=k_splits) reduces them."""
+    is the output (bias and R in the first); a layernorm_ex(nparts=k_splits) reduces them.
+    c2 (a_mode A_CONV3X3_NCHW with fp32 A2 rows): a second output out + A2, laid out like C."""
     if k_splits > 1 and C.numel() < k_splits * M * ldc:
         raise RuntimeError("gemm: a split-K C needs k_splits blocks of M * ldc elements")
     g = _gemm_args(A, W, C, M=M, N=N, K=K, lda=lda, ldw=ldw, ldc=ldc, bias=bias, relu=relu, R=R, ldr=ldr, A2=A2,
@@ -290,6 +291,16 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
         g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
     if k_splits > 1:
         g.k_splits, g.c_split_stride = k_splits, M * ldc
+    if c2 is not None:
+        # a second output (A_CONV3X3_NCHW with A2): C's layout, at c_offset elements into c2
+        _dev(c2)
+        if c2.dtype != C.dtype or k_splits > 1:
+            raise RuntimeError("gemm: c2 must have C's dtype (and no split-K)")
+        es = C.element_size()
+        d = c2.data_ptr() + c_offset * _ps(C) * es - g.C
+        if d % es:
+            raise RuntimeError("gemm: c2 misaligned against C")
+        g.c_split_stride = d // es
     _check(lib().cmt_gemm(ctypes.byref(g), _stream()), "cmt_gemm")
 
 

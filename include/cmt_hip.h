@@ -100,7 +100,10 @@ int64_t cmt_adamw_args_size(void);
  * as CONV3X3, M = conv_h * conv_w per batch element; split (CMT_F16P) W only (the
  * reference-numerics shared_conv: each input pixel is split into f16 hi / lo once per
  * workgroup and serves all nine taps from LDS); conv_c % 16 == 0, conv_w <= 180,
- * N % 128 == 0, fp32 or CMT_F16P row C. */
+ * N % 128 == 0, fp32 or CMT_F16P row C.  Optional second output: with A2 (fp32 rows
+ * A2[m * lda2 + n], the same for every batch element -- the weight-only BEV position
+ * rows) it also writes out + A2 at C + c_split_stride (same layout as C): lowp(memory +
+ * pos), the K-projection operand, without a separate GEMM. */
 enum cmt_gemm_amode { CMT_A_ROWS = 0, CMT_A_CONV3X3 = 1, CMT_A_CONV1D3 = 2, CMT_A_CONV3X3_NCHW = 3 };
 enum cmt_gemm_cmode { CMT_C_ROWS = 0, CMT_C_HEADSPLIT = 1 };
 enum cmt_gemm_a2mode { CMT_A2_ADD = 0, CMT_A2_SELECT = 1 };

@@ -264,7 +264,8 @@ def test_gemm_split_conv3x3_nchw(N, dev, B, Cin, H, W, Cout, cdt):
     """shared_conv at the reference's numerics straight from the NCHW fp32 map
     (CMT_A_CONV3X3_NCHW: per-workgroup pixel halo split once, nine taps from
     LDS, image-edge zeroing) + BN-folded bias + ReLU, into batch-strided pair
-    memory rows or fp32 rows, against float64 conv2d."""
+    memory rows or fp32 rows, and the second output out + P (lowp(memory + pos)),
+    against float64 conv2d."""
     g = torch.Generator().manual_seed(7 + H + W)
     x = torch.randn(B, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
@@ -273,19 +274,26 @@ def test_gemm_split_conv3x3_nchw(N, dev, B, Cin, H, W, Cout, cdt):
     Nk = H * W + 37
     out = (torch.full((B * Nk, 2, Cout), 0x7e00, dtype=torch.int16, device=dev).view(SPLIT) if cdt == "pair"
            else torch.full((B * Nk, Cout), float("nan"), device=dev))
+    # second output out + P (the kept BEV position rows, the same for every image): lowp(memory + pos)
+    P = torch.randn(H * W, Cout, generator=g)
+    out2 = torch.full_like(out, float("nan")) if cdt != "pair" else torch.full_like(out.view(torch.int16), 0x7e00).view(SPLIT)
     N.gemm(x.to(dev), wp, out, M=H * W, N=Cout, K=9 * Cin, lda=H * W, ldw=9 * Cin, ldc=Cout, bias=b.to(dev),
            relu=True, a_mode=N.A_CONV3X3_NCHW, conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W,
-           c_bstride=Nk * Cout)
+           c_bstride=Nk * Cout, A2=P.to(dev), lda2=Cout, c2=out2)
     ref = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=1))
     ref = ref.flatten(2).permute(0, 2, 1)
-    o = _unpair(out.cpu()) if cdt == "pair" else out.cpu().double()
+    un = (lambda t: _unpair(t.cpu())) if cdt == "pair" else (lambda t: t.cpu().double())
+    o, o2 = un(out), un(out2)
     got = o.view(B, Nk, Cout)[:, :H * W]
     err = (got - ref).abs().max().item()
     tol = _tol(ref, 9 * Cin) + (2 ** -21 * ref.abs().max().item() if cdt == "pair" else 0)
     print(f"NCHW split conv B{B} {Cin}->{Cout} {H}x{W}: max abs err {err:.2e} (bound {tol:.2e})")
     assert err <= tol, err
+    ref2 = ref + P.double()
+    err2 = (o2.view(B, Nk, Cout)[:, :H * W] - ref2).abs().max().item()
+    assert err2 <= tol + 2 ** -21 * ref2.abs().max().item(), err2
     # rows past each image's map are untouched
-    assert torch.isnan(o.view(B, Nk, Cout)[:, H * W:]).all()
+    assert torch.isnan(o.view(B, Nk, Cout)[:, H * W:]).all() and torch.isnan(o2.view(B, Nk, Cout)[:, H * W:]).all()
 
 
 def test_gemm_split_conv3x3_nchw_rejects(N, dev):
