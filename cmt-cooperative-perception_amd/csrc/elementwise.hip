@@ -28,7 +28,11 @@ __device__ __forceinline__ void store_dt(void* p, int64_t idx, int dt, float v) 
 // the same registers: a second LN of the result (post_norm), and the next
 // GEMMs' operands in the compute dtype (lowp(y), lowp(y + P)).
 // ---------------------------------------------------------------------------
-template <int VPT, typename LT, bool PAIR = false>
+// NP > 0: the number of split-K parts known at compile time -- every part's loads, the
+// affine weights and P are issued before the first use (one memory round trip per row
+// instead of one per part: the decoder's 900-row LayerNorms are latency-bound); NP = 0
+// reads a.nparts at run time.  Same summation order either way.
+template <int VPT, typename LT, bool PAIR = false, int NP = 0>
 __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -36,12 +40,45 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
     constexpr int C = VPT * 64;
     float v[VPT];
     const float* x = a.X + (int64_t)row * a.ldx;
+    float wv[VPT], bv[VPT];
+    if constexpr (NP > 0) {
+        float xv[NP][VPT];
 #pragma unroll
-    for (int i = 0; i < VPT; ++i) v[i] = x[lane + 64 * i];
-    for (int q = 1; q < a.nparts; ++q) {   // split-K partial products (cmt_gemm k_splits)
-        const float* xq = x + q * a.part_stride;
+        for (int q = 0; q < NP; ++q)
 #pragma unroll
-        for (int i = 0; i < VPT; ++i) v[i] += xq[lane + 64 * i];
+            for (int i = 0; i < VPT; ++i) xv[q][i] = x[q * a.part_stride + lane + 64 * i];
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            wv[i] = a.W[lane + 64 * i];
+            bv[i] = a.B[lane + 64 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            v[i] = xv[0][i];
+#pragma unroll
+            for (int q = 1; q < NP; ++q) v[i] += xv[q][i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) v[i] = x[lane + 64 * i];
+        for (int q = 1; q < a.nparts; ++q) {   // split-K partial products (cmt_gemm k_splits)
+            const float* xq = x + q * a.part_stride;
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) v[i] += xq[lane + 64 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            wv[i] = a.W[lane + 64 * i];
+            bv[i] = a.B[lane + 64 * i];
+        }
+    }
+    float w2v[VPT], b2v[VPT];
+    if (a.Y2) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            w2v[i] = a.W2[lane + 64 * i];
+            b2v[i] = a.B2[lane + 64 * i];
+        }
     }
     float pv[VPT];
     if (a.Yp) {
@@ -70,7 +107,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = lane + 64 * i;
-        float o = (v[i] - mean) * rstd * a.W[c] + a.B[c];
+        float o = (v[i] - mean) * rstd * wv[i] + bv[i];
         v[i] = o;   // the second LN consumes the first LN's output
         if (a.flags & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
         if (a.flags & CMT_LN_MAX_INTO) o = fmaxf(o, yold[i]);
@@ -96,7 +133,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(cmt_ln_args a) {
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = lane + 64 * i;
-        float o = (v[i] - mean2) * rstd2 * a.W2[c] + a.B2[c];
+        float o = (v[i] - mean2) * rstd2 * w2v[i] + b2v[i];
         if (a.flags2 & CMT_LN_NAN_TO_NUM) o = nan_to_num(o);
         if (a.flags2 & CMT_LN_MAX_INTO) o = fmaxf(o, y2old[i]);
         y2[c] = o;
@@ -633,6 +670,18 @@ extern "C" int cmt_layernorm_ex(const cmt_ln_args* ap, void* stream) {
     if (a.rows == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     dim3 grid(cdiv(a.rows, 4));
+    const int np = a.nparts > 1 ? a.nparts : 1;
+    if (a.C == 256 && (np == 1 || np == 2 || np == 4)) {   // the decoder's LayerNorms
+#define LN_NP(NP)                                                                                          \
+        if (np == NP) {                                                                                    \
+            if (a.lowp_dtype == CMT_F16) layernorm_kernel<4, f16_t, false, NP><<<grid, 256, 0, s>>>(a);     \
+            else if (a.lowp_dtype == CMT_F16P) layernorm_kernel<4, pair_t, true, NP><<<grid, 256, 0, s>>>(a); \
+            else layernorm_kernel<4, bf16_t, false, NP><<<grid, 256, 0, s>>>(a);                            \
+        }
+        LN_NP(1) LN_NP(2) LN_NP(4)
+#undef LN_NP
+        return cmt_check_launch("cmt_layernorm");
+    }
 #define LN_CASE(V)                                                                              \
     case V:                                                                                     \
         if (a.lowp_dtype == CMT_F16) layernorm_kernel<V, f16_t><<<grid, 256, 0, s>>>(a);        \
