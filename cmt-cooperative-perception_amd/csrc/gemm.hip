@@ -670,22 +670,21 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     const int part = ksp > 1 ? z : 0;
     if (ksp > 1) z = 0;
     const int nkp = a.K / Tile::KS / ksp;
-    Tile::run(a, smem, m0, n0, z, acc, part * nkp, nkp);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int lr = lane & 31;
     const int lh = lane >> 5;
-
-    // ---- epilogue: lane = output row, 4 consecutive columns per register group.
-    // Every bias / residual load is issued before the first store: vmcnt counts
-    // stores too on CDNA4, so a load waited for after a store would drain it.
     const int esz = a.c_dtype == CMT_F32 ? 4 : 2;
     char* Cz = (char*)a.C + ((int64_t)z * a.c_bstride + part * a.c_split_stride) * esz;
     const float* biasz = a.bias && part == 0 ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
     const char* Rz = a.R && part == 0 ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2)
                                       : nullptr;
-    f32x4 bv[TN][4];
+    // bias and residual are read BEFORE the k loop: issued ahead of the first LDS-DMA stage they
+    // complete with it (vmcnt is in order), instead of costing the epilogue one more memory round
+    // trip -- the decoder's 900-row GEMMs are latency-bound (the split-K out-projections and fc2
+    // carry the residual in part 0)
+    f32x4 bv[TN][4], rv[TM][TN][4];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
@@ -700,9 +699,22 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    rv[tm][tn][g] = load4(Rz, (int64_t)m * a.ldr + n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh,
+                                          a.r_dtype, a.N);
+        }
+    }
+    Tile::run(a, smem, m0, n0, z, acc, part * nkp, nkp);
+
+    // ---- epilogue: lane = output row, 4 consecutive columns per register group.
+    if (Rz) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int n = n0 + wn * (BN / 2) + tn * 32 + 8 * g + 4 * lh;
-                    const f32x4 r = load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype, a.N);
+                    const f32x4 r = rv[tm][tn][g];
                     // bias + relu come first; keep R apart only when relu is on
                     if (a.relu) {
 #pragma unroll
