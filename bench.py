@@ -167,7 +167,7 @@ def load_traffic(workload, nk):
     """HBM bytes per launch of the dominant kernel (cross-attention core + its
     split combine) for THIS workload's shape, from the committed rocprofv3 PMC
     summary profiles/*_<workload>_attn_pmc_summary.json (FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE, separate passes; tools/traffic_summary.py).
+    correction + WRITE_SIZE, separate passes; dev/traffic_summary.py).
     Raises when no summary matches the workload and key length."""
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_attn_pmc_summary.json")))
     for path in reversed(cands):
@@ -176,7 +176,7 @@ def load_traffic(workload, nk):
         if s.get("workload") == workload and int(s.get("nk", -1)) == int(nk):
             return s["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     raise RuntimeError(f"no committed PMC traffic summary for workload {workload!r} at Nk={nk} under profiles/ "
-                       "(collect one with tools/gpu_check.sh ... prof; or pass --no-traffic)")
+                       "(collect one with dev/gpu_check.sh ... prof; or pass --no-traffic)")
 
 
 def spawn_ranks(args):

@@ -126,6 +126,15 @@ class _GradBuckets:
                 self._launch_ready()
         return hook
 
+    def drain(self):
+        """Wait for the all-reduces launched so far and restart the bucket
+        state: a backward() that step() never finished (called twice, or one
+        that raised part-way) must not leave ``next`` / ``pending`` behind, or
+        the next step would exchange nothing and the ranks would drift apart."""
+        for w in self.works:
+            w.wait()
+        self.reset()
+
     def finish(self):
         self._launch_ready(upto=len(self.buckets))
         for w in self.works:
@@ -179,7 +188,12 @@ class Trainer:
             torch.autograd.graph.increment_version(p)
 
     def backward(self, losses):
+        """Backward of the summed losses into freshly zeroed flat gradients
+        (no accumulation across calls: a second backward() before step()
+        replaces the first one's gradients and exchange)."""
         total = sum(losses.values()) if isinstance(losses, dict) else losses
+        if self.buckets is not None:
+            self.buckets.drain()   # outstanding all-reduces write fp.grad: finish them before zeroing it
         self.fp.zero_grad()
         total.backward()
         return total

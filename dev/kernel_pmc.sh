@@ -1,0 +1,28 @@
+#!/bin/bash
+# SQ / TCC counter passes (one rocprofv3 --pmc run per group) over
+# dev/kernel_probe.py: gpurun -- bash .../kernel_pmc.sh TAG kv|conv MATCH
+set -uo pipefail
+TAG=${1:-kpmc}; WHAT=${2:-kv}; MATCH=${3:-kvproj}
+OUT=gpurun_out/${TAG}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+PROBE="dev/kernel_probe.py $WHAT --iters 5"
+i=0
+for group in \
+    "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" \
+    "SQ_INST_CYCLES_VMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM" \
+    "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i + 1))
+    rc=0
+    timeout -s KILL 60 rocprofv3 --pmc $group -d "$OUT/pass$i" -o run -- python3 $PROBE > "$OUT/pass$i.log" 2>&1 || rc=$?
+    echo "pass $i rc=$rc: $group"
+    if [[ $rc -ne 0 ]]; then tail -5 "$OUT/pass$i.log"; exit $rc; fi
+done
+for db in "$OUT"/pass*/*/*.db "$OUT"/pass*/*.db; do
+    [[ -f $db ]] && python3 dev/pmc_summary.py "$db" --match "$MATCH" \
+        > "${db%.db}_summary.json" && cat "${db%.db}_summary.json"
+done
+find "$OUT" -name "*.db" -delete
+exit 0

@@ -1,0 +1,56 @@
+"""Numerics report: native head (each precision policy) vs the CPU oracle in
+exact fp32 math and in the reference's numerics (fp16 cross-attention core).
+Run on a GPU box:  python dev/numerics_report.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "cmt-cooperative-perception_amd"))
+
+import torch  # noqa: E402
+
+from oracle import cmt_oracle as O  # noqa: E402
+from projects.mmdet3d_plugin import set_precision  # noqa: E402
+from projects.mmdet3d_plugin import synthetic as S  # noqa: E402
+
+KEYS = ("cls_logits", "center", "height", "dim", "rot", "vel")
+
+
+def run(name, variant, Nq, L, grid, B, cams, precs=("ref", "fp16", "bf16")):
+    dev = torch.device("cuda:0")
+    head, cfg, meta = S.build_synthetic_head(name, num_query=Nq, num_layers=L, grid_size=grid)
+    sd = S.head_state_dict(head)
+    oc = O.cfg_from_head_cfg(cfg)
+    g = grid or [1440, 1440]
+    x = S.synthetic_bev(B, g[0] // 8, g[1] // 8, seed=1)
+    xi = S.synthetic_img(B * cams, 8, 20, seed=2) if cams else None
+    metas = S.synthetic_metas(B, yaws=S.NUS_YAWS[:max(cams, 1)], pad_shape=(128, 320, 3), seed=3)
+    refs = {"fp16core": O.head_forward(oc, sd, x, xi, metas, variant, cross_core="fp16", self_core="fp32")[0],
+            "fp32math": O.head_forward(oc, sd, x, xi, metas, variant, cross_core="fp32", self_core="fp32")[0]}
+    d = refs["fp16core"]
+    e = {k: (d[k] - refs["fp32math"][k]).abs().max().item() for k in KEYS}
+    print(f"{name} Nq={Nq} L={L} B={B} cams={cams}: oracle fp16core vs fp32math",
+          {k: f"{v:.2e}" for k, v in e.items()})
+    head.to(dev)
+    for prec in precs:
+        set_precision(prec)
+        with torch.no_grad():
+            got = head([x.to(dev)], [xi.to(dev)] if xi is not None else None, metas)[0][0]
+        for rn, r in refs.items():
+            err = {k: (got[k].cpu().double() - r[k].double()).abs() for k in KEYS}
+            mx = {k: f"{v.max().item():.2e}" for k, v in err.items()}
+            mean = {k: f"{v.mean().item():.1e}" for k, v in err.items()}
+            print(f"  {prec:5s} vs {rn}: max {mx}\n{'':22s}mean {mean}")
+    set_precision("ref")
+    head.cpu()
+
+
+if __name__ == "__main__":
+    run("cmt_lidar_nus", "lidar", 64, 2, [256, 256, 40], 1, 0)
+    run("cmt_fusion_nus", "fusion", 64, 2, [256, 256, 40], 1, 3)
+    run("cmt_fusion_nus", "fusion", 48, 1, [192, 256, 40], 2, 2)
+    run("cmt_fusion_nus", "fusion", 48, 1, [256, 256, 40], 2, 2, precs=("ref",))
+    run("cmt_fusion_nus", "fusion", 48, 1, [192, 256, 40], 1, 2, precs=("ref",))
+    run("cmt_lidar_nus", "lidar", 900, 1, None, 1, 0)
