@@ -10,8 +10,10 @@ Policies (``set_precision`` / env ``CMT_PRECISION``):
   'ref'   -- the reference's numerics with fp32-accurate split GEMMs: every
              fp32 GEMM operand is carried as an f16 pair (hi, lo) (``SPLIT``,
              cmt_hip.h CMT_F16P) and multiplied in three f16 MFMA passes
-             (hi*hi + lo*hi + hi*lo, fp32 accumulate: ~2^-21 relative per
-             product, against TF32's 2^-11); self-attention core
+             (hi*hi + lo*hi + hi*lo, fp32 accumulate: per operand an error
+             <= max(2^-22 |x|, 2^-25) -- 2^-22 relative for |x| >= ~2^-3, the
+             absolute 2^-25 of an f16-subnormal lo below, ~2^-19 relative
+             for xavier-scale weights; TF32 would be 2^-11); self-attention core
              in exact f32 (nn.MultiheadAttention); cross-attention core in
              fp16 with fp32 accumulation, P rounded to fp16 and an fp16-rounded
              output (flash-attn 0.2.2 under auto_fp16).

@@ -12,7 +12,7 @@ for r in $(seq 1 "$ROUNDS"); do
     i=0
     for variant in "$@"; do
         i=$((i + 1))
-        env $variant timeout -k 10 200 python -u bench.py --steps 200 --warmup 30 --no-cpu-baseline --no-ref --no-batch2 \
+        env $variant timeout -k 10 200 python -u bench.py --steps 200 --warmup 30 --no-cpu-baseline --no-ref --no-recompute \
             --no-traffic > "$OUT/b_${r}_$i.json" 2> "$OUT/b_${r}_$i.log" || { echo "bench [$variant] failed"; tail -20 "$OUT/b_${r}_$i.log"; exit 1; }
         echo "round $r [$variant] $(python -c "import json; d=json.load(open('$OUT/b_${r}_$i.json')); print(d['value'], 'fps', d['ms_per_step'], 'ms attn', d['roofline']['avg_launch_ms'])")"
     done

@@ -18,7 +18,7 @@ for variant in "" "$@"; do
     i=$((i + 1))
     env $variant timeout -k 10 120 python -u dev/attn_exp.py --nk 56400 --bound \
         --check --tag "v$i:$variant" >> "$OUT/attn.txt" 2>&1 || { echo "attn_exp [$variant] failed"; tail -20 "$OUT/attn.txt"; exit 1; }
-    env $variant timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-ref --no-traffic --no-batch2 > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.log" \
+    env $variant timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-ref --no-traffic --no-recompute > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.log" \
         || { echo "bench [$variant] failed"; tail -20 "$OUT/bench_$i.log"; exit 1; }
     echo "[$variant] $(python -c "import json,sys; d=json.load(open('$OUT/bench_$i.json')); print(d['value'], 'fps', d['ms_per_step'], 'ms', 'attn', d['roofline']['avg_launch_ms'], 'ms', d['roofline']['frac'])")"
 done

@@ -28,13 +28,13 @@ if [[ $WHAT == all || $WHAT == prof ]]; then
     P=$OUT/prof_$WL
     mkdir -p "$P"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$P/trace" -o run --output-format csv -- \
-        python3 bench.py --workload $WL --steps 20 --warmup 5 --no-cpu-baseline --no-ref --no-traffic --no-batch2 \
+        python3 bench.py --workload $WL --steps 20 --warmup 5 --no-cpu-baseline --no-ref --no-traffic --no-recompute \
         > "$P/bench_trace.json" 2> "$P/trace.log" || { echo "trace pass failed"; tail -20 "$P/trace.log"; exit 1; }
     timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$P/fetch" -o run -- \
-        python3 bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-ref --no-traffic --no-graph --no-batch2 \
+        python3 bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-ref --no-traffic --no-graph --no-recompute \
         > "$P/bench_fetch.json" 2> "$P/fetch.log" || { echo "fetch pass failed"; tail -20 "$P/fetch.log"; exit 1; }
     timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$P/write" -o run -- \
-        python3 bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-ref --no-traffic --no-graph --no-batch2 \
+        python3 bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-ref --no-traffic --no-graph --no-recompute \
         > "$P/bench_write.json" 2> "$P/write.log" || { echo "write pass failed"; tail -20 "$P/write.log"; exit 1; }
     python3 dev/traffic_summary.py "$P" --tag "$TAG" --workload $WL \
         --nk ${NK[$WL]} --outdir "$P" > "$P/traffic.txt" 2>&1 || { echo "traffic summary failed"; cat "$P/traffic.txt"; exit 1; }

@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG}/trace
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-batch2 --no-ref "$@" \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-recompute --no-ref "$@" \
     > "$OUT/bench.json" 2> "$OUT/trace.log" || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
 cat "$OUT/bench.json"
 python3 dev/trace_table.py "$OUT" 28 > "gpurun_out/${TAG}/table.txt"

@@ -33,15 +33,20 @@ extern "C" {
 #define CMT_ABI_VERSION 14
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
- * x = hi + lo with hi = f16(x), lo = f16(x - hi) (22 significant bits: relative
- * error <= 2^-22 for |x| in f16's normal range, absolute <= 2^-25 below it;
- * |x| must stay below 65504).  A row of logical width C is stored as C hi
- * values followed by C lo values ([rows][2C] 16-bit words, leading dimensions
- * in 16-bit elements).  A GEMM whose A and W are both CMT_F16P computes
- * A_hi W_hi + A_lo W_hi + A_hi W_lo with fp32 accumulation (three f16 MFMA
- * passes; the dropped A_lo W_lo term is ~2^-22 of a product): the fp32 GEMMs
- * of the reference at 3/16 of the f16 rate instead of the exact-f32 MFMA's
- * 1/16, 16x tighter than a bf16 pair would be (2^-16) at the same rate.
+ * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
+ * |x - hi - lo| <= max(2^-22 |x|, 2^-25).  The relative 2^-22 (22 significant
+ * bits) holds only while lo is itself a normal f16 number, i.e. for |x| >= ~2^-3;
+ * below that lo is subnormal and the error is the absolute 2^-25 (the f16
+ * subnormal half-step): ~2^-19 relative at |x| ~ 0.05, the scale of xavier
+ * weights of a 256-wide layer, ~2^-16 at |x| ~ 0.005.  |x| must stay below
+ * 65504.  A row of logical width C is stored as C hi values followed by C lo
+ * values ([rows][2C] 16-bit words, leading dimensions in 16-bit elements).  A
+ * GEMM whose A and W are both CMT_F16P computes A_hi W_hi + A_lo W_hi + A_hi W_lo
+ * with fp32 accumulation (three f16 MFMA passes; the dropped A_lo W_lo term is
+ * <= 2^-22 of a product): per product the error is the two operands'
+ * representation errors above (tests/test_gpu_split.py::
+ * test_gemm_split_small_weights holds the kernel to that bound on xavier-range
+ * weights), at 3/16 of the f16 rate instead of the exact-f32 MFMA's 1/16.
  * Producers (LayerNorm, layout, geometry, GEMM epilogues, attention outputs)
  * write this format directly. */
 enum cmt_dtype { CMT_F32 = 0, CMT_F16 = 1, CMT_BF16 = 2, CMT_F16P = 3 };

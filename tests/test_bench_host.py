@@ -56,3 +56,15 @@ def test_missing_traffic_profile_fails_loudly():
 def test_cpu_threads_respects_omp(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
     assert 1 <= bench.cpu_threads() <= 3
+
+
+def test_bench_line_names_what_it_keeps():
+    """The headline keeps weight-only encodings like weight packs: the line must
+    list each of them and carry the recomputed-per-frame side key."""
+    import inspect
+    src = inspect.getsource(bench.main)
+    assert '"weight_only_kept"' in src and '"weight_only_recomputed"' in src
+    assert len(bench.WEIGHT_ONLY_KEPT) == 3
+    assert "stage_metas" in src            # the host fp64 inverse + staging runs once per timed step
+    _, _, fwd, _, _ = bench.make_workload("fusion", seed=0)
+    assert len(fwd.metas) == 1 and "lidar2img" in fwd.metas[0]

@@ -432,7 +432,7 @@ def test_bev_pos_hidden_cache(dev):
 
 
 def test_fusion_batch2_equals_two_single_frames(dev):
-    """Two frames in one forward (bench.py's `batch2` key) give each frame
+    """Two frames in one forward (bench.py --batch 2) give each frame
     exactly its single-frame outputs (bf16 bench policy, chain path, side
     stream): every kernel is per-row / per-(batch, head), so batching changes
     only how many rows a launch covers."""

@@ -72,6 +72,35 @@ def test_gemm_split_rows(N, dev, M, N_, K):
     assert err * 300 < bf
 
 
+@pytest.mark.parametrize("wscale", [0.05, 0.005])
+def test_gemm_split_small_weights(N, dev, wscale):
+    """Xavier-range weights (|w| <= 0.05 for a 256-wide layer; 0.005 as a harder
+    case): their f16-pair lo half is subnormal, so each weight carries the
+    absolute 2^-25 of CMT_F16P (include/cmt_hip.h), not 2^-22 relative.  The
+    kernel is held, element by element, to the bound that representation allows:
+    sum_k |a_k| e(w_k) + e(a_k) |w_k| (+ the dropped lo*lo term and fp32
+    accumulation), with e(x) = max(2^-22 |x|, 2^-25)."""
+    g = torch.Generator().manual_seed(7)
+    M, N_, K = 900, 256, 256
+    A = torch.randn(M, K, generator=g)
+    A[:, :32] *= 1e-3                       # small activations too (subnormal lo on that side)
+    W = (torch.rand(N_, K, generator=g) * 2 - 1) * wscale
+    ref = A.double() @ W.double().t()
+    out = torch.empty(M, N_, device=dev)
+    N.gemm(_pair(A).to(dev), _pair(W).to(dev), out, M=M, N=N_, K=K, lda=K, ldw=K, ldc=N_)
+    err = (out.cpu().double() - ref).abs()
+
+    def e(x):
+        return torch.maximum(x.abs().double() * 2 ** -22, torch.full_like(x.double(), 2 ** -25))
+    a, w = A.abs().double(), W.abs().double()
+    bound = a @ e(W).t() + e(A) @ w.t() + (a @ w.t()) * (K * 2 ** -24 + 2 ** -21)
+    worst = (err / bound).max().item()
+    rel = (err.max() / ref.abs().max()).item()
+    print(f"split GEMM, |w| <= {wscale}: max err {err.max().item():.2e} ({rel:.2e} of scale, ~2^{math.log2(rel):.1f}),"
+          f" max err / representation bound {worst:.3f}")
+    assert worst <= 1.0, worst
+
+
 @pytest.mark.parametrize("K,ks", [(256, 4), (1024, 4), (512, 2)])
 def test_gemm_split_k_into_layernorm(N, dev, K, ks):
     """Split-K pair GEMM (the decoder's out-projections / fc2 at 900 rows): ks fp32
