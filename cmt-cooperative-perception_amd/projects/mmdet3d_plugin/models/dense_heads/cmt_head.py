@@ -316,14 +316,27 @@ class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
         batch_y = (batch_y + 0.5) / y_size
         return torch.cat([batch_x[None], batch_y[None]], dim=0).view(2, -1).transpose(1, 0)
 
-    def _forward_agents(self, agents, img_metas, B, meta_fns=None):
+    def _forward_agents(self, agents, img_metas, B, meta_fns=None, shard=None):
         """Run the decoder for each (x, x_img, metas) agent, max-fusing into one
         [L, B*Nq, C] buffer, then the task heads.  ``meta_fns[i]`` maps the
         frame's img_metas to agent i's metas (identity by default); the ones of
-        the agents with cameras are kept for stage_metas."""
+        the agents with cameras are kept for stage_metas.
+
+        ``shard`` = (rank, world, group): agent sharding over the ranks of a
+        process group (SURVEY 8(e)'s optional second axis, configs[4]).  Rank r
+        decodes agents r, r + world, ... into its own buffer, and ONE
+        all_reduce(MAX) of the post-normed [L, B*Nq, C] outputs replaces the
+        in-process max over agents -- torch.max(torch.stack(...), 0) of
+        cmt_head_coop.py:383-389.  Max is exact and order-free, so every rank
+        then holds the single-process fused outputs bit for bit and runs the
+        task heads on them."""
         self._check_eval()
         fns = meta_fns if meta_fns is not None else [lambda m: m] * len(agents)
-        self._meta_plan = [fn for (_, x_img, _), fn in zip(agents, fns) if x_img is not None and self.variant != "lidar"]
+        mine = list(range(len(agents)))
+        if shard is not None:
+            rank, world, _ = shard
+            mine = [i for i in mine if i % world == rank]
+        self._meta_plan = [fns[i] for i in mine if agents[i][1] is not None and self.variant != "lidar"]
         prec = get_precision()
         L = self.transformer.decoder.num_layers
         outs = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=torch.float32,
@@ -332,9 +345,20 @@ class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
         if prec.gemm != torch.float32:
             outs16 = op_empty(B * self.num_query, self.hidden_dim, prec.gemm, outs.device, lead=(L,))
         self._h2d_seq = 0    # staging-buffer slot of each camera-matrix upload in this forward (engine._h2d)
-        for i, (x, x_img, metas) in enumerate(agents):
-            flags = native.LN_NAN_TO_NUM | (native.LN_MAX_INTO if i > 0 else 0)
+        if not mine:
+            outs.fill_(-float("inf"))   # a rank without an agent: the identity of the MAX all-reduce
+        for j, i in enumerate(mine):
+            x, x_img, metas = agents[i]
+            flags = native.LN_NAN_TO_NUM | (native.LN_MAX_INTO if j > 0 else 0)
             self._decode_agent(x, x_img, metas, B, outs, flags, self.variant, prec, out16=outs16)
+        if shard is not None:
+            import torch.distributed as dist
+            dist.all_reduce(outs, op=dist.ReduceOp.MAX, group=shard[2])
+            if outs16 is not None:   # the compute-dtype copy of the fused outputs (task-head GEMM operand)
+                if is_split(outs16):
+                    native.split_rows(outs.view(-1, self.hidden_dim), outs16.view(-1, 2, self.hidden_dim))
+                else:
+                    native.cast(outs, outs16)
         return self._task_outputs(outs, B, prec, outs16)
 
     def forward_single(self, x, x_img, img_metas):

@@ -7,7 +7,8 @@ Reference: projects/mmdet3d_plugin/models/dense_heads/cmt_head_coop.py
 One decoder pass per agent with the shared head weights; the element-wise
 max over agents is fused into the post_norm kernel of the second agent
 (LN_MAX_INTO), then the task heads run once.  ``forward_agents`` generalises
-the two-agent max to any number of agents (the 4-agent stress config).
+the two-agent max to any number of agents (the 4-agent stress config) and can
+shard the agents over the ranks of a process group (one MAX all-reduce).
 """
 import torch
 
@@ -72,12 +73,18 @@ class CmtHeadCoop(CmtHead):
         return multi_apply(self.forward_single, vehicle_pts_feats or none, infrastructure_pts_feats or none,
                            vehicle_img_feats or none, infrastructure_img_feats or none, img_metas)
 
-    def forward_agents(self, agents, img_metas):
+    def forward_agents(self, agents, img_metas, group=None):
         """Any number of agents: ``agents`` = list of (prefix, pts_feat, img_feat);
         outputs max-fused over agents (the reference fuses exactly two).  Agent
         metas are selected by key prefix as filter_img_metas does for the two
         reference agents; with other prefixes (e.g. 'agent2_') every other
-        agent's prefixed keys are dropped."""
+        agent's prefixed keys are dropped.
+
+        ``group``: a torch.distributed process group (or True for the default
+        group) over which the agents are SHARDED -- rank r decodes agents r,
+        r + world, ... and one all_reduce(MAX) fuses them (configs[4] latency
+        option); every rank passes the same agent list (a rank
+        only reads the features of its own agents) and gets the fused outputs."""
         B = len(img_metas)
         prefixes = [p for p, _, _ in agents]
         if set(prefixes) <= {"vehicle_", "infrastructure_"}:
@@ -88,7 +95,12 @@ class CmtHeadCoop(CmtHead):
         triples = [(x, xi, fn(img_metas)) for (_, x, xi), fn in zip(agents, fns)]
         if self.training:
             return self.forward_train(triples, img_metas, *gt_from_metas(img_metas))
-        return self._forward_agents(triples, img_metas, B, meta_fns=fns)
+        shard = None
+        if group is not None:
+            import torch.distributed as dist
+            g = None if group is True else group
+            shard = (dist.get_rank(g), dist.get_world_size(g), g)
+        return self._forward_agents(triples, img_metas, B, meta_fns=fns, shard=shard)
 
     @staticmethod
     def _select_metas(meta, prefix, prefixes):

@@ -89,3 +89,60 @@ def test_spawned_ranks_run_head_frames(tmp_path):
     assert r[0]["fps"] == pytest.approx(2 * 3 / r[0]["elapsed"])   # whole-job frames / max time
     assert r[0]["frames"] == r[1]["frames"] == 4
     assert r[0]["checksum"] != r[1]["checksum"]                 # each rank its own frames
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "cmt-cooperative-perception_amd")]
+    import torch.distributed as dist
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.models.dense_heads.cmt_head import CmtHead
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    set_precision("exact")     # fp32 GEMM policy: no compute-dtype copy of the outputs
+    head, _, _ = S.build_synthetic_head("cmtcoop_lidar_tumtraf", num_query=8, num_layers=2)
+    decoded = []
+
+    def fake_decode(self, x, x_img, metas, B, out, flags, variant, prec, out16=None):
+        # agent-specific values; MAX_INTO semantics of the post-norm kernel
+        decoded.append(int(x[0, 0, 0, 0].item()))
+        val = torch.sin(torch.arange(out.numel(), dtype=torch.float32) * (1 + x[0, 0, 0, 0])).view_as(out)
+        if flags & 2:   # native.LN_MAX_INTO
+            torch.maximum(out, val, out=out)
+        else:
+            out.copy_(val)
+    CmtHead._decode_agent = fake_decode
+    CmtHead._task_outputs = lambda self, outs, B, prec, outs16=None: [dict(outs=outs.clone())]
+    CmtHead._check_eval = lambda self: None
+    agents = [(f"agent{i}_", torch.full((1, 4, 2, 2), float(i)), None) for i in range(5)]
+    single = head.forward_agents(agents, [dict()])[0]["outs"]
+    n_single = len(decoded)
+    decoded.clear()
+    sharded = head.forward_agents(agents, [dict()], group=True)[0]["outs"]
+    q.put((rank, decoded, n_single, torch.equal(single, sharded)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_agent_sharding_assignment_and_max(world):
+    """forward_agents(group=...): rank r decodes agents r, r + world, ... and
+    the MAX all-reduce reproduces the single-process max-fused outputs
+    (the decoder itself is faked: the GPU test covers it bit-exactly)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, dec, n_single, eq in res:
+        assert n_single == 5
+        assert dec == [i for i in range(5) if i % world == rank]
+        assert eq
