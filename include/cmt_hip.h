@@ -186,8 +186,11 @@ int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
  *        CMT_ATTN_FOLD_SCALE    the kernel may fold scale*log2(e) into Q when
  *                               it loads Q (one extra rounding of Q in the
  *                               compute dtype; used by the f16/bf16 policies,
- *                               not by the reference-numerics policy) */
-enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2 };
+ *                               not by the reference-numerics policy)
+ *        CMT_ATTN_FORCE_PINGPONG  diagnostic: the f16 bounded long-key path
+ *                               runs the ping-pong kernel instead of the
+ *                               software-pipelined one (A/B and tests) */
+enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2, CMT_ATTN_FORCE_PINGPONG = 256 };
 
 typedef struct cmt_attn_args {
     int B, H, Nq, Nk;
