@@ -1407,8 +1407,12 @@ __device__ __forceinline__ void sp_online_split(const AttnKParams& p, const f16_
 }
 
 // BAR2: one workgroup barrier per two tiles (the steady loop's pairs) instead of per tile;
-// PRIO: s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md 'Two waves per SIMD', item 4)
-template <bool QS, bool BAR2, bool PRIO>
+// PRIO: s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md 'Two waves per SIMD', item 4).
+// (Running waves 4-7 half an iteration behind -- the halves below allow it -- needs a second
+// copy of the loop whose live ranges spill: 256 VGPRs + 170 spilled; not kept.)
+// NOSYNC (diagnostic only, CMT_ATTN_SP bit 16, wrong results): no barrier and no LDS-DMA after
+// the prologue -- the compute stream alone, on whatever the ring holds
+template <bool QS, bool BAR2, bool PRIO, bool NOSYNC = false>
 __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
     typedef f16x8 frag;
     constexpr int STAGE = 2 * KT * D;                  // f16 elements per ring slot: K tile then V tile
@@ -1452,9 +1456,15 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
     const f16_t* const dsrc = isk ? Kb + 8 * (cch ^ ((prow >> 2) & 3)) : Vb + 8 * cch;
     const int64_t drs = isk ? p.k_rs : p.v_rs;
     f16_t* const ddst = ring + (isk ? 0 : KT * D) + (wave & 3) * 16 * D;
+    // tiles are issued in order: the source advances by one tile per issue (no per-issue
+    // multiply); only the ragged last tile clamps its rows (masked in compute)
+    const f16_t* dcur = dsrc + (int64_t)(t_begin * KT + prow) * drs;
+    const int64_t dstep = (int64_t)KT * drs;
     auto issue = [&](int i, int slot) {   // split-local tile i into ring slot `slot`
-        const int key = min((t_begin + i) * KT + prow, p.Nk - 1);   // ragged tail: clamped, masked in compute
-        dma16(dsrc + (int64_t)key * drs, ddst + slot * STAGE);
+        const f16_t* src = dcur;
+        if ((t_begin + i + 1) * KT > p.Nk) src = dsrc + (int64_t)min((t_begin + i) * KT + prow, p.Nk - 1) * drs;
+        dma16(src, ddst + slot * STAGE);
+        dcur += dstep;
     };
     const int npre = min(nt, SP_RING - 1);
     for (int i = 0; i < npre; ++i) issue(i, i);
@@ -1489,7 +1499,7 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
     const PpLane lane_ofs = pp_lane(lane, 2);
     f32x16 S[2][2];        // [parity of the tile][kb]: S^T = K Q^T - off
     frag P[2][2][2];       // [parity][kb][ss]: P^T fragments (f16)
-    frag kf[2][2], vf[2][2];
+    frag kf[2][2], vf[2][2][2];   // vf[parity of the tile]: V is read one iteration ahead
     f32x16 o;
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[r] = 0.f;
@@ -1525,12 +1535,12 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) pf[kb][r >> 3][r & 7] = (f16_t)__builtin_amdgcn_exp2f(s[kb][r]);
     };
-    auto pv = [&](const frag (&pf)[2][2]) {
+    auto pv = [&](const frag (&pf)[2][2], const frag (&vv)[2][2]) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[kb][ss], pf[kb][ss], o, 0, 0, 0);
+                o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[kb][ss], pf[kb][ss], o, 0, 0, 0);
                 lsum = rs16_mma<f16_t>(pf[kb][ss], lsum, lane);
             }
     };
@@ -1538,6 +1548,7 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
     // end of iteration t: tile t+2 landed for everyone, every wave done with tile t-1's slot,
     // which then takes tile t + SP_RING - 1
     auto sync = [&](int t) {
+        if constexpr (NOSYNC) return;
         if (t + 2 < nt) wait_tile(t + 2, last_issued);
         barrier_mem();
         if (t + SP_RING - 1 < nt) {
@@ -1549,71 +1560,79 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
     // steady-state form (QKN and PVP) is written slot by slot: slot i = one MFMA, then the two
     // exponentials of score pair i and the f16 pack of pair i-1, fenced by sched_barrier so the
     // compiler keeps this order (left alone it clusters the exponentials ahead of the MFMAs).
-    // MFMA order: the four row sums of P[t-1] (no LDS operand: cover the fragment reads), the
-    // QK^T chains of tile t+1, then P[t-1] V[t-1].
+    // MFMA order: the four row sums of P[t-1], then P[t-1] V[t-1] (V read one iteration ahead),
+    // then the QK^T chains of tile t+1, whose K fragments (read at the top of the iteration) get
+    // eight slots to land.  It is written as two halves (slots [0, NM/2)
+    // with the fragment reads first, then [NM/2, NM) and the last pack).
+    float ea = 0.f, eb = 0.f;   // the exponentials of the pending pack (the previous pair) between slots
+    auto half = [&](auto par, auto hf, int t) {
+        constexpr int PAR = decltype(par)::value, HF = decltype(hf)::value;
+        constexpr int NM = QS ? 16 : 12;                      // MFMAs of the iteration
+        f32x16(&sn)[2] = S[PAR ^ 1];
+        const f32x16(&sc)[2] = S[PAR];
+        frag(&pn)[2][2] = P[PAR];
+        const frag(&pp)[2][2] = P[PAR ^ 1];
+        const frag(&vp)[2][2] = vf[PAR ^ 1];                 // V[t-1], read in iteration t-1
+        if constexpr (HF == 0) {
+            const PpLane l = pp_launder(lane_ofs);
+            pp_load_k<f16_t>(slot_of(t + 1), l, kf);
+            pp_load_v<f16_t>(slot_of(t) + KV_B, l, vf[PAR]);   // V[t] for the next iteration
+        }
+        auto mfma = [&](int i) {
+            if (i < 4) {                                      // row sums of P[t-1]
+                lsum = rs16_mma<f16_t>(pp[i >> 1][i & 1], lsum, lane);
+            } else if (i < 8) {                               // P[t-1] V[t-1] (registers since the last iteration)
+                const int j = i - 4;
+                o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vp[j >> 1][j & 1], pp[j >> 1][j & 1], o, 0, 0, 0);
+            } else {                                          // QK^T(t+1): per kb 2 (fold) or 4 (QS) MFMAs
+                const int j = i - 8, per = QS ? 4 : 2, kb = j / per, k = j % per;
+                const frag& qop = (k >> 1) ? ql[k & 1] : qf[k & 1];
+                sn[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][k & 1], qop, k == 0 ? sinit : sn[kb], 0, 0, 0);
+            }
+        };
+        // score pair m (0..15): s[kb][r], s[kb][r + 1] with kb = m >> 3, r = 2 (m & 7).  The
+        // exponentials are volatile asm (they cannot be hoisted above their slot); the packs are
+        // laundered (they cannot sink below it); sched_barrier keeps the slots apart.
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        auto pack = [&](int m) {
+            h2 v = {(f16_t)ea, (f16_t)eb};
+            asm volatile("" : "+v"(v));
+            const int kb = m >> 3, r = 2 * (m & 7);
+            pn[kb][r >> 3][r & 7] = v[0];
+            pn[kb][r >> 3][(r & 7) + 1] = v[1];
+        };
+#pragma unroll
+        for (int i = HF * NM / 2; i < (HF + 1) * NM / 2; ++i) {
+            mfma(i);
+            const int m0 = i * 16 / NM, m1 = (i + 1) * 16 / NM;
+#pragma unroll
+            for (int m = m0; m < m1; ++m) {
+                const int kb = m >> 3, r = 2 * (m & 7);
+                // (an MFMA result of the previous iteration: the VALU read-after-MFMA wait
+                // states are long covered by the sync in between)
+                float na, nb;
+                asm volatile("v_exp_f32 %0, %1" : "=v"(na) : "v"(sc[kb][r]));
+                asm volatile("v_exp_f32 %0, %1" : "=v"(nb) : "v"(sc[kb][r + 1]));
+                if (m > 0) pack(m - 1);
+                ea = na;
+                eb = nb;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (HF == 1) pack(15);
+    };
     auto iter = [&](auto par, auto qkn, auto pvp, int t, bool mask_t) {
         constexpr int PAR = decltype(par)::value;
         constexpr bool QKN = decltype(qkn)::value, PVP = decltype(pvp)::value;
-        {
-            const PpLane l = pp_launder(lane_ofs);
-            if constexpr (QKN) pp_load_k<f16_t>(slot_of(t + 1), l, kf);
-            if constexpr (PVP) pp_load_v<f16_t>(slot_of(t - 1) + KV_B, l, vf);
-        }
         if constexpr (QKN && PVP) {
-            constexpr int NM = QS ? 16 : 12;                  // MFMAs of the iteration
-            f32x16(&sn)[2] = S[PAR ^ 1];
-            const f32x16(&sc)[2] = S[PAR];
-            frag(&pn)[2][2] = P[PAR];
-            const frag(&pp)[2][2] = P[PAR ^ 1];
-            auto mfma = [&](int i) {
-                if (i < 4) {                                  // row sums of P[t-1]
-                    lsum = rs16_mma<f16_t>(pp[i >> 1][i & 1], lsum, lane);
-                } else if (i < 4 + (NM - 8)) {                // QK^T(t+1): per kb 2 (fold) or 4 (QS) MFMAs
-                    const int j = i - 4, per = QS ? 4 : 2, kb = j / per, k = j % per;
-                    const frag& qop = (k >> 1) ? ql[k & 1] : qf[k & 1];
-                    sn[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][k & 1], qop, k == 0 ? sinit : sn[kb], 0,
-                                                                   0, 0);
-                } else {                                      // P[t-1] V[t-1]
-                    const int j = i - (NM - 4);
-                    o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[j >> 1][j & 1], pp[j >> 1][j & 1], o, 0, 0, 0);
-                }
-            };
-            // score pair m (0..15): s[kb][r], s[kb][r + 1] with kb = m >> 3, r = 2 (m & 7).  Slot i:
-            // MFMA i, the exponentials of its pairs (volatile asm, so they cannot be hoisted above
-            // the slot) and the packs of the previous pairs (laundered, so they cannot sink below
-            // it); sched_barrier keeps the slots apart.
-            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-            float ea = 0.f, eb = 0.f;
-            int mprev = -1;
-            auto pack = [&](int m) {
-                h2 v = {(f16_t)ea, (f16_t)eb};
-                asm volatile("" : "+v"(v));
-                const int kb = m >> 3, r = 2 * (m & 7);
-                pn[kb][r >> 3][r & 7] = v[0];
-                pn[kb][r >> 3][(r & 7) + 1] = v[1];
-            };
-#pragma unroll
-            for (int i = 0; i < NM; ++i) {
-                mfma(i);
-                const int m0 = i * 16 / NM, m1 = (i + 1) * 16 / NM;
-#pragma unroll
-                for (int m = m0; m < m1; ++m) {
-                    const int kb = m >> 3, r = 2 * (m & 7);
-                    // v_exp_f32 as volatile asm: ordered with the slot's fences and reading the
-                    // accumulator in place (an MFMA result of the previous iteration: the VALU
-                    // read-after-MFMA wait states are long covered by the sync in between)
-                    float na, nb;
-                    asm volatile("v_exp_f32 %0, %1" : "=v"(na) : "v"(sc[kb][r]));
-                    asm volatile("v_exp_f32 %0, %1" : "=v"(nb) : "v"(sc[kb][r + 1]));
-                    if (mprev >= 0) pack(mprev);
-                    ea = na;
-                    eb = nb;
-                    mprev = m;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            pack(mprev);
+            half(par, std::integral_constant<int, 0>{}, t);
+            half(par, std::integral_constant<int, 1>{}, t);
         } else {
+            {
+                const PpLane l = pp_launder(lane_ofs);
+                if constexpr (QKN) pp_load_k<f16_t>(slot_of(t + 1), l, kf);
+                pp_load_v<f16_t>(slot_of(t) + KV_B, l, vf[PAR]);   // V[t] for the next iteration / the drain
+            }
             if (mask_t) {   // the ragged last tile of the last split: keys >= Nk score -inf
                 const int key0 = (t_begin + t) * KT;
 #pragma unroll
@@ -1625,7 +1644,7 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
             }
             ex(S[PAR], P[PAR]);
             if constexpr (QKN) qk(S[PAR ^ 1]);
-            if constexpr (PVP) pv(P[PAR ^ 1]);
+            if constexpr (PVP) pv(P[PAR ^ 1], vf[PAR ^ 1]);
         }
     };
     using I0 = std::integral_constant<int, 0>;
@@ -1680,17 +1699,19 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
             if constexpr (BAR2) sync_first();
             else sync(0);
             int t = 1;
-            for (; t + 2 < nt; t += 2) {   // iterations t (odd) and t + 1 (even), both < nt - 1
-                if (live) iter(I1{}, BT{}, BT{}, t, false);
-                if constexpr (!BAR2) sync(t);
-                if (live) iter(I0{}, BT{}, BT{}, t + 1, false);
-                if constexpr (BAR2) sync2(t);
-                else sync(t + 1);
-            }
-            if (t < nt - 1) {              // one more middle iteration (odd t)
-                if (live) iter(I1{}, BT{}, BT{}, t, false);
-                sync(t);
-                ++t;
+            {
+                for (; t + 2 < nt; t += 2) {   // iterations t (odd) and t + 1 (even), both < nt - 1
+                    if (live) iter(I1{}, BT{}, BT{}, t, false);
+                    if constexpr (!BAR2) sync(t);
+                    if (live) iter(I0{}, BT{}, BT{}, t + 1, false);
+                    if constexpr (BAR2) sync2(t);
+                    else sync(t + 1);
+                }
+                if (t < nt - 1) {              // one more middle iteration (odd t)
+                    if (live) iter(I1{}, BT{}, BT{}, t, false);
+                    sync(t);
+                    ++t;
+                }
             }
             // last tile: exp (masked if ragged) and the previous tile's PV
             if (live) {
@@ -1699,12 +1720,10 @@ __global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
             }
         }
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-        // drain: PV of the last tile
+        // drain: PV of the last tile (its V read by the last iteration)
         if (live) {
-            const PpLane l = pp_launder(lane_ofs);
-            pp_load_v<f16_t>(slot_of(nt - 1) + KV_B, l, vf);
-            if ((nt - 1) & 1) pv(P[1]);
-            else pv(P[0]);
+            if ((nt - 1) & 1) pv(P[1], vf[1]);
+            else pv(P[0], vf[0]);
         }
     }
     float l_tot = rs16_total(lsum, lane);
@@ -2072,7 +2091,8 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
             // f16 with bounded offsets: the software-pipelined single-stream kernel
 #define SPK(QS, B2, PR) attn_sp_kernel<QS, B2, PR><<<nwg, 512, 0, s>>>(p)
             const bool b2 = (spm & 2) != 0, pr = (spm & 4) != 0;
-            if (fold) {
+            if (spm & 16) attn_sp_kernel<true, false, false, true><<<nwg, 512, 0, s>>>(p);   // diagnostic
+            else if (fold) {
                 if (b2) { if (pr) SPK(false, true, true); else SPK(false, true, false); }
                 else { if (pr) SPK(false, false, true); else SPK(false, false, false); }
             } else {

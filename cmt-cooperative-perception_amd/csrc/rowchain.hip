@@ -500,12 +500,15 @@ __global__ __launch_bounds__(NTC, 1) void chain_kernel(cmt_chain_args a) {
 
 }  // namespace
 
+int cmt_chain_x3(const cmt_chain_args& a, hipStream_t s);   // rowchain_x3.hip
+
 extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_chain: null args");
     const cmt_chain_args& a = *ap;
     CMT_REQUIRE(a.kind >= 0 && a.kind <= 2, "cmt_chain: kind must be 0 (A), 1 (B1) or 2 (B2)");
     CMT_REQUIRE(a.rows > 0 && a.Nq > 0 && a.rows % a.Nq == 0, "cmt_chain: rows must be B * Nq");
-    CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16, "cmt_chain: dtype must be f16 or bf16");
+    CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16 || a.dtype == CMT_F16P,
+                "cmt_chain: dtype must be f16, bf16 or the f16 pair (CMT_F16P)");
     CMT_REQUIRE(a.prm && a.Y, "cmt_chain: null pointer");
     if (a.kind == 0) CMT_REQUIRE(a.X && a.P && a.Wo && a.W1 && a.Q, "cmt_chain: chain A needs X, P, Wo, W1, Q");
     if (a.kind == 1) CMT_REQUIRE(a.X && a.Wo && a.W1 && a.W2 && a.WS, "cmt_chain: chain B1 needs X, Wo, W1, W2, WS");
@@ -520,6 +523,7 @@ extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
                  (uintptr_t)a.WS | (uintptr_t)a.Q) % 16 == 0 && (uintptr_t)a.OUT16 % 8 == 0,
                 "cmt_chain: buffers must be 16-byte aligned");
     hipStream_t s = (hipStream_t)stream;
+    if (a.dtype == CMT_F16P) return cmt_chain_x3(a, s);   // rowchain_x3.hip
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
 #define CHAIN_LAUNCH(T)                                                    \

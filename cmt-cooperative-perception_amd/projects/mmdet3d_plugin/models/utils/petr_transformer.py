@@ -43,6 +43,14 @@ def _wo(lw):
     return lw["sa_owp"] if lw.get("sa_owp") is not None else lw["sa_ow"]
 
 
+def _b1w(lw):
+    """Chain B1's out_proj and fc1 weights: row-major (f16 / bf16 chains) or fragment-major pair
+    packs (the split chains)."""
+    if lw.get("ca_owp") is not None:
+        return lw["ca_owp"], lw["f1_wp"]
+    return lw["ca_ow"], lw["f1_w"]
+
+
 def _rows(x):
     """[N, B, C] -> contiguous fp32 [N*B, C]."""
     return x.reshape(-1, x.shape[-1]).contiguous().float()
@@ -527,6 +535,8 @@ class PETRTransformerDecoder(nn.Module):
                 ca = lay.attentions[1].attn
                 ffn = lay.ffns[0]
                 chain = g in (torch.float16, torch.bfloat16)   # the row-block chains' fragment-major copies
+                # the split chains (rowchain_x3.hip): every chain weight as a fragment-major pair pack
+                sp = g == SPLIT and self._chain_ok() and tuple(ffn.layers[1].weight.shape) == (256, 1024)
                 layers.append(dict(
                     sa_w=to_dtype(sa.in_proj_weight, g), sa_b=sa.in_proj_bias.detach().contiguous(),
                     # chain B2's copy of the in_proj weights, fragment-major (cmt_hip.h cmt_chain_args.Wn)
@@ -548,6 +558,14 @@ class PETRTransformerDecoder(nn.Module):
                            if chain and tuple(ffn.layers[1].weight.shape) == (256, 1024) else None),
                     norms=[(n.weight.detach().contiguous(), n.bias.detach().contiguous(), n.eps)
                            for n in lay.norms]))
+                if sp:
+                    lw = layers[-1]
+                    lw.update(sa_wp=native.pack_chain_pair(lw["sa_w"].view(3 * C, 2, C)),
+                              sa_owp=native.pack_chain_pair(lw["sa_ow"].view(C, 2, C)),
+                              ca_wqp=native.pack_chain_pair(lw["ca_wq"].view(C, 2, C)),
+                              ca_owp=native.pack_chain_pair(lw["ca_ow"].view(C, 2, C)),
+                              f1_wp=native.pack_chain_pair(lw["f1_w"].view(4 * C, 2, C)),
+                              f2_wp=native.pack_chain_fc2_pair(lw["f2_w"].view(C, 2, 4 * C)))
                 kw.append(ca.in_proj_weight[C:2 * C])
                 vw.append(ca.in_proj_weight[2 * C:])
                 if ca.in_proj_bias is not None:
@@ -642,8 +660,9 @@ class PETRTransformerDecoder(nn.Module):
         return out
 
     def _use_chain(self, prec):
-        """Row-block chains (f16 / bf16 policies; CMT_CHAIN=0: separate launches)."""
-        return self._chain_ok() and get_precision(prec).gemm != SPLIT and OPTIONS.chain
+        """Row-block chains (f16 / bf16 policies, and their split-f16 form under the 'ref'
+        policy; CMT_CHAIN=0: separate launches)."""
+        return self._chain_ok() and get_precision(prec).gemm != torch.float32 and OPTIONS.chain
 
     def prologue_ok(self, prec):
         """Whether run_rows takes a lowp_state whose layer 0 up to the
@@ -843,7 +862,7 @@ class PETRTransformerDecoder(nn.Module):
                              eps=eps, R=tgt, Q=st["qc"])
                 self._cross_attn(st["qc"], kv, kvl[l], st["ob"], B=B, Nq=Nq, Nk=Nk, ws=st["ws"], prec=prec)
                 nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
-                native.chain(1, st["ob"], None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
+                native.chain(1, st["ob"], None, ch["B"][l], *_b1w(lw), tgt, rows=rows, Nq=Nq, eps=eps,
                              R=st["t1n"], W2=lw["f2_wp"], WS=st["cws"])
                 native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                              Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
@@ -911,7 +930,7 @@ class PETRTransformerDecoder(nn.Module):
                              R=tgt, Q=qc)
             self._cross_attn(qc, kv, kvl[l], ob, B=B, Nq=Nq, Nk=Nk, ws=ws, prec=prec)
             nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
-            native.chain(1, ob, None, ch["B"][l], lw["ca_ow"], lw["f1_w"], tgt, rows=rows, Nq=Nq, eps=eps,
+            native.chain(1, ob, None, ch["B"][l], *_b1w(lw), tgt, rows=rows, Nq=Nq, eps=eps,
                          R=t1n, W2=lw["f2_wp"], WS=cws)
             native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                          Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,

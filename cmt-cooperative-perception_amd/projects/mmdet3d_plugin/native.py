@@ -530,33 +530,74 @@ def pack_chain_fc2(W2):
     return pack_chain_wn(torch.cat([W2[:, 256 * g:256 * (g + 1)] for g in range(4)], 0))
 
 
+def pack_chain_pair(Wp):
+    """Split-f16 weight (uint16 [256 G, 2, 256], the CMT_F16P rows to_dtype
+    writes) -> the split chains' fragment-major pair pack: pack_chain_wn of the
+    hi halves, then of the lo halves (cmt_hip.h cmt_chain_args, dtype CMT_F16P)."""
+    if Wp.dtype != torch.uint16 or Wp.dim() != 3 or Wp.shape[1] != 2:
+        raise RuntimeError("pack_chain_pair: weight must be split-f16 rows [R, 2, C]")
+    h = Wp.view(torch.float16)
+    return torch.cat([pack_chain_wn(h[:, 0].contiguous()), pack_chain_wn(h[:, 1].contiguous())]).view(torch.uint16)
+
+
+def pack_chain_fc2_pair(W2p):
+    """Split-f16 fc2.weight [256, 2, 1024] -> its four K blocks packed as
+    pack_chain_fc2 does, hi halves then lo halves."""
+    if W2p.dtype != torch.uint16 or tuple(W2p.shape) != (256, 2, 1024):
+        raise RuntimeError("pack_chain_fc2_pair: fc2.weight must be split-f16 [256, 2, 1024]")
+    h = W2p.view(torch.float16)
+    return torch.cat([pack_chain_fc2(h[:, 0].contiguous()), pack_chain_fc2(h[:, 1].contiguous())]).view(torch.uint16)
+
+
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
           out_flags=0, Q=None, WS=None, OUT16=None):
     """One row-block chain of a decoder layer's query side (cmt_chain): kind 0
-    after self-attention; kinds 1 then 2 after cross-attention (cmt_hip.h)."""
+    after self-attention; kinds 1 then 2 after cross-attention (cmt_hip.h).
+    Split-f16 operands (torch.uint16: the 'ref' policy) select the split chains:
+    X / OUT16 pair rows, every weight a fragment-major pair pack
+    (pack_chain_pair / pack_chain_fc2_pair; chain B1's W1 is fc1's), chain A's
+    Q f16 head-split, chain B2's Q head-split pairs."""
     _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16)
-    if Wn is not None and (Wn.dim() != 1 or Wn.numel() != 768 * 256):
-        raise RuntimeError("cmt_chain: Wn must be fragment-major (pack_chain_wn)")
-    if kind == 1 and (W2 is None or W2.dim() != 1 or W2.numel() != 256 * 1024):
-        raise RuntimeError("cmt_chain: chain B1's W2 must be fragment-major (pack_chain_fc2)")
-    if kind == 0 and (W1 is None or W1.dim() != 1 or W1.numel() != 256 * 256):
-        raise RuntimeError("cmt_chain: chain A's W1 must be fragment-major (pack_chain_wn)")
+    split = any(t is not None and t.dtype == torch.uint16 for t in (X, Wo, W1, W2, Wn))
+    pw = 2 if split else 1   # a pair pack holds the hi pack, then the lo pack
+    if Wn is not None and (Wn.dim() != 1 or Wn.numel() != pw * 768 * 256):
+        raise RuntimeError("cmt_chain: Wn must be fragment-major (pack_chain_wn / pack_chain_pair)")
+    if kind == 1 and (W2 is None or W2.dim() != 1 or W2.numel() != pw * 256 * 1024):
+        raise RuntimeError("cmt_chain: chain B1's W2 must be fragment-major (pack_chain_fc2 / pack_chain_fc2_pair)")
+    if kind == 0 and (W1 is None or W1.dim() != 1 or W1.numel() != pw * 256 * 256):
+        raise RuntimeError("cmt_chain: chain A's W1 must be fragment-major (pack_chain_wn / pack_chain_pair)")
     # chain A's Wo: row-major [256, 256] (LDS weight ring) or fragment-major 1-D (pack_chain_wn: registers)
     wo_frag = int(kind == 0 and Wo is not None and Wo.dim() == 1)
-    if wo_frag and Wo.numel() != 256 * 256:
-        raise RuntimeError("cmt_chain: a fragment-major Wo must be pack_chain_wn of [256, 256]")
-    if OUT16 is not None and (OUT is None or OUT16.dtype not in (torch.float16, torch.bfloat16)):
-        raise RuntimeError("cmt_chain: OUT16 must be a 16-bit copy target beside OUT")
+    if wo_frag and Wo.numel() != pw * 256 * 256:
+        raise RuntimeError("cmt_chain: a fragment-major Wo must be pack_chain_wn / pack_chain_pair of [256, 256]")
     if prm.dtype != torch.float32 or prm.numel() != CHAIN_PRM[kind]:
         raise RuntimeError(f"cmt_chain: parameter block must be {CHAIN_PRM[kind]} fp32 values")
     if WS is not None and (WS.dtype != torch.float32 or WS.numel() < chain_ws_numel(rows)):
         raise RuntimeError("cmt_chain: WS must hold chain_ws_numel(rows) fp32")
-    lows = [t for t in (X, Wo, W1, W2, Wn, Q, OUT16) if t is not None]
-    if any(t.dtype != lows[0].dtype for t in lows) or (lows and lows[0].dtype not in (torch.float16, torch.bfloat16)):
-        raise RuntimeError("cmt_chain: X, Wo, W1, W2, Wn, Q and OUT16 must share one 16-bit dtype (f16 or bf16)")
     a = ChainArgs()
     a.kind, a.rows, a.Nq, a.eps = kind, rows, Nq, eps
-    a.dtype = DT[lows[0].dtype] if lows else BF16   # B2 without in_proj: no 16-bit operand
+    if split:
+        if kind != 2 and (X is None or X.dtype != torch.uint16):
+            raise RuntimeError("cmt_chain: the split chains take pair-row X")
+        if any(t is not None and (t.dtype != torch.uint16 or t.dim() != 1) for t in (Wo, W1, W2, Wn)):
+            raise RuntimeError("cmt_chain: the split chains take fragment-major pair weights")
+        if kind == 1 and (W1.numel() != 2 * 1024 * 256 or Wo.numel() != 2 * 256 * 256):
+            raise RuntimeError("cmt_chain: split chain B1 takes fragment-major pair packs of Wo and fc1")
+        if kind == 0 and not wo_frag:
+            raise RuntimeError("cmt_chain: split chain A takes a fragment-major pair pack of Wo")
+        if Q is not None and Q.dtype != (torch.float16 if kind == 0 else torch.uint16):
+            raise RuntimeError("cmt_chain: split chain A writes an f16 Q, chain B2 head-split pairs")
+        if OUT16 is not None and (OUT is None or OUT16.dtype != torch.uint16):
+            raise RuntimeError("cmt_chain: split OUT16 is the pair copy of OUT")
+        a.dtype = F16P
+    else:
+        if OUT16 is not None and (OUT is None or OUT16.dtype not in (torch.float16, torch.bfloat16)):
+            raise RuntimeError("cmt_chain: OUT16 must be a 16-bit copy target beside OUT")
+        lows = [t for t in (X, Wo, W1, W2, Wn, Q, OUT16) if t is not None]
+        if any(t.dtype != lows[0].dtype for t in lows) or (lows and lows[0].dtype not in (torch.float16,
+                                                                                          torch.bfloat16)):
+            raise RuntimeError("cmt_chain: X, Wo, W1, W2, Wn, Q and OUT16 must share one 16-bit dtype (f16 or bf16)")
+        a.dtype = DT[lows[0].dtype] if lows else BF16   # B2 without in_proj: no 16-bit operand
 
     def ptr(t):
         return None if t is None else t.data_ptr()
@@ -567,7 +608,8 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     a.out_flags = out_flags
     a.Q = ptr(Q)
     a.WS = ptr(WS)
-    a.OUT16 = None if OUT16 is None else OUT16.data_ptr() + 2 * out_offset
+    # OUT16 holds the layer outputs like OUT: 2 bytes per element, 4 for a pair (hi and lo)
+    a.OUT16 = None if OUT16 is None else OUT16.data_ptr() + (4 if split else 2) * out_offset
     a.wo_frag = wo_frag
     _check(lib().cmt_chain(ctypes.byref(a), _stream()), "cmt_chain")
 

@@ -359,12 +359,14 @@ def test_chain_path_matches_separate_launches(dev, prec):
         assert (a - b).abs().max().item() <= 2e-2 * scale, (k, (a - b).abs().max().item(), scale)
 
 
-@pytest.mark.parametrize("opt", ["conv_halo", "bev_pos_cache"])
+@pytest.mark.parametrize("opt", ["conv_halo", "bev_pos_cache", "chain"])
 def test_ref_path_selections_agree(dev, opt):
     """OPTIONS.conv_halo (CMT_CONV_HALO: shared_conv straight from the NCHW map
-    vs NCHW -> pair rows + the per-tap gathered GEMM) and OPTIONS.bev_pos_cache
+    vs NCHW -> pair rows + the per-tap gathered GEMM), OPTIONS.bev_pos_cache
     (CMT_BEV_POS_CACHE: kept BEV position rows added in the conv epilogue vs the
-    position MLP per call) at the reference-numerics policy: both forms are
+    position MLP per call) and OPTIONS.chain (CMT_CHAIN: the split row-block
+    chains of rowchain_x3.hip vs split-K GEMMs + LayerNorm launches) at the
+    reference-numerics policy: both forms are
     fp32-accurate, summed in
     other orders; a ~2^-21 difference still flips the f16 rounding of a few K / V
     elements of the fp16 flash core (2^-11 each), so the logits agree to ~1e-4,
