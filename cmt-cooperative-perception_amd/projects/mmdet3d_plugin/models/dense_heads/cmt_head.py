@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from ... import native
 from ...registry import HEADS, build_bbox_coder, build_from_cfg, build_transformer
-from ...runtime import get_precision, is_split, op_empty
+from ...runtime import check_f16_range, get_precision, is_split, op_empty
 from ..utils.packing import PackCache, to_dtype
 from .engine import HeadEngineMixin, _inv_lidar2img
 from .train_engine import HeadTrainMixin
@@ -338,6 +338,7 @@ class CmtHead(HeadTrainMixin, HeadEngineMixin, nn.Module):
             mine = [i for i in mine if i % world == rank]
         self._meta_plan = [fns[i] for i in mine if agents[i][1] is not None and self.variant != "lidar"]
         prec = get_precision()
+        check_f16_range(prec, [t for i in mine for t in agents[i][:2]])
         L = self.transformer.decoder.num_layers
         outs = torch.empty((L, B * self.num_query, self.hidden_dim), dtype=torch.float32,
                            device=self.reference_points.weight.device)

@@ -22,6 +22,12 @@ Policies (``set_precision`` / env ``CMT_PRECISION``):
              split GEMMs are checked against.
   'fp16'  -- GEMMs and attention in fp16 MFMA (fp32 accumulate).
   'bf16'  -- GEMMs and attention in bf16 MFMA (fp32 accumulate).
+Input range of 'ref' and 'fp16': an operand written as f16 (or an f16 pair)
+must stay below 65504 in magnitude, where the reference's fp32 GEMMs would
+stay finite.  The head checks its external inputs (BEV / image feature maps)
+against that limit on every eager forward (``check_f16_range``; skipped while a
+graph is being captured, where a host read cannot run) and raises ValueError
+pointing at the 'exact' policy.
 The residual stream and LayerNorm statistics stay fp32 in every policy; the
 producer of each GEMM operand writes it in the policy's operand format, and
 K/V/Q for the attention kernels are written by the projection epilogue in the
@@ -34,7 +40,7 @@ from dataclasses import dataclass
 import torch
 
 __all__ = ["Precision", "get_precision", "set_precision", "PRECISIONS", "SPLIT", "op_empty", "is_split",
-           "Options", "OPTIONS", "options"]
+           "Options", "OPTIONS", "options", "check_f16_range", "F16_MAX"]
 
 # Storage dtype of a split operand: 16-bit words, a tensor of logical shape
 # [..., C] stored as [..., 2, C] (the C f16 hi values, then the C f16 lo values).
@@ -50,6 +56,25 @@ def op_empty(rows, C, dtype, device, lead=()):
     [*lead, rows, 2, C] 16-bit words)."""
     shape = tuple(lead) + ((rows, 2, C) if dtype == SPLIT else (rows, C))
     return torch.empty(shape, dtype=dtype, device=device)
+
+
+F16_MAX = 65504.0
+
+
+def check_f16_range(prec, tensors):
+    """Raise ValueError if an external input of an f16-operand policy ('ref',
+    'fp16') holds a value the f16 (pair) format cannot carry (|x| > 65504, inf
+    or NaN).  One fused max-abs per tensor and ONE host read; a no-op under
+    graph capture and for the f32/bf16 policies."""
+    ts = [t for t in tensors if t is not None and t.numel()]
+    if prec.gemm not in (SPLIT, torch.float16) or not ts:
+        return
+    if ts[0].is_cuda and torch.cuda.is_current_stream_capturing():
+        return
+    m = torch.stack([t.detach().abs().amax().float() for t in ts]).max().item()
+    if not m <= F16_MAX:   # also catches NaN
+        raise ValueError(f"input feature map max |x| = {m} exceeds the f16 operand range ({F16_MAX}) of the "
+                         f"'{prec.name}' policy; use set_precision('exact') for such inputs")
 
 
 @dataclass(frozen=True)

@@ -32,6 +32,20 @@ from projects.mmdet3d_plugin import synthetic as S  # noqa: E402
 
 KEYS = ("center", "height", "dim", "rot", "vel", "cls_logits")
 
+
+def host_fingerprint():
+    """What decides the host's fp32 matmul rounding: CPU model, torch build,
+    intra-op threads.  The fixtures are bit-exact on the host that made them
+    (test_golden.py checks them with zero tolerance there)."""
+    import platform
+    model = platform.processor()
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
+    return {"cpu": model, "torch": torch.__version__.split("+")[0], "threads": torch.get_num_threads()}
+
 CASES = {
     "lidar_q32_l1": dict(name="cmt_lidar_nus", variant="lidar", num_query=32, num_layers=1, grid=[128, 128, 40],
                          B=1, cams=0),
@@ -103,7 +117,7 @@ def make_voxel_fixture(path):
 
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    index = {"cases": {}, "kat_pos2embed": {}}
+    index = {"cases": {}, "kat_pos2embed": {}, "host": host_fingerprint()}
     for cname, c in CASES.items():
         arrs = {}
         for core in ("fp16", "fp32"):
