@@ -243,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void kvproj_kernel(cmt_gemm_args a, int par
 // ---------------------------------------------------------------------------
 constexpr int KV3_RING = 4;
 
-template <typename TC>
+template <typename TC, int SCHED>
 __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int parts) {
     // A tile hi plane | lo plane, each [128 tokens][256] f16 with 16-byte chunks XOR-swizzled by row & 15
     __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2];
@@ -309,6 +309,12 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
         }
     };
     read_a(0, fa[0]);
+    if constexpr (SCHED & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // SCHED bit 2: the younger half of the workgroup (waves 4-7) at priority 1 for the whole
+    // loop (cdna_hip_programming.md T5, static form); bits 4 / 8: diagnostics only (no W loads /
+    // no A fragment reads: wrong results, for timing what those streams cost)
+    if constexpr (SCHED & 2)
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int j = 0; j < planes_w; ++j) {
         const int plane = plane0 + j;
         f32x16 acc[4];
@@ -327,19 +333,49 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
         for (int ks = 0; ks < KP_KS; ++ks) {
             const int slot = ks % KV3_RING;
-            read_a((ks + 1) % KP_KS, fa[(ks + 1) & 1]);
-            const pair8_t (&f)[4][2] = fa[ks & 1];
+            if constexpr (!(SCHED & 8)) read_a((ks + 1) % KP_KS, fa[(ks + 1) & 1]);
+            const pair8_t (&f)[4][2] = fa[(SCHED & 8) ? 0 : (ks & 1)];
+            if constexpr (SCHED & 1) {
+                // pass-major: each accumulator's three passes three MFMAs apart (no back-to-back
+                // dependent MFMA of one wave)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][0], acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][1], acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], f[t][0], acc[t], 0, 0, 0);
+                for (int t = 0; t < 4; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][1], acc[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], f[t][0], acc[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][0], acc[t], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][0], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][1], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], f[t][0], acc[t], 0, 0, 0);
+                }
             }
             const int kn = ks + KV3_RING;
             const int64_t woff = kn < KP_KS ? (int64_t)j * (KP_KS * 512) + kn * 512
                                             : (int64_t)jn * (KP_KS * 512) + (kn - KP_KS) * 512;
-            rh[slot] = *(const pair8_t*)(Wh + woff);
-            rl[slot] = *(const pair8_t*)(Wl + woff);
+            if constexpr (!(SCHED & 4)) {
+                rh[slot] = *(const pair8_t*)(Wh + woff);
+                rl[slot] = *(const pair8_t*)(Wl + woff);
+            } else {
+                asm volatile("" : "+v"(rh[slot]), "+v"(rl[slot]));
+            }
+            if constexpr ((SCHED & 13) == 1) {
+                // the next k-step's 8 fragment reads one per MFMA gap from the top of the step (left
+                // to itself the compiler issues them after 8 of the 12 MFMAs, and the next step's
+                // first MFMA then waits on them), then the rest of the MFMAs, then the W loads
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+            }
             // each k-step's LDS fragment reads stay beside its MFMAs
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -402,8 +438,23 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                     "cmt_kv_proj: 16-byte aligned operands");
         const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts);
         hipStream_t s3 = (hipStream_t)stream;
-        if (a.c_dtype == CMT_F16) kvproj_x3_kernel<f16_t><<<g3, 512, 0, s3>>>(a, parts);
-        else kvproj_x3_kernel<bf16_t><<<g3, 512, 0, s3>>>(a, parts);
+        static const int sched = [] {
+            const char* e = getenv("CMT_KV_SCHED");
+            return e ? atoi(e) : 1;
+        }();
+        if (a.c_dtype == CMT_F16) {
+            switch (sched) {   // CMT_KV_SCHED (kvproj_x3_kernel's SCHED bits); 4 / 8: diagnostics
+                case 0: kvproj_x3_kernel<f16_t, 0><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 2: kvproj_x3_kernel<f16_t, 2><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 3: kvproj_x3_kernel<f16_t, 3><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 5: kvproj_x3_kernel<f16_t, 5><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 9: kvproj_x3_kernel<f16_t, 9><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 13: kvproj_x3_kernel<f16_t, 13><<<g3, 512, 0, s3>>>(a, parts); break;
+                default: kvproj_x3_kernel<f16_t, 1><<<g3, 512, 0, s3>>>(a, parts); break;
+            }
+        } else {
+            kvproj_x3_kernel<bf16_t, 1><<<g3, 512, 0, s3>>>(a, parts);
+        }
         return cmt_check_launch("cmt_kv_proj");
     }
     CMT_REQUIRE(a.w_dtype == CMT_BF16 || a.w_dtype == CMT_F16, "cmt_kv_proj: w_dtype must be f16 or bf16");

@@ -558,7 +558,7 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     (pack_chain_pair / pack_chain_fc2_pair; chain B1's W1 is fc1's), chain A's
     Q f16 head-split, chain B2's Q head-split pairs."""
     _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16)
-    split = any(t is not None and t.dtype == torch.uint16 for t in (X, Wo, W1, W2, Wn))
+    split = any(t is not None and t.dtype == torch.uint16 for t in (X, Wo, W1, W2, Wn, Q, OUT16))
     pw = 2 if split else 1   # a pair pack holds the hi pack, then the lo pack
     if Wn is not None and (Wn.dim() != 1 or Wn.numel() != pw * 768 * 256):
         raise RuntimeError("cmt_chain: Wn must be fragment-major (pack_chain_wn / pack_chain_pair)")
