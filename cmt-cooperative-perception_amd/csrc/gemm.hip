@@ -1182,6 +1182,10 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// VAR bits: 1 = the younger half of the workgroup (waves 4-7) at priority 1 for the whole loop
+// (cdna_hip_programming.md T5, static form); 2 = s_setprio(1) around every tap's MFMA cluster;
+// 4 / 8 = diagnostics only (no halo loads / no W refills: wrong results, for timing those streams)
+template <int VAR>
 __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
     typedef HaloConv T;
     typedef pair8_t frag;
@@ -1225,8 +1229,13 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
             // read the zero page
             const float* src = u_ok[i] ? Xc + u_src[i] : (const float*)g_zero_page;
             const int es = u_ok[i] ? HW : 0;
+            if constexpr (VAR & 4) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) hv[i][e] = src[e * es];
+                for (int e = 0; e < 8; ++e) hv[i][e] = (float)(es + e) * 1e-3f;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) hv[i][e] = src[e * es];
+            }
         }
     };
     auto store_halo = [&](int buf) {
@@ -1258,6 +1267,9 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
     auto issue_w = [&](int g) {   // step g = (chunk g / 3, kernel row g % 3): its three taps
         const int c = g / 3, dy = g - 3 * (g / 3);
         char* slot = smem + 2 * T::HALO + (g % S) * T::WSLOT + wave * 1024;
+        if constexpr (VAR & 8) {
+            if (g >= S) return;
+        }
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) glds16(wsrc + (3 * dy + dx) * Cin + c * T::CK, slot + dx * T::WTAP);
     };
@@ -1299,6 +1311,8 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
     // the issue stream is the same for every chunk and each wait below counts the ops issued
     // after W(g) exactly.
     constexpr int WOPS = 3;                                   // DMAs per thread per W stage
+    if constexpr (VAR & 1)
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int c = 0; c < nchunks; ++c) {
         const char* Hs = smem + (c & 1) * T::HALO;
 #pragma unroll
@@ -1334,6 +1348,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
                     bh[tn] = *(const frag*)(Ws + dx * T::WTAP + woff[tn]);
                     bl[tn] = *(const frag*)(Ws + dx * T::WTAP + (woff[tn] ^ (2 << 4)));
                 }
+                if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -1349,6 +1364,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
                     for (int tn = 0; tn < TN; ++tn)
                         acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], af[tm], acc[tm][tn]);
+                if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(0);
             }
         }
         // chunk c + 1's halo into the other buffer (its last readers, chunk c - 1's taps, are
@@ -1364,7 +1380,18 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.conv_h * a.conv_w, HaloConv::BM), tn = a.N / HaloConv::BN;
     const unsigned nwg = (unsigned)((int64_t)tm * tn * a.batch);
-    conv_halo_x3_kernel<<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
+    static const int var = [] {
+        const char* e = getenv("CMT_CONV_VAR");
+        return e ? atoi(e) : 0;
+    }();
+    switch (var) {   // CMT_CONV_VAR (conv_halo_x3_kernel's VAR bits); 4 / 8: diagnostics
+        case 1: conv_halo_x3_kernel<1><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+        case 2: conv_halo_x3_kernel<2><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+        case 4: conv_halo_x3_kernel<4><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+        case 8: conv_halo_x3_kernel<8><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+        case 12: conv_halo_x3_kernel<12><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+        default: conv_halo_x3_kernel<0><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+    }
     return cmt_check_launch("cmt_gemm");
 }
 

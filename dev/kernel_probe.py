@@ -3,7 +3,8 @@ shape a few times (for rocprofv3 counter passes, dev/kernel_pmc.sh):
 
     python dev/kernel_probe.py kv|conv [--iters N]
 kv:   cmt_kv_proj split form, M = 56 400 tokens, N = 3072 (all layers' K|V), K = 256
-conv: shared_conv as the split implicit 3x3 GEMM, 180 x 180 x 512 -> 256"""
+conv: shared_conv as the split implicit 3x3 GEMM, 180 x 180 x 512 -> 256
+convh: shared_conv straight from the NCHW fp32 map (conv_halo_x3_kernel, the 'ref' path)"""
 import argparse
 import os
 import sys
@@ -22,7 +23,7 @@ def pairs(*shape):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["kv", "conv"])
+    ap.add_argument("what", choices=["kv", "conv", "convh"])
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--time", action="store_true", help="also print the mean of 20 back-to-back launches")
     a = ap.parse_args()
@@ -36,6 +37,14 @@ def main():
         bias = torch.randn(Nn, device="cuda")
         run = lambda: N.kv_proj(A, W, C, M=M, N=Nn, bias=bias, A2=A2, headsplit_rows=M, plane_max2=pm,  # noqa: E731
                                 plane_max_cols=Nn // 2)
+    elif a.what == "convh":
+        X = torch.randn(1, 512, 180, 180, device="cuda")
+        W = pairs(256, 2, 4608)
+        C = torch.empty(32400, 2, 256, dtype=torch.uint16, device="cuda")
+        bias = torch.randn(256, device="cuda")
+        run = lambda: N.gemm(X, W, C, M=32400, N=256, K=4608, lda=32400, ldw=4608, ldc=256, bias=bias,  # noqa: E731
+                             relu=True, a_mode=N.A_CONV3X3_NCHW, conv=(180, 180, 512), batch=1,
+                             a_bstride=512 * 32400, c_bstride=32400 * 256)
     else:
         A = pairs(32400, 2, 512)
         W = pairs(256, 2, 4608)

@@ -21,6 +21,11 @@ for v in ${KV_VARIANTS:-0 1 2 3 5 9 13 0 1 3}; do
     CMT_KV_SCHED=$v timeout -k 10 120 python -u dev/kernel_probe.py kv --time >> "$OUT/kv.txt" 2>&1 || { echo "kv probe failed"; tail -5 "$OUT/kv.txt"; exit 1; }
 done
 grep "kv sched" -A1 "$OUT/kv.txt"
+for v in ${CONV_VARIANTS:-0 1 2 4 8 12 0 1 2}; do
+    echo -n "conv var $v: " >> "$OUT/conv.txt"
+    CMT_CONV_VAR=$v timeout -k 10 120 python -u dev/kernel_probe.py convh --time >> "$OUT/conv.txt" 2>&1 || { echo "conv probe failed"; tail -5 "$OUT/conv.txt"; exit 1; }
+done
+grep "conv var" -A1 "$OUT/conv.txt"
 for c in 1 0; do
     CMT_CHAIN=$c timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-ref --no-traffic \
         --no-recompute > "$OUT/bench_chain$c.json" 2> "$OUT/bench_chain$c.log" || { echo "bench failed"; tail -20 "$OUT/bench_chain$c.log"; exit 1; }
