@@ -1972,13 +1972,16 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
 // self-attention) the in-workgroup key split attn_kw_kernel; anything else the
 // 4-wave single-phase attn_fwd_kernel with split partials.  f32 always takes
 // the exact-f32 kernel.
-// f16 bounded long-key path: CMT_ATTN_SP = 0 -> attn_pb2_kernel; otherwise attn_sp_kernel with
-// the variant bits 2 (one barrier per two tiles) and 4 (s_setprio 1 for waves 4-7); default 1
-int sp_mode() {
+// f16 bounded long-key path: CMT_ATTN_SP = 0 (default) -> attn_pb2_kernel; otherwise
+// attn_sp_kernel with the variant bits 2 (one barrier per two tiles) and 4 (s_setprio 1 for
+// waves 4-7).  The per-call flags CMT_ATTN_FORCE_PINGPONG / _PIPELINED override it.
+int sp_mode(int flags) {
     static const int m = [] {
         const char* e = std::getenv("CMT_ATTN_SP");
-        return e && e[0] >= '0' && e[0] <= '9' ? std::atoi(e) : 1;
+        return e && e[0] >= '0' && e[0] <= '9' ? std::atoi(e) : 0;
     }();
+    if (flags & CMT_ATTN_FORCE_PINGPONG) return 0;
+    if (flags & CMT_ATTN_FORCE_PIPELINED) return m != 0 ? m : 1;
     return m;
 }
 
@@ -2086,8 +2089,8 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     } else if (use_long(a)) {
         // the scale is folded into Q either way; without the FOLD permission q * c is kept as hi + lo
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
-        const int spm = sp_mode();
-        if (a.dtype == CMT_F16 && a.kmax2 != nullptr && spm != 0 && !(a.flags & CMT_ATTN_FORCE_PINGPONG)) {
+        const int spm = sp_mode(a.flags);
+        if (a.dtype == CMT_F16 && a.kmax2 != nullptr && spm != 0) {
             // f16 with bounded offsets: the software-pipelined single-stream kernel
 #define SPK(QS, B2, PR) attn_sp_kernel<QS, B2, PR><<<nwg, 512, 0, s>>>(p)
             const bool b2 = (spm & 2) != 0, pr = (spm & 4) != 0;

@@ -311,8 +311,9 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     read_a(0, fa[0]);
     if constexpr (SCHED & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // SCHED bit 2: the younger half of the workgroup (waves 4-7) at priority 1 for the whole
-    // loop (cdna_hip_programming.md T5, static form); bits 4 / 8: diagnostics only (no W loads /
-    // no A fragment reads: wrong results, for timing what those streams cost)
+    // loop (cdna_hip_programming.md T5, static form); bits 4 / 8 / 16 / 32: diagnostics only (no W
+    // loads / no A fragment reads / no K-V stores / no bias loads: wrong results, for timing what
+    // each costs)
     if constexpr (SCHED & 2)
         if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int j = 0; j < planes_w; ++j) {
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int c = (r & 3) + 8 * (r >> 2);
-                const float b = a.bias ? (lh ? bp[c + 4] : bp[c]) : 0.f;
+                const float b = (SCHED & 32) ? 0.f : a.bias ? (lh ? bp[c + 4] : bp[c]) : 0.f;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) acc[t][r] = b;
             }
@@ -389,7 +390,8 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
             for (int g = 0; g < 4; ++g) {
                 const t4 v = t4{(TC)acc[t][4 * g], (TC)acc[t][4 * g + 1], (TC)acc[t][4 * g + 2],
                                 (TC)acc[t][4 * g + 3]};
-                if (m < a.M) *(t4*)(C + rbase[t] + 8 * g + 4 * lh) = v;
+                if constexpr (SCHED & 16) asm volatile("" ::"v"(v));
+                else if (m < a.M) *(t4*)(C + rbase[t] + 8 * g + 4 * lh) = v;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
             }
@@ -440,20 +442,24 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
         hipStream_t s3 = (hipStream_t)stream;
         static const int sched = [] {
             const char* e = getenv("CMT_KV_SCHED");
-            return e ? atoi(e) : 1;
+            return e ? atoi(e) : 0;
         }();
         if (a.c_dtype == CMT_F16) {
             switch (sched) {   // CMT_KV_SCHED (kvproj_x3_kernel's SCHED bits); 4 / 8: diagnostics
-                case 0: kvproj_x3_kernel<f16_t, 0><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 1: kvproj_x3_kernel<f16_t, 1><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 16: kvproj_x3_kernel<f16_t, 16><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 32: kvproj_x3_kernel<f16_t, 32><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 48: kvproj_x3_kernel<f16_t, 48><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 60: kvproj_x3_kernel<f16_t, 60><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 2: kvproj_x3_kernel<f16_t, 2><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 3: kvproj_x3_kernel<f16_t, 3><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 5: kvproj_x3_kernel<f16_t, 5><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 9: kvproj_x3_kernel<f16_t, 9><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 13: kvproj_x3_kernel<f16_t, 13><<<g3, 512, 0, s3>>>(a, parts); break;
-                default: kvproj_x3_kernel<f16_t, 1><<<g3, 512, 0, s3>>>(a, parts); break;
+                default: kvproj_x3_kernel<f16_t, 0><<<g3, 512, 0, s3>>>(a, parts); break;
             }
         } else {
-            kvproj_x3_kernel<bf16_t, 1><<<g3, 512, 0, s3>>>(a, parts);
+            kvproj_x3_kernel<bf16_t, 0><<<g3, 512, 0, s3>>>(a, parts);
         }
         return cmt_check_launch("cmt_kv_proj");
     }

@@ -18,7 +18,7 @@ done
 grep attn "$OUT/attn.txt"
 for v in ${KV_VARIANTS:-0 1 2 3 5 9 13 0 1 3}; do
     echo -n "kv sched $v: " >> "$OUT/kv.txt"
-    CMT_KV_SCHED=$v timeout -k 10 120 python -u dev/kernel_probe.py kv --time >> "$OUT/kv.txt" 2>&1 || { echo "kv probe failed"; tail -5 "$OUT/kv.txt"; exit 1; }
+    CMT_KV_SCHED=$v timeout -k 10 120 python -u dev/kernel_probe.py kv --time 2>/dev/null >> "$OUT/kv.txt" || { echo "kv probe failed"; tail -5 "$OUT/kv.txt"; exit 1; }
 done
 grep "kv sched" -A1 "$OUT/kv.txt"
 for v in ${CONV_VARIANTS:-0 1 2 4 8 12 0 1 2}; do

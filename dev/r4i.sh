@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-4 step i: kvproj epilogue diagnostics, the pipelined/ping-pong attention test, and a
+# kernel trace of the bench (frame timeline with the split chains).
+set -uo pipefail
+TAG=${1:-r4i}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 200 python -u -m pytest tests/test_gpu_split.py -v -k "pipelined or f16_long or kvproj" \
+    --timeout 150 --timeout-method thread > "$OUT/tests.log" 2>&1
+rc=$?
+[[ $rc -eq 0 || $rc -eq 1 ]] || { echo "tests rc=$rc"; tail -30 "$OUT/tests.log"; exit 1; }
+grep -E "passed|failed" "$OUT/tests.log" | tail -2
+for v in ${KV_VARIANTS:-0 16 32 48 60 13 0 16 32}; do
+    echo -n "kv sched $v: " >> "$OUT/kv.txt"
+    CMT_KV_SCHED=$v timeout -k 10 120 python -u dev/kernel_probe.py kv --time 2>/dev/null >> "$OUT/kv.txt" \
+        || { echo "kv probe failed"; tail -5 "$OUT/kv.txt"; exit 1; }
+done
+grep "kv sched" "$OUT/kv.txt"
+mkdir -p "$OUT/trace"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ref --no-recompute --no-traffic \
+    > "$OUT/trace/bench.json" 2> "$OUT/trace/trace.log" || { echo "trace failed"; tail -20 "$OUT/trace/trace.log"; exit 1; }
+cat "$OUT/trace/bench.json"

@@ -187,10 +187,14 @@ int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
  *                               it loads Q (one extra rounding of Q in the
  *                               compute dtype; used by the f16/bf16 policies,
  *                               not by the reference-numerics policy)
- *        CMT_ATTN_FORCE_PINGPONG  diagnostic: the f16 bounded long-key path
- *                               runs the ping-pong kernel instead of the
- *                               software-pipelined one (A/B and tests) */
-enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2, CMT_ATTN_FORCE_PINGPONG = 256 };
+ *        CMT_ATTN_FORCE_PINGPONG   the f16 bounded long-key path runs the
+ *                               ping-pong kernel (the default)
+ *        CMT_ATTN_FORCE_PIPELINED  the f16 bounded long-key path runs the
+ *                               software-pipelined kernel (measured slower:
+ *                               101.4 vs 98.8 us at the fusion shape, r4h;
+ *                               kept selectable for A/B and tests) */
+enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2, CMT_ATTN_FORCE_PINGPONG = 256,
+       CMT_ATTN_FORCE_PIPELINED = 512 };
 
 typedef struct cmt_attn_args {
     int B, H, Nq, Nk;

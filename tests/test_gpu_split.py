@@ -501,8 +501,9 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
 @pytest.mark.parametrize("B,Nq,Nk,splits", [(1, 900, 56400, 0), (2, 300, 4097, 3), (1, 257, 8192, 1),
                                            (1, 900, 4160, 5), (1, 100, 64 * 9, 1)])
 def test_attention_f16_pipelined_matches_pingpong(N, dev, B, Nq, Nk, splits):
-    """The software-pipelined f16 long-key kernel (attn_sp_kernel, the default)
-    against the ping-pong kernel (CMT_ATTN_FORCE_PINGPONG) on the same bounded
+    """The software-pipelined f16 long-key kernel (attn_sp_kernel,
+    CMT_ATTN_FORCE_PIPELINED) against the ping-pong kernel (attn_pb2_kernel, the
+    default; CMT_ATTN_FORCE_PINGPONG) on the same bounded
     inputs.  With the fold (Q*c rounded once) both run the same products in the
     same order: bit-equal.  With Q*c kept as hi + lo the two compile the offset's
     |q|^2 with different fp32 contractions, so a few P round to the other f16
@@ -517,7 +518,7 @@ def test_attention_f16_pipelined_matches_pingpong(N, dev, B, Nq, Nk, splits):
     km = _kmax2(k, B, Nk, H).to(dev)
     qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
     outs = []
-    for diag in (0, 256):
+    for diag in (512, 256):
         for fold in (False, True):
             O = torch.full((B, Nq, H * 32), float("nan"), device=dev)
             N.attention(qd, kd, vd, O, B=B, H=H, Nq=Nq, Nk=Nk,
