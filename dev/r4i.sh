@@ -17,6 +17,17 @@ for v in ${KV_VARIANTS:-0 16 32 48 60 13 0 16 32}; do
         || { echo "kv probe failed"; tail -5 "$OUT/kv.txt"; exit 1; }
 done
 grep "kv sched" "$OUT/kv.txt"
+CMT_CONV_VAR=16 timeout -k 10 200 python -u -m pytest tests/test_gpu_split.py -v -k "conv3x3_nchw" \
+    --timeout 150 --timeout-method thread > "$OUT/tests_v4.log" 2>&1
+rc=$?
+[[ $rc -eq 0 || $rc -eq 1 ]] || { echo "v4 tests rc=$rc"; tail -30 "$OUT/tests_v4.log"; exit 1; }
+grep -E "passed|failed" "$OUT/tests_v4.log" | tail -2
+for v in 16 0 16 0 20; do
+    echo -n "conv var $v: " >> "$OUT/conv.txt"
+    CMT_CONV_VAR=$v timeout -k 10 120 python -u dev/kernel_probe.py convh --time 2>/dev/null >> "$OUT/conv.txt" \
+        || { echo "conv probe failed"; tail -5 "$OUT/conv.txt"; exit 1; }
+done
+grep "conv var" "$OUT/conv.txt"
 mkdir -p "$OUT/trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ref --no-recompute --no-traffic \
