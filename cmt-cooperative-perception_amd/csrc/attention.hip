@@ -1055,8 +1055,13 @@ __device__ __forceinline__ void pb2_wait(int tiles) {
     else pp_wait_n<0>();
 }
 
-template <typename T, bool QS>
+// US (f16, bounded offsets or not): Q enters the QK^T MFMAs unscaled, exactly the f16 q the
+// reference's flash core multiplies, and the vector segment applies s * c - offset in fp32 (one
+// packed FMA per two scores) -- flash-attn's own order (q k in fp32, then the scale), with half
+// the QK^T MFMAs of QS.
+template <typename T, bool QS, bool US = false>
 __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
+    static_assert(!(QS && US), "QS and US are alternatives");
     typedef typename mfma_traits<T>::frag frag;
     constexpr bool F16 = std::is_same<T, f16_t>::value;
     constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
@@ -1139,11 +1144,11 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const float x0 = (float)r0[j] * c, x1 = (float)r1[j] * c;
-            qf[0][j] = (T)x0;
-            qf[1][j] = (T)x1;
+            qf[0][j] = US ? r0[j] : (T)x0;
+            qf[1][j] = US ? r1[j] : (T)x1;
             ql[0][j] = (T)(x0 - (float)qf[0][j]);
             ql[1][j] = (T)(x1 - (float)qf[1][j]);
-            const float e0 = QS ? x0 : (float)qf[0][j], e1 = QS ? x1 : (float)qf[1][j];
+            const float e0 = QS || US ? x0 : (float)qf[0][j], e1 = QS || US ? x1 : (float)qf[1][j];
             qq += e0 * e0 + e1 * e1;
         }
     }
@@ -1163,11 +1168,26 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
     }
     f32x16 sinit;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sinit[r] = F16 && fast ? -off : 0.f;
+    for (int r = 0; r < 16; ++r) sinit[r] = F16 && fast && !US ? -off : 0.f;
 
     f32x16 o;
     f32x4 lsum;
     float m_run = 0.f;   // slow path: set by the first tiles
+    // US: the raw scores q k -> exp2 units s * c - offset (fast) or s * c (online max)
+    auto us_scale = [&](f32x16 (&sx)[2], bool fastw) {
+        if constexpr (US) {
+            const f32x2 c2 = {c, c};
+            const f32x2 sub2 = fastw ? f32x2{-off, -off} : f32x2{0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    const f32x2 v = __builtin_elementwise_fma(f32x2{sx[kb][r], sx[kb][r + 1]}, c2, sub2);
+                    sx[kb][r] = v[0];
+                    sx[kb][r + 1] = v[1];
+                }
+        }
+    };
 
     // One pass over the split's keys.  fastw: bounded offsets (else online max); livew: this wave
     // computes (else it only keeps the barriers and, in half A, the LDS-DMA) and restarts O / l.
@@ -1193,6 +1213,8 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             if (livew) pb_mseg<T, true, false, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
             if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
             pp_barrier();
+            if (livew) us_scale(s0, fastw);
+            if (livew) us_scale(s1, fastw);
             if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, true);
             {
                 const PpLane l = pp_launder(lane_ofs);
@@ -1208,6 +1230,8 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
                 if (livew) pb_mseg<T, true, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);   // QK^T 2j+1, PV 2j-1
                 if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
                 pp_barrier();
+                if (livew) us_scale(s0, fastw);
+                if (livew) us_scale(s1, fastw);
                 if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, false);
                 const PpLane l = pp_launder(lane_ofs);
                 if (livew) pp_load_k<T>(slot_b(2 * j + 2), l, kf0);   // stale (unused) on the last pair
@@ -1232,6 +1256,7 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             if (livew) pp_load_k<T>(slot_b(nt - 1), l, kf0);
             if (livew) pp_load_v<T>(slot_b(nt - 1) + KV_B, l, vf0);
             if (livew) pb_mseg<T, true, false, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
+            if (livew) us_scale(s0, fastw);
             if (livew) pb_vseg<T>(s0, pf0, o, lsum, m_run, fastw, np == 0);
             if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
         }
@@ -1258,6 +1283,7 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
                     if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s0[kb][r] = -__builtin_inff();
+            if (livew) us_scale(s0, fastw);
             if (livew) pb_vseg<T>(s0, pf0, o, lsum, m_run, fastw, nt == 0);
             if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
         }
@@ -1985,6 +2011,16 @@ int sp_mode(int flags) {
     return m;
 }
 
+// the reference-numerics f16 core (no fold permission): CMT_ATTN_US = 1 (default 0) or the
+// per-call CMT_ATTN_UNSCALED_Q flag -> unscaled Q (attn_pb2_kernel US); else Q * c as hi + lo (QS)
+bool us_mode(int flags) {
+    static const int m = [] {
+        const char* e = std::getenv("CMT_ATTN_US");
+        return e && e[0] >= '0' && e[0] <= '9' ? std::atoi(e) : 0;
+    }();
+    return (flags & CMT_ATTN_UNSCALED_Q) != 0 || m != 0;
+}
+
 bool use_long(const cmt_attn_args& a) {
     return a.dtype != CMT_F32 && a.dtype != CMT_F16P && a.Nk >= 4096 && a.Nq > 128;
 }
@@ -2105,6 +2141,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
 #undef SPK
         } else if (a.dtype == CMT_F16) {
             if (fold) attn_pb2_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
+            else if (us_mode(a.flags)) attn_pb2_kernel<f16_t, false, true><<<nwg, 512, 0, s>>>(p);
             else attn_pb2_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);
         } else {
             if (fold) attn_pb2_kernel<bf16_t, false><<<nwg, 512, 0, s>>>(p);

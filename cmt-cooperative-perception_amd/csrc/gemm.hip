@@ -1184,20 +1184,17 @@ __device__ __forceinline__ void vm_wait() {
 
 // VAR bits: 1 = the younger half of the workgroup (waves 4-7) at priority 1 for the whole loop
 // (cdna_hip_programming.md T5, static form); 2 = s_setprio(1) around every tap's MFMA cluster;
-// 16 = 16-byte halo loads (V4, needs HW % 4 == 0 and a 16-byte aligned map): a unit is one
-// channel octet of 4 consecutive halo pixels -- 8 dwordx4 loads per thread and chunk instead of
-// 24 dword loads -- with halo row 0 moved back to the 16-byte aligned pixel at or before
-// p0 - W - 1 (the taps' row shift grows by that offset);
+// 16 = the halo loads as inline asm, waited for by a counted vmcnt of our own: hipcc's own wait
+// for a VGPR-destination load beside the W ring's LDS-DMA is vmcnt(0) (cdna_hip_programming.md
+// 'Three .s-level traps' (b)), which drained the W ring at the end of every chunk;
 // 4 / 8 = diagnostics only (no halo loads / no W refills: wrong results, for timing those streams)
 template <int VAR>
 __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
     typedef HaloConv T;
     typedef pair8_t frag;
-    constexpr bool V4 = (VAR & 16) != 0;
-    constexpr int BM = T::BM, S = T::S, TM = T::TM, TN = T::TN, UPT = V4 ? 1 : T::UPT;
-    constexpr int HLOADS = 8 * UPT;                           // halo loads per thread per chunk
-    static_assert(!V4 || ((T::NHMAX + 6) / 4 * 4 * T::ROWB <= T::HALO && (T::NHMAX + 6) / 4 * 2 <= T::NTX),
-                  "V4 halo groups");
+    constexpr bool AH = (VAR & 16) != 0;
+    constexpr int BM = T::BM, S = T::S, TM = T::TM, TN = T::TN, UPT = T::UPT;
+    constexpr int HLOADS = UPT * 8;                           // halo loads per thread per chunk
     __shared__ __attribute__((aligned(16))) char smem[T::SMEM];
     int z, mt, nt;
     xcd_tile(tiles_m, tiles_n, a.batch, z, mt, nt);
@@ -1207,30 +1204,26 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
     const int lr = lane & 31, lh = lane >> 5;
     const int Wd = a.conv_w, HW = a.conv_h * a.conv_w, Cin = a.conv_c;
     const int NH = BM + 2 * Wd + 2;                           // halo pixels of this launch
-    const int hoff = V4 ? (m0 - Wd - 1) & 3 : 0;              // V4: p0 - W - 1 minus its 16-byte aligned floor
-    const int hs = m0 - Wd - 1 - hoff;                        // image pixel of halo row 0
+    const int hs = m0 - Wd - 1;                               // image pixel of halo row 0
     const float* X = (const float*)a.A + (int64_t)z * a.a_bstride;
     const pair_t* Wb = (const pair_t*)a.W;
 
     // halo units of this thread: (halo row h, channel octet o); lanes walk consecutive rows
-    // (V4: (4-row group q, octet o), halo rows 4q .. 4q + 3)
-    const int NU = V4 ? (NH + hoff + 3) >> 2 : NH;           // units per octet
     int u_src[UPT], u_lds[UPT];
     bool u_ok[UPT], u_on[UPT];
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
         const int u = tid + i * T::NTX;
-        const int o = u >= NU ? 1 : 0;
-        const int h = (u - o * NU) * (V4 ? 4 : 1);
+        const int o = u >= NH ? 1 : 0;
+        const int h = u - o * NH;
         const int p = hs + h;
-        u_on[i] = u < 2 * NU;                                 // a unit of this tile at all
-        u_ok[i] = u_on[i] && p >= 0 && p < HW;                // inside the image (else zeros; V4: HW % 4 == 0)
+        u_on[i] = u < 2 * NH;                                 // a unit of this tile at all
+        u_ok[i] = u_on[i] && p >= 0 && p < HW;                // inside the image (else zeros)
         u_src[i] = 8 * o * HW + p;
         const int sw = (h >> 2) & 3;
         u_lds[i] = h * T::ROWB + ((o ^ sw) << 4);             // hi chunk; the lo chunk is (2 + o) ^ sw
     }
     float hv[UPT][8];
-    f32x4 hv4[8];
     auto load_halo = [&](int c) {
         const float* Xc = X + (int64_t)c * T::CK * HW;
 #pragma unroll
@@ -1243,49 +1236,53 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
             if constexpr (VAR & 4) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) hv[i][e] = (float)(es + e) * 1e-3f;
-            } else if constexpr (V4) {
+            } else if constexpr (AH) {
+                // SGPR base (the chunk's channel block) + a 32-bit VGPR byte offset per load;
+                // padding units load pixel 0 of the channel and are zeroed after the wait
+                uint32_t vo = (uint32_t)(u_ok[i] ? u_src[i] : 0) * 4u;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) hv4[e] = *(const f32x4*)(src + e * es);
+                for (int e = 0; e < 8; ++e) {
+                    asm volatile("global_load_dword %0, %1, %2" : "=v"(hv[i][e]) : "v"(vo), "s"(Xc) : "memory");
+                    vo += (uint32_t)HW * 4u;
+                }
             } else {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) hv[i][e] = src[e * es];
             }
         }
     };
-    auto store_halo = [&](int buf) {
+    auto store_halo = [&](int buf, auto first) {
         char* hb = smem + buf * T::HALO;
-        // pin the halo registers here: without this the split arithmetic below (no memory
-        // dependence) is hoisted right behind the loads and waits for them there
-        if constexpr (V4 && !(VAR & 4)) {
+        if constexpr (AH && !(VAR & 4)) {
+            // the halo loads went out at the chunk's first step; two W stages (3 DMAs each) since
+            // (none before chunk 0's, in the prologue): wait for the loads, naming every
+            // destination so nothing reads them before
+            asm volatile("s_waitcnt vmcnt(%24)"
+                         : "+v"(hv[0][0]), "+v"(hv[0][1]), "+v"(hv[0][2]), "+v"(hv[0][3]), "+v"(hv[0][4]),
+                           "+v"(hv[0][5]), "+v"(hv[0][6]), "+v"(hv[0][7]), "+v"(hv[1][0]), "+v"(hv[1][1]),
+                           "+v"(hv[1][2]), "+v"(hv[1][3]), "+v"(hv[1][4]), "+v"(hv[1][5]), "+v"(hv[1][6]),
+                           "+v"(hv[1][7]), "+v"(hv[2][0]), "+v"(hv[2][1]), "+v"(hv[2][2]), "+v"(hv[2][3]),
+                           "+v"(hv[2][4]), "+v"(hv[2][5]), "+v"(hv[2][6]), "+v"(hv[2][7])
+                         : "n"(decltype(first)::value ? 0 : 6)
+                         : "memory");
+            static_assert(!AH || UPT == 3, "the wait statement names three units");
+        } else {
+            // pin the halo registers here: without this the split arithmetic below (no memory
+            // dependence) is hoisted right behind the loads and waits for them there
 #pragma unroll
-            for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(hv4[e]));
-            if (u_on[0]) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {                 // halo row 4q + j: the same swizzle for all four
-                    pair8_t hi, lo;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        hi[e] = (pair_t)hv4[e][j];
-                        lo[e] = (pair_t)(hv4[e][j] - (float)hi[e]);
-                    }
-                    *(pair8_t*)(hb + u_lds[0] + j * T::ROWB) = hi;
-                    *(pair8_t*)(hb + ((u_lds[0] + j * T::ROWB) ^ (2 << 4))) = lo;
-                }
-            }
-            return;
+            for (int i = 0; i < UPT; ++i)
+                asm volatile("" : "+v"(hv[i][0]), "+v"(hv[i][1]), "+v"(hv[i][2]), "+v"(hv[i][3]), "+v"(hv[i][4]),
+                             "+v"(hv[i][5]), "+v"(hv[i][6]), "+v"(hv[i][7]));
         }
-#pragma unroll
-        for (int i = 0; i < UPT; ++i)
-            asm volatile("" : "+v"(hv[i][0]), "+v"(hv[i][1]), "+v"(hv[i][2]), "+v"(hv[i][3]), "+v"(hv[i][4]),
-                         "+v"(hv[i][5]), "+v"(hv[i][6]), "+v"(hv[i][7]));
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
             if (!u_on[i]) continue;
             pair8_t hi, lo;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                hi[e] = (pair_t)hv[i][e];
-                lo[e] = (pair_t)(hv[i][e] - (float)hi[e]);
+                const float x = AH && !u_ok[i] ? 0.f : hv[i][e];
+                hi[e] = (pair_t)x;
+                lo[e] = (pair_t)(x - (float)hi[e]);
             }
             *(pair8_t*)(hb + u_lds[i]) = hi;
             *(pair8_t*)(hb + (u_lds[i] ^ (2 << 4))) = lo;     // (2 + o) ^ sw == (o ^ sw) ^ 2
@@ -1333,7 +1330,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 
     // prologue: chunk 0's halo, W of steps 0 .. S-1
     load_halo(0);
-    store_halo(0);
+    store_halo(0, std::true_type{});
 #pragma unroll
     for (int g = 0; g < S; ++g) issue_w(g);
 
@@ -1362,7 +1359,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
             const char* Ws = smem + 2 * T::HALO + (g % S) * T::WSLOT;
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
-                const int tsh = dy * Wd + dx + hoff;          // halo row of (pixel, tap) - tile row
+                const int tsh = dy * Wd + dx;                 // halo row of (pixel, tap) - tile row
                 frag af[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm) {
@@ -1401,7 +1398,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
         }
         // chunk c + 1's halo into the other buffer (its last readers, chunk c - 1's taps, are
         // all past this chunk's first barrier); the next step's barrier publishes it
-        store_halo((c + 1) & 1);
+        store_halo((c + 1) & 1, std::false_type{});
     }
     // the dummy W refills and the last halo loads are still in flight: drain them before
     // the epilogue reuses the LDS
@@ -1416,9 +1413,7 @@ int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
         const char* e = getenv("CMT_CONV_VAR");
         return e ? atoi(e) : 0;
     }();
-    // the 16-byte halo loads need 4-pixel groups that never straddle the image end or a channel
-    const bool v4ok = (a.conv_h * a.conv_w) % 4 == 0 && a.a_bstride % 4 == 0 && (uintptr_t)a.A % 16 == 0;
-    const int var = (env_var & 16) && !v4ok ? env_var & ~16 : env_var;
+    const int var = env_var;
     switch (var) {   // CMT_CONV_VAR (conv_halo_x3_kernel's VAR bits); 4 / 8: diagnostics
         case 1: conv_halo_x3_kernel<1><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
         case 2: conv_halo_x3_kernel<2><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
@@ -1426,7 +1421,7 @@ int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
         case 8: conv_halo_x3_kernel<8><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
         case 12: conv_halo_x3_kernel<12><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
         case 16: conv_halo_x3_kernel<16><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 20: conv_halo_x3_kernel<20><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
+        case 17: conv_halo_x3_kernel<17><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
         default: conv_halo_x3_kernel<0><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
     }
     return cmt_check_launch("cmt_gemm");

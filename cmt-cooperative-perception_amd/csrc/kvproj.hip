@@ -245,8 +245,9 @@ constexpr int KV3_RING = 4;
 
 template <typename TC, int SCHED>
 __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int parts) {
-    // A tile hi plane | lo plane, each [128 tokens][256] f16 with 16-byte chunks XOR-swizzled by row & 15
-    __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2];
+    // A tile hi plane | lo plane, each [128 tokens][256] f16 with 16-byte chunks XOR-swizzled by
+    // row & 15, then the column part's bias (fp32)
+    __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2 + KP_MAXB * 4];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int lr = lane & 31, lh = lane >> 5;
@@ -279,6 +280,9 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
         rh[ks] = *(const pair8_t*)(Wh + ks * 512);
         rl[ks] = *(const pair8_t*)(Wl + ks * 512);
     }
+    float* bsm = (float*)(lds + 2 * KP_BM * KP_K * 2);
+    if constexpr (!(SCHED & 64))
+        for (int i = tid; i < ncols; i += 512) bsm[i] = a.bias ? a.bias[n_part + i] : 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_mem();
     // head-split element offset of each tile's token row (plane 0)
@@ -319,7 +323,19 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     for (int j = 0; j < planes_w; ++j) {
         const int plane = plane0 + j;
         f32x16 acc[4];
-        {
+        if constexpr (!(SCHED & 64)) {
+            // the bias from LDS (a global load here made the compiler drain the W ring, vmcnt(0),
+            // at every plane): lane (lr, lh) holds columns 8 q + 4 lh + 0..3 of the plane
+            const float* bp = bsm + plane * 32 - n_part + 4 * lh;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 b = (SCHED & 32) ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(bp + 8 * q);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[t][4 * q + e] = b[e];
+            }
+        } else {
             const float* bp = a.bias + plane * 32;   // wave-uniform: scalar loads
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -386,14 +402,47 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
         for (int t = 0; t < 4; ++t) {
             const int m = m0 + 32 * t + lr;
             float ss = 0.f;
+            if constexpr (!(SCHED & 64)) {
+                // lane (lr, lh) holds columns 8 g + 4 lh + 0..3 (g = 0..3) of token lr: the lane
+                // pair swaps two 4-column groups (v_permlane32_swap) so that lh = 0 holds columns
+                // 0..15 and lh = 1 columns 16..31, then stores them as two 16-byte pieces (half
+                // the store instructions, twice the bytes each, of the 8-byte form below)
+                uint32_t pk[4][2];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const t4 v = t4{(TC)acc[t][4 * g], (TC)acc[t][4 * g + 1], (TC)acc[t][4 * g + 2],
-                                (TC)acc[t][4 * g + 3]};
-                if constexpr (SCHED & 16) asm volatile("" ::"v"(v));
-                else if (m < a.M) *(t4*)(C + rbase[t] + 8 * g + 4 * lh) = v;
+                for (int g = 0; g < 4; ++g)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
+                    for (int e = 0; e < 2; ++e) {
+                        const TC x0 = (TC)acc[t][4 * g + 2 * e], x1 = (TC)acc[t][4 * g + 2 * e + 1];
+                        ss += (float)x0 * (float)x0 + (float)x1 * (float)x1;
+                        pk[g][e] = (uint32_t)__builtin_bit_cast(uint16_t, x0) |
+                                   ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
+                    }
+                uint32_t rcv[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t snd = lh ? pk[d >> 1][d & 1] : pk[2 + (d >> 1)][d & 1];
+                    const auto r = __builtin_amdgcn_permlane32_swap(snd, snd, false, false);
+                    rcv[d] = lh ? r[1] : r[0];
+                }
+                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                const u4 o0 = lh ? u4{rcv[0], rcv[1], pk[2][0], pk[2][1]} : u4{pk[0][0], pk[0][1], rcv[0], rcv[1]};
+                const u4 o1 = lh ? u4{rcv[2], rcv[3], pk[3][0], pk[3][1]} : u4{pk[1][0], pk[1][1], rcv[2], rcv[3]};
+                if constexpr (SCHED & 16) {
+                    asm volatile("" ::"v"(o0), "v"(o1));
+                } else if (m < a.M) {
+                    *(u4*)(C + rbase[t] + 16 * lh) = o0;
+                    *(u4*)(C + rbase[t] + 16 * lh + 8) = o1;
+                }
+            } else {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const t4 v = t4{(TC)acc[t][4 * g], (TC)acc[t][4 * g + 1], (TC)acc[t][4 * g + 2],
+                                    (TC)acc[t][4 * g + 3]};
+                    if constexpr (SCHED & 16) asm volatile("" ::"v"(v));
+                    else if (m < a.M) *(t4*)(C + rbase[t] + 8 * g + 4 * lh) = v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ss += (float)v[e] * (float)v[e];
+                }
             }
             ss = pair_sum(m < a.M ? ss : 0.f);
             pm[t >> 1] = (t & 1) ? fmaxf(pm[t >> 1], ss) : ss;
@@ -430,7 +479,8 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                         a.c_mode == CMT_C_HEADSPLIT && a.R == nullptr && !a.relu && a.rows_per_batch > 0 &&
                         a.M % a.rows_per_batch == 0,
                     "cmt_kv_proj: row A, K = 256, head-split C, no residual / relu, batch 1");
-        CMT_REQUIRE(a.N % (256 * parts) == 0, "cmt_kv_proj: N must be a multiple of 256 per column part");
+        CMT_REQUIRE(a.N % (256 * parts) == 0 && a.N / parts <= KP_MAXB,
+                    "cmt_kv_proj: N must be a multiple of 256 per column part, at most 2048 per part");
         CMT_REQUIRE(a.A2 == nullptr || (a.a2_mode == CMT_A2_SELECT && a.a2_cols * 2 == a.N),
                     "cmt_kv_proj: A2 selects the first half of the columns");
         CMT_REQUIRE(a.plane_max2 == nullptr || (a.plane_max_cols % (a.N / parts) == 0 && a.plane_max_cols <= a.N),
@@ -447,6 +497,7 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
         if (a.c_dtype == CMT_F16) {
             switch (sched) {   // CMT_KV_SCHED (kvproj_x3_kernel's SCHED bits); 4 / 8: diagnostics
                 case 1: kvproj_x3_kernel<f16_t, 1><<<g3, 512, 0, s3>>>(a, parts); break;
+                case 64: kvproj_x3_kernel<f16_t, 64><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 16: kvproj_x3_kernel<f16_t, 16><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 32: kvproj_x3_kernel<f16_t, 32><<<g3, 512, 0, s3>>>(a, parts); break;
                 case 48: kvproj_x3_kernel<f16_t, 48><<<g3, 512, 0, s3>>>(a, parts); break;

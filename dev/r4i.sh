@@ -28,6 +28,16 @@ for v in 16 0 16 0 20; do
         || { echo "conv probe failed"; tail -5 "$OUT/conv.txt"; exit 1; }
 done
 grep "conv var" "$OUT/conv.txt"
+for v in 1 0 1 0; do
+    env CMT_ATTN_US=$v CMT_ATTN_VARIANT=us$v timeout -k 10 120 python -u dev/attn_exp.py --dtype f16 --nk 56400 --bound \
+        --round --qs >> "$OUT/attn.txt" 2>/dev/null || { echo "attn_exp failed"; tail -5 "$OUT/attn.txt"; exit 1; }
+done
+grep attn "$OUT/attn.txt"
+CMT_ATTN_US=1 timeout -k 10 500 python -u -m pytest tests/test_gpu_fullsize.py -v -rA --timeout 200 \
+    --timeout-method thread > "$OUT/fullsize_us.log" 2>&1
+rc=$?
+[[ $rc -eq 0 || $rc -eq 1 ]] || { echo "fullsize rc=$rc"; tail -30 "$OUT/fullsize_us.log"; exit 1; }
+grep -E "passed|failed" "$OUT/fullsize_us.log" | tail -2
 mkdir -p "$OUT/trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ref --no-recompute --no-traffic \

@@ -192,9 +192,13 @@ int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
  *        CMT_ATTN_FORCE_PIPELINED  the f16 bounded long-key path runs the
  *                               software-pipelined kernel (measured slower:
  *                               101.4 vs 98.8 us at the fusion shape, r4h;
- *                               kept selectable for A/B and tests) */
+ *                               kept selectable for A/B and tests)
+ *        CMT_ATTN_UNSCALED_Q       f16 long-key core without the fold
+ *                               permission: Q enters the QK^T MFMAs unscaled
+ *                               and the scores are scaled in fp32 (flash-attn's
+ *                               order) instead of Q * scale as hi + lo */
 enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2, CMT_ATTN_FORCE_PINGPONG = 256,
-       CMT_ATTN_FORCE_PIPELINED = 512 };
+       CMT_ATTN_FORCE_PIPELINED = 512, CMT_ATTN_UNSCALED_Q = 1024 };
 
 typedef struct cmt_attn_args {
     int B, H, Nq, Nk;

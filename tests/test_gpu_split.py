@@ -460,8 +460,10 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
     from the K norm partials, the loose-bound redo (one key of huge norm
     orthogonal to every query: its bound puts every P of the split below
     f16's normal range, so the workgroup reruns that split on the online max),
-    the online max alone (no partials), and the scale fold with q kept as
-    hi + lo.  Held to the f16 core's own output rounding."""
+    the online max alone (no partials), q * scale kept as hi + lo (QS) or q
+    unscaled with the scale applied to the fp32 scores (US,
+    CMT_ATTN_UNSCALED_Q), and the scale fold.  Held to the f16 core's own
+    output rounding."""
     H = 8
     g = torch.Generator().manual_seed(Nk + Nq)
     sq = 3.0 if mode == "scaled" else 1.0
@@ -476,13 +478,14 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
     km = _kmax2(k, B, Nk, H).to(dev)
     qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
     outs = {}
-    for name, kmax2, fold in (("bounded", km, False), ("online", None, False), ("fold", km, True)):
+    for name, kmax2, fold, fl in (("bounded", km, False, 0), ("online", None, False, 0), ("fold", km, True, 0),
+                                  ("bounded_us", km, False, 1024), ("online_us", None, False, 1024)):
         O = torch.full((B, Nq, H * 32), float("nan"), device=dev)
         N.attention(qd, kd, vd, O, B=B, H=H, Nq=Nq, Nk=Nk,
                     q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
                     v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32), scale=1 / math.sqrt(32),
                     kv_splits=splits, round_output=True, fold_scale=fold, kmax2=kmax2, kmax_ld=H if kmax2 is not None
-                    else 0, kmax_plane0=0)
+                    else 0, kmax_plane0=0, _diag_flags=fl)
         torch.cuda.synchronize()
         got = O.cpu().double()
         assert torch.isfinite(got).all(), name
@@ -491,7 +494,7 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
     # 2^-9 |x| covers one ulp of the larger neighbour at a binade boundary), plus the f16 rounding of
     # the dominant P itself when a few keys carry the row (scaled q): 2^-11 of the largest |v|
     tol = 2 ** -9 * ref.abs().clamp(min=2 ** -4) + 2 ** -11 * v.double().abs().max().item()
-    for name in ("bounded", "online"):
+    for name in ("bounded", "online", "bounded_us", "online_us"):
         d = (outs[name] - ref).abs()
         assert (d <= tol).all(), (name, d.max().item())
     # the fold permission rounds q*c once to f16: a slightly larger deviation, still small
