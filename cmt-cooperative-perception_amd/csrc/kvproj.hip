@@ -421,8 +421,10 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
                     const uint32_t snd = lh ? pk[d >> 1][d & 1] : pk[2 + (d >> 1)][d & 1];
+                    // v_permlane32_swap exchanges vdst of lanes 32..63 with vsrc of lanes 0..31:
+                    // the partner's value lands in vsrc (r[1]) on the low half, vdst (r[0]) on the high
                     const auto r = __builtin_amdgcn_permlane32_swap(snd, snd, false, false);
-                    rcv[d] = lh ? r[1] : r[0];
+                    rcv[d] = lh ? r[0] : r[1];
                 }
                 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
                 const u4 o0 = lh ? u4{rcv[0], rcv[1], pk[2][0], pk[2][1]} : u4{pk[0][0], pk[0][1], rcv[0], rcv[1]};
