@@ -1,0 +1,265 @@
+// Linear -> ReLU -> Linear in one launch at the reference's fp32 numerics
+// (cmt_mlp2_x3, cmt_hip.h): the camera position encoder rv_embedding
+// (cmt_head.py:297-301) over the frustum coordinates of _rv_pe (cmt_head.py:
+// 417-433, 24 000 rows per nuScenes frame) and the query coordinates of
+// _rv_query_embed (cmt_head.py:439-467).
+//
+// The two-GEMM form writes the 1024-wide hidden activation as f16 pairs to HBM
+// (98 MB per frame) and reads it back; its short-K first GEMM (K = 192, six
+// k-stages per tile) is pipeline fill and epilogue, its 256-column second GEMM
+// covers 188 tiles of a 256-CU chip.  Here one wave owns 32 rows end to end:
+//
+//   A fragments (its rows, all K) stay in registers for the whole launch;
+//   for each 32-unit hidden block hb:
+//     H^T[hb] = W1[hb] . A^T            (swapped 32x32x16 form: lane = row,
+//                                        registers = hidden units)
+//     H = relu(H + b1) split into f16 hi / lo in registers
+//     OUT^T += W2[:, hb] . H^T          (H^T's registers are the B operand: the
+//                                        pack orders W2's k like them, so the
+//                                        hidden tile never leaves the wave)
+//
+// Every product is the three-pass split-f16 product of cmt_gemm (W_hi A_lo +
+// W_lo A_hi + W_hi A_hi, fp32 accumulation); fc1 runs cmt_gemm's k order, so H
+// equals the two-GEMM path's hidden values bit for bit.  The weights of a hidden
+// block (W1: K/16 x 2 KB, W2: 32 KB) are shared by the workgroup's 4 waves
+// through LDS: a two-slot ring per matrix filled by LDS-DMA one block ahead, one
+// barrier per block, and the MFMAs of fc2(hb) interleaved with those of
+// fc1(hb + 1) (independent accumulators).  One wave per SIMD: the 8 output
+// accumulator tiles (128 registers), the A fragments (96 at K = 192) and the
+// hidden tile need the whole 512-register file.
+#include "cmt_common.h"
+
+#include <type_traits>
+
+namespace {
+
+constexpr int MW = 4;               // waves per workgroup, one per SIMD
+constexpr int MROWS = 32 * MW;      // rows per workgroup
+constexpr int NOUT = 256;           // output width
+constexpr int NOT = NOUT / 32;      // output tiles per wave
+constexpr int FRAG_B = 1024;        // one fragment image: 64 lanes x 16 bytes
+constexpr int W2_BLK = NOT * 2 * 2 * FRAG_B;   // one hidden block of W2p: 32 KB
+constexpr int MAX_HD = 2048;        // hidden width bound (b1 staged in LDS)
+
+typedef const __attribute__((address_space(1))) void* mlp_gaddr_t;
+typedef __attribute__((address_space(3))) void* mlp_laddr_t;
+
+__device__ __forceinline__ void mlp_glds16(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds((mlp_gaddr_t)src, (mlp_laddr_t)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 mma3(const pair8_t& wh, const pair8_t& wl, const pair8_t& xh, const pair8_t& xl,
+                                       f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc, 0, 0, 0);
+}
+
+template <int KS>   // K / 16
+__global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
+    constexpr int W1_BLK = KS * 2 * FRAG_B;
+    __shared__ __attribute__((aligned(16))) char lds[2 * W1_BLK + 2 * W2_BLK + MAX_HD * 4];
+    char* const s1 = lds;                 // W1 ring: 2 x W1_BLK
+    char* const s2 = lds + 2 * W1_BLK;    // W2 ring: 2 x W2_BLK
+    float* const sb1 = (float*)(lds + 2 * W1_BLK + 2 * W2_BLK);   // b1 (a global load per block
+                                                                  // cost a memory round trip each)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+    const int z = blockIdx.y;
+    const int m = blockIdx.x * MROWS + wave * 32 + lr;
+    const int row = min(m, a.M - 1);
+    const int nhb = a.Hd / 32;
+    const char* const w1g = (const char*)a.W1p;
+    const char* const w2g = (const char*)a.W2p;
+
+    // LDS-DMA of hidden block hb's fragments: piece p of a matrix by wave p % MW
+    auto issue_w1 = [&](int hb) {
+        if (hb >= nhb) return;
+        const char* src = w1g + (int64_t)hb * W1_BLK + lane * 16;
+        char* dst = s1 + (hb & 1) * W1_BLK;
+#pragma unroll
+        for (int p = wave; p < 2 * KS; p += MW) mlp_glds16(src + p * FRAG_B, dst + p * FRAG_B);
+    };
+    auto issue_w2 = [&](int hb) {
+        if (hb >= nhb) return;
+        const char* src = w2g + (int64_t)hb * W2_BLK + lane * 16;
+        char* dst = s2 + (hb & 1) * W2_BLK;
+#pragma unroll
+        for (int p = wave; p < 4 * NOT; p += MW) mlp_glds16(src + p * FRAG_B, dst + p * FRAG_B);
+    };
+    issue_w1(0);
+    issue_w2(0);
+    issue_w1(1);
+    for (int i = tid; i < a.Hd / 4; i += 64 * MW) *(f32x4*)(sb1 + 4 * i) = *(const f32x4*)(a.b1 + 4 * i);
+
+    // this lane's row of A as the B operand of fc1 (k = 16 ks + 8 lh + j), hi and lo planes
+    const pair_t* Ar = (const pair_t*)a.A + (int64_t)z * a.a_bstride + (int64_t)row * a.lda;
+    pair8_t ah[KS], al[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        ah[ks] = *(const pair8_t*)(Ar + 16 * ks + 8 * lh);
+        al[ks] = *(const pair8_t*)(Ar + a.K + 16 * ks + 8 * lh);
+    }
+
+    f32x16 oacc[NOT], hacc;
+#pragma unroll
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[t][r] = 0.f;
+    pair8_t hh[2], hl[2];   // the hidden tile as fc2's B operand (k-steps 0, 1), hi and lo
+
+    // fc1 of block hb from its W1 slot into hacc
+    auto fc1 = [&](int hb) {
+        const char* w = s1 + (hb & 1) * W1_BLK + lane * 16;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hacc[r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const pair8_t wh = *(const pair8_t*)(w + (2 * ks) * FRAG_B);
+            const pair8_t wl = *(const pair8_t*)(w + (2 * ks + 1) * FRAG_B);
+            hacc = mma3(wh, wl, ah[ks], al[ks], hacc);
+        }
+    };
+    // relu(hacc + b1) -> pairs; register r of lane half lh is hidden unit 8 (r >> 2) + 4 lh + (r & 3)
+    auto split_hidden = [&](int hb) {
+        const float* b1 = sb1 + hb * 32 + 4 * lh;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 bv = *(const f32x4*)(b1 + 8 * g);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = fmaxf(hacc[4 * g + e] + bv[e], 0.f) + 0.f;
+                const pair_t h = (pair_t)x;
+                hh[g >> 1][4 * (g & 1) + e] = h;
+                hl[g >> 1][4 * (g & 1) + e] = (pair_t)(x - (float)h);
+            }
+        }
+    };
+    // fc2 over block hb (its W2 slot), interleaved with fc1 of block hb + 1 when there is one.
+    // Step t of the block's MFMA stream: with fc1, t < 2 KS alternates fc2 step t / 2 and fc1
+    // step t / 2, then fc2 steps KS .. 15 follow; each step is a triple on one accumulator whose
+    // two weight fragments (hi, lo) are read from LDS two steps ahead (a 3-slot register ring),
+    // the order pinned by scheduling barriers -- left to itself the compiler read each pair right
+    // before its MFMAs and waited for it (lgkmcnt(0)) 28 times per block.
+    auto fc2_fc1 = [&](int hb, auto next_c) {
+        constexpr bool next = decltype(next_c)::value;   // compile-time: a branch-free MFMA stream
+        constexpr int NSTEP = next ? 2 * NOT + KS : 2 * NOT;
+        const char* w2 = s2 + (hb & 1) * W2_BLK + lane * 16;
+        const char* w1 = s1 + ((hb + 1) & 1) * W1_BLK + lane * 16;
+        auto is_fc2 = [](int t) { return !next || t >= 2 * KS || (t & 1) == 0; };
+        auto index = [](int t) { return !next ? t : (t < 2 * KS ? t >> 1 : t - KS); };
+        auto addr = [&](int t) { return (is_fc2(t) ? w2 : w1) + index(t) * 2 * FRAG_B; };
+        if constexpr (next) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hacc[r] = 0.f;
+        }
+        pair8_t fh[3], fl[3];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            fh[t] = *(const pair8_t*)addr(t);
+            fl[t] = *(const pair8_t*)(addr(t) + FRAG_B);
+        }
+#pragma unroll
+        for (int t = 0; t < NSTEP; ++t) {
+            if (t + 2 < NSTEP) {
+                fh[(t + 2) % 3] = *(const pair8_t*)addr(t + 2);
+                fl[(t + 2) % 3] = *(const pair8_t*)(addr(t + 2) + FRAG_B);
+            }
+            const int i = index(t);
+            if (is_fc2(t)) oacc[i >> 1] = mma3(fh[t % 3], fl[t % 3], hh[i & 1], hl[i & 1], oacc[i >> 1]);
+            else hacc = mma3(fh[t % 3], fl[t % 3], ah[i], al[i], hacc);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_mem();   // W1(0), W2(0), W1(1) landed for every wave's pieces
+    fc1(0);
+    split_hidden(0);
+    for (int hb = 0; hb + 1 < nhb; ++hb) {
+        // W2(hb) and W1(hb + 1) (issued one block ago) landed; every wave is past block hb - 1,
+        // so the slots of W2(hb - 1) and W1(hb) take W2(hb + 1) and W1(hb + 2)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_mem();
+        issue_w2(hb + 1);
+        issue_w1(hb + 2);
+        fc2_fc1(hb, std::true_type{});
+        split_hidden(hb + 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_mem();
+    fc2_fc1(nhb - 1, std::false_type{});   // the last block: fc2 only
+
+    // ---- epilogue: out = acc + (b2 + R) (cmt_gemm's order), row lr, columns 32 ot + 8 g + 4 lh + 0..3
+    if (m >= a.M) return;
+    const char* Rrow = nullptr;
+    if (a.R) {
+        const int resz = a.r_dtype == CMT_F32 ? 4 : 2;
+        Rrow = (const char*)a.R + ((int64_t)z * a.r_bstride + (int64_t)row * a.ldr) * resz;
+    }
+    const int cesz = a.c_dtype == CMT_F32 ? 4 : 2;
+    char* Crow = (char*)a.C + ((int64_t)z * a.c_bstride + (int64_t)row * a.ldc) * cesz;
+    typedef pair_t p4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = ot * 32 + 8 * g + 4 * lh;
+            const f32x4 bv = *(const f32x4*)(a.b2 + n);
+            f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+            if (Rrow) {
+                if (a.r_dtype == CMT_F32) {
+                    rv = *(const f32x4*)((const float*)Rrow + n);
+                } else {
+                    const p4 h = *(const p4*)((const pair_t*)Rrow + n);
+                    const p4 l = *(const p4*)((const pair_t*)Rrow + NOUT + n);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) rv[e] = (float)h[e] + (float)l[e];
+                }
+            }
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = oacc[ot][4 * g + e] + (bv[e] + rv[e]);
+            if (a.c_dtype == CMT_F32) *(f32x4*)((float*)Crow + n) = v;
+            else store_pair4((pair_t*)Crow, NOUT, n, v);
+        }
+}
+
+}  // namespace
+
+extern "C" int64_t cmt_mlp2_args_size(void) { return (int64_t)sizeof(cmt_mlp2_args); }
+
+extern "C" int cmt_mlp2_x3(const cmt_mlp2_args* ap, void* stream) {
+    CMT_REQUIRE(ap != nullptr, "cmt_mlp2_x3: null args");
+    const cmt_mlp2_args& a = *ap;
+    CMT_REQUIRE(a.M > 0 && a.batch > 0, "cmt_mlp2_x3: empty problem");
+    CMT_REQUIRE(a.N == NOUT, "cmt_mlp2_x3: the output width must be 256");
+    CMT_REQUIRE(a.K > 0 && a.K % 16 == 0 && a.K <= 192, "cmt_mlp2_x3: K must be a multiple of 16, at most 192");
+    CMT_REQUIRE(a.Hd > 0 && a.Hd % 32 == 0 && a.Hd <= MAX_HD,
+                "cmt_mlp2_x3: the hidden width must be a multiple of 32, at most 2048");
+    CMT_REQUIRE(a.A && a.W1p && a.W2p && a.b1 && a.b2 && a.C, "cmt_mlp2_x3: null pointer");
+    CMT_REQUIRE(a.lda >= 2 * a.K && a.lda % 8 == 0 && a.a_bstride % 8 == 0,
+                "cmt_mlp2_x3: A pair rows need lda >= 2K, 16-byte aligned");
+    CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16P, "cmt_mlp2_x3: C must be fp32 or an f16 pair");
+    CMT_REQUIRE(a.c_dtype == CMT_F32 ? a.ldc >= NOUT && a.ldc % 4 == 0 && a.c_bstride % 4 == 0
+                                     : a.ldc >= 2 * NOUT && a.ldc % 4 == 0 && a.c_bstride % 4 == 0,
+                "cmt_mlp2_x3: bad C row stride");
+    CMT_REQUIRE(a.R == nullptr || ((a.r_dtype == CMT_F32 && a.ldr >= NOUT) ||
+                                   (a.r_dtype == CMT_F16P && a.ldr >= 2 * NOUT)) && a.ldr % 4 == 0 &&
+                                      a.r_bstride % 4 == 0,
+                "cmt_mlp2_x3: R must be fp32 or f16-pair rows of 256");
+    CMT_REQUIRE(((uintptr_t)a.A | (uintptr_t)a.W1p | (uintptr_t)a.W2p) % 16 == 0 && (uintptr_t)a.b1 % 16 == 0 &&
+                    (uintptr_t)a.b2 % 16 == 0,
+                "cmt_mlp2_x3: A / packs / biases must be 16-byte aligned");
+    const dim3 grid((unsigned)cdiv(a.M, MROWS), (unsigned)a.batch);
+    hipStream_t s = (hipStream_t)stream;
+    switch (a.K / 16) {
+#define MLP_K(KS) case KS: mlp2_x3_kernel<KS><<<grid, 64 * MW, 0, s>>>(a); break;
+        MLP_K(1) MLP_K(2) MLP_K(3) MLP_K(4) MLP_K(5) MLP_K(6) MLP_K(7) MLP_K(8) MLP_K(9) MLP_K(10) MLP_K(11)
+        MLP_K(12)
+#undef MLP_K
+        default: return cmt_fail(CMT_ENOTSUP, "cmt_mlp2_x3: unsupported K");
+    }
+    return cmt_check_launch("cmt_mlp2_x3");
+}

@@ -68,6 +68,11 @@ class HeadEngineMixin:
                 re = self.rv_embedding
                 pk["rv"] = (to_dtype(re[0].weight, g), re[0].bias.detach().contiguous(),
                             to_dtype(re[2].weight, g), re[2].bias.detach().contiguous())
+                w0, _, w2, _ = pk["rv"]
+                if (g == SPLIT and w2.shape[0] == 256 and w0.shape[0] % 32 == 0 and w0.shape[-1] % 16 == 0
+                        and w0.shape[-1] <= 192):
+                    # fragment packs of the one-launch MLP (cmt_mlp2_x3)
+                    pk["rv_fused"] = native.mlp2_pack(w0, w2)
             return pk
         return self._pack.get("engine", params, prec.name, build)
 
@@ -212,10 +217,16 @@ class HeadEngineMixin:
         both = self._h2d(np.stack([l2i, i2l]), dev, "cams")
         return both[0], both[1]
 
+    def _rv_fused(self, pk):
+        """The fragment packs of the one-launch rv_embedding (cmt_mlp2_x3) when
+        that path applies (split policy, CMT_MLP_FUSED), else None."""
+        return pk.get("rv_fused") if OPTIONS.mlp_fused else None
+
     def _rv_pe_hidden(self, x_img, metas, B, pk, cams=None):
         """First half of _rv_pe + rv_embedding (cmt_head.py:417-433, 297-301):
         the frustum coordinates and rv_embedding[0] + ReLU -- they read only
-        the camera matrices and the feature-map shape."""
+        the camera matrices and the feature-map shape.  With the one-launch MLP
+        (_rv_fused) this returns the coordinates and _rv_pe_out runs both layers."""
         BV, _, h, w = x_img.shape
         pad_h, pad_w, _ = metas[0]["pad_shape"][0]
         dev = x_img.device
@@ -226,14 +237,23 @@ class HeadEngineMixin:
         coords = op_empty(BV * h * w, 3 * D, cdt, dev)
         native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w, D=D, pad_h=float(pad_h), pad_w=float(pad_w),
                             depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
+        if self._rv_fused(pk) is not None and cdt == SPLIT:
+            return coords                                                    # [BV*h*w, 2, 3D]
         hdt = cdt if cdt == w0.dtype else torch.float32
         return native.linear(coords, w0, b0, relu=True, out_dtype=hdt)       # [BV*h*w, 4C]
 
     def _rv_pe_out(self, hid, pos, B, Nk, offset, pk, R=None):
         """Second half: rv_embedding[2] into the camera pos rows (+ R as in _bev_pos_out)."""
         C = self.hidden_dim
-        _, _, w2, b2 = pk["rv"]
+        _, b0, w2, b2 = pk["rv"]
         M = hid.shape[0] // B   # V * h * w rows per batch element
+        fused = self._rv_fused(pk)
+        if fused is not None and hid.shape[-1] != w2.shape[-1]:
+            # hid holds the coordinates: both layers in one launch, the hidden rows stay on chip
+            native.mlp2(hid, fused[0], b0, fused[1], b2, pos, M=M, K=native.width(hid), Hd=w2.shape[-1], R=R,
+                        batch=B, a_bstride=M * native.width(hid), c_offset=offset * C, c_bstride=Nk * C,
+                        r_offset=offset * C, r_bstride=Nk * C)
+            return
         native.gemm(hid, w2, pos, M=M, N=C, K=w2.shape[-1], lda=hid.shape[-1], ldw=w2.shape[-1], ldc=C,
                     bias=b2, batch=B, a_bstride=M * hid.shape[-1], c_bstride=Nk * C, c_offset=offset * C,
                     R=R, ldr=C if R is not None else 0, r_bstride=Nk * C if R is not None else 0,
@@ -297,7 +317,16 @@ class HeadEngineMixin:
             coords = torch.empty((B * V * Nq, 3 * D), dtype=torch.float32, device=dev)
             native.rv_query_coords(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
                                    pad_w=float(pad_w), pc_range=self.pc_range)
-        r = self._mlp(coords, pk["rv"])
+        fused = self._rv_fused(pk)
+        # the one-launch MLP runs 128 rows per workgroup: below ~half the chip's CUs of
+        # workgroups (900 queries x 6 views = 43) the two GEMMs' finer tiles are faster
+        if fused is not None and coords.dtype == SPLIT and coords.shape[0] >= 128 * 128:
+            r = torch.empty((coords.shape[0], C), dtype=torch.float32, device=dev)
+            _, b0, w2, b2 = pk["rv"]
+            native.mlp2(coords, fused[0], b0, fused[1], b2, r, M=coords.shape[0], K=native.width(coords),
+                        Hd=w2.shape[-1])
+        else:
+            r = self._mlp(coords, pk["rv"])
         tl, tp = first_ops if first_ops is not None else (None, None)
         native.masked_view_sum(r, mask, qpos, B=B, V=V, Nq=Nq, C=C, base=qb, Yl=tl, Yp=tp)
         return qpos, first_ops is not None

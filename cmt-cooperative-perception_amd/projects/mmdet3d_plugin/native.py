@@ -27,7 +27,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 14
+ABI_VERSION = 15
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -131,9 +131,17 @@ class AdamwArgs(ctypes.Structure):
                 ("exp_avg_sq", _vp), ("sumsq", _vp)]
 
 
+class Mlp2Args(ctypes.Structure):
+    _fields_ = [("M", _int), ("K", _int), ("Hd", _int), ("N", _int), ("batch", _int),
+                ("A", _vp), ("lda", _i64), ("a_bstride", _i64),
+                ("W1p", _vp), ("b1", _vp), ("W2p", _vp), ("b2", _vp),
+                ("R", _vp), ("ldr", _i64), ("r_bstride", _i64), ("r_dtype", _int),
+                ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int)]
+
+
 STRUCTS = {"gemm": GemmArgs, "attn": AttnArgs, "ln": LnArgs, "chain": ChainArgs, "gemm_ex": GemmExArgs,
            "attn_train": AttnTrainArgs, "ln_train": LnTrainArgs, "bn": BnArgs, "det_loss": DetLossArgs,
-           "match_cost": MatchCostArgs, "adamw": AdamwArgs}
+           "match_cost": MatchCostArgs, "adamw": AdamwArgs, "mlp2": Mlp2Args}
 
 _LIB = None
 
@@ -159,6 +167,8 @@ def _load():
         "cmt_gemm_ln": ([P(GemmArgs), P(LnArgs), _vp], _int),
         "cmt_chain": ([P(ChainArgs), _vp], _int),
         "cmt_kv_proj": ([P(GemmArgs), _vp], _int),
+        "cmt_mlp2_x3": ([P(Mlp2Args), _vp], _int),
+        "cmt_mlp2_args_size": ([], _i64),
         "cmt_add_cast": ([_vp, _vp, _int, _int, _int, _vp, _vp, _vp], _int),
         "cmt_pos2embed": ([_vp, _i64, _int, _int, _int, _int, _int, _vp, _int, _i64, _vp], _int),
         "cmt_rv_pe_coords": ([_int, _int, _int, _int, _flt, _flt, _flt, _vp, P(_flt), _vp, _int, _vp], _int),
@@ -331,6 +341,49 @@ def kv_proj(A, Wp, C, *, M, N, bias=None, A2=None, headsplit_rows, plane_max2=No
             raise RuntimeError("plane_max2 must be fp32 with ceil(M/64) * plane_max_cols/32 entries")
         g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
     _check(lib().cmt_kv_proj(ctypes.byref(g), _stream()), "cmt_kv_proj")
+
+
+def mlp2_pack(W1, W2):
+    """Fragment packs of the pair weights of Linear(K, Hd) -> ReLU -> Linear(Hd, 256)
+    for cmt_mlp2_x3 (cmt_hip.h): W1 [Hd, 2, K], W2 [256, 2, Hd] (runtime.SPLIT)
+    -> (W1p, W2p).  W2p orders each 16-unit k-step of a 32-unit hidden block as
+    the hidden accumulator's registers: position 8 lh + j holds unit
+    8 (j >> 2) + 4 lh + (j & 3)."""
+    if W1.dtype != torch.uint16 or W2.dtype != torch.uint16 or W1.dim() != 3 or W2.dim() != 3:
+        raise RuntimeError("mlp2_pack: W1 / W2 must be split pair weights [N, 2, K]")
+    hd, _, k = W1.shape
+    n, _, hd2 = W2.shape
+    if hd2 != hd or n != 256 or hd % 32 or k % 16:
+        raise RuntimeError("mlp2_pack: W1 [Hd, 2, K] and W2 [256, 2, Hd] with Hd % 32 == 0, K % 16 == 0")
+    # W1p[hb][ks][pl][lh][lr][j] = W1[32 hb + lr][pl][16 ks + 8 lh + j]
+    w1p = W1.view(hd // 32, 32, 2, k // 16, 2, 8).permute(0, 3, 2, 4, 1, 5).contiguous()
+    # W2p[hb][ot][s][pl][lh][lr][jh][jl] = W2[32 ot + lr][pl][32 hb + 16 s + 8 jh + 4 lh + jl]
+    w2p = W2.view(8, 32, 2, hd // 32, 2, 2, 2, 4).permute(3, 0, 4, 2, 6, 1, 5, 7).contiguous()
+    return w1p, w2p
+
+
+def mlp2(A, W1p, b1, W2p, b2, C, *, M, K, Hd, R=None, batch=1, a_bstride=0, c_offset=0, c_bstride=0,
+         r_offset=0, r_bstride=0):
+    """C = Linear2(ReLU(Linear1(A) + b1)) + b2 (+ R) in one launch (cmt_mlp2_x3):
+    A pair rows [.., 2, K]; packs from mlp2_pack; C / R fp32 [.., 256] or pair
+    [.., 2, 256] rows.  Offsets and strides are LOGICAL (rows of the operand)."""
+    _dev(A, W1p, b1, W2p, b2, C, R)
+    if A.dtype != torch.uint16 or W1p.dtype != torch.uint16 or W2p.dtype != torch.uint16:
+        raise RuntimeError("mlp2: A and the packs must be split pairs (torch.uint16)")
+    g = Mlp2Args()
+    g.M, g.K, g.Hd, g.N, g.batch = M, K, Hd, 256, batch
+    g.A, g.lda, g.a_bstride = A.data_ptr(), lstride(A) * 2, a_bstride * 2
+    g.W1p, g.b1, g.W2p, g.b2 = W1p.data_ptr(), b1.data_ptr(), W2p.data_ptr(), b2.data_ptr()
+    sc = _ps(C)
+    g.C = C.data_ptr() + c_offset * sc * C.element_size()
+    g.ldc, g.c_bstride, g.c_dtype = lstride(C) * sc, c_bstride * sc, DT[C.dtype]
+    if R is not None:
+        sr = _ps(R)
+        g.R = R.data_ptr() + r_offset * sr * R.element_size()
+        g.ldr, g.r_bstride, g.r_dtype = lstride(R) * sr, r_bstride * sr, DT[R.dtype]
+    else:
+        g.R, g.ldr, g.r_bstride, g.r_dtype = None, 0, 0, F32
+    _check(lib().cmt_mlp2_x3(ctypes.byref(g), _stream()), "cmt_mlp2_x3")
 
 
 def _ps(t):

@@ -122,6 +122,7 @@ class Options:
     chain: bool            # CMT_CHAIN=0: f16/bf16 decoder as separate GEMM / LayerNorm launches
     bev_pos_cache: bool    # CMT_BEV_POS_CACHE=0: rebuild the BEV position-MLP hidden rows per call
     conv_halo: bool        # CMT_CONV_HALO=0: split shared_conv via NCHW->pair rows + per-tap gathered GEMM
+    mlp_fused: bool        # CMT_MLP_FUSED=0: split rv_embedding as two GEMMs (hidden pair rows via HBM)
 
 
 def _env_on(name):
@@ -129,7 +130,8 @@ def _env_on(name):
 
 
 OPTIONS = Options(side_stream=_env_on("CMT_SIDE_STREAM"), chain=_env_on("CMT_CHAIN"),
-                  bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"), conv_halo=_env_on("CMT_CONV_HALO"))
+                  bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"), conv_halo=_env_on("CMT_CONV_HALO"),
+                  mlp_fused=_env_on("CMT_MLP_FUSED"))
 
 
 @contextlib.contextmanager

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 14
+#define CMT_ABI_VERSION 15
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -159,6 +159,40 @@ int cmt_gemm(const cmt_gemm_args* args, void* stream);
  * a larger [B][planes][Nk][32] buffer (one launch per layer, C pointing at the
  * layer's first plane). */
 int cmt_kv_proj(const cmt_gemm_args* args, void* stream);
+
+/* cmt_mlp2_x3 (ABI 15): Linear(K, Hd) + ReLU + Linear(Hd, 256) in one launch at the
+ * reference's fp32 numerics (mlp.hip) -- the camera position encoder rv_embedding
+ * (cmt_head.py:297-301, applied at 433 on the frustum coordinates of _rv_pe and at
+ * 464 on the query coordinates of _rv_query_embed).  Replaces the two cmt_gemm
+ * calls (fc1 -> hidden pair rows in HBM -> fc2): the hidden activation never
+ * leaves the registers.  Every product is the split-f16 three-pass product of
+ * cmt_gemm (hi*hi + lo*hi + hi*lo, fp32 accumulation, fc1 in cmt_gemm's k order,
+ * so the hidden values equal the two-GEMM path's bit for bit).
+ *   A   CMT_F16P rows [M][2][K] (lda, a_bstride in 16-bit words), K % 16 == 0, K <= 192
+ *   W1p / W2p  the fragment packs of the pair weights W1 [Hd][2][K] and W2 [256][2][Hd]
+ *       (Hd % 32 == 0):
+ *       W1p[(((hb * K/16 + ks) * 2 + pl) * 64 + lane) * 8 + j]
+ *           = W1[32 hb + (lane & 31)][pl][16 ks + 8 (lane >> 5) + j]
+ *       W2p[((((hb * 8 + ot) * 2 + s) * 2 + pl) * 64 + lane) * 8 + j]
+ *           = W2[32 ot + (lane & 31)][pl][32 hb + 16 s + 8 (j >> 2) + 4 (lane >> 5) + (j & 3)]
+ *       (the second k order is the hidden accumulator's register order: fc1's
+ *       output tile is fc2's operand without leaving the registers)
+ *   b1 [Hd] (Hd <= 2048), b2 [256] fp32; out = fc2(relu(fc1(A) + b1)) + b2 (+ R)
+ *   R   optional residual rows (CMT_F16P [.][2][256] or fp32), ldr / r_bstride
+ *   C   CMT_F16P or fp32 rows, ldc / c_bstride (16-bit words for a pair C, else
+ *       elements); batch = grid y. */
+typedef struct cmt_mlp2_args {
+    int M, K, Hd, N;           /* N must be 256 */
+    int batch;
+    const void* A; int64_t lda; int64_t a_bstride;
+    const void* W1p; const float* b1;
+    const void* W2p; const float* b2;
+    const void* R; int64_t ldr; int64_t r_bstride; int r_dtype;
+    void* C; int64_t ldc; int64_t c_bstride; int c_dtype;
+} cmt_mlp2_args;
+
+int cmt_mlp2_x3(const cmt_mlp2_args* args, void* stream);
+int64_t cmt_mlp2_args_size(void);
 
 /* ------------------------------------------------------------------------
  * Multi-head attention core, head_dim = 32 (flash-style, online softmax,

@@ -359,10 +359,12 @@ def test_chain_path_matches_separate_launches(dev, prec):
         assert (a - b).abs().max().item() <= 2e-2 * scale, (k, (a - b).abs().max().item(), scale)
 
 
-@pytest.mark.parametrize("opt", ["conv_halo", "bev_pos_cache", "chain"])
+@pytest.mark.parametrize("opt", ["conv_halo", "bev_pos_cache", "chain", "mlp_fused"])
 def test_ref_path_selections_agree(dev, opt):
     """OPTIONS.conv_halo (CMT_CONV_HALO: shared_conv straight from the NCHW map
-    vs NCHW -> pair rows + the per-tap gathered GEMM), OPTIONS.bev_pos_cache
+    vs NCHW -> pair rows + the per-tap gathered GEMM), OPTIONS.mlp_fused
+    (CMT_MLP_FUSED: rv_embedding in one launch, mlp.hip, vs two split GEMMs with
+    the hidden pair rows through HBM), OPTIONS.bev_pos_cache
     (CMT_BEV_POS_CACHE: kept BEV position rows added in the conv epilogue vs the
     position MLP per call) and OPTIONS.chain (CMT_CHAIN: the split row-block
     chains of rowchain_x3.hip vs split-K GEMMs + LayerNorm launches) at the
