@@ -22,13 +22,29 @@
 // row & 15).  The weights never touch LDS: each of the 8 waves owns 32 output
 // columns of every 256-wide sub-GEMM and streams its fragments (hi and lo,
 // fragment-major packs: 1 KB contiguous per load instruction) from L2 straight
-// into a WRING-deep register ring that runs across sub-GEMM boundaries --
+// into a WRING-deep register ring (a whole sub-GEMM) that runs across sub-GEMM boundaries --
 // with pairs the per-workgroup weight bytes double, and the f16 kernels'
 // LDS-DMA ring would hold two stages in what LDS is left.  All loads are
 // ordinary compiler-visible loads (its waitcnt pass counts them exactly).
 // MFMA 32x32x16 in the swapped form (lane = query row), so a row's LayerNorm
 // reduces over registers, the lane pair and the 8 waves.
 #include "cmt_common.h"
+
+#ifdef CMT_STAMPS
+// diagnostic build only (make OUT=../lib_stamps HIPFLAGS+=-DCMT_STAMPS): shader-clock stamps of
+// wave 0 of the first 16 workgroups of the last launch of each chain kind, read back by
+// cmt_debug_chain_stamps (dev/chain_stamps.py)
+__device__ unsigned long long g_chain_stamps[3][16][16];
+#define STAMP(K, i)                                                                            \
+    do {                                                                                      \
+        if (blockIdx.x < 16 && threadIdx.x == 0) g_chain_stamps[K][blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+extern "C" int cmt_debug_chain_stamps(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps));
+}
+#else
+#define STAMP(K, i) do { } while (0)
+#endif
 
 namespace {
 
@@ -38,7 +54,8 @@ constexpr int NWV = 8;                    // waves
 constexpr int NTC = 64 * NWV;             // threads
 constexpr int VPL = CE / NWV / 2;         // values per lane of a row (16)
 constexpr int KS = CE / 16;               // MFMA k-steps per sub-GEMM
-constexpr int WRING = 8;                  // k-steps of weight fragments in flight per wave
+constexpr int WRING_DEFAULT = 16;         // k-steps of weight fragments in flight per wave (a whole
+                                          // sub-GEMM: one sub-GEMM ahead)
 constexpr int PLANE = RB * CE * 2;        // one f16 image [32][256]: 16 KB
 constexpr int ACT = 2 * PLANE;            // a pair image: hi plane, lo plane
 constexpr int OFF_A = 0, OFF_B = ACT;
@@ -52,7 +69,7 @@ __device__ __forceinline__ int xcol(int wave, int lh, int r) { return wave * 32 
 
 // Weight stream of one wave: up to 3 sub-GEMMs, each a fragment-major pair pack (the Wn layout,
 // cmt_hip.h: hi pack then lo pack, lo_off elements apart) of which this wave reads block g.
-template <int NSUB>
+template <int NSUB, int WRING>
 struct WStream {
     const pair_t* base[NSUB];   // this wave's first fragment (hi) of each sub-GEMM
     int64_t lo_off[NSUB];
@@ -130,8 +147,8 @@ struct Ctx {
 
     // acc = act . W^T of sub-GEMM SUB over K = 256: three f16 passes per k-step; the stream's
     // ring slot of each step refills with the step WRING ahead (into the next sub-GEMM too)
-    template <int SUB, int NSUB>
-    __device__ __forceinline__ void sub_gemm(const char* act, WStream<NSUB>& ws, f32x16& acc) const {
+    template <int SUB, int NSUB, int WRING>
+    __device__ __forceinline__ void sub_gemm(const char* act, WStream<NSUB, WRING>& ws, f32x16& acc) const {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
@@ -192,11 +209,12 @@ __device__ __forceinline__ const pair_t* frag_base(const void* W, int g, int wav
     return (const pair_t*)W + (int64_t)((g * 4 + (wave >> 1)) * 8) * 4 * 512 + lane * 8;
 }
 
-template <int KIND>
+template <int KIND, int WRING>
 __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_TOTAL];
     Ctx e;
     e.lds = lds;
+    STAMP(KIND, 0);
     const int tid = threadIdx.x;
     e.lane = tid & 63;
     e.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -215,7 +233,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
     const int64_t plane = (int64_t)((a.rows + RB - 1) / RB) * RB * CE;   // one partial in tile order
 
     // ---- the weight stream of this wave (fragment-major pair packs, hi then lo)
-    WStream<NSUB> wst;
+    WStream<NSUB, WRING> wst;
     wst.nt = e.wave & 1;
     if constexpr (KIND == 0) {
         wst.base[0] = frag_base(a.Wo, 0, e.wave, e.lane);   // self-attn out_proj
@@ -232,15 +250,14 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
         wst.lo_off[0] = (int64_t)3 * CE * CE;
     }
     const bool gemm = KIND != 2 || has_next;
-    if (gemm) {
-#pragma unroll
-        for (int s = 0; s < WRING; ++s) wst.load(s);
-    }
 
-    // ---- prologue loads: the attention output rows -> actA (ordinary loads + LDS writes), the
-    // parameter block -> LDS, this lane's residual / query_pos / partial / old-output values
+    // ---- prologue loads, in the order their values are needed (vmcnt counts in issue order: a
+    // wait for a value loaded after the weight ring's first WRING steps would wait for those
+    // too -- the stamps showed ~6 700 cycles to the first barrier that way): the attention output
+    // rows and the parameter block (-> LDS), B2's partials / query_pos / old output, then the
+    // weight ring, then the LDS writes and the values first used after the first sub-GEMM
+    f32x4 xv[4];
     if constexpr (KIND != 2) {
-        f32x4 xv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {                      // 2048 16-byte pieces: hi then lo planes
             const int piece = tid + NTC * i;
@@ -249,6 +266,45 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
             const int src_row = min(m0 + r, a.rows - 1);
             xv[i] = *(const f32x4*)((const pair_t*)a.X + (int64_t)src_row * (2 * CE) + pl * CE + 8 * ch);
         }
+    }
+    constexpr int NPRM4 = (KIND == 0 ? PRM_A : PRM_B) / 4;
+    constexpr int PRM_IT = (NPRM4 + NTC - 1) / NTC;
+    f32x4 pv[PRM_IT];
+#pragma unroll
+    for (int i = 0; i < PRM_IT; ++i) {
+        const int piece = tid + NTC * i;
+        if (piece < NPRM4) pv[i] = *(const f32x4*)(a.prm + 4 * piece);
+    }
+    float res[VPL], qp[VPL], oold[VPL];
+    const bool need_p = KIND == 0 || (KIND == 2 && has_next && g < 2);
+    const bool max_into = KIND == 2 && g == 0 && (a.out_flags & CMT_LN_MAX_INTO);
+    if constexpr (KIND == 2) {
+        float t[3][VPL];
+        load_tile(ws, rb, e.wave, e.lane, res);
+#pragma unroll
+        for (int p = 1; p < 4; ++p) load_tile(ws + p * plane, rb, e.wave, e.lane, t[p - 1]);
+#pragma unroll
+        for (int p = 1; p < 4; ++p)
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) res[i] += t[p - 1][i];
+        if (need_p) {
+            load_row(a.P, row, e.wave, e.lh, qp);
+        } else {
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) qp[i] = 0.f;
+        }
+        if (max_into) {
+            load_row(a.OUT, row, e.wave, e.lh, oold);
+        } else {
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) oold[i] = 0.f;
+        }
+    }
+    if (gemm) {
+#pragma unroll
+        for (int s = 0; s < WRING; ++s) wst.load(s);
+    }
+    if constexpr (KIND != 2) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int piece = tid + NTC * i;
@@ -257,40 +313,30 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
             *(f32x4*)(actA + pl * PLANE + r * (CE * 2) + ((ch ^ (r & 15)) << 4)) = xv[i];
         }
     }
-    const int nprm = KIND == 0 ? PRM_A : PRM_B;
-    for (int piece = tid; piece < (nprm >> 2); piece += NTC)
-        *(f32x4*)(lds + OFF_PRM + piece * 16) = *(const f32x4*)(a.prm + 4 * piece);
-    float res[VPL], qp[VPL], oold[VPL];
-    if constexpr (KIND == 2) {
-        float t[VPL];
-        load_tile(ws, rb, e.wave, e.lane, res);
 #pragma unroll
-        for (int p = 1; p < 4; ++p) {
-            load_tile(ws + p * plane, rb, e.wave, e.lane, t);
+    for (int i = 0; i < PRM_IT; ++i) {
+        const int piece = tid + NTC * i;
+        if (piece < NPRM4) *(f32x4*)(lds + OFF_PRM + piece * 16) = pv[i];
+    }
+    if constexpr (KIND != 2) {
+        if (a.R) {
+            load_row(a.R, row, e.wave, e.lh, res);
+        } else {
 #pragma unroll
-            for (int i = 0; i < VPL; ++i) res[i] += t[i];
+            for (int i = 0; i < VPL; ++i) res[i] = 0.f;
         }
-    } else if (a.R) {
-        load_row(a.R, row, e.wave, e.lh, res);
-    } else {
+        if (need_p) {
+            load_row(a.P, row, e.wave, e.lh, qp);
+        } else {
 #pragma unroll
-        for (int i = 0; i < VPL; ++i) res[i] = 0.f;
-    }
-    const bool need_p = KIND == 0 || (KIND == 2 && has_next && g < 2);
-    if (need_p) {
-        load_row(a.P, row, e.wave, e.lh, qp);
-    } else {
-#pragma unroll
-        for (int i = 0; i < VPL; ++i) qp[i] = 0.f;
-    }
-    const bool max_into = KIND == 2 && g == 0 && (a.out_flags & CMT_LN_MAX_INTO);
-    if (max_into) {
-        load_row(a.OUT, row, e.wave, e.lh, oold);
-    } else {
+            for (int i = 0; i < VPL; ++i) qp[i] = 0.f;
+        }
 #pragma unroll
         for (int i = 0; i < VPL; ++i) oold[i] = 0.f;
     }
+    STAMP(KIND, 1);
     barrier_mem();   // actA and the parameter block written by every wave
+    STAMP(KIND, 2);
 
     f32x16 acc;
     float v[VPL];
@@ -300,18 +346,22 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
     if constexpr (KIND == 0) {
         // ---------------- chain A
         e.sub_gemm<0>(actA, wst, acc);                                  // self-attn out_proj
+        STAMP(0, 3);
         {
             const float* bo = e.prm();
 #pragma unroll
             for (int r = 0; r < VPL; ++r) v[r] = acc[r] + bo[e.col(r)] + res[r];
         }
         e.layernorm(v, 256, 512, eps);                                  // norms[0]
+        STAMP(0, 4);
         float u[VPL];
 #pragma unroll
         for (int i = 0; i < VPL; ++i) u[i] = v[i] + qp[i];
         e.put_act(actB, u);                                             // (y + query_pos) pairs
         barrier_mem();
+        STAMP(0, 5);
         e.sub_gemm<1>(actB, wst, acc);                                  // cross-attn Q projection
+        STAMP(0, 6);
         const float* bq = e.prm() + 768;
         h4 qo[4];
 #pragma unroll
@@ -329,20 +379,25 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
                 *(h4*)((f16_t*)a.Q + (((int64_t)b * 8 + (c0 >> 5)) * a.Nq + rr) * 32 + (c0 & 31)) = qo[gg];
             }
         }
+        STAMP(0, 7);
         return;
     }
     if constexpr (KIND == 1) {
         // ---------------- chain B1: out_proj + norms[1], then FFN quarter g
         e.sub_gemm<0>(actA, wst, acc);                                  // cross-attn out_proj
+        STAMP(1, 3);
         {
             const float* bo = e.prm();
 #pragma unroll
             for (int r = 0; r < VPL; ++r) v[r] = acc[r] + bo[e.col(r)] + res[r];
         }
         e.layernorm(v, 256, 512, eps);                                  // norms[1] -> o (FFN residual)
+        STAMP(1, 4);
         e.put_act(actB, v);                                             // fc1 operand
         barrier_mem();
+        STAMP(1, 5);
         e.sub_gemm<1>(actB, wst, acc);                                  // fc1 rows [256g, 256g + 256)
+        STAMP(1, 6);
         {
             const float* b1 = e.prm() + 768 + 256 * g;
             float h[VPL];
@@ -351,7 +406,9 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
             e.put_act(actA, h);                                         // hidden quarter g = fc2 K block g
         }
         barrier_mem();
+        STAMP(1, 7);
         e.sub_gemm<2>(actA, wst, acc);                                  // fc2 partial over K block g
+        STAMP(1, 8);
         const float* b2 = e.prm() + 1792;
 #pragma unroll
         for (int r = 0; r < VPL; ++r) {
@@ -360,12 +417,14 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
             v[r] = x;
         }
         store_tile(ws + g * plane, rb, e.wave, e.lane, v);              // whole row block (clamped rows too)
+        STAMP(1, 9);
         return;
     }
     // ---------------- chain B2: norms[2] (+ post_norm), next layer's in_proj block g
 #pragma unroll
     for (int i = 0; i < VPL; ++i) v[i] = res[i];
     e.layernorm(v, 2048, 2304, eps);                                    // norms[2] -> next query
+    STAMP(2, 3);
     float y[VPL];
 #pragma unroll
     for (int i = 0; i < VPL; ++i) y[i] = v[i];
@@ -383,9 +442,12 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
         float u[VPL];
 #pragma unroll
         for (int i = 0; i < VPL; ++i) u[i] = y[i] + qp[i];              // qp = 0 for the V block
+        STAMP(2, 4);
         e.put_act(actA, u);                                             // (y + pos) (Q|K) / y (V) pairs
         barrier_mem();
+        STAMP(2, 5);
         e.sub_gemm<0>(actA, wst, acc);
+        STAMP(2, 6);
     }
     if (row_ok) {
         if (g == 0) {
@@ -418,6 +480,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
             }
         }
     }
+    STAMP(2, 7);
 }
 
 }  // namespace
@@ -427,8 +490,19 @@ int cmt_chain_x3(const cmt_chain_args& a, hipStream_t s) {
     CMT_REQUIRE(a.kind != 0 || a.wo_frag, "cmt_chain: the split chains take fragment-major pair weights (wo_frag)");
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
-    if (a.kind == 0) chain_x3_kernel<0><<<grid, NTC, 0, s>>>(a);
-    else if (a.kind == 1) chain_x3_kernel<1><<<grid, NTC, 0, s>>>(a);
-    else chain_x3_kernel<2><<<grid, NTC, 0, s>>>(a);
+    // CMT_CHAIN_RING=8: the weight ring half a sub-GEMM deep (A/B switch)
+    static const int ring = [] {
+        const char* e = getenv("CMT_CHAIN_RING");
+        return e && e[0] == '8' ? 8 : WRING_DEFAULT;
+    }();
+    if (ring == 8) {
+        if (a.kind == 0) chain_x3_kernel<0, 8><<<grid, NTC, 0, s>>>(a);
+        else if (a.kind == 1) chain_x3_kernel<1, 8><<<grid, NTC, 0, s>>>(a);
+        else chain_x3_kernel<2, 8><<<grid, NTC, 0, s>>>(a);
+    } else {
+        if (a.kind == 0) chain_x3_kernel<0, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
+        else if (a.kind == 1) chain_x3_kernel<1, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
+        else chain_x3_kernel<2, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
+    }
     return cmt_check_launch("cmt_chain");
 }
