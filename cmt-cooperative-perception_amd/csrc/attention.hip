@@ -59,6 +59,8 @@ struct AttnKParams {
     int splits;
     int tiles_per_split;
     int round_out;                  // 0, or the dtype code to round O to (CMT_ATTN_ROUND_OUTPUT)
+    float* lse;                     // optional (training forward, attn_pb2_kernel path): per (b, h, q)
+                                    // row statistic log2(sum exp2(s)) in exp2 units, [b][h][q]
 };
 
 // Final normalised output: 4 consecutive head dims of one query row.  A
@@ -1325,6 +1327,7 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             }
             store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
         }
+        if (p.lse && lh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + q] = (fast ? off : m_run) + __log2f(l_tot);
     } else {
         const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
         float* dst = p.Op + row * D;
@@ -1991,6 +1994,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
         for (int j = 0; j < 4; ++j) r[j] = (float)(bf16_t)r[j];
     }
     store_o4(p, b, q, h * D + d4, r);
+    if (p.lse && d4 == 0) p.lse[bhq] = M + __log2f(den);
 }
 
 // Path choice.  Long key ranges (the cross-attention shape) take the 8-wave
@@ -2055,9 +2059,22 @@ extern "C" int64_t cmt_attn_workspace_bytes(const cmt_attn_args* a) {
     return rows * (D + 2) * (int64_t)sizeof(float);
 }
 
+// the training forward (attn_train.hip) runs the long-key f16 path with the row statistic
+int attn_fwd_impl(const cmt_attn_args& a, float* lse, void* stream);
+
 extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_attn_fwd: null args");
-    const cmt_attn_args& a = *ap;
+    return attn_fwd_impl(*ap, nullptr, stream);
+}
+
+int cmt_attn_fwd_lse(const cmt_attn_args& a, float* lse, void* stream) {
+    CMT_REQUIRE(lse != nullptr && a.dtype == CMT_F16 && use_long(a) && a.kmax2 != nullptr &&
+                    !(a.flags & CMT_ATTN_FOLD_SCALE),
+                "cmt_attn_fwd_lse: the row statistic comes from the long-key f16 bounded path only");
+    return attn_fwd_impl(a, lse, stream);
+}
+
+int attn_fwd_impl(const cmt_attn_args& a, float* lse, void* stream) {
     CMT_REQUIRE(a.B > 0 && a.H > 0 && a.Nq > 0 && a.Nk > 0, "cmt_attn_fwd: empty problem");
     CMT_REQUIRE(a.dtype == CMT_F16 || a.dtype == CMT_BF16 || a.dtype == CMT_F32 || a.dtype == CMT_F16P,
                 "cmt_attn_fwd: dtype must be f32, f16, bf16 or f16 pair");
@@ -2095,6 +2112,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     p.splits = splits;
     p.tiles_per_split = cdiv(ntiles, splits);
     p.round_out = (a.flags & CMT_ATTN_ROUND_OUTPUT) && a.dtype != CMT_F32 ? a.dtype : 0;
+    p.lse = lse;
     p.Op = p.Mp = p.Lp = nullptr;
     if (splits > 1) {
         const int64_t need = cmt_attn_workspace_bytes(&a);
@@ -2125,7 +2143,7 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     } else if (use_long(a)) {
         // the scale is folded into Q either way; without the FOLD permission q * c is kept as hi + lo
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
-        const int spm = sp_mode(a.flags);
+        const int spm = lse ? 0 : sp_mode(a.flags);   // the row statistic: ping-pong kernel
         if (a.dtype == CMT_F16 && a.kmax2 != nullptr && spm != 0) {
             // f16 with bounded offsets: the software-pipelined single-stream kernel
 #define SPK(QS, B2, PR) attn_sp_kernel<QS, B2, PR><<<nwg, 512, 0, s>>>(p)

@@ -27,6 +27,8 @@
 // recomputed identically in the backward.
 #include "cmt_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int D = 32;
@@ -302,8 +304,10 @@ __global__ __launch_bounds__(256) void train_dq_kernel(AP p) {
     }
 }
 
-// dK, dV: waves own 32 keys; loop over 64-query tiles (Q, dO, LSE2, delta in LDS)
-__global__ __launch_bounds__(256) void train_dkv_kernel(AP p) {
+// dK, dV: waves own 32 keys; loop over 64-query tiles (Q, dO, LSE2, delta in LDS), query tiles
+// [z qt_per, (z + 1) qt_per) of split z = blockIdx.z (f32 atomics into zeroed dK / dV when split:
+// the self-attention's ~1 100 keys alone are 9 x 8 workgroups)
+__global__ __launch_bounds__(256) void train_dkv_kernel(AP p, int qt_per) {
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) float Qs[KT * LDK];
     __shared__ __attribute__((aligned(16))) float Ds[KT * LDK];
@@ -330,7 +334,8 @@ __global__ __launch_bounds__(256) void train_dkv_kernel(AP p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
     const int nqt = (a.Nq + KT - 1) / KT;
-    for (int t = 0; t < nqt; ++t) {
+    const int tq0 = blockIdx.z * qt_per, tq1 = min(nqt, tq0 + qt_per);
+    for (int t = tq0; t < tq1; ++t) {
         __syncthreads();
         stage64(Qs, Qb, a.q_rs, t * KT, a.Nq, f16, tid);
         stage64(Ds, dOb, a.o_rs, t * KT, a.Nq, false, tid);
@@ -371,8 +376,13 @@ __global__ __launch_bounds__(256) void train_dkv_kernel(AP p) {
     float* dVb = a.dV + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs + (int64_t)k * a.v_rs;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        dKb[key_of(r, lh)] = dk[r] * a.scale;
-        dVb[key_of(r, lh)] = dv[r];
+        if (gridDim.z > 1) {
+            atomicAdd(dKb + key_of(r, lh), dk[r] * a.scale);
+            atomicAdd(dVb + key_of(r, lh), dv[r]);
+        } else {
+            dKb[key_of(r, lh)] = dk[r] * a.scale;
+            dVb[key_of(r, lh)] = dv[r];
+        }
     }
 }
 
@@ -693,6 +703,251 @@ __global__ __launch_bounds__(256) void train16_dkv_kernel(AP p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Long-key fp16 path (the cross-attention of the training step: FlashMHA's fp16
+// core, no DN mask, no dropout; Nk of 36 400 / 44 400 keys against ~1 100
+// queries).  The operands are first rounded to f16 ONCE into head-split copies
+// [B][H][N][32] (to16_kernel, with the K projection's per-64-key max |k|^2 for
+// the bounded forward), then:
+//   forward   the inference core (attention.hip attn_pb2_kernel + split combine,
+//             cmt_attn_fwd_lse) with the row statistic;
+//   dK / dV   train16_dkv2_kernel: 8 waves x 32 keys, the head's whole Q and dO
+//             (f16, <= 1 152 queries) resident in LDS -- no per-tile staging or
+//             barrier; S and dP with the key on the lane, so P and dS are the B
+//             operands of dV^T += dO^T P and dK^T += Q^T dS, whose A operands are
+//             ds_read_b64_tr_b16 transposed reads of the same row-major images;
+//   dQ        train16_dq2_kernel: 8 waves x 32 queries, K / V tiles by LDS-DMA
+//             into a 4-slot ring (one barrier per tile), S^T and dP^T with the
+//             query on the lane, dQ^T += K^T dS^T on transposed reads of the K
+//             image, key splits summed by f32 atomics.
+// Each f16 image row is 64 bytes with its 16-byte chunks XOR-swizzled by
+// (row >> 2) & 3 (row reads and transposed reads both conflict-free).
+// ---------------------------------------------------------------------------
+constexpr int NQ_RES = 1152;   // queries resident in LDS (dkv2): 2 x 72 KB images + statistics
+constexpr int DQ_RING = 4;
+
+__device__ __forceinline__ int sw_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// A operand of a product over 16 rows [r0, r0 + 16) of a row-major swizzled image (the rows in
+// the accumulator order of frag_acc): lane (lh, d = lane & 31) gets rows r0 + 4 lh + 0..3 and
+// r0 + 8 + 4 lh + 0..3 of column d (two ds_read_b64_tr_b16, cdna_hip_programming.md T10)
+__device__ __forceinline__ h8_t tr_frag(const char* img, int r0, int lane) {
+    const int g = lane >> 4, lh = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int c = 2 * (g & 1) + (pp >> 1);
+    const int ra = r0 + 4 * lh + qq, rb = ra + 8;
+    const char* pa = img + ra * 64 + ((c ^ ((ra >> 2) & 3)) << 4) + 8 * (pp & 1);
+    const char* pb = img + rb * 64 + ((c ^ ((rb >> 2) & 3)) << 4) + 8 * (pp & 1);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)pa);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)pb);
+    s16x8 v;
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    return __builtin_bit_cast(h8_t, v);
+}
+
+// f16 head-split copy Y[(b H + h) N + n][32] of X[b bs + h hs + n rs + d]; with kmax2, also
+// kmax2[e * H + h] = max over rows r = b N + n in [64 e, 64 e + 64) of |Y row|^2 (the rounded
+// values: the bound of the forward's bounded offsets).  Block (e, h): 64 rows x 4 threads.
+__global__ __launch_bounds__(256) void to16_kernel(const float* X, int64_t bs, int64_t hs, int64_t rs, int B, int H,
+                                                   int N, f16_t* Y, float* kmax2) {
+    const int e = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+    const int64_t r = (int64_t)e * 64 + (tid >> 2);
+    const int d0 = (tid & 3) * 8;
+    float ss = 0.f;
+    if (r < (int64_t)B * N) {
+        const int b = (int)(r / N), n = (int)(r - (int64_t)b * N);
+        const float* x = X + (int64_t)b * bs + (int64_t)h * hs + (int64_t)n * rs + d0;
+        const f32x4 u = *(const f32x4*)x, w = *(const f32x4*)(x + 4);
+        h8_t v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = (f16_t)u[j];
+            v[4 + j] = (f16_t)w[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += (float)v[j] * (float)v[j];
+        *(h8_t*)(Y + (((int64_t)b * H + h) * N + n) * D + d0) = v;
+    }
+    if (kmax2 == nullptr) return;
+    ss += __shfl_xor(ss, 1);
+    ss += __shfl_xor(ss, 2);
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) ss = fmaxf(ss, __shfl_xor(ss, o));
+    __shared__ float wm[4];
+    if ((tid & 63) == 0) wm[tid >> 6] = ss;
+    __syncthreads();
+    if (tid == 0) kmax2[(int64_t)e * H + h] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+__global__ __launch_bounds__(512, 1) void train16_dkv2_kernel(AP p, const f16_t* Q16, const f16_t* D16,
+                                                            const f16_t* K16, const f16_t* V16, int nqp) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) char Qs[NQ_RES * 64];
+    __shared__ __attribute__((aligned(16))) char Ds[NQ_RES * 64];
+    __shared__ __attribute__((aligned(16))) float Ls[NQ_RES];
+    __shared__ __attribute__((aligned(16))) float Dl[NQ_RES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+    const f16_t* Qh = Q16 + (int64_t)bh * a.Nq * D;
+    const f16_t* Dh = D16 + (int64_t)bh * a.Nq * D;
+    // the head's Q and dO (padded rows zero) and statistics (padded rows: P = 0)
+    for (int i = tid; i < nqp * 4; i += 512) {
+        const int r = i >> 2, c = i & 3;
+        h8_t qv = {}, dv = {};
+        if (r < a.Nq) {
+            qv = *(const h8_t*)(Qh + (int64_t)r * D + 8 * c);
+            dv = *(const h8_t*)(Dh + (int64_t)r * D + 8 * c);
+        }
+        *(h8_t*)(Qs + sw_off(r, c)) = qv;
+        *(h8_t*)(Ds + sw_off(r, c)) = dv;
+    }
+    for (int i = tid; i < nqp; i += 512) {
+        Ls[i] = i < a.Nq ? a.LSE[(int64_t)bh * a.Nq + i] : __builtin_inff();
+        Dl[i] = i < a.Nq ? a.delta[(int64_t)bh * a.Nq + i] : 0.f;
+    }
+    // this lane's key row of K and V as the B operands (k = d = 16 kk + 8 lh + j)
+    const int k = blockIdx.x * 256 + wave * 32 + lr;
+    const int kc = min(k, a.Nk - 1);
+    const f16_t* Kr = K16 + ((int64_t)bh * a.Nk + kc) * D;
+    const f16_t* Vr = V16 + ((int64_t)bh * a.Nk + kc) * D;
+    h8_t kf[2], vf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        kf[kk] = *(const h8_t*)(Kr + 16 * kk + 8 * lh);
+        vf[kk] = *(const h8_t*)(Vr + 16 * kk + 8 * lh);
+    }
+    __syncthreads();
+    f32x16 dk, dv;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
+    const float c = p.c;
+    for (int q0 = 0; q0 < nqp; q0 += 32) {
+        f32x16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int o = sw_off(q0 + lr, 2 * kk + lh);
+            s = mma16(*(const h8_t*)(Qs + o), kf[kk], s);      // S = Q K^T (lane = key)
+            dp = mma16(*(const h8_t*)(Ds + o), vf[kk], dp);    // dP = dO V^T
+        }
+        // register r of lane half lh is query q0 + 8 (r >> 2) + 4 lh + (r & 3)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 L = *(const f32x4*)(Ls + q0 + 8 * g + 4 * lh);
+            const f32x4 Dv = *(const f32x4*)(Dl + q0 + 8 * g + 4 * lh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * g + e;
+                const float pr = __builtin_amdgcn_exp2f(s[r] * c - L[e]);
+                s[r] = pr;                                        // P
+                dp[r] = pr * (dp[r] - Dv[e]);                     // dS
+            }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            dv = mma16(tr_frag(Ds, q0 + 16 * ss, lane), frag_acc(s, ss), dv);    // dV^T += dO^T P
+            dk = mma16(tr_frag(Qs, q0 + 16 * ss, lane), frag_acc(dp, ss), dk);   // dK^T += Q^T dS
+        }
+    }
+    if (k >= a.Nk) return;
+    float* dKb = a.dK + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs + (int64_t)k * a.k_rs;
+    float* dVb = a.dV + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs + (int64_t)k * a.v_rs;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        *(f32x4*)(dKb + 8 * g + 4 * lh) = f32x4{dk[4 * g] * a.scale, dk[4 * g + 1] * a.scale, dk[4 * g + 2] * a.scale,
+                                                dk[4 * g + 3] * a.scale};
+        *(f32x4*)(dVb + 8 * g + 4 * lh) = f32x4{dv[4 * g], dv[4 * g + 1], dv[4 * g + 2], dv[4 * g + 3]};
+    }
+}
+
+__device__ __forceinline__ void dq2_wait(int n) {   // n = this wave's DMA pieces allowed in flight
+    if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(512) void train16_dq2_kernel(AP p, const f16_t* Q16, const f16_t* D16,
+                                                         const f16_t* K16, const f16_t* V16) {
+    const cmt_attn_train_args& a = p.a;
+    __shared__ __attribute__((aligned(16))) char ring[DQ_RING * 2 * KT * 64];   // [slot][K | V][64 rows][64 B]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H, split = blockIdx.z;
+    const int q = blockIdx.x * 256 + wave * 32 + lr;
+    const int qc = min(q, a.Nq - 1);
+    const f16_t* Qr = Q16 + ((int64_t)bh * a.Nq + qc) * D;
+    const f16_t* Dr = D16 + ((int64_t)bh * a.Nq + qc) * D;
+    h8_t qf[2], df[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        qf[kk] = *(const h8_t*)(Qr + 16 * kk + 8 * lh);
+        df[kk] = *(const h8_t*)(Dr + 16 * kk + 8 * lh);
+    }
+    const float L = a.LSE[(int64_t)bh * a.Nq + qc];
+    const float dl = a.delta[(int64_t)bh * a.Nq + qc];
+    const int ntiles = (a.Nk + KT - 1) / KT;
+    const int t0 = split * p.tiles_per_split, t1 = min(ntiles, t0 + p.tiles_per_split);
+    // wave w copies piece w & 3 (16 rows) of the K (w < 4) or V tile; its lanes' LDS destination is
+    // lane-linear, the swizzle sits on the source chunk
+    const int piece = wave & 3, mat = wave >> 2;
+    const int prow = 16 * piece + (lane >> 2);
+    const f16_t* src0 = (mat ? V16 : K16) + (int64_t)bh * a.Nk * D;
+    const int schunk = (lane & 3) ^ ((prow >> 2) & 3);
+    char* const mydst = ring + mat * KT * 64 + piece * 1024;
+    int issued = t0;
+    auto issue_upto = [&](int n) {
+        const int e = min(n, t1);
+        while (issued < e) {
+            const int key = min(issued * KT + prow, a.Nk - 1);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (int64_t)key * D + 8 * schunk),
+                                             (__attribute__((address_space(3))) void*)(mydst + (issued % DQ_RING) * 2 * KT * 64),
+                                             16, 0, 0);
+            ++issued;
+        }
+    };
+    issue_upto(t0 + DQ_RING - 1);
+    f32x16 dq;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+    const float c = p.c;
+    for (int t = t0; t < t1; ++t) {
+        dq2_wait(issued - t - 1);
+        barrier_mem();                                  // tile t landed for every wave; tile t-1 consumed
+        issue_upto(t + DQ_RING);
+        const char* Ks = ring + (t % DQ_RING) * 2 * KT * 64;
+        const char* Vs = Ks + KT * 64;
+        const bool edge = (t + 1) * KT > a.Nk;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int o = sw_off(kb * 32 + lr, 2 * kk + lh);
+                s = mma16(*(const h8_t*)(Ks + o), qf[kk], s);      // S^T = K Q^T (lane = query)
+                dp = mma16(*(const h8_t*)(Vs + o), df[kk], dp);    // dP^T = V dO^T
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float pr = __builtin_amdgcn_exp2f(s[r] * c - L);
+                if (edge && t * KT + kb * 32 + key_of(r, lh) >= a.Nk) pr = 0.f;
+                s[r] = pr * (dp[r] - dl);                          // dS^T
+            }
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) dq = mma16(tr_frag(Ks, kb * 32 + 16 * ss, lane), frag_acc(s, ss), dq);
+        }
+    }
+    if (q >= a.Nq) return;
+    float* dQb = a.dQ + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs + (int64_t)q * a.q_rs;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float v = dq[r] * a.scale;
+        if (gridDim.z > 1) atomicAdd(dQb + key_of(r, lh), v);
+        else dQb[key_of(r, lh)] = v;
+    }
+}
+
 AP make_ap(const cmt_attn_train_args& a, int splits) {
     AP p;
     p.a = a;
@@ -726,10 +981,53 @@ int check_args(const cmt_attn_train_args& a, const char* who) {
     return 0;
 }
 
+// ---- the long-key fp16 path: applicability and workspace layout
+bool fast_path(const cmt_attn_train_args& a) {
+    static const bool off = [] {
+        const char* e = std::getenv("CMT_TRAIN_ATTN_FAST");
+        return e && e[0] == '0';
+    }();
+    return !off && a.fp16_inputs && a.dn_pad <= 0 && !(a.dropout_p > 0.f) && a.Nk >= 4096 && a.Nq > 128 &&
+           a.Nq <= NQ_RES && a.o_hs == D && a.kv_splits <= 0;
+}
+
+int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+// forward key splits: one round of one-per-CU workgroups (the ping-pong kernel holds a CU); at
+// ~1 100 queries the inference core's automatic choice (8 splits, 320 workgroups) ran two rounds
+int fwd_splits(const cmt_attn_train_args& a) { return max(1, min(16, 256 / (cdiv(a.Nq, 256) * a.B * a.H))); }
+
+struct FastWs {   // byte offsets into the workspace
+    int64_t q16, k16, v16, d16, kmax, attn, total;
+};
+
+FastWs fast_ws(const cmt_attn_train_args& a) {
+    FastWs w;
+    const int64_t qn = (int64_t)a.B * a.H * a.Nq * D * 2, kn = (int64_t)a.B * a.H * a.Nk * D * 2;
+    w.q16 = 0;
+    w.k16 = align256(w.q16 + qn);
+    w.v16 = align256(w.k16 + kn);
+    w.d16 = align256(w.v16 + kn);
+    w.kmax = align256(w.d16 + qn);
+    w.attn = align256(w.kmax + cdiv64((int64_t)a.B * a.Nk, 64) * a.H * 4);
+    cmt_attn_args g = {};
+    g.B = a.B; g.H = a.H; g.Nq = a.Nq; g.Nk = a.Nk; g.dtype = CMT_F16;
+    g.kv_splits = fwd_splits(a);
+    w.total = align256(w.attn + cmt_attn_workspace_bytes(&g));
+    return w;
+}
+
+void to16(const float* X, int64_t bs, int64_t hs, int64_t rs, int B, int H, int N, f16_t* Y, float* kmax,
+          hipStream_t s) {
+    to16_kernel<<<dim3((unsigned)cdiv64((int64_t)B * N, 64), (unsigned)H), 256, 0, s>>>(X, bs, hs, rs, B, H, N, Y,
+                                                                                        kmax);
+}
+
 }  // namespace
 
 extern "C" int64_t cmt_attn_train_workspace_bytes(const cmt_attn_train_args* a) {
     if (!a) return 0;
+    if (fast_path(*a)) return fast_ws(*a).total;
     const int s = train_splits(*a);
     if (s <= 1) return 0;
     return (int64_t)s * a->B * a->H * a->Nq * (D + 2) * (int64_t)sizeof(float);
@@ -743,6 +1041,34 @@ extern "C" int cmt_attn_train_fwd(const cmt_attn_train_args* ap, void* stream) {
         return cmt_fail(CMT_EWORKSPACE, "cmt_attn_train_fwd: workspace too small");
     AP p = make_ap(*ap, splits);
     hipStream_t s = (hipStream_t)stream;
+    if (fast_path(*ap)) {
+        // f16 head-split operands (+ the keys' per-64-row max |k|^2), then the inference core with
+        // the row statistic (attention.hip; output rounded to f16 like the flash core's)
+        const cmt_attn_train_args& a = *ap;
+        const FastWs w = fast_ws(a);
+        char* base = (char*)a.workspace;
+        f16_t* q16 = (f16_t*)(base + w.q16);
+        f16_t* k16 = (f16_t*)(base + w.k16);
+        f16_t* v16 = (f16_t*)(base + w.v16);
+        float* kmax = (float*)(base + w.kmax);
+        to16(a.Q, a.q_bs, a.q_hs, a.q_rs, a.B, a.H, a.Nq, q16, nullptr, s);
+        to16(a.K, a.k_bs, a.k_hs, a.k_rs, a.B, a.H, a.Nk, k16, kmax, s);
+        to16(a.V, a.v_bs, a.v_hs, a.v_rs, a.B, a.H, a.Nk, v16, nullptr, s);
+        if (int rc = cmt_check_launch("cmt_attn_train_fwd (f16 copies)")) return rc;
+        cmt_attn_args g = {};
+        g.B = a.B; g.H = a.H; g.Nq = a.Nq; g.Nk = a.Nk; g.dtype = CMT_F16;
+        g.Q = q16; g.q_bstride = (int64_t)a.H * a.Nq * D; g.q_hstride = (int64_t)a.Nq * D; g.q_rstride = D;
+        g.K = k16; g.k_bstride = (int64_t)a.H * a.Nk * D; g.k_hstride = (int64_t)a.Nk * D; g.k_rstride = D;
+        g.V = v16; g.v_bstride = g.k_bstride; g.v_hstride = g.k_hstride; g.v_rstride = D;
+        g.O = a.O; g.o_bstride = a.o_bs; g.o_rstride = a.o_rs; g.o_dtype = CMT_F32;
+        g.scale = a.scale;
+        g.flags = CMT_ATTN_ROUND_OUTPUT;
+        g.kv_splits = fwd_splits(a);
+        g.workspace = base + w.attn;
+        g.workspace_bytes = w.total - w.attn;
+        g.kmax2 = kmax; g.kmax_ld = a.H; g.kmax_plane0 = 0; g.kmax_rows = 64;
+        return cmt_attn_fwd_lse(g, a.LSE, s);
+    }
     const dim3 grid(cdiv(ap->Nq, 128), ap->B * ap->H, splits);
     if (ap->fp16_inputs) {
         const bool mask = ap->dn_pad > 0, drop = ap->dropout_p > 0.f;
@@ -772,6 +1098,41 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const int64_t rows = (int64_t)ap->B * ap->H * ap->Nq;
     train_delta_kernel<<<(unsigned)cdiv64(rows, 4), 256, 0, s>>>(p);
+    if (fast_path(*ap) && ap->workspace != nullptr && ap->workspace_bytes >= fast_ws(*ap).total) {
+        const cmt_attn_train_args& a = *ap;
+        const FastWs w = fast_ws(a);
+        char* base = (char*)a.workspace;
+        f16_t* q16 = (f16_t*)(base + w.q16);
+        f16_t* k16 = (f16_t*)(base + w.k16);
+        f16_t* v16 = (f16_t*)(base + w.v16);
+        f16_t* d16 = (f16_t*)(base + w.d16);
+        to16(a.Q, a.q_bs, a.q_hs, a.q_rs, a.B, a.H, a.Nq, q16, nullptr, s);
+        to16(a.dO, a.o_bs, a.o_hs, a.o_rs, a.B, a.H, a.Nq, d16, nullptr, s);
+        to16(a.K, a.k_bs, a.k_hs, a.k_rs, a.B, a.H, a.Nk, k16, nullptr, s);
+        to16(a.V, a.v_bs, a.v_hs, a.v_rs, a.B, a.H, a.Nk, v16, nullptr, s);
+        // dQ: key splits of 8-wave workgroups, about two per CU
+        // (two 8-wave workgroups per CU: about 512 workgroups in one balanced round)
+        const int nqb = cdiv(a.Nq, 256);
+        const int ds = max(1, min(512 / (nqb * a.B * a.H), ntiles / 8));
+        AP pq = make_ap(a, ds);
+        if (ds > 1) {
+            const bool dense = a.q_hs == D && a.q_rs == (int64_t)a.H * D && a.q_bs == (int64_t)a.Nq * a.H * D;
+            if (dense) {
+                hipMemsetAsync(a.dQ, 0, (size_t)a.B * a.Nq * a.H * D * sizeof(float), s);
+            } else {
+                for (int b = 0; b < a.B; ++b)
+                    for (int h = 0; h < a.H; ++h)
+                        hipMemset2DAsync(a.dQ + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs, a.q_rs * sizeof(float), 0,
+                                         D * sizeof(float), a.Nq, s);
+            }
+        }
+        const int nqp = cdiv(a.Nq, 64) * 64;
+        train16_dkv2_kernel<<<dim3((unsigned)cdiv(a.Nk, 256), (unsigned)(a.B * a.H)), 512, 0, s>>>(p, q16, d16, k16,
+                                                                                                   v16, nqp);
+        train16_dq2_kernel<<<dim3((unsigned)nqb, (unsigned)(a.B * a.H), (unsigned)ds), 512, 0, s>>>(pq, q16, d16,
+                                                                                                    k16, v16);
+        return cmt_check_launch("cmt_attn_train_bwd");
+    }
     if (qs > 1) {
         // dQ is accumulated: zero it (its [Nq x 32] rows per (b, h), strided)
         for (int b = 0; b < ap->B; ++b)
@@ -797,7 +1158,26 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
         }
     } else {
         train_dq_kernel<<<gq, 256, 0, s>>>(p);
-        train_dkv_kernel<<<gk, 256, 0, s>>>(p);
+        // query splits of the dK / dV pass until the grid covers ~2 workgroups per CU
+        const int nqt = cdiv(ap->Nq, KT);
+        int ks = 1;
+        while ((int64_t)gk.x * gk.y * ks * 2 <= 512 && nqt / (ks * 2) >= 2) ks *= 2;
+        if (ks > 1) {
+            const cmt_attn_train_args& a = *ap;
+            for (int which = 0; which < 2; ++which) {
+                float* X = which ? a.dV : a.dK;
+                const int64_t bs = which ? a.v_bs : a.k_bs, hs = which ? a.v_hs : a.k_hs, rs = which ? a.v_rs : a.k_rs;
+                if (hs == D && rs == (int64_t)a.H * D && bs == (int64_t)a.Nk * a.H * D) {
+                    hipMemsetAsync(X, 0, (size_t)a.B * a.Nk * a.H * D * sizeof(float), s);
+                } else {
+                    for (int b = 0; b < a.B; ++b)
+                        for (int h = 0; h < a.H; ++h)
+                            hipMemset2DAsync(X + (int64_t)b * bs + (int64_t)h * hs, rs * sizeof(float), 0,
+                                             D * sizeof(float), a.Nk, s);
+                }
+            }
+        }
+        train_dkv_kernel<<<dim3(gk.x, gk.y, ks), 256, 0, s>>>(p, cdiv(nqt, ks));
     }
     return cmt_check_launch("cmt_attn_train_bwd");
 }

@@ -127,5 +127,10 @@ __device__ __forceinline__ void store_pair8(pair_t* row, int C, int c, const flo
     *(pair8_t*)(row + C + c) = l;
 }
 
+// The long-key f16 attention forward (attention.hip, cmt_attn_fwd's bounded-offset path) that
+// also writes the row statistic lse[(b * H + h) * Nq + q] = log2(sum_k exp2(c s_qk)) (exp2 units
+// of c = scale * log2 e): the training forward's flash-attn fp16 core (attn_train.hip).
+int cmt_attn_fwd_lse(const cmt_attn_args& a, float* lse, void* stream);
+
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }

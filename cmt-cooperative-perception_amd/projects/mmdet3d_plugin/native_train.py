@@ -125,6 +125,12 @@ def attn_train_bwd(Q, K, V, O, LSE, dO, dQ, dK, dV, **kw):
     a = _attn_args(Q, K, V, O, LSE, **kw)
     delta = torch.empty(kw["B"] * kw["H"] * kw["Nq"], dtype=torch.float32, device=O.device)
     a.dO, a.dQ, a.dK, a.dV, a.delta = dO.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dV.data_ptr(), delta.data_ptr()
+    # the long-key fp16 path takes f16 copies of Q, dO, K, V in the workspace (cmt_hip.h)
+    need = N.lib().cmt_attn_train_workspace_bytes(ctypes.byref(a))
+    ws = None
+    if need > 0:
+        ws = torch.empty(need, dtype=torch.uint8, device=O.device)
+        a.workspace, a.workspace_bytes = ws.data_ptr(), need
     N._check(N.lib().cmt_attn_train_bwd(ctypes.byref(a), N._stream()), "cmt_attn_train_bwd")
 
 

@@ -536,6 +536,14 @@ typedef struct cmt_attn_train_args {
     int kv_splits;             /* fwd: 0 = automatic */
     void* workspace; int64_t workspace_bytes;
 } cmt_attn_train_args;
+/* Long-key fp16 path (ABI 15; fp16_inputs, no DN mask, no dropout, Nk >= 4096,
+ * 128 < Nq <= 1152, heads contiguous in O (o_hs == 32), kv_splits 0 -- the
+ * cross-attention of the training step): the forward runs cmt_attn_fwd's
+ * bounded long-key core with the row statistic, the backward the dK/dV kernel
+ * with the head's Q / dO resident in LDS and a K/V-streaming dQ kernel, all on
+ * f16 copies of the operands held in the workspace.  cmt_attn_train_workspace_bytes
+ * covers both directions; the backward takes the same workspace (with less it
+ * runs the general kernels).  CMT_TRAIN_ATTN_FAST=0 disables the path. */
 int64_t cmt_attn_train_workspace_bytes(const cmt_attn_train_args* args);
 int cmt_attn_train_fwd(const cmt_attn_train_args* args, void* stream);
 int cmt_attn_train_bwd(const cmt_attn_train_args* args, void* stream);

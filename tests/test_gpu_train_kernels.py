@@ -84,7 +84,13 @@ def dn_mask(Nq, Nk, pad, grp):
 @pytest.mark.parametrize("B,Nq,Nk,pad,grp,fp16,p", [(1, 100, 1000, 0, 0, False, 0.0), (2, 70, 70, 30, 10, False, 0.0),
                                                     (1, 140, 140, 40, 8, False, 0.25), (1, 96, 3000, 0, 0, True, 0.0),
                                                     (2, 150, 1100, 50, 10, True, 0.25), (1, 200, 2049, 0, 0, True, 0.1),
-                                                    (1, 77, 300, 40, 8, True, 0.0)])
+                                                    (1, 77, 300, 40, 8, True, 0.0),
+                                                    # the long-key fp16 path (cross-attention of the training step:
+                                                    # attention core with the row statistic, LDS-resident dK/dV,
+                                                    # K/V-streaming dQ): ragged key tiles, two batch elements, the
+                                                    # LDS bound of 1 152 queries; 1 200 queries take the general kernels
+                                                    (1, 900, 8192, 0, 0, True, 0.0), (2, 1100, 4100, 0, 0, True, 0.0),
+                                                    (1, 1152, 5000, 0, 0, True, 0.0), (1, 1200, 4096, 0, 0, True, 0.0)])
 def test_attention_train_fwd_bwd(dev, B, Nq, Nk, pad, grp, fp16, p):
     T = _T()
     H, C = 8, 256
