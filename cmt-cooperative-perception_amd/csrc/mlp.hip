@@ -39,7 +39,8 @@ constexpr int NOUT = 256;           // output width
 constexpr int NOT = NOUT / 32;      // output tiles per wave
 constexpr int FRAG_B = 1024;        // one fragment image: 64 lanes x 16 bytes
 constexpr int W2_BLK = NOT * 2 * 2 * FRAG_B;   // one hidden block of W2p: 32 KB
-constexpr int MAX_HD = 2048;        // hidden width bound (b1 staged in LDS)
+constexpr int MAX_HD = 2048;
+        // hidden width bound (b1 staged in LDS)
 
 typedef const __attribute__((address_space(1))) void* mlp_gaddr_t;
 typedef __attribute__((address_space(3))) void* mlp_laddr_t;
@@ -55,7 +56,9 @@ __device__ __forceinline__ f32x16 mma3(const pair8_t& wh, const pair8_t& wl, con
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc, 0, 0, 0);
 }
 
-template <int KS>   // K / 16
+// KS = K / 16; PD = the LDS fragment prefetch distance in steps (3: same time, 4: +8 %,
+// profiles/r4t_mlp_prefetch.txt)
+template <int KS, int PD = 2>
 __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
     constexpr int W1_BLK = KS * 2 * FRAG_B;
     __shared__ __attribute__((aligned(16))) char lds[2 * W1_BLK + 2 * W2_BLK + MAX_HD * 4];
@@ -154,21 +157,23 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) hacc[r] = 0.f;
         }
-        pair8_t fh[3], fl[3];
+        // fragments PD steps ahead (a register ring of PD + 1 slots)
+        pair8_t fh[PD + 1], fl[PD + 1];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < PD; ++t) {
             fh[t] = *(const pair8_t*)addr(t);
             fl[t] = *(const pair8_t*)(addr(t) + FRAG_B);
         }
 #pragma unroll
         for (int t = 0; t < NSTEP; ++t) {
-            if (t + 2 < NSTEP) {
-                fh[(t + 2) % 3] = *(const pair8_t*)addr(t + 2);
-                fl[(t + 2) % 3] = *(const pair8_t*)(addr(t + 2) + FRAG_B);
+            if (t + PD < NSTEP) {
+                fh[(t + PD) % (PD + 1)] = *(const pair8_t*)addr(t + PD);
+                fl[(t + PD) % (PD + 1)] = *(const pair8_t*)(addr(t + PD) + FRAG_B);
             }
             const int i = index(t);
-            if (is_fc2(t)) oacc[i >> 1] = mma3(fh[t % 3], fl[t % 3], hh[i & 1], hl[i & 1], oacc[i >> 1]);
-            else hacc = mma3(fh[t % 3], fl[t % 3], ah[i], al[i], hacc);
+            const int sl = t % (PD + 1);
+            if (is_fc2(t)) oacc[i >> 1] = mma3(fh[sl], fl[sl], hh[i & 1], hl[i & 1], oacc[i >> 1]);
+            else hacc = mma3(fh[sl], fl[sl], ah[i], al[i], hacc);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
