@@ -309,6 +309,56 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(cmt_ln_train_args a) {
             if (a.dB) atomicAdd(a.dB + cur_g * C + lane + 64 * e, db[e]);
         }
     };
+    if (a.rows_per_wset <= 0) {
+        // one weight set (nn.LayerNorm): the block's 4 waves sum their dW / dB partials through LDS
+        // and the block issues one atomic per column (one per row and column made the ~1 100-row
+        // decoder LayerNorms ~30 us of atomic contention on 512 addresses)
+        __shared__ float red[2][4][C];
+#pragma unroll
+        for (int e = 0; e < E; ++e) dw[e] = db[e] = 0.f;
+        for (int row = w0; row < a.rows; row += nw) {
+            const float* x = a.X + (int64_t)row * a.ldx;
+            const float* dy = a.dY + (int64_t)row * a.ldy;
+            const float mean = a.mean[row], rstd = a.rstd[row];
+            float xh[E], gw[E], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int c = lane + 64 * e;
+                xh[e] = (x[c] - mean) * rstd;
+                const float d = dy[c];
+                gw[e] = d * a.W[c];
+                s1 += gw[e];
+                s2 += gw[e] * xh[e];
+                dw[e] += d * xh[e];
+                db[e] += d;
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) { s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); }
+            s1 /= C;
+            s2 /= C;
+            float* dx = a.dX + (int64_t)row * a.lddx;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int c = lane + 64 * e;
+                const float v = rstd * (gw[e] - s1 - xh[e] * s2);
+                dx[c] = a.accumulate ? dx[c] + v : v;
+            }
+        }
+        const int wv = threadIdx.x >> 6;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            red[0][wv][lane + 64 * e] = dw[e];
+            red[1][wv][lane + 64 * e] = db[e];
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 2 * C; i += 256) {
+            const int which = i / C, c = i - which * C;
+            const float v = red[which][0][c] + red[which][1][c] + red[which][2][c] + red[which][3][c];
+            float* dst = which ? a.dB : a.dW;
+            if (dst) atomicAdd(dst + c, v);
+        }
+        return;
+    }
     for (int row = w0; row < a.rows; row += nw) {
         const int g = a.rows_per_wset > 0 ? row / a.rows_per_wset : 0;
         if (g != cur_g) {
@@ -596,7 +646,9 @@ extern "C" int cmt_ln_train_fwd(const cmt_ln_train_args* ap, void* stream) {
 extern "C" int cmt_ln_train_bwd(const cmt_ln_train_args* ap, void* stream) {
     CMT_REQUIRE(ap && ap->rows > 0 && (ap->C == 64 || ap->C == 256), "cmt_ln_train_bwd: C must be 64 or 256");
     CMT_REQUIRE(ap->X && ap->dY && ap->dX && ap->W && ap->mean && ap->rstd, "cmt_ln_train_bwd: null pointer");
-    const unsigned g = (unsigned)min(cdiv(ap->rows, 4), 512);
+    // one weight set: ~2 rows per wave, blocks reduce before their atomics; GroupLayerNorm1d: a wave
+    // per row as before
+    const unsigned g = ap->rows_per_wset <= 0 ? (unsigned)min(cdiv(ap->rows, 8), 128) : (unsigned)min(cdiv(ap->rows, 4), 512);
     if (ap->C == 64) ln_bwd_kernel<64><<<g, 256, 0, (hipStream_t)stream>>>(*ap);
     else ln_bwd_kernel<256><<<g, 256, 0, (hipStream_t)stream>>>(*ap);
     return cmt_check_launch("cmt_ln_train_bwd");
