@@ -108,7 +108,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(cmt_gemm_ex_args a, int kc
     float* C = a.C + (int64_t)z * a.c_bs;
     const int col = n0 + wn * 32 + lr;
     if (col >= a.N) return;
-    const float bias = (a.bias && ks == 0) ? a.bias[col] : 0.f;
+    const float bias = (a.bias && ks == 0) ? a.bias[(int64_t)z * a.bias_bs + col] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -142,29 +142,68 @@ __device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
     lo = (bf16_t)(x - (float)hi);
 }
 
-// stage a 64-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) as bf16 hi / lo images
+// A 64-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) moves in two steps so the
+// next tile's global loads are in flight while the current one is multiplied: fetch_x3 loads this
+// thread's 8 elements into registers, put_x3 splits them into the bf16 hi / lo LDS images.
 template <int MODE>
-__device__ __forceinline__ void stage_x3(char* __restrict__ hi, char* __restrict__ lo, const float* __restrict__ X,
-                                         int64_t s_r, int64_t s_k, int rows, int K, int r0, int k0, int tid) {
-    typedef bf16_t b4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict__ X, int64_t s_r, int64_t s_k,
+                                         int rows, int K, int r0, int k0, int tid) {
     if (MODE == OP_KC) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int idx = tid + TNT * i;
             const int r = idx >> 3, c = (idx & 7) * 4;
             const int gr = r0 + r, gk = k0 + c;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            f32x4 t = {0.f, 0.f, 0.f, 0.f};
             if (gr < rows) {
                 const float* p = X + (int64_t)gr * s_r + gk;
-                if (gk + 3 < K) v = *(const f32x4*)p;
+                if (gk + 3 < K) t = *(const f32x4*)p;
                 else
-                    for (int j = 0; j < 4; ++j) v[j] = gk + j < K ? p[j] : 0.f;
+                    for (int j = 0; j < 4; ++j) t[j] = gk + j < K ? p[j] : 0.f;
             }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = t[j];
+        }
+    } else if (MODE == OP_MC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int gr = r0 + r, gk = k0 + k;
+            f32x4 t = {0.f, 0.f, 0.f, 0.f};
+            if (gk < K) {
+                const float* p = X + (int64_t)gk * s_k + gr;
+                if (gr + 3 < rows) t = *(const f32x4*)p;
+                else
+                    for (int j = 0; j < 4; ++j) t[j] = gr + j < rows ? p[j] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = t[j];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int idx = tid + TNT * i;
+            const int r = idx >> 5, k = idx & 31;
+            const int gr = r0 + r, gk = k0 + k;
+            v[i] = (gr < rows && gk < K) ? X[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
+        }
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__ lo, const float (&v)[8], int tid) {
+    typedef bf16_t b4 __attribute__((ext_vector_type(4)));
+    if (MODE == OP_KC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int r = idx >> 3, c = (idx & 7) * 4;
             b4 h, l;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 bf16_t hj, lj;
-                split_bf16(v[j], hj, lj);
+                split_bf16(v[4 * i + j], hj, lj);
                 h[j] = hj;
                 l[j] = lj;
             }
@@ -176,18 +215,10 @@ __device__ __forceinline__ void stage_x3(char* __restrict__ hi, char* __restrict
         for (int i = 0; i < 2; ++i) {
             const int idx = tid + TNT * i;
             const int k = idx >> 4, r = (idx & 15) * 4;
-            const int gr = r0 + r, gk = k0 + k;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (gk < K) {
-                const float* p = X + (int64_t)gk * s_k + gr;
-                if (gr + 3 < rows) v = *(const f32x4*)p;
-                else
-                    for (int j = 0; j < 4; ++j) v[j] = gr + j < rows ? p[j] : 0.f;
-            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 bf16_t h, l;
-                split_bf16(v[j], h, l);
+                split_bf16(v[4 * i + j], h, l);
                 *(bf16_t*)(hi + x3_off(r + j, k)) = h;
                 *(bf16_t*)(lo + x3_off(r + j, k)) = l;
             }
@@ -197,24 +228,36 @@ __device__ __forceinline__ void stage_x3(char* __restrict__ hi, char* __restrict
         for (int i = 0; i < 8; ++i) {
             const int idx = tid + TNT * i;
             const int r = idx >> 5, k = idx & 31;
-            const int gr = r0 + r, gk = k0 + k;
-            const float v = (gr < rows && gk < K) ? X[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
             bf16_t h, l;
-            split_bf16(v, h, l);
+            split_bf16(v[i], h, l);
             *(bf16_t*)(hi + x3_off(r, k)) = h;
             *(bf16_t*)(lo + x3_off(r, k)) = l;
         }
     }
 }
 
+// Workgroups are dealt to the 8 XCDs round-robin by linear id; renumber them so each XCD runs a
+// contiguous range of tiles (the column tiles of one row block, the tiles of one K chunk) and
+// reads their shared operand rows through its own L2 once.
+__device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
+    const int nx = gridDim.x, ny = gridDim.y, total = nx * ny * gridDim.z;
+    int b = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    if ((total & 7) == 0) b = (b & 7) * (total >> 3) + (b >> 3);
+    bx = b % nx;
+    by = (b / nx) % ny;
+    bz = b / (nx * ny);
+}
+
 template <int AM, int BM>
 __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int kchunk) {
-    __shared__ __attribute__((aligned(16))) char As[2][64 * X3RB];   // hi, lo
-    __shared__ __attribute__((aligned(16))) char Bs[2][64 * X3RB];
+    __shared__ __attribute__((aligned(16))) char As[2][2][64 * X3RB];   // [buffer][hi, lo]
+    __shared__ __attribute__((aligned(16))) char Bs[2][2][64 * X3RB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
-    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
-    const int z = blockIdx.z / a.ksplit, ks = blockIdx.z - z * a.ksplit;
+    int bx, by, bz;
+    xcd_tile(bx, by, bz);
+    const int n0 = bx * 64, m0 = by * 64;
+    const int z = bz / a.ksplit, ks = bz - z * a.ksplit;
     const float* A = a.A + (int64_t)z * a.a_bs;
     const float* B = a.B + (int64_t)z * a.b_bs;
     const int kb = ks * kchunk, ke = min(a.K, kb + kchunk);
@@ -222,16 +265,26 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const int ar = wm * 32 + lr, br = wn * 32 + lr;
-    for (int k0 = kb; k0 < ke; k0 += TBK) {
+    float va[8], vb[8];
+    fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
+    fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid);
+    int buf = 0;
+    for (int k0 = kb; k0 < ke; k0 += TBK, buf ^= 1) {
+        // one barrier per step: buffer buf was last read two steps ago, before the previous barrier
+        put_x3<AM>(As[buf][0], As[buf][1], va, tid);
+        put_x3<BM>(Bs[buf][0], Bs[buf][1], vb, tid);
         __syncthreads();
-        stage_x3<AM>(As[0], As[1], A, a.a_sm, a.a_sk, a.M, ke, m0, k0, tid);
-        stage_x3<BM>(Bs[0], Bs[1], B, a.b_sn, a.b_sk, a.N, ke, n0, k0, tid);
-        __syncthreads();
+        if (k0 + TBK < ke) {
+            fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, k0 + TBK, tid);
+            fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid);
+        }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int c = 16 * kk + 8 * lh;
-            const bf16x8 ah = *(const bf16x8*)(As[0] + x3_off(ar, c)), al = *(const bf16x8*)(As[1] + x3_off(ar, c));
-            const bf16x8 bh = *(const bf16x8*)(Bs[0] + x3_off(br, c)), bl = *(const bf16x8*)(Bs[1] + x3_off(br, c));
+            const bf16x8 ah = *(const bf16x8*)(As[buf][0] + x3_off(ar, c));
+            const bf16x8 al = *(const bf16x8*)(As[buf][1] + x3_off(ar, c));
+            const bf16x8 bh = *(const bf16x8*)(Bs[buf][0] + x3_off(br, c));
+            const bf16x8 bl = *(const bf16x8*)(Bs[buf][1] + x3_off(br, c));
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
@@ -240,7 +293,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
     float* C = a.C + (int64_t)z * a.c_bs;
     const int col = n0 + wn * 32 + lr;
     if (col >= a.N) return;
-    const float bias = (a.bias && ks == 0) ? a.bias[col] : 0.f;
+    const float bias = (a.bias && ks == 0) ? a.bias[(int64_t)z * a.bias_bs + col] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;

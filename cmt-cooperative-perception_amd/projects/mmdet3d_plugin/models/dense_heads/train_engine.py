@@ -218,7 +218,7 @@ class HeadTrainMixin:
             c1, gln, c2 = seq[0], seq[1], seq[3]
             hc = c1.weight.shape[0] // L
             w1 = c1.weight.view(L, hc, C, k).permute(0, 1, 3, 2).reshape(L, hc, k * C)
-            h = torch.stack([ops.linear(xin[l], w1[l]) for l in range(L)])               # [L, B, Nq, hc]
+            h = ops.linear_batched(xin, w1)                                              # [L, B, Nq, hc]
             h = ops.group_layer_norm(h.reshape(L, B * Nq, hc), gln.weight, gln.bias, gln.eps).view(L, B, Nq, hc)
             h = torch.relu(h)
             if k == 3:
@@ -227,7 +227,7 @@ class HeadTrainMixin:
             on = c2.weight.shape[0] // L
             w2 = c2.weight.view(L, on, hc, k).permute(0, 1, 3, 2).reshape(L, on, k * hc)
             b2 = c2.bias.view(L, on)
-            out[name] = torch.stack([ops.linear(h[l], w2[l], b2[l]) for l in range(L)])
+            out[name] = ops.linear_batched(h, w2, b2)
         pcr = self.pc_range
         c = (out["center"] + reference[None, :, :, :2]).sigmoid()
         z = (out["height"] + reference[None, :, :, 2:3]).sigmoid()
@@ -292,7 +292,18 @@ class HeadTrainMixin:
                     match_cls_weight=float(asg.get("cls_cost", {}).get("weight", 2.0)),
                     match_reg_weight=float(asg.get("reg_cost", {}).get("weight", 0.25)), code_weights=cw)
 
-    def _assign_all(self, preds, gtb, gtl, cfg, code_w):
+    def _gt_split(self, gtb, gtl):
+        """{(task, sample): (boxes, labels relative to the task)}: the GT of each task's classes,
+        selected once per step (each boolean selection is a device -> host sync)."""
+        out, flag = {}, 0
+        for t, ncls in enumerate(self.num_classes):
+            for b in range(len(gtl)):
+                m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
+                out[(t, b)] = (gtb[b][m], gtl[b][m] - flag)
+            flag += ncls
+        return out
+
+    def _assign_all(self, preds, gts, cfg, code_w):
         """HungarianAssigner3D (hungarian_assigner_3d.py:68-156) for every
         (layer, task, sample): the [Nq, n_gt] cost matrices are built on the
         device (cmt_match_cost), copied to the host in ONE transfer, solved by
@@ -302,24 +313,21 @@ class HeadTrainMixin:
         L, B = preds[0]["center"].shape[:2]
         dev = preds[0]["center"].device
         jobs, costs = [], []
-        flag = 0
         for t, d in enumerate(preds):
-            ncls = self.num_classes[t]
+            pb_all = torch.cat([d[k].detach() for k in ("center", "height", "dim", "rot", "vel")], -1)  # [L, B, Nq, 10]
+            pl_all = d["cls_logits"].detach()
             for l in range(L):
-                pb = torch.cat([d[k][l] for k in ("center", "height", "dim", "rot", "vel")], -1)    # [B, Nq, 10]
-                pl = d["cls_logits"][l]
+                pb, pl = pb_all[l], pl_all[l]
                 for b in range(B):
-                    m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
-                    g_b, gl_b = gtb[b][m], gtl[b][m] - flag
+                    g_b, gl_b = gts[(t, b)]
                     if g_b.shape[0] == 0:
                         continue
-                    cost = T.match_cost(pl[b].detach().contiguous(), pb[b].detach().contiguous(),
+                    cost = T.match_cost(pl[b].contiguous(), pb[b].contiguous(),
                                         _normalize_bbox(g_b).contiguous(), gl_b.int().contiguous(), code_w,
                                         gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["match_cls_weight"],
                                         reg_weight=cfg["match_reg_weight"])
                     jobs.append(((l, t, b), cost.shape))
                     costs.append(cost.reshape(-1))
-            flag += ncls
         out = {}
         if not jobs:
             return out
@@ -372,7 +380,8 @@ class HeadTrainMixin:
         gtl = [l.to(dev).long() for l in gt_labels_3d]
         L, B = preds[0]["center"].shape[:2]
         eps = float(torch.finfo(torch.float32).eps)   # mmdet weight_reduce_loss avg_factor + eps
-        matches = self._assign_all(preds, gtb, gtl, cfg, code_w)
+        gts = self._gt_split(gtb, gtl)
+        matches = self._assign_all(preds, gts, cfg, code_w)
         # reduce_mean of the DN target count (cmt_head_coop.py:686): the same for every layer and task, so
         # one all-reduce per step -- issued on EVERY rank, also when its frames carry no GT (a rank that
         # skipped it would pair the next collective, the gradient all-reduce, with this one)
@@ -384,18 +393,25 @@ class HeadTrainMixin:
             num_tgt = float(nt_t.item()) / dist.get_world_size()
         num_tgt = max(num_tgt, 1.0)
         losses = {}
+        # per task, once: the layers' box / logit views (one unbind each, so the backward writes every
+        # layer's gradient into one buffer instead of a zero-filled full copy per selected layer) and
+        # the layer-invariant DN terms
+        pbs, pls, dns = [], [], []
+        for t, d in enumerate(preds):
+            pbs.append(torch.cat([d[k] for k in ("center", "height", "dim", "rot", "vel")], -1).unbind(0))
+            pls.append(d["cls_logits"].unbind(0))
+            md = d.get("dn_mask_dict")
+            dns.append(self._dn_prep(d, md, self.num_classes[t], code_w)
+                       if md is not None and md["pad_size"] > 0 else None)
         for l in range(L):
             tot = {"loss_cls": 0.0, "loss_bbox": 0.0, "dn_loss_cls": 0.0, "dn_loss_bbox": 0.0}
-            flag = 0
             for t, d in enumerate(preds):
                 ncls = self.num_classes[t]
-                pb = torch.cat([d[k][l] for k in ("center", "height", "dim", "rot", "vel")], -1)    # [B, Nq, 10]
-                pl = d["cls_logits"][l]
+                pb, pl = pbs[t][l], pls[t][l]                                              # [B, Nq, 10 / ncls]
                 labs, tgts, bws, npos, nneg = [], [], [], 0, 0
                 for b in range(B):
-                    m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
-                    lab, tg, bw, p_, n_ = self._targets(pl.shape[1], ncls, gtb[b][m], gtl[b][m] - flag,
-                                                        matches.get((l, t, b)), dev)
+                    g_b, gl_b = gts[(t, b)]
+                    lab, tg, bw, p_, n_ = self._targets(pl.shape[1], ncls, g_b, gl_b, matches.get((l, t, b)), dev)
                     labs.append(lab); tgts.append(tg); bws.append(bw)
                     npos += p_; nneg += n_
                 nt, w = self._box_terms(torch.cat(tgts), torch.cat(bws), code_w)
@@ -406,41 +422,45 @@ class HeadTrainMixin:
                                    box_avg=float(npos) + eps)
                 tot["loss_cls"] = tot["loss_cls"] + torch.nan_to_num(out[0])
                 tot["loss_bbox"] = tot["loss_bbox"] + torch.nan_to_num(out[1])
-                md = d.get("dn_mask_dict")
-                if md is not None and md["pad_size"] > 0:
-                    dout = self._dn_loss(d, l, md, ncls, cfg, code_w, eps, num_tgt)
+                if dns[t] is not None:
+                    dout = self._dn_loss(dns[t], l, ncls, cfg, eps, num_tgt)
                     tot["dn_loss_cls"] = tot["dn_loss_cls"] + dout[0]
                     tot["dn_loss_bbox"] = tot["dn_loss_bbox"] + dout[1]
-                flag += ncls
             key = "" if l == L - 1 else f"d{l}."
             for k, v in tot.items():
                 if isinstance(v, torch.Tensor):
                     losses[key + k] = v
         return losses
 
-    def _dn_loss(self, d, l, md, ncls, cfg, code_w, eps, nt):
-        """_dn_loss_single_task (cmt_head.py:760-806); ``nt``: the reduce_mean'd,
-        clamped DN target count of the step (loss())."""
+    def _dn_prep(self, d, md, ncls, code_w):
+        """The layer-invariant part of _dn_loss_single_task (cmt_head.py:760-806): the known
+        queries' logits / boxes of every layer (one gather), targets, weights and averages."""
         kl, kb = md["known_lbs_bboxes"]
         raw = md["known_labels_raw"]
         bid = md["batch_idx"][md["known_indice"]]
         mk = md["map_known_indice"]
-        pl = d["dn_cls_logits"][l][bid, mk]                                        # [nk, ncls]
-        pb = torch.cat([d["dn_" + k][l] for k in ("center", "height", "dim", "rot", "vel")], -1)[bid, mk]
+        pl = d["dn_cls_logits"][:, bid, mk]                                         # [L, nk, ncls]
+        pb = torch.cat([d["dn_" + k] for k in ("center", "height", "dim", "rot", "vel")], -1)[:, bid, mk]
         num_tgt = md["known_indice"].numel()
         task_mask = raw != ncls
         any_task = bool(task_mask.any())
-        rows = task_mask if any_task else torch.ones_like(task_mask)
-        cls_avg = max(num_tgt * 3.14159 / 6 * self.split ** 3, 1)
-        ntg, w = self._box_terms(kb[rows].float(), torch.ones((int(rows.sum()), 10), device=pl.device), code_w)
+        rows = (task_mask if any_task else torch.ones_like(task_mask)).nonzero().squeeze(1)
+        ntg, w = self._box_terms(kb[rows].float(), torch.ones((rows.numel(), 10), device=pl.device), code_w)
+        return dict(pls=pl.unbind(0), pbs=pb[:, rows].unbind(0), kl=kl.int(), ntg=ntg, w=w, any_task=any_task,
+                    cls_avg=max(num_tgt * 3.14159 / 6 * self.split ** 3, 1),
+                    lw=torch.ones(pl.shape[1], dtype=torch.float32, device=pl.device),
+                    lab0=torch.full((0,), ncls, dtype=torch.int32, device=pl.device))
+
+    def _dn_loss(self, p, l, ncls, cfg, eps, nt):
+        """_dn_loss_single_task (cmt_head.py:760-806) of layer l from _dn_prep's terms; ``nt``: the
+        reduce_mean'd, clamped DN target count of the step (loss())."""
+        pl, pb, lw, ntg, w = p["pls"][l], p["pbs"][l], p["lw"], p["ntg"], p["w"]
         # the classification term covers every DN row, the box term only the task's rows
-        lw = torch.ones(pl.shape[0], dtype=torch.float32, device=pl.device)
-        out_c = ops.det_loss(pl, pb[:0], kl.int(), lw, ntg[:0], w[:0], gamma=cfg["gamma"], alpha=cfg["alpha"],
-                             cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=cls_avg + eps,
+        out_c = ops.det_loss(pl, pb[:0], p["kl"], lw, ntg[:0], w[:0], gamma=cfg["gamma"], alpha=cfg["alpha"],
+                             cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=p["cls_avg"] + eps,
                              box_avg=1.0)
-        lab_dummy = torch.full((0,), ncls, dtype=torch.int32, device=pl.device)
-        out_b = ops.det_loss(pl[:0], pb[rows], lab_dummy, lw[:0], ntg, w, gamma=cfg["gamma"], alpha=cfg["alpha"],
+        out_b = ops.det_loss(pl[:0], pb, p["lab0"], lw[:0], ntg, w, gamma=cfg["gamma"], alpha=cfg["alpha"],
                              cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=1.0,
                              box_avg=nt + eps)
-        lb = torch.nan_to_num(out_b[1]) * (1.0 if any_task else 0.0)
+        lb = torch.nan_to_num(out_b[1]) * (1.0 if p["any_task"] else 0.0)
         return self.dn_weight * torch.nan_to_num(out_c[0]), self.dn_weight * lb

@@ -24,7 +24,7 @@ from ... import native
 from ... import native_train as T
 from ...runtime import SPLIT
 
-__all__ = ["linear", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss"]
+__all__ = ["linear", "linear_batched", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss"]
 
 
 class _Linear(torch.autograd.Function):
@@ -47,6 +47,29 @@ def linear(x, w, b=None):
     shape = x.shape
     y = _Linear.apply(x.reshape(-1, shape[-1]).contiguous(), w.contiguous(), b)
     return y.view(*shape[:-1], w.shape[0])
+
+
+class _LinearBatched(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return T.linear_fwd_batched(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        return T.linear_bwd_batched(dy, x, w, need_dx=ctx.needs_input_grad[0], need_dw=ctx.needs_input_grad[1],
+                                    need_db=ctx.has_b and ctx.needs_input_grad[2])
+
+
+def linear_batched(x, w, b=None):
+    """x [L, ..., K], w [L, N, K], b [L, N] -> [L, ..., N]: one Linear per leading index (the task
+    heads' per-layer grouped Conv1d) in one launch, forward and backward."""
+    shape = x.shape
+    y = _LinearBatched.apply(x.reshape(shape[0], -1, shape[-1]).contiguous(), w.contiguous(),
+                             None if b is None else b.contiguous())
+    return y.view(*shape[:-1], w.shape[1])
 
 
 class _Attention(torch.autograd.Function):

@@ -27,7 +27,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 15
+ABI_VERSION = 16
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -85,7 +85,8 @@ class GemmExArgs(ctypes.Structure):
     _fields_ = [("M", _int), ("N", _int), ("K", _int), ("batch", _int), ("alpha", _flt), ("beta", _flt),
                 ("A", _vp), ("a_sm", _i64), ("a_sk", _i64), ("a_bs", _i64),
                 ("B", _vp), ("b_sn", _i64), ("b_sk", _i64), ("b_bs", _i64),
-                ("C", _vp), ("ldc", _i64), ("c_bs", _i64), ("bias", _vp), ("ksplit", _int)]
+                ("C", _vp), ("ldc", _i64), ("c_bs", _i64), ("bias", _vp), ("ksplit", _int),
+                ("bias_bs", _i64)]
 
 
 class AttnTrainArgs(ctypes.Structure):
@@ -261,8 +262,14 @@ def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_cur_device = torch._C._cuda_getDevice
+_cur_raw_stream = torch._C._cuda_getCurrentRawStream
+
+
 def _stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """the current HIP stream of the current device (torch.cuda.current_stream() costs ~10 us of
+    device-index bookkeeping per call: a training step launches ~3 000 native kernels)"""
+    return ctypes.c_void_p(_cur_raw_stream(_cur_device()))
 
 
 def dtype_code(dt):

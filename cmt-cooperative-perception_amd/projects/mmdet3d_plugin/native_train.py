@@ -40,7 +40,7 @@ def set_train_gemm(mode):
 
 
 def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0, bias=None, batch=1, a_bs=0,
-            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0, mode=None):
+            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0, mode=None, bias_bs=0):
     """C[z][m][n] = alpha sum_k A(m,k) B(n,k) (+bias) + beta C; strides in elements:
     a_strides = (s_m, s_k), b_strides = (s_n, s_k).  ``mode``: see set_train_gemm."""
     _f32(A, B, C, bias)
@@ -49,7 +49,7 @@ def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0
     g.A, (g.a_sm, g.a_sk), g.a_bs = A.data_ptr() + 4 * a_offset, a_strides, a_bs
     g.B, (g.b_sn, g.b_sk), g.b_bs = B.data_ptr() + 4 * b_offset, b_strides, b_bs
     g.C, g.ldc, g.c_bs = C.data_ptr() + 4 * c_offset, ldc, c_bs
-    g.bias, g.ksplit = _ptr(bias), ksplit
+    g.bias, g.ksplit, g.bias_bs = _ptr(bias), ksplit, bias_bs
     entry = _GEMM_ENTRY[mode or _gemm_mode]
     N._check(getattr(N.lib(), entry)(ctypes.byref(g), N._stream()), entry)
 
@@ -90,6 +90,34 @@ def linear_bwd(dY, X, W, need_dx=True, need_dw=True, need_db=True):
         # one column-sum launch (a split-K GEMM against a ones vector took a ones fill, a zero fill
         # and the GEMM: ~300 of the step's ~1 100 fill / elementwise launches)
         dB = dY.sum(0)
+    return dX, dW, dB
+
+
+def linear_fwd_batched(X, W, b=None):
+    """Y[l] = X[l] W[l]^T + b[l] for every l in one launch: X [L, M, K], W [L, N, K], b [L, N]
+    (all contiguous) -> Y [L, M, N]."""
+    L, M, K = X.shape
+    Nn = W.shape[1]
+    Y = torch.empty((L, M, Nn), dtype=torch.float32, device=X.device)
+    gemm_ex(X, (K, 1), W, (K, 1), Y, M=M, N_=Nn, K=K, ldc=Nn, bias=b, batch=L, a_bs=M * K, b_bs=Nn * K,
+            c_bs=M * Nn, bias_bs=Nn)
+    return Y
+
+
+def linear_bwd_batched(dY, X, W, need_dx=True, need_dw=True, need_db=True):
+    """(dX, dW, dB) of linear_fwd_batched, one launch each."""
+    L, M, K = X.shape
+    Nn = W.shape[1]
+    dY = dY.contiguous()
+    dX = dW = dB = None
+    if need_dx:
+        dX = torch.empty((L, M, K), dtype=torch.float32, device=X.device)
+        gemm_ex(dY, (Nn, 1), W, (1, K), dX, M=M, N_=K, K=Nn, ldc=K, batch=L, a_bs=M * Nn, b_bs=Nn * K, c_bs=M * K)
+    if need_dw:
+        dW = torch.empty((L, Nn, K), dtype=torch.float32, device=X.device)
+        gemm_ex(dY, (1, Nn), X, (1, K), dW, M=Nn, N_=K, K=M, ldc=K, batch=L, a_bs=M * Nn, b_bs=M * K, c_bs=Nn * K)
+    if need_db:
+        dB = dY.sum(1)
     return dX, dW, dB
 
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 15
+#define CMT_ABI_VERSION 16
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -498,8 +498,9 @@ typedef struct cmt_gemm_ex_args {
     const float* A; int64_t a_sm, a_sk, a_bs;
     const float* B; int64_t b_sn, b_sk, b_bs;
     float* C; int64_t ldc, c_bs;
-    const float* bias;         /* optional [N] */
+    const float* bias;         /* optional [N] per batch entry, at bias + z * bias_bs */
     int ksplit;
+    int64_t bias_bs;           /* ABI 16: batch stride of bias (0: one bias for every z) */
 } cmt_gemm_ex_args;
 int cmt_gemm_f32_ex(const cmt_gemm_ex_args* args, void* stream);
 /* cmt_gemm_bf16x3_ex: the same contract, each fp32 operand split into a bf16

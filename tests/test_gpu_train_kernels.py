@@ -54,6 +54,27 @@ def test_gemm_ex_transposes(dev, M, N, K, ta, tb, mode):
         assert (C3.cpu().double() - ref3).abs().max().item() < tol * tiny * tiny
 
 
+@pytest.mark.parametrize("L,M,K,N", [(6, 1100, 192, 64), (3, 70, 33, 10)])
+def test_linear_batched_fwd_bwd(dev, L, M, K, N):
+    """train_ops.linear_batched (one batched launch per product, per-entry bias through the
+    ABI-16 bias batch stride) against float64 autograd of L separate Linears."""
+    from projects.mmdet3d_plugin.models.utils import train_ops as ops
+    g = torch.Generator().manual_seed(L * M + K)
+    x, w, b = torch.randn(L, M, K, generator=g), torch.randn(L, N, K, generator=g) * 0.1, torch.randn(L, N, generator=g)
+    dy = torch.randn(L, M, N, generator=g)
+    xd, wd, bd = (t.double().requires_grad_() for t in (x, w, b))
+    yd = torch.einsum("lmk,lnk->lmn", xd, wd) + bd[:, None]
+    yd.backward(dy.double())
+    xg, wg, bg = (t.to(dev).requires_grad_() for t in (x, w, b))
+    y = ops.linear_batched(xg, wg, bg)
+    y.backward(dy.to(dev))
+    torch.cuda.synchronize()
+    tol = 2 ** -15 * math.sqrt(max(K, M)) * 8
+    for got, want in ((y, yd), (xg.grad, xd.grad), (wg.grad, wd.grad), (bg.grad, bd.grad)):
+        err = (got.detach().cpu().double() - want.detach()).abs().max().item()
+        assert err < tol * max(1.0, want.abs().max().item() / 10), err
+
+
 def _mix32(x):
     x = x.astype(np.uint64) & 0xFFFFFFFF
     x ^= x >> 16
