@@ -34,6 +34,14 @@ from ..utils import train_ops as ops
 __all__ = ["HeadTrainMixin", "Boxes3D", "inverse_sigmoid"]
 
 
+def _to_dev_async(t, dev):
+    """host tensor -> device without a stream sync (pinned staging, non-blocking copy; the caching
+    host allocator keeps the staging block until the copy has run)"""
+    if t.device.type != "cpu" or torch.device(dev).type == "cpu":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def inverse_sigmoid(x, eps=1e-5):
     """mmdet 2.28.2 inverse_sigmoid."""
     x = x.clamp(min=0, max=1)
@@ -100,7 +108,9 @@ class HeadTrainMixin:
             return ref.unsqueeze(0).repeat(B, 1, 1), None
         labels = torch.cat(gt_labels).long()
         boxes = torch.cat(gt_boxes).float()
-        batch_idx = torch.cat([torch.full((n,), i, dtype=torch.long) for i, n in enumerate(known_num)]).to(dev)
+        # built on the device (a pageable host -> device copy waits for the stream: the previous
+        # step's backward would have to drain before this step's forward could be issued)
+        batch_idx = torch.cat([torch.full((n,), i, dtype=torch.long, device=dev) for i, n in enumerate(known_num)])
         groups = min(self.scalar, self.num_query // max(known_num))
         known_indice = torch.arange(labels.numel(), device=dev).repeat(groups)
         known_labels = labels.repeat(groups)
@@ -110,16 +120,15 @@ class HeadTrainMixin:
         scale = known_bboxs[:, 3:6]
         if self.bbox_noise_scale > 0:
             if rand_prob is None:
-                rand_prob = torch.rand(center.shape, generator=generator).to(dev) * 2 - 1.0
-            rand_prob = rand_prob.to(dev)
+                rand_prob = _to_dev_async(torch.rand(center.shape, generator=generator), dev) * 2 - 1.0
+            rand_prob = _to_dev_async(rand_prob, dev)
             center = center + rand_prob * (scale / 2 + self.bbox_noise_trans) * self.bbox_noise_scale
             pcr = self.pc_range
             center = torch.stack([(center[:, 0] - pcr[0]) / (pcr[3] - pcr[0]),
                                   (center[:, 1] - pcr[1]) / (pcr[4] - pcr[1]),
                                   (center[:, 2] - pcr[2]) / (pcr[5] - pcr[2])], -1).clamp(0.0, 1.0)
             mask = torch.norm(rand_prob, 2, 1) > self.split
-            known_labels = known_labels.clone()
-            known_labels[mask] = sum(self.num_classes)
+            known_labels = torch.where(mask, torch.full_like(known_labels, sum(self.num_classes)), known_labels)
         single_pad = int(max(known_num))
         pad = single_pad * groups
         padded = torch.cat([ref.new_zeros(pad, 3), ref], 0).unsqueeze(0).repeat(B, 1, 1)
@@ -143,10 +152,11 @@ class HeadTrainMixin:
         """cmt_head.py:439-467 (geometry as device tensor ops, differentiable in rp)."""
         pad_h, pad_w, _ = metas[0]["pad_shape"][0]
         dev, dt = rp.device, rp.dtype
-        l2i = torch.from_numpy(np.stack([np.asarray(m["lidar2img"], dtype=np.float64) for m in metas])).to(dev, dt)
-        i2l = torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
-                                         for m in metas])).to(dev, dt)
-        pcr = torch.tensor(self.pc_range, dtype=dt, device=dev)
+        l2i = _to_dev_async(torch.from_numpy(np.stack([np.asarray(m["lidar2img"], dtype=np.float64)
+                                                       for m in metas])).to(dt), dev)
+        i2l = _to_dev_async(torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
+                                                       for m in metas])).to(dt), dev)
+        pcr = _to_dev_async(torch.tensor(self.pc_range, dtype=dt), dev)
         pts = rp * (pcr[3:] - pcr[:3]) + pcr[:3]
         proj = torch.einsum("bnd,bvcd->bvnc", torch.cat([pts, torch.ones_like(pts[..., :1])], -1), l2i)
         zm = proj[..., 2:3] > 0
@@ -375,7 +385,7 @@ class HeadTrainMixin:
         preds = [p[0] if isinstance(p, (list, tuple)) else p for p in preds_dicts]
         cfg = self._loss_cfg()
         dev = preds[0]["center"].device
-        code_w = torch.tensor(cfg["code_weights"], dtype=torch.float32, device=dev)
+        code_w = _to_dev_async(torch.tensor(cfg["code_weights"], dtype=torch.float32), dev)
         gtb = [_gravity_boxes(g).to(dev).float() for g in gt_bboxes_3d]
         gtl = [l.to(dev).long() for l in gt_labels_3d]
         L, B = preds[0]["center"].shape[:2]
