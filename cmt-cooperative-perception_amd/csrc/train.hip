@@ -715,7 +715,7 @@ extern "C" int cmt_bn_relu_train_fwd(const cmt_bn_args* ap, void* stream) {
     const cmt_bn_args& a = *ap;
     hipStream_t s = (hipStream_t)stream;
     float* sums = (float*)a.workspace;   // [0:C) centred squares, [C:2C) mean
-    hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s);
+    if (hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s) != hipSuccess) return cmt_fail(CMT_EINVAL, "bn: hipMemsetAsync failed");
     const int rpb = 256;
     dim3 grid(cdiv(a.rows, rpb), cdiv(a.C, 256));
     col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, nullptr, sums + a.C, 0, rpb);
@@ -732,7 +732,7 @@ extern "C" int cmt_bn_relu_train_bwd(const cmt_bn_args* ap, void* stream) {
     const cmt_bn_args& a = *ap;
     hipStream_t s = (hipStream_t)stream;
     float* sums = (float*)a.workspace;
-    hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s);
+    if (hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s) != hipSuccess) return cmt_fail(CMT_EINVAL, "bn: hipMemsetAsync failed");
     const int rpb = 256;
     bn_bwd_sums_kernel<<<dim3(cdiv(a.rows, rpb), cdiv(a.C, 256)), 256, 0, s>>>(a, sums, rpb);
     bn_bwd_apply_kernel<<<(unsigned)cdiv64((int64_t)a.rows * a.C, 256), 256, 0, s>>>(a, sums);
