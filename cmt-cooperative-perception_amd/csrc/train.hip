@@ -236,6 +236,14 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
     }
 }
 
+// Row (m) of each of fetch_x3's 8 elements within the 64-row tile.
+template <int MODE>
+__device__ __forceinline__ int x3_row(int e, int tid) {
+    if (MODE == OP_KC) return ((tid + TNT * (e >> 2)) >> 3);
+    if (MODE == OP_MC) return ((tid + TNT * (e >> 2)) & 15) * 4 + (e & 3);
+    return (tid + TNT * e) >> 5;
+}
+
 // Workgroups are dealt to the 8 XCDs round-robin by linear id; renumber them so each XCD runs a
 // contiguous range of tiles (the column tiles of one row block, the tiles of one K chunk) and
 // reads their shared operand rows through its own L2 once.
@@ -266,10 +274,19 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const int ar = wm * 32 + lr, br = wn * 32 + lr;
     float va[8], vb[8];
+    // a_rowsum: the first column tile also sums its A elements (fp32, before the split) per row
+    const bool rowsum = a.a_rowsum != nullptr && bx == 0;
+    float rs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rs[e] = 0.f;
     fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
     fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid);
     int buf = 0;
     for (int k0 = kb; k0 < ke; k0 += TBK, buf ^= 1) {
+        if (rowsum) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) rs[e] += va[e];
+        }
         // one barrier per step: buffer buf was last read two steps ago, before the previous barrier
         put_x3<AM>(As[buf][0], As[buf][1], va, tid);
         put_x3<BM>(Bs[buf][0], Bs[buf][1], vb, tid);
@@ -289,6 +306,16 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
         }
+    }
+    if (rowsum) {   // uniform per workgroup: per-row partials through LDS, one atomic per row
+        float* red = (float*)As[0][0];
+        __syncthreads();
+        if (tid < 64) red[tid] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(red + x3_row<AM>(e, tid), rs[e]);
+        __syncthreads();
+        if (tid < 64 && m0 + tid < a.M) atomicAdd(a.a_rowsum + (int64_t)z * a.M + m0 + tid, red[tid]);
     }
     float* C = a.C + (int64_t)z * a.c_bs;
     const int col = n0 + wn * 32 + lr;

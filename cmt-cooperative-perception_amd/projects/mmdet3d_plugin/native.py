@@ -27,7 +27,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 16
+ABI_VERSION = 17
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -86,7 +86,7 @@ class GemmExArgs(ctypes.Structure):
                 ("A", _vp), ("a_sm", _i64), ("a_sk", _i64), ("a_bs", _i64),
                 ("B", _vp), ("b_sn", _i64), ("b_sk", _i64), ("b_bs", _i64),
                 ("C", _vp), ("ldc", _i64), ("c_bs", _i64), ("bias", _vp), ("ksplit", _int),
-                ("bias_bs", _i64)]
+                ("bias_bs", _i64), ("a_rowsum", _vp)]
 
 
 class AttnTrainArgs(ctypes.Structure):

@@ -40,7 +40,7 @@ def set_train_gemm(mode):
 
 
 def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0, bias=None, batch=1, a_bs=0,
-            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0, mode=None, bias_bs=0):
+            b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0, mode=None, bias_bs=0, a_rowsum=None):
     """C[z][m][n] = alpha sum_k A(m,k) B(n,k) (+bias) + beta C; strides in elements:
     a_strides = (s_m, s_k), b_strides = (s_n, s_k).  ``mode``: see set_train_gemm."""
     _f32(A, B, C, bias)
@@ -51,6 +51,10 @@ def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0
     g.C, g.ldc, g.c_bs = C.data_ptr() + 4 * c_offset, ldc, c_bs
     g.bias, g.ksplit, g.bias_bs = _ptr(bias), ksplit, bias_bs
     entry = _GEMM_ENTRY[mode or _gemm_mode]
+    if a_rowsum is not None:
+        if entry != "cmt_gemm_bf16x3_ex":
+            raise ValueError("a_rowsum: bf16x3 GEMM only")
+        g.a_rowsum = a_rowsum.data_ptr()
     N._check(getattr(N.lib(), entry)(ctypes.byref(g), N._stream()), entry)
 
 
@@ -83,12 +87,17 @@ def linear_bwd(dY, X, W, need_dx=True, need_dw=True, need_db=True):
         gemm_ex(dY, (Nn, 1), W, (1, W.stride(0)), dX, M=M, N_=K, K=Nn, ldc=K)
     if need_dw:
         ks = _ksplit(M, Nn, K)
-        dW = torch.zeros((Nn, K), dtype=torch.float32, device=X.device) if ks > 1 else \
-            torch.empty((Nn, K), dtype=torch.float32, device=X.device)
-        gemm_ex(dY, (1, Nn), X, (1, X.stride(0)), dW, M=Nn, N_=K, K=M, ldc=K, beta=1.0 if ks > 1 else 0.0, ksplit=ks)
-    if need_db:
-        # one column-sum launch (a split-K GEMM against a ones vector took a ones fill, a zero fill
-        # and the GEMM: ~300 of the step's ~1 100 fill / elementwise launches)
+        # the bias gradient (column sums of dY = row sums of the GEMM's A = dY^T) comes out of the
+        # weight-gradient GEMM itself (a_rowsum); split-K dW and dB share one zero fill
+        fuse_db = need_db and _gemm_mode == "bf16x3"
+        nz, nb = (Nn * K if ks > 1 else 0), (Nn if fuse_db else 0)
+        buf = torch.zeros((nz + nb,), dtype=torch.float32, device=X.device) if nz + nb else None
+        dW = buf[:nz].view(Nn, K) if ks > 1 else torch.empty((Nn, K), dtype=torch.float32, device=X.device)
+        if fuse_db:
+            dB = buf[nz:]
+        gemm_ex(dY, (1, Nn), X, (1, X.stride(0)), dW, M=Nn, N_=K, K=M, ldc=K, beta=1.0 if ks > 1 else 0.0, ksplit=ks,
+                a_rowsum=dB)
+    if need_db and dB is None:
         dB = dY.sum(0)
     return dX, dW, dB
 
@@ -115,8 +124,11 @@ def linear_bwd_batched(dY, X, W, need_dx=True, need_dw=True, need_db=True):
         gemm_ex(dY, (Nn, 1), W, (1, K), dX, M=M, N_=K, K=Nn, ldc=K, batch=L, a_bs=M * Nn, b_bs=Nn * K, c_bs=M * K)
     if need_dw:
         dW = torch.empty((L, Nn, K), dtype=torch.float32, device=X.device)
-        gemm_ex(dY, (1, Nn), X, (1, K), dW, M=Nn, N_=K, K=M, ldc=K, batch=L, a_bs=M * Nn, b_bs=M * K, c_bs=Nn * K)
-    if need_db:
+        if need_db and _gemm_mode == "bf16x3":
+            dB = torch.zeros((L, Nn), dtype=torch.float32, device=X.device)
+        gemm_ex(dY, (1, Nn), X, (1, K), dW, M=Nn, N_=K, K=M, ldc=K, batch=L, a_bs=M * Nn, b_bs=M * K, c_bs=Nn * K,
+                a_rowsum=dB)
+    if need_db and dB is None:
         dB = dY.sum(1)
     return dX, dW, dB
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 step z2: fewer host launches in the training step (raw stream lookup, batched task-head
+# Round-4 step z2: training step changes: kernel + head training tests, training bench x2, host profile.
 # Linears with the ABI-16 bias stride, layer-invariant loss terms hoisted): kernel + head training
 # tests, training bench x2, host profile.
 set -uo pipefail

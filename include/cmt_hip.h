@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 16
+#define CMT_ABI_VERSION 17
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -501,6 +501,9 @@ typedef struct cmt_gemm_ex_args {
     const float* bias;         /* optional [N] per batch entry, at bias + z * bias_bs */
     int ksplit;
     int64_t bias_bs;           /* ABI 16: batch stride of bias (0: one bias for every z) */
+    float* a_rowsum;           /* ABI 17, optional [batch][M], zero-initialised by the caller:
+                                * += sum over this launch's k of A(m, k) in fp32 (cmt_gemm_bf16x3_ex
+                                * only; a Linear's bias gradient from its weight-gradient GEMM) */
 } cmt_gemm_ex_args;
 int cmt_gemm_f32_ex(const cmt_gemm_ex_args* args, void* stream);
 /* cmt_gemm_bf16x3_ex: the same contract, each fp32 operand split into a bf16

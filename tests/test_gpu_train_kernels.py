@@ -46,6 +46,13 @@ def test_gemm_ex_transposes(dev, M, N, K, ta, tb, mode):
     assert (C.cpu().double() - ref).abs().max().item() < tol
     assert (C2.cpu().double() - ref).abs().max().item() < tol
     if mode == "bf16x3":
+        # a_rowsum (ABI 17): the fp32 row sums of A accumulated by the first column tile, split-K too
+        rs = torch.zeros(M, device=dev)
+        C4 = torch.zeros(M, N, device=dev)
+        T.gemm_ex(Ad, a_str, Bd, b_str, C4, M=M, N_=N, K=K, ldc=N, beta=1.0, ksplit=4, mode=mode, a_rowsum=rs)
+        torch.cuda.synchronize()
+        want = (A.double().t() if ta else A.double()).sum(1)
+        assert (rs.cpu().double() - want).abs().max().item() < 1e-5 * math.sqrt(K) * 4
         tiny = 2.0 ** -30
         C3 = torch.empty(M, N, device=dev)
         T.gemm_ex(Ad * tiny, a_str, Bd * tiny, b_str, C3, M=M, N_=N, K=K, ldc=N, alpha=0.5, mode=mode)
