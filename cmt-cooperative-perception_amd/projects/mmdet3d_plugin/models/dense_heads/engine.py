@@ -318,9 +318,11 @@ class HeadEngineMixin:
             native.rv_query_coords(refB, l2i, i2l, coords, mask, B=B, V=V, Nq=Nq, D=D, pad_h=float(pad_h),
                                    pad_w=float(pad_w), pc_range=self.pc_range)
         fused = self._rv_fused(pk)
-        # the one-launch MLP runs 128 rows per workgroup: below ~half the chip's CUs of
-        # workgroups (900 queries x 6 views = 43) the two GEMMs' finer tiles are faster
-        if fused is not None and coords.dtype == SPLIT and coords.shape[0] >= 128 * 128:
+        # the one-launch MLP also for the queries' 900 x 6 view rows (43 workgroups): alone the two
+        # GEMMs' finer tiles finish sooner, but this runs on the second stream beside the K/V
+        # side of the frame, where fewer, longer workgroups take fewer CUs from it (661.1 vs 658.3
+        # frames/s alternating, profiles/r4z10_query_mlp_fused.txt)
+        if fused is not None and coords.dtype == SPLIT:
             r = torch.empty((coords.shape[0], C), dtype=torch.float32, device=dev)
             _, b0, w2, b2 = pk["rv"]
             native.mlp2(coords, fused[0], b0, fused[1], b2, r, M=coords.shape[0], K=native.width(coords),
