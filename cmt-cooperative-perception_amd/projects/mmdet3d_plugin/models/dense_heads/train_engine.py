@@ -194,8 +194,8 @@ class HeadTrainMixin:
             V = BV // B
             mems.append(ops.nchw_rows(x_img, B).view(B, V * h * w_, C))
             pad_h, pad_w, _ = metas[0]["pad_shape"][0]
-            i2l = torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
-                                             for m in metas])).float().to(x_img.device)
+            i2l = _to_dev_async(torch.from_numpy(np.stack([np.linalg.inv(np.asarray(m["lidar2img"], dtype=np.float64))
+                                                           for m in metas])).float(), x_img.device)
             D = self.depth_num
             coords = torch.empty((BV * h * w_, 3 * D), dtype=torch.float32, device=x_img.device)
             native.rv_pe_coords(i2l, coords, BV=BV, h=h, w=w_, D=D, pad_h=float(pad_h), pad_w=float(pad_w),

@@ -198,8 +198,8 @@ def ln_train_bwd(dY, X, W, mean, rstd, *, eps, rows_per_wset=0, wsets=1):
     rows, C = X.shape
     dY = dY.contiguous()
     dX = torch.empty((rows, C), dtype=torch.float32, device=X.device)
-    dW = torch.zeros((wsets, C), dtype=torch.float32, device=X.device)
-    dB = torch.zeros_like(dW)
+    dWB = torch.zeros((2, wsets, C), dtype=torch.float32, device=X.device)   # one fill for both sums
+    dW, dB = dWB[0], dWB[1]
     a = _ln_args(X, W, W, C=C, eps=eps, rows_per_wset=rows_per_wset)
     a.ldy, a.mean, a.rstd = C, mean.data_ptr(), rstd.data_ptr()
     a.dY, a.dX, a.lddx, a.accumulate, a.dW, a.dB = dY.data_ptr(), dX.data_ptr(), C, 0, dW.data_ptr(), dB.data_ptr()
@@ -256,8 +256,9 @@ def det_loss(logits, labels, label_w, boxes, targets, box_w, *, gamma, alpha, cl
     _f32(logits, boxes, targets, box_w, label_w)
     N._dev(labels)
     out = torch.empty(2, dtype=torch.float32, device=logits.device)
-    dl = torch.zeros_like(logits) if need_grad else None
-    db = torch.zeros_like(boxes) if need_grad else None
+    # the kernel writes every gradient element (rows x ncls, rows x 10): no fill for dense operands
+    dl = (torch.empty_like if logits.is_contiguous() else torch.zeros_like)(logits) if need_grad else None
+    db = (torch.empty_like if boxes.is_contiguous() else torch.zeros_like)(boxes) if need_grad else None
     a = N.DetLossArgs()
     a.R, a.ncls = logits.shape
     a.logits, a.ld_logits, a.labels, a.label_w = logits.data_ptr(), logits.stride(0), labels.data_ptr(), _ptr(label_w)
