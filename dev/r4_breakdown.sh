@@ -5,8 +5,8 @@
 set -uo pipefail
 OUT=gpurun_out/${1:-r4g}
 mkdir -p "$OUT"
-timeout -k 10 300 python -u dev/ref_error_diag.py > "$OUT/ref_error_diag.txt" 2>&1 || { tail -20 "$OUT/ref_error_diag.txt"; exit 1; }
+timeout -k 10 300 python -u tests/diag/ref_error_diag.py > "$OUT/ref_error_diag.txt" 2>&1 || { tail -20 "$OUT/ref_error_diag.txt"; exit 1; }
 cat "$OUT/ref_error_diag.txt"
-timeout -k 10 400 python -u dev/parity_sweep.py --seeds 0 --variants ref exact --no-fp32-gap \
+timeout -k 10 400 python -u tests/diag/parity_sweep.py --seeds 0 --variants ref exact --no-fp32-gap \
     --out "$OUT/parity_exact.json" > "$OUT/parity_exact.txt" 2>&1 || { tail -20 "$OUT/parity_exact.txt"; exit 1; }
 cat "$OUT/parity_exact.txt"

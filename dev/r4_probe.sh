@@ -15,6 +15,6 @@ for v in "--qs" ""; do
         || { echo "attn_exp failed"; tail -20 "$OUT/attn.txt"; exit 1; }
 done
 cat "$OUT/attn.txt"
-timeout -k 10 700 python -u dev/parity_sweep.py ${SWEEP_ARGS:-} --out "$OUT/parity_sweep.json" > "$OUT/parity_sweep.txt" 2>&1 \
+timeout -k 10 700 python -u tests/diag/parity_sweep.py ${SWEEP_ARGS:-} --out "$OUT/parity_sweep.json" > "$OUT/parity_sweep.txt" 2>&1 \
     || { echo "sweep failed"; tail -30 "$OUT/parity_sweep.txt"; exit 1; }
 cat "$OUT/parity_sweep.txt"

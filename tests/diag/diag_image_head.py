@@ -4,7 +4,7 @@ reports where the head outputs differ most."""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "cmt-cooperative-perception_amd"))
 import numpy as np  # noqa: E402

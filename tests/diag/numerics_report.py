@@ -1,11 +1,11 @@
 """Numerics report: native head (each precision policy) vs the CPU oracle in
 exact fp32 math and in the reference's numerics (fp16 cross-attention core).
-Run on a GPU box:  python dev/numerics_report.py
+Run on a GPU box:  python tests/diag/numerics_report.py
 """
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "cmt-cooperative-perception_amd"))
 

@@ -9,7 +9,7 @@ Variants:
   exact     -- exact-f32 GEMMs (v_mfma_f32_32x32x2_f32), QS core: separates the
                split-GEMM error from the attention core's
 
-    python dev/parity_sweep.py [--seeds 0 1 2] [--variants ref ref_fold] [--out FILE]
+    python tests/diag/parity_sweep.py [--seeds 0 1 2] [--variants ref ref_fold] [--out FILE]
 """
 import argparse
 import json
@@ -17,7 +17,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cmt-cooperative-perception_amd")]
 import torch  # noqa: E402
 

@@ -4,7 +4,7 @@ online f16 cross-attention offsets."""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cmt-cooperative-perception_amd")]
 import torch  # noqa: E402
 

@@ -5,7 +5,7 @@ same state_dict.
 The reference runs its cross-attention core in fp16 (flash-attn: fp16 q/k/v,
 fp16 P, fp16 output) and everything else in fp32.  That fp16 core alone moves
 the head outputs by up to ~1e-3..4e-3 from exact fp32 math on these inputs
-(oracle 'fp16' core vs oracle 'fp32', tools/numerics_report.py), and the fp16
+(oracle 'fp16' core vs oracle 'fp32', tests/diag/numerics_report.py), and the fp16
 rounding of P and of the output depends on flash-attn's tile order, so no
 re-implementation can match it bit-for-bit: two faithful fp16 implementations
 differ by the same order.  Tolerances on cls_logits, dim, rot, vel and on
