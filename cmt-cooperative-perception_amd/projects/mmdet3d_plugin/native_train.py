@@ -2,6 +2,7 @@
 PATH": train.hip, attn_train.hip).  Same contract as native.py: device
 tensors only, the current torch stream, no CPU or eager-PyTorch fallback."""
 import ctypes
+import threading
 
 import torch
 
@@ -39,12 +40,20 @@ def set_train_gemm(mode):
     return old
 
 
+_tls = threading.local()
+
+
 def gemm_ex(A, a_strides, B, b_strides, C, *, M, N_, K, ldc, alpha=1.0, beta=0.0, bias=None, batch=1, a_bs=0,
             b_bs=0, c_bs=0, ksplit=1, a_offset=0, b_offset=0, c_offset=0, mode=None, bias_bs=0, a_rowsum=None):
     """C[z][m][n] = alpha sum_k A(m,k) B(n,k) (+bias) + beta C; strides in elements:
     a_strides = (s_m, s_k), b_strides = (s_n, s_k).  ``mode``: see set_train_gemm."""
     _f32(A, B, C, bias)
-    g = N.GemmExArgs()
+    # one argument struct per thread (the library copies it at the call; autograd runs the
+    # backward on its own thread): no ctypes allocation per launch
+    g = getattr(_tls, "gemm_args", None)
+    if g is None:
+        g = _tls.gemm_args = N.GemmExArgs()
+    g.a_rowsum = None
     g.M, g.N, g.K, g.batch, g.alpha, g.beta = M, N_, K, batch, alpha, beta
     g.A, (g.a_sm, g.a_sk), g.a_bs = A.data_ptr() + 4 * a_offset, a_strides, a_bs
     g.B, (g.b_sn, g.b_sk), g.b_bs = B.data_ptr() + 4 * b_offset, b_strides, b_bs
