@@ -490,6 +490,7 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
     const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
     const float sh = shift ? shift[c] : 0.f;
     float s = 0.f;
+#pragma unroll 8
     for (int r = r0; r < r1; ++r) {
         const float v = X[(int64_t)r * C + c] - sh;
         s += squares ? v * v : v;
@@ -530,6 +531,7 @@ __global__ __launch_bounds__(256) void bn_bwd_sums_kernel(cmt_bn_args a, float* 
     const int r0 = blockIdx.x * rpb, r1 = min(a.rows, r0 + rpb);
     const float mu = a.mean_save[c], rs = a.rstd_save[c];
     float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
     for (int r = r0; r < r1; ++r) {
         const int64_t i = (int64_t)r * a.C + c;
         const float g = a.Y[i] > 0.f ? a.dY[i] : 0.f;
@@ -743,7 +745,7 @@ extern "C" int cmt_bn_relu_train_fwd(const cmt_bn_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     float* sums = (float*)a.workspace;   // [0:C) centred squares, [C:2C) mean
     if (hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s) != hipSuccess) return cmt_fail(CMT_EINVAL, "bn: hipMemsetAsync failed");
-    const int rpb = 256;
+    const int rpb = 64;   // ~500 workgroups over 32 400 rows (256: 127, a serial 256-row loop each)
     dim3 grid(cdiv(a.rows, rpb), cdiv(a.C, 256));
     col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, nullptr, sums + a.C, 0, rpb);
     scale_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(sums + a.C, a.C, 1.f / a.rows);
@@ -760,7 +762,7 @@ extern "C" int cmt_bn_relu_train_bwd(const cmt_bn_args* ap, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     float* sums = (float*)a.workspace;
     if (hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s) != hipSuccess) return cmt_fail(CMT_EINVAL, "bn: hipMemsetAsync failed");
-    const int rpb = 256;
+    const int rpb = 64;   // ~500 workgroups over 32 400 rows (256: 127, a serial 256-row loop each)
     bn_bwd_sums_kernel<<<dim3(cdiv(a.rows, rpb), cdiv(a.C, 256)), 256, 0, s>>>(a, sums, rpb);
     bn_bwd_apply_kernel<<<(unsigned)cdiv64((int64_t)a.rows * a.C, 256), 256, 0, s>>>(a, sums);
     bn_param_grads_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(a, sums);
