@@ -1057,6 +1057,36 @@ __device__ __forceinline__ void pb2_wait(int tiles) {
     else pp_wait_n<0>();
 }
 
+// Segment priorities (dev experiments, CMT_ATTN_EXP build define; 0 in the product build):
+// bit 1: the wave entering a matrix segment raises its issue priority to 2 and drops it to 0
+// at the start of its vector segment, so the partner's exponentials fill the MFMA gaps
+// instead of holding the issue port ahead of the MFMAs; bit 2: half B one level above half A
+// throughout (MI355X_MICROARCH.md 'Two waves per SIMD', items 2 and 4).
+#ifndef CMT_ATTN_EXP
+#define CMT_ATTN_EXP 0
+#endif
+template <int PR>
+__device__ __forceinline__ void set_prio() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(PR);
+    __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void prio_m(bool hb) {
+    if constexpr (CMT_ATTN_EXP & 3) {
+        const int pr = ((CMT_ATTN_EXP & 1) ? 2 : 0) + ((CMT_ATTN_EXP & 2) && hb ? 1 : 0);
+        if (pr == 3) set_prio<3>();
+        else if (pr == 2) set_prio<2>();
+        else if (pr == 1) set_prio<1>();
+        else set_prio<0>();
+    }
+}
+__device__ __forceinline__ void prio_v(bool hb) {
+    if constexpr (CMT_ATTN_EXP & 3) {
+        if ((CMT_ATTN_EXP & 2) && hb) set_prio<1>();
+        else set_prio<0>();
+    }
+}
+
 // US (f16, bounded offsets or not): Q enters the QK^T MFMAs unscaled, exactly the f16 q the
 // reference's flash core multiplies, and the vector segment applies s * c - offset in fp32 (one
 // packed FMA per two scores) -- flash-attn's own order (q k in fp32, then the scale), with half
@@ -1205,6 +1235,7 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
         if (np > 0) {
             if (!hb) pb2_wait(issued - 2);                 // tiles 0, 1 landed
             pp_barrier();
+            prio_m(hb);
             if (!hb) issue_upto(8);
             {
                 const PpLane l = pp_launder(lane_ofs);
@@ -1215,6 +1246,7 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             if (livew) pb_mseg<T, true, false, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
             if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
             pp_barrier();
+            prio_v(hb);
             if (livew) us_scale(s0, fastw);
             if (livew) us_scale(s1, fastw);
             if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, true);
@@ -1227,11 +1259,13 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             }
             for (int j = 1; j < np; ++j) {
                 pp_barrier();
+                prio_m(hb);
                 if (!hb) issue_upto(2 * j + 8);
                 if (livew) pb_mseg<T, true, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);   // QK^T 2j, PV 2j-2
                 if (livew) pb_mseg<T, true, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);   // QK^T 2j+1, PV 2j-1
                 if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
                 pp_barrier();
+                prio_v(hb);
                 if (livew) us_scale(s0, fastw);
                 if (livew) us_scale(s1, fastw);
                 if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, false);
@@ -1242,8 +1276,10 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
                 if (livew) pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
             }
             pp_barrier();
+            prio_m(hb);
             if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
             if (livew) pb_mseg<T, false, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
+            prio_v(false);
         }
         if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
 
@@ -1338,454 +1374,6 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
         }
         if (lh == 0) {
             p.Mp[row] = fast ? off : m_run;   // exp2 units: the offset P was taken against
-            p.Lp[row] = l_tot;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Software-pipelined long-key kernel (the cross-attention shape), f16 with
-// bounded offsets: attn_sp_kernel.
-//
-// attn_pb2_kernel splits a SIMD's two waves into an MFMA-only and a VALU-only
-// role per window, coupled by a barrier per segment; its windows measured
-// ~1.8x the issue bound (profiles/r3x_ref_attn_sq_counters.json).  The
-// co-execution probe (dev/coexec_probe.hip, profiles/r4a_coexec_probe.txt)
-// shows why a single mixed stream per wave is the better shape: an MFMA wave
-// beside an exp-only partner keeps its full rate while the exps run ~12
-// cycles each, and two waves that each interleave ~3 exps per MFMA reach 80 %
-// MFMA-pipe occupancy without any role split.  So here every wave runs the
-// same three-stage pipeline over its split's 64-key tiles:
-//
-//   iteration t:  QK^T of tile t+1 (S[t+1], into the other register set)
-//                 exponentials of tile t (P[t] = exp2(S[t]), f16)
-//                 P.V and row sums of tile t-1 (P[t-1], V[t-1])
-//
-// all three independent of one another inside the iteration, interleaved at
-// ~3 VALU instructions per MFMA (sched_group_barrier).  Bounded offsets as
-// attn_pb2_kernel's f16 path (S starts from -(|q| max|k| - 15), so P <= 2^15;
-// no running max); a wave whose row total shows a too-loose bound re-runs its
-// split with an online max straight from global memory (sp_online_split;
-// never taken on the decoder's data, exercised by the loose-bound tests).
-//
-// K/V tiles arrive by LDS-DMA into an SP_RING-slot ring (wave w copies piece w
-// -- one 16-row quarter of K or V -- of every tile), with one workgroup
-// barrier per tile: after iteration t every wave has finished reading tile t-1
-// (its V, the last use), whose slot then takes tile t + SP_RING - 1.
-// ---------------------------------------------------------------------------
-constexpr int SP_RING = 10;
-
-// sched_group_barrier masks (LLVM AMDGPU SchedGroupMask)
-constexpr int SG_VALU = 0x002, SG_MFMA = 0x008, SG_DS_READ = 0x100, SG_TRANS = 0x400;
-
-// one-wave online-max pass over keys [key0, key1) straight from global memory
-// (the loose-bound fallback): O, row total and offset (exp2 units) of the wave's 32 queries
-template <bool QS>
-__device__ __forceinline__ void sp_online_split(const AttnKParams& p, const f16_t* Kb, const f16_t* Vb, int key0,
-                                             int key1, const f16x8 (&qf)[2], const f16x8 (&ql)[2], f32x16& o,
-                                             float& l_tot, float& m_out, int lane) {
-    const int lr = lane & 31, lh = lane >> 5;
-    float m = -__builtin_inff(), l = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    for (int k0 = key0; k0 < key1; k0 += 32) {
-        const int kr = min(k0 + lr, p.Nk - 1);
-        const f16x8 k0f = *(const f16x8*)(Kb + (int64_t)kr * p.k_rs + 8 * lh);
-        const f16x8 k1f = *(const f16x8*)(Kb + (int64_t)kr * p.k_rs + 16 + 8 * lh);
-        f32x16 s = {};
-        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0f, qf[0], s, 0, 0, 0);
-        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1f, qf[1], s, 0, 0, 0);
-        if constexpr (QS) {
-            s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0f, ql[0], s, 0, 0, 0);
-            s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1f, ql[1], s, 0, 0, 0);
-        }
-        float mt = -__builtin_inff();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = k0 + 8 * (r >> 2) + 4 * lh + (r & 3);
-            if (key >= key1) s[r] = -__builtin_inff();
-            mt = vmax(mt, s[r]);
-        }
-        mt = pair_max(mt);
-        const float mn = vmax(m, mt);   // finite: every block holds at least one key of the range
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first block -> 0
-        o *= alpha;
-        l *= alpha;
-        m = mn;
-        f16x8 pf[2];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(s[r] - m);
-            l += pv;
-            pf[r >> 3][r & 7] = (f16_t)pv;
-        }
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-            // V^T fragment: lane (d = lr, lh) element j <-> key 16 ss + 8 (j >> 2) + 4 lh + (j & 3)
-            f16x8 vf;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int key = min(k0 + 16 * ss + 8 * (j >> 2) + 4 * lh + (j & 3), p.Nk - 1);
-                vf[j] = Vb[(int64_t)key * p.v_rs + lr];
-            }
-            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[ss], o, 0, 0, 0);
-        }
-    }
-    l_tot = pair_sum(l);
-    m_out = m;
-}
-
-// BAR2: one workgroup barrier per two tiles (the steady loop's pairs) instead of per tile;
-// PRIO: s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md 'Two waves per SIMD', item 4).
-// (Running waves 4-7 half an iteration behind -- the halves below allow it -- needs a second
-// copy of the loop whose live ranges spill: 256 VGPRs + 170 spilled; not kept.)
-// NOSYNC (diagnostic only, CMT_ATTN_SP bit 16, wrong results): no barrier and no LDS-DMA after
-// the prologue -- the compute stream alone, on whatever the ring holds
-template <bool QS, bool BAR2, bool PRIO, bool NOSYNC = false>
-__global__ __launch_bounds__(512, 2) void attn_sp_kernel(AttnKParams p) {
-    typedef f16x8 frag;
-    constexpr int STAGE = 2 * KT * D;                  // f16 elements per ring slot: K tile then V tile
-    constexpr int STAGE_B = STAGE * 2, KV_B = KT * D * 2;
-    __shared__ __attribute__((aligned(16))) f16_t ring[SP_RING * STAGE];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lr = lane & 31, lh = lane >> 5;
-
-    // XCD-aware block order (as attn_pb2_kernel): the query blocks of one (b, h, split) on one XCD
-    const int nwg = gridDim.x;
-    const int orig = blockIdx.x;
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int qb = wg % p.nqb;
-    const int rest = wg / p.nqb;
-    const int BH = p.B * p.H;
-    const int bh = rest % BH;
-    const int split = rest / BH;
-    const int b = bh / p.H;
-    const int h = bh - b * p.H;
-
-    const bool live = qb * (8 * QW) + wave * QW < p.Nq;
-    const f16_t* Qb = (const f16_t*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
-    const f16_t* Kb = (const f16_t*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
-    const f16_t* Vb = (const f16_t*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
-    const float c = p.c;
-
-    const int ntiles = (p.Nk + KT - 1) / KT;
-    const int t_begin = split * p.tiles_per_split;
-    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
-    const int nt = max(0, t_end - t_begin);
-    const bool ragged = (p.Nk % KT) != 0 && t_end == ntiles;   // this split's last tile is the ragged one
-
-    // ---- LDS-DMA: wave w copies piece w (K rows 16 (w & 3) .. +15 for w < 4, else V) of every tile
-    const int crow = lane >> 2, cch = lane & 3;
-    const int prow = (wave & 3) * 16 + crow;
-    const bool isk = wave < 4;
-    const f16_t* const dsrc = isk ? Kb + 8 * (cch ^ ((prow >> 2) & 3)) : Vb + 8 * cch;
-    const int64_t drs = isk ? p.k_rs : p.v_rs;
-    f16_t* const ddst = ring + (isk ? 0 : KT * D) + (wave & 3) * 16 * D;
-    // tiles are issued in order: the source advances by one tile per issue (no per-issue
-    // multiply); only the ragged last tile clamps its rows (masked in compute)
-    const f16_t* dcur = dsrc + (int64_t)(t_begin * KT + prow) * drs;
-    const int64_t dstep = (int64_t)KT * drs;
-    auto issue = [&](int i, int slot) {   // split-local tile i into ring slot `slot`
-        const f16_t* src = dcur;
-        if ((t_begin + i + 1) * KT > p.Nk) src = dsrc + (int64_t)min((t_begin + i) * KT + prow, p.Nk - 1) * drs;
-        dma16(src, ddst + slot * STAGE);
-        dcur += dstep;
-    };
-    const int npre = min(nt, SP_RING - 1);
-    for (int i = 0; i < npre; ++i) issue(i, i);
-
-    // ---- Q^T fragments with the folded scale (s in exp2 units); QS keeps q * c as hi + lo
-    const int q = qb * (8 * QW) + wave * QW + lr;
-    const int qc = q < p.Nq ? q : p.Nq - 1;
-    frag qf[2], ql[2];
-    float qq = 0.f;
-    {
-        const frag r0 = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-        const frag r1 = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float x0 = (float)r0[j] * c, x1 = (float)r1[j] * c;
-            qf[0][j] = (f16_t)x0;
-            qf[1][j] = (f16_t)x1;
-            ql[0][j] = (f16_t)(x0 - (float)qf[0][j]);
-            ql[1][j] = (f16_t)(x1 - (float)qf[1][j]);
-            const float e0 = QS ? x0 : (float)qf[0][j], e1 = QS ? x1 : (float)qf[1][j];
-            qq += e0 * e0 + e1 * e1;
-        }
-    }
-    // ---- bounded offset: every score of this split <= |q| max|k| (Cauchy-Schwarz); P <= 2^15
-    const float km = kmax_reduce(p, b, h, split, lane);
-    const float off = sqrtf(pair_sum(qq) * km) * 1.001f + 1e-6f - kF16Top;
-    f32x16 sinit;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sinit[r] = -off;
-
-    const char* const rb = (const char*)ring;
-    const PpLane lane_ofs = pp_lane(lane, 2);
-    f32x16 S[2][2];        // [parity of the tile][kb]: S^T = K Q^T - off
-    frag P[2][2][2];       // [parity][kb][ss]: P^T fragments (f16)
-    frag kf[2][2], vf[2][2][2];   // vf[parity of the tile]: V is read one iteration ahead
-    f32x16 o;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
-
-    // tiles still allowed in flight (this wave's pieces) behind tile `need`, given the last issued
-    auto wait_tile = [&](int need, int last_issued) {
-        const int n = last_issued - need;
-        if (n >= 6) pp_wait_n<6>();
-        else if (n == 5) pp_wait_n<5>();
-        else if (n == 4) pp_wait_n<4>();
-        else if (n == 3) pp_wait_n<3>();
-        else if (n == 2) pp_wait_n<2>();
-        else if (n == 1) pp_wait_n<1>();
-        else pp_wait_n<0>();
-    };
-    int last_issued = npre - 1;
-
-    auto qk = [&](f32x16 (&s)[2]) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][0], qf[0], sinit, 0, 0, 0);
-            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][1], qf[1], s[kb], 0, 0, 0);
-            if constexpr (QS) {
-                s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][0], ql[0], s[kb], 0, 0, 0);
-                s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][1], ql[1], s[kb], 0, 0, 0);
-            }
-        }
-    };
-    auto ex = [&](const f32x16 (&s)[2], frag (&pf)[2][2]) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) pf[kb][r >> 3][r & 7] = (f16_t)__builtin_amdgcn_exp2f(s[kb][r]);
-    };
-    auto pv = [&](const frag (&pf)[2][2], const frag (&vv)[2][2]) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv[kb][ss], pf[kb][ss], o, 0, 0, 0);
-                lsum = rs16_mma<f16_t>(pf[kb][ss], lsum, lane);
-            }
-    };
-    auto slot_of = [&](int i) { return rb + (i % SP_RING) * STAGE_B; };
-    // end of iteration t: tile t+2 landed for everyone, every wave done with tile t-1's slot,
-    // which then takes tile t + SP_RING - 1
-    auto sync = [&](int t) {
-        if constexpr (NOSYNC) return;
-        if (t + 2 < nt) wait_tile(t + 2, last_issued);
-        barrier_mem();
-        if (t + SP_RING - 1 < nt) {
-            issue(t + SP_RING - 1, (t + SP_RING - 1) % SP_RING);
-            last_issued = t + SP_RING - 1;
-        }
-    };
-    // one pipeline iteration t (parity PAR): QK^T(t+1) if QKN, exp(t), PV(t-1) if PVP.  The
-    // steady-state form (QKN and PVP) is written slot by slot: slot i = one MFMA, then the two
-    // exponentials of score pair i and the f16 pack of pair i-1, fenced by sched_barrier so the
-    // compiler keeps this order (left alone it clusters the exponentials ahead of the MFMAs).
-    // MFMA order: the four row sums of P[t-1], then P[t-1] V[t-1] (V read one iteration ahead),
-    // then the QK^T chains of tile t+1, whose K fragments (read at the top of the iteration) get
-    // eight slots to land.  It is written as two halves (slots [0, NM/2)
-    // with the fragment reads first, then [NM/2, NM) and the last pack).
-    float ea = 0.f, eb = 0.f;   // the exponentials of the pending pack (the previous pair) between slots
-    auto half = [&](auto par, auto hf, int t) {
-        constexpr int PAR = decltype(par)::value, HF = decltype(hf)::value;
-        constexpr int NM = QS ? 16 : 12;                      // MFMAs of the iteration
-        f32x16(&sn)[2] = S[PAR ^ 1];
-        const f32x16(&sc)[2] = S[PAR];
-        frag(&pn)[2][2] = P[PAR];
-        const frag(&pp)[2][2] = P[PAR ^ 1];
-        const frag(&vp)[2][2] = vf[PAR ^ 1];                 // V[t-1], read in iteration t-1
-        if constexpr (HF == 0) {
-            const PpLane l = pp_launder(lane_ofs);
-            pp_load_k<f16_t>(slot_of(t + 1), l, kf);
-            pp_load_v<f16_t>(slot_of(t) + KV_B, l, vf[PAR]);   // V[t] for the next iteration
-        }
-        auto mfma = [&](int i) {
-            if (i < 4) {                                      // row sums of P[t-1]
-                lsum = rs16_mma<f16_t>(pp[i >> 1][i & 1], lsum, lane);
-            } else if (i < 8) {                               // P[t-1] V[t-1] (registers since the last iteration)
-                const int j = i - 4;
-                o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vp[j >> 1][j & 1], pp[j >> 1][j & 1], o, 0, 0, 0);
-            } else {                                          // QK^T(t+1): per kb 2 (fold) or 4 (QS) MFMAs
-                const int j = i - 8, per = QS ? 4 : 2, kb = j / per, k = j % per;
-                const frag& qop = (k >> 1) ? ql[k & 1] : qf[k & 1];
-                sn[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kb][k & 1], qop, k == 0 ? sinit : sn[kb], 0, 0, 0);
-            }
-        };
-        // score pair m (0..15): s[kb][r], s[kb][r + 1] with kb = m >> 3, r = 2 (m & 7).  The
-        // exponentials are volatile asm (they cannot be hoisted above their slot); the packs are
-        // laundered (they cannot sink below it); sched_barrier keeps the slots apart.
-        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-        auto pack = [&](int m) {
-            h2 v = {(f16_t)ea, (f16_t)eb};
-            asm volatile("" : "+v"(v));
-            const int kb = m >> 3, r = 2 * (m & 7);
-            pn[kb][r >> 3][r & 7] = v[0];
-            pn[kb][r >> 3][(r & 7) + 1] = v[1];
-        };
-#pragma unroll
-        for (int i = HF * NM / 2; i < (HF + 1) * NM / 2; ++i) {
-            mfma(i);
-            const int m0 = i * 16 / NM, m1 = (i + 1) * 16 / NM;
-#pragma unroll
-            for (int m = m0; m < m1; ++m) {
-                const int kb = m >> 3, r = 2 * (m & 7);
-                // (an MFMA result of the previous iteration: the VALU read-after-MFMA wait
-                // states are long covered by the sync in between)
-                float na, nb;
-                asm volatile("v_exp_f32 %0, %1" : "=v"(na) : "v"(sc[kb][r]));
-                asm volatile("v_exp_f32 %0, %1" : "=v"(nb) : "v"(sc[kb][r + 1]));
-                if (m > 0) pack(m - 1);
-                ea = na;
-                eb = nb;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (HF == 1) pack(15);
-    };
-    auto iter = [&](auto par, auto qkn, auto pvp, int t, bool mask_t) {
-        constexpr int PAR = decltype(par)::value;
-        constexpr bool QKN = decltype(qkn)::value, PVP = decltype(pvp)::value;
-        if constexpr (QKN && PVP) {
-            half(par, std::integral_constant<int, 0>{}, t);
-            half(par, std::integral_constant<int, 1>{}, t);
-        } else {
-            {
-                const PpLane l = pp_launder(lane_ofs);
-                if constexpr (QKN) pp_load_k<f16_t>(slot_of(t + 1), l, kf);
-                pp_load_v<f16_t>(slot_of(t) + KV_B, l, vf[PAR]);   // V[t] for the next iteration / the drain
-            }
-            if (mask_t) {   // the ragged last tile of the last split: keys >= Nk score -inf
-                const int key0 = (t_begin + t) * KT;
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (key0 + kb * 32 + 8 * (r >> 2) + 4 * lh + (r & 3) >= p.Nk)
-                            S[PAR][kb][r] = -__builtin_inff();
-            }
-            ex(S[PAR], P[PAR]);
-            if constexpr (QKN) qk(S[PAR ^ 1]);
-            if constexpr (PVP) pv(P[PAR ^ 1], vf[PAR ^ 1]);
-        }
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using BT = std::true_type;
-    using BF = std::false_type;
-
-    // BAR2: after iteration 0, tiles up to 3 landed (the first pair reads K(2), K(3))
-    auto sync_first = [&]() {
-        const int need = min(3, nt - 1);
-        if (need > 1) wait_tile(need, last_issued);
-        barrier_mem();
-        if (SP_RING - 1 < nt) {
-            issue(SP_RING - 1, SP_RING - 1);
-            last_issued = SP_RING - 1;
-        }
-    };
-    // BAR2: after the pair of iterations t, t+1 -- tiles up to t+4 landed (the next pair reads
-    // K(t+3), K(t+4)); tiles t-1 and t (their V read by the pair) free for tiles t+R-1, t+R
-    auto sync2 = [&](int t) {
-        const int need = min(t + 4, nt - 1);
-        if (need > t + 1) wait_tile(need, last_issued);
-        barrier_mem();
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int ti = t + SP_RING - 1 + k;
-            if (ti < nt) {
-                issue(ti, ti % SP_RING);
-                last_issued = ti;
-            }
-        }
-    };
-
-    // control flow (barriers, LDS-DMA duty) is the same for every wave; a padding wave (its 32
-    // queries past Nq) skips the compute
-    if (nt > 0) {
-        // prologue: QK^T of tile 0
-        wait_tile(1 < nt ? 1 : 0, last_issued);
-        barrier_mem();
-        if (live) {
-            const PpLane l = pp_launder(lane_ofs);
-            pp_load_k<f16_t>(slot_of(0), l, kf);
-            qk(S[0]);
-        }
-        if constexpr (PRIO) {
-            if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-        }
-        if (nt == 1) {
-            if (live) iter(I0{}, BF{}, BF{}, 0, ragged);
-        } else {
-            if (live) iter(I0{}, BT{}, BF{}, 0, false);
-            if constexpr (BAR2) sync_first();
-            else sync(0);
-            int t = 1;
-            {
-                for (; t + 2 < nt; t += 2) {   // iterations t (odd) and t + 1 (even), both < nt - 1
-                    if (live) iter(I1{}, BT{}, BT{}, t, false);
-                    if constexpr (!BAR2) sync(t);
-                    if (live) iter(I0{}, BT{}, BT{}, t + 1, false);
-                    if constexpr (BAR2) sync2(t);
-                    else sync(t + 1);
-                }
-                if (t < nt - 1) {              // one more middle iteration (odd t)
-                    if (live) iter(I1{}, BT{}, BT{}, t, false);
-                    sync(t);
-                    ++t;
-                }
-            }
-            // last tile: exp (masked if ragged) and the previous tile's PV
-            if (live) {
-                if (t & 1) iter(I1{}, BF{}, BT{}, t, ragged);
-                else iter(I0{}, BF{}, BT{}, t, ragged);
-            }
-        }
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-        // drain: PV of the last tile (its V read by the last iteration)
-        if (live) {
-            if ((nt - 1) & 1) pv(P[1], vf[1]);
-            else pv(P[0], vf[0]);
-        }
-    }
-    float l_tot = rs16_total(lsum, lane);
-    float m_fin = off;
-    // a loose bound left some row's P too small for full f16 precision: this wave re-runs its
-    // split with the online max (global loads; no LDS, no barrier)
-    if (live && nt > 0 && __any(!(l_tot >= kF16MinSum))) {
-        sp_online_split<QS>(p, Kb, Vb, t_begin * KT, min(p.Nk, t_end * KT), qf, ql, o, l_tot, m_fin, lane);
-    }
-
-    // ---- write
-    if (q >= p.Nq) return;
-    if (p.splits == 1) {
-        const float inv = 1.f / l_tot;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-            if (p.round_out) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (float)(f16_t)v[j];
-            }
-            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
-        }
-    } else {
-        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
-        float* dst = p.Op + row * D;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
-        }
-        if (lh == 0) {
-            p.Mp[row] = m_fin;   // exp2 units: the offset P was taken against
             p.Lp[row] = l_tot;
         }
     }
@@ -2002,28 +1590,9 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
 // self-attention) the in-workgroup key split attn_kw_kernel; anything else the
 // 4-wave single-phase attn_fwd_kernel with split partials.  f32 always takes
 // the exact-f32 kernel.
-// f16 bounded long-key path: CMT_ATTN_SP = 0 (default) -> attn_pb2_kernel; otherwise
-// attn_sp_kernel with the variant bits 2 (one barrier per two tiles) and 4 (s_setprio 1 for
-// waves 4-7).  The per-call flags CMT_ATTN_FORCE_PINGPONG / _PIPELINED override it.
-int sp_mode(int flags) {
-    static const int m = [] {
-        const char* e = std::getenv("CMT_ATTN_SP");
-        return e && e[0] >= '0' && e[0] <= '9' ? std::atoi(e) : 0;
-    }();
-    if (flags & CMT_ATTN_FORCE_PINGPONG) return 0;
-    if (flags & CMT_ATTN_FORCE_PIPELINED) return m != 0 ? m : 1;
-    return m;
-}
-
-// the reference-numerics f16 core (no fold permission): CMT_ATTN_US = 1 (default 0) or the
-// per-call CMT_ATTN_UNSCALED_Q flag -> unscaled Q (attn_pb2_kernel US); else Q * c as hi + lo (QS)
-bool us_mode(int flags) {
-    static const int m = [] {
-        const char* e = std::getenv("CMT_ATTN_US");
-        return e && e[0] >= '0' && e[0] <= '9' ? std::atoi(e) : 0;
-    }();
-    return (flags & CMT_ATTN_UNSCALED_Q) != 0 || m != 0;
-}
+// the reference-numerics f16 core (no fold permission): the per-call CMT_ATTN_UNSCALED_Q flag ->
+// unscaled Q (attn_pb2_kernel US); else Q * c as hi + lo (QS)
+bool us_mode(int flags) { return (flags & CMT_ATTN_UNSCALED_Q) != 0; }
 
 bool use_long(const cmt_attn_args& a) {
     return a.dtype != CMT_F32 && a.dtype != CMT_F16P && a.Nk >= 4096 && a.Nq > 128;
@@ -2143,21 +1712,7 @@ int attn_fwd_impl(const cmt_attn_args& a, float* lse, void* stream) {
     } else if (use_long(a)) {
         // the scale is folded into Q either way; without the FOLD permission q * c is kept as hi + lo
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
-        const int spm = lse ? 0 : sp_mode(a.flags);   // the row statistic: ping-pong kernel
-        if (a.dtype == CMT_F16 && a.kmax2 != nullptr && spm != 0) {
-            // f16 with bounded offsets: the software-pipelined single-stream kernel
-#define SPK(QS, B2, PR) attn_sp_kernel<QS, B2, PR><<<nwg, 512, 0, s>>>(p)
-            const bool b2 = (spm & 2) != 0, pr = (spm & 4) != 0;
-            if (spm & 16) attn_sp_kernel<true, false, false, true><<<nwg, 512, 0, s>>>(p);   // diagnostic
-            else if (fold) {
-                if (b2) { if (pr) SPK(false, true, true); else SPK(false, true, false); }
-                else { if (pr) SPK(false, false, true); else SPK(false, false, false); }
-            } else {
-                if (b2) { if (pr) SPK(true, true, true); else SPK(true, true, false); }
-                else { if (pr) SPK(true, false, true); else SPK(true, false, false); }
-            }
-#undef SPK
-        } else if (a.dtype == CMT_F16) {
+        if (a.dtype == CMT_F16) {
             if (fold) attn_pb2_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
             else if (us_mode(a.flags)) attn_pb2_kernel<f16_t, false, true><<<nwg, 512, 0, s>>>(p);
             else attn_pb2_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);

@@ -1026,11 +1026,7 @@ int check_args(const cmt_attn_train_args& a, const char* who) {
 
 // ---- the long-key fp16 path: applicability and workspace layout
 bool fast_path(const cmt_attn_train_args& a) {
-    static const bool off = [] {
-        const char* e = std::getenv("CMT_TRAIN_ATTN_FAST");
-        return e && e[0] == '0';
-    }();
-    return !off && a.fp16_inputs && a.dn_pad <= 0 && !(a.dropout_p > 0.f) && a.Nk >= 4096 && a.Nq > 128 &&
+    return a.fp16_inputs && a.dn_pad <= 0 && !(a.dropout_p > 0.f) && a.Nk >= 4096 && a.Nq > 128 &&
            a.Nq <= NQ_RES && a.o_hs == D && a.kv_splits <= 0;
 }
 
@@ -1080,7 +1076,9 @@ extern "C" int cmt_attn_train_fwd(const cmt_attn_train_args* ap, void* stream) {
     CMT_REQUIRE(ap != nullptr, "cmt_attn_train_fwd: null args");
     if (int rc = check_args(*ap, "cmt_attn_train_fwd")) return rc;
     const int splits = train_splits(*ap);
-    if (splits > 1 && (ap->workspace == nullptr || ap->workspace_bytes < cmt_attn_train_workspace_bytes(ap)))
+    // the long-key f16 path always writes its f16 copies into the workspace (also at one split)
+    if ((splits > 1 || fast_path(*ap)) &&
+        (ap->workspace == nullptr || ap->workspace_bytes < cmt_attn_train_workspace_bytes(ap)))
         return cmt_fail(CMT_EWORKSPACE, "cmt_attn_train_fwd: workspace too small");
     AP p = make_ap(*ap, splits);
     hipStream_t s = (hipStream_t)stream;

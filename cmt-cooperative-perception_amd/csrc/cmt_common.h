@@ -134,3 +134,11 @@ int cmt_attn_fwd_lse(const cmt_attn_args& a, float* lse, void* stream);
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// f16-operand range guard (ABI 18): an fp32 value the f16 / f16-pair operand formats cannot
+// carry -- non-finite, or |x| >= 65520 where the f16 (hi) rounding overflows.  A kernel that
+// sees one ORs 1 into the caller's flag word with a vector atomic (rare path only).
+__device__ __forceinline__ bool f16_unrepresentable(float x) { return !(__builtin_fabsf(x) < 65520.f); }
+__device__ __forceinline__ void raise_range_flag(int* flag, bool bad) {
+    if (flag != nullptr && bad) __hip_atomic_fetch_or(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

@@ -423,17 +423,20 @@ __global__ void masked_view_sum_ex_kernel(const float* __restrict__ X, const flo
 template <typename TO, bool PAIR = false>
 __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restrict__ X, int nv, int C, int HW,
                                                            TO* Y, int64_t ldy, int64_t rows_per_batch,
-                                                           int64_t row_offset) {
+                                                           int64_t row_offset, int* range_flag) {
     __shared__ float tile[64][65];
     const int img = blockIdx.z;
     const int c0 = blockIdx.y * 64;
     const int p0 = blockIdx.x * 64;
     const float* xs = X + (int64_t)img * C * HW;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    bool bad = false;
     for (int i = ty; i < 64; i += 4) {
         const int c = c0 + i, p = p0 + tx;
         tile[i][tx] = (c < C && p < HW) ? xs[(int64_t)c * HW + p] : 0.f;
+        bad |= f16_unrepresentable(tile[i][tx]);
     }
+    if constexpr (PAIR || std::is_same<TO, f16_t>::value) raise_range_flag(range_flag, bad);
     __syncthreads();
     const int bo = img / nv, v = img - bo * nv;
     for (int i = ty; i < 64; i += 4) {
@@ -455,7 +458,7 @@ __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restri
 template <typename TO, bool PAIR = false>
 __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __restrict__ X, int nv, int C, int HW,
                                                                TO* Y, int64_t ldy, int64_t rows_per_batch,
-                                                               int64_t row_offset) {
+                                                               int64_t row_offset, int* range_flag) {
     constexpr int VW = 16 / sizeof(TO);          // channels per 16-byte store
     constexpr int TPP = 64 / VW;                 // threads per pixel
     __shared__ float tile[64][65];
@@ -472,10 +475,15 @@ __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __re
             const int c = c0 + cr + 16 * k, p = p0 + q;
             v[k] = p < HW ? *(const f32x4*)(xs + (int64_t)c * HW + p) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        bool bad = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) tile[cr + 16 * k][q + e] = v[k][e];
+            for (int e = 0; e < 4; ++e) {
+                tile[cr + 16 * k][q + e] = v[k][e];
+                bad |= f16_unrepresentable(v[k][e]);
+            }
+        if constexpr (PAIR || std::is_same<TO, f16_t>::value) raise_range_flag(range_flag, bad);
     }
     __syncthreads();
     const int bo = img / nv, v = img - bo * nv;
@@ -860,8 +868,16 @@ extern "C" int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, 
     return cmt_check_launch("cmt_masked_view_sum_ex");
 }
 
+extern "C" int cmt_nchw_to_rows_ex(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype, int64_t ldy,
+                                   int64_t rows_per_batch, int64_t row_offset, int* range_flag, void* stream);
+
 extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype, int64_t ldy,
                                 int64_t rows_per_batch, int64_t row_offset, void* stream) {
+    return cmt_nchw_to_rows_ex(X, nb, nv, C, HW, Y, ydtype, ldy, rows_per_batch, row_offset, nullptr, stream);
+}
+
+extern "C" int cmt_nchw_to_rows_ex(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype, int64_t ldy,
+                                   int64_t rows_per_batch, int64_t row_offset, int* range_flag, void* stream) {
     CMT_REQUIRE(X && Y && nb > 0 && nv > 0 && C > 0 && HW > 0, "cmt_nchw_to_rows: bad arguments");
     dim3 grid(cdiv(HW, 64), cdiv(C, 64), nb * nv);
     hipStream_t s = (hipStream_t)stream;
@@ -870,31 +886,31 @@ extern "C" int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, v
         CMT_REQUIRE(ldy == 2 * C, "cmt_nchw_to_rows: f16-pair rows need ldy == 2C (hi row, then lo row)");
         if (HW % 4 == 0 && C % 64 == 0 && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0)
             nchw_to_rows_vec_kernel<pair_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (pair_t*)Y, ldy, rows_per_batch,
-                                                                       row_offset);
+                                                                       row_offset, range_flag);
         else
             nchw_to_rows_kernel<pair_t, true><<<grid, 256, 0, s>>>(X, nv, C, HW, (pair_t*)Y, ldy, rows_per_batch,
-                                                                   row_offset);
+                                                                   row_offset, range_flag);
         return cmt_check_launch("cmt_nchw_to_rows");
     }
     if (HW % 4 == 0 && C % 64 == 0 && (ldy * esz) % 16 == 0 && (uintptr_t)Y % 16 == 0 && (uintptr_t)X % 16 == 0 &&
         (ydtype == CMT_F32 || ydtype == CMT_F16 || ydtype == CMT_BF16)) {
         if (ydtype == CMT_F32)
             nchw_to_rows_vec_kernel<float><<<grid, 256, 0, s>>>(X, nv, C, HW, (float*)Y, ldy, rows_per_batch,
-                                                                row_offset);
+                                                                row_offset, range_flag);
         else if (ydtype == CMT_F16)
             nchw_to_rows_vec_kernel<f16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (f16_t*)Y, ldy, rows_per_batch,
-                                                                row_offset);
+                                                                row_offset, range_flag);
         else
             nchw_to_rows_vec_kernel<bf16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch,
-                                                                 row_offset);
+                                                                 row_offset, range_flag);
         return cmt_check_launch("cmt_nchw_to_rows");
     }
     if (ydtype == CMT_F32)
-        nchw_to_rows_kernel<float><<<grid, 256, 0, s>>>(X, nv, C, HW, (float*)Y, ldy, rows_per_batch, row_offset);
+        nchw_to_rows_kernel<float><<<grid, 256, 0, s>>>(X, nv, C, HW, (float*)Y, ldy, rows_per_batch, row_offset, range_flag);
     else if (ydtype == CMT_F16)
-        nchw_to_rows_kernel<f16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (f16_t*)Y, ldy, rows_per_batch, row_offset);
+        nchw_to_rows_kernel<f16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (f16_t*)Y, ldy, rows_per_batch, row_offset, range_flag);
     else if (ydtype == CMT_BF16)
-        nchw_to_rows_kernel<bf16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch, row_offset);
+        nchw_to_rows_kernel<bf16_t><<<grid, 256, 0, s>>>(X, nv, C, HW, (bf16_t*)Y, ldy, rows_per_batch, row_offset, range_flag);
     else
         return cmt_fail(CMT_EINVAL, "cmt_nchw_to_rows: bad ydtype");
     return cmt_check_launch("cmt_nchw_to_rows");

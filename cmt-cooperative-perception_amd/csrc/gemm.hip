@@ -19,6 +19,12 @@
 
 #include <cstdlib>
 
+// conv_halo_x3_kernel's variant bits for dev experiments (dev/build_exp.sh -DCMT_CONV_VAR=n); the
+// product build compiles variant 0 only
+#ifndef CMT_CONV_VAR
+#define CMT_CONV_VAR 0
+#endif
+
 namespace {
 
 constexpr int BK = 32;
@@ -875,6 +881,10 @@ __device__ __forceinline__ void x3_epilogue(const cmt_gemm_args& a, f32x16 (&acc
     char* Cz = (char*)a.C + (int64_t)z * a.c_bstride * esz;
     const float* biasz = a.bias ? a.bias + (int64_t)z * a.bias_bstride : nullptr;
     const char* Rz = a.R ? (const char*)a.R + (int64_t)z * a.r_bstride * (a.r_dtype == CMT_F32 ? 4 : 2) : nullptr;
+    // range guard (a.range_flag): a pre-activation value outside the f16 pair format means a
+    // non-finite or too large input element reached this tile (0 x inf is NaN, so every output
+    // of its 3x3 neighbourhood shows it), or the output itself cannot be carried as a pair
+    bool bad = false;
     f32x4 bv[TN][4];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
@@ -894,11 +904,17 @@ __device__ __forceinline__ void x3_epilogue(const cmt_gemm_args& a, f32x16 (&acc
                 const f32x4 r = Rz ? load4(Rz, (int64_t)m * a.ldr + n, a.r_dtype, a.N) : f32x4{0.f, 0.f, 0.f, 0.f};
                 if (a.relu) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[tm][tn][4 * g + j] = fmaxf(acc[tm][tn][4 * g + j] + bv[tn][g][j], 0.f) + r[j];
+                    for (int j = 0; j < 4; ++j) {
+                        const float t = acc[tm][tn][4 * g + j] + bv[tn][g][j];
+                        bad |= f16_unrepresentable(t);
+                        acc[tm][tn][4 * g + j] = fmaxf(t, 0.f) + r[j];
+                    }
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                    for (int j = 0; j < 4; ++j) {
+                        acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                        bad |= f16_unrepresentable(acc[tm][tn][4 * g + j]);
+                    }
                 }
             }
     }
@@ -921,10 +937,15 @@ __device__ __forceinline__ void x3_epilogue(const cmt_gemm_args& a, f32x16 (&acc
                     const int n = n0 + wn * (BN / WNW) + tn * 32 + 8 * g + 4 * lh;
                     const f32x4 pv = *(const f32x4*)((const float*)a.A2 + (int64_t)m * a.lda2 + n);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += pv[j];
+                    for (int j = 0; j < 4; ++j) {
+                        acc[tm][tn][4 * g + j] += pv[j];
+                        bad |= f16_unrepresentable(acc[tm][tn][4 * g + j]);
+                    }
                 }
         }
+        raise_range_flag(a.range_flag, bad);
     }
+    if (!two) raise_range_flag(a.range_flag, bad);
     for (int pass = 0; pass < npass; ++pass) {
         barrier_mem();                                        // every wave is done with the ring / last pass
 #pragma unroll
@@ -1409,21 +1430,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.conv_h * a.conv_w, HaloConv::BM), tn = a.N / HaloConv::BN;
     const unsigned nwg = (unsigned)((int64_t)tm * tn * a.batch);
-    static const int env_var = [] {
-        const char* e = getenv("CMT_CONV_VAR");
-        return e ? atoi(e) : 0;
-    }();
-    const int var = env_var;
-    switch (var) {   // CMT_CONV_VAR (conv_halo_x3_kernel's VAR bits); 4 / 8: diagnostics
-        case 1: conv_halo_x3_kernel<1><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 2: conv_halo_x3_kernel<2><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 4: conv_halo_x3_kernel<4><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 8: conv_halo_x3_kernel<8><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 12: conv_halo_x3_kernel<12><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 16: conv_halo_x3_kernel<16><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        case 17: conv_halo_x3_kernel<17><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-        default: conv_halo_x3_kernel<0><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn); break;
-    }
+    conv_halo_x3_kernel<CMT_CONV_VAR><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
     return cmt_check_launch("cmt_gemm");
 }
 

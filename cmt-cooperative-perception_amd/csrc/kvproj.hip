@@ -28,6 +28,12 @@
 // squared-norm reduction is one permlane32 swap.
 #include "cmt_common.h"
 
+// kvproj_x3_kernel's schedule bits for dev experiments (dev/build_exp.sh -DCMT_KV_SCHED=n); the
+// product build compiles schedule 0 only
+#ifndef CMT_KV_SCHED
+#define CMT_KV_SCHED 0
+#endif
+
 namespace {
 
 constexpr int KP_BM = 128;            // token rows per workgroup
@@ -492,25 +498,8 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                     "cmt_kv_proj: 16-byte aligned operands");
         const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts);
         hipStream_t s3 = (hipStream_t)stream;
-        static const int sched = [] {
-            const char* e = getenv("CMT_KV_SCHED");
-            return e ? atoi(e) : 0;
-        }();
         if (a.c_dtype == CMT_F16) {
-            switch (sched) {   // CMT_KV_SCHED (kvproj_x3_kernel's SCHED bits); 4 / 8: diagnostics
-                case 1: kvproj_x3_kernel<f16_t, 1><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 64: kvproj_x3_kernel<f16_t, 64><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 16: kvproj_x3_kernel<f16_t, 16><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 32: kvproj_x3_kernel<f16_t, 32><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 48: kvproj_x3_kernel<f16_t, 48><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 60: kvproj_x3_kernel<f16_t, 60><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 2: kvproj_x3_kernel<f16_t, 2><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 3: kvproj_x3_kernel<f16_t, 3><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 5: kvproj_x3_kernel<f16_t, 5><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 9: kvproj_x3_kernel<f16_t, 9><<<g3, 512, 0, s3>>>(a, parts); break;
-                case 13: kvproj_x3_kernel<f16_t, 13><<<g3, 512, 0, s3>>>(a, parts); break;
-                default: kvproj_x3_kernel<f16_t, 0><<<g3, 512, 0, s3>>>(a, parts); break;
-            }
+            kvproj_x3_kernel<f16_t, CMT_KV_SCHED><<<g3, 512, 0, s3>>>(a, parts);
         } else {
             kvproj_x3_kernel<bf16_t, 0><<<g3, 512, 0, s3>>>(a, parts);
         }

@@ -490,19 +490,8 @@ int cmt_chain_x3(const cmt_chain_args& a, hipStream_t s) {
     CMT_REQUIRE(a.kind != 0 || a.wo_frag, "cmt_chain: the split chains take fragment-major pair weights (wo_frag)");
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
-    // CMT_CHAIN_RING=8: the weight ring half a sub-GEMM deep (A/B switch)
-    static const int ring = [] {
-        const char* e = getenv("CMT_CHAIN_RING");
-        return e && e[0] == '8' ? 8 : WRING_DEFAULT;
-    }();
-    if (ring == 8) {
-        if (a.kind == 0) chain_x3_kernel<0, 8><<<grid, NTC, 0, s>>>(a);
-        else if (a.kind == 1) chain_x3_kernel<1, 8><<<grid, NTC, 0, s>>>(a);
-        else chain_x3_kernel<2, 8><<<grid, NTC, 0, s>>>(a);
-    } else {
-        if (a.kind == 0) chain_x3_kernel<0, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
-        else if (a.kind == 1) chain_x3_kernel<1, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
-        else chain_x3_kernel<2, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
-    }
+    if (a.kind == 0) chain_x3_kernel<0, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
+    else if (a.kind == 1) chain_x3_kernel<1, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
+    else chain_x3_kernel<2, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
     return cmt_check_launch("cmt_chain");
 }

@@ -479,11 +479,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(cmt_ln_train_args a) {
 
 // ---------------------------------------------------------------------------
 // BatchNorm2d (training: batch statistics over all rows) + ReLU on [rows][C]
-// NHWC rows.  Column sums by 256-row slabs + f32 atomics (two passes: mean,
-// then centred squares).
+// NHWC rows.  Column sums are deterministic at any row count: each row block
+// writes its partial sums to the workspace (no atomics), and bn_reduce_kernel
+// adds the partials of every column in a fixed order (two passes: mean, then
+// centred squares).  Row blocks of >= 64 rows, at most BN_MAXB of them.
 // ---------------------------------------------------------------------------
+constexpr int BN_MAXB = 512;
+inline int bn_rows_per_block(int rows) { return max(64, (cdiv(rows, BN_MAXB) + 7) / 8 * 8); }
+
 __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ X, int rows, int C,
-                                                      const float* __restrict__ shift, float* __restrict__ out,
+                                                      const float* __restrict__ shift, float* __restrict__ part,
                                                       int squares, int rows_per_block) {
     const int c = blockIdx.y * 256 + threadIdx.x;
     if (c >= C) return;
@@ -495,7 +500,30 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
         const float v = X[(int64_t)r * C + c] - sh;
         s += squares ? v * v : v;
     }
-    atomicAdd(out + c, s);
+    part[(int64_t)blockIdx.x * C + c] = s;
+}
+
+// out[c] = scale * sum over blocks of part[blk][c], c < ncols (ldp floats per block): 8 groups of
+// 32 columns per workgroup, group g adds blocks g, g + 8, ... in order, then the 8 group sums are
+// added in order -- the same order on every run
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const float* __restrict__ part, int nblk, int ldp, int ncols,
+                                                        float* __restrict__ out, float scale) {
+    __shared__ float red[8][32];
+    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int c = blockIdx.x * 32 + cl;
+    float s = 0.f;
+    if (c < ncols) {
+#pragma unroll 4
+        for (int b = g; b < nblk; b += 8) s += part[(int64_t)b * ldp + c];
+    }
+    red[g][cl] = s;
+    __syncthreads();
+    if (g == 0 && c < ncols) {
+        float t = red[0][cl];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) t += red[j][cl];
+        out[c] = t * scale;
+    }
 }
 
 __global__ __launch_bounds__(256) void bn_finalize_kernel(cmt_bn_args a, const float* __restrict__ sums) {
@@ -511,11 +539,6 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(cmt_bn_args a, const f
     }
 }
 
-__global__ __launch_bounds__(256) void scale_kernel(float* x, int n, float s) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) x[i] *= s;
-}
-
 __global__ __launch_bounds__(256) void bn_apply_kernel(cmt_bn_args a) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)a.rows * a.C) return;
@@ -524,8 +547,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(cmt_bn_args a) {
     a.Y[i] = fmaxf(v, 0.f);
 }
 
-// backward: g = dY * (Y > 0); sums[0:C] = sum g, sums[C:2C] = sum g * xhat
-__global__ __launch_bounds__(256) void bn_bwd_sums_kernel(cmt_bn_args a, float* __restrict__ sums, int rpb) {
+// backward: g = dY * (Y > 0); per row block part[blk][0:C] = sum g, part[blk][C:2C] = sum g * xhat
+__global__ __launch_bounds__(256) void bn_bwd_sums_kernel(cmt_bn_args a, float* __restrict__ part, int rpb) {
     const int c = blockIdx.y * 256 + threadIdx.x;
     if (c >= a.C) return;
     const int r0 = blockIdx.x * rpb, r1 = min(a.rows, r0 + rpb);
@@ -538,8 +561,9 @@ __global__ __launch_bounds__(256) void bn_bwd_sums_kernel(cmt_bn_args a, float* 
         s1 += g;
         s2 += g * (a.X[i] - mu) * rs;
     }
-    atomicAdd(sums + c, s1);
-    atomicAdd(sums + a.C + c, s2);
+    float* row = part + (int64_t)blockIdx.x * 2 * a.C;
+    row[c] = s1;
+    row[a.C + c] = s2;
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(cmt_bn_args a, const float* __restrict__ sums) {
@@ -736,7 +760,8 @@ extern "C" int cmt_ln_train_bwd(const cmt_ln_train_args* ap, void* stream) {
     return cmt_check_launch("cmt_ln_train_bwd");
 }
 
-extern "C" int64_t cmt_bn_workspace_bytes(int C) { return (int64_t)2 * C * sizeof(float); }
+// sums (2C floats) + the row blocks' partial sums (BN_MAXB x 2C floats)
+extern "C" int64_t cmt_bn_workspace_bytes(int C) { return (int64_t)(2 + 2 * BN_MAXB) * C * sizeof(float); }
 
 extern "C" int cmt_bn_relu_train_fwd(const cmt_bn_args* ap, void* stream) {
     CMT_REQUIRE(ap && ap->rows > 0 && ap->C > 0 && ap->X && ap->Y && ap->W && ap->B && ap->mean_save &&
@@ -744,13 +769,14 @@ extern "C" int cmt_bn_relu_train_fwd(const cmt_bn_args* ap, void* stream) {
     const cmt_bn_args& a = *ap;
     hipStream_t s = (hipStream_t)stream;
     float* sums = (float*)a.workspace;   // [0:C) centred squares, [C:2C) mean
-    if (hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s) != hipSuccess) return cmt_fail(CMT_EINVAL, "bn: hipMemsetAsync failed");
-    const int rpb = 256;   // 127 workgroups at 32 400 rows; 64-row blocks (~500) ran the backward sums in
-                           // 49 instead of 213 us but made the batch statistics arrival-order dependent
-    dim3 grid(cdiv(a.rows, rpb), cdiv(a.C, 256));
-    col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, nullptr, sums + a.C, 0, rpb);
-    scale_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(sums + a.C, a.C, 1.f / a.rows);
-    col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, sums + a.C, sums, 1, rpb);
+    float* part = sums + 2 * a.C;        // [nblk][C] partial sums of one pass
+    const int rpb = bn_rows_per_block(a.rows);   // 507 blocks of 64 rows at 32 400 rows
+    const int nblk = cdiv(a.rows, rpb);
+    dim3 grid(nblk, cdiv(a.C, 256));
+    col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, nullptr, part, 0, rpb);
+    bn_reduce_kernel<<<cdiv(a.C, 32), 256, 0, s>>>(part, nblk, a.C, a.C, sums + a.C, 1.f / a.rows);
+    col_sum_kernel<<<grid, 256, 0, s>>>(a.X, a.rows, a.C, sums + a.C, part, 1, rpb);
+    bn_reduce_kernel<<<cdiv(a.C, 32), 256, 0, s>>>(part, nblk, a.C, a.C, sums, 1.f);
     bn_finalize_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(a, sums);
     bn_apply_kernel<<<(unsigned)cdiv64((int64_t)a.rows * a.C, 256), 256, 0, s>>>(a);
     return cmt_check_launch("cmt_bn_relu_train_fwd");
@@ -762,10 +788,11 @@ extern "C" int cmt_bn_relu_train_bwd(const cmt_bn_args* ap, void* stream) {
     const cmt_bn_args& a = *ap;
     hipStream_t s = (hipStream_t)stream;
     float* sums = (float*)a.workspace;
-    if (hipMemsetAsync(sums, 0, 2 * a.C * sizeof(float), s) != hipSuccess) return cmt_fail(CMT_EINVAL, "bn: hipMemsetAsync failed");
-    const int rpb = 256;   // 127 workgroups at 32 400 rows; 64-row blocks (~500) ran the backward sums in
-                           // 49 instead of 213 us but made the batch statistics arrival-order dependent
-    bn_bwd_sums_kernel<<<dim3(cdiv(a.rows, rpb), cdiv(a.C, 256)), 256, 0, s>>>(a, sums, rpb);
+    float* part = sums + 2 * a.C;        // [nblk][2C]
+    const int rpb = bn_rows_per_block(a.rows);
+    const int nblk = cdiv(a.rows, rpb);
+    bn_bwd_sums_kernel<<<dim3(nblk, cdiv(a.C, 256)), 256, 0, s>>>(a, part, rpb);
+    bn_reduce_kernel<<<cdiv(2 * a.C, 32), 256, 0, s>>>(part, nblk, 2 * a.C, 2 * a.C, sums, 1.f);
     bn_bwd_apply_kernel<<<(unsigned)cdiv64((int64_t)a.rows * a.C, 256), 256, 0, s>>>(a, sums);
     bn_param_grads_kernel<<<cdiv(a.C, 256), 256, 0, s>>>(a, sums);
     return cmt_check_launch("cmt_bn_relu_train_bwd");

@@ -99,6 +99,32 @@ class HeadEngineMixin:
         return (prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 180
                 and pk["conv_w"].shape[0] % 128 == 0)
 
+    def _range_flag(self, dev):
+        """The head's f16-operand range flag: an int32 device word the kernels that read the
+        external feature maps (the NCHW shared_conv's epilogue, the camera-row layout pass) set
+        when a value falls outside the f16 / f16-pair operand format (cmt_hip.h ABI 18).  Made on
+        the first (eager) forward, so a captured graph writes the same word on every replay."""
+        f = self.__dict__.get("_range_flag_t")
+        if f is None or f.device != dev:
+            f = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.__dict__["_range_flag_t"] = f
+        return f
+
+    def check_input_range(self):
+        """Raise ValueError if a forward since the last call -- eager or a replayed HIP
+        graph, where the host-side check_f16_range cannot run -- met a feature-map value
+        the f16-operand policies cannot carry (non-finite or |x| >= 65520), and clear the
+        flag.  One 4-byte device read (it waits for the work queued before it); call it
+        after consuming a replay's outputs."""
+        f = self.__dict__.get("_range_flag_t")
+        if f is None:
+            return
+        if int(f.item()):
+            f.zero_()
+            raise ValueError("an input feature map held a value outside the f16 operand range (non-finite or "
+                             "|x| >= 65520) of the current precision policy; the outputs of that forward are "
+                             "not valid -- use set_precision('exact') for such inputs")
+
     def _shared_conv_into(self, x, mem, Nk, pk, prec, pos=None, P=None):
         """shared_conv into the memory rows; with ``P`` (the weight-only BEV
         position rows, fp32 [H*W, C]) the NCHW conv also writes lowp(memory + pos)
@@ -112,11 +138,13 @@ class HeadEngineMixin:
             native.gemm(x.contiguous().float(), pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=H * W,
                         ldw=9 * Cin, ldc=Cout, bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3_NCHW,
                         conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W, c_bstride=Nk * Cout,
-                        A2=P, lda2=Cout if P is not None else 0, c2=pos if P is not None else None)
+                        A2=P, lda2=Cout if P is not None else 0, c2=pos if P is not None else None,
+                        range_flag=self._range_flag(x.device))
             return
         assert P is None
         xin = op_empty(B * H * W, Cin, prec.gemm, x.device)
-        native.nchw_to_rows(x.contiguous().float(), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W)
+        native.nchw_to_rows(x.contiguous().float(), xin, nb=B, nv=1, C=Cin, HW=H * W, ldy=Cin, rows_per_batch=H * W,
+                            range_flag=self._range_flag(x.device))
         native.gemm(xin, pk["conv_w"], mem, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,
                     bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B,
                     a_bstride=H * W * Cin, c_bstride=Nk * Cout)
@@ -401,6 +429,7 @@ class HeadEngineMixin:
                 bev_ready.record(side)
                 if use_img:
                     native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C,
+                                        range_flag=self._range_flag(x_img.device),
                                         rows_per_batch=Nk, row_offset=HW)
                     if not rv_main:
                         hr = self._rv_pe_hidden(x_img, metas, B, pk, cams=cams)
@@ -428,6 +457,7 @@ class HeadEngineMixin:
                 self._bev_pos_into(pos, B, Nk, H, W, pk, R=R)
             if use_img:
                 native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C,
+                                    range_flag=self._range_flag(x_img.device),
                                     rows_per_batch=Nk, row_offset=HW)
                 self._rv_pe_into(pos, x_img, metas, B, Nk, HW, pk, R=R, cams=cams)
         if side is None:

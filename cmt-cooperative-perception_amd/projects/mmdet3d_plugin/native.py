@@ -27,7 +27,7 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 17
+ABI_VERSION = 18
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -47,7 +47,7 @@ class GemmArgs(ctypes.Structure):
                 ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int),
                 ("c_mode", _int), ("rows_per_batch", _int), ("relu", _int),
                 ("plane_max2", _vp), ("plane_max_cols", _int),
-                ("k_splits", _int), ("c_split_stride", _i64)]
+                ("k_splits", _int), ("c_split_stride", _i64), ("range_flag", _vp)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -179,6 +179,7 @@ def _load():
                                    _int),
         "cmt_masked_view_sum_ex": ([_vp, _vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _int, _vp], _int),
         "cmt_nchw_to_rows": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp], _int),
+        "cmt_nchw_to_rows_ex": ([_vp, _int, _int, _int, _int, _vp, _int, _i64, _i64, _i64, _vp, _vp], _int),
         "cmt_cast": ([_vp, _int, _vp, _int, _i64, _vp], _int),
         "cmt_split_rows": ([_vp, _i64, _i64, _int, _vp, _vp], _int),
         "cmt_task_head_tail": ([_vp, _int, _int, _int, _int, _int, _vp, _vp, _vp, _vp, P(_int), _int, _int, _vp,
@@ -285,7 +286,7 @@ def _farr(vals, n):
 def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=0, A2=None, lda2=0, a2_cols=0,
          a_mode=A_ROWS, conv=(0, 0, 0), seg_len=0, batch=1, a_bstride=0, w_bstride=0, bias_bstride=0,
          r_bstride=0, c_bstride=0, headsplit_rows=0, a_offset=0, c_offset=0, r_offset=0, a2_offset=0,
-         plane_max2=None, plane_max_cols=0, k_splits=0, c2=None):
+         plane_max2=None, plane_max_cols=0, k_splits=0, c2=None, range_flag=None):
     """C = act(A W^T + bias) + R with the fused prologue/epilogue of cmt_gemm.
     Offsets are in elements of the respective tensor.  A2 of A's dtype selects
     (replaces A for output columns < a2_cols); an fp32 A2 beside fp32 A is
@@ -293,7 +294,9 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
     16-bit C only) receives the per-64-row max squared row norm of each head plane.
     k_splits >= 2: C holds k_splits fp32 partial blocks of M * ldc elements whose sum
     is the output (bias and R in the first); a layernorm_ex(nparts=k_splits) reduces them.
-    c2 (a_mode A_CONV3X3_NCHW with fp32 A2 rows): a second output out + A2, laid out like C."""
+    c2 (a_mode A_CONV3X3_NCHW with fp32 A2 rows): a second output out + A2, laid out like C.
+    range_flag (int32 device word; split x3 kernels): set to 1 by the kernel when a value
+    falls outside the f16-pair format (cmt_hip.h cmt_gemm_args.range_flag)."""
     if k_splits > 1 and C.numel() < k_splits * M * ldc:
         raise RuntimeError("gemm: a split-K C needs k_splits blocks of M * ldc elements")
     g = _gemm_args(A, W, C, M=M, N=N, K=K, lda=lda, ldw=ldw, ldc=ldc, bias=bias, relu=relu, R=R, ldr=ldr, A2=A2,
@@ -308,6 +311,11 @@ def gemm(A, W, C, *, M, N, K, lda, ldw, ldc, bias=None, relu=False, R=None, ldr=
         g.plane_max2, g.plane_max_cols = plane_max2.data_ptr(), plane_max_cols
     if k_splits > 1:
         g.k_splits, g.c_split_stride = k_splits, M * ldc
+    if range_flag is not None:
+        _dev(range_flag)
+        if range_flag.dtype != torch.int32:
+            raise RuntimeError("gemm: range_flag must be an int32 device word")
+        g.range_flag = range_flag.data_ptr()
     if c2 is not None:
         # a second output (A_CONV3X3_NCHW with A2): C's layout, at c_offset elements into c2
         _dev(c2)
@@ -720,10 +728,15 @@ def rv_query_coords_lowp(ref, l2i, i2l, out, mask, *, B, V, Nq, D, pad_h, pad_w,
                                         _p(out), DT[out.dtype], _p(mask), _stream()), "cmt_rv_query_coords_ex")
 
 
-def nchw_to_rows(X, Y, *, nb, nv, C, HW, ldy, rows_per_batch, row_offset=0):
-    _dev(X, Y)
-    _check(lib().cmt_nchw_to_rows(_p(X), nb, nv, C, HW, _p(Y), DT[Y.dtype], ldy * _ps(Y), rows_per_batch, row_offset,
-                                  _stream()), "cmt_nchw_to_rows")
+def nchw_to_rows(X, Y, *, nb, nv, C, HW, ldy, rows_per_batch, row_offset=0, range_flag=None):
+    """NCHW fp32 -> rows of Y's dtype; range_flag: int32 device word set to 1 when an f16 /
+    f16-pair output meets a value outside that format (cmt_nchw_to_rows_ex)."""
+    _dev(X, Y, range_flag)
+    if range_flag is not None and range_flag.dtype != torch.int32:
+        raise RuntimeError("nchw_to_rows: range_flag must be an int32 device word")
+    _check(lib().cmt_nchw_to_rows_ex(_p(X), nb, nv, C, HW, _p(Y), DT[Y.dtype], ldy * _ps(Y), rows_per_batch,
+                                     row_offset, _p(range_flag) if range_flag is not None else None, _stream()),
+           "cmt_nchw_to_rows")
 
 
 def cast(X, Y):

@@ -21,21 +21,26 @@ import torch.distributed as dist
 
 from . import native_train as T
 
-__all__ = ["FlatParams", "Trainer", "allreduce_buckets"]
+__all__ = ["FlatParams", "Trainer", "PeerBackwardError", "allreduce_buckets"]
 
 
 class FlatParams:
-    """Trainable parameters of ``module`` as views of one flat buffer."""
+    """Trainable parameters of ``module`` as views of one flat buffer.
 
-    def __init__(self, module):
+    With ``status_words`` > 0 the buffers start with that many words that are
+    no parameter (kept 256-byte aligned for the parameters after them); the
+    data-parallel exchange uses gradient word 0 as a per-step failure flag."""
+
+    def __init__(self, module, status_words=0):
         self.params = [p for p in module.parameters() if p.requires_grad]
         if not self.params:
             raise ValueError("no trainable parameters")
         dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        self.head = int(status_words)
+        n = self.head + sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
+        off = self.head
         self.slices = []
         for p in self.params:
             k = p.numel()
@@ -71,6 +76,10 @@ def allreduce_buckets(flat, bucket_bytes=25 << 20, group=None):
     return len(works)
 
 
+class PeerBackwardError(RuntimeError):
+    """Another rank's backward raised in this step; no rank applies it."""
+
+
 class _GradBuckets:
     """Gradient all-reduce overlapped with backward (mmcv
     MMDistributedDataParallel / torch DDP semantics, tools/train.py:282-289):
@@ -81,7 +90,16 @@ class _GradBuckets:
     of every complete bucket in bucket order -- the same launch sequence on
     every rank whatever order autograd finishes them in, so the collectives
     pair up.  finish() flushes buckets whose parameters got no gradient, waits
-    for all of them and scales by 1 / world."""
+    for all of them and scales by 1 / world.
+
+    A backward that raises on SOME ranks only: the failing rank's abort()
+    sets the step's failure flag (gradient word 0, in the last bucket) and
+    launches every bucket it has not launched yet, so each rank still issues
+    the same sequence of all-reduces and none is paired with a later step's;
+    every rank's finish() then sees the summed flag, drops the step's
+    gradients and raises PeerBackwardError.  (A backward that raises after
+    its last bucket was launched -- all gradients already exchanged -- is not
+    covered: the flag no longer travels.)"""
 
     def __init__(self, fp, bucket_bytes, group):
         self.fp, self.group = fp, group
@@ -103,6 +121,8 @@ class _GradBuckets:
                 members = 0
         if hi is not None:
             self.buckets.append((lo, hi, members))
+        lo, hi, members = self.buckets[-1]
+        self.buckets[-1] = (0, hi, members)    # the last bucket also carries the status words
         self.handles = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(fp.params)]
         self.reset()
 
@@ -128,9 +148,19 @@ class _GradBuckets:
 
     def drain(self):
         """Wait for the all-reduces launched so far and restart the bucket
-        state: a backward() that step() never finished (called twice, or one
-        that raised part-way) must not leave ``next`` / ``pending`` behind, or
-        the next step would exchange nothing and the ranks would drift apart."""
+        state: a backward() that step() never finished (called twice on every
+        rank) must not leave ``next`` / ``pending`` behind, or the next step
+        would exchange nothing and the ranks would drift apart."""
+        for w in self.works:
+            w.wait()
+        self.reset()
+
+    def abort(self):
+        """This rank's backward raised: flag the step and complete its
+        all-reduce sequence (see the class docstring)."""
+        if self.next < len(self.buckets):
+            self.fp.grad[0] = 1.0
+        self._launch_ready(upto=len(self.buckets))
         for w in self.works:
             w.wait()
         self.reset()
@@ -139,9 +169,14 @@ class _GradBuckets:
         self._launch_ready(upto=len(self.buckets))
         for w in self.works:
             w.wait()
-        self.fp.grad.mul_(1.0 / self.world)
         n = len(self.works)
         self.reset()
+        failed = self.fp.grad[0].item() if self.fp.head else 0.0
+        if failed > 0:
+            self.fp.grad.zero_()
+            raise PeerBackwardError(f"the backward of {int(failed)} rank(s) failed in this step: "
+                                    "its gradients were dropped on every rank")
+        self.fp.grad.mul_(1.0 / self.world)
         return n
 
 
@@ -155,7 +190,8 @@ class Trainer:
     def __init__(self, module, lr=1e-4, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-8, max_norm=35.0,
                  bucket_mb=25, group=None):
         self.module = module
-        self.fp = FlatParams(module)
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.fp = FlatParams(module, status_words=64 if multi else 0)
         self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.group = group
@@ -164,7 +200,7 @@ class Trainer:
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=self.fp.flat.device)
         self.step_count = 0
         self.buckets = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if multi:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             dist.broadcast(self.fp.flat, src, group=group)
             for b in module.buffers():
@@ -195,7 +231,12 @@ class Trainer:
         if self.buckets is not None:
             self.buckets.drain()   # outstanding all-reduces write fp.grad: finish them before zeroing it
         self.fp.zero_grad()
-        total.backward()
+        try:
+            total.backward()
+        except BaseException:
+            if self.buckets is not None:
+                self.buckets.abort()
+            raise
         return total
 
     def step(self, losses):

@@ -1,0 +1,167 @@
+// Issue-ceiling probe (diagnostic, not product code) for the d_h = 32 cross-attention core:
+// each wave runs the per-tile instruction mix of attn_pb2_kernel<f16, QS> from registers only
+// (no LDS, no global memory in the loop), software-pipelined in one stream:
+//   QK^T of tile i (8 x v_mfma_f32_32x32x16_f16: two 32-key blocks x (Q hi + Q lo) x 2 k-steps),
+//   P of tile i-1 (32 x v_exp_f32 + 16 x v_cvt_pk_f16_f32 per lane),
+//   PV + row sums of tile i-2 (4 x 32x32x16 + 4 x 16x16x32),
+// at W = 1, 2, 3, 4 waves per SIMD (one 4W-wave workgroup per CU, LDS-pinned), and reports
+// SIMD cycles per tile (s_memtime) against the 448-cycle matrix-pipe floor of one tile and the
+// issue floor (16 MFMA x 8 + 32 exp x 8 + 16 cvt x 4 = 448).
+//   hipcc -O3 --offload-arch=gfx950 dev/issue_probe.hip -o dev/issue_probe && ./dev/issue_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0)
+#define MMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0)
+
+template <int MODE>   // 0 full mix (pipelined), 1 MFMA only, 2 exp + cvt only, 3 full mix, one tile at a time
+__device__ __forceinline__ void tile_body(f16x8 (&kf)[2][2], const f16x8 (&qf)[2], const f16x8 (&ql)[2],
+                                          const f16x8 (&vf)[2][2], const f16x8& sel, f32x16 (&sa)[2],
+                                          f32x16 (&sb)[2], f16x8 (&pf)[2][2], f32x16& o, f32x4& l) {
+    asm volatile("" : "+v"(kf[0][0]), "+v"(kf[1][1]));   // keep QK^T in the loop
+    if (MODE == 3) {
+        // QK^T, P and PV of the SAME tile: the overlap has to come from the other waves
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            sa[kb] = MMA32(kf[kb][0], qf[0], f32x16{});
+            sa[kb] = MMA32(kf[kb][1], qf[1], sa[kb]);
+            sa[kb] = MMA32(kf[kb][0], ql[0], sa[kb]);
+            sa[kb] = MMA32(kf[kb][1], ql[1], sa[kb]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            pf[0][r >> 3][r & 7] = (_Float16)__builtin_amdgcn_exp2f(sa[0][r]);
+            pf[1][r >> 3][r & 7] = (_Float16)__builtin_amdgcn_exp2f(sa[1][r]);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                o = MMA32(vf[kb][ss], pf[kb][ss], o);
+                l = MMA16(sel, pf[kb][ss], l);
+            }
+        return;
+    }
+    if (MODE != 2) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            sa[kb] = MMA32(kf[kb][0], qf[0], f32x16{});
+            sa[kb] = MMA32(kf[kb][1], qf[1], sa[kb]);
+            sa[kb] = MMA32(kf[kb][0], ql[0], sa[kb]);
+            sa[kb] = MMA32(kf[kb][1], ql[1], sa[kb]);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                o = MMA32(vf[kb][ss], pf[kb][ss], o);
+                l = MMA16(sel, pf[kb][ss], l);
+            }
+    }
+    if (MODE != 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            pf[0][r >> 3][r & 7] = (_Float16)__builtin_amdgcn_exp2f(sb[0][r]);
+            pf[1][r >> 3][r & 7] = (_Float16)__builtin_amdgcn_exp2f(sb[1][r]);
+        }
+    } else {
+        asm volatile("" : "+v"(pf[0][0]), "+v"(pf[1][1]));
+    }
+    if (MODE == 2) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sa[kb][r] = sb[kb][r] * 0.999f;
+    }
+}
+
+template <int W, int MODE>
+__global__ __launch_bounds__(256 * W, W) void probe(int nt, float* out, long long* cyc) {
+    extern __shared__ char pin[];   // dynamic LDS: one workgroup per CU
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    f16x8 kf[2][2], vf[2][2], qf[2], ql[2], sel, pf[2][2];
+    for (int j = 0; j < 8; ++j) {
+        const float x = 0.01f * (lane + j);
+        kf[0][0][j] = (_Float16)x; kf[0][1][j] = (_Float16)(x * 0.5f);
+        kf[1][0][j] = (_Float16)(-x); kf[1][1][j] = (_Float16)(x * 0.25f);
+        vf[0][0][j] = (_Float16)(x + 1.f); vf[0][1][j] = (_Float16)(x - 1.f);
+        vf[1][0][j] = (_Float16)(x * 2.f); vf[1][1][j] = (_Float16)(x * 3.f);
+        qf[0][j] = (_Float16)(0.3f - x); qf[1][j] = (_Float16)(0.2f + x);
+        ql[0][j] = (_Float16)(1e-4f * x); ql[1][j] = (_Float16)(-1e-4f * x);
+        sel[j] = (_Float16)((lane & 15) < 2 ? 1.f : 0.f);
+        pf[0][0][j] = pf[0][1][j] = pf[1][0][j] = pf[1][1][j] = (_Float16)0.5f;
+    }
+    f32x16 sa[2], sb[2], o = {};
+    f32x4 l = {};
+    for (int r = 0; r < 16; ++r) sa[0][r] = sa[1][r] = sb[0][r] = sb[1][r] = -1.f - 0.01f * r;
+    if (threadIdx.x == 0) pin[0] = 0;
+    __syncthreads();
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < nt; i += 2) {
+        tile_body<MODE>(kf, qf, ql, vf, sel, sa, sb, pf, o, l);
+        tile_body<MODE>(kf, qf, ql, vf, sel, sb, sa, pf, o, l);
+    }
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    float s = l[0] + l[1];
+    for (int r = 0; r < 16; ++r) s += o[r] + sa[0][r] + sb[1][r];
+    out[blockIdx.x * 256 * W + threadIdx.x] = s;
+    if (lane == 0) cyc[blockIdx.x * 4 * W + wave] = t1 - t0;
+}
+
+template <int W, int MODE>
+void measure(const char* name, int nt, float* out, long long* cyc, int nblk) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const size_t lds = 96 * 1024;
+    hipFuncSetAttribute((const void*)probe<W, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (int it = 0; it < 3; ++it) probe<W, MODE><<<nblk, 256 * W, lds>>>(nt, out, cyc);
+    hipEventRecord(e0);
+    for (int it = 0; it < 5; ++it) probe<W, MODE><<<nblk, 256 * W, lds>>>(nt, out, cyc);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    std::vector<long long> h(nblk * 4 * W);
+    hipMemcpy(h.data(), cyc, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
+    std::sort(h.begin(), h.end());
+    const double med = (double)h[h.size() / 2];
+    // per SIMD: W waves x nt tiles in ~med cycles
+    const double per_tile = med / (W * (double)nt);
+    const double us = ms / 5 * 1e3;
+    // one tile = 32 queries x 64 keys x d 32: 4 * 2048 * 32 = 262144 algorithmic FLOP
+    const double tf = 262144.0 * nt * W * 4 * nblk / (us * 1e-6) / 1e12;
+    printf("%-26s W=%d  SIMD cycles/tile %7.1f  (floor 448: %.2f)  kernel %8.2f us  %7.1f TF/s algorithmic  clk %.2f GHz\n",
+           name, W, per_tile, 448.0 / per_tile, us, tf, med / (us * 1e3));
+}
+
+int main() {
+    const int nblk = 256;
+    float* out;
+    long long* cyc;
+    hipMalloc(&out, nblk * 1024 * sizeof(float));
+    hipMalloc(&cyc, nblk * 16 * sizeof(long long));
+    const int nt = 1000;
+    measure<1, 0>("mix", nt, out, cyc, nblk);
+    measure<2, 0>("mix", nt, out, cyc, nblk);
+    measure<3, 0>("mix", nt, out, cyc, nblk);
+    measure<1, 3>("mix, tile at a time", nt, out, cyc, nblk);
+    measure<2, 3>("mix, tile at a time", nt, out, cyc, nblk);
+    measure<3, 3>("mix, tile at a time", nt, out, cyc, nblk);
+    measure<4, 3>("mix, tile at a time", nt, out, cyc, nblk);
+    measure<1, 1>("mfma only", nt, out, cyc, nblk);
+    measure<2, 1>("mfma only", nt, out, cyc, nblk);
+    measure<1, 2>("exp+cvt only", nt, out, cyc, nblk);
+    measure<2, 2>("exp+cvt only", nt, out, cyc, nblk);
+    measure<4, 2>("exp+cvt only", nt, out, cyc, nblk);
+    hipFree(out);
+    hipFree(cyc);
+    return 0;
+}

@@ -1,10 +1,11 @@
 """Launch one of the 'ref' policy's memory-side kernels at the fusion frame's
 shape a few times (for rocprofv3 counter passes, dev/kernel_pmc.sh):
 
-    python dev/kernel_probe.py kv|conv [--iters N]
+    python dev/kernel_probe.py kv|conv|convh|mlp [--iters N]
 kv:   cmt_kv_proj split form, M = 56 400 tokens, N = 3072 (all layers' K|V), K = 256
 conv: shared_conv as the split implicit 3x3 GEMM, 180 x 180 x 512 -> 256
-convh: shared_conv straight from the NCHW fp32 map (conv_halo_x3_kernel, the 'ref' path)"""
+convh: shared_conv straight from the NCHW fp32 map (conv_halo_x3_kernel, the 'ref' path)
+mlp:  rv_embedding in one launch (cmt_mlp2_x3), 24 000 camera tokens, 192 -> 1024 -> 256"""
 import argparse
 import os
 import sys
@@ -23,7 +24,7 @@ def pairs(*shape):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["kv", "conv", "convh"])
+    ap.add_argument("what", choices=["kv", "conv", "convh", "mlp"])
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--time", action="store_true", help="also print the mean of 20 back-to-back launches")
     a = ap.parse_args()
@@ -37,6 +38,13 @@ def main():
         bias = torch.randn(Nn, device="cuda")
         run = lambda: N.kv_proj(A, W, C, M=M, N=Nn, bias=bias, A2=A2, headsplit_rows=M, plane_max2=pm,  # noqa: E731
                                 plane_max_cols=Nn // 2)
+    elif a.what == "mlp":
+        M, K, Hd = 24000, 192, 1024
+        A = pairs(M, 2, K)
+        W1p, W2p = N.mlp2_pack(pairs(Hd, 2, K), pairs(256, 2, Hd))
+        b1, b2 = torch.randn(Hd, device="cuda"), torch.randn(256, device="cuda")
+        C = torch.empty(M, 2, 256, dtype=torch.uint16, device="cuda")
+        run = lambda: N.mlp2(A, W1p, b1, W2p, b2, C, M=M, K=K, Hd=Hd)  # noqa: E731
     elif a.what == "convh":
         X = torch.randn(1, 512, 180, 180, device="cuda")
         W = pairs(256, 2, 4608)

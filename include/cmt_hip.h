@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 17
+#define CMT_ABI_VERSION 18
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -141,6 +141,13 @@ typedef struct cmt_gemm_args {
      * decoder's 900-row GEMMs, whose tile grid alone covers a quarter of the CUs; the
      * LayerNorm after them sums the parts (cmt_ln_args.nparts).  0 or 1: no split. */
     int k_splits; int64_t c_split_stride;
+    /* optional f16-operand range guard (ABI 18; the split x3 kernels: CMT_A_CONV3X3_NCHW and
+     * the CMT_F16P row GEMMs): when a pre-activation value -- or the second output of
+     * CMT_A_CONV3X3_NCHW with A2 -- is non-finite or |x| >= 65520 (outside the f16-pair
+     * format: a bad input element makes every output of its 3x3 neighbourhood NaN / inf, since
+     * 0 x inf is NaN), the kernel ORs 1 into *range_flag.  Never cleared by the library: the
+     * caller zeroes it and reads it after the stream (or a replayed graph) has run.  NULL: off. */
+    int* range_flag;
 } cmt_gemm_args;
 
 int cmt_gemm(const cmt_gemm_args* args, void* stream);
@@ -221,12 +228,10 @@ int64_t cmt_mlp2_args_size(void);
  *                               it loads Q (one extra rounding of Q in the
  *                               compute dtype; used by the f16/bf16 policies,
  *                               not by the reference-numerics policy)
- *        CMT_ATTN_FORCE_PINGPONG   the f16 bounded long-key path runs the
- *                               ping-pong kernel (the default)
- *        CMT_ATTN_FORCE_PIPELINED  the f16 bounded long-key path runs the
- *                               software-pipelined kernel (measured slower:
- *                               101.4 vs 98.8 us at the fusion shape, r4h;
- *                               kept selectable for A/B and tests)
+ *        CMT_ATTN_FORCE_PINGPONG, CMT_ATTN_FORCE_PIPELINED   reserved, ignored
+ *                               (ABI 17 selected a software-pipelined variant
+ *                               with the second; it measured slower and was
+ *                               removed in round 5)
  *        CMT_ATTN_UNSCALED_Q       f16 long-key core without the fold
  *                               permission: Q enters the QK^T MFMAs unscaled
  *                               and the scores are scaled in fp32 (flash-attn's
@@ -412,6 +417,11 @@ int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int 
  * ------------------------------------------------------------------------ */
 int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype,
                      int64_t ldy, int64_t rows_per_batch, int64_t row_offset, void* stream);
+/* cmt_nchw_to_rows_ex (ABI 18): the same with the f16-operand range guard of
+ * cmt_gemm_args.range_flag: for a CMT_F16 / CMT_F16P ydtype, an input element that is
+ * non-finite or |x| >= 65520 ORs 1 into *range_flag (NULL: off). */
+int cmt_nchw_to_rows_ex(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype,
+                        int64_t ldy, int64_t rows_per_batch, int64_t row_offset, int* range_flag, void* stream);
 int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* stream);
 /* cmt_split_rows (ABI 12): fp32 rows X[r * ldx + c] -> CMT_F16P rows Y [rows][2C]
  * (the split f16 GEMM operand of an fp32 tensor, e.g. the module-level API's inputs). */
@@ -546,8 +556,8 @@ typedef struct cmt_attn_train_args {
  * bounded long-key core with the row statistic, the backward the dK/dV kernel
  * with the head's Q / dO resident in LDS and a K/V-streaming dQ kernel, all on
  * f16 copies of the operands held in the workspace.  cmt_attn_train_workspace_bytes
- * covers both directions; the backward takes the same workspace (with less it
- * runs the general kernels).  CMT_TRAIN_ATTN_FAST=0 disables the path. */
+ * covers both directions; the forward returns CMT_EWORKSPACE on this path
+ * with a smaller workspace, the backward runs the general kernels with less. */
 int64_t cmt_attn_train_workspace_bytes(const cmt_attn_train_args* args);
 int cmt_attn_train_fwd(const cmt_attn_train_args* args, void* stream);
 int cmt_attn_train_bwd(const cmt_attn_train_args* args, void* stream);

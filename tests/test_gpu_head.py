@@ -230,6 +230,49 @@ def test_fusion_head_graph_replay_matches_eager(dev):
     set_precision("ref")
 
 
+@pytest.mark.parametrize("where", ["bev_inf", "img_nan", "bev_big"])
+def test_graph_replay_range_guard(dev, where):
+    """A 'ref' forward replayed from a HIP graph cannot run the host-side
+    check_f16_range, so the kernels that read the feature maps (the NCHW
+    shared_conv's epilogue, the camera-row layout pass) flag a value outside the
+    f16-pair operand format in a device word: one inf in the BEV map, one NaN in
+    a camera map or one finite 1e6 makes head.check_input_range() raise after
+    the replay; clean inputs pass before and after, and the flag clears."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=0, num_query=64, num_layers=2,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(1, 32, 32, seed=21).to(dev)
+    xi = S.synthetic_img(6, 8, 20, seed=22).to(dev)
+    metas = S.synthetic_metas(1, pad_shape=(128, 320, 3), seed=23)
+    set_precision("ref")
+    with torch.no_grad():
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            head([x], [xi], metas)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                head([x], [xi], metas)
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        head.check_input_range()                       # clean inputs: no flag
+        t, idx = (x, (0, 3, 5, 7)) if where.startswith("bev") else (xi, (2, 10, 3, 4))
+        keep = t[idx].item()
+        t[idx] = {"bev_inf": float("inf"), "img_nan": float("nan"), "bev_big": 1e6}[where]
+        g.replay()
+        torch.cuda.synchronize()
+        with pytest.raises(ValueError, match="f16 operand range"):
+            head.check_input_range()
+        head.check_input_range()                       # the flag was cleared
+        t[idx] = keep
+        g.replay()
+        torch.cuda.synchronize()
+        head.check_input_range()
+
+
 @pytest.mark.parametrize("prec,coop", [("bf16", False), ("ref", False), ("ref", True)])
 def test_graph_replay_with_new_metas(dev, prec, coop):
     """Capture a forward with the cameras of frame A, stage frame B's cameras

@@ -501,48 +501,6 @@ def test_attention_f16_long(N, dev, B, Nq, Nk, splits, mode):
     assert (outs["fold"] - ref).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("B,Nq,Nk,splits", [(1, 900, 56400, 0), (2, 300, 4097, 3), (1, 257, 8192, 1),
-                                           (1, 900, 4160, 5), (1, 100, 64 * 9, 1)])
-def test_attention_f16_pipelined_matches_pingpong(N, dev, B, Nq, Nk, splits):
-    """The software-pipelined f16 long-key kernel (attn_sp_kernel,
-    CMT_ATTN_FORCE_PIPELINED) against the ping-pong kernel (attn_pb2_kernel, the
-    default; CMT_ATTN_FORCE_PINGPONG) on the same bounded
-    inputs.  With the fold (Q*c rounded once) both run the same products in the
-    same order: bit-equal.  With Q*c kept as hi + lo the two compile the offset's
-    |q|^2 with different fp32 contractions, so a few P round to the other f16
-    neighbour: outputs within the f16 core's own rounding spread
-    (test_attention_f16_long's bound) and bit-equal for >= 90 % of them
-    (r4d: 96.7 % at the fusion shape, dev/sp_diag.py)."""
-    H = 8
-    g = torch.Generator().manual_seed(Nk + 3 * Nq)
-    q = torch.randn(B, H, Nq, 32, generator=g).half()
-    k = torch.randn(B, H, Nk, 32, generator=g).half()
-    v = torch.randn(B, H, Nk, 32, generator=g).half()
-    km = _kmax2(k, B, Nk, H).to(dev)
-    qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
-    outs = []
-    for diag in (512, 256):
-        for fold in (False, True):
-            O = torch.full((B, Nq, H * 32), float("nan"), device=dev)
-            N.attention(qd, kd, vd, O, B=B, H=H, Nq=Nq, Nk=Nk,
-                        q_strides=(H * Nq * 32, Nq * 32, 32), k_strides=(H * Nk * 32, Nk * 32, 32),
-                        v_strides=(H * Nk * 32, Nk * 32, 32), o_strides=(Nq * H * 32, H * 32),
-                        scale=1 / math.sqrt(32), kv_splits=splits, round_output=True, fold_scale=fold, kmax2=km,
-                        kmax_ld=H, kmax_plane0=0, _diag_flags=diag)
-            torch.cuda.synchronize()
-            outs.append(O.cpu().double())
-    tol = 2 ** -9 * outs[2].abs().clamp(min=2 ** -4) + 2 ** -11 * v.double().abs().max().item()
-    for i, fold in enumerate((False, True)):
-        sp, pp = outs[i], outs[2 + i]
-        assert torch.isfinite(sp).all()
-        d = (sp - pp).abs()
-        if fold:
-            assert torch.equal(sp, pp), d.max().item()
-        else:
-            assert (d <= tol).all(), d.max().item()
-            assert (d == 0).double().mean().item() >= 0.9
-
-
 def test_attention_pair_output(N, dev):
     """Attention output written as the split f16 operand of the out-projection:
     exactly the split of the f32 output (f16-rounded values are exact as hi + lo)."""

@@ -213,6 +213,32 @@ def test_bn_relu_and_conv_weight_grad(dev):
     assert (bng.running_var.cpu().double() - bn.running_var).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("rows", [1000, 32400])
+def test_bn_relu_train_deterministic(dev, rows):
+    """BatchNorm batch statistics and parameter gradients do not depend on the arrival order of
+    the row blocks: two forward + backward passes are bitwise equal at 1 000 and 32 400 rows
+    (4 and 507 row blocks), and the statistics match a float64 restatement."""
+    from projects.mmdet3d_plugin import native_train as NT
+    g = torch.Generator().manual_seed(11)
+    C = 256
+    x = (torch.randn(rows, C, generator=g) * 2 + 0.5).to(dev)
+    w = (torch.rand(C, generator=g) + 0.5).to(dev)
+    b = (torch.rand(C, generator=g) - 0.5).to(dev)
+    dy = torch.randn(rows, C, generator=g).to(dev)
+    outs = []
+    for _ in range(2):
+        y, mean, rstd = NT.bn_relu_train_fwd(x, w, b)
+        dx, dw, db = NT.bn_relu_train_bwd(dy, x, y, w, mean, rstd)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (y, mean, rstd, dx, dw, db)])
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    xd = x.cpu().double()
+    assert (outs[0][1].double() - xd.mean(0)).abs().max().item() < 1e-5
+    var = xd.var(0, unbiased=False)
+    assert ((outs[0][2].double() - (var + 1e-5).rsqrt()).abs() / (var + 1e-5).rsqrt()).max().item() < 1e-5
+
+
 def test_det_loss_and_match_cost(dev):
     from oracle import cmt_train_oracle as TO
     T = _T()

@@ -99,7 +99,7 @@ def _trainer_worker(rank, world, port, q):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "cmt-cooperative-perception_amd"))
-    from projects.mmdet3d_plugin.trainer import Trainer
+    from projects.mmdet3d_plugin.trainer import PeerBackwardError, Trainer
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(rank)          # different inits: the Trainer broadcasts rank 0's
     model = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 10))
@@ -112,22 +112,39 @@ def _trainer_worker(rank, world, port, q):
     tr.backward(model(xs[1]).pow(2).sum())
     local = torch.autograd.grad(model(xs[1]).pow(2).sum(), tr.fp.params)
     nb = tr.buckets.finish()
-    out.append((torch.cat([t.reshape(-1) for t in local]).numpy(), tr.fp.grad.numpy().copy(), nb))
-    # 2) a backward that raises part-way, then a normal one
+    out.append((torch.cat([t.reshape(-1) for t in local]).numpy(), tr.fp.grad[tr.fp.head:].numpy().copy(), nb))
+    # 2) a backward that raises part-way on every rank, then a normal one
     try:
         tr.backward(model[2](_Boom.apply(model[1](model[0](xs[2])))).pow(2).sum())
-    except RuntimeError:
-        pass
+    except RuntimeError as e:
+        assert "boom" in str(e)
     tr.backward(model(xs[0]).pow(2).sum())
     local = torch.autograd.grad(model(xs[0]).pow(2).sum(), tr.fp.params)
     nb = tr.buckets.finish()
-    out.append((torch.cat([t.reshape(-1) for t in local]).numpy(), tr.fp.grad.numpy().copy(), nb))
-    q.put((rank, out))
+    out.append((torch.cat([t.reshape(-1) for t in local]).numpy(), tr.fp.grad[tr.fp.head:].numpy().copy(), nb))
+    # 3) a backward that raises on rank 0 only: rank 0 sees its own error, rank 1's finish() the
+    # peer's, nobody applies the step, and the next exchange pairs up again
+    seen = None
+    try:
+        y = model[2](_Boom.apply(model[1](model[0](xs[2])))) if rank == 0 else model(xs[2])
+        tr.backward(y.pow(2).sum())
+        tr.buckets.finish()
+    except PeerBackwardError:
+        seen = "peer"
+    except RuntimeError as e:
+        seen = "own" if "boom" in str(e) else str(e)
+    tr.backward(model(xs[1]).pow(2).sum())
+    local = torch.autograd.grad(model(xs[1]).pow(2).sum(), tr.fp.params)
+    nb = tr.buckets.finish()
+    out.append((torch.cat([t.reshape(-1) for t in local]).numpy(), tr.fp.grad[tr.fp.head:].numpy().copy(), nb))
+    q.put((rank, out, seen))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_trainer_backward_twice_and_failed_backward_keep_the_exchange():
+    """backward twice, a backward failing on every rank, and one failing on rank 0 only: the
+    bucket all-reduces stay paired and the next exchange is the plain mean."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -139,7 +156,8 @@ def test_trainer_backward_twice_and_failed_backward_keep_the_exchange():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for case in range(2):
+    assert res[0][2] == "own" and res[1][2] == "peer", (res[0][2], res[1][2])
+    for case in range(3):
         (l0, r0, nb), (l1, r1, _) = res[0][1][case], res[1][1][case]
         l0, r0, l1, r1 = (torch.from_numpy(t) for t in (l0, r0, l1, r1))
         assert nb > 1
