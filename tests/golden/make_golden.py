@@ -7,7 +7,8 @@ Only data is stored: the case descriptor (config name, shapes, seeds -- the
 inputs and the random-init weights are regenerated from these seeds by
 projects/mmdet3d_plugin/synthetic.py on the CPU torch RNG) and the expected
 outputs of the last decoder layer for both reference numerics ('fp16' flash
-core) and exact fp32 math.  Reference outputs cannot be produced here: running
+core) and exact fp32 math, and the task heads' logits of every decoder layer
+(no box epilogue) for both.  Reference outputs cannot be produced here: running
 the reference was refused by the environment; parity stays
 "unpinned" in that sense, and these fixtures pin the oracle against drift and
 carry it to the GPU box.
@@ -73,14 +74,18 @@ def case_inputs(c):
     return head, cfg, sd, x, xi, metas
 
 
-def oracle_outputs(c, core):
+def oracle_outputs(c, core, epilogue=True):
+    """Per task, the dict of [L, B, Nq, k] outputs: after the box epilogue (center / height
+    sigmoid-scaled to pc_range) or, with epilogue=False, the task heads' logits."""
     head, cfg, sd, x, xi, metas = case_inputs(c)
     oc = O.cfg_from_head_cfg(cfg)
     if c["variant"] == "coop_lidar":
         agents = [("vehicle_", x[0], None), ("infrastructure_", x[1], None)]
-        out = O.head_coop_forward(oc, sd, agents, metas, "lidar", cross_core=core, self_core="fp32")
+        out = O.head_coop_forward(oc, sd, agents, metas, "lidar", cross_core=core, self_core="fp32",
+                                  epilogue=epilogue)
     else:
-        out = O.head_forward(oc, sd, x, xi, metas, c["variant"], cross_core=core, self_core="fp32")
+        out = O.head_forward(oc, sd, x, xi, metas, c["variant"], cross_core=core, self_core="fp32",
+                             epilogue=epilogue)
     return out
 
 
@@ -125,6 +130,11 @@ def main():
             for t, task in enumerate(out):
                 for k in KEYS:
                     arrs[f"{core}.{t}.{k}"] = task[k][-1].detach().cpu().numpy().astype(np.float32)   # last layer
+            # the task heads' logits of EVERY decoder layer (no box epilogue): the north_star's
+            # 1e-3-abs parity target
+            for t, task in enumerate(oracle_outputs(c, core, epilogue=False)):
+                for k in KEYS:
+                    arrs[f"logits.{core}.{t}.{k}"] = task[k].detach().cpu().numpy().astype(np.float32)
         np.savez_compressed(os.path.join(HERE, f"{cname}.npz"), **arrs)
         index["cases"][cname] = c
         print(cname, {k: v.shape for k, v in list(arrs.items())[:3]})

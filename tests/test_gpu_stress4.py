@@ -5,9 +5,12 @@
     queries): 'ref' policy vs the oracle's 4-agent max fusion at the logit
     level (<= 1e-3 abs), and the fp16 policy vs the same oracle (<= 1 % of
     each output's scale);
-  * full size (4 x 48 400 tokens, 6 layers, 1500 queries, fp16): properties that
-    hold exactly -- agent order does not change the max-fused outputs, and
-    four copies of one agent equal that agent alone.
+  * full size (4 x 48 400 tokens, 6 layers, 1500 queries): 'ref' vs the
+    oracle's 4-agent max fusion at the logit level (every layer, <= 1e-3 abs,
+    headroom per key in the parity log) and the fp16 policy vs the same oracle
+    (<= 1 % of each output's scale); and properties that hold exactly at fp16 --
+    agent order does not change the max-fused outputs, and four copies of one
+    agent equal that agent alone.
 """
 import pytest
 import torch
@@ -61,6 +64,34 @@ def test_stress4_reduced_parity(dev, parity_log):
     parity_log.append(f"stress4 reduced (4 agents, Nq 1500, L 2) 'ref' logits max abs {max(e.values()):.2e} "
                       f"bound 1e-3; 'fp16' max rel-to-scale {max(r16.values()):.2e} bound 1e-2")
     assert max(e.values()) <= 1e-3, e
+    assert max(r16.values()) <= 1e-2, r16
+
+
+def test_stress4_fullsize_parity(dev, parity_log):
+    """configs[4] at full size against the oracle (cmt_head_coop.py:372-389, the max over
+    agents generalised to four): 4 x (180 x 180 BEV + 4 x 40 x 100 camera tokens) = 4 x 48 400
+    keys, 1500 queries, 6 layers."""
+    from oracle import cmt_oracle as O
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmtcoop_fusion_tumtraf", seed=0, num_query=1500)
+    oc, sd = O.cfg_from_head_cfg(cfg), S.head_state_dict(head)
+    agents, metas = _agents(4, 180, (40, 100), seed=80)
+    ref = O.head_coop_forward(oc, sd, agents, metas, "fusion", cross_core="fp16", epilogue=False)[0]
+    head.to(dev)
+    head.box_epilogue = False
+    got = _fwd(head, dev, "ref", agents, metas)
+    e = {k: (got[k].double() - ref[k].double()).abs().max().item() for k in KEYS}
+    got16 = _fwd(head, dev, "fp16", agents, metas)
+    r16 = {k: (got16[k].double() - ref[k].double()).abs().max().item() / max(ref[k].abs().max().item(), 1e-6)
+           for k in KEYS}
+    worst = max(e.values())
+    parity_log.append(f"stress4 full size (4 x 48400 tokens, Nq 1500, L 6) 'ref' vs fp16-core oracle (logits): "
+                      f"max abs {worst:.2e} (worst key {max(e, key=e.get)}, headroom {1 - worst / 1e-3:.0%}) "
+                      f"[{', '.join(f'{k} {v:.1e}' for k, v in e.items())}] bound 1e-3; "
+                      f"'fp16' max rel-to-scale {max(r16.values()):.2e} bound 1e-2")
+    for k in KEYS:
+        assert got[k].shape == ref[k].shape == (6, 1, 1500, ref[k].shape[-1]), k
+    assert worst <= 1e-3, e
     assert max(r16.values()) <= 1e-2, r16
 
 
