@@ -82,6 +82,85 @@ __device__ __forceinline__ void tile_body(f16x8 (&kf)[2][2], const f16x8 (&qf)[2
     }
 }
 
+// MODE 4: MODE 3's tile with the K fragments (4 x ds_read_b128) and V^T fragments (16 x
+// ds_read_b64_tr_b16) read from an LDS ring of 8 tiles each tile, and a workgroup barrier every
+// two tiles -- the attention kernel's per-tile LDS traffic and synchronisation, without the DMA
+template <int W>
+__device__ __forceinline__ void tile_lds(const char* ring, int t, int lane, const f16x8 (&qf)[2], const f16x8 (&ql)[2],
+                                         const f16x8& sel, f32x16 (&sa)[2], f16x8 (&pf)[2][2], f32x16& o, f32x4& l) {
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    const char* kt = ring + (t & 7) * 8192;
+    const char* vt = kt + 4096;
+    const int lr = lane & 31, lh = lane >> 5;
+    f16x8 kf[2][2], vf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            kf[kb][h] = *(const f16x8*)(kt + ((kb * 32 + lr) * 32 + 8 * ((2 * h + lh) ^ ((lr >> 2) & 3))) * 2);
+    const int vo = ((4 * lh + ((lane & 15) >> 2)) * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3)) * 2;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            const char* b0 = vt + vo + (kb * 32 + 16 * ss) * 64;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)b0);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b0 + 512));
+            short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            vf[kb][ss] = __builtin_bit_cast(f16x8, v8);
+        }
+    f32x16 sinit;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sinit[r] = -4.f;   // the bounded offset enters as the accumulator's start
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        sa[kb] = MMA32(kf[kb][0], qf[0], sinit);
+        sa[kb] = MMA32(kf[kb][1], qf[1], sa[kb]);
+        sa[kb] = MMA32(kf[kb][0], ql[0], sa[kb]);
+        sa[kb] = MMA32(kf[kb][1], ql[1], sa[kb]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        pf[0][r >> 3][r & 7] = (_Float16)__builtin_amdgcn_exp2f(sa[0][r]);
+        pf[1][r >> 3][r & 7] = (_Float16)__builtin_amdgcn_exp2f(sa[1][r]);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            o = MMA32(vf[kb][ss], pf[kb][ss], o);
+            l = MMA16(sel, pf[kb][ss], l);
+        }
+}
+
+template <int W>
+__global__ __launch_bounds__(256 * W, W) void probe_lds(int nt, float* out, long long* cyc) {
+    __shared__ __attribute__((aligned(16))) char ring[8 * 8192];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 8 * 8192 / 4; i += 256 * W) ((float*)ring)[i] = 1e-3f * (float)(i & 255);
+    f16x8 qf[2], ql[2], sel, pf[2][2];
+    for (int j = 0; j < 8; ++j) {
+        const float x = 0.01f * (lane + j);
+        qf[0][j] = (_Float16)(0.3f - x); qf[1][j] = (_Float16)(0.2f + x);
+        ql[0][j] = (_Float16)(1e-4f * x); ql[1][j] = (_Float16)(-1e-4f * x);
+        sel[j] = (_Float16)((lane & 15) < 2 ? 1.f : 0.f);
+    }
+    f32x16 sa[2], o = {};
+    f32x4 l = {};
+    __syncthreads();
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < nt; i += 2) {
+        tile_lds<W>(ring, i + wave, lane, qf, ql, sel, sa, pf, o, l);
+        tile_lds<W>(ring, i + wave + 1, lane, qf, ql, sel, sa, pf, o, l);
+        __syncthreads();
+    }
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    float s = l[0] + l[1];
+    for (int r = 0; r < 16; ++r) s += o[r];
+    out[blockIdx.x * 256 * W + threadIdx.x] = s;
+    if (lane == 0) cyc[blockIdx.x * 4 * W + wave] = t1 - t0;
+}
+
 template <int W, int MODE>
 __global__ __launch_bounds__(256 * W, W) void probe(int nt, float* out, long long* cyc) {
     extern __shared__ char pin[];   // dynamic LDS: one workgroup per CU
@@ -142,6 +221,25 @@ void measure(const char* name, int nt, float* out, long long* cyc, int nblk) {
            name, W, per_tile, 448.0 / per_tile, us, tf, med / (us * 1e3));
 }
 
+template <int W>
+void measure_lds(const char* name, int nt, float* out, long long* cyc, int nblk) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const size_t lds = 96 * 1024 - 8 * 8192;   // pin one workgroup per CU
+    hipFuncSetAttribute((const void*)probe_lds<W>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (int it = 0; it < 3; ++it) probe_lds<W><<<nblk, 256 * W, lds>>>(nt, out, cyc);
+    hipEventRecord(e0);
+    for (int it = 0; it < 5; ++it) probe_lds<W><<<nblk, 256 * W, lds>>>(nt, out, cyc);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double us = ms / 5 * 1e3;
+    const double tf = 262144.0 * nt * W * 4 * nblk / (us * 1e-6) / 1e12;
+    printf("%-26s W=%d  kernel %8.2f us  %7.1f TF/s algorithmic  (%.3f of 2.5 PF)\n", name, W, us, tf, tf / 2500);
+}
+
 int main() {
     const int nblk = 256;
     float* out;
@@ -156,11 +254,11 @@ int main() {
     measure<2, 3>("mix, tile at a time", nt, out, cyc, nblk);
     measure<3, 3>("mix, tile at a time", nt, out, cyc, nblk);
     measure<4, 3>("mix, tile at a time", nt, out, cyc, nblk);
+    measure_lds<2>("lds + barrier/2 tiles", nt, out, cyc, nblk);
+    measure_lds<3>("lds + barrier/2 tiles", nt, out, cyc, nblk);
+    measure_lds<4>("lds + barrier/2 tiles", nt, out, cyc, nblk);
     measure<1, 1>("mfma only", nt, out, cyc, nblk);
     measure<2, 1>("mfma only", nt, out, cyc, nblk);
-    measure<1, 2>("exp+cvt only", nt, out, cyc, nblk);
-    measure<2, 2>("exp+cvt only", nt, out, cyc, nblk);
-    measure<4, 2>("exp+cvt only", nt, out, cyc, nblk);
     hipFree(out);
     hipFree(cyc);
     return 0;
