@@ -133,6 +133,19 @@ __device__ __forceinline__ void store_pair8(pair_t* row, int C, int c, const flo
 int cmt_attn_fwd_lse(const cmt_attn_args& a, float* lse, void* stream);
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// compute units of the current device (cached per device): grids of one workgroup per CU
+static inline int cmt_cu_count() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // f16-operand range guard (ABI 18): an fp32 value the f16 / f16-pair operand formats cannot

@@ -9,9 +9,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 180 ./dev/issue_probe > "$OUT/issue_probe.txt" 2>&1 || { echo "probe failed"; cat "$OUT/issue_probe.txt"; exit 1; }
 cat "$OUT/issue_probe.txt"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_head.py tests/test_golden.py tests/test_gpu_stress4.py -m gpu -x -q \
+timeout -k 10 500 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_head.py tests/test_golden.py tests/test_gpu_stress4.py -m gpu -x -q \
     --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1
 rc=$?; tail -12 "$OUT/tests.log"; [[ $rc -eq 0 ]] || { grep -E "^FAILED|Error" "$OUT/tests.log" | head -20; exit 1; }
+timeout -k 10 60 python dev/kernel_probe.py kv --time | grep "per launch"
 for i in 1 2; do
     timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-traffic > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.log" \
         || { echo "bench failed"; tail -20 "$OUT/bench_$i.log"; exit 1; }
