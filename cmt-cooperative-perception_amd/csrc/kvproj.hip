@@ -33,6 +33,10 @@
 #ifndef CMT_KV_SCHED
 #define CMT_KV_SCHED 0
 #endif
+// dev A/B (dev/build_exp.sh -DCMT_KV_PERSIST=0): the one-workgroup-per-(row tile, half) grid
+#ifndef CMT_KV_PERSIST
+#define CMT_KV_PERSIST 0
+#endif
 
 namespace {
 
@@ -672,7 +676,7 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                     "cmt_kv_proj: 16-byte aligned operands");
         const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts);
         hipStream_t s3 = (hipStream_t)stream;
-        if (CMT_KV_SCHED == 0 && a.N <= KPP_MAXB) {
+        if (CMT_KV_PERSIST && CMT_KV_SCHED == 0 && a.N <= KPP_MAXB) {
             // balanced persistent form: one workgroup per CU (never more than the one-per-unit grid)
             const unsigned gp = std::min<unsigned>(g3, (unsigned)cmt_cu_count());
             if (a.c_dtype == CMT_F16) kvproj_x3p_kernel<f16_t><<<gp, 512, 0, s3>>>(a);

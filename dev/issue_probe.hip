@@ -221,6 +221,72 @@ void measure(const char* name, int nt, float* out, long long* cyc, int nblk) {
            name, W, per_tile, 448.0 / per_tile, us, tf, med / (us * 1e3));
 }
 
+// The LDS loop plus the K/V stream: DMA 0 none; 1 every wave issues 2 LDS-DMA pieces (1 KB) per
+// two-tile interval (the tile-at-a-time kernel); 2 waves 0-3 issue 4; 3 a ninth, loader-only wave
+// issues all 16 (compute waves issue none).  Pieces come from a 64 MB buffer (HBM / L3 stream),
+// each into the ring slot the barrier just freed; vmcnt(8) before each barrier keeps two
+// intervals in flight.
+typedef const __attribute__((address_space(1))) void* g_addr_t;
+typedef __attribute__((address_space(3))) void* l_addr_t;
+
+template <int DMA>
+__global__ __launch_bounds__(DMA == 3 ? 576 : 512, 2) void probe_dma(int nt, const char* src, float* out) {
+    __shared__ __attribute__((aligned(16))) char ring[8 * 8192];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 8 * 8192 / 4; i += blockDim.x) ((float*)ring)[i] = 1e-3f * (float)(i & 255);
+    f16x8 qf[2], ql[2], sel, pf[2][2];
+    for (int j = 0; j < 8; ++j) {
+        const float x = 0.01f * (lane + j);
+        qf[0][j] = (_Float16)(0.3f - x); qf[1][j] = (_Float16)(0.2f + x);
+        ql[0][j] = (_Float16)(1e-4f * x); ql[1][j] = (_Float16)(-1e-4f * x);
+        sel[j] = (_Float16)((lane & 15) < 2 ? 1.f : 0.f);
+    }
+    f32x16 sa[2], o = {};
+    f32x4 l = {};
+    const bool loader = DMA == 3 && wave == 8;
+    const int npieces = DMA == 1 ? 2 : DMA == 2 ? (wave < 4 ? 4 : 0) : DMA == 3 ? (loader ? 16 : 0) : 0;
+    const char* s0 = src + ((size_t)blockIdx.x * 16 * 1024 + lane * 16) % (60u << 20);
+    __syncthreads();
+    for (int i = 0; i < nt; i += 2) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __syncthreads();
+        for (int k = 0; k < npieces; ++k) {
+            const int piece = (wave * npieces + k) & 15;
+            const char* g = s0 + ((size_t)(i * 8 + piece) * 1024) % (60u << 20);
+            __builtin_amdgcn_global_load_lds((g_addr_t)g, (l_addr_t)(ring + ((i + 6) & 7) * 8192 / 2 + (piece & 7) * 1024),
+                                             16, 0, 0);
+        }
+        if (!loader) {
+            tile_lds<2>(ring, i, lane, qf, ql, sel, sa, pf, o, l);
+            tile_lds<2>(ring, i + 1, lane, qf, ql, sel, sa, pf, o, l);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float s = l[0] + l[1];
+    for (int r = 0; r < 16; ++r) s += o[r];
+    out[blockIdx.x * 576 + threadIdx.x] = s;
+}
+
+template <int DMA>
+void measure_dma(const char* name, int nt, const char* src, float* out, int nblk) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const size_t lds = 96 * 1024 - 8 * 8192;
+    const int nth = DMA == 3 ? 576 : 512;
+    hipFuncSetAttribute((const void*)probe_dma<DMA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (int it = 0; it < 3; ++it) probe_dma<DMA><<<nblk, nth, lds>>>(nt, src, out);
+    hipEventRecord(e0);
+    for (int it = 0; it < 5; ++it) probe_dma<DMA><<<nblk, nth, lds>>>(nt, src, out);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double us = ms / 5 * 1e3;
+    const double tf = 262144.0 * nt * 8 * nblk / (us * 1e-6) / 1e12;
+    printf("%-26s kernel %8.2f us  %7.1f TF/s algorithmic  (%.3f of 2.5 PF)\n", name, us, tf, tf / 2500);
+}
+
 template <int W>
 void measure_lds(const char* name, int nt, float* out, long long* cyc, int nblk) {
     hipEvent_t e0, e1;
@@ -244,7 +310,7 @@ int main() {
     const int nblk = 256;
     float* out;
     long long* cyc;
-    hipMalloc(&out, nblk * 1024 * sizeof(float));
+    hipMalloc(&out, nblk * 1152 * sizeof(float));
     hipMalloc(&cyc, nblk * 16 * sizeof(long long));
     const int nt = 1000;
     measure<1, 0>("mix", nt, out, cyc, nblk);
@@ -257,6 +323,16 @@ int main() {
     measure_lds<2>("lds + barrier/2 tiles", nt, out, cyc, nblk);
     measure_lds<3>("lds + barrier/2 tiles", nt, out, cyc, nblk);
     measure_lds<4>("lds + barrier/2 tiles", nt, out, cyc, nblk);
+    {
+        char* src;
+        hipMalloc(&src, 64u << 20);
+        hipMemset(src, 0, 64u << 20);
+        measure_dma<0>("dma none (W=2)", nt, src, out, nblk);
+        measure_dma<1>("dma 2/wave/interval", nt, src, out, nblk);
+        measure_dma<2>("dma 4/wave, waves 0-3", nt, src, out, nblk);
+        measure_dma<3>("dma by a 9th loader wave", nt, src, out, nblk);
+        hipFree(src);
+    }
     measure<1, 1>("mfma only", nt, out, cyc, nblk);
     measure<2, 1>("mfma only", nt, out, cyc, nblk);
     hipFree(out);
