@@ -439,6 +439,15 @@ __global__ __launch_bounds__(NWAVES * 64, SUB == 2 ? 1 : (NWAVES == 8 ? 2 : 2)) 
 // KW partial (O, row sum, offset) triples merge through LDS at the end.  No
 // split partials in HBM and no combine launch: a 900 x 900 problem is 29 x H
 // workgroups of KW waves, each wave ~ntiles / KW tiles deep.
+//
+// f16 with the scale unfolded (the 'ref' policy's cross-attention core on short
+// key ranges): a pre-pass over K finds each query's exact row maximum first, so
+// P = exp(s * scale - max) is rounded to f16 at the scale the reference's flash
+// core rounds it (flash-attn 0.2.2 keeps one running maximum per 128-key block, so
+// for the short ranges this path takes the maximum is the global one at each
+// rounding; the oracle's flash_core_fp16 does the same) instead of at an online
+// offset that lags it.  Costs the QK^T MFMAs once more; the path is off the
+// long-key hot loop.
 // ---------------------------------------------------------------------------
 constexpr int KWR = 2;      // ring slots per wave
 constexpr int KWO = 36;     // merge image row stride (floats): 16-byte aligned rows
@@ -448,7 +457,8 @@ __global__ __launch_bounds__(KW * 64) void attn_kw_kernel(AttnKParams p) {
     typedef typename mfma_traits<T>::frag frag;
     constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
     __shared__ __attribute__((aligned(16))) T ring[KW * KWR * STAGE];
-    __shared__ float xm[KW][QW], xl[KW][QW];
+    constexpr bool EXACT = std::is_same<T, f16_t>::value && !FOLD;
+    __shared__ float xm[KW][QW], xl[KW][QW], xg[EXACT ? KW : 1][QW];
     static_assert(KWR * STAGE * (int)sizeof(T) >= QW * KWO * (int)sizeof(float), "merge image fits a wave's ring");
 
     const int tid = threadIdx.x;
@@ -504,6 +514,47 @@ __global__ __launch_bounds__(KW * 64) void attn_kw_kernel(AttnKParams p) {
         negm[r] = 0.f;
     }
     float m_run = 0.f;
+    if constexpr (EXACT) {
+        // pre-pass: this wave's row maximum over its tiles, K fragments straight from global
+        // memory (row kb * 32 + lr of the tile, columns 8 lh.. and 16 + 8 lh..), then the
+        // maximum over the KW waves through LDS
+        float mw = -__builtin_inff();
+        for (int i = 0; i < my_n; ++i) {
+            const int t = wave + i * KW;
+            f32x16 s[2];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const int key = min(t * KT + kb * 32 + lr, p.Nk - 1);
+                const frag k0 = *(const frag*)(Kb + (int64_t)key * p.k_rs + 8 * lh);
+                const frag k1 = *(const frag*)(Kb + (int64_t)key * p.k_rs + 16 + 8 * lh);
+                f32x16 z;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) z[r] = 0.f;
+                s[kb] = mfma_traits<T>::mma(k0, qf[0], z);
+                s[kb] = mfma_traits<T>::mma(k1, qf[1], s[kb]);
+            }
+            if (ragged && t == ntiles - 1) {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        if (key >= p.Nk) s[kb][r] = -__builtin_inff();
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mw = vmax3(mw, s[0][r], s[1][r]);
+        }
+        mw = pair_max(mw);
+        if (lh == 0) xg[wave][lr] = mw;
+        barrier_mem();
+        float M = xg[0][lr];
+#pragma unroll
+        for (int w = 1; w < KW; ++w) M = vmax(M, xg[w][lr]);
+        m_run = M;   // finite: every query sees >= 1 key in the workgroup
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[r] = -M;
+    }
     for (int i = 0; i < my_n; ++i) {
         // tile i landed (the Q loads above are older: in-order completion covers them)
         if (i + 1 < my_n) wait_vm_lgkm<8>();
@@ -511,10 +562,11 @@ __global__ __launch_bounds__(KW * 64) void attn_kw_kernel(AttnKParams p) {
         const T* Kt = myring + (i & 1) * STAGE;
         const T* Vt = Kt + KT * D;
         const int t = wave + i * KW;
+        const bool first = !EXACT && i == 0;   // EXACT: the offset is the final maximum from the start
         if (ragged && t == ntiles - 1)
-            attn_tile_lowp<T, true, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, i == 0, c, t * KT, p.Nk, lane);
+            attn_tile_lowp<T, true, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, first, c, t * KT, p.Nk, lane);
         else
-            attn_tile_lowp<T, false, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, i == 0, c, t * KT, p.Nk, lane);
+            attn_tile_lowp<T, false, FOLD>(Kt, Vt, qf, o, lsum, negm, m_run, first, c, t * KT, p.Nk, lane);
         if (i + 2 < my_n) {
             wait_vm_lgkm<0>();   // the slot's ds_reads are done (lgkmcnt) before the DMA overwrites it
             issue(i & 1, wave + (i + 2) * KW);
@@ -671,7 +723,7 @@ __global__ __launch_bounds__(KW * 64) void attn_kw_pair_kernel(AttnKParams p) {
     constexpr int STAGE = 2 * KTP * PRW;   // 16-bit elements: K tile then V tile (8 KB)
     __shared__ __attribute__((aligned(16))) f16_t ring[KW * KWR * STAGE];
     __shared__ float xm[KW][QW], xl[KW][QW];
-    static_assert(KWR * STAGE * 2 >= QW * KWO * (int)sizeof(float), "merge image fits a wave's ring");
+    static_assert(KWR * STAGE * 2 >=QW * KWO * (int)sizeof(float), "merge image fits a wave's ring");
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1059,36 +1111,6 @@ __device__ __forceinline__ void pb2_wait(int tiles) {
     else pp_wait_n<0>();
 }
 
-// Segment priorities (dev experiments, CMT_ATTN_EXP build define; 0 in the product build):
-// bit 1: the wave entering a matrix segment raises its issue priority to 2 and drops it to 0
-// at the start of its vector segment, so the partner's exponentials fill the MFMA gaps
-// instead of holding the issue port ahead of the MFMAs; bit 2: half B one level above half A
-// throughout (MI355X_MICROARCH.md 'Two waves per SIMD', items 2 and 4).
-#ifndef CMT_ATTN_EXP
-#define CMT_ATTN_EXP 0
-#endif
-template <int PR>
-__device__ __forceinline__ void set_prio() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(PR);
-    __builtin_amdgcn_sched_barrier(0);
-}
-__device__ __forceinline__ void prio_m(bool hb) {
-    if constexpr (CMT_ATTN_EXP & 3) {
-        const int pr = ((CMT_ATTN_EXP & 1) ? 2 : 0) + ((CMT_ATTN_EXP & 2) && hb ? 1 : 0);
-        if (pr == 3) set_prio<3>();
-        else if (pr == 2) set_prio<2>();
-        else if (pr == 1) set_prio<1>();
-        else set_prio<0>();
-    }
-}
-__device__ __forceinline__ void prio_v(bool hb) {
-    if constexpr (CMT_ATTN_EXP & 3) {
-        if ((CMT_ATTN_EXP & 2) && hb) set_prio<1>();
-        else set_prio<0>();
-    }
-}
-
 // US (f16, bounded offsets or not): Q enters the QK^T MFMAs unscaled, exactly the f16 q the
 // reference's flash core multiplies, and the vector segment applies s * c - offset in fp32 (one
 // packed FMA per two scores) -- flash-attn's own order (q k in fp32, then the scale), with half
@@ -1237,7 +1259,6 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
         if (np > 0) {
             if (!hb) pb2_wait(issued - 2);                 // tiles 0, 1 landed
             pp_barrier();
-            prio_m(hb);
             if (!hb) issue_upto(8);
             {
                 const PpLane l = pp_launder(lane_ofs);
@@ -1248,7 +1269,6 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             if (livew) pb_mseg<T, true, false, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
             if (!hb && np > 1) pb2_wait(issued - 4);       // tiles 2, 3 landed
             pp_barrier();
-            prio_v(hb);
             if (livew) us_scale(s0, fastw);
             if (livew) us_scale(s1, fastw);
             if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, true);
@@ -1261,13 +1281,11 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
             }
             for (int j = 1; j < np; ++j) {
                 pp_barrier();
-                prio_m(hb);
                 if (!hb) issue_upto(2 * j + 8);
                 if (livew) pb_mseg<T, true, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);   // QK^T 2j, PV 2j-2
                 if (livew) pb_mseg<T, true, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);   // QK^T 2j+1, PV 2j-1
                 if (!hb && j + 1 < np) pb2_wait(issued - (2 * j + 4));       // tiles 2j+2, 2j+3 landed
                 pp_barrier();
-                prio_v(hb);
                 if (livew) us_scale(s0, fastw);
                 if (livew) us_scale(s1, fastw);
                 if (livew) pb2_vseg<T>(s0, s1, pf0, pf1, o, lsum, m_run, fastw, false);
@@ -1278,10 +1296,8 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
                 if (livew) pp_load_v<T>(slot_b(2 * j + 1) + KV_B, l, vf1);
             }
             pp_barrier();
-            prio_m(hb);
             if (livew) pb_mseg<T, false, true, QS>(kf0, vf0, qf, ql, sinit, pf0, s0, o, lsum);
             if (livew) pb_mseg<T, false, true, QS>(kf1, vf1, qf, ql, sinit, pf1, s1, o, lsum);
-            prio_v(false);
         }
         if (!hb) pp_barrier();   // half A: the window half B spends on its last PV
 
@@ -1376,296 +1392,6 @@ __global__ __launch_bounds__(512, 2) void attn_pb2_kernel(AttnKParams p) {
         }
         if (lh == 0) {
             p.Mp[row] = fast ? off : m_run;   // exp2 units: the offset P was taken against
-            p.Lp[row] = l_tot;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Tile-at-a-time long-key kernel (round 5): attn_tt_kernel.
-//
-// The ping-pong kernel above splits each SIMD's two waves into an MFMA-only and a
-// VALU-only role per window.  The issue-ceiling probe (dev/issue_probe.hip,
-// profiles/r5c_issue_probe.txt) runs the same per-tile mix -- 8 (QS) QK^T MFMAs,
-// 32 v_exp_f32 + 16 packs, 4 PV + 4 row-sum MFMAs, K / V^T fragments read from LDS,
-// one barrier per two tiles -- with NO role split, each wave doing QK^T, P and PV of
-// its own tile in program order and the two waves of a SIMD interleaving freely:
-// 801 TF/s algorithmic at two waves per SIMD (0.32 of the dense f16 peak) against
-// the ping-pong kernel's ~540.  This kernel is that loop with the K/V stream:
-//
-//   8 waves, wave w = queries 32 w .. 32 w + 31 of the workgroup's 256-query block;
-//   every wave runs every 64-key tile of the split: K fragments (4 x ds_read_b128
-//   of the XOR-swizzled image) -> QK^T from the bounded offset (accumulator start,
-//   QS: Q * c as hi + lo) -> P = exp2(S) as f16 -> V^T fragments (transposed
-//   reads) -> O^T += V^T P^T and the row sums (16x16x32 selector MFMAs);
-//   K / V tiles arrive by LDS-DMA into a TT_RING-slot ring, each wave copying one
-//   1-KB piece of every tile (waves 0-3: K rows, 4-7: V rows); one barrier per
-//   two tiles frees the two slots read before it, which then take the tiles
-//   TT_RING - 2 ahead.
-//
-// Numerics are attn_pb2_kernel's (same products, same order per tile, the f16
-// bounded offset with the online-max rerun for a too-loose bound).
-// ---------------------------------------------------------------------------
-constexpr int TT_RING = 10;   // tile slots (80 KB); TT_RING - 2 tiles in flight ahead of the pair being read
-
-// vmcnt wait leaving n (0..TT_RING - 4) of this wave's LDS-DMA pieces in flight
-__device__ __forceinline__ void tt_wait(int n) {
-    if (n >= 6) pp_wait_n<6>();
-    else if (n == 5) pp_wait_n<5>();
-    else if (n == 4) pp_wait_n<4>();
-    else if (n == 3) pp_wait_n<3>();
-    else if (n == 2) pp_wait_n<2>();
-    else if (n == 1) pp_wait_n<1>();
-    else pp_wait_n<0>();
-}
-
-// LDR: a ninth, loader-only wave issues every LDS-DMA piece (16 per two-tile interval) and the
-// eight compute waves none -- an LDS-DMA issue costs the issuing wave ~60-185 cycles beside MFMAs
-// (MI355X_MICROARCH.md constants), which the loader pays off the compute waves' critical path.
-template <typename T, bool QS, bool LDR = false>
-__global__ __launch_bounds__(LDR ? 576 : 512, LDR ? 3 : 2) void attn_tt_kernel(AttnKParams p) {
-    static_assert(TT_RING - 4 <= 6, "tt_wait covers up to 6 pieces in flight");
-    typedef typename mfma_traits<T>::frag frag;
-    constexpr bool F16 = std::is_same<T, f16_t>::value;
-    constexpr int STAGE = 2 * KT * D;   // elements: K tile then V tile
-    __shared__ __attribute__((aligned(16))) T ring[TT_RING * STAGE];
-    __shared__ int redo;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lr = lane & 31;
-    const int lh = lane >> 5;
-    const bool loader = LDR && wave == 8;
-    if (tid == 0) redo = 0;
-
-    // XCD-aware block order (as attn_pb2_kernel): consecutive query blocks of one (b, h, split) on one XCD
-    const int nwg = gridDim.x;
-    const int orig = blockIdx.x;
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int qb = wg % p.nqb;
-    const int rest = wg / p.nqb;
-    const int BH = p.B * p.H;
-    const int bh = rest % BH;
-    const int split = rest / BH;
-    const int b = bh / p.H;
-    const int h = bh - b * p.H;
-
-    const bool live = !loader && qb * (8 * QW) + wave * QW < p.Nq;
-    const T* Qb = (const T*)p.Q + (int64_t)b * p.q_bs + (int64_t)h * p.q_hs;
-    const T* Kb = (const T*)p.K + (int64_t)b * p.k_bs + (int64_t)h * p.k_hs;
-    const T* Vb = (const T*)p.V + (int64_t)b * p.v_bs + (int64_t)h * p.v_hs;
-    const float c = p.c;
-
-    const int ntiles = (p.Nk + KT - 1) / KT;
-    const int t_begin = split * p.tiles_per_split;
-    const int t_end = min(ntiles, t_begin + p.tiles_per_split);
-    const int nt = max(0, t_end - t_begin);                         // tiles of this split (ragged last one included)
-    const bool ragged = (p.Nk % KT) != 0 && t_end == ntiles && nt > 0;
-
-    // this wave's DMA piece of every tile: waves 0-3 K rows 16 (w & 3) .. + 15, waves 4-7 the V rows
-    // (LDR: the loader issues all eight pieces of a tile, piece j as wave j would)
-    const int crow = lane >> 2, cch = lane & 3;
-    const int prow = (wave & 3) * 16 + crow;
-    const bool kpiece = wave < 4;
-    const T* const psrc0 = kpiece ? Kb + 8 * (cch ^ ((prow >> 2) & 3)) : Vb + 8 * cch;
-    const int64_t prs = kpiece ? p.k_rs : p.v_rs;
-    T* const pdst = ring + (kpiece ? 0 : KT * D) + (wave & 3) * 16 * D;
-    int issued = 0;
-    auto ldr_issue = [&](int t) {   // the loader: all eight pieces of tile t
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int row = (j & 3) * 16 + crow;
-            const int key = min((t_begin + t) * KT + row, p.Nk - 1);
-            const T* src = j < 4 ? Kb + (int64_t)key * p.k_rs + 8 * (cch ^ ((row >> 2) & 3))
-                                 : Vb + (int64_t)key * p.v_rs + 8 * cch;
-            dma16(src, ring + (t % TT_RING) * STAGE + (j < 4 ? 0 : KT * D) + (j & 3) * 16 * D);
-        }
-    };
-    auto issue_upto = [&](int n) {   // tiles [issued, min(n, nt)) into their slots
-        const int e = min(n, nt);
-        while (issued < e) {
-            if (LDR) {
-                if (loader) ldr_issue(issued);
-            } else {
-                const int key = min((t_begin + issued) * KT + prow, p.Nk - 1);   // ragged tile: clamped rows, masked below
-                dma16(psrc0 + (int64_t)key * prs, pdst + (issued % TT_RING) * STAGE);
-            }
-            ++issued;
-        }
-    };
-    issue_upto(TT_RING - 2);
-
-    // ---- Q^T fragments with the folded scale (s is in exp2 units), as attn_pb2_kernel
-    const int q = qb * (8 * QW) + wave * QW + lr;
-    const int qc = q < p.Nq ? q : p.Nq - 1;
-    frag qf[2], ql[2];
-    float qq = 0.f;
-    {
-        const frag r0 = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 8 * lh);
-        const frag r1 = *(const frag*)(Qb + (int64_t)qc * p.q_rs + 16 + 8 * lh);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float x0 = (float)r0[j] * c, x1 = (float)r1[j] * c;
-            qf[0][j] = (T)x0;
-            qf[1][j] = (T)x1;
-            ql[0][j] = (T)(x0 - (float)qf[0][j]);
-            ql[1][j] = (T)(x1 - (float)qf[1][j]);
-            const float e0 = QS ? x0 : (float)qf[0][j], e1 = QS ? x1 : (float)qf[1][j];
-            qq += e0 * e0 + e1 * e1;
-        }
-    }
-    bool fast = false;
-    float off = 0.f;
-    if (p.kmax2 != nullptr) {
-        const float km = kmax_reduce(p, b, h, split, lane);
-        const float bound = sqrtf(pair_sum(qq) * km) * 1.001f + 1e-6f;
-        if constexpr (F16) {
-            fast = true;
-            off = bound - kF16Top;
-        } else {
-            fast = __all(bound <= kBoundMax);
-        }
-    }
-    f32x16 sinit;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sinit[r] = F16 && fast ? -off : 0.f;
-
-    const char* const rb = (const char*)ring;
-    constexpr int STAGE_B = STAGE * (int)sizeof(T), KV_B = KT * D * (int)sizeof(T);
-    const PpLane lane_ofs = pp_lane(lane, (int)sizeof(T));
-    f32x16 o;
-    f32x4 lsum;
-    float m_run = 0.f;
-
-    // one tile (index i of the split, slot i % TT_RING): QK^T, P, PV + row sums.  FAST (bounded
-    // offsets, compile-time) and no ragged keys: straight-line code, so the compiler interleaves the
-    // two tiles of an interval (one's exponentials beside the other's MFMAs) -- a branch between them
-    // (the ragged mask, the online-max test) serialises the pair (profiles/r5d_attn_tt.txt)
-    auto tile = [&](int i, auto fast_c, bool fastw, bool first, bool mask) {
-        const char* sb = rb + (i % TT_RING) * STAGE_B;
-        frag kf[2][2], vf[2][2], pf[2][2];
-        f32x16 s[2];
-        const PpLane l = pp_launder(lane_ofs);
-        pp_load_k<T>(sb, l, kf);
-        pb_mseg<T, true, false, QS>(kf, vf, qf, ql, sinit, pf, s, o, lsum);
-        if (mask) {
-            const int key0 = (t_begin + i) * KT;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= p.Nk) s[kb][r] = -__builtin_inff();
-        }
-        if constexpr (decltype(fast_c)::value) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                pf[0][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[0][r]);
-                pf[1][r >> 3][r & 7] = (T)__builtin_amdgcn_exp2f(s[1][r]);
-            }
-        } else {
-            pb_vseg<T>(s, pf, o, lsum, m_run, fastw, first);
-        }
-        pp_load_v<T>(sb + KV_B, l, vf);
-        pb_mseg<T, false, true, QS>(kf, vf, qf, ql, sinit, pf, s, o, lsum);
-    };
-
-    // One pass over the split's keys.  fastw: bounded offsets (else online max); livew: this wave
-    // computes (else it keeps the barriers and its DMA duty only).  Dead waves of the fast steady
-    // state compute too (on the clamped last query, discarded): no branch in the loop body.
-    auto run = [&](bool fastw, bool livew) {
-        if (livew || fastw) {   // a rerun (online max) keeps the results of the waves it does not redo
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[r] = 0.f;
-            lsum = f32x4{0.f, 0.f, 0.f, 0.f};
-            m_run = 0.f;
-        }
-        const int nfull = ragged ? nt - 1 : nt;   // tiles without masked keys
-        int i = 0;
-        if (fastw) {
-            // steady state: both tiles of the interval full, both next DMAs inside the split
-            for (; i + 2 <= nfull && i + TT_RING <= nt; i += 2) {
-                if constexpr (LDR) {
-                    if (loader) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * (TT_RING - 4)) : "memory");
-                    pp_barrier();
-                    if (loader) {
-                        ldr_issue(issued);
-                        ldr_issue(issued + 1);
-                    } else {
-                        tile(i, std::true_type{}, true, false, false);
-                        tile(i + 1, std::true_type{}, true, false, false);
-                    }
-                    issued += 2;
-                } else {
-                    pp_wait_n<TT_RING - 4>();
-                    pp_barrier();
-                    const int t0 = issued, t1 = issued + 1;
-                    dma16(psrc0 + (int64_t)((t_begin + t0) * KT + prow) * prs, pdst + (t0 % TT_RING) * STAGE);
-                    dma16(psrc0 + (int64_t)((t_begin + t1) * KT + prow) * prs, pdst + (t1 % TT_RING) * STAGE);
-                    issued += 2;
-                    tile(i, std::true_type{}, true, false, false);
-                    tile(i + 1, std::true_type{}, true, false, false);
-                }
-            }
-        }
-        for (; i < nt; i += 2) {
-            if (LDR) {
-                if (loader) pp_wait_n<0>();
-            } else {
-                tt_wait(issued - min(i + 2, nt));
-            }
-            pp_barrier();
-            issue_upto(i + TT_RING);
-            if (livew) tile(i, std::false_type{}, fastw, i == 0, ragged && i == nt - 1);
-            if (livew && i + 1 < nt) tile(i + 1, std::false_type{}, fastw, false, ragged && i + 1 == nt - 1);
-        }
-    };
-    run(fast, live);
-    float l_tot = rs16_total(lsum, lane);
-
-    if constexpr (F16) {
-        const bool bad = fast && live && __any(!(l_tot >= kF16MinSum));
-        if (bad && lane == 0) redo = 1;
-        pp_wait_n<0>();
-        barrier_mem();   // every wave past its last ring read, its vote visible
-        if (redo) {
-            issued = 0;
-            issue_upto(TT_RING - 2);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sinit[r] = 0.f;
-            run(false, bad);
-            if (bad) {
-                fast = false;
-                l_tot = rs16_total(lsum, lane);
-            }
-        }
-    }
-
-    // ---- write (attn_pb2_kernel's layout)
-    if (loader || q >= p.Nq) return;
-    if (p.splits == 1) {
-        const float inv = 1.f / l_tot;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-            if (p.round_out) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (float)(T)v[j];
-            }
-            store_o4(p, b, q, h * D + 8 * g + 4 * lh, v);
-        }
-        if (p.lse && lh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + q] = (fast ? off : m_run) + __log2f(l_tot);
-    } else {
-        const int64_t row = (((int64_t)split * p.B + b) * p.H + h) * p.Nq + q;
-        float* dst = p.Op + row * D;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            *(f32x4*)(dst + 8 * g + 4 * lh) = v;
-        }
-        if (lh == 0) {
-            p.Mp[row] = fast ? off : m_run;
             p.Lp[row] = l_tot;
         }
     }
@@ -2004,13 +1730,7 @@ int attn_fwd_impl(const cmt_attn_args& a, float* lse, void* stream) {
     } else if (use_long(a)) {
         // the scale is folded into Q either way; without the FOLD permission q * c is kept as hi + lo
         const unsigned nwg = (unsigned)p.nqb * a.B * a.H * splits;
-        if (a.dtype == CMT_F16 && (CMT_ATTN_EXP & 8) && !us_mode(a.flags)) {
-            if (fold) attn_tt_kernel<f16_t, false, true><<<nwg, 576, 0, s>>>(p);
-            else attn_tt_kernel<f16_t, true, true><<<nwg, 576, 0, s>>>(p);
-        } else if (a.dtype == CMT_F16 && (CMT_ATTN_EXP & 4) && !us_mode(a.flags)) {
-            if (fold) attn_tt_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
-            else attn_tt_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);
-        } else if (a.dtype == CMT_F16) {
+        if (a.dtype == CMT_F16) {
             if (fold) attn_pb2_kernel<f16_t, false><<<nwg, 512, 0, s>>>(p);
             else if (us_mode(a.flags)) attn_pb2_kernel<f16_t, false, true><<<nwg, 512, 0, s>>>(p);
             else attn_pb2_kernel<f16_t, true><<<nwg, 512, 0, s>>>(p);

@@ -33,10 +33,6 @@
 #ifndef CMT_KV_SCHED
 #define CMT_KV_SCHED 0
 #endif
-// dev A/B (dev/build_exp.sh -DCMT_KV_PERSIST=0): the one-workgroup-per-(row tile, half) grid
-#ifndef CMT_KV_PERSIST
-#define CMT_KV_PERSIST 0
-#endif
 
 namespace {
 
@@ -472,180 +468,6 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     }
 }
 
-// ---------------------------------------------------------------------------
-// Balanced persistent form of kvproj_x3_kernel (round 5).  The one-workgroup-per-
-// (row tile, K|V half) grid is 882 workgroups at the fusion frame: 3.45 rounds
-// of 256 CUs, so the last round runs 45 % full and ~14 % of the launch is tail.
-// Here exactly one workgroup per CU walks a contiguous range of the (row tile,
-// head plane) units in row-tile-major order -- every workgroup the same number
-// of units to within one.  A range is cut into segments of one row tile and
-// one half (the A operand: A2 = lowp(mem + pos) for the K planes, A = lowp(mem)
-// for the V planes); per segment the A tile (hi + lo planes) is staged into LDS
-// once and the 8 waves take the segment's planes round-robin.  The k-loop, the
-// W register ring (KV3_RING k-steps ahead, across the wave's planes of a
-// segment) and the epilogue are kvproj_x3_kernel's.
-// ---------------------------------------------------------------------------
-constexpr int KPP_MAXB = 4096;   // bias floats of all columns held in LDS
-
-template <typename TC>
-__global__ __launch_bounds__(512, 1) void kvproj_x3p_kernel(cmt_gemm_args a) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2 + KPP_MAXB * 4];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int lr = lane & 31, lh = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nplanes = a.N >> 5;
-    const int a2_planes = a.A2 ? (a.a2_cols >> 5) : 0;
-    const int ntile = (a.M + KP_BM - 1) / KP_BM;
-    const int64_t U = (int64_t)ntile * nplanes;
-    const int64_t u_begin = (int64_t)blockIdx.x * U / gridDim.x;
-    const int64_t u_end = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
-    float* bsm = (float*)(lds + 2 * KP_BM * KP_K * 2);
-    for (int i = tid; i < a.N; i += 512) bsm[i] = a.bias ? a.bias[i] : 0.f;
-    const pair_t* Wh0 = (const pair_t*)a.W + lane * 8;
-    const int64_t wlo = (int64_t)a.N * KP_K;
-    const int rpb = a.rows_per_batch;
-    const int64_t cbs = kv_c_bstride(a);
-    const char* lhi = lds;
-    const char* llo = lds + KP_BM * KP_K * 2;
-    const int pm_planes = a.plane_max_cols >> 5;
-    typedef TC t4 __attribute__((ext_vector_type(4)));
-    pair8_t rh[KV3_RING], rl[KV3_RING];
-    pair8_t fa[2][4][2];
-    auto read_a = [&](int ks, pair8_t (&f)[4][2]) {
-        const int sw = ((2 * ks + lh) ^ (lr & 15)) << 4;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            f[t][0] = *(const pair8_t*)(lhi + (t * 32 + lr) * (KP_K * 2) + sw);
-            f[t][1] = *(const pair8_t*)(llo + (t * 32 + lr) * (KP_K * 2) + sw);
-        }
-    };
-
-    for (int64_t u = u_begin; u < u_end;) {
-        const int rt = (int)(u / nplanes);
-        const int p0 = (int)(u - (int64_t)rt * nplanes);
-        const bool sel_a2 = p0 < a2_planes;
-        const int pend = sel_a2 ? a2_planes : nplanes;                    // end of this half
-        const int np = (int)min((int64_t)(pend - p0), u_end - u);          // planes of the segment
-        const int m0 = rt * KP_BM;
-        // every wave is past its reads of the previous segment's A tile
-        barrier_mem();
-        const pair_t* Ab = (const pair_t*)(sel_a2 ? a.A2 : a.A);
-        const int64_t lda = sel_a2 ? a.lda2 : a.lda;
-#pragma unroll
-        for (int i = 0; i < 2 * KP_BM * KP_K * 2 / 16 / 512; ++i) {
-            const int piece = tid + 512 * i;
-            const int plane_lo = piece >= KP_BM * 32;
-            const int pc = piece - plane_lo * KP_BM * 32;
-            const int r = pc >> 5;
-            const int lc = (pc & 31) ^ (r & 15);
-            const int src = min(m0 + r, a.M - 1);
-            __builtin_amdgcn_global_load_lds((kp_gaddr_t)(Ab + (int64_t)src * lda + plane_lo * KP_K + 8 * lc),
-                                             (kp_laddr_t)(lds + piece * 16), 16, 0, 0);
-        }
-        // this wave's first plane of the segment: its W ring
-        const int pw0 = p0 + min(wave, np - 1);
-        {
-            const pair_t* Wh = Wh0 + (int64_t)pw0 * (KP_KS * 512);
-#pragma unroll
-            for (int ks = 0; ks < KV3_RING; ++ks) {
-                rh[ks] = *(const pair8_t*)(Wh + ks * 512);
-                rl[ks] = *(const pair8_t*)(Wh + wlo + ks * 512);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier_mem();
-        int64_t rbase[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int m = min(m0 + 32 * t + lr, a.M - 1);
-            const int bb = m / rpb;
-            rbase[t] = (int64_t)bb * cbs + (int64_t)(m - bb * rpb) * 32;
-        }
-        read_a(0, fa[0]);
-        for (int j = wave; j < np; j += 8) {
-            const int plane = p0 + j;
-            const int pn = j + 8 < np ? plane + 8 : plane;   // the ring's next plane (past the last: itself)
-            const pair_t* Wh = Wh0 + (int64_t)plane * (KP_KS * 512);
-            const pair_t* Whn = Wh0 + (int64_t)pn * (KP_KS * 512);
-            f32x16 acc[4];
-            {
-                const float* bp = bsm + plane * 32 + 4 * lh;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const f32x4 b = *(const f32x4*)(bp + 8 * q);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) acc[t][4 * q + e] = b[e];
-                }
-            }
-#pragma unroll
-            for (int ks = 0; ks < KP_KS; ++ks) {
-                const int slot = ks % KV3_RING;
-                read_a((ks + 1) % KP_KS, fa[(ks + 1) & 1]);
-                const pair8_t (&f)[4][2] = fa[ks & 1];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][0], acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rh[slot], f[t][1], acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(rl[slot], f[t][0], acc[t], 0, 0, 0);
-                }
-                const int kn = ks + KV3_RING;
-                const pair_t* wsrc = kn < KP_KS ? Wh + kn * 512 : Whn + (kn - KP_KS) * 512;
-                rh[slot] = *(const pair8_t*)wsrc;
-                rl[slot] = *(const pair8_t*)(wsrc + wlo);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            TC* C = (TC*)a.C + (int64_t)plane * rpb * 32;
-            const bool maxq = a.plane_max2 != nullptr && plane < pm_planes;
-            float pm[2] = {0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int m = m0 + 32 * t + lr;
-                float ss = 0.f;
-                uint32_t pk[4][2];
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        const TC x0 = (TC)acc[t][4 * g + 2 * e], x1 = (TC)acc[t][4 * g + 2 * e + 1];
-                        ss += (float)x0 * (float)x0 + (float)x1 * (float)x1;
-                        pk[g][e] = (uint32_t)__builtin_bit_cast(uint16_t, x0) |
-                                   ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
-                    }
-                uint32_t rcv[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const uint32_t snd = lh ? pk[d >> 1][d & 1] : pk[2 + (d >> 1)][d & 1];
-                    const auto r = __builtin_amdgcn_permlane32_swap(snd, snd, false, false);
-                    rcv[d] = lh ? r[0] : r[1];
-                }
-                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-                const u4 o0 = lh ? u4{rcv[0], rcv[1], pk[2][0], pk[2][1]} : u4{pk[0][0], pk[0][1], rcv[0], rcv[1]};
-                const u4 o1 = lh ? u4{rcv[2], rcv[3], pk[3][0], pk[3][1]} : u4{pk[1][0], pk[1][1], rcv[2], rcv[3]};
-                if (m < a.M) {
-                    *(u4*)(C + rbase[t] + 16 * lh) = o0;
-                    *(u4*)(C + rbase[t] + 16 * lh + 8) = o1;
-                }
-                ss = pair_sum(m < a.M ? ss : 0.f);
-                pm[t >> 1] = (t & 1) ? fmaxf(pm[t >> 1], ss) : ss;
-            }
-            if (maxq) {
-#pragma unroll
-                for (int gq = 0; gq < 2; ++gq) {
-                    float x = pm[gq];
-#pragma unroll
-                    for (int off = 1; off < 32; off <<= 1) x = fmaxf(x, __shfl_xor(x, off));
-                    const int mg = m0 + 64 * gq;
-                    if (lane == 0 && mg < a.M) a.plane_max2[(int64_t)(mg >> 6) * pm_planes + plane] = x;
-                }
-            }
-        }
-        u += np;
-    }
-}
-
 }  // namespace
 
 extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
@@ -676,12 +498,7 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
                     "cmt_kv_proj: 16-byte aligned operands");
         const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts);
         hipStream_t s3 = (hipStream_t)stream;
-        if (CMT_KV_PERSIST && CMT_KV_SCHED == 0 && a.N <= KPP_MAXB) {
-            // balanced persistent form: one workgroup per CU (never more than the one-per-unit grid)
-            const unsigned gp = std::min<unsigned>(g3, (unsigned)cmt_cu_count());
-            if (a.c_dtype == CMT_F16) kvproj_x3p_kernel<f16_t><<<gp, 512, 0, s3>>>(a);
-            else kvproj_x3p_kernel<bf16_t><<<gp, 512, 0, s3>>>(a);
-        } else if (a.c_dtype == CMT_F16) {
+        if (a.c_dtype == CMT_F16) {
             kvproj_x3_kernel<f16_t, CMT_KV_SCHED><<<g3, 512, 0, s3>>>(a, parts);
         } else {
             kvproj_x3_kernel<bf16_t, 0><<<g3, 512, 0, s3>>>(a, parts);
