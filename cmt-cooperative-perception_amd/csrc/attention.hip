@@ -1587,8 +1587,9 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnKParams p) {
     for (int s = 0; s < NS; ++s) {
         // an empty split (no keys) has l == 0 and contributes nothing
         const float w = ls[s] > 0.f ? __builtin_amdgcn_exp2f(ms[s] - M) : 0.f;
-        num += w * os[s];
-        den += w * ls[s];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) num[j] = __builtin_fmaf(w, os[s][j], num[j]);   // explicit: chain B1's
+        den = __builtin_fmaf(w, ls[s], den);                                       // combine matches bitwise
     }
     const float inv = 1.f / den;
     f32x4 r = num * inv;
@@ -1654,9 +1655,13 @@ extern "C" int cmt_attn_fwd(const cmt_attn_args* ap, void* stream) {
     return attn_fwd_impl(*ap, nullptr, stream);
 }
 
+extern "C" int cmt_attn_splits(const cmt_attn_args* a) {
+    return a ? choose_splits(*a) : 0;
+}
+
 int cmt_attn_fwd_lse(const cmt_attn_args& a, float* lse, void* stream) {
     CMT_REQUIRE(lse != nullptr && a.dtype == CMT_F16 && use_long(a) && a.kmax2 != nullptr &&
-                    !(a.flags & CMT_ATTN_FOLD_SCALE),
+                    !(a.flags & (CMT_ATTN_FOLD_SCALE | CMT_ATTN_KEEP_PARTIALS)),
                 "cmt_attn_fwd_lse: the row statistic comes from the long-key f16 bounded path only");
     return attn_fwd_impl(a, lse, stream);
 }
@@ -1749,7 +1754,7 @@ int attn_fwd_impl(const cmt_attn_args& a, float* lse, void* stream) {
         }
     }
     int rc = cmt_check_launch("cmt_attn_fwd");
-    if (rc || splits == 1) return rc;
+    if (rc || splits == 1 || (a.flags & CMT_ATTN_KEEP_PARTIALS)) return rc;   // KEEP: partials for chain B1
     const int64_t total = (int64_t)a.B * a.H * a.Nq * 8;
     const unsigned nb = (unsigned)cdiv64(total, 256);
     switch (splits) {

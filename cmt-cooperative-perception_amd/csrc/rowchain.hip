@@ -511,7 +511,10 @@ extern "C" int cmt_chain(const cmt_chain_args* ap, void* stream) {
                 "cmt_chain: dtype must be f16, bf16 or the f16 pair (CMT_F16P)");
     CMT_REQUIRE(a.prm && a.Y, "cmt_chain: null pointer");
     if (a.kind == 0) CMT_REQUIRE(a.X && a.P && a.Wo && a.W1 && a.Q, "cmt_chain: chain A needs X, P, Wo, W1, Q");
-    if (a.kind == 1) CMT_REQUIRE(a.X && a.Wo && a.W1 && a.W2 && a.WS, "cmt_chain: chain B1 needs X, Wo, W1, W2, WS");
+    if (a.kind == 1)
+        CMT_REQUIRE((a.X || a.xpart) && a.Wo && a.W1 && a.W2 && a.WS,
+                    "cmt_chain: chain B1 needs X (or xpart), Wo, W1, W2, WS");
+    CMT_REQUIRE(a.xpart == nullptr || a.dtype == CMT_F16P, "cmt_chain: xpart is a split-chain (CMT_F16P) input");
     if (a.kind == 2) {
         CMT_REQUIRE(a.WS && a.OUT, "cmt_chain: chain B2 needs WS and OUT");
         CMT_REQUIRE(a.Wn == nullptr || (a.P && a.Q), "cmt_chain: chain B2 with Wn needs P and Q");

@@ -209,8 +209,15 @@ __device__ __forceinline__ const pair_t* frag_base(const void* W, int g, int wav
     return (const pair_t*)W + (int64_t)((g * 4 + (wave >> 1)) * 8) * 4 * 512 + lane * 8;
 }
 
-template <int KIND, int WRING>
+// XP (chain B1, ABI 19): the attention output is not read as X but combined here from the
+// cross-attention's XS split partials (cmt_attn_fwd with CMT_ATTN_KEEP_PARTIALS; attn_combine_kernel's
+// arithmetic in its order, explicit fmas in both), each of the 4 workgroups of a row block
+// combining its 32 rows itself -- no combine launch, no pair-row round trip through HBM.
+constexpr int XS = 8;
+
+template <int KIND, int WRING, bool XP = false>
 __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
+    static_assert(!XP || KIND == 1, "split partials feed chain B1 only");
     __shared__ __attribute__((aligned(16))) char lds[LDS_TOTAL];
     Ctx e;
     e.lds = lds;
@@ -257,7 +264,7 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
     // rows and the parameter block (-> LDS), B2's partials / query_pos / old output, then the
     // weight ring, then the LDS writes and the values first used after the first sub-GEMM
     f32x4 xv[4];
-    if constexpr (KIND != 2) {
+    if constexpr (KIND != 2 && !XP) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {                      // 2048 16-byte pieces: hi then lo planes
             const int piece = tid + NTC * i;
@@ -304,7 +311,62 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
 #pragma unroll
         for (int s = 0; s < WRING; ++s) wst.load(s);
     }
-    if constexpr (KIND != 2) {
+    if constexpr (XP) {
+        // the split combine (attn_combine_kernel<XS>), rounded to f16 per xround, as pair chunks:
+        // pieces (row r, 8-column chunk ch) tid and tid + 512, one at a time behind the weight
+        // ring's loads; their XS partial rows of 8 values, offsets and sums from the workspace
+        // layout of cmt_attn_fwd (O [XS][B][8][Nq][32], then M, then L)
+        const int64_t prow = (int64_t)(a.rows / a.Nq) * 8 * a.Nq;   // partial rows per split
+        const float* Op = a.xpart;
+        const float* Mp = Op + XS * prow * 32;
+        const float* Lp = Mp + XS * prow;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int piece = tid + NTC * i;
+            const int r = piece >> 5, ch = piece & 31;
+            const int src_row = min(m0 + r, a.rows - 1);
+            const int b = src_row / a.Nq, q = src_row - b * a.Nq;
+            const int64_t bhq = ((int64_t)b * 8 + (ch >> 2)) * a.Nq + q;
+            f32x4 po[XS][2];
+            float pm[XS], pls[XS];
+#pragma unroll
+            for (int s = 0; s < XS; ++s) {
+                const float* o = Op + (s * prow + bhq) * 32 + 8 * (ch & 3);
+                po[s][0] = *(const f32x4*)o;
+                po[s][1] = *(const f32x4*)(o + 4);
+                pm[s] = Mp[s * prow + bhq];
+                pls[s] = Lp[s * prow + bhq];
+            }
+            float M = -__builtin_inff();
+#pragma unroll
+            for (int s = 0; s < XS; ++s) M = pls[s] > 0.f ? fmaxf(M, pm[s]) : M;
+            f32x4 n0 = {0.f, 0.f, 0.f, 0.f}, n1 = {0.f, 0.f, 0.f, 0.f};
+            float den = 0.f;
+#pragma unroll
+            for (int s = 0; s < XS; ++s) {
+                const float w = pls[s] > 0.f ? __builtin_amdgcn_exp2f(pm[s] - M) : 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    n0[j] = __builtin_fmaf(w, po[s][0][j], n0[j]);
+                    n1[j] = __builtin_fmaf(w, po[s][1][j], n1[j]);
+                }
+                den = __builtin_fmaf(w, pls[s], den);
+            }
+            const float inv = 1.f / den;
+            pair8_t h, l;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float x = (j < 4 ? n0[j] : n1[j - 4]) * inv;
+                if (a.xround) x = (float)(f16_t)x;
+                h[j] = (pair_t)x;
+                l[j] = (pair_t)(x - (float)h[j]);
+            }
+            const int off = r * (CE * 2) + ((ch ^ (r & 15)) << 4);
+            *(pair8_t*)(actA + off) = h;
+            *(pair8_t*)(actA + PLANE + off) = l;
+        }
+    }
+    if constexpr (KIND != 2 && !XP) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int piece = tid + NTC * i;
@@ -488,9 +550,13 @@ __global__ __launch_bounds__(NTC, 1) void chain_x3_kernel(cmt_chain_args a) {
 // cmt_chain with dtype CMT_F16P (capi/rowchain.hip routes here)
 int cmt_chain_x3(const cmt_chain_args& a, hipStream_t s) {
     CMT_REQUIRE(a.kind != 0 || a.wo_frag, "cmt_chain: the split chains take fragment-major pair weights (wo_frag)");
+    CMT_REQUIRE(a.xpart == nullptr || (a.kind == 1 && a.xsplits == XS && a.Nq > 0 && a.rows % a.Nq == 0 &&
+                                       (uintptr_t)a.xpart % 16 == 0),
+                "cmt_chain: xpart (split partials) feeds chain B1 with xsplits == 8, rows = B * Nq, 16-byte aligned");
     const int parts = a.kind == 0 ? 1 : a.kind == 1 ? 4 : (a.Wn ? 3 : 1);
     const unsigned grid = (unsigned)(cdiv(a.rows, RB) * parts);
     if (a.kind == 0) chain_x3_kernel<0, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
+    else if (a.kind == 1 && a.xpart) chain_x3_kernel<1, WRING_DEFAULT, true><<<grid, NTC, 0, s>>>(a);
     else if (a.kind == 1) chain_x3_kernel<1, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
     else chain_x3_kernel<2, WRING_DEFAULT><<<grid, NTC, 0, s>>>(a);
     return cmt_check_launch("cmt_chain");

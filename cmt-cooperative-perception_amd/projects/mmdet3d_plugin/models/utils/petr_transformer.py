@@ -790,16 +790,18 @@ class PETRTransformerDecoder(nn.Module):
                         A2=mposb, lda2=C, a2_cols=L * C, headsplit_rows=Nk, plane_max2=kmax2, plane_max_cols=L * C)
         return kv, [dict(k=l * C * Nk, v=(L + l) * C * Nk, kmax=kmax2, ld=L * H, p0=l * H) for l in range(L)]
 
-    def _cross_attn(self, qc, kv, ent, ob, *, B, Nq, Nk, ws, prec):
-        """Cross-attention core of one layer."""
+    def _cross_attn(self, qc, kv, ent, ob, *, B, Nq, Nk, ws, prec, keep=False):
+        """Cross-attention core of one layer.  keep: a split launch may leave its
+        partials in ``ws`` for chain B1 (ABI 19) -- returns their count, 0 when
+        ``ob`` was written."""
         L, C, H = self.num_layers, self.embed_dims, self.embed_dims // 32
         with timed("cross_attn"):
-            native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
-                             q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
-                             v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=ent["k"], v_offset=ent["v"],
-                             o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0), workspace=ws,
-                             round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=ent["kmax"],
-                             kmax_ld=ent["ld"], kmax_plane0=ent["p0"])
+            return native.attention(qc, kv, kv, ob, B=B, H=H, Nq=Nq, Nk=Nk,
+                                    q_strides=(C * Nq, 32 * Nq, 32), k_strides=(2 * L * C * Nk, 32 * Nk, 32),
+                                    v_strides=(2 * L * C * Nk, 32 * Nk, 32), k_offset=ent["k"], v_offset=ent["v"],
+                                    o_strides=(Nq * C, C), scale=1.0 / math.sqrt(32.0), workspace=ws,
+                                    round_output=prec.round_cross_out, fold_scale=prec.fold_q, kmax2=ent["kmax"],
+                                    kmax_ld=ent["ld"], kmax_plane0=ent["p0"], keep_partials=keep)
 
     def _run_rows_lowp(self, mem, pos, qpos, *, B, Nk, Nq, out, post_flags, prec, tgt0, kv_operands, out16=None,
                        state=None):
@@ -860,10 +862,11 @@ class PETRTransformerDecoder(nn.Module):
                 self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
                 native.chain(0, st["ob"], qpos, ch["A"][l], lw["sa_ow"], lw["ca_wqp"], st["t1n"], rows=rows, Nq=Nq,
                              eps=eps, R=tgt, Q=st["qc"])
-                self._cross_attn(st["qc"], kv, kvl[l], st["ob"], B=B, Nq=Nq, Nk=Nk, ws=st["ws"], prec=prec)
+                xs = self._cross_attn(st["qc"], kv, kvl[l], st["ob"], B=B, Nq=Nq, Nk=Nk, ws=st["ws"], prec=prec,
+                                      keep=self._keep_partials(prec))
                 nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
                 native.chain(1, st["ob"], None, ch["B"][l], *_b1w(lw), tgt, rows=rows, Nq=Nq, eps=eps,
-                             R=st["t1n"], W2=lw["f2_wp"], WS=st["cws"])
+                             R=st["t1n"], W2=lw["f2_wp"], WS=st["cws"], **self._xpart(st["ws"], xs, prec))
                 native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                              Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
                              Q=st["qkv"] if nxt is not None else None, WS=st["cws"], OUT16=out16)
@@ -912,6 +915,18 @@ class PETRTransformerDecoder(nn.Module):
                 native.cast(out, out16)
         return out
 
+    @staticmethod
+    def _keep_partials(prec):
+        """Split chains ('ref'): chain B1 combines the cross-attention's split partials itself
+        (ABI 19) -- one launch and one pair-row round trip fewer per layer."""
+        return prec.gemm == SPLIT and OPTIONS.chain_combine
+
+    @staticmethod
+    def _xpart(ws, kept, prec):
+        if not kept:
+            return {}
+        return dict(xpart=ws.view(torch.float32), xsplits=kept, xround=prec.round_cross_out)
+
     def _chain_layers(self, st, qpos, kv, kvl, *, B, Nk, Nq, out, post_flags, prec, out16):
         """Chain path from layer 0's cross-attention core on (layer 0's self
         block already queued by lowp_layer0): per layer the cross-attention
@@ -928,10 +943,11 @@ class PETRTransformerDecoder(nn.Module):
                 self._self_attn(st, B=B, H=H, Nq=Nq, C=C)
                 native.chain(0, ob, qpos, ch["A"][l], _wo(lw), lw["ca_wqp"], t1n, rows=rows, Nq=Nq, eps=eps,
                              R=tgt, Q=qc)
-            self._cross_attn(qc, kv, kvl[l], ob, B=B, Nq=Nq, Nk=Nk, ws=ws, prec=prec)
+            xs = self._cross_attn(qc, kv, kvl[l], ob, B=B, Nq=Nq, Nk=Nk, ws=ws, prec=prec,
+                                  keep=self._keep_partials(prec))
             nxt = pk["layers"][l + 1]["sa_wp"] if l + 1 < L else None
             native.chain(1, ob, None, ch["B"][l], *_b1w(lw), tgt, rows=rows, Nq=Nq, eps=eps,
-                         R=t1n, W2=lw["f2_wp"], WS=cws)
+                         R=t1n, W2=lw["f2_wp"], WS=cws, **self._xpart(ws, xs, prec))
             native.chain(2, None, qpos if nxt is not None else None, ch["B"][l], None, None, tgt, rows=rows,
                          Nq=Nq, eps=eps, Wn=nxt, OUT=out, out_offset=l * rows * C, out_flags=post_flags,
                          Q=qkv if nxt is not None else None, WS=cws, OUT16=out16)

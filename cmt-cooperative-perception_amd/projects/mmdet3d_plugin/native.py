@@ -27,7 +27,9 @@ LN_NAN_TO_NUM, LN_MAX_INTO = 1, 2
 A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
-ABI_VERSION = 18
+ATTN_KEEP_PARTIALS = 2048   # cmt_hip.h CMT_ATTN_KEEP_PARTIALS (ABI 19)
+CHAIN_XSPLITS = 8           # the split count chain B1 combines (cmt_chain_args.xsplits)
+ABI_VERSION = 19
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -67,7 +69,8 @@ class ChainArgs(ctypes.Structure):
                 ("X", _vp), ("R", _vp), ("P", _vp), ("prm", _vp),
                 ("Wo", _vp), ("W1", _vp), ("W2", _vp), ("Wn", _vp),
                 ("Y", _vp), ("OUT", _vp), ("out_flags", _int), ("Q", _vp), ("WS", _vp),
-                ("OUT16", _vp), ("wo_frag", _int)]
+                ("OUT16", _vp), ("wo_frag", _int),
+                ("xpart", _vp), ("xsplits", _int), ("xround", _int)]
 
 
 class LnArgs(ctypes.Structure):
@@ -161,6 +164,7 @@ def _load():
         "cmt_last_error": ([], ctypes.c_char_p),
         "cmt_gemm": ([P(GemmArgs), _vp], _int),
         "cmt_attn_workspace_bytes": ([P(AttnArgs)], _i64),
+        "cmt_attn_splits": ([P(AttnArgs)], _int),
         "cmt_attn_fwd": ([P(AttnArgs), _vp], _int),
         "cmt_layernorm": ([_vp, _i64, _int, _int, _vp, _vp, _flt, _vp, _i64, _int, _vp, _vp, _vp, _i64, _int, _vp],
                           _int),
@@ -480,14 +484,17 @@ _WS_CACHE = {}
 
 def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, q_offset=0,
               k_offset=0, v_offset=0, o_offset=0, kv_splits=0, workspace=None, round_output=False,
-              fold_scale=False, kmax2=None, kmax_ld=0, kmax_plane0=0, _diag_flags=0):
+              fold_scale=False, kmax2=None, kmax_ld=0, kmax_plane0=0, keep_partials=False, _diag_flags=0):
     """Strides are (batch, head, row) in elements; o_strides = (batch, row).
     f16-pair Q/K/V (torch.uint16, the split self-attention): strides and offsets
     count 16-bit elements, a pair row being 64 of them (32 hi, 32 lo).
     fold_scale lets the kernel fold scale*log2(e) into Q on load (one extra
     rounding of Q; the f16/bf16 policies only).  kmax2: the K projection's
     plane_max2 partials (see gemm) -- lets the bf16 long-key kernel fix each
-    query's softmax offset at |q| max|k| instead of tracking a running max."""
+    query's softmax offset at |q| max|k| instead of tracking a running max.
+    keep_partials (ABI 19): a launch with CHAIN_XSPLITS key splits leaves its
+    partials in ``workspace`` (which must then be given) for chain B1 and does
+    not write O.  Returns the number of partials kept (0: O written)."""
     _dev(Q, K, V, O, kmax2)
     a = AttnArgs()
     a.B, a.H, a.Nq, a.Nk, a.dtype = B, H, Nq, Nk, DT[Q.dtype]
@@ -506,12 +513,20 @@ def attention(Q, K, V, O, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_st
     a.flags = (1 if round_output else 0) | (2 if fold_scale else 0) | _diag_flags
     if kmax2 is not None:
         a.kmax2, a.kmax_ld, a.kmax_plane0, a.kmax_rows = kmax2.data_ptr(), kmax_ld, kmax_plane0, PLANE_MAX_ROWS
+    kept = 0
+    if keep_partials and int(lib().cmt_attn_splits(ctypes.byref(a))) == CHAIN_XSPLITS:
+        a.flags |= ATTN_KEEP_PARTIALS
+        kept = CHAIN_XSPLITS
     need = lib().cmt_attn_workspace_bytes(ctypes.byref(a))
     if need > 0:
         if workspace is None or workspace.numel() < need:
+            if keep_partials:
+                raise RuntimeError("cmt_attn_fwd: keep_partials needs a caller workspace of "
+                                   "cmt_attn_workspace_bytes (the partials' consumer reads it)")
             workspace = torch.empty(need, dtype=torch.uint8, device=O.device)
         a.workspace, a.workspace_bytes = workspace.data_ptr(), workspace.numel()
     _check(lib().cmt_attn_fwd(ctypes.byref(a), _stream()), "cmt_attn_fwd")
+    return kept
 
 
 def attn_workspace_bytes(*, B, H, Nq, Nk, kv_splits=0):
@@ -618,14 +633,16 @@ def pack_chain_fc2_pair(W2p):
 
 
 def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None, OUT=None, out_offset=0,
-          out_flags=0, Q=None, WS=None, OUT16=None):
+          out_flags=0, Q=None, WS=None, OUT16=None, xpart=None, xsplits=0, xround=False):
     """One row-block chain of a decoder layer's query side (cmt_chain): kind 0
     after self-attention; kinds 1 then 2 after cross-attention (cmt_hip.h).
     Split-f16 operands (torch.uint16: the 'ref' policy) select the split chains:
     X / OUT16 pair rows, every weight a fragment-major pair pack
     (pack_chain_pair / pack_chain_fc2_pair; chain B1's W1 is fc1's), chain A's
-    Q f16 head-split, chain B2's Q head-split pairs."""
-    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16)
+    Q f16 head-split, chain B2's Q head-split pairs.  xpart (ABI 19, split chain
+    B1): the cross-attention workspace a keep_partials attention() left its
+    ``xsplits`` partials in, combined inside the chain (X is then not read)."""
+    _dev(X, P, prm, Wo, W1, Y, R, W2, Wn, OUT, Q, WS, OUT16, xpart)
     split = any(t is not None and t.dtype == torch.uint16 for t in (X, Wo, W1, W2, Wn, Q, OUT16))
     pw = 2 if split else 1   # a pair pack holds the hi pack, then the lo pack
     if Wn is not None and (Wn.dim() != 1 or Wn.numel() != pw * 768 * 256):
@@ -645,7 +662,7 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     a = ChainArgs()
     a.kind, a.rows, a.Nq, a.eps = kind, rows, Nq, eps
     if split:
-        if kind != 2 and (X is None or X.dtype != torch.uint16):
+        if kind != 2 and xpart is None and (X is None or X.dtype != torch.uint16):
             raise RuntimeError("cmt_chain: the split chains take pair-row X")
         if any(t is not None and (t.dtype != torch.uint16 or t.dim() != 1) for t in (Wo, W1, W2, Wn)):
             raise RuntimeError("cmt_chain: the split chains take fragment-major pair weights")
@@ -679,6 +696,10 @@ def chain(kind, X, P, prm, Wo, W1, Y, *, rows, Nq, eps, R=None, W2=None, Wn=None
     # OUT16 holds the layer outputs like OUT: 2 bytes per element, 4 for a pair (hi and lo)
     a.OUT16 = None if OUT16 is None else OUT16.data_ptr() + (4 if split else 2) * out_offset
     a.wo_frag = wo_frag
+    if xpart is not None:
+        if kind != 1 or not split:
+            raise RuntimeError("cmt_chain: xpart feeds the split chain B1 only")
+        a.xpart, a.xsplits, a.xround = xpart.data_ptr(), xsplits, int(bool(xround))
     _check(lib().cmt_chain(ctypes.byref(a), _stream()), "cmt_chain")
 
 

@@ -123,6 +123,8 @@ class Options:
     bev_pos_cache: bool    # CMT_BEV_POS_CACHE=0: rebuild the BEV position-MLP hidden rows per call
     conv_halo: bool        # CMT_CONV_HALO=0: split shared_conv via NCHW->pair rows + per-tap gathered GEMM
     mlp_fused: bool        # CMT_MLP_FUSED=0: split rv_embedding as two GEMMs (hidden pair rows via HBM)
+    chain_combine: bool    # CMT_CHAIN_COMBINE=0: split cross-attention combined by its own launch (pair rows
+                           # via HBM) instead of inside chain B1
 
 
 def _env_on(name):
@@ -131,7 +133,7 @@ def _env_on(name):
 
 OPTIONS = Options(side_stream=_env_on("CMT_SIDE_STREAM"), chain=_env_on("CMT_CHAIN"),
                   bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"), conv_halo=_env_on("CMT_CONV_HALO"),
-                  mlp_fused=_env_on("CMT_MLP_FUSED"))
+                  mlp_fused=_env_on("CMT_MLP_FUSED"), chain_combine=_env_on("CMT_CHAIN_COMBINE"))
 
 
 @contextlib.contextmanager

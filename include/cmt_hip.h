@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 18
+#define CMT_ABI_VERSION 19
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -235,9 +235,12 @@ int64_t cmt_mlp2_args_size(void);
  *        CMT_ATTN_UNSCALED_Q       f16 long-key core without the fold
  *                               permission: Q enters the QK^T MFMAs unscaled
  *                               and the scores are scaled in fp32 (flash-attn's
- *                               order) instead of Q * scale as hi + lo */
+ *                               order) instead of Q * scale as hi + lo
+ *        CMT_ATTN_KEEP_PARTIALS (ABI 19) a split launch (cmt_attn_splits() > 1) skips its
+ *                               combine pass and does not write O: the split partials stay in
+ *                               the workspace for cmt_chain's chain B1 (cmt_chain_args.xpart) */
 enum { CMT_ATTN_ROUND_OUTPUT = 1, CMT_ATTN_FOLD_SCALE = 2, CMT_ATTN_FORCE_PINGPONG = 256,
-       CMT_ATTN_FORCE_PIPELINED = 512, CMT_ATTN_UNSCALED_Q = 1024 };
+       CMT_ATTN_FORCE_PIPELINED = 512, CMT_ATTN_UNSCALED_Q = 1024, CMT_ATTN_KEEP_PARTIALS = 2048 };
 
 typedef struct cmt_attn_args {
     int B, H, Nq, Nk;
@@ -262,6 +265,8 @@ typedef struct cmt_attn_args {
 
 int64_t cmt_attn_workspace_bytes(const cmt_attn_args* args);
 int cmt_attn_fwd(const cmt_attn_args* args, void* stream);
+/* ABI 19: the key-split count a cmt_attn_fwd launch with these arguments uses (1 = no partials) */
+int cmt_attn_splits(const cmt_attn_args* args);
 
 /* ------------------------------------------------------------------------
  * LayerNorm over the last dim C (C % 64 == 0, C <= 1024), eps given.
@@ -359,6 +364,12 @@ typedef struct cmt_chain_args {
     void* OUT16;               /* B2 (optional): the layer output again in dtype (the task-head GEMM operand) */
     int wo_frag;               /* A: 1 = Wo is FRAGMENT-MAJOR (the Wn layout, g = 0) and streams into registers
                                   with W1 (no LDS weight ring); 0 = row-major Wo through the ring (ABI 10) */
+    /* ABI 19, B1 with dtype CMT_F16P (optional, NULL = off): the cross-attention output as the split
+     * partials a cmt_attn_fwd launch with CMT_ATTN_KEEP_PARTIALS left in its workspace (xpart = that
+     * workspace; xsplits = cmt_attn_splits() of the launch, must be 8; B = rows / Nq, 8 heads).
+     * Each workgroup combines its 32 rows itself (attn_combine_kernel's arithmetic, rounded to f16
+     * when xround, as CMT_ATTN_ROUND_OUTPUT does) and X is not read. */
+    const float* xpart; int xsplits; int xround;
 } cmt_chain_args;
 int cmt_chain(const cmt_chain_args* args, void* stream);
 /* bytes of the B1 -> B2 partials workspace WS for `rows` query rows */
