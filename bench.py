@@ -328,8 +328,11 @@ def main():
                                          sync=torch.cuda.synchronize, device=dev)
         value *= args.batch   # frames per forward
 
-        # --- dominant kernel: cross-attention, HIP events on its launch stream
-        with region_timer() as rt:
+        # --- dominant kernel: cross-attention, HIP events on its launch stream.  Timed with its
+        # split combine as a launch of its own (OPTIONS.chain_combine off: the frame's chain B1 does
+        # that combine in its prologue instead), so the pair is the "core + split combine" of the
+        # roofline object and of the earlier rounds' figures; PMC traffic from the same form
+        with region_timer() as rt, options(chain_combine=False):
             for _ in range(3):
                 step()
         attn_ms_all = rt.durations_ms("cross_attn")
