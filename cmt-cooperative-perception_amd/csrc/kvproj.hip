@@ -46,6 +46,20 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* kp_laddr_t;
 template <typename T> using frag_of = typename mfma_traits<T>::frag;
 
+// acc + the squares of the two 16-bit values packed in w (v_dot2_f32_f16 for f16)
+template <typename TC>
+__device__ __forceinline__ float sq2(uint32_t w, float acc) {
+    if constexpr (std::is_same<TC, f16_t>::value) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        const h2 v = __builtin_bit_cast(h2, w);
+        return __builtin_amdgcn_fdot2(v, v, acc, false);
+    } else {
+        const float x0 = (float)__builtin_bit_cast(TC, (uint16_t)(w & 0xffffu));
+        const float x1 = (float)__builtin_bit_cast(TC, (uint16_t)(w >> 16));
+        return acc + x0 * x0 + x1 * x1;
+    }
+}
+
 // Batch stride of the head-split C in 16-bit elements: c_bstride when given (one
 // layer's K/V planes written into a larger [B][planes][Nk][32] buffer), else the
 // launch's own N/32 planes per batch element.
@@ -326,6 +340,11 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     // each costs)
     if constexpr (SCHED & 2)
         if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#ifdef CMT_KV_SLEEP
+    // dev: the SIMD's second wave (waves 4-7) starts CMT_KV_SLEEP x 64 cycles late, so its plane
+    // epilogues fall inside the partner's MFMA runs instead of beside the partner's own epilogues
+    if (wave >= 4) __builtin_amdgcn_s_sleep(CMT_KV_SLEEP);
+#endif
     for (int j = 0; j < planes_w; ++j) {
         const int plane = plane0 + j;
         f32x16 acc[4];
@@ -413,28 +432,37 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
                 // pair swaps two 4-column groups (v_permlane32_swap) so that lh = 0 holds columns
                 // 0..15 and lh = 1 columns 16..31, then stores them as two 16-byte pieces (half
                 // the store instructions, twice the bytes each, of the 8-byte form below)
-                uint32_t pk[4][2];
+                // lane (lr, lh) packs its columns 8 g + 4 lh + 0..3 as X = groups 0, 1 and Y = groups
+                // 2, 3 (two f16 per dword); one v_permlane32_swap per dword, X as the high half's
+                // vdst and Y as the low half's vsrc, leaves lh = 0 with columns 0..15 and lh = 1
+                // with 16..31 as (vdst, vsrc) dword pairs in the same order on both halves -- no
+                // per-half selects -- stored as two 16-byte pieces
+                uint32_t X[4], Y[4];
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         const TC x0 = (TC)acc[t][4 * g + 2 * e], x1 = (TC)acc[t][4 * g + 2 * e + 1];
-                        ss += (float)x0 * (float)x0 + (float)x1 * (float)x1;
-                        pk[g][e] = (uint32_t)__builtin_bit_cast(uint16_t, x0) |
-                                   ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
+                        const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, x0) |
+                                           ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
+                        if (g < 2) X[2 * g + e] = w;
+                        else Y[2 * (g - 2) + e] = w;
                     }
-                uint32_t rcv[4];
+                if (maxq) {
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) ss = sq2<TC>(Y[d], sq2<TC>(X[d], ss));
+                }
+                uint32_t f[4], s2[4];
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
-                    const uint32_t snd = lh ? pk[d >> 1][d & 1] : pk[2 + (d >> 1)][d & 1];
-                    // v_permlane32_swap exchanges vdst of lanes 32..63 with vsrc of lanes 0..31:
-                    // the partner's value lands in vsrc (r[1]) on the low half, vdst (r[0]) on the high
-                    const auto r = __builtin_amdgcn_permlane32_swap(snd, snd, false, false);
-                    rcv[d] = lh ? r[0] : r[1];
+                    // v_permlane32_swap exchanges vdst of lanes 32..63 with vsrc of lanes 0..31
+                    const auto r = __builtin_amdgcn_permlane32_swap(X[d], Y[d], false, false);
+                    f[d] = r[0];
+                    s2[d] = r[1];
                 }
                 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-                const u4 o0 = lh ? u4{rcv[0], rcv[1], pk[2][0], pk[2][1]} : u4{pk[0][0], pk[0][1], rcv[0], rcv[1]};
-                const u4 o1 = lh ? u4{rcv[2], rcv[3], pk[3][0], pk[3][1]} : u4{pk[1][0], pk[1][1], rcv[2], rcv[3]};
+                const u4 o0 = u4{f[0], f[1], s2[0], s2[1]};
+                const u4 o1 = u4{f[2], f[3], s2[2], s2[3]};
                 if constexpr (SCHED & 16) {
                     asm volatile("" ::"v"(o0), "v"(o1));
                 } else if (m < a.M) {
