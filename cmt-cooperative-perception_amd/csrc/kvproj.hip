@@ -46,6 +46,14 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* kp_laddr_t;
 template <typename T> using frag_of = typename mfma_traits<T>::frag;
 
+// two fp32 values rounded (RNE) into one dword of 16-bit values, x0 low (v_cvt_pk_f16_f32 for f16)
+template <typename TC>
+__device__ __forceinline__ uint32_t pack2(float x0, float x1) {
+    typedef TC v2 __attribute__((ext_vector_type(2)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{x0, x1}, v2));
+}
+
 // acc + the squares of the two 16-bit values packed in w (v_dot2_f32_f16 for f16)
 template <typename TC>
 __device__ __forceinline__ float sq2(uint32_t w, float acc) {
@@ -442,9 +450,7 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
                 for (int g = 0; g < 4; ++g)
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
-                        const TC x0 = (TC)acc[t][4 * g + 2 * e], x1 = (TC)acc[t][4 * g + 2 * e + 1];
-                        const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, x0) |
-                                           ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
+                        const uint32_t w = pack2<TC>(acc[t][4 * g + 2 * e], acc[t][4 * g + 2 * e + 1]);
                         if (g < 2) X[2 * g + e] = w;
                         else Y[2 * (g - 2) + e] = w;
                     }
