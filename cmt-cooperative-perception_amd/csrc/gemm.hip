@@ -713,6 +713,8 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
     Tile::run(a, smem, m0, n0, z, acc, part * nkp, nkp);
 
     // ---- epilogue: lane = output row, 4 consecutive columns per register group.
+    // X3 with a.range_flag: the f16-pair range guard of x3_epilogue on the pre-activation values
+    bool bad = false;
     if (Rz) {
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
@@ -724,10 +726,17 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
                     // bias + relu come first; keep R apart only when relu is on
                     if (a.relu) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] = fmaxf(acc[tm][tn][4 * g + j] + bv[tn][g][j], 0.f) + r[j];
+                        for (int j = 0; j < 4; ++j) {
+                            const float v = acc[tm][tn][4 * g + j] + bv[tn][g][j];
+                            if constexpr (X3) bad |= f16_unrepresentable(v);
+                            acc[tm][tn][4 * g + j] = fmaxf(v, 0.f) + r[j];
+                        }
                     } else {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                        for (int j = 0; j < 4; ++j) {
+                            acc[tm][tn][4 * g + j] += bv[tn][g][j] + r[j];
+                            if constexpr (X3) bad |= f16_unrepresentable(acc[tm][tn][4 * g + j]);
+                        }
                     }
                 }
         }
@@ -741,9 +750,11 @@ __global__ __launch_bounds__(NT) void gemm_dma_kernel(cmt_gemm_args a, int tiles
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const float v = acc[tm][tn][4 * g + j] + bv[tn][g][j];
+                        if constexpr (X3) bad |= f16_unrepresentable(v);
                         acc[tm][tn][4 * g + j] = a.relu ? fmaxf(v, 0.f) : v;
                     }
     }
+    if constexpr (X3) raise_range_flag(a.range_flag, bad);
     // ---- stores staged through LDS: the swapped layout leaves each lane 4
     // columns of one row (8/16-byte pieces at a row stride); the tile is
     // written to LDS (16-byte chunks XOR-swizzled by row) and read back so

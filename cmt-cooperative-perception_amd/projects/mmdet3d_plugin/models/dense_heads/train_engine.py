@@ -182,7 +182,8 @@ class HeadTrainMixin:
             xr = ops.nchw_rows(x, B)
             conv = self.shared_conv.conv
             w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1)
-            y = ops.bn_relu(ops.conv3x3(xr, w, (B, H, W, Cin)), self.shared_conv.bn)
+            y = ops.bn_relu(ops.conv3x3(xr, w, (B, H, W, Cin), range_flag=self._range_flag(x.device)),
+                            self.shared_conv.bn)
             mems.append(y.view(B, H * W, C))
             cfg = self.train_cfg if self.train_cfg else self.test_cfg
             xs, ys = cfg["grid_size"][1] // self.downsample_scale, cfg["grid_size"][0] // self.downsample_scale

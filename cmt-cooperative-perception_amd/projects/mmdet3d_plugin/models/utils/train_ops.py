@@ -157,7 +157,7 @@ class _Conv3x3(torch.autograd.Function):
     """NHWC rows [B*H*W, Cin] -> [B*H*W, Cout]; weight [Cout, 9*Cin] tap-major."""
 
     @staticmethod
-    def forward(ctx, x, w, geom):
+    def forward(ctx, x, w, geom, range_flag=None):
         B, H, W, Cin = geom
         Cout = w.shape[0]
         y = torch.empty((B * H * W, Cout), dtype=torch.float32, device=x.device)
@@ -168,12 +168,15 @@ class _Conv3x3(torch.autograd.Function):
         else:
             # the split-f16 implicit-GEMM conv of the inference path (three f16 MFMA passes on pair
             # operands, ~2^-21 relative per product): 3x the exact-f32 MFMA's speed at this size
+            # operands the pair format cannot carry (|x| >= 65520, non-finite) make a non-finite or
+            # out-of-range conv output, which the kernel's epilogue reports through range_flag (the
+            # head's device word, CmtHead.check_input_range(); no host sync in the step)
             xs = native.split_rows(x)
             wh = w.detach().half()                                   # pair weights (no host range check:
             ws = torch.stack([wh, (w.detach() - wh.float()).half()], dim=-2).contiguous().view(SPLIT)   # no sync)
             native.gemm(xs, ws, y, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,
                         a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin,
-                        c_bstride=H * W * Cout)
+                        c_bstride=H * W * Cout, range_flag=range_flag)
         ctx.save_for_backward(x, w)
         ctx.geom = geom
         return y
@@ -200,11 +203,13 @@ class _Conv3x3(torch.autograd.Function):
             native.gemm(dy.contiguous(), wt, dx, M=H * W, N=Cin, K=9 * Cout, lda=Cout, ldw=9 * Cout, ldc=Cin,
                         a_mode=native.A_CONV3X3, conv=(H, W, Cout), batch=B, a_bstride=H * W * Cout,
                         c_bstride=H * W * Cin)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
-def conv3x3(x_rows, w_tap_major, geom):
-    return _Conv3x3.apply(x_rows, w_tap_major, geom)
+def conv3x3(x_rows, w_tap_major, geom, range_flag=None):
+    """range_flag: the head's f16-operand range word (int32 device tensor), set when the split
+    conv met a value the f16 pair format cannot carry."""
+    return _Conv3x3.apply(x_rows, w_tap_major, geom, range_flag)
 
 
 class _NchwRows(torch.autograd.Function):

@@ -141,8 +141,9 @@ typedef struct cmt_gemm_args {
      * decoder's 900-row GEMMs, whose tile grid alone covers a quarter of the CUs; the
      * LayerNorm after them sums the parts (cmt_ln_args.nparts).  0 or 1: no split. */
     int k_splits; int64_t c_split_stride;
-    /* optional f16-operand range guard (ABI 18; the split x3 kernels: CMT_A_CONV3X3_NCHW and
-     * the CMT_F16P row GEMMs): when a pre-activation value -- or the second output of
+    /* optional f16-operand range guard (ABI 18; the split (CMT_F16P) cmt_gemm kernels: the x3
+     * tiles, CMT_A_CONV3X3_NCHW and the 128-wide split tile -- not cmt_kv_proj / cmt_gemm_ln,
+     * whose operands are outputs of guarded kernels): when a pre-activation value -- or the second output of
      * CMT_A_CONV3X3_NCHW with A2 -- is non-finite or |x| >= 65520 (outside the f16-pair
      * format: a bad input element makes every output of its 3x3 neighbourhood NaN / inf, since
      * 0 x inf is NaN), the kernel ORs 1 into *range_flag.  Never cleared by the library: the

@@ -286,3 +286,28 @@ def test_transformer_forward_with_dn_mask_training(dev, parity_log):
     bad[0, -1] = True
     with pytest.raises(NotImplementedError):
         tr(x.to(dev), None, qe.to(dev), pe.to(dev), attn_masks=[bad.to(dev), None])
+
+
+def test_training_conv_range_guard(dev):
+    """The training shared_conv runs on split-f16 pairs (train_ops._Conv3x3): a BEV value the
+    pair format cannot carry (|x| >= 65520) sets the head's range word in the conv's epilogue --
+    no host sync in the step -- and CmtHead.check_input_range() raises after the step; a clean
+    step leaves it clear."""
+    from projects.mmdet3d_plugin import synthetic as S
+    head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=32, num_layers=1, grid_size=[128, 128, 40],
+                                        device=dev)
+    head.train()
+    head.train_dropout = False
+    gtb, gtl = _gt(1, list(head.pc_range), head.num_classes[0], 4, seed=8)
+    gtb, gtl = [b.to(dev) for b in gtb], [l.to(dev) for l in gtl]
+    x = S.synthetic_bev(1, 16, 16, seed=9).to(dev)
+    head.forward_train([(x, None, [dict()])], [dict()], gtb, gtl)
+    torch.cuda.synchronize()
+    head.check_input_range()                            # clean: no flag
+    bad = x.clone()
+    bad[0, 3, 5, 7] = 1e6
+    head.forward_train([(bad, None, [dict()])], [dict()], gtb, gtl)
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError):
+        head.check_input_range()
+    head.check_input_range()                            # cleared by the raise
