@@ -58,10 +58,12 @@ __device__ __forceinline__ f32x16 mma3(const pair8_t& wh, const pair8_t& wl, con
 
 // KS = K / 16; PD = the LDS fragment prefetch distance in steps (3: same time, 4: +8 %,
 // profiles/r4t_mlp_prefetch.txt)
-template <int KS, int PD = 2>
+// GEO / RX (ABI 20): the frustum coordinates generated in the prologue and the residual read
+// from the NCHW image features in the epilogue (cmt_hip.h cmt_mlp2_args.geo_i2l / rx)
+template <int KS, int PD = 2, bool GEO = false, bool RX = false>
 __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
     constexpr int W1_BLK = KS * 2 * FRAG_B;
-    __shared__ __attribute__((aligned(16))) char lds[2 * W1_BLK + 2 * W2_BLK + MAX_HD * 4];
+    __shared__ __attribute__((aligned(16))) char lds[2 * W1_BLK + 2 * W2_BLK + MAX_HD * 4 + (GEO ? 64 * 4 : 0)];
     char* const s1 = lds;                 // W1 ring: 2 x W1_BLK
     char* const s2 = lds + 2 * W1_BLK;    // W2 ring: 2 x W2_BLK
     float* const sb1 = (float*)(lds + 2 * W1_BLK + 2 * W2_BLK);   // b1 (a global load per block
@@ -97,12 +99,62 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
     for (int i = tid; i < a.Hd / 4; i += 64 * MW) *(f32x4*)(sb1 + 4 * i) = *(const f32x4*)(a.b1 + 4 * i);
 
     // this lane's row of A as the B operand of fc1 (k = 16 ks + 8 lh + j), hi and lo planes
-    const pair_t* Ar = (const pair_t*)a.A + (int64_t)z * a.a_bstride + (int64_t)row * a.lda;
     pair8_t ah[KS], al[KS];
+    const int ghw = GEO || RX ? a.geo_h * a.geo_w : 1;
+    const int gview = row / ghw, gpix = row - gview * ghw;      // GEO / RX: view and pixel of the row
+    const int gimg = z * (a.M / ghw) + gview;
+#ifndef CMT_MLP_DIAG
+#define CMT_MLP_DIAG 0   // dev diagnostics (wrong results): 1 no C2 stores, 2 no NCHW loads, 4 no coordinates
+#endif
+    if constexpr (GEO && (CMT_MLP_DIAG & 4)) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        ah[ks] = *(const pair8_t*)(Ar + 16 * ks + 8 * lh);
-        al[ks] = *(const pair8_t*)(Ar + a.K + 16 * ks + 8 * lh);
+        for (int ks = 0; ks < KS; ++ks) { ah[ks] = pair8_t{}; al[ks] = pair8_t{}; }
+    } else if constexpr (GEO) {
+        // rv_pe_coords_kernel8's arithmetic (elementwise.hip), element k = 3 depth + coordinate.
+        // Element 16 ks + 8 lh + j is coordinate (ks + 2 lh + j) mod 3: with the matrix rows and
+        // the range rotated by 2 lh once per lane, the row index (ks + j) mod 3 is a compile-time
+        // constant (a lane-divergent register-array index is a waterfall loop); the depth values
+        // d (one fp32 division each) come from an LDS table the workgroup fills first
+        const int gw = gpix % a.geo_w, gh = gpix / a.geo_w;
+        const float u = (float)gw * a.geo_pad_w / (float)a.geo_w;
+        const float v = (float)gh * a.geo_pad_h / (float)a.geo_h;
+        const float* Mx = a.geo_i2l + (int64_t)gimg * 16;
+        float mr[3][4], plo[3], pspan[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int src0 = q, src1 = (q + 2) % 3;        // lh = 0 / lh = 1
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mr[q][i] = lh ? Mx[src1 * 4 + i] : Mx[src0 * 4 + i];
+            plo[q] = lh ? a.geo_pc[src1] : a.geo_pc[src0];
+            pspan[q] = lh ? a.geo_pc[3 + src1] - a.geo_pc[src1] : a.geo_pc[3 + src0] - a.geo_pc[src0];
+        }
+        float* dtab = sb1 + MAX_HD;                         // 3 D depth values after b1 (KS * 16 / 3 <= 64)
+        if (tid < a.geo_D) dtab[tid] = 1.f + (float)tid * (a.geo_depth_max - 1.f) / (float)a.geo_D;
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int kk = 16 * ks + 8 * lh + j;
+                const int r = (ks + j) % 3;                 // the rotated row: compile-time
+                const float d = dtab[kk / 3];
+                const float c0 = u * d, c1 = v * d;
+                float s = mr[r][0] * c0;
+                s = fmaf(mr[r][1], c1, s);
+                s = fmaf(mr[r][2], d, s);
+                s = fmaf(mr[r][3], 1.f, s);
+                const float x = (s - plo[r]) / pspan[r];
+                const pair_t h = (pair_t)x;
+                ah[ks][j] = h;
+                al[ks][j] = (pair_t)(x - (float)h);
+            }
+    } else {
+        const pair_t* Ar = (const pair_t*)a.A + (int64_t)z * a.a_bstride + (int64_t)row * a.lda;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            ah[ks] = *(const pair8_t*)(Ar + 16 * ks + 8 * lh);
+            al[ks] = *(const pair8_t*)(Ar + a.K + 16 * ks + 8 * lh);
+        }
     }
 
     f32x16 oacc[NOT], hacc;
@@ -196,6 +248,66 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
     barrier_mem();
     fc2_fc1(nhb - 1, std::false_type{});   // the last block: fc2 only
 
+    if constexpr (RX) {
+        // ---- fused camera rows: the memory-row pair (C2) from the NCHW features and
+        // out = acc + (b2 + pair value) (C), both staged through LDS per column quarter so every
+        // global store is 16 contiguous bytes of a 128-byte row segment (8 lanes per row)
+        __syncthreads();   // every wave is past its last weight-ring read: the rings become staging
+        char* const stg = lds + wave * 16384;            // 4 slices [32 rows][64 cols] f16: C hi / lo, C2 hi / lo
+        const float* xrow = a.rx + (int64_t)gimg * NOUT * ghw + gpix;
+        const int mw0 = blockIdx.x * MROWS + wave * 32;  // the wave's first row
+        bool bad = false;
+        typedef pair_t p4 __attribute__((ext_vector_type(4)));
+        auto sw = [](int r, int c16) { return r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4); };
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int ot = 2 * q + tt;
+                    const int n = ot * 32 + 8 * g + 4 * lh;
+                    const f32x4 bv = *(const f32x4*)(a.b2 + n);
+                    p4 h2, l2, hc, lc;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        // the pair cmt_nchw_to_rows writes, and its value as the pair R row reads back
+                        const float x = (CMT_MLP_DIAG & 2) ? 0.f : xrow[(int64_t)(n + e) * ghw];
+                        bad |= f16_unrepresentable(x);
+                        h2[e] = (pair_t)x;
+                        l2[e] = (pair_t)(x - (float)h2[e]);
+                        const float rv = (float)h2[e] + (float)l2[e];
+                        const float v = oacc[ot][4 * g + e] + (bv[e] + rv);
+                        hc[e] = (pair_t)v;
+                        lc[e] = (pair_t)(v - (float)hc[e]);
+                    }
+                    const int off = sw(lr, 4 * tt + g) + 8 * lh;
+                    *(p4*)(stg + off) = hc;
+                    *(p4*)(stg + 4096 + off) = lc;
+                    *(p4*)(stg + 8192 + off) = h2;
+                    *(p4*)(stg + 12288 + off) = l2;
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = 8 * i + (lane >> 3), ch = lane & 7;
+                const int mr = mw0 + r;
+                const int off = sw(r, ch);
+                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                const u4 v0 = *(const u4*)(stg + off), v1 = *(const u4*)(stg + 4096 + off);
+                const u4 v2 = *(const u4*)(stg + 8192 + off), v3 = *(const u4*)(stg + 12288 + off);
+                if (mr < a.M && !(CMT_MLP_DIAG & 1)) {
+                    pair_t* cr = (pair_t*)a.C + (int64_t)z * a.c_bstride + (int64_t)mr * a.ldc + 64 * q + 8 * ch;
+                    pair_t* c2 = (pair_t*)a.C2 + (int64_t)z * a.c2_bstride + (int64_t)mr * a.ldc2 + 64 * q + 8 * ch;
+                    *(u4*)cr = v0;
+                    *(u4*)(cr + NOUT) = v1;
+                    *(u4*)c2 = v2;
+                    *(u4*)(c2 + NOUT) = v3;
+                }
+            }
+        }
+        raise_range_flag(a.range_flag, bad);
+        return;
+    }
     // ---- epilogue: out = acc + (b2 + R) (cmt_gemm's order), row lr, columns 32 ot + 8 g + 4 lh + 0..3
     if (m >= a.M) return;
     const char* Rrow = nullptr;
@@ -243,8 +355,8 @@ extern "C" int cmt_mlp2_x3(const cmt_mlp2_args* ap, void* stream) {
     CMT_REQUIRE(a.K > 0 && a.K % 16 == 0 && a.K <= 192, "cmt_mlp2_x3: K must be a multiple of 16, at most 192");
     CMT_REQUIRE(a.Hd > 0 && a.Hd % 32 == 0 && a.Hd <= MAX_HD,
                 "cmt_mlp2_x3: the hidden width must be a multiple of 32, at most 2048");
-    CMT_REQUIRE(a.A && a.W1p && a.W2p && a.b1 && a.b2 && a.C, "cmt_mlp2_x3: null pointer");
-    CMT_REQUIRE(a.lda >= 2 * a.K && a.lda % 8 == 0 && a.a_bstride % 8 == 0,
+    CMT_REQUIRE((a.A || a.geo_i2l) && a.W1p && a.W2p && a.b1 && a.b2 && a.C, "cmt_mlp2_x3: null pointer");
+    CMT_REQUIRE(a.geo_i2l || (a.lda >= 2 * a.K && a.lda % 8 == 0 && a.a_bstride % 8 == 0),
                 "cmt_mlp2_x3: A pair rows need lda >= 2K, 16-byte aligned");
     CMT_REQUIRE(a.c_dtype == CMT_F32 || a.c_dtype == CMT_F16P, "cmt_mlp2_x3: C must be fp32 or an f16 pair");
     CMT_REQUIRE(a.c_dtype == CMT_F32 ? a.ldc >= NOUT && a.ldc % 4 == 0 && a.c_bstride % 4 == 0
@@ -259,6 +371,16 @@ extern "C" int cmt_mlp2_x3(const cmt_mlp2_args* ap, void* stream) {
                 "cmt_mlp2_x3: A / packs / biases must be 16-byte aligned");
     const dim3 grid((unsigned)cdiv(a.M, MROWS), (unsigned)a.batch);
     hipStream_t s = (hipStream_t)stream;
+    if (a.geo_i2l || a.rx) {
+        CMT_REQUIRE(a.geo_i2l && a.rx && a.C2 && a.K == 192 && a.geo_D * 3 == a.K && a.geo_h > 0 && a.geo_w > 0 &&
+                        a.M % (a.geo_h * a.geo_w) == 0 && a.c_dtype == CMT_F16P && a.R == nullptr &&
+                        a.ldc2 >= 2 * NOUT && a.ldc2 % 4 == 0 && a.c2_bstride % 4 == 0 &&
+                        (uintptr_t)a.C2 % 8 == 0,
+                    "cmt_mlp2_x3: the fused camera-row form takes geo_i2l, rx and C2 together, K = 3 geo_D = 192, "
+                    "M a multiple of geo_h * geo_w, a pair C and no R");
+        mlp2_x3_kernel<12, 2, true, true><<<grid, 64 * MW, 0, s>>>(a);
+        return cmt_check_launch("cmt_mlp2_x3");
+    }
     switch (a.K / 16) {
 #define MLP_K(KS) case KS: mlp2_x3_kernel<KS><<<grid, 64 * MW, 0, s>>>(a); break;
         MLP_K(1) MLP_K(2) MLP_K(3) MLP_K(4) MLP_K(5) MLP_K(6) MLP_K(7) MLP_K(8) MLP_K(9) MLP_K(10) MLP_K(11)

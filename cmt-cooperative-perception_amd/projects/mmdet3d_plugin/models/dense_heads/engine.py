@@ -287,6 +287,30 @@ class HeadEngineMixin:
                     R=R, ldr=C if R is not None else 0, r_bstride=Nk * C if R is not None else 0,
                     r_offset=offset * C)
 
+    def _rv_geo_ok(self, x_img, pk, prec):
+        """The camera memory rows in one launch (cmt_mlp2_x3's fused form, ABI 20): the one-launch
+        MLP with the reference's depth_num = 64 (K = 192) at the split policy."""
+        return (OPTIONS.rv_geo and self._rv_fused(pk) is not None and prec.gemm == SPLIT
+                and 3 * self.depth_num == 192 and x_img.shape[1] == self.hidden_dim)
+
+    def _rv_rows_geo(self, x_img, metas, B, Nk, offset, pk, mem, pos, cams):
+        """rv_embedding over the frustum coordinates (cmt_head.py:417-433, 297-301) and the
+        camera memory rows "(bs v) c h w -> bs (v h w) c" (cmt_transformer.py:104-105) in ONE
+        launch: the coordinates are generated in the MLP's prologue from the inverse camera
+        matrices, the image features read as NCHW in its epilogue, where they become the memory
+        rows (mem) and the residual of lowp(memory + pos) (pos)."""
+        C = self.hidden_dim
+        BV, _, h, w = x_img.shape
+        pad_h, pad_w, _ = metas[0]["pad_shape"][0]
+        _, b0, w2, b2 = pk["rv"]
+        fused = self._rv_fused(pk)
+        M = BV // B * h * w
+        geo = dict(i2l=cams[1], h=h, w=w, D=self.depth_num, pad_h=float(pad_h), pad_w=float(pad_w),
+                   depth_max=float(self.pc_range[3]), pc_range=self.pc_range)
+        native.mlp2(None, fused[0], b0, fused[1], b2, pos, M=M, K=3 * self.depth_num, Hd=w2.shape[-1], batch=B,
+                    c_offset=offset * C, c_bstride=Nk * C, geo=geo, rx=x_img.contiguous().float(), C2=mem,
+                    c2_offset=offset * C, c2_bstride=Nk * C, range_flag=self._range_flag(x_img.device))
+
     def _rv_pe_into(self, pos, x_img, metas, B, Nk, offset, pk, R=None, cams=None):
         self._rv_pe_out(self._rv_pe_hidden(x_img, metas, B, pk, cams=cams), pos, B, Nk, offset, pk, R=R)
 
@@ -415,9 +439,16 @@ class HeadEngineMixin:
             # RV encoder's first half on the main stream, ahead of the conv: on the second stream
             # its kernels share the chip with the conv's and RV fc2 waits for them
             rv_main = use_img and fuse_bev
-            if rv_main:
+            # the camera memory rows in one launch after the conv (ABI 20): no coordinates or
+            # layout launches ahead of the conv, no cross-stream wait before the RV MLP; the
+            # second stream forks before the conv but is captured after it, so the conv takes the
+            # chip first (profiles/r5_experiments.txt r5k / r5l)
+            geo = rv_main and self._rv_geo_ok(x_img, pk, prec)
+            if rv_main and not geo:
                 hr = self._rv_pe_hidden(x_img, metas, B, pk, cams=cams)
             side.wait_stream(main)
+            if geo:
+                self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=P)
             ready = torch.cuda.Event()
             bev_ready = torch.cuda.Event()
             with torch.cuda.stream(side):
@@ -427,7 +458,7 @@ class HeadEngineMixin:
                 # kept pack: no kernel), not for the RV encoder's first half -- whose kernels
                 # cannot start until shared_conv's workgroups leave the CUs
                 bev_ready.record(side)
-                if use_img:
+                if use_img and not geo:
                     native.nchw_to_rows(x_img.contiguous().float(), mem, nb=B, nv=V, C=C, HW=hw, ldy=C,
                                         range_flag=self._range_flag(x_img.device),
                                         rows_per_batch=Nk, row_offset=HW)
@@ -440,15 +471,18 @@ class HeadEngineMixin:
             for t in (qpos, hb, hr):
                 if t is not None:
                     t.record_stream(main)
-            if use_bev and fuse_bev:
-                self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=P)
-            elif use_bev:
-                self._shared_conv_into(x, mem, Nk, pk, prec)
-                main.wait_event(bev_ready)
-                self._bev_pos_out(hb, pos, B, Nk, pk, R=R)
-            main.wait_event(ready)
-            if use_img:
-                self._rv_pe_out(hr, pos, B, Nk, HW, pk, R=R)
+            if geo:
+                self._rv_rows_geo(x_img, metas, B, Nk, HW, pk, mem, pos, cams)
+            else:
+                if use_bev and fuse_bev:
+                    self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=P)
+                elif use_bev:
+                    self._shared_conv_into(x, mem, Nk, pk, prec)
+                    main.wait_event(bev_ready)
+                    self._bev_pos_out(hb, pos, B, Nk, pk, R=R)
+                main.wait_event(ready)
+                if use_img:
+                    self._rv_pe_out(hr, pos, B, Nk, HW, pk, R=R)
         else:
             if use_bev and fuse_bev:
                 self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=self._bev_pos_rows(H, W, pk))

@@ -29,7 +29,7 @@ C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
 ATTN_KEEP_PARTIALS = 2048   # cmt_hip.h CMT_ATTN_KEEP_PARTIALS (ABI 19)
 CHAIN_XSPLITS = 8           # the split count chain B1 combines (cmt_chain_args.xsplits)
-ABI_VERSION = 19
+ABI_VERSION = 20
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -140,7 +140,10 @@ class Mlp2Args(ctypes.Structure):
                 ("A", _vp), ("lda", _i64), ("a_bstride", _i64),
                 ("W1p", _vp), ("b1", _vp), ("W2p", _vp), ("b2", _vp),
                 ("R", _vp), ("ldr", _i64), ("r_bstride", _i64), ("r_dtype", _int),
-                ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int)]
+                ("C", _vp), ("ldc", _i64), ("c_bstride", _i64), ("c_dtype", _int),
+                ("geo_i2l", _vp), ("geo_h", _int), ("geo_w", _int), ("geo_D", _int), ("geo_pad_h", _flt),
+                ("geo_pad_w", _flt), ("geo_depth_max", _flt), ("geo_pc", _flt * 6),
+                ("rx", _vp), ("C2", _vp), ("ldc2", _i64), ("c2_bstride", _i64), ("range_flag", _vp)]
 
 
 STRUCTS = {"gemm": GemmArgs, "attn": AttnArgs, "ln": LnArgs, "chain": ChainArgs, "gemm_ex": GemmExArgs,
@@ -382,16 +385,38 @@ def mlp2_pack(W1, W2):
 
 
 def mlp2(A, W1p, b1, W2p, b2, C, *, M, K, Hd, R=None, batch=1, a_bstride=0, c_offset=0, c_bstride=0,
-         r_offset=0, r_bstride=0):
+         r_offset=0, r_bstride=0, geo=None, rx=None, C2=None, c2_offset=0, c2_bstride=0, range_flag=None):
     """C = Linear2(ReLU(Linear1(A) + b1)) + b2 (+ R) in one launch (cmt_mlp2_x3):
     A pair rows [.., 2, K]; packs from mlp2_pack; C / R fp32 [.., 256] or pair
-    [.., 2, 256] rows.  Offsets and strides are LOGICAL (rows of the operand)."""
-    _dev(A, W1p, b1, W2p, b2, C, R)
-    if A.dtype != torch.uint16 or W1p.dtype != torch.uint16 or W2p.dtype != torch.uint16:
+    [.., 2, 256] rows.  Offsets and strides are LOGICAL (rows of the operand).
+    ABI 20, the camera memory rows in one launch: geo = dict(i2l, h, w, D, pad_h, pad_w,
+    depth_max, pc_range) generates A (the _rv_pe frustum coordinates; A is then None), rx (NCHW
+    fp32 image features) replaces R, and C2 (pair rows) receives the memory rows themselves."""
+    _dev(A, W1p, b1, W2p, b2, C, R, rx, C2, range_flag)
+    if (A is not None and A.dtype != torch.uint16) or W1p.dtype != torch.uint16 or W2p.dtype != torch.uint16:
         raise RuntimeError("mlp2: A and the packs must be split pairs (torch.uint16)")
+    if (geo is None) != (rx is None) or (geo is None) != (C2 is None) or (geo is None) == (A is None):
+        raise RuntimeError("mlp2: give A, or geo + rx + C2 (the fused camera-row form)")
     g = Mlp2Args()
     g.M, g.K, g.Hd, g.N, g.batch = M, K, Hd, 256, batch
-    g.A, g.lda, g.a_bstride = A.data_ptr(), lstride(A) * 2, a_bstride * 2
+    if A is not None:
+        g.A, g.lda, g.a_bstride = A.data_ptr(), lstride(A) * 2, a_bstride * 2
+    else:
+        _dev(geo["i2l"])
+        if rx.dtype != torch.float32 or not rx.is_contiguous() or C2.dtype != torch.uint16:
+            raise RuntimeError("mlp2: rx must be contiguous NCHW fp32, C2 pair rows")
+        g.geo_i2l = geo["i2l"].data_ptr()
+        g.geo_h, g.geo_w, g.geo_D = geo["h"], geo["w"], geo["D"]
+        g.geo_pad_h, g.geo_pad_w, g.geo_depth_max = geo["pad_h"], geo["pad_w"], geo["depth_max"]
+        for i in range(6):
+            g.geo_pc[i] = float(geo["pc_range"][i])
+        g.rx = rx.data_ptr()
+        g.C2 = C2.data_ptr() + c2_offset * 2 * C2.element_size()   # logical elements (pair: 2 words each)
+        g.ldc2, g.c2_bstride = lstride(C2) * 2, c2_bstride * 2
+        if range_flag is not None:
+            if range_flag.dtype != torch.int32:
+                raise RuntimeError("mlp2: range_flag must be an int32 device word")
+            g.range_flag = range_flag.data_ptr()
     g.W1p, g.b1, g.W2p, g.b2 = W1p.data_ptr(), b1.data_ptr(), W2p.data_ptr(), b2.data_ptr()
     sc = _ps(C)
     g.C = C.data_ptr() + c_offset * sc * C.element_size()

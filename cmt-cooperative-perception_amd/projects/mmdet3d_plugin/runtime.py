@@ -125,6 +125,8 @@ class Options:
     mlp_fused: bool        # CMT_MLP_FUSED=0: split rv_embedding as two GEMMs (hidden pair rows via HBM)
     chain_combine: bool    # CMT_CHAIN_COMBINE=0: split cross-attention combined by its own launch (pair rows
                            # via HBM) instead of inside chain B1
+    rv_geo: bool           # CMT_RV_GEO=0: the camera rows' frustum coordinates and layout pass as launches of
+                           # their own instead of inside the one-launch RV position MLP
 
 
 def _env_on(name):
@@ -133,7 +135,8 @@ def _env_on(name):
 
 OPTIONS = Options(side_stream=_env_on("CMT_SIDE_STREAM"), chain=_env_on("CMT_CHAIN"),
                   bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"), conv_halo=_env_on("CMT_CONV_HALO"),
-                  mlp_fused=_env_on("CMT_MLP_FUSED"), chain_combine=_env_on("CMT_CHAIN_COMBINE"))
+                  mlp_fused=_env_on("CMT_MLP_FUSED"), chain_combine=_env_on("CMT_CHAIN_COMBINE"),
+                  rv_geo=_env_on("CMT_RV_GEO"))
 
 
 @contextlib.contextmanager

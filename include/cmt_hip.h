@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 19
+#define CMT_ABI_VERSION 20
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -197,6 +197,21 @@ typedef struct cmt_mlp2_args {
     const void* W2p; const float* b2;
     const void* R; int64_t ldr; int64_t r_bstride; int r_dtype;
     void* C; int64_t ldc; int64_t c_bstride; int c_dtype;
+    /* ABI 20, the camera memory rows in one launch (each optional, NULL = off; K == 192):
+     * geo_i2l: A is not read but generated -- the _rv_pe frustum coordinates of
+     *   cmt_rv_pe_coords (cmt_head.py:417-432, the same arithmetic and f16-pair split): row r of
+     *   batch z is pixel r % (geo_h * geo_w) of view v = r / (geo_h * geo_w), V = M / (geo_h *
+     *   geo_w) views per batch element, inverse matrix geo_i2l[(z * V + v) * 16], geo_D = K / 3
+     *   depths up to geo_depth_max, geo_pc the point-cloud range;
+     * rx: the residual R is read from the NCHW fp32 image features instead (the camera memory
+     *   rows "(bs v) c h w -> bs (v h w) c", cmt_transformer.py:104-105): element n of row r is
+     *   rx[((z * V + v) * 256 + n) * geo_h * geo_w + pixel]; it enters as its f16 pair (the
+     *   rounding cmt_nchw_to_rows applies), those pair rows are written to C2 (ldc2 / c2_bstride
+     *   in 16-bit words: the memory rows themselves), and a value the pair format cannot carry
+     *   ORs 1 into *range_flag (optional) as cmt_nchw_to_rows_ex does. */
+    const float* geo_i2l; int geo_h, geo_w, geo_D; float geo_pad_h, geo_pad_w, geo_depth_max;
+    float geo_pc[6];
+    const float* rx; void* C2; int64_t ldc2; int64_t c2_bstride; int* range_flag;
 } cmt_mlp2_args;
 
 int cmt_mlp2_x3(const cmt_mlp2_args* args, void* stream);

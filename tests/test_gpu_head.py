@@ -482,6 +482,37 @@ def test_chain_combine_bit_exact(dev, parity_log):
                       "launch, bit-exact (900 queries, 13 056 keys, 2 layers)")
 
 
+def test_rv_rows_one_launch_bit_exact(dev, parity_log):
+    """OPTIONS.rv_geo (CMT_RV_GEO, ABI 20): the camera memory rows -- frustum coordinates,
+    rv_embedding and the "(bs v) c h w -> bs (v h w) c" layout -- in one cmt_mlp2_x3 launch
+    (coordinates generated in its prologue, NCHW features read in its epilogue) vs the
+    coordinates kernel + layout pass + one-launch MLP: the same arithmetic, so every output of
+    the head is bit-identical (fusion, 6 cameras, two frames of a batch)."""
+    from projects.mmdet3d_plugin import set_precision
+    from projects.mmdet3d_plugin import synthetic as S
+    head, cfg, _ = S.build_synthetic_head("cmt_fusion_nus", seed=4, num_query=64, num_layers=2,
+                                          grid_size=[256, 256, 40], device=dev)
+    x = S.synthetic_bev(2, 32, 32, seed=81).to(dev)
+    xi = S.synthetic_img(12, 8, 20, seed=82).to(dev)
+    metas = S.synthetic_metas(2, pad_shape=(128, 320, 3), seed=83)
+    outs = {}
+    set_precision("ref")
+    head.box_epilogue = False
+    try:
+        for on in (True, False):
+            with torch.no_grad(), options(rv_geo=on):
+                o = head([x], [xi], metas)[0][0]
+            torch.cuda.synchronize()
+            outs[on] = {k: v.clone() for k, v in o.items()}
+    finally:
+        head.box_epilogue = True
+    for k in KEYS:
+        assert torch.isfinite(outs[True][k]).all(), k
+        assert torch.equal(outs[True][k], outs[False][k]), (k, (outs[True][k] - outs[False][k]).abs().max().item())
+    parity_log.append("camera memory rows in one launch (coordinates + rv_embedding + layout) == three launches, "
+                      "bit-exact (fusion, batch 2, 6 cameras)")
+
+
 def test_bev_pos_hidden_cache(dev):
     """The input-independent first half of the BEV position MLP (pos2embed of
     the grid + bev_embedding[0] + ReLU) is kept like a weight pack: a forward
