@@ -4,7 +4,7 @@
 # WRITE_SIZE passes (separate; the roofline form: split combine as its own launch), the default
 # bench line and the coop training bench.
 set -uo pipefail
-TAG=${1:-r5final}
+TAG=${1:-r5zfinal}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
