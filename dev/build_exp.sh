@@ -2,7 +2,7 @@
 # Experiment libraries (dev only, never loaded by the product path): rebuild ONE source with
 # extra -D defines and link it with the product objects into lib/exp/libcmt_hip_<tag>.so.
 # Select one at run time with CMT_HIP_LIB=<path> (native.py).
-#   bash dev/build_exp.sh <tag> <source.hip> "-DCMT_ATTN_EXP=1 ..."
+#   bash dev/build_exp.sh <tag> <source.hip> "-DCMT_KV_SCHED=16 ..."   (dev-only defines: CMT_KV_SCHED, CMT_CONV_VAR, CMT_MLP_DIAG)
 set -euo pipefail
 TAG=$1; SRC=$2; DEFS=${3:-}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
