@@ -27,7 +27,14 @@ constexpr int TBK = 32;     // k-step
 constexpr int TLD = 36;     // padded LDS row (floats)
 constexpr int TNT = 256;
 
-enum { OP_KC = 0, OP_MC = 1, OP_SC = 2 };   // k-contiguous, row(m/n)-contiguous, scalar
+// k-contiguous, row(m/n)-contiguous, scalar; OP_IM: the implicit im2col of a 3x3 / pad 1 conv on
+// NHWC rows (bf16x3 GEMM only): element (n, k) = X[token k shifted by tap n / Cin][channel n % Cin]
+enum { OP_KC = 0, OP_MC = 1, OP_SC = 2, OP_IM = 3 };
+
+// OP_IM's geometry: H x W images of Cin channels, rows (img * H + y) * W + x
+struct X3Conv {
+    int H, W, Cin;
+};
 
 // Stage a 64-row x 32-k tile of X (rows r0.., k0..) into LDS [row][TLD]:
 // element (r, k) at X[r * s_r + k * s_k].
@@ -129,14 +136,56 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(cmt_gemm_ex_args a, int kc
 // relative per product (the dropped lo*lo term and the pair's representation),
 // at 3 x 32 cycles per 16 k against 8 x 64 for the f32 MFMA (5.3x the rate).
 // Tiles 64 x 64 x 32 as gemm_ex_kernel, staged through registers (any operand
-// stride) into bf16 LDS images [row][32 k] (64-byte rows, 16-byte chunks
-// XOR-swizzled by (row >> 2) & 3), hi and lo planes.
+// stride) into bf16 LDS images, hi and lo planes: [row][32 k] (64-byte rows, 16-byte
+// chunks XOR-swizzled by (row >> 2) & 3) for k-contiguous and scalar operands,
+// [32 k][row] for row-contiguous ones (x3_timg below).
 // ---------------------------------------------------------------------------
 constexpr int X3RB = 64;   // bytes per staged row (32 k of bf16)
 
 __device__ __forceinline__ int x3_off(int row, int k) {
     return row * X3RB + ((((k >> 3) ^ ((row >> 2) & 3))) << 4) + (k & 7) * 2;
 }
+// Row-contiguous operands (OP_MC, OP_IM: four consecutive rows per fetched vector) are staged
+// TRANSPOSED, [k][row] -- two 32-row halves of 32 k-rows x 64 bytes, 16-byte chunks XOR-swizzled by
+// (k >> 2) & 3 -- so each fetched vector leaves as one 8-byte LDS write per plane (the [row][k]
+// image took four conflicted 2-byte writes), and the MFMA operand comes back through
+// ds_read_b64_tr_b16.  Both images hand lane (lr, lh) of a 16-deep k slice the k order
+// 4 lh + 0..3, 8 + 4 lh + 0..3 (the transposed read's), so the two operands agree.  Conv-shaped
+// weight gradient 950 -> 611 us, K/V-shaped 77 -> 61 us (profiles/r5_experiments.txt r5af).
+template <int MODE>
+constexpr bool x3_timg() {
+    return MODE == 1 || MODE == 3;   // OP_MC, OP_IM
+}
+__device__ __forceinline__ int x3_toff(int row, int k) {
+    return ((row >> 5) << 11) + k * 64 + (((((row & 31) >> 3) ^ ((k >> 2) & 3))) << 4) + (row & 7) * 2;
+}
+// the 32x32x16 MFMA operand of rows [r0, r0 + 32) (lane row = r) and k slice 16 kk .. 16 kk + 15;
+// PERM: the transposed read's k order (some operand of the product is transposed), else the
+// natural 8 lh + 0..7 in one ds_read_b128
+template <int MODE, bool PERM>
+__device__ __forceinline__ bf16x8 x3_frag(const char* img, int r0, int r, int kk, int lane) {
+    const int lh = lane >> 5;
+    if constexpr (x3_timg<MODE>()) {
+        const char* base = img + ((r0 >> 5) << 11);
+        const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+        const int c = 2 * (g & 1) + (pp >> 1);
+        const int ka = 16 * kk + 4 * lh + qq, kb = ka + 8;
+        const char* pa = base + ka * 64 + ((c ^ ((ka >> 2) & 3)) << 4) + 8 * (pp & 1);
+        const char* pb = base + kb * 64 + ((c ^ ((kb >> 2) & 3)) << 4) + 8 * (pp & 1);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)pa);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((CMT_LDS s16v4_lds*)pb);
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    } else if constexpr (PERM) {
+        const s16x4 lo = *(const s16x4*)(img + x3_off(r, 16 * kk + 4 * lh));
+        const s16x4 hi = *(const s16x4*)(img + x3_off(r, 16 * kk + 8 + 4 * lh));
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    } else {
+        return *(const bf16x8*)(img + x3_off(r, 16 * kk + 8 * lh));
+    }
+}
+
 __device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
     hi = (bf16_t)x;
     lo = (bf16_t)(x - (float)hi);
@@ -147,8 +196,28 @@ __device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
 // thread's 8 elements into registers, put_x3 splits them into the bf16 hi / lo LDS images.
 template <int MODE>
 __device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict__ X, int64_t s_r, int64_t s_k,
-                                         int rows, int K, int r0, int k0, int tid) {
-    if (MODE == OP_KC) {
+                                         int rows, int K, int r0, int k0, int tid, const X3Conv& cv = X3Conv{}) {
+    if (MODE == OP_IM) {
+        // OP_MC's thread layout: 4 consecutive n (channels of one tap, Cin % 4 == 0) at one token
+        const int hw = cv.H * cv.W;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + TNT * i;
+            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int gr = r0 + r, gk = k0 + k;
+            f32x4 t = {0.f, 0.f, 0.f, 0.f};
+            if (gk < K && gr < rows) {
+                const int tap = gr / cv.Cin, c = gr - tap * cv.Cin;
+                const int img = gk / hw, pix = gk - img * hw;
+                const int py = pix / cv.W;
+                const int y = py + tap / 3 - 1, x = pix - py * cv.W + tap % 3 - 1;
+                if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
+                    t = *(const f32x4*)(X + (((int64_t)img * cv.H + y) * cv.W + x) * cv.Cin + c);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = t[j];
+        }
+    } else if (MODE == OP_KC) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int idx = tid + TNT * i;
@@ -210,18 +279,21 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
             *(b4*)(hi + x3_off(r, c)) = h;
             *(b4*)(lo + x3_off(r, c)) = l;
         }
-    } else if (MODE == OP_MC) {
+    } else if (x3_timg<MODE>()) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int idx = tid + TNT * i;
             const int k = idx >> 4, r = (idx & 15) * 4;
+            b4 h, l;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                bf16_t h, l;
-                split_bf16(v[4 * i + j], h, l);
-                *(bf16_t*)(hi + x3_off(r + j, k)) = h;
-                *(bf16_t*)(lo + x3_off(r + j, k)) = l;
+                bf16_t hj, lj;
+                split_bf16(v[4 * i + j], hj, lj);
+                h[j] = hj;
+                l[j] = lj;
             }
+            *(b4*)(hi + x3_toff(r, k)) = h;
+            *(b4*)(lo + x3_toff(r, k)) = l;
         }
     } else {
 #pragma unroll
@@ -240,7 +312,7 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
 template <int MODE>
 __device__ __forceinline__ int x3_row(int e, int tid) {
     if (MODE == OP_KC) return ((tid + TNT * (e >> 2)) >> 3);
-    if (MODE == OP_MC) return ((tid + TNT * (e >> 2)) & 15) * 4 + (e & 3);
+    if (MODE == OP_MC || MODE == OP_IM) return ((tid + TNT * (e >> 2)) & 15) * 4 + (e & 3);
     return (tid + TNT * e) >> 5;
 }
 
@@ -257,7 +329,7 @@ __device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
 }
 
 template <int AM, int BM>
-__global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int kchunk) {
+__global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int kchunk, X3Conv cv) {
     __shared__ __attribute__((aligned(16))) char As[2][2][64 * X3RB];   // [buffer][hi, lo]
     __shared__ __attribute__((aligned(16))) char Bs[2][2][64 * X3RB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -280,7 +352,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
 #pragma unroll
     for (int e = 0; e < 8; ++e) rs[e] = 0.f;
     fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
-    fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid);
+    fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid, cv);
     int buf = 0;
     for (int k0 = kb; k0 < ke; k0 += TBK, buf ^= 1) {
         if (rowsum) {
@@ -293,15 +365,15 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
         __syncthreads();
         if (k0 + TBK < ke) {
             fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, k0 + TBK, tid);
-            fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid);
+            fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid, cv);
         }
+        constexpr bool perm = x3_timg<AM>() || x3_timg<BM>();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            const int c = 16 * kk + 8 * lh;
-            const bf16x8 ah = *(const bf16x8*)(As[buf][0] + x3_off(ar, c));
-            const bf16x8 al = *(const bf16x8*)(As[buf][1] + x3_off(ar, c));
-            const bf16x8 bh = *(const bf16x8*)(Bs[buf][0] + x3_off(br, c));
-            const bf16x8 bl = *(const bf16x8*)(Bs[buf][1] + x3_off(br, c));
+            const bf16x8 ah = x3_frag<AM, perm>(As[buf][0], wm * 32, ar, kk, lane);
+            const bf16x8 al = x3_frag<AM, perm>(As[buf][1], wm * 32, ar, kk, lane);
+            const bf16x8 bh = x3_frag<BM, perm>(Bs[buf][0], wn * 32, br, kk, lane);
+            const bf16x8 bl = x3_frag<BM, perm>(Bs[buf][1], wn * 32, br, kk, lane);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
@@ -724,7 +796,7 @@ int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
     hipStream_t s = (hipStream_t)stream;
 #define GX(AM, BM)                                                       \
     do {                                                                 \
-        if (x3) gemm_ex3_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk); \
+        if (x3) gemm_ex3_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{}); \
         else gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk);     \
     } while (0)
     switch (am * 3 + bm) {
@@ -739,6 +811,29 @@ int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
 
 extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, false); }
 extern "C" int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, true); }
+
+// shared_conv's weight gradient as the bf16x3 GEMM dW[cout][n] = sum_r dY[r][cout] im2col(X)[r][n]
+// with the im2col operand gathered inside the kernel (OP_IM): no [rows, 9 Cin] matrix
+extern "C" int cmt_conv3x3_wgrad_bf16x3(const float* X, const float* dY, float* dW, int nimg, int H, int W, int Cin,
+                                        int Cout, int ksplit, void* stream) {
+    CMT_REQUIRE(X && dY && dW && nimg > 0 && H > 0 && W > 0 && Cout > 0, "cmt_conv3x3_wgrad_bf16x3: bad arguments");
+    CMT_REQUIRE(Cin > 0 && Cin % 4 == 0 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)dY & 15) == 0 && Cout % 4 == 0,
+                "cmt_conv3x3_wgrad_bf16x3: Cin and Cout multiples of 4, 16-byte aligned X / dY");
+    const int64_t rows = (int64_t)nimg * H * W;
+    CMT_REQUIRE(rows < (int64_t)1 << 31, "cmt_conv3x3_wgrad_bf16x3: too many rows");
+    cmt_gemm_ex_args a{};
+    a.M = Cout; a.N = 9 * Cin; a.K = (int)rows; a.batch = 1;
+    a.alpha = 1.f; a.beta = ksplit > 1 ? 1.f : 0.f;
+    a.A = dY; a.a_sm = 1; a.a_sk = Cout;    // A(m, k) = dY[k][m]: OP_MC
+    a.B = X;                                // B(n, k): the implicit im2col
+    a.C = dW; a.ldc = 9 * Cin;
+    a.ksplit = ksplit < 1 ? 1 : ksplit;
+    int kchunk = cdiv(cdiv(a.K, a.ksplit), TBK) * TBK;
+    a.ksplit = cdiv(a.K, kchunk);
+    const dim3 grid(cdiv(a.N, 64), cdiv(a.M, 64), a.ksplit);
+    gemm_ex3_kernel<OP_MC, OP_IM><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, X3Conv{H, W, Cin});
+    return cmt_check_launch("cmt_conv3x3_wgrad_bf16x3");
+}
 
 extern "C" int cmt_ln_train_fwd(const cmt_ln_train_args* ap, void* stream) {
     CMT_REQUIRE(ap && ap->rows > 0 && (ap->C == 64 || ap->C == 256), "cmt_ln_train_fwd: C must be 64 or 256");

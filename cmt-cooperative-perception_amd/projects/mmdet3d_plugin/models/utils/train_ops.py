@@ -188,12 +188,16 @@ class _Conv3x3(torch.autograd.Function):
         Cout = w.shape[0]
         dw = None
         if ctx.needs_input_grad[1]:
-            col = T.im2col3x3(x, B, H, W, Cin)                     # [rows, 9*Cin]
-            rows = col.shape[0]
-            ks = T._ksplit(rows, Cout, 9 * Cin)
-            dw = torch.zeros((Cout, 9 * Cin), dtype=torch.float32, device=x.device)
-            T.gemm_ex(dy.contiguous(), (1, Cout), col, (1, 9 * Cin), dw, M=Cout, N_=9 * Cin, K=rows, ldc=9 * Cin,
-                      beta=1.0, ksplit=max(ks, 2))
+            rows = B * H * W
+            ks = max(T._ksplit(rows, Cout, 9 * Cin), 2)
+            if T._gemm_mode == "bf16x3" and Cin % 4 == 0 and Cout % 4 == 0:
+                # the im2col operand gathered inside the GEMM (no [rows, 9 Cin] matrix)
+                dw = T.conv3x3_wgrad(x, dy, B, H, W, Cin, ks)
+            else:
+                col = T.im2col3x3(x, B, H, W, Cin)                 # [rows, 9*Cin]
+                dw = torch.zeros((Cout, 9 * Cin), dtype=torch.float32, device=x.device)
+                T.gemm_ex(dy.contiguous(), (1, Cout), col, (1, 9 * Cin), dw, M=Cout, N_=9 * Cin, K=rows,
+                          ldc=9 * Cin, beta=1.0, ksplit=ks)
         dx = None
         if ctx.needs_input_grad[0]:
             # dX = conv3x3(dY, W'), W'[cin][tap][cout] = W[cout][8 - tap][cin]: the transposed conv is the

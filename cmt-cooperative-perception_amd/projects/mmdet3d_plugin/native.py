@@ -29,7 +29,7 @@ C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
 ATTN_KEEP_PARTIALS = 2048   # cmt_hip.h CMT_ATTN_KEEP_PARTIALS (ABI 19)
 CHAIN_XSPLITS = 8           # the split count chain B1 combines (cmt_chain_args.xsplits)
-ABI_VERSION = 20
+ABI_VERSION = 21
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -220,6 +220,7 @@ def _load():
         "cmt_bn_relu_train_fwd": ([P(BnArgs), _vp], _int),
         "cmt_bn_relu_train_bwd": ([P(BnArgs), _vp], _int),
         "cmt_im2col3x3": ([_vp, _int, _int, _int, _int, _vp, _vp], _int),
+        "cmt_conv3x3_wgrad_bf16x3": ([_vp, _vp, _vp, _int, _int, _int, _int, _int, _int, _vp], _int),
         "cmt_det_loss": ([P(DetLossArgs), _vp], _int),
         "cmt_match_cost": ([P(MatchCostArgs), _vp], _int),
         "cmt_sumsq": ([_vp, _i64, _vp, _vp], _int),

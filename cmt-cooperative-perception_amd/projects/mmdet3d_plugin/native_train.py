@@ -9,7 +9,7 @@ import torch
 from . import native as N
 
 __all__ = ["gemm_ex", "set_train_gemm", "linear_fwd", "linear_bwd", "attn_train_fwd", "attn_train_bwd", "ln_train_fwd", "ln_train_bwd",
-           "bn_relu_train_fwd", "bn_relu_train_bwd", "im2col3x3", "det_loss", "match_cost", "sumsq", "adamw_step"]
+           "bn_relu_train_fwd", "bn_relu_train_bwd", "im2col3x3", "conv3x3_wgrad", "det_loss", "match_cost", "sumsq", "adamw_step"]
 
 
 def _ptr(t):
@@ -257,6 +257,18 @@ def im2col3x3(X, nimg, H, W, C):
     out = torch.empty((nimg * H * W, 9 * C), dtype=torch.float32, device=X.device)
     N._check(N.lib().cmt_im2col3x3(X.data_ptr(), nimg, H, W, C, out.data_ptr(), N._stream()), "cmt_im2col3x3")
     return out
+
+
+def conv3x3_wgrad(X, dY, nimg, H, W, Cin, ksplit):
+    """dW [Cout, 9 Cin] (tap-major) of the 3x3 / pad 1 conv on NHWC rows X [nimg*H*W, Cin] given
+    dY [nimg*H*W, Cout]: the bf16x3 GEMM with the im2col operand gathered in the kernel."""
+    _f32(X, dY)
+    X, dY = X.contiguous(), dY.contiguous()
+    Cout = dY.shape[1]
+    dW = (torch.zeros if ksplit > 1 else torch.empty)((Cout, 9 * Cin), dtype=torch.float32, device=X.device)
+    N._check(N.lib().cmt_conv3x3_wgrad_bf16x3(X.data_ptr(), dY.data_ptr(), dW.data_ptr(), nimg, H, W, Cin, Cout,
+                                              ksplit, N._stream()), "cmt_conv3x3_wgrad_bf16x3")
+    return dW
 
 
 def det_loss(logits, labels, label_w, boxes, targets, box_w, *, gamma, alpha, cls_weight, box_weight, cls_avg,

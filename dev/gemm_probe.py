@@ -47,5 +47,27 @@ def main():
               f"  (ks {T._ksplit(M, Nn, K)})  rel err {e_f:.1e} {e_x:.1e} {e_w:.1e}", flush=True)
 
 
+def conv_wgrad():
+    """shared_conv's weight gradient at the coop shape: im2col + GEMM vs the implicit form."""
+    torch.manual_seed(0)
+    lib = os.environ.get("CMT_HIP_LIB", "lib")
+    H = W = 180
+    Cin, Cout = 512, 256
+    x = torch.randn(H * W, Cin, device="cuda")
+    dy = torch.randn(H * W, Cout, device="cuda")
+    ks = max(T._ksplit(H * W, Cout, 9 * Cin), 2)
+
+    def im2col():
+        col = T.im2col3x3(x, 1, H, W, Cin)
+        dw = torch.zeros(Cout, 9 * Cin, device="cuda")
+        T.gemm_ex(dy, (1, Cout), col, (1, 9 * Cin), dw, M=Cout, N_=9 * Cin, K=H * W, ldc=9 * Cin, beta=1.0, ksplit=ks)
+        return dw
+    a, b = im2col(), T.conv3x3_wgrad(x, dy, 1, H, W, Cin, ks)
+    err = ((a - b).abs().max() / a.abs().max()).item()
+    print(f"{lib} conv_wgrad 180x180 {Cin}->{Cout} ks {ks}: im2col+gemm {timed(im2col, 5):8.1f} us  implicit "
+          f"{timed(lambda: T.conv3x3_wgrad(x, dy, 1, H, W, Cin, ks), 5):8.1f} us  rel diff {err:.1e}", flush=True)
+
+
 if __name__ == "__main__":
+    conv_wgrad()
     main()

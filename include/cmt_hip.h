@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 20
+#define CMT_ABI_VERSION 21
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -628,6 +628,13 @@ int cmt_bn_relu_train_bwd(const cmt_bn_args* args, void* stream);
 /* im2col of the 3x3 / pad 1 conv on NHWC rows (the weight-gradient operand of
  * shared_conv): out[(img*H+y)*W+x][tap*C + c], tap = 3*dy + dx. */
 int cmt_im2col3x3(const float* X, int nimg, int H, int W, int C, float* out, void* stream);
+/* The same weight gradient without the im2col matrix (ABI 21): dW[cout][tap*Cin + c]
+ * = sum over the nimg*H*W rows r of dY[r][cout] * im2col(X)[r][tap*Cin + c], the
+ * im2col elements gathered inside cmt_gemm_bf16x3_ex's kernel (its arithmetic);
+ * ksplit > 1 adds into dW with f32 atomics (zero it first), 1 overwrites it.
+ * Cin, Cout multiples of 4; X, dY 16-byte aligned. */
+int cmt_conv3x3_wgrad_bf16x3(const float* X, const float* dY, float* dW, int nimg, int H, int W, int Cin,
+                             int Cout, int ksplit, void* stream);
 
 /* FocalLoss(use_sigmoid, gamma, alpha) + L1Loss of one task / decoder layer
  * (mmdet 2.28.2; cmt_head.py:702-720, 777-812): out[0] = cls loss, out[1] =

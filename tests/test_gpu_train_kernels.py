@@ -213,6 +213,34 @@ def test_bn_relu_and_conv_weight_grad(dev):
     assert (bng.running_var.cpu().double() - bn.running_var).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("nimg,H,W,Cin,Cout,ks", [(2, 9, 11, 36, 20, 1), (1, 40, 37, 64, 128, 3), (1, 180, 180, 8, 4, 7)])
+def test_conv3x3_wgrad_implicit(dev, nimg, H, W, Cin, Cout, ks):
+    """cmt_conv3x3_wgrad_bf16x3 (ABI 21: the im2col operand gathered inside the bf16x3 GEMM) against
+    float64 conv2d's weight gradient and bitwise against the im2col matrix + cmt_gemm_bf16x3_ex at
+    ksplit 1 (the same products in the same order): ragged tiles (9 Cin = 324, Cout = 20), split-K,
+    a 32 400-row reduction."""
+    T = _T()
+    g = torch.Generator().manual_seed(H * W + Cin)
+    x = torch.randn(nimg, Cin, H, W, generator=g)
+    dy = torch.randn(nimg, Cout, H, W, generator=g)
+    wd = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    torch.nn.functional.conv2d(x.double(), wd, padding=1).backward(dy.double())
+    want = wd.grad.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)           # tap-major
+    xr = x.permute(0, 2, 3, 1).reshape(-1, Cin).contiguous().to(dev)
+    dyr = dy.permute(0, 2, 3, 1).reshape(-1, Cout).contiguous().to(dev)
+    got = T.conv3x3_wgrad(xr, dyr, nimg, H, W, Cin, ks)
+    torch.cuda.synchronize()
+    rows = nimg * H * W
+    err = (got.cpu().double() - want).abs().max().item()
+    assert err < 2 ** -15 * math.sqrt(rows) * 4, err
+    if ks == 1:
+        col = T.im2col3x3(xr, nimg, H, W, Cin)
+        ref = torch.empty(Cout, 9 * Cin, device=dev)
+        T.gemm_ex(dyr, (1, Cout), col, (1, 9 * Cin), ref, M=Cout, N_=9 * Cin, K=rows, ldc=9 * Cin, mode="bf16x3")
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), ref.cpu())
+
+
 @pytest.mark.parametrize("rows", [1000, 32400])
 def test_bn_relu_train_deterministic(dev, rows):
     """BatchNorm batch statistics and parameter gradients do not depend on the arrival order of
