@@ -55,6 +55,10 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
     return x;
 }
+// the dropout seed of the launch: seed (+ *seed_dev, ABI 22), resolved once per kernel into p.a.seed
+__device__ __forceinline__ void resolve_seed(AP& p) {
+    if (p.a.seed_dev) p.a.seed += *p.a.seed_dev;
+}
 __device__ __forceinline__ bool keep(const AP& p, int bh, int q, int k) {
     uint32_t h = mix32(p.a.seed ^ mix32((uint32_t)bh * 0x9e3779b9U + (uint32_t)q));
     h = mix32(h ^ (uint32_t)k * 0x85ebca6bU);
@@ -100,6 +104,7 @@ __device__ __forceinline__ void mma_acc(f32x16& acc, const float* zbase, const f
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void train_fwd_kernel(AP p) {
+    resolve_seed(p);
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) float Ks[KT * LDK];
     __shared__ __attribute__((aligned(16))) float Vs[KT * LDK];
@@ -243,6 +248,7 @@ __global__ __launch_bounds__(256) void train_delta_kernel(AP p) {
 
 // dQ: waves own 32 queries; key tiles [t0, t1) of this split; f32 atomics into dQ
 __global__ __launch_bounds__(256) void train_dq_kernel(AP p) {
+    resolve_seed(p);
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) float Ks[KT * LDK];
     __shared__ __attribute__((aligned(16))) float Vs[KT * LDK];
@@ -308,6 +314,7 @@ __global__ __launch_bounds__(256) void train_dq_kernel(AP p) {
 // [z qt_per, (z + 1) qt_per) of split z = blockIdx.z (f32 atomics into zeroed dK / dV when split:
 // the self-attention's ~1 100 keys alone are 9 x 8 workgroups)
 __global__ __launch_bounds__(256) void train_dkv_kernel(AP p, int qt_per) {
+    resolve_seed(p);
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) float Qs[KT * LDK];
     __shared__ __attribute__((aligned(16))) float Ds[KT * LDK];
@@ -468,6 +475,7 @@ __device__ __forceinline__ f32x16 mma16(h8_t a, h8_t b, f32x16 c) {
 
 template <bool MASK, bool DROP>
 __global__ __launch_bounds__(256) void train16_fwd_kernel(AP p) {
+    resolve_seed(p);
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) char Ks[KT * RMB];   // [key][d]
     __shared__ __attribute__((aligned(16))) char Vt[D * TRB];    // [d][key]
@@ -566,6 +574,7 @@ __global__ __launch_bounds__(256) void train16_fwd_kernel(AP p) {
 
 template <bool MASK, bool DROP>
 __global__ __launch_bounds__(256) void train16_dq_kernel(AP p) {
+    resolve_seed(p);
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) char Ks[KT * RMB];   // [key][d]
     __shared__ __attribute__((aligned(16))) char Kt[D * TRB];    // [d][key]
@@ -629,6 +638,7 @@ __global__ __launch_bounds__(256) void train16_dq_kernel(AP p) {
 
 template <bool MASK, bool DROP>
 __global__ __launch_bounds__(256) void train16_dkv_kernel(AP p) {
+    resolve_seed(p);
     const cmt_attn_train_args& a = p.a;
     __shared__ __attribute__((aligned(16))) char Qs[KT * RMB];   // [q][d]
     __shared__ __attribute__((aligned(16))) char Qt[D * TRB];    // [d][q]

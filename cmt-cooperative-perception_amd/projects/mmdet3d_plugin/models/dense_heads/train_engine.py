@@ -29,6 +29,7 @@ from scipy.optimize import linear_sum_assignment
 
 from ... import native
 from ... import native_train as T
+from ...runtime import OPTIONS
 from ..utils import train_ops as ops
 
 __all__ = ["HeadTrainMixin", "Boxes3D", "inverse_sigmoid"]
@@ -40,6 +41,19 @@ def _to_dev_async(t, dev):
     if t.device.type != "cpu" or torch.device(dev).type == "cpu":
         return t.to(dev)
     return t.pin_memory().to(dev, non_blocking=True)
+
+
+class _DecoderStep(torch.nn.Module):
+    """One agent's decoder training walk with its static switches, as a module whose parameters
+    are the decoder's (the callable torch.cuda.make_graphed_callables captures)."""
+
+    def __init__(self, decoder, **opts):
+        super().__init__()
+        self.decoder = decoder
+        self.opts = opts
+
+    def forward(self, tgt, qpos, mem, pos, seed):
+        return self.decoder.train_rows(tgt, qpos, mem, pos, seed_dev=seed, **self.opts)
 
 
 def inverse_sigmoid(x, eps=1e-5):
@@ -204,14 +218,41 @@ class HeadTrainMixin:
             poss.append(self._mlp_t(coords, self.rv_embedding).view(B, V * h * w_, C))
         return torch.cat(mems, 1), torch.cat(poss, 1)
 
-    def _decoder_t(self, tgt, qpos, mem, pos, mask_dict):
+    def _decoder_t(self, tgt, qpos, mem, pos, mask_dict, agent=0):
         """PETRTransformerDecoder with the training op walk (post-norm,
         petr_transformer.py:324-487; mmcv BaseTransformerLayer): the decoder's
-        own train_rows, with this head's DN padding and dropout switches."""
-        return self.transformer.decoder.train_rows(
-            tgt, qpos, mem, pos, pad=mask_dict["pad_size"] if mask_dict else 0,
-            group=mask_dict["single_pad"] if mask_dict else 0, dropout=self.train_dropout,
-            cross_fp16=self.train_cross_fp16)
+        own train_rows, with this head's DN padding and dropout switches.
+        With OPTIONS.train_graph (CMT_TRAIN_GRAPH=1; off by default) the walk's
+        forward and backward are HIP graphs (torch.cuda.make_graphed_callables)
+        captured once per agent and shape, the attention dropout seed drawn on
+        the device each step: the Python thread issues a coop step in 34.9
+        instead of 39.2 ms, but the step runs at 27.7 against 28.8 steps/s op
+        by op (profiles/r5_experiments.txt r5ai) -- the GPU, not the host, then
+        bounds it."""
+        pad = mask_dict["pad_size"] if mask_dict else 0
+        group = mask_dict["single_pad"] if mask_dict else 0
+        dec = self.transformer.decoder
+        if not (OPTIONS.train_graph and tgt.is_cuda and torch.is_grad_enabled()
+                and not torch.cuda.is_current_stream_capturing()):
+            return dec.train_rows(tgt, qpos, mem, pos, pad=pad, group=group, dropout=self.train_dropout,
+                                  cross_fp16=self.train_cross_fp16)
+        ins = (tgt, qpos, mem, pos)
+        # a graph reads its inputs, parameters and outputs at fixed addresses: one per agent slot
+        # (two agents' outputs are alive together), shape, DN geometry and parameter storage
+        key = (agent, pad, group, self.train_dropout, self.train_cross_fp16,
+               tuple((tuple(t.shape), t.requires_grad) for t in ins),
+               tuple(p.data_ptr() for p in dec.parameters()))
+        cache = self.__dict__.setdefault("_dec_graphs", {})
+        fn = cache.get(key)
+        seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=tgt.device)
+        if fn is None:
+            if len(cache) >= 8:          # shapes follow the GT count: keep the cache bounded
+                cache.clear()
+            step = _DecoderStep(dec, pad=pad, group=group, dropout=self.train_dropout,
+                                cross_fp16=self.train_cross_fp16)
+            samples = tuple(t.detach().clone().requires_grad_(t.requires_grad) for t in ins) + (seed.clone(),)
+            fn = cache[key] = torch.cuda.make_graphed_callables(step, samples, allow_unused_input=True)
+        return fn(*ins, seed)
 
     def _task_head_t(self, task, x, reference):
         """SeparateTaskHead (cmt_head.py:136-203) + box epilogue (501-513).
@@ -264,7 +305,7 @@ class HeadTrainMixin:
             if x_img is not None and self.rv_embedding is not None:
                 q = q + self._rv_query_embed_t(rp, metas)
             mem, pos = self._memory_t(x, x_img, metas, B)
-            decs.append(self._decoder_t(torch.zeros_like(q), q, mem, pos, mask_dict))
+            decs.append(self._decoder_t(torch.zeros_like(q), q, mem, pos, mask_dict, agent=len(decs)))
         # coop max fusion as the reference writes it (cmt_head_coop.py:388-389): torch.max over the
         # stacked agents routes each element's gradient to ONE agent (the max index), also on ties
         dec = decs[0] if len(decs) == 1 else torch.max(torch.stack(decs), 0).values

@@ -87,7 +87,7 @@ def dn_mask_params(mask):
     return pad, single
 
 
-def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cross_fp16=True, seed=0):
+def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cross_fp16=True, seed=0, seed_dev=None):
     """One PETRTransformerDecoderLayer in training (petr_transformer.py:374-487,
     mmcv BaseTransformerLayer post-norm walk) on the differentiable native ops:
     rows batch-first [B, N, C]; memk = memory + key_pos.  The self-attention
@@ -106,7 +106,7 @@ def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cros
     bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
     qi = tgt + qpos
     o = ops.attention(ops.linear(qi, wq, bq), ops.linear(qi, wk, bk), ops.linear(tgt, wv, bv), H, dn_pad=pad,
-                      dn_group=group, dropout_p=sa.attn_drop_p if dropout else 0.0, seed=seed)
+                      dn_group=group, dropout_p=sa.attn_drop_p if dropout else 0.0, seed=seed, seed_dev=seed_dev)
     tgt = ops.layer_norm(tgt + drop(ops.linear(o, w.out_proj.weight, w.out_proj.bias), sa.drop_prob),
                          nm[0].weight, nm[0].bias, nm[0].eps)
     w = ca.attn
@@ -456,18 +456,23 @@ class PETRTransformerDecoder(nn.Module):
             return (self._post(query) if self.post_norm is not None else query)[None]
         return torch.stack(inter)
 
-    def train_rows(self, tgt, qpos, mem, pos, *, pad=0, group=0, dropout=True, cross_fp16=True):
+    def train_rows(self, tgt, qpos, mem, pos, *, pad=0, group=0, dropout=True, cross_fp16=True, seed_dev=None):
         """The decoder in training on batch-first rows (tgt / qpos [B, Nq, C],
         mem / pos [B, Nk, C]): every layer (train_layer) and its post_norm
         (petr_transformer.py:347-371), nan_to_num (cmt_head.py:499) ->
-        [L, B, Nq, C], differentiable in every input and parameter."""
+        [L, B, Nq, C], differentiable in every input and parameter.
+        seed_dev: int32 device tensor [1], the attention dropout seed read on the device
+        (no host draw: the graph-captured form, train_engine._decoder_t)."""
         from . import train_ops as ops
         memk = mem + pos
         outs = []
-        seed0 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
+        if seed_dev is not None:
+            seed0 = 0
+        else:
+            seed0 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
         for li, lay in enumerate(self.layers):
             tgt = train_layer(lay, tgt, qpos, memk, mem, pad=pad, group=group, dropout=dropout,
-                              cross_fp16=cross_fp16, seed=seed0 + li)
+                              cross_fp16=cross_fp16, seed=seed0 + li, seed_dev=seed_dev)
             outs.append(ops.layer_norm(tgt, self.post_norm.weight, self.post_norm.bias, self.post_norm.eps))
         return torch.nan_to_num(torch.stack(outs))
 

@@ -76,14 +76,14 @@ class _Attention(torch.autograd.Function):
     """q [B, Nq, H*32], k / v [B, Nk, H*32] (contiguous rows) -> o [B, Nq, H*32]."""
 
     @staticmethod
-    def forward(ctx, q, k, v, H, scale, dn_pad, dn_group, fp16, dropout_p, seed):
+    def forward(ctx, q, k, v, H, scale, dn_pad, dn_group, fp16, dropout_p, seed, seed_dev):
         B, Nq, C = q.shape
         Nk = k.shape[1]
         o = torch.empty_like(q)
         lse = torch.empty((B * H * Nq,), dtype=torch.float32, device=q.device)
         kw = dict(B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * C, 32, C), k_strides=(Nk * C, 32, C),
                   v_strides=(Nk * C, 32, C), o_strides=(Nq * C, 32, C), scale=scale, dn_pad=dn_pad,
-                  dn_group=dn_group, fp16_inputs=fp16, dropout_p=dropout_p, seed=seed)
+                  dn_group=dn_group, fp16_inputs=fp16, dropout_p=dropout_p, seed=seed, seed_dev=seed_dev)
         T.attn_train_fwd(q, k, v, o, lse, **kw)
         ctx.kw = kw
         ctx.save_for_backward(q, k, v, o, lse)
@@ -94,12 +94,14 @@ class _Attention(torch.autograd.Function):
         q, k, v, o, lse = ctx.saved_tensors
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         T.attn_train_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, **ctx.kw)
-        return dq, dk, dv, None, None, None, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None, None, None, None
 
 
-def attention(q, k, v, num_heads, *, dn_pad=0, dn_group=0, fp16=False, dropout_p=0.0, seed=0):
+def attention(q, k, v, num_heads, *, dn_pad=0, dn_group=0, fp16=False, dropout_p=0.0, seed=0, seed_dev=None):
+    """seed_dev: optional int32 device tensor [1] added to seed on the device (graph-replayed steps)"""
     return _Attention.apply(q.contiguous(), k.contiguous(), v.contiguous(), num_heads,
-                            1.0 / math.sqrt(q.shape[-1] // num_heads), dn_pad, dn_group, fp16, dropout_p, seed)
+                            1.0 / math.sqrt(q.shape[-1] // num_heads), dn_pad, dn_group, fp16, dropout_p, seed,
+                            seed_dev)
 
 
 class _LayerNorm(torch.autograd.Function):

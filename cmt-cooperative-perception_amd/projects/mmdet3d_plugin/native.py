@@ -29,7 +29,7 @@ C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
 ATTN_KEEP_PARTIALS = 2048   # cmt_hip.h CMT_ATTN_KEEP_PARTIALS (ABI 19)
 CHAIN_XSPLITS = 8           # the split count chain B1 combines (cmt_chain_args.xsplits)
-ABI_VERSION = 21
+ABI_VERSION = 22
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -101,7 +101,7 @@ class AttnTrainArgs(ctypes.Structure):
                 ("LSE", _vp), ("dO", _vp), ("dQ", _vp), ("dK", _vp), ("dV", _vp), ("delta", _vp),
                 ("scale", _flt), ("dn_pad", _int), ("dn_group", _int), ("fp16_inputs", _int),
                 ("dropout_p", _flt), ("seed", ctypes.c_uint32), ("kv_splits", _int),
-                ("workspace", _vp), ("workspace_bytes", _i64)]
+                ("workspace", _vp), ("workspace_bytes", _i64), ("seed_dev", _vp)]
 
 
 class LnTrainArgs(ctypes.Structure):

@@ -143,7 +143,8 @@ def linear_bwd_batched(dY, X, W, need_dx=True, need_dw=True, need_db=True):
 
 
 def _attn_args(Q, K, V, O, LSE, *, B, H, Nq, Nk, q_strides, k_strides, v_strides, o_strides, scale, dn_pad=0,
-               dn_group=0, fp16_inputs=False, dropout_p=0.0, seed=0):
+               dn_group=0, fp16_inputs=False, dropout_p=0.0, seed=0, seed_dev=None):
+    """seed_dev: optional int32 device tensor [1]; the kernels' dropout seed is seed + seed_dev[0]"""
     a = N.AttnTrainArgs()
     a.B, a.H, a.Nq, a.Nk = B, H, Nq, Nk
     a.Q, (a.q_bs, a.q_hs, a.q_rs) = Q.data_ptr(), q_strides
@@ -153,6 +154,10 @@ def _attn_args(Q, K, V, O, LSE, *, B, H, Nq, Nk, q_strides, k_strides, v_strides
     a.LSE = LSE.data_ptr()
     a.scale, a.dn_pad, a.dn_group = scale, dn_pad, dn_group
     a.fp16_inputs, a.dropout_p, a.seed = int(bool(fp16_inputs)), dropout_p, seed & 0xFFFFFFFF
+    if seed_dev is not None:
+        if seed_dev.dtype != torch.int32 or not seed_dev.is_cuda:
+            raise RuntimeError("seed_dev must be an int32 device tensor")
+        a.seed_dev = seed_dev.data_ptr()
     return a
 
 

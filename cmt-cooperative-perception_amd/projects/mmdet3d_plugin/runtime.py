@@ -127,6 +127,9 @@ class Options:
                            # via HBM) instead of inside chain B1
     rv_geo: bool           # CMT_RV_GEO=0: the camera rows' frustum coordinates and layout pass as launches of
                            # their own instead of inside the one-launch RV position MLP
+    train_graph: bool      # CMT_TRAIN_GRAPH=1 (off by default): the training decoder's forward / backward
+                           # replayed as HIP graphs instead of issued op by op (train_engine._decoder_t):
+                           # host issue 39.2 -> 34.9 ms/step, step rate 27.7 vs 28.8 steps/s (r5ai)
 
 
 def _env_on(name):
@@ -136,7 +139,7 @@ def _env_on(name):
 OPTIONS = Options(side_stream=_env_on("CMT_SIDE_STREAM"), chain=_env_on("CMT_CHAIN"),
                   bev_pos_cache=_env_on("CMT_BEV_POS_CACHE"), conv_halo=_env_on("CMT_CONV_HALO"),
                   mlp_fused=_env_on("CMT_MLP_FUSED"), chain_combine=_env_on("CMT_CHAIN_COMBINE"),
-                  rv_geo=_env_on("CMT_RV_GEO"))
+                  rv_geo=_env_on("CMT_RV_GEO"), train_graph=os.environ.get("CMT_TRAIN_GRAPH", "0") == "1")
 
 
 @contextlib.contextmanager

@@ -237,6 +237,67 @@ def test_trainer_step_reduces_loss(dev):
     assert vals[-1] < vals[0], vals
 
 
+def _small_coop_step(dev, graph, dropout, steps=1):
+    """forward_train + loss + backward of a small two-agent head with the decoder graphed or
+    issued op by op; returns (losses of each step, gradients of the last)."""
+    from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.runtime import options
+    from projects.mmdet3d_plugin.models.dense_heads.cmt_head_coop import (get_infrastructure_image_metas,
+                                                                          get_vehicle_image_metas)
+    torch.manual_seed(0)
+    head, _, _ = S.build_synthetic_head("cmtcoop_fusion_tumtraf", seed=0, num_query=48, num_layers=2,
+                                        grid_size=[128, 128, 40], device=dev)
+    head.train()
+    head.train_dropout = dropout
+    mv = S.synthetic_metas(1, yaws=S.VEHICLE_YAWS, prefix="vehicle_", pad_shape=(128, 320, 3), seed=7)
+    mi = S.synthetic_metas(1, yaws=S.INFRA_YAWS[:2], prefix="infrastructure_", pad_shape=(128, 320, 3), seed=17)
+    metas = [dict(mv[0], **mi[0])]
+    agents = [(S.synthetic_bev(1, 16, 16, seed=5, device=dev), S.synthetic_img(1, 8, 20, seed=6, device=dev),
+               get_vehicle_image_metas(metas)),
+              (S.synthetic_bev(1, 16, 16, seed=15, device=dev), S.synthetic_img(2, 8, 20, seed=16, device=dev),
+               get_infrastructure_image_metas(metas))]
+    gtb, gtl = _gt(1, list(head.pc_range), head.num_classes[0], 5, seed=3)
+    gtb, gtl = [b.to(dev) for b in gtb], [l.to(dev) for l in gtl]
+    groups = min(head.scalar, 48 // 5)
+    rp = torch.rand(groups * 5, 3, generator=torch.Generator().manual_seed(4)).to(dev) * 2 - 1
+    vals = []
+    with options(train_graph=graph):
+        for _ in range(steps):
+            head.zero_grad(set_to_none=True)
+            preds = head.forward_train(agents, metas, gtb, gtl, rand_prob=rp)
+            loss = sum(head.loss(gtb, gtl, [[p] for p in preds]).values())
+            loss.backward()
+            vals.append(loss.item())
+    torch.cuda.synchronize()
+    return vals, {k: p.grad.detach().clone() for k, p in head.named_parameters() if p.grad is not None}
+
+
+def test_training_graph_matches_eager(dev, parity_log):
+    """The decoder's forward / backward replayed as HIP graphs (OPTIONS.train_graph, CMT_TRAIN_GRAPH=1)
+    against the same walk issued op by op: losses and every gradient agree (dropout off; the
+    split-K weight gradients sum by f32 atomics, so not bitwise), over three steps of one graph."""
+    lg, gg = _small_coop_step(dev, True, False, steps=3)
+    le, ge = _small_coop_step(dev, False, False, steps=3)
+    assert set(gg) == set(ge)
+    lerr = max(abs(a - b) / max(abs(b), 1e-3) for a, b in zip(lg, le))
+    # each gradient relative to its own scale, floored at 1e-3 of the step's largest entry (layer 0's
+    # self-attention Q / K in_proj gradients are rounding noise in both: see _run_mode)
+    floor = 1e-3 * max(g.abs().max().item() for g in ge.values())
+    errs = {k: (gg[k] - ge[k]).abs().max().item() / max(ge[k].abs().max().item(), floor) for k in ge}
+    worst = max(errs, key=errs.get)
+    gerr = errs[worst]
+    parity_log.append(f"training decoder as HIP graphs vs op by op (coop, 2 layers, 3 steps): losses max rel "
+                      f"{lerr:.1e}, param grads max rel {gerr:.1e} ({worst})")
+    assert lerr < 1e-5 and gerr < 1e-4, sorted(errs.items(), key=lambda kv: -kv[1])[:8]
+
+
+def test_training_graph_dropout_draws_fresh_masks(dev):
+    """With dropout on, each replay draws a new attention-dropout seed on the device (and torch's
+    dropout its graph-safe offsets): two steps on the same inputs differ."""
+    lg, _ = _small_coop_step(dev, True, True, steps=2)
+    assert lg[0] != lg[1]
+
+
 def test_transformer_forward_with_dn_mask_training(dev, parity_log):
     """Transformer-level drop-in for training: CmtLidarTransformer.forward(...,
     attn_masks=[dn_mask, None]) in training mode (cmt_transformer.py:166-204,
