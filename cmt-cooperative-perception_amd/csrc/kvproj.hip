@@ -271,8 +271,11 @@ __global__ __launch_bounds__(512, 1) void kvproj_kernel(cmt_gemm_args a, int par
 // ---------------------------------------------------------------------------
 constexpr int KV3_RING = 4;
 
+// Work units are (128-token tile, column part); the grid's first nfull workgroups take one unit
+// each, the rest take HALF a unit (each wave the first or second half of its head planes), so the
+// last round of a 3.45-round grid is 2 x 114 short units instead of 114 long ones beside 142 idle CUs.
 template <typename TC, int SCHED>
-__global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int parts) {
+__global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int parts, int nfull) {
     // A tile hi plane | lo plane, each [128 tokens][256] f16 with 16-byte chunks XOR-swizzled by
     // row & 15, then the column part's bias (fp32)
     __shared__ __attribute__((aligned(16))) char lds[2 * KP_BM * KP_K * 2 + KP_MAXB * 4];
@@ -280,7 +283,10 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
     const int lane = tid & 63;
     const int lr = lane & 31, lh = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rt = blockIdx.x / parts, part = blockIdx.x - rt * parts;
+    const int bid = blockIdx.x;
+    const int hx = bid - nfull;                                    // >= 0: a half unit
+    const int unit = hx < 0 ? bid : nfull + (hx >> 1);
+    const int rt = unit / parts, part = unit - rt * parts;
     const int m0 = rt * KP_BM;
     const int ncols = a.N / parts;
     const int n_part = part * ncols;
@@ -298,8 +304,10 @@ __global__ __launch_bounds__(512, 1) void kvproj_x3_kernel(cmt_gemm_args a, int 
         __builtin_amdgcn_global_load_lds((kp_gaddr_t)(Ab + (int64_t)src * lda + plane_lo * KP_K + 8 * lc),
                                          (kp_laddr_t)(lds + piece * 16), 16, 0, 0);
     }
-    const int planes_w = ncols / 32 / 8;
-    const int plane0 = (n_part >> 5) + wave * planes_w;
+    const int planes_all = ncols / 32 / 8;                         // the wave's head planes of a whole unit
+    const int h0 = planes_all >> 1;                                // a half unit: planes [0, h0) or [h0, all)
+    const int planes_w = hx < 0 ? planes_all : (hx & 1) ? planes_all - h0 : h0;
+    const int plane0 = (n_part >> 5) + wave * planes_all + (hx >= 0 && (hx & 1) ? h0 : 0);
     const pair_t* Wh = (const pair_t*)a.W + (int64_t)plane0 * (KP_KS * 512) + lane * 8;
     const pair_t* Wl = Wh + (int64_t)a.N * KP_K;
     pair8_t rh[KV3_RING], rl[KV3_RING];
@@ -531,12 +539,18 @@ extern "C" int cmt_kv_proj(const cmt_gemm_args* ap, void* stream) {
         CMT_REQUIRE(a.lda % 8 == 0 && (a.A2 == nullptr || a.lda2 % 8 == 0) &&
                         ((uintptr_t)a.A | (uintptr_t)a.W | (uintptr_t)a.C | (uintptr_t)a.A2) % 16 == 0,
                     "cmt_kv_proj: 16-byte aligned operands");
-        const unsigned g3 = (unsigned)(cdiv(a.M, KP_BM) * parts);
+        const int units = cdiv(a.M, KP_BM) * parts;
+        // the units past the last full round of one workgroup per CU run as two half units (when a
+        // wave has at least two head planes to share)
+        const int ncu = cmt_cu_count();
+        const int tail = (a.N / parts / 256 >= 2) ? units % ncu : 0;   // 287-296 vs 303-305 us alone (r5al)
+        const int nfull = units - tail;
+        const unsigned g3 = (unsigned)(nfull + 2 * tail);
         hipStream_t s3 = (hipStream_t)stream;
         if (a.c_dtype == CMT_F16) {
-            kvproj_x3_kernel<f16_t, CMT_KV_SCHED><<<g3, 512, 0, s3>>>(a, parts);
+            kvproj_x3_kernel<f16_t, CMT_KV_SCHED><<<g3, 512, 0, s3>>>(a, parts, nfull);
         } else {
-            kvproj_x3_kernel<bf16_t, 0><<<g3, 512, 0, s3>>>(a, parts);
+            kvproj_x3_kernel<bf16_t, 0><<<g3, 512, 0, s3>>>(a, parts, nfull);
         }
         return cmt_check_launch("cmt_kv_proj");
     }
