@@ -416,11 +416,16 @@ class HeadEngineMixin:
         # reference numerics with the NCHW conv: lowp(memory + pos) of the BEV rows comes from the
         # conv epilogue plus the kept BEV position rows (CMT_BEV_POS_CACHE=0: the MLP runs per call)
         fuse_bev = use_bev and OPTIONS.bev_pos_cache and self._conv_halo_ok(x, pk, prec)
-        cams = self._cams(metas, dev) if use_img else None
         dec = self.transformer.decoder
         Nq = self.num_query
         state = None
         side = self._side_stream(dev) if dec.prologue_ok(prec) else None
+        # with the one-launch camera rows the camera matrices are first read after the conv: their
+        # upload goes on the second stream, so the conv is the frame's first node (675.1 vs 672.8
+        # frames/s, 3 alternating pairs; the main stream's wait for it before the camera rows costs
+        # ~6 us of the ~10 it saves -- profiles/r5_experiments.txt r5am)
+        late_cams = side is not None and use_img and use_bev and fuse_bev and self._rv_geo_ok(x_img, pk, prec)
+        cams = self._cams(metas, dev) if use_img and not late_cams else None
         if side is not None:
             # A second stream runs everything that does not read the conv output: the
             # input-independent first halves of the BEV / RV position MLPs and the camera
@@ -451,7 +456,11 @@ class HeadEngineMixin:
                 self._shared_conv_into(x, mem, Nk, pk, prec, pos=pos, P=P)
             ready = torch.cuda.Event()
             bev_ready = torch.cuda.Event()
+            cams_ready = torch.cuda.Event()
             with torch.cuda.stream(side):
+                if late_cams:
+                    cams = self._cams(metas, dev)
+                    cams_ready.record(side)
                 if use_bev and not fuse_bev:
                     hb = self._bev_pos_hidden(H, W, pk)
                 # the BEV position MLP's second GEMM waits only for its own hidden rows (usually a
@@ -468,10 +477,12 @@ class HeadEngineMixin:
                 qpos, firsts = self._query_pos(B, metas, use_img, pk, cams=cams,
                                                first_ops=(state["tl"], state["tp"]))
                 dec.lowp_layer0(state, qpos, B=B, Nq=Nq, prec=prec, first_ops_ready=firsts)
-            for t in (qpos, hb, hr):
+            for t in (qpos, hb, hr) + (tuple(cams) if late_cams else ()):
                 if t is not None:
                     t.record_stream(main)
             if geo:
+                if late_cams:
+                    main.wait_event(cams_ready)
                 self._rv_rows_geo(x_img, metas, B, Nk, HW, pk, mem, pos, cams)
             else:
                 if use_bev and fuse_bev:
