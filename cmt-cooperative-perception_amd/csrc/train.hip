@@ -191,19 +191,21 @@ __device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
     lo = (bf16_t)(x - (float)hi);
 }
 
-// A 64-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) moves in two steps so the
+// A (64 T)-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) moves in two steps so the
 // next tile's global loads are in flight while the current one is multiplied: fetch_x3 loads this
-// thread's 8 elements into registers, put_x3 splits them into the bf16 hi / lo LDS images.
-template <int MODE>
-__device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict__ X, int64_t s_r, int64_t s_k,
+// thread's 8 T elements into registers, put_x3 splits them into the bf16 hi / lo LDS images.
+// Row-contiguous modes: 16 T threads per k row, each four consecutive rows.
+template <int MODE, int T>
+__device__ __forceinline__ void fetch_x3(float (&v)[8 * T], const float* __restrict__ X, int64_t s_r, int64_t s_k,
                                          int rows, int K, int r0, int k0, int tid, const X3Conv& cv = X3Conv{}) {
+    constexpr int TPR = 16 * T;
     if (MODE == OP_IM) {
         // OP_MC's thread layout: 4 consecutive n (channels of one tap, Cin % 4 == 0) at one token
         const int hw = cv.H * cv.W;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 2 * T; ++i) {
             const int idx = tid + TNT * i;
-            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int k = idx / TPR, r = (idx % TPR) * 4;
             const int gr = r0 + r, gk = k0 + k;
             f32x4 t = {0.f, 0.f, 0.f, 0.f};
             if (gk < K && gr < rows) {
@@ -219,7 +221,7 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict_
         }
     } else if (MODE == OP_KC) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 2 * T; ++i) {
             const int idx = tid + TNT * i;
             const int r = idx >> 3, c = (idx & 7) * 4;
             const int gr = r0 + r, gk = k0 + c;
@@ -235,9 +237,9 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict_
         }
     } else if (MODE == OP_MC) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 2 * T; ++i) {
             const int idx = tid + TNT * i;
-            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int k = idx / TPR, r = (idx % TPR) * 4;
             const int gr = r0 + r, gk = k0 + k;
             f32x4 t = {0.f, 0.f, 0.f, 0.f};
             if (gk < K) {
@@ -251,7 +253,7 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict_
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 8 * T; ++i) {
             const int idx = tid + TNT * i;
             const int r = idx >> 5, k = idx & 31;
             const int gr = r0 + r, gk = k0 + k;
@@ -260,12 +262,13 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8], const float* __restrict_
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__ lo, const float (&v)[8], int tid) {
+template <int MODE, int T>
+__device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__ lo, const float (&v)[8 * T], int tid) {
     typedef bf16_t b4 __attribute__((ext_vector_type(4)));
+    constexpr int TPR = 16 * T;
     if (MODE == OP_KC) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 2 * T; ++i) {
             const int idx = tid + TNT * i;
             const int r = idx >> 3, c = (idx & 7) * 4;
             b4 h, l;
@@ -281,9 +284,9 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
         }
     } else if (x3_timg<MODE>()) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 2 * T; ++i) {
             const int idx = tid + TNT * i;
-            const int k = idx >> 4, r = (idx & 15) * 4;
+            const int k = idx / TPR, r = (idx % TPR) * 4;
             b4 h, l;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -297,7 +300,7 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 8 * T; ++i) {
             const int idx = tid + TNT * i;
             const int r = idx >> 5, k = idx & 31;
             bf16_t h, l;
@@ -308,11 +311,11 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
     }
 }
 
-// Row (m) of each of fetch_x3's 8 elements within the 64-row tile.
-template <int MODE>
+// Row (m) of each of fetch_x3's 8 T elements within the (64 T)-row tile.
+template <int MODE, int T>
 __device__ __forceinline__ int x3_row(int e, int tid) {
     if (MODE == OP_KC) return ((tid + TNT * (e >> 2)) >> 3);
-    if (MODE == OP_MC || MODE == OP_IM) return ((tid + TNT * (e >> 2)) & 15) * 4 + (e & 3);
+    if (MODE == OP_MC || MODE == OP_IM) return ((tid + TNT * (e >> 2)) % (16 * T)) * 4 + (e & 3);
     return (tid + TNT * e) >> 5;
 }
 
@@ -328,79 +331,101 @@ __device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
     bz = b / (nx * ny);
 }
 
-template <int AM, int BM>
+// T = 1: 64 x 64 tiles, each wave one 32 x 32 accumulator; T = 2: 128 x 128 tiles, each wave 2 x 2
+// of them -- 4x the MFMAs per staged k-step for 2x the loads and splits (the long-K weight gradients
+// and the 44 400-row K/V products, gemm_ex_launch)
+template <int AM, int BM, int T>
 __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int kchunk, X3Conv cv) {
-    __shared__ __attribute__((aligned(16))) char As[2][2][64 * X3RB];   // [buffer][hi, lo]
-    __shared__ __attribute__((aligned(16))) char Bs[2][2][64 * X3RB];
+    constexpr int R = 64 * T;   // tile rows and columns
+    __shared__ __attribute__((aligned(16))) char As[2][2][R * X3RB];   // [buffer][hi, lo]
+    __shared__ __attribute__((aligned(16))) char Bs[2][2][R * X3RB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
     int bx, by, bz;
     xcd_tile(bx, by, bz);
-    const int n0 = bx * 64, m0 = by * 64;
+    const int n0 = bx * R, m0 = by * R;
     const int z = bz / a.ksplit, ks = bz - z * a.ksplit;
     const float* A = a.A + (int64_t)z * a.a_bs;
     const float* B = a.B + (int64_t)z * a.b_bs;
     const int kb = ks * kchunk, ke = min(a.K, kb + kchunk);
-    f32x16 acc;
+    f32x16 acc[T][T];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int ar = wm * 32 + lr, br = wn * 32 + lr;
-    float va[8], vb[8];
+    for (int i = 0; i < T; ++i)
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int ar0 = wm * 32 * T, br0 = wn * 32 * T;   // the wave's first A / B tile row
+    float va[8 * T], vb[8 * T];
     // a_rowsum: the first column tile also sums its A elements (fp32, before the split) per row
     const bool rowsum = a.a_rowsum != nullptr && bx == 0;
-    float rs[8];
+    float rs[8 * T];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) rs[e] = 0.f;
-    fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
-    fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid, cv);
+    for (int e = 0; e < 8 * T; ++e) rs[e] = 0.f;
+    fetch_x3<AM, T>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
+    fetch_x3<BM, T>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid, cv);
     int buf = 0;
     for (int k0 = kb; k0 < ke; k0 += TBK, buf ^= 1) {
         if (rowsum) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) rs[e] += va[e];
+            for (int e = 0; e < 8 * T; ++e) rs[e] += va[e];
         }
         // one barrier per step: buffer buf was last read two steps ago, before the previous barrier
-        put_x3<AM>(As[buf][0], As[buf][1], va, tid);
-        put_x3<BM>(Bs[buf][0], Bs[buf][1], vb, tid);
+        put_x3<AM, T>(As[buf][0], As[buf][1], va, tid);
+        put_x3<BM, T>(Bs[buf][0], Bs[buf][1], vb, tid);
         __syncthreads();
         if (k0 + TBK < ke) {
-            fetch_x3<AM>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, k0 + TBK, tid);
-            fetch_x3<BM>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid, cv);
+            fetch_x3<AM, T>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, k0 + TBK, tid);
+            fetch_x3<BM, T>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid, cv);
         }
         constexpr bool perm = x3_timg<AM>() || x3_timg<BM>();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            const bf16x8 ah = x3_frag<AM, perm>(As[buf][0], wm * 32, ar, kk, lane);
-            const bf16x8 al = x3_frag<AM, perm>(As[buf][1], wm * 32, ar, kk, lane);
-            const bf16x8 bh = x3_frag<BM, perm>(Bs[buf][0], wn * 32, br, kk, lane);
-            const bf16x8 bl = x3_frag<BM, perm>(Bs[buf][1], wn * 32, br, kk, lane);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+            bf16x8 ah[T], al[T], bh[T], bl[T];
+#pragma unroll
+            for (int i = 0; i < T; ++i) {
+                ah[i] = x3_frag<AM, perm>(As[buf][0], ar0 + 32 * i, ar0 + 32 * i + lr, kk, lane);
+                al[i] = x3_frag<AM, perm>(As[buf][1], ar0 + 32 * i, ar0 + 32 * i + lr, kk, lane);
+                bh[i] = x3_frag<BM, perm>(Bs[buf][0], br0 + 32 * i, br0 + 32 * i + lr, kk, lane);
+                bl[i] = x3_frag<BM, perm>(Bs[buf][1], br0 + 32 * i, br0 + 32 * i + lr, kk, lane);
+            }
+#pragma unroll
+            for (int i = 0; i < T; ++i)
+#pragma unroll
+                for (int j = 0; j < T; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
         }
     }
     if (rowsum) {   // uniform per workgroup: per-row partials through LDS, one atomic per row
         float* red = (float*)As[0][0];
         __syncthreads();
-        if (tid < 64) red[tid] = 0.f;
+        if (tid < R) red[tid] = 0.f;
         __syncthreads();
 #pragma unroll
-        for (int e = 0; e < 8; ++e) atomicAdd(red + x3_row<AM>(e, tid), rs[e]);
+        for (int e = 0; e < 8 * T; ++e) atomicAdd(red + x3_row<AM, T>(e, tid), rs[e]);
         __syncthreads();
-        if (tid < 64 && m0 + tid < a.M) atomicAdd(a.a_rowsum + (int64_t)z * a.M + m0 + tid, red[tid]);
+        if (tid < R && m0 + tid < a.M) atomicAdd(a.a_rowsum + (int64_t)z * a.M + m0 + tid, red[tid]);
     }
     float* C = a.C + (int64_t)z * a.c_bs;
-    const int col = n0 + wn * 32 + lr;
-    if (col >= a.N) return;
-    const float bias = (a.bias && ks == 0) ? a.bias[(int64_t)z * a.bias_bs + col] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= a.M) continue;
-        float* c = C + (int64_t)row * a.ldc + col;
-        const float v = a.alpha * acc[r] + bias;
-        if (a.ksplit > 1) atomicAdd(c, v);
-        else *c = a.beta != 0.f ? v + a.beta * *c : v;
+    for (int j = 0; j < T; ++j) {
+        const int col = n0 + br0 + 32 * j + lr;
+        if (col >= a.N) continue;
+        const float bias = (a.bias && ks == 0) ? a.bias[(int64_t)z * a.bias_bs + col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < T; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + ar0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (row >= a.M) continue;
+                float* c = C + (int64_t)row * a.ldc + col;
+                const float v = a.alpha * acc[i][j][r] + bias;
+                if (a.ksplit > 1) atomicAdd(c, v);
+                else *c = a.beta != 0.f ? v + a.beta * *c : v;
+            }
     }
 }
 
@@ -782,6 +807,22 @@ __global__ __launch_bounds__(256) void adamw_kernel(cmt_adamw_args a) {
 }  // namespace
 
 namespace {
+// 128 x 128 tiles for long reductions (the weight gradients) and very large products, when they
+// alone, or with the reduction split further, still give the chip >= 256 workgroups: a split-K launch
+// (C accumulated, beta 1) may re-choose its split (chunks >= 256 k).  A 44 400 x 256 x 256 product
+// keeps 64 x 64 tiles (694 big tiles are 1.4 rounds of two per CU: 49 vs 42 us, r5an).
+bool x3_big_tiles(cmt_gemm_ex_args& a) {
+    if (a.M < 128 || a.N < 128) return false;
+    const int64_t tiles = (int64_t)cdiv(a.M, 128) * cdiv(a.N, 128) * a.batch;
+    if (a.K < 1024 && tiles < 1536) return false;
+    int ks = a.ksplit;
+    if (ks > 1)
+        while (tiles * ks < 512 && a.K / (2 * ks) >= 256) ks *= 2;
+    if (tiles * ks < 256) return false;
+    a.ksplit = ks;
+    return true;
+}
+
 int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm_f32_ex: null args");
     cmt_gemm_ex_args a = *ap;
@@ -790,14 +831,17 @@ int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
     if (a.ksplit < 1) a.ksplit = 1;
     CMT_REQUIRE(a.ksplit == 1 || a.beta == 1.f, "cmt_gemm_f32_ex: split-K accumulates (beta must be 1)");
     const int am = op_mode(a.a_sm, a.a_sk, a.A), bm = op_mode(a.b_sn, a.b_sk, a.B);
+    const bool big = x3 && x3_big_tiles(a);
     int kchunk = cdiv(cdiv(a.K, a.ksplit), TBK) * TBK;
     a.ksplit = cdiv(a.K, kchunk);
-    dim3 grid(cdiv(a.N, 64), cdiv(a.M, 64), a.batch * a.ksplit);
+    const int R = big ? 128 : 64;
+    dim3 grid(cdiv(a.N, R), cdiv(a.M, R), a.batch * a.ksplit);
     hipStream_t s = (hipStream_t)stream;
-#define GX(AM, BM)                                                       \
-    do {                                                                 \
-        if (x3) gemm_ex3_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{}); \
-        else gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk);     \
+#define GX(AM, BM)                                                                      \
+    do {                                                                                \
+        if (big) gemm_ex3_kernel<AM, BM, 2><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{});  \
+        else if (x3) gemm_ex3_kernel<AM, BM, 1><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{}); \
+        else gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk);                    \
     } while (0)
     switch (am * 3 + bm) {
         case 0: GX(0, 0); break; case 1: GX(0, 1); break; case 2: GX(0, 2); break;
@@ -828,10 +872,13 @@ extern "C" int cmt_conv3x3_wgrad_bf16x3(const float* X, const float* dY, float* 
     a.B = X;                                // B(n, k): the implicit im2col
     a.C = dW; a.ldc = 9 * Cin;
     a.ksplit = ksplit < 1 ? 1 : ksplit;
+    const bool big = x3_big_tiles(a);
     int kchunk = cdiv(cdiv(a.K, a.ksplit), TBK) * TBK;
     a.ksplit = cdiv(a.K, kchunk);
-    const dim3 grid(cdiv(a.N, 64), cdiv(a.M, 64), a.ksplit);
-    gemm_ex3_kernel<OP_MC, OP_IM><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, X3Conv{H, W, Cin});
+    const int R = big ? 128 : 64;
+    const dim3 grid(cdiv(a.N, R), cdiv(a.M, R), a.ksplit);
+    if (big) gemm_ex3_kernel<OP_MC, OP_IM, 2><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, X3Conv{H, W, Cin});
+    else gemm_ex3_kernel<OP_MC, OP_IM, 1><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, X3Conv{H, W, Cin});
     return cmt_check_launch("cmt_conv3x3_wgrad_bf16x3");
 }
 

@@ -20,7 +20,11 @@ def _T():
 
 @pytest.mark.parametrize("mode", ["f32", "bf16x3"])
 @pytest.mark.parametrize("M,N,K,ta,tb", [(100, 70, 50, False, False), (256, 256, 900, True, True),
-                                         (33, 257, 64, False, True), (64, 64, 4000, True, False)])
+                                         (33, 257, 64, False, True), (64, 64, 4000, True, False),
+                                         # 128 x 128 tiles (>= 256 workgroups): ragged, no split; and a
+                                         # long reduction whose split-K the launcher re-chooses
+                                         (4100, 1030, 100, False, False), (4100, 1030, 100, True, True),
+                                         (256, 256, 70000, True, False)])
 def test_gemm_ex_transposes(dev, M, N, K, ta, tb, mode):
     """cmt_gemm_f32_ex (exact f32) and cmt_gemm_bf16x3_ex (three bf16 passes on split
     operands) against float64, every transpose, split-K; the bf16x3 form also on
@@ -213,7 +217,8 @@ def test_bn_relu_and_conv_weight_grad(dev):
     assert (bng.running_var.cpu().double() - bn.running_var).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("nimg,H,W,Cin,Cout,ks", [(2, 9, 11, 36, 20, 1), (1, 40, 37, 64, 128, 3), (1, 180, 180, 8, 4, 7)])
+@pytest.mark.parametrize("nimg,H,W,Cin,Cout,ks", [(2, 9, 11, 36, 20, 1), (1, 40, 37, 64, 128, 3), (1, 180, 180, 8, 4, 7),
+                                                   (1, 180, 180, 64, 128, 2)])   # 128 x 128 tiles, split re-chosen
 def test_conv3x3_wgrad_implicit(dev, nimg, H, W, Cin, Cout, ks):
     """cmt_conv3x3_wgrad_bf16x3 (ABI 21: the im2col operand gathered inside the bf16x3 GEMM) against
     float64 conv2d's weight gradient and bitwise against the im2col matrix + cmt_gemm_bf16x3_ex at
