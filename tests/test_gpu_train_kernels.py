@@ -21,9 +21,9 @@ def _T():
 @pytest.mark.parametrize("mode", ["f32", "bf16x3"])
 @pytest.mark.parametrize("M,N,K,ta,tb", [(100, 70, 50, False, False), (256, 256, 900, True, True),
                                          (33, 257, 64, False, True), (64, 64, 4000, True, False),
-                                         # 128 x 128 tiles (>= 256 workgroups): ragged, no split; and a
-                                         # long reduction whose split-K the launcher re-chooses
-                                         (4100, 1030, 100, False, False), (4100, 1030, 100, True, True),
+                                         # 128 x 128 tiles: a very large ragged product (>= 1 536 tiles, no
+                                         # split) and a long reduction whose split-K the launcher re-chooses
+                                         (12300, 2060, 40, False, False), (12300, 2060, 40, True, True),
                                          (256, 256, 70000, True, False)])
 def test_gemm_ex_transposes(dev, M, N, K, ta, tb, mode):
     """cmt_gemm_f32_ex (exact f32) and cmt_gemm_bf16x3_ex (three bf16 passes on split
