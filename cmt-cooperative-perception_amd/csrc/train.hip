@@ -191,20 +191,20 @@ __device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
     lo = (bf16_t)(x - (float)hi);
 }
 
-// A (64 T)-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) moves in two steps so the
-// next tile's global loads are in flight while the current one is multiplied: fetch_x3 loads this
-// thread's 8 T elements into registers, put_x3 splits them into the bf16 hi / lo LDS images.
-// Row-contiguous modes: 16 T threads per k row, each four consecutive rows.
-template <int MODE, int T>
-__device__ __forceinline__ void fetch_x3(float (&v)[8 * T], const float* __restrict__ X, int64_t s_r, int64_t s_k,
+// An R-row x 32-k fp32 tile (element (r, k) at X[r * s_r + k * s_k]) staged by NT threads moves in
+// two steps so the next tile's global loads are in flight while the current one is multiplied:
+// fetch_x3 loads this thread's R * 32 / NT elements into registers, put_x3 splits them into the bf16
+// hi / lo LDS images.  Row-contiguous modes: R / 4 threads per k row, each four consecutive rows.
+template <int MODE, int R, int NT>
+__device__ __forceinline__ void fetch_x3(float (&v)[R * 32 / NT], const float* __restrict__ X, int64_t s_r, int64_t s_k,
                                          int rows, int K, int r0, int k0, int tid, const X3Conv& cv = X3Conv{}) {
-    constexpr int TPR = 16 * T;
+    constexpr int TPR = R / 4, VI = R * 8 / NT;
     if (MODE == OP_IM) {
         // OP_MC's thread layout: 4 consecutive n (channels of one tap, Cin % 4 == 0) at one token
         const int hw = cv.H * cv.W;
 #pragma unroll
-        for (int i = 0; i < 2 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < VI; ++i) {
+            const int idx = tid + NT * i;
             const int k = idx / TPR, r = (idx % TPR) * 4;
             const int gr = r0 + r, gk = k0 + k;
             f32x4 t = {0.f, 0.f, 0.f, 0.f};
@@ -221,8 +221,8 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8 * T], const float* __restr
         }
     } else if (MODE == OP_KC) {
 #pragma unroll
-        for (int i = 0; i < 2 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < VI; ++i) {
+            const int idx = tid + NT * i;
             const int r = idx >> 3, c = (idx & 7) * 4;
             const int gr = r0 + r, gk = k0 + c;
             f32x4 t = {0.f, 0.f, 0.f, 0.f};
@@ -237,8 +237,8 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8 * T], const float* __restr
         }
     } else if (MODE == OP_MC) {
 #pragma unroll
-        for (int i = 0; i < 2 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < VI; ++i) {
+            const int idx = tid + NT * i;
             const int k = idx / TPR, r = (idx % TPR) * 4;
             const int gr = r0 + r, gk = k0 + k;
             f32x4 t = {0.f, 0.f, 0.f, 0.f};
@@ -253,8 +253,8 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8 * T], const float* __restr
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 8 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < 4 * VI; ++i) {
+            const int idx = tid + NT * i;
             const int r = idx >> 5, k = idx & 31;
             const int gr = r0 + r, gk = k0 + k;
             v[i] = (gr < rows && gk < K) ? X[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
@@ -262,14 +262,14 @@ __device__ __forceinline__ void fetch_x3(float (&v)[8 * T], const float* __restr
     }
 }
 
-template <int MODE, int T>
-__device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__ lo, const float (&v)[8 * T], int tid) {
+template <int MODE, int R, int NT>
+__device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__ lo, const float (&v)[R * 32 / NT], int tid) {
     typedef bf16_t b4 __attribute__((ext_vector_type(4)));
-    constexpr int TPR = 16 * T;
+    constexpr int TPR = R / 4, VI = R * 8 / NT;
     if (MODE == OP_KC) {
 #pragma unroll
-        for (int i = 0; i < 2 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < VI; ++i) {
+            const int idx = tid + NT * i;
             const int r = idx >> 3, c = (idx & 7) * 4;
             b4 h, l;
 #pragma unroll
@@ -284,8 +284,8 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
         }
     } else if (x3_timg<MODE>()) {
 #pragma unroll
-        for (int i = 0; i < 2 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < VI; ++i) {
+            const int idx = tid + NT * i;
             const int k = idx / TPR, r = (idx % TPR) * 4;
             b4 h, l;
 #pragma unroll
@@ -300,8 +300,8 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 8 * T; ++i) {
-            const int idx = tid + TNT * i;
+        for (int i = 0; i < 4 * VI; ++i) {
+            const int idx = tid + NT * i;
             const int r = idx >> 5, k = idx & 31;
             bf16_t h, l;
             split_bf16(v[i], h, l);
@@ -311,12 +311,12 @@ __device__ __forceinline__ void put_x3(char* __restrict__ hi, char* __restrict__
     }
 }
 
-// Row (m) of each of fetch_x3's 8 T elements within the (64 T)-row tile.
-template <int MODE, int T>
+// Row (m) of each of fetch_x3's elements within the R-row tile.
+template <int MODE, int R, int NT>
 __device__ __forceinline__ int x3_row(int e, int tid) {
-    if (MODE == OP_KC) return ((tid + TNT * (e >> 2)) >> 3);
-    if (MODE == OP_MC || MODE == OP_IM) return ((tid + TNT * (e >> 2)) % (16 * T)) * 4 + (e & 3);
-    return (tid + TNT * e) >> 5;
+    if (MODE == OP_KC) return ((tid + NT * (e >> 2)) >> 3);
+    if (MODE == OP_MC || MODE == OP_IM) return ((tid + NT * (e >> 2)) % (R / 4)) * 4 + (e & 3);
+    return (tid + NT * e) >> 5;
 }
 
 // Workgroups are dealt to the 8 XCDs round-robin by linear id; renumber them so each XCD runs a
@@ -362,8 +362,8 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
     float rs[8 * T];
 #pragma unroll
     for (int e = 0; e < 8 * T; ++e) rs[e] = 0.f;
-    fetch_x3<AM, T>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
-    fetch_x3<BM, T>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid, cv);
+    fetch_x3<AM, R, TNT>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb, tid);
+    fetch_x3<BM, R, TNT>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb, tid, cv);
     int buf = 0;
     for (int k0 = kb; k0 < ke; k0 += TBK, buf ^= 1) {
         if (rowsum) {
@@ -371,12 +371,12 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
             for (int e = 0; e < 8 * T; ++e) rs[e] += va[e];
         }
         // one barrier per step: buffer buf was last read two steps ago, before the previous barrier
-        put_x3<AM, T>(As[buf][0], As[buf][1], va, tid);
-        put_x3<BM, T>(Bs[buf][0], Bs[buf][1], vb, tid);
+        put_x3<AM, R, TNT>(As[buf][0], As[buf][1], va, tid);
+        put_x3<BM, R, TNT>(Bs[buf][0], Bs[buf][1], vb, tid);
         __syncthreads();
         if (k0 + TBK < ke) {
-            fetch_x3<AM, T>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, k0 + TBK, tid);
-            fetch_x3<BM, T>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid, cv);
+            fetch_x3<AM, R, TNT>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, k0 + TBK, tid);
+            fetch_x3<BM, R, TNT>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, k0 + TBK, tid, cv);
         }
         constexpr bool perm = x3_timg<AM>() || x3_timg<BM>();
 #pragma unroll
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
         if (tid < R) red[tid] = 0.f;
         __syncthreads();
 #pragma unroll
-        for (int e = 0; e < 8 * T; ++e) atomicAdd(red + x3_row<AM, T>(e, tid), rs[e]);
+        for (int e = 0; e < 8 * T; ++e) atomicAdd(red + x3_row<AM, R, TNT>(e, tid), rs[e]);
         __syncthreads();
         if (tid < R && m0 + tid < a.M) atomicAdd(a.a_rowsum + (int64_t)z * a.M + m0 + tid, red[tid]);
     }
@@ -426,6 +426,130 @@ __global__ __launch_bounds__(TNT) void gemm_ex3_kernel(cmt_gemm_ex_args a, int k
                 if (a.ksplit > 1) atomicAdd(c, v);
                 else *c = a.beta != 0.f ? v + a.beta * *c : v;
             }
+    }
+}
+
+// Small products (fewer than 256 workgroups of 64 x 64 tiles, >= 4 k-steps each): a workgroup's
+// chain of dependent k-steps is its time (each step's MFMAs far shorter than its loads' latency).
+// Here the 4 waves split the tile's k-steps round-robin, each staging its own steps through a
+// private LDS slice (no workgroup barrier in the loop) into a full 64 x 64 partial tile, then the
+// partials are summed through LDS: a quarter of the chain per workgroup.
+template <int AM, int BM>
+__global__ __launch_bounds__(TNT) void gemm_ex3_kw_kernel(cmt_gemm_ex_args a, int kchunk, X3Conv cv) {
+    constexpr int R = 64, NT = 64, EPT = R * 32 / NT;   // 32 staged elements per lane and operand
+    constexpr int PLANE = R * X3RB;                      // one bf16 plane image: 4 KB
+    // [wave][A hi, A lo, B hi, B lo] staging; after the k loop: [wave][tile (i, j)][lane][16] partials
+    __shared__ __attribute__((aligned(16))) char lds[4 * 4 * PLANE];
+    __shared__ float red[R];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+    int bx, by, bz;
+    xcd_tile(bx, by, bz);
+    const int n0 = bx * R, m0 = by * R;
+    const int z = bz / a.ksplit, ks = bz - z * a.ksplit;
+    const float* A = a.A + (int64_t)z * a.a_bs;
+    const float* B = a.B + (int64_t)z * a.b_bs;
+    const int kb = ks * kchunk, ke = min(a.K, kb + kchunk);
+    const int nsteps = (ke - kb + TBK - 1) / TBK;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool rowsum = a.a_rowsum != nullptr && bx == 0;
+    float rs[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) rs[e] = 0.f;
+    char* const my = lds + wave * 4 * PLANE;
+    float va[EPT], vb[EPT];
+    if (wave < nsteps) {
+        fetch_x3<AM, R, NT>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb + wave * TBK, lane);
+        fetch_x3<BM, R, NT>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb + wave * TBK, lane, cv);
+    }
+    constexpr bool perm = x3_timg<AM>() || x3_timg<BM>();
+    for (int s = wave; s < nsteps; s += 4) {
+        if (rowsum) {
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) rs[e] += va[e];
+        }
+        put_x3<AM, R, NT>(my, my + PLANE, va, lane);
+        put_x3<BM, R, NT>(my + 2 * PLANE, my + 3 * PLANE, vb, lane);
+        // the wave reads what its own lanes wrote: LDS operations of a wave complete in order, the
+        // fence keeps the compiler from moving the reads above the writes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (s + 4 < nsteps) {
+            fetch_x3<AM, R, NT>(va, A, a.a_sm, a.a_sk, a.M, ke, m0, kb + (s + 4) * TBK, lane);
+            fetch_x3<BM, R, NT>(vb, B, a.b_sn, a.b_sk, a.N, ke, n0, kb + (s + 4) * TBK, lane, cv);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ah[i] = x3_frag<AM, perm>(my, 32 * i, 32 * i + lr, kk, lane);
+                al[i] = x3_frag<AM, perm>(my + PLANE, 32 * i, 32 * i + lr, kk, lane);
+                bh[i] = x3_frag<BM, perm>(my + 2 * PLANE, 32 * i, 32 * i + lr, kk, lane);
+                bl[i] = x3_frag<BM, perm>(my + 3 * PLANE, 32 * i, 32 * i + lr, kk, lane);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        // this step's fragment reads complete before the next step's writes to the same slice
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (rowsum) {
+        if (tid < R) red[tid] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) atomicAdd(red + x3_row<AM, R, NT>(e, lane), rs[e]);
+    }
+    __syncthreads();   // every wave is past its staging: the slices take the partial tiles
+    float* part = (float*)lds;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *(f32x4*)(part + (((wave * 4 + 2 * i + j) * 64 + lane) * 16 + 4 * q)) =
+                    f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+    __syncthreads();
+    if (rowsum && tid < R && m0 + tid < a.M) atomicAdd(a.a_rowsum + (int64_t)z * a.M + m0 + tid, red[tid]);
+    // wave w sums tile (w >> 1, w & 1) of the four partials, in wave order
+    const int ti = wave >> 1, tj = wave & 1;
+    f32x16 sum;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sum[r] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 v = *(const f32x4*)(part + (((w * 4 + 2 * ti + tj) * 64 + lane) * 16 + 4 * q));
+            sum[4 * q] += v[0]; sum[4 * q + 1] += v[1]; sum[4 * q + 2] += v[2]; sum[4 * q + 3] += v[3];
+        }
+    float* C = a.C + (int64_t)z * a.c_bs;
+    const int col = n0 + 32 * tj + lr;
+    if (col >= a.N) return;
+    const float bias = (a.bias && ks == 0) ? a.bias[(int64_t)z * a.bias_bs + col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = m0 + 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= a.M) continue;
+        float* c = C + (int64_t)row * a.ldc + col;
+        const float v = a.alpha * sum[r] + bias;
+        if (a.ksplit > 1) atomicAdd(c, v);
+        else *c = a.beta != 0.f ? v + a.beta * *c : v;
     }
 }
 
@@ -823,6 +947,13 @@ bool x3_big_tiles(cmt_gemm_ex_args& a) {
     return true;
 }
 
+// the k-wave split (gemm_ex3_kw_kernel) for unsplit launches of < 256 64 x 64 tiles with >= 4 k-steps
+// each: the decoder's forward / dX products 15.3-16.3 -> 12.1-13.3 us; a split-K weight gradient
+// (16 tiles x 4 splits) measured 18.1 -> 24.9 us and keeps the one-wave-per-tile kernel (r5aq)
+bool x3_kwave(const dim3& grid, int kchunk, int ksplit) {
+    return ksplit == 1 && (int64_t)grid.x * grid.y * grid.z < 256 && kchunk >= 4 * TBK;
+}
+
 int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
     CMT_REQUIRE(ap != nullptr, "cmt_gemm_f32_ex: null args");
     cmt_gemm_ex_args a = *ap;
@@ -836,10 +967,13 @@ int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
     a.ksplit = cdiv(a.K, kchunk);
     const int R = big ? 128 : 64;
     dim3 grid(cdiv(a.N, R), cdiv(a.M, R), a.batch * a.ksplit);
+    // small products with >= 4 k-steps per tile: the waves of a workgroup split its k-steps
+    const bool kw = x3 && !big && x3_kwave(grid, kchunk, a.ksplit);
     hipStream_t s = (hipStream_t)stream;
 #define GX(AM, BM)                                                                      \
     do {                                                                                \
         if (big) gemm_ex3_kernel<AM, BM, 2><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{});  \
+        else if (kw) gemm_ex3_kw_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{}); \
         else if (x3) gemm_ex3_kernel<AM, BM, 1><<<grid, TNT, 0, s>>>(a, kchunk, X3Conv{}); \
         else gemm_ex_kernel<AM, BM><<<grid, TNT, 0, s>>>(a, kchunk);                    \
     } while (0)
@@ -877,8 +1011,10 @@ extern "C" int cmt_conv3x3_wgrad_bf16x3(const float* X, const float* dY, float* 
     a.ksplit = cdiv(a.K, kchunk);
     const int R = big ? 128 : 64;
     const dim3 grid(cdiv(a.N, R), cdiv(a.M, R), a.ksplit);
-    if (big) gemm_ex3_kernel<OP_MC, OP_IM, 2><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, X3Conv{H, W, Cin});
-    else gemm_ex3_kernel<OP_MC, OP_IM, 1><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, X3Conv{H, W, Cin});
+    const X3Conv cv{H, W, Cin};
+    if (big) gemm_ex3_kernel<OP_MC, OP_IM, 2><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, cv);
+    else if (x3_kwave(grid, kchunk, a.ksplit)) gemm_ex3_kw_kernel<OP_MC, OP_IM><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, cv);
+    else gemm_ex3_kernel<OP_MC, OP_IM, 1><<<grid, TNT, 0, (hipStream_t)stream>>>(a, kchunk, cv);
     return cmt_check_launch("cmt_conv3x3_wgrad_bf16x3");
 }
 
