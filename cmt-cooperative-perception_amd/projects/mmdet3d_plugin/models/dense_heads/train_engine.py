@@ -47,12 +47,16 @@ class _DecoderStep(torch.nn.Module):
     """One agent's decoder training walk with its static switches, as a module whose parameters
     are the decoder's (the callable torch.cuda.make_graphed_callables captures)."""
 
-    def __init__(self, decoder, **opts):
+    def __init__(self, decoder, n_agents=0, **opts):
         super().__init__()
         self.decoder = decoder
+        self.n_agents = n_agents   # > 0: the inputs are tgt, qpos, the agents' mem rows, their pos rows
         self.opts = opts
 
-    def forward(self, tgt, qpos, mem, pos, seed):
+    def forward(self, tgt, qpos, *rest):
+        *rows, seed = rest
+        n = self.n_agents
+        mem, pos = (list(rows[:n]), list(rows[n:])) if n else (rows[0], rows[1])
         return self.decoder.train_rows(tgt, qpos, mem, pos, seed_dev=seed, **self.opts)
 
 
@@ -218,17 +222,15 @@ class HeadTrainMixin:
             poss.append(self._mlp_t(coords, self.rv_embedding).view(B, V * h * w_, C))
         return torch.cat(mems, 1), torch.cat(poss, 1)
 
-    def _decoder_t(self, tgt, qpos, mem, pos, mask_dict, agent=0):
+    def _decoder_t(self, tgt, qpos, mem, pos, mask_dict):
         """PETRTransformerDecoder with the training op walk (post-norm,
         petr_transformer.py:324-487; mmcv BaseTransformerLayer): the decoder's
         own train_rows, with this head's DN padding and dropout switches.
+        mem / pos may be lists (one per agent: every agent's decoder in one walk).
         With OPTIONS.train_graph (CMT_TRAIN_GRAPH=1; off by default) the walk's
         forward and backward are HIP graphs (torch.cuda.make_graphed_callables)
-        captured once per agent and shape, the attention dropout seed drawn on
-        the device each step: the Python thread issues a coop step in 34.9
-        instead of 39.2 ms, but the step runs at 27.7 against 28.8 steps/s op
-        by op (profiles/r5_experiments.txt r5ai) -- the GPU, not the host, then
-        bounds it."""
+        captured once per shape, the attention dropout seed drawn on the device
+        each step (profiles/r5_experiments.txt r5ai, r5at)."""
         pad = mask_dict["pad_size"] if mask_dict else 0
         group = mask_dict["single_pad"] if mask_dict else 0
         dec = self.transformer.decoder
@@ -236,10 +238,11 @@ class HeadTrainMixin:
                 and not torch.cuda.is_current_stream_capturing()):
             return dec.train_rows(tgt, qpos, mem, pos, pad=pad, group=group, dropout=self.train_dropout,
                                   cross_fp16=self.train_cross_fp16)
-        ins = (tgt, qpos, mem, pos)
-        # a graph reads its inputs, parameters and outputs at fixed addresses: one per agent slot
-        # (two agents' outputs are alive together), shape, DN geometry and parameter storage
-        key = (agent, pad, group, self.train_dropout, self.train_cross_fp16,
+        agents = isinstance(mem, (list, tuple))
+        ins = (tgt, qpos) + (tuple(mem) + tuple(pos) if agents else (mem, pos))
+        # a graph reads its inputs, parameters and outputs at fixed addresses: one per shape, DN
+        # geometry and parameter storage
+        key = (pad, group, self.train_dropout, self.train_cross_fp16,
                tuple((tuple(t.shape), t.requires_grad) for t in ins),
                tuple(p.data_ptr() for p in dec.parameters()))
         cache = self.__dict__.setdefault("_dec_graphs", {})
@@ -248,7 +251,7 @@ class HeadTrainMixin:
         if fn is None:
             if len(cache) >= 8:          # shapes follow the GT count: keep the cache bounded
                 cache.clear()
-            step = _DecoderStep(dec, pad=pad, group=group, dropout=self.train_dropout,
+            step = _DecoderStep(dec, len(mem) if agents else 0, pad=pad, group=group, dropout=self.train_dropout,
                                 cross_fp16=self.train_cross_fp16)
             samples = tuple(t.detach().clone().requires_grad_(t.requires_grad) for t in ins) + (seed.clone(),)
             fn = cache[key] = torch.cuda.make_graphed_callables(step, samples, allow_unused_input=True)
@@ -299,13 +302,23 @@ class HeadTrainMixin:
         ref, mask_dict = self.prepare_for_dn_train(B, gt_boxes, gt_labels, rand_prob)
         rp = inverse_sigmoid(ref.clone()).sigmoid()
         qpos = self._mlp_t(_pos2embed(rp, C), self.bev_embedding)
-        decs = []
+        qs, mems, poss = [], [], []
         for x, x_img, metas in agents:
             q = qpos
             if x_img is not None and self.rv_embedding is not None:
                 q = q + self._rv_query_embed_t(rp, metas)
             mem, pos = self._memory_t(x, x_img, metas, B)
-            decs.append(self._decoder_t(torch.zeros_like(q), q, mem, pos, mask_dict, agent=len(decs)))
+            qs.append(q)
+            mems.append(mem)
+            poss.append(pos)
+        if len(agents) > 1:
+            # the agents' decoders as one walk: the query side of every layer on all agents' rows at
+            # once (half the launches of two walks), the cross-attention per agent: 28.0-29.2 ->
+            # 31.8-32.5 steps/s (profiles/r5_experiments.txt r5as)
+            qa = torch.cat(qs, 0)
+            decs = list(self._decoder_t(torch.zeros_like(qa), qa, mems, poss, mask_dict).split(B, dim=1))
+        else:
+            decs = [self._decoder_t(torch.zeros_like(qs[0]), qs[0], mems[0], poss[0], mask_dict)]
         # coop max fusion as the reference writes it (cmt_head_coop.py:388-389): torch.max over the
         # stacked agents routes each element's gradient to ONE agent (the max index), also on ties
         dec = decs[0] if len(decs) == 1 else torch.max(torch.stack(decs), 0).values

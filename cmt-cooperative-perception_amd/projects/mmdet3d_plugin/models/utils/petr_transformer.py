@@ -94,7 +94,9 @@ def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cros
     core applies the DN mask (pad, group) and attn_drop, both attentions the
     dropout_layer after their out-projection (mmcv's deprecated ``dropout``
     kwarg sets both, 0.1 in every config); the cross core emulates flash-attn's
-    fp16 inputs when cross_fp16."""
+    fp16 inputs when cross_fp16.  memk / mem may be lists, one [B, Nk_a, C] pair
+    per agent whose queries are the consecutive B-row blocks of tgt / qpos: the
+    query-side products run once for all agents, the cross-attention per agent."""
     from . import train_ops as ops
     sa, ca, ffn, nm = lay.attentions[0], lay.attentions[1], lay.ffns[0], lay.norms
     H = sa.num_heads
@@ -112,8 +114,13 @@ def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cros
     w = ca.attn
     wq, wk, wv = w.in_proj_weight.chunk(3)
     bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
-    o = ops.attention(ops.linear(tgt + qpos, wq, bq), ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H,
-                      fp16=cross_fp16)
+    qx = ops.linear(tgt + qpos, wq, bq)
+    if isinstance(mem, (list, tuple)):
+        nb = qx.shape[0] // len(mem)
+        o = torch.cat([ops.attention(qx[i * nb:(i + 1) * nb], ops.linear(mk, wk, bk), ops.linear(m, wv, bv), H,
+                                     fp16=cross_fp16) for i, (mk, m) in enumerate(zip(memk, mem))], 0)
+    else:
+        o = ops.attention(qx, ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H, fp16=cross_fp16)
     tgt = ops.layer_norm(tgt + drop(ops.linear(o, w.out_proj.weight, w.out_proj.bias), ca.drop_prob),
                          nm[1].weight, nm[1].bias, nm[1].eps)
     l1, l2 = ffn.layers[0][0], ffn.layers[1]
@@ -462,9 +469,10 @@ class PETRTransformerDecoder(nn.Module):
         (petr_transformer.py:347-371), nan_to_num (cmt_head.py:499) ->
         [L, B, Nq, C], differentiable in every input and parameter.
         seed_dev: int32 device tensor [1], the attention dropout seed read on the device
-        (no host draw: the graph-captured form, train_engine._decoder_t)."""
+        (no host draw: the graph-captured form, train_engine._decoder_t).  mem / pos may be
+        lists (one per agent, train_layer): every agent's decoder in one walk."""
         from . import train_ops as ops
-        memk = mem + pos
+        memk = [m + p for m, p in zip(mem, pos)] if isinstance(mem, (list, tuple)) else mem + pos
         outs = []
         if seed_dev is not None:
             seed0 = 0
