@@ -990,6 +990,38 @@ int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
 extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, false); }
 extern "C" int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, true); }
 
+extern "C" int cmt_linear_bwd_bf16x3(const float* dY, const float* X, const float* W, float* dX, float* dW, float* dB,
+                                     int M, int K, int N, int64_t ldx, int ksplit, void* stream) {
+    CMT_REQUIRE(dY && X && W && M > 0 && K > 0 && N > 0 && ldx >= K, "cmt_linear_bwd_bf16x3: bad arguments");
+    CMT_REQUIRE(dB == nullptr || dW != nullptr, "cmt_linear_bwd_bf16x3: dB comes with dW");
+    hipStream_t s = (hipStream_t)stream;
+    if (dX) {
+        cmt_gemm_ex_args a{};
+        a.M = M; a.N = K; a.K = N; a.batch = 1; a.alpha = 1.f; a.beta = 0.f; a.ksplit = 1;
+        a.A = dY; a.a_sm = N; a.a_sk = 1;
+        a.B = W; a.b_sn = 1; a.b_sk = K;
+        a.C = dX; a.ldc = K;
+        const int rc = gemm_ex_launch(&a, stream, true);
+        if (rc != 0) return rc;
+    }
+    if (dW) {
+        cmt_gemm_ex_args a{};
+        a.M = N; a.N = K; a.K = M; a.batch = 1; a.alpha = 1.f;
+        a.ksplit = ksplit < 1 ? 1 : ksplit;
+        a.beta = a.ksplit > 1 ? 1.f : 0.f;
+        a.A = dY; a.a_sm = 1; a.a_sk = N;
+        a.B = X; a.b_sn = 1; a.b_sk = ldx;
+        a.C = dW; a.ldc = K;
+        a.a_rowsum = dB;
+        if (a.ksplit > 1) CMT_REQUIRE(hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s) == hipSuccess,
+                                      "cmt_linear_bwd_bf16x3: memset");
+        if (dB) CMT_REQUIRE(hipMemsetAsync(dB, 0, (size_t)N * sizeof(float), s) == hipSuccess,
+                            "cmt_linear_bwd_bf16x3: memset");
+        return gemm_ex_launch(&a, stream, true);
+    }
+    return 0;
+}
+
 // shared_conv's weight gradient as the bf16x3 GEMM dW[cout][n] = sum_r dY[r][cout] im2col(X)[r][n]
 // with the im2col operand gathered inside the kernel (OP_IM): no [rows, 9 Cin] matrix
 extern "C" int cmt_conv3x3_wgrad_bf16x3(const float* X, const float* dY, float* dW, int nimg, int H, int W, int Cin,

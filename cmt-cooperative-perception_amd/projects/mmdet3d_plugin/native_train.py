@@ -91,6 +91,25 @@ def linear_bwd(dY, X, W, need_dx=True, need_dw=True, need_db=True):
     Nn = W.shape[0]
     dY = dY.contiguous()
     dX = dW = dB = None
+    if _gemm_mode == "bf16x3" and (need_dx or need_dw):
+        # one native call: both GEMMs, the split-K / bias-gradient zeroing on the stream (ABI 23)
+        _f32(dY, X, W)
+        if X.stride(1) != 1 or not W.is_contiguous():
+            raise RuntimeError("linear_bwd: X rows and W must be contiguous")
+        dev = X.device
+        if need_dx:
+            dX = torch.empty((M, K), dtype=torch.float32, device=dev)
+        if need_dw:
+            dW = torch.empty((Nn, K), dtype=torch.float32, device=dev)
+            if need_db:
+                dB = torch.empty((Nn,), dtype=torch.float32, device=dev)
+        N._check(N.lib().cmt_linear_bwd_bf16x3(dY.data_ptr(), X.data_ptr(), W.data_ptr(), _ptr(dX), _ptr(dW),
+                                                _ptr(dB), M, K, Nn, X.stride(0),
+                                                _ksplit(M, Nn, K) if need_dw else 1, N._stream()),
+                 "cmt_linear_bwd_bf16x3")
+        if need_db and dB is None:
+            dB = dY.sum(0)
+        return dX, dW, dB
     if need_dx:
         dX = torch.empty((M, K), dtype=torch.float32, device=X.device)
         gemm_ex(dY, (Nn, 1), W, (1, W.stride(0)), dX, M=M, N_=K, K=Nn, ldc=K)

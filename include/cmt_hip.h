@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 22
+#define CMT_ABI_VERSION 23
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -549,6 +549,15 @@ int cmt_gemm_f32_ex(const cmt_gemm_ex_args* args, void* stream);
  * the training step's Linear forward / dX / dW (the reference's fp32 cuBLAS
  * GEMMs, which torch 1.9.1 runs as TF32, ~2^-11, on Ampere by default). */
 int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* args, void* stream);
+/* A Linear's backward in one call (ABI 23) on cmt_gemm_bf16x3_ex's arithmetic:
+ * dX[M][K] = dY W (dX optional), dW[N][K] = dY^T X and dB[N] = the column sums of
+ * dY (both optional; dB needs dW), with dY [M][N] and W [N][K] contiguous and X
+ * [M][K] of row stride ldx.  dW and dB are overwritten: when the weight-gradient
+ * reduction is split (ksplit > 1) or dB is asked for, they are zeroed on the
+ * stream first and accumulated with f32 atomics.  Replaces, per call, the two
+ * GEMM launches and the zero fill a caller of cmt_gemm_bf16x3_ex issues. */
+int cmt_linear_bwd_bf16x3(const float* dY, const float* X, const float* W, float* dX, float* dW, float* dB,
+                          int M, int K, int N, int64_t ldx, int ksplit, void* stream);
 
 /* Attention forward with row statistics, and its backward (attn_train.hip),
  * exact f32, head_dim 32.  Replaces, in the training step, the fp32
