@@ -263,8 +263,7 @@ class HeadTrainMixin:
         L, B, Nq, C = x.shape
         k = task.final_kernel
         if k == 3:   # conv along queries, zero padded per (layer, sample): taps q-1, q, q+1
-            xp = F.pad(x, (0, 0, 1, 1))
-            xin = torch.cat([xp[:, :, 0:Nq], xp[:, :, 1:Nq + 1], xp[:, :, 2:Nq + 2]], -1)   # [L, B, Nq, 3C]
+            xin = ops.taps3(x)                                                          # [L, B, Nq, 3C]
         else:
             xin = x
         out = {}
@@ -277,8 +276,7 @@ class HeadTrainMixin:
             h = ops.group_layer_norm(h.reshape(L, B * Nq, hc), gln.weight, gln.bias, gln.eps).view(L, B, Nq, hc)
             h = torch.relu(h)
             if k == 3:
-                hp = F.pad(h, (0, 0, 1, 1))
-                h = torch.cat([hp[:, :, 0:Nq], hp[:, :, 1:Nq + 1], hp[:, :, 2:Nq + 2]], -1)
+                h = ops.taps3(h)
             on = c2.weight.shape[0] // L
             w2 = c2.weight.view(L, on, hc, k).permute(0, 1, 3, 2).reshape(L, on, k * hc)
             b2 = c2.bias.view(L, on)

@@ -116,8 +116,9 @@ def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cros
     bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
     qx = ops.linear(tgt + qpos, wq, bq)
     if isinstance(mem, (list, tuple)):
-        nb = qx.shape[0] // len(mem)
-        o = torch.cat([ops.attention(qx[i * nb:(i + 1) * nb], ops.linear(mk, wk, bk), ops.linear(m, wv, bv), H,
+        # split, not slicing: its backward is one cat where each slice's is a zero fill + copy + add
+        qxs = qx.split(qx.shape[0] // len(mem), 0)
+        o = torch.cat([ops.attention(qxs[i], ops.linear(mk, wk, bk), ops.linear(m, wv, bv), H,
                                      fp16=cross_fp16) for i, (mk, m) in enumerate(zip(memk, mem))], 0)
     else:
         o = ops.attention(qx, ops.linear(memk, wk, bk), ops.linear(mem, wv, bv), H, fp16=cross_fp16)

@@ -24,7 +24,7 @@ from ... import native
 from ... import native_train as T
 from ...runtime import SPLIT
 
-__all__ = ["linear", "linear_batched", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss"]
+__all__ = ["linear", "linear_batched", "taps3", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss"]
 
 
 class _Linear(torch.autograd.Function):
@@ -102,6 +102,32 @@ def attention(q, k, v, num_heads, *, dn_pad=0, dn_group=0, fp16=False, dropout_p
     return _Attention.apply(q.contiguous(), k.contiguous(), v.contiguous(), num_heads,
                             1.0 / math.sqrt(q.shape[-1] // num_heads), dn_pad, dn_group, fp16, dropout_p, seed,
                             seed_dev)
+
+
+class _Taps3(torch.autograd.Function):
+    """x [..., Nq, C] -> [..., Nq, 3C]: the three taps q - 1, q, q + 1 of a kernel-3 Conv1d along
+    the queries (zero padded), as the GEMM operand of the task heads' grouped convs; the backward
+    sums the three shifted gradient slices (one fill + three adds, where the autograd of pad +
+    three slices + cat took a zero fill, a copy and an add per slice)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        Nq = x.shape[-2]
+        xp = torch.nn.functional.pad(x, (0, 0, 1, 1))
+        return torch.cat([xp[..., 0:Nq, :], xp[..., 1:Nq + 1, :], xp[..., 2:Nq + 2, :]], -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        Nq, C = g.shape[-2], g.shape[-1] // 3
+        gp = g.new_zeros(g.shape[:-2] + (Nq + 2, C))
+        gp[..., 0:Nq, :] += g[..., 0:C]
+        gp[..., 1:Nq + 1, :] += g[..., C:2 * C]
+        gp[..., 2:Nq + 2, :] += g[..., 2 * C:]
+        return gp[..., 1:Nq + 1, :]
+
+
+def taps3(x):
+    return _Taps3.apply(x)
 
 
 class _LayerNorm(torch.autograd.Function):
