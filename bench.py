@@ -198,16 +198,16 @@ def spawn_ranks(args):
     return dp.spawn(os.path.abspath(__file__), sys.argv[1:], args.gpus)
 
 
-def train_bench(args, env, dev):
+def train_bench(workload, steps, warmup, env, dev):
     """BASELINE configs[3]: CMTCoop head DDP training step on TUMTraf-shape
     synthetic frames (vehicle BEV 180x180 + 1 cam, infrastructure BEV 180x180
     + 3 cams, 900 queries + DN groups from 20 GT boxes, 6 layers), one frame
     per rank: training forward, Hungarian-matched losses, backward on the
     native kernels, bucketed RCCL gradient all-reduce, clip + AdamW.  Returns
-    (elapsed_max_s, steps_per_s_whole_job, last loss)."""
+    (elapsed_max_s, steps_per_s_whole_job, last loss, memory lengths, params)."""
     from projects.mmdet3d_plugin.trainer import Trainer
-    head, cfg, _, nks, _ = make_workload(args.workload, seed=dp.frame_seed(0, env), device=dev)
-    w = WORKLOADS[args.workload]
+    head, cfg, _, nks, _ = make_workload(workload, seed=dp.frame_seed(0, env), device=dev)
+    w = WORKLOADS[workload]
     head.train()
     seed = dp.frame_seed(0, env)
     B = 1
@@ -222,15 +222,17 @@ def train_bench(args, env, dev):
             m = S.synthetic_metas(1, yaws=yaws, seed=seed + 3 + 10 * i)
         agents.append((x, xi, m))
     gtb, gtl = S.synthetic_gt(B, list(head.pc_range), head.num_classes[0], n=20, seed=seed, device=dev)
-    tr = Trainer(head, lr=1e-4, weight_decay=0.01, max_norm=35.0)
     loss = [None]
-
-    def step():
-        preds = head.forward_train(agents, metas, gtb, gtl)
-        loss[0] = tr.step(head.loss(gtb, gtl, [[p] for p in preds]))
-    elapsed, value = dp.timed_frames(step, steps=args.steps, warmup=args.warmup, env=env,
-                                     sync=torch.cuda.synchronize, device=dev)
-    return elapsed, value, float(loss[0].item()), nks, sum(p.numel() for p in tr.fp.params)
+    # freeze_gc: while the steps run, the long-lived objects stay out of the cyclic collector's
+    # scans (process-wide gc.freeze, trainer.py), undone when the Trainer closes
+    with Trainer(head, lr=1e-4, weight_decay=0.01, max_norm=35.0, freeze_gc=True) as tr:
+        def step():
+            preds = head.forward_train(agents, metas, gtb, gtl)
+            loss[0] = tr.step(head.loss(gtb, gtl, [[p] for p in preds]))
+        elapsed, value = dp.timed_frames(step, steps=steps, warmup=warmup, env=env,
+                                         sync=torch.cuda.synchronize, device=dev)
+        nparam = sum(p.numel() for p in tr.fp.params)
+    return elapsed, value, float(loss[0].item()), nks, nparam
 
 
 def capture(step):
@@ -248,6 +250,48 @@ def capture(step):
             step()
     torch.cuda.current_stream().wait_stream(s)
     return graph
+
+
+def with_metas(head, metas, replay, graph=True):
+    """One timed step: the host fp64 inverse of every camera matrix + its staging into the
+    pinned buffers the captured graph's copy nodes read (cmt_head.py:428, 441-444, as the
+    reference does per forward), then the replay.  The same frame's metas are staged every
+    step, so a staging that overlaps the previous replay's copy writes identical values."""
+    if not graph or not getattr(head, "_meta_plan", None):
+        return replay
+
+    def run():
+        head.stage_metas(metas)
+        replay()
+    return run
+
+
+def side_frames(name, steps, env, dev, graph=True):
+    """GPU frames/s of another BASELINE config's forward on this run's line (no CPU leg):
+    the workload's own policy, captured and replayed like the headline."""
+    w = WORKLOADS[name]
+    set_precision(w["precision"])
+    head, _, step, nks, _ = make_workload(name, seed=dp.frame_seed(0, env), device=dev)
+    with torch.no_grad():
+        run = capture(step).replay if graph else step
+        e, v = dp.timed_frames(with_metas(head, step.metas, run, graph), steps=steps, warmup=3, env=env,
+                               sync=torch.cuda.synchronize, device=dev)
+    return {"value": round(v, 3), "unit": "frames/s", "steps": steps, "ms_per_step": round(e / steps * 1e3, 4),
+            "dtype": DTYPE_LABEL[w["precision"]], "seq_len": sum(nks), "num_query": w["nq"],
+            "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nq=w["nq"], nk=nk) for nk in nks) / 1e9, 2),
+            "workload": w["desc"]}
+
+
+def side_train(steps, warmup, env, dev):
+    """configs[3]: the coop head's DDP training step (RCCL gradient all-reduce at world > 1)."""
+    set_precision(WORKLOADS["coop"]["precision"])
+    e, v, loss, nks, nparam = train_bench("coop", steps, warmup, env, dev)
+    return {"value": round(v, 3), "unit": "steps/s (whole job, one frame per GPU per step)", "steps": steps,
+            "warmup": warmup, "ms_per_step": round(e / steps * 1e3, 3), "last_loss": round(loss, 4),
+            "dtype": "fp32 (bf16x3 GEMMs) + fp16 cross-attention core", "seq_len": sum(nks),
+            "trainable_params": nparam,
+            "workload": WORKLOADS["coop"]["desc"] + " -- TRAINING step: DN queries, Hungarian-matched focal/L1 "
+                        "losses, native backward, bucketed RCCL gradient all-reduce, clip 35 + AdamW"}
 
 
 def main():
@@ -269,6 +313,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="profiling runs: do not read the committed PMC summary")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the other configs' side keys (lidar, stress4 frames/s; coop training steps/s)")
+    ap.add_argument("--side-steps", type=int, default=20)
     ap.add_argument("--train", action="store_true",
                     help="time the head TRAINING step instead (configs[3]: use --workload coop)")
     args = ap.parse_args()
@@ -288,7 +335,7 @@ def main():
     prec = args.precision or w["precision"]
     set_precision(prec)
     if args.train:
-        elapsed, value, loss, nks, nparam = train_bench(args, env, dev)
+        elapsed, value, loss, nks, nparam = train_bench(args.workload, args.steps, args.warmup, env, dev)
         if rank == 0:
             print(json.dumps({
                 "metric": "head training steps/sec (DDP, one frame per GPU per step)", "value": round(value, 3),
@@ -309,22 +356,9 @@ def main():
     head, cfg, step, nks, _ = make_workload(args.workload, seed=dp.frame_seed(0, env), device=dev, batch=args.batch)
     metas = step.metas
 
-    def with_metas(replay):
-        """One timed step: the host fp64 inverse of every camera matrix + its staging into the
-        pinned buffers the captured graph's copy nodes read (cmt_head.py:428, 441-444, as the
-        reference does per forward), then the replay.  The same frame's metas are staged every
-        step, so a staging that overlaps the previous replay's copy writes identical values."""
-        if args.no_graph or not getattr(head, "_meta_plan", None):
-            return replay
-
-        def run():
-            head.stage_metas(metas)
-            replay()
-        return run
-
     with torch.no_grad():
         run = capture(step).replay if not args.no_graph else step
-        elapsed, value = dp.timed_frames(with_metas(run), steps=args.steps, warmup=args.warmup, env=env,
+        elapsed, value = dp.timed_frames(with_metas(head, metas, run, not args.no_graph), steps=args.steps, warmup=args.warmup, env=env,
                                          sync=torch.cuda.synchronize, device=dev)
         value *= args.batch   # frames per forward
 
@@ -346,7 +380,7 @@ def main():
             with options(bev_pos_cache=False):
                 run_r = capture(step).replay if not args.no_graph else step
                 st_r = max(10, args.steps // 2)
-                e_r, v_r = dp.timed_frames(with_metas(run_r), steps=st_r, warmup=3, env=env,
+                e_r, v_r = dp.timed_frames(with_metas(head, metas, run_r, not args.no_graph), steps=st_r, warmup=3, env=env,
                                            sync=torch.cuda.synchronize, device=dev)
             recompute = {"value": round(v_r * args.batch, 3), "unit": "frames/s", "steps": st_r,
                          "ms_per_step": round(e_r / st_r * 1e3, 4),
@@ -361,7 +395,7 @@ def main():
             set_precision("bf16")
             run_b = capture(step).replay if not args.no_graph else step
             st_b = max(10, args.steps // 2)
-            e_b, v_b = dp.timed_frames(with_metas(run_b), steps=st_b, warmup=3, env=env, sync=torch.cuda.synchronize, device=dev)
+            e_b, v_b = dp.timed_frames(with_metas(head, metas, run_b, not args.no_graph), steps=st_b, warmup=3, env=env, sync=torch.cuda.synchronize, device=dev)
             side = {"value": round(v_b, 3), "unit": "frames/s", "steps": st_b, "ms_per_step": round(e_b / st_b * 1e3, 4),
                     "dtype": "bf16 GEMM and attention operands (fp32 accumulate): ~2.5 % of scale from the "
                              "reference, outside north_star's 1e-3"}
@@ -384,6 +418,20 @@ def main():
             vrun()
         torch.cuda.synchronize()
         vox_ms = (time.perf_counter() - tv) / nvox * 1e3
+
+    # --- every other BASELINE config's number on the same line (GPU only): configs[1] lidar and
+    # configs[4] stress4 forward frames/s, configs[3] coop training steps/s (tools/benchmark.py:110-138
+    # timing pattern: warm-up, synchronize, timed loop)
+    sides = {}
+    if not args.no_side and args.workload == "fusion" and args.batch == 1:
+        del run
+        torch.cuda.empty_cache()
+        for key, fn in (("lidar", lambda: side_frames("lidar", args.side_steps, env, dev, not args.no_graph)),
+                        ("stress4", lambda: side_frames("stress4", args.side_steps, env, dev, not args.no_graph)),
+                        ("train_coop", lambda: side_train(args.side_steps, 5, env, dev))):
+            sides[key] = fn()
+            torch.cuda.empty_cache()
+        set_precision(prec)
 
     ms_per_step = elapsed / args.steps * 1e3
     # mean algorithmic FLOPs of one cross-attention launch (agents may differ in Nk)
@@ -424,6 +472,7 @@ def main():
         "bf16_policy": side,
         "weight_only_recomputed": recompute,
         "voxel_scatter_mean_ms": round(vox_ms, 4),
+        **sides,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -436,7 +436,9 @@ __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restri
         tile[i][tx] = (c < C && p < HW) ? xs[(int64_t)c * HW + p] : 0.f;
         bad |= f16_unrepresentable(tile[i][tx]);
     }
-    if constexpr (PAIR || std::is_same<TO, f16_t>::value) raise_range_flag(range_flag, bad);
+    // f16 / pair outputs cannot carry the value; an fp32 output with a flag is the training conv's
+    // input, which the split-f16 conv reads as pairs next (bf16 carries any fp32 exponent)
+    if constexpr (!std::is_same<TO, bf16_t>::value) raise_range_flag(range_flag, bad);
     __syncthreads();
     const int bo = img / nv, v = img - bo * nv;
     for (int i = ty; i < 64; i += 4) {

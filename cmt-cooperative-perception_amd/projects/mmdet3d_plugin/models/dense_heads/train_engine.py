@@ -197,11 +197,10 @@ class HeadTrainMixin:
         mems, poss = [], []
         if x is not None and self.shared_conv is not None:
             _, Cin, H, W = x.shape
-            xr = ops.nchw_rows(x, B)
+            xr = ops.nchw_rows(x, B, range_flag=self._range_flag(x.device))   # the split conv's operand
             conv = self.shared_conv.conv
             w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1)
-            y = ops.bn_relu(ops.conv3x3(xr, w, (B, H, W, Cin), range_flag=self._range_flag(x.device)),
-                            self.shared_conv.bn)
+            y = ops.bn_relu(ops.conv3x3(xr, w, (B, H, W, Cin)), self.shared_conv.bn)
             mems.append(y.view(B, H * W, C))
             cfg = self.train_cfg if self.train_cfg else self.test_cfg
             xs, ys = cfg["grid_size"][1] // self.downsample_scale, cfg["grid_size"][0] // self.downsample_scale
@@ -230,7 +229,11 @@ class HeadTrainMixin:
         With OPTIONS.train_graph (CMT_TRAIN_GRAPH=1; off by default) the walk's
         forward and backward are HIP graphs (torch.cuda.make_graphed_callables)
         captured once per shape, the attention dropout seed drawn on the device
-        each step (profiles/r5_experiments.txt r5ai, r5at)."""
+        each step (profiles/r5_experiments.txt r5ai, r5at).  Limits of the graph
+        mode: the key holds the DN padding, which follows the batch's GT count, so
+        real data with a varying GT count re-captures often (the cache keeps 8
+        shapes); a forward whose previous replay's backward has not run yet takes
+        the eager walk."""
         pad = mask_dict["pad_size"] if mask_dict else 0
         group = mask_dict["single_pad"] if mask_dict else 0
         dec = self.transformer.decoder
@@ -255,7 +258,19 @@ class HeadTrainMixin:
                                 cross_fp16=self.train_cross_fp16)
             samples = tuple(t.detach().clone().requires_grad_(t.requires_grad) for t in ins) + (seed.clone(),)
             fn = cache[key] = torch.cuda.make_graphed_callables(step, samples, allow_unused_input=True)
-        return fn(*ins, seed)
+        # a graphed callable replays into static output / saved buffers: a second forward of the same
+        # key before the first one's backward would overwrite what that backward reads -- take the
+        # eager walk for it instead (gradient accumulation, a second head pass)
+        pending = self.__dict__.setdefault("_dec_graph_pending", set())
+        if key in pending:
+            return dec.train_rows(tgt, qpos, mem, pos, pad=pad, group=group, dropout=self.train_dropout,
+                                  cross_fp16=self.train_cross_fp16)
+        out = fn(*ins, seed)
+        first = out[0] if isinstance(out, (tuple, list)) else out
+        if first.requires_grad:
+            pending.add(key)
+            first.register_hook(lambda g, k=key: pending.discard(k))
+        return out
 
     def _task_head_t(self, task, x, reference):
         """SeparateTaskHead (cmt_head.py:136-203) + box epilogue (501-513).

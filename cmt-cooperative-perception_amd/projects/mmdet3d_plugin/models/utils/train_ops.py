@@ -185,7 +185,7 @@ class _Conv3x3(torch.autograd.Function):
     """NHWC rows [B*H*W, Cin] -> [B*H*W, Cout]; weight [Cout, 9*Cin] tap-major."""
 
     @staticmethod
-    def forward(ctx, x, w, geom, range_flag=None):
+    def forward(ctx, x, w, geom):
         B, H, W, Cin = geom
         Cout = w.shape[0]
         y = torch.empty((B * H * W, Cout), dtype=torch.float32, device=x.device)
@@ -195,16 +195,16 @@ class _Conv3x3(torch.autograd.Function):
                         c_bstride=H * W * Cout)
         else:
             # the split-f16 implicit-GEMM conv of the inference path (three f16 MFMA passes on pair
-            # operands, ~2^-21 relative per product): 3x the exact-f32 MFMA's speed at this size
-            # operands the pair format cannot carry (|x| >= 65520, non-finite) make a non-finite or
-            # out-of-range conv output, which the kernel's epilogue reports through range_flag (the
-            # head's device word, CmtHead.check_input_range(); no host sync in the step)
+            # operands, ~2^-21 relative per product): 3x the exact-f32 MFMA's speed at this size.
+            # Its input operand is range-checked where it is laid out (nchw_rows(range_flag=...):
+            # the head's device word, CmtHead.check_input_range(); no host sync in the step); the
+            # conv OUTPUT stays fp32 into BatchNorm, so a large but valid output is not flagged
             xs = native.split_rows(x)
             wh = w.detach().half()                                   # pair weights (no host range check:
             ws = torch.stack([wh, (w.detach() - wh.float()).half()], dim=-2).contiguous().view(SPLIT)   # no sync)
             native.gemm(xs, ws, y, M=H * W, N=Cout, K=9 * Cin, lda=Cin, ldw=9 * Cin, ldc=Cout,
                         a_mode=native.A_CONV3X3, conv=(H, W, Cin), batch=B, a_bstride=H * W * Cin,
-                        c_bstride=H * W * Cout, range_flag=range_flag)
+                        c_bstride=H * W * Cout)
         ctx.save_for_backward(x, w)
         ctx.geom = geom
         return y
@@ -235,13 +235,11 @@ class _Conv3x3(torch.autograd.Function):
             native.gemm(dy.contiguous(), wt, dx, M=H * W, N=Cin, K=9 * Cout, lda=Cout, ldw=9 * Cout, ldc=Cin,
                         a_mode=native.A_CONV3X3, conv=(H, W, Cout), batch=B, a_bstride=H * W * Cout,
                         c_bstride=H * W * Cin)
-        return dx, dw, None, None
+        return dx, dw, None
 
 
-def conv3x3(x_rows, w_tap_major, geom, range_flag=None):
-    """range_flag: the head's f16-operand range word (int32 device tensor), set when the split
-    conv met a value the f16 pair format cannot carry."""
-    return _Conv3x3.apply(x_rows, w_tap_major, geom, range_flag)
+def conv3x3(x_rows, w_tap_major, geom):
+    return _Conv3x3.apply(x_rows, w_tap_major, geom)
 
 
 class _NchwRows(torch.autograd.Function):
@@ -251,22 +249,25 @@ class _NchwRows(torch.autograd.Function):
     the maps receives its gradient as in the reference."""
 
     @staticmethod
-    def forward(ctx, x, B):
+    def forward(ctx, x, B, range_flag=None):
         BV, C, H, W = x.shape
         y = torch.empty((BV * H * W, C), dtype=torch.float32, device=x.device)
         native.nchw_to_rows(x.contiguous().float(), y, nb=B, nv=BV // B, C=C, HW=H * W, ldy=C,
-                            rows_per_batch=BV // B * H * W)
+                            rows_per_batch=BV // B * H * W, range_flag=range_flag)
         ctx.shape = x.shape
         return y
 
     @staticmethod
     def backward(ctx, dy):
         BV, C, H, W = ctx.shape
-        return dy.view(BV, H * W, C).transpose(1, 2).reshape(BV, C, H, W), None
+        return dy.view(BV, H * W, C).transpose(1, 2).reshape(BV, C, H, W), None, None
 
 
-def nchw_rows(x, B):
-    return _NchwRows.apply(x, B)
+def nchw_rows(x, B, range_flag=None):
+    """range_flag: the head's f16-operand range word (int32 device tensor), set when an input
+    value cannot be carried as an f16 pair (|x| >= 65520, non-finite) -- for rows a split-f16
+    kernel reads next (the training shared_conv)."""
+    return _NchwRows.apply(x, B, range_flag)
 
 
 class _DetLoss(torch.autograd.Function):

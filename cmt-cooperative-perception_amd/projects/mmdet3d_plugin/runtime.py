@@ -129,7 +129,9 @@ class Options:
                            # their own instead of inside the one-launch RV position MLP
     train_graph: bool      # CMT_TRAIN_GRAPH=1 (off by default): the training decoder's forward / backward
                            # replayed as HIP graphs instead of issued op by op (train_engine._decoder_t):
-                           # host issue 39.2 -> 34.9 ms/step, step rate 27.7 vs 28.8 steps/s (r5ai)
+                           # host issue 39.2 -> 34.9 ms/step, step rate 27.7 vs 28.8 steps/s (r5ai).
+                           # Limits: one capture per DN padding (it follows the GT count; 8 kept), and
+                           # a second forward before the first one's backward runs eagerly
 
 
 def _env_on(name):

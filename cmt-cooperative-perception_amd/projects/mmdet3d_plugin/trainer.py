@@ -101,7 +101,9 @@ class _GradBuckets:
     every rank's finish() then sees the summed flag, drops the step's
     gradients and raises PeerBackwardError.  (A backward that raises after
     its last bucket was launched -- all gradients already exchanged -- is not
-    covered: the flag no longer travels.)"""
+    covered: the flag no longer travels; abort() then returns False and the
+    Trainer refuses every later step, since this rank's weights can no longer
+    follow the others'.)"""
 
     def __init__(self, fp, bucket_bytes, group):
         self.fp, self.group = fp, group
@@ -159,13 +161,16 @@ class _GradBuckets:
 
     def abort(self):
         """This rank's backward raised: flag the step and complete its
-        all-reduce sequence (see the class docstring)."""
-        if self.next < len(self.buckets):
+        all-reduce sequence (see the class docstring).  Returns whether the
+        flag travels (False: the last bucket was already launched)."""
+        travels = self.next < len(self.buckets)
+        if travels:
             self.fp.grad[0] = 1.0
         self._launch_ready(upto=len(self.buckets))
         for w in self.works:
             w.wait()
         self.reset()
+        return travels
 
     def finish(self):
         self._launch_ready(upto=len(self.buckets))
@@ -190,14 +195,17 @@ class Trainer:
     that started from different initialisations train the same model."""
 
     def __init__(self, module, lr=1e-4, weight_decay=0.01, betas=(0.9, 0.999), eps=1e-8, max_norm=35.0,
-                 bucket_mb=25, group=None, freeze_gc=True):
+                 bucket_mb=25, group=None, freeze_gc=False):
         self.module = module
-        # freeze_gc: after the first step, the objects alive then (module, weight packs, optimizer
-        # state, caches) leave the cyclic collector's generations (gc.freeze), so the one collection
-        # a step triggers scans only that step's objects: 33.1-33.8 -> 34.6-34.9 steps/s coop
-        # (profiles/r5_experiments.txt r5aw)
+        # freeze_gc (opt-in, PROCESS-WIDE): after the first step gc.freeze() moves every object alive
+        # in the process then -- the module, weight packs, optimizer state, but also the caller's
+        # objects and iterators -- out of the cyclic collector's generations, so the one collection
+        # a step triggers scans only that step's objects (33.1-33.8 -> 34.6-34.9 steps/s coop,
+        # profiles/r5_experiments.txt r5aw).  Cycles among the frozen objects are not collected
+        # until close() (or leaving the Trainer's `with` block) calls gc.unfreeze().
         self.freeze_gc = freeze_gc
         self._gc_frozen = False
+        self._broken = None
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         self.fp = FlatParams(module, status_words=64 if multi else 0)
         self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
@@ -231,10 +239,34 @@ class Trainer:
         for p in self.fp.params:
             torch.autograd.graph.increment_version(p)
 
+    def close(self):
+        """Undo the process-wide gc.freeze() of ``freeze_gc`` and detach the
+        gradient hooks; the Trainer takes no further step."""
+        if self._gc_frozen:
+            gc.unfreeze()
+            self._gc_frozen = False
+        if self.buckets is not None:
+            for h in self.buckets.handles:
+                h.remove()
+            self.buckets = None
+        self._broken = self._broken or "the Trainer was closed"
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def _check_usable(self):
+        if self._broken:
+            raise RuntimeError(f"Trainer unusable: {self._broken}")
+
     def backward(self, losses):
         """Backward of the summed losses into freshly zeroed flat gradients
         (no accumulation across calls: a second backward() before step()
         replaces the first one's gradients and exchange)."""
+        self._check_usable()
         total = sum(losses.values()) if isinstance(losses, dict) else losses
         if self.buckets is not None:
             self.buckets.drain()   # outstanding all-reduces write fp.grad: finish them before zeroing it
@@ -242,12 +274,16 @@ class Trainer:
         try:
             total.backward()
         except BaseException:
-            if self.buckets is not None:
-                self.buckets.abort()
+            if self.buckets is not None and not self.buckets.abort():
+                # every gradient was already exchanged: the other ranks apply this step and this
+                # rank cannot, so its weights would drift from theirs -- refuse every later step
+                self._broken = ("a backward raised after its last gradient bucket was exchanged; "
+                                "the other ranks applied that step and this rank did not")
             raise
         return total
 
     def step(self, losses):
+        self._check_usable()
         total = self.backward(losses)
         if self.buckets is not None:
             self.buckets.finish()

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 final evidence on the final tree: full GPU suite (parity lines -> r5_parity), smoke,
+# Final evidence of a round on the final tree: full GPU suite (parity lines -> r5_parity), smoke,
 # rocprofv3 kernel trace + stats of the default bench, one 'ref' frame's timeline, FETCH_SIZE and
 # WRITE_SIZE passes (separate; the roofline form: split combine as its own launch), the default
 # bench line and the coop training bench.
 set -uo pipefail
-TAG=${1:-r5zfinal}
+TAG=${1:?tag}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-5 counter passes, one rocprofv3 --pmc run per group (gfx950 slot limits: <= 8 SQ,
+# Counter passes, one rocprofv3 --pmc run per group (gfx950 slot limits: <= 8 SQ,
 # FETCH_SIZE and WRITE_SIZE in passes of their own), over one probe command.
-#   bash dev/r5_pmc.sh OUTDIR MATCH probe.py args...
+#   bash dev/pmc_passes.sh OUTDIR MATCH probe.py args...
 set -uo pipefail
 OUT=$1; MATCH=$2; shift 2
 mkdir -p "$OUT"

@@ -445,8 +445,9 @@ int cmt_masked_view_sum_ex(const float* X, const float* mask, int B, int V, int 
 int cmt_nchw_to_rows(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype,
                      int64_t ldy, int64_t rows_per_batch, int64_t row_offset, void* stream);
 /* cmt_nchw_to_rows_ex (ABI 18): the same with the f16-operand range guard of
- * cmt_gemm_args.range_flag: for a CMT_F16 / CMT_F16P ydtype, an input element that is
- * non-finite or |x| >= 65520 ORs 1 into *range_flag (NULL: off). */
+ * cmt_gemm_args.range_flag: for a CMT_F32 / CMT_F16 / CMT_F16P ydtype, an input element
+ * that is non-finite or |x| >= 65520 ORs 1 into *range_flag (NULL: off; CMT_F32 with a flag:
+ * rows a split-f16 consumer reads as pairs next, e.g. the training shared_conv). */
 int cmt_nchw_to_rows_ex(const float* X, int nb, int nv, int C, int HW, void* Y, int ydtype,
                         int64_t ldy, int64_t rows_per_batch, int64_t row_offset, int* range_flag, void* stream);
 int cmt_cast(const void* X, int xdtype, void* Y, int ydtype, int64_t n, void* stream);

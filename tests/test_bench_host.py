@@ -65,6 +65,9 @@ def test_bench_line_names_what_it_keeps():
     src = inspect.getsource(bench.main)
     assert '"weight_only_kept"' in src and '"weight_only_recomputed"' in src
     assert len(bench.WEIGHT_ONLY_KEPT) == 3
-    assert "stage_metas" in src            # the host fp64 inverse + staging runs once per timed step
+    assert "with_metas(head, metas, run" in src     # every timed step re-stages the camera matrices ...
+    assert "stage_metas" in inspect.getsource(bench.with_metas)   # ... (host fp64 inverse + staging)
+    # every other BASELINE config's number rides on the default line
+    assert all(k in src for k in ('"lidar"', '"stress4"', '"train_coop"'))
     _, _, fwd, _, _ = bench.make_workload("fusion", seed=0)
     assert len(fwd.metas) == 1 and "lidar2img" in fwd.metas[0]

@@ -194,9 +194,15 @@ def test_eval_after_train_step_sees_new_weights(dev):
     head.train_dropout = False
     gtb, gtl = _gt(1, list(head.pc_range), head.num_classes[0], 4, seed=8)
     gtb, gtl = [b.to(dev) for b in gtb], [l.to(dev) for l in gtl]
-    tr = Trainer(head, lr=1e-2)
-    preds = head.forward_train([(x, None, [dict()])], [dict()], gtb, gtl)
-    tr.step(head.loss(gtb, gtl, [[p] for p in preds]))
+    import gc
+    frozen0 = gc.get_freeze_count()
+    with Trainer(head, lr=1e-2, freeze_gc=True) as tr:   # opt-in, process-wide gc.freeze ...
+        preds = head.forward_train([(x, None, [dict()])], [dict()], gtb, gtl)
+        tr.step(head.loss(gtb, gtl, [[p] for p in preds]))
+        assert gc.get_freeze_count() > frozen0
+    assert gc.get_freeze_count() == 0                     # ... undone by close()
+    with pytest.raises(RuntimeError, match="closed"):
+        tr.step(head.loss(gtb, gtl, [[p] for p in preds]))
     head.eval()
     with torch.no_grad():
         after = head([x], None, [dict()])[0][0]["cls_logits"].clone()
@@ -351,9 +357,10 @@ def test_transformer_forward_with_dn_mask_training(dev, parity_log):
 
 def test_training_conv_range_guard(dev):
     """The training shared_conv runs on split-f16 pairs (train_ops._Conv3x3): a BEV value the
-    pair format cannot carry (|x| >= 65520) sets the head's range word in the conv's epilogue --
-    no host sync in the step -- and CmtHead.check_input_range() raises after the step; a clean
-    step leaves it clear."""
+    pair format cannot carry (|x| >= 65520) sets the head's range word in the layout pass that
+    feeds the conv -- no host sync in the step -- and CmtHead.check_input_range() raises after the
+    step; a clean step leaves it clear, and so does a valid input whose fp32 conv OUTPUT is beyond
+    the f16 range (it goes to BatchNorm in fp32, never as a pair: ADVICE r5)."""
     from projects.mmdet3d_plugin import synthetic as S
     head, _, _ = S.build_synthetic_head("cmt_lidar_nus", num_query=32, num_layers=1, grid_size=[128, 128, 40],
                                         device=dev)
@@ -372,3 +379,9 @@ def test_training_conv_range_guard(dev):
     with pytest.raises(ValueError):
         head.check_input_range()
     head.check_input_range()                            # cleared by the raise
+    big = torch.full_like(x, 60000.0)                   # representable input ...
+    with torch.no_grad():
+        head.shared_conv.conv.weight.abs_()             # ... whose conv output is ~1e6: not flagged
+    head.forward_train([(big, None, [dict()])], [dict()], gtb, gtl)
+    torch.cuda.synchronize()
+    head.check_input_range()

@@ -65,6 +65,52 @@ def test_gemm_ex_transposes(dev, M, N, K, ta, tb, mode):
         assert (C3.cpu().double() - ref3).abs().max().item() < tol * tiny * tiny
 
 
+@pytest.mark.parametrize("M,K,N,ks,case", [
+    (384, 256, 256, 1, "dX and dW on the k-wave kernel (< 256 tiles, >= 4 k-steps, unsplit)"),
+    (8192, 256, 1024, 8, "dW on 128 x 128 tiles, the split re-chosen 8 -> 32 after the zero fill"),
+    (4096, 256, 64, 8, "dX on the plain 64 x 64 tile (2-step reduction), dW split on 64 x 64"),
+    (30, 96, 48, 2, "split 2 rounded back to 1 by the k chunk while beta is 1 (zero-filled dW)")])
+@pytest.mark.parametrize("need", [(True, True, True), (True, True, False), (True, False, True), (False, True, True)])
+def test_linear_bwd_bf16x3_direct(dev, M, K, N, ks, case, need):
+    """cmt_linear_bwd_bf16x3 (ABI 23, one call: dX = dY W, dW = dY^T X with the bias gradient
+    as the A row sums of the weight-gradient GEMM) against float64, with the split chosen
+    by the caller -- each shape selects another kernel path (``case``) -- and every
+    need_dx / need_dw / need_db combination (need_db without need_dw: the column sum)."""
+    from projects.mmdet3d_plugin import native as N_
+    T = _T()
+    need_dx, need_dw, need_db = need
+    g = torch.Generator().manual_seed(M + K + N)
+    dY, X, W = torch.randn(M, N, generator=g), torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    dYd, Xd, Wd = dY.to(dev), X.to(dev), W.to(dev)
+    if need_dw:       # the raw entry point, with this case's split (the wrapper picks its own)
+        dX = torch.full((M, K), float("nan"), device=dev) if need_dx else None
+        dW = torch.full((N, K), float("nan"), device=dev)
+        dB = torch.full((N,), float("nan"), device=dev) if need_db else None
+        p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        N_._check(N_.lib().cmt_linear_bwd_bf16x3(dYd.data_ptr(), Xd.data_ptr(), Wd.data_ptr(), p(dX), p(dW), p(dB),
+                                                 M, K, N, K, ks, N_._stream()), "cmt_linear_bwd_bf16x3")
+    else:
+        prev = T._gemm_mode
+        T.set_train_gemm("bf16x3")
+        try:
+            dX, dW, dB = T.linear_bwd(dYd, Xd, Wd, need_dx=need_dx, need_dw=False, need_db=need_db)
+        finally:
+            T.set_train_gemm(prev)
+    torch.cuda.synchronize()
+    want = {"dX": dY.double() @ W.double(), "dW": dY.double().t() @ X.double(), "dB": dY.double().sum(0)}
+    got = {"dX": dX, "dW": dW, "dB": dB}
+    for name, on in (("dX", need_dx), ("dW", need_dw), ("dB", need_db)):
+        if not on:
+            assert got[name] is None, (case, name)
+            continue
+        red = {"dX": N, "dW": M, "dB": M}[name]
+        # bf16x3: ~2^-16 of each product, a random walk over the reduction; dB is an fp32 sum
+        tol = (2 ** -15 if name != "dB" else 1e-6) * math.sqrt(red) * 4
+        err = (got[name].cpu().double() - want[name]).abs().max().item()
+        assert err < tol, (case, name, err, tol)
+
+
+
 @pytest.mark.parametrize("L,M,K,N", [(6, 1100, 192, 64), (3, 70, 33, 10)])
 def test_linear_batched_fwd_bwd(dev, L, M, K, N):
     """train_ops.linear_batched (one batched launch per product, per-entry bias through the

@@ -137,7 +137,22 @@ def _trainer_worker(rank, world, port, q):
     local = torch.autograd.grad(model(xs[1]).pow(2).sum(), tr.fp.params)
     nb = tr.buckets.finish()
     out.append((torch.cat([t.reshape(-1) for t in local]).numpy(), tr.fp.grad[tr.fp.head:].numpy().copy(), nb))
-    q.put((rank, out, seen))
+    # 4) rank 0's backward raises AFTER its last bucket went out (the failure is below every
+    # parameter): rank 1 applies the step, so rank 0's Trainer refuses every later step
+    late = None
+    x = xs[0].clone().requires_grad_(True)
+    try:
+        tr.backward(model(_Boom.apply(x) if rank == 0 else x).pow(2).sum())
+        tr.buckets.finish()
+        late = "applied"
+    except RuntimeError as e:
+        late = "own" if "boom" in str(e) else str(e)
+    if rank == 0:
+        try:
+            tr.backward(model(xs[1]).pow(2).sum())
+        except RuntimeError as e:
+            late += "+refused" if "unusable" in str(e) else "+" + str(e)
+    q.put((rank, out, (seen, late)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -156,7 +171,8 @@ def test_trainer_backward_twice_and_failed_backward_keep_the_exchange():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0][2] == "own" and res[1][2] == "peer", (res[0][2], res[1][2])
+    assert res[0][2][0] == "own" and res[1][2][0] == "peer", (res[0][2], res[1][2])
+    assert res[0][2][1] == "own+refused" and res[1][2][1] == "applied", (res[0][2], res[1][2])
     for case in range(3):
         (l0, r0, nb), (l1, r1, _) = res[0][1][case], res[1][1][case]
         l0, r0, l1, r1 = (torch.from_numpy(t) for t in (l0, r0, l1, r1))
