@@ -1177,7 +1177,7 @@ int launch_x3(const cmt_gemm_args& a, hipStream_t s) {
 // zero outside the image -- from the NCHW map (each channel's run is
 // contiguous: one coalesced scalar load per channel and lane), splits it into
 // f16 hi / lo in registers and writes it to LDS once as 64-byte pixel rows (hi
-// 16 | lo 16, 16-byte chunks XOR-swizzled by (row >> 2) & 3).  The nine taps'
+// 16 | lo 16, 16-byte chunks XOR-swizzled by hsw(row)).  The nine taps'
 // A fragments are then ds_reads of that halo at a per-tap row shift (W x dy +
 // dx); a lane whose pixel sits on the left / right image edge zeroes its
 // fragment for dx = -1 / +1 (the row-wrapped neighbour is padding).  W is
@@ -1203,11 +1203,14 @@ struct HaloConv {
     static constexpr int WSLOT = 3 * WTAP;                    // one step = one kernel row (3 taps)
     static constexpr int S = 3;                               // W ring slots
     static constexpr int SMEM = 2 * HALO + S * WSLOT;
-    static constexpr int UPT = (2 * NHMAX + NTX - 1) / NTX;   // (pixel, channel octet) units per thread
+    static constexpr int UPT = (2 * NHMAX + 15 + NTX - 1) / NTX;   // (pixel, channel octet) units per thread
     static constexpr int WNW = 2, TM = 2, TN = 2;
     static_assert(SMEM <= 160 * 1024 && SMEM >= BM * BN * 4, "halo conv LDS");
     static_assert(WTAP == NTX * 16, "one 16-byte DMA per thread per tap of a W slot");
 };
+
+// halo row swizzle of conv_halo_x3_kernel (see its unit setup)
+__device__ __forceinline__ int hsw(int h) { return ((h >> 2) + 2 * ((h >> 1) & 1)) & 3; }
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -1240,20 +1243,27 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
     const float* X = (const float*)a.A + (int64_t)z * a.a_bstride;
     const pair_t* Wb = (const pair_t*)a.W;
 
-    // halo units of this thread: (halo row h, channel octet o); lanes walk consecutive rows
+    // halo units of this thread: (halo row h, channel octet o); lanes walk consecutive rows (coalesced
+    // loads), octet 1's rows start at a 16-aligned unit.  Halo row h's 16-byte chunks are XOR-swizzled
+    // by hsw(h) = ((h >> 2) + 2 ((h >> 1) & 1)) & 3: every 8-lane group of a ds_write_b128 (banks mod 32,
+    // two 64-byte rows per bank row) then stores 8 aligned consecutive rows on 8 distinct slots, and the
+    // 16-lane groups of the tap-shifted ds_read_b128 stay conflict-free at any shift.  (The former
+    // (h >> 2) & 3 put rows h and h + 2 on one slot: 2-way on every halo store, ~2.5 M extra LDS
+    // cycles per launch, profiles/r5b_convh_pmc_summary.json; permuting the lanes instead cost more
+    // in the halo loads than it saved, r6b.)
+    const int NHA = (NH + 15) & ~15;
     int u_src[UPT], u_lds[UPT];
     bool u_ok[UPT], u_on[UPT];
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
         const int u = tid + i * T::NTX;
-        const int o = u >= NH ? 1 : 0;
-        const int h = u - o * NH;
+        const int o = u >= NHA ? 1 : 0;
+        const int h = u - o * NHA;
         const int p = hs + h;
-        u_on[i] = u < 2 * NH;                                 // a unit of this tile at all
+        u_on[i] = h < NH && u < NHA + NH;                     // a unit of this tile at all
         u_ok[i] = u_on[i] && p >= 0 && p < HW;                // inside the image (else zeros)
         u_src[i] = 8 * o * HW + p;
-        const int sw = (h >> 2) & 3;
-        u_lds[i] = h * T::ROWB + ((o ^ sw) << 4);             // hi chunk; the lo chunk is (2 + o) ^ sw
+        u_lds[i] = h * T::ROWB + ((o ^ hsw(h)) << 4);         // hi chunk; the lo chunk is (2 + o) ^ hsw
     }
     float hv[UPT][8];
     auto load_halo = [&](int c) {
@@ -1396,7 +1406,7 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm) {
                     const int hr = arow[tm] + tsh;
-                    const int base = hr * T::ROWB, sw = (hr >> 2) & 3;
+                    const int base = hr * T::ROWB, sw = hsw(hr);
                     af[tm] = *(const frag*)(Hs + base + ((lh ^ sw) << 4));
                     al[tm] = *(const frag*)(Hs + base + (((2 + lh) ^ sw) << 4));
                     if ((dx == 0 && edl[tm]) || (dx == 2 && edr[tm])) {
