@@ -177,8 +177,8 @@ def cpu_baseline(workload, seconds, seed):
 
 
 def load_traffic(workload, nk):
-    """HBM bytes per launch of the dominant kernel (cross-attention core + its
-    split combine) for THIS workload's shape, from the committed rocprofv3 PMC
+    """HBM bytes per launch of the dominant kernel (the cross-attention core as
+    the frame runs it) for THIS workload's shape, from the committed rocprofv3 PMC
     summary profiles/*_<workload>_attn_pmc_summary.json (FETCH_SIZE x2 gfx950
     correction + WRITE_SIZE, separate passes; dev/traffic_summary.py).
     Raises when no summary matches the workload and key length."""
@@ -362,11 +362,10 @@ def main():
                                          sync=torch.cuda.synchronize, device=dev)
         value *= args.batch   # frames per forward
 
-        # --- dominant kernel: cross-attention, HIP events on its launch stream.  Timed with its
-        # split combine as a launch of its own (OPTIONS.chain_combine off: the frame's chain B1 does
-        # that combine in its prologue instead), so the pair is the "core + split combine" of the
-        # roofline object and of the earlier rounds' figures; PMC traffic from the same form
-        with region_timer() as rt, options(chain_combine=False):
+        # --- dominant kernel: the cross-attention core as the timed frame runs it (its 8 split
+        # partials stay in the workspace for chain B1, which combines them in its prologue, ABI 19),
+        # HIP events on its launch stream; PMC traffic from the same form
+        with region_timer() as rt:
             for _ in range(3):
                 step()
         attn_ms_all = rt.durations_ms("cross_attn")
@@ -465,7 +464,8 @@ def main():
                    "weight_only_kept": WEIGHT_ONLY_KEPT if OPTIONS.bev_pos_cache else [],
                    "camera_metas_staged_per_step": bool(getattr(head, "_meta_plan", None)) and not args.no_graph,
                    "decoder_gflop_per_frame": round(sum(decoder_frame_flops(nq=nq, nk=nk) for nk in nks) / 1e9, 2)},
-        "roofline": {"kernel": "cmt_attn_fwd (cross-attention core + split combine)", "bound": "mfma",
+        "roofline": {"kernel": "cmt_attn_fwd (cross-attention core attn_pb2_kernel; its split partials are "
+                               "combined by the next kernel, chain B1, as in the timed frame)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": round(attn_ms, 5), "flop_per_launch": flop_launch},

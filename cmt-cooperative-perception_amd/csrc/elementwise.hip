@@ -485,7 +485,8 @@ __global__ __launch_bounds__(256) void nchw_to_rows_vec_kernel(const float* __re
                 tile[cr + 16 * k][q + e] = v[k][e];
                 bad |= f16_unrepresentable(v[k][e]);
             }
-        if constexpr (PAIR || std::is_same<TO, f16_t>::value) raise_range_flag(range_flag, bad);
+        // as nchw_to_rows_kernel: every format but bf16 (an fp32 output with a flag feeds a split conv)
+        if constexpr (!std::is_same<TO, bf16_t>::value) raise_range_flag(range_flag, bad);
     }
     __syncthreads();
     const int bo = img / nv, v = img - bo * nv;

@@ -990,10 +990,13 @@ int gemm_ex_launch(const cmt_gemm_ex_args* ap, void* stream, bool x3) {
 extern "C" int cmt_gemm_f32_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, false); }
 extern "C" int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* ap, void* stream) { return gemm_ex_launch(ap, stream, true); }
 
-extern "C" int cmt_linear_bwd_bf16x3(const float* dY, const float* X, const float* W, float* dX, float* dW, float* dB,
-                                     int M, int K, int N, int64_t ldx, int ksplit, void* stream) {
+extern "C" int cmt_linear_bwd_bf16x3_ex(const float* dY, const float* X, const float* W, float* dX, float* dW,
+                                        float* dB, int M, int K, int N, int64_t ldx, int ksplit, int flags,
+                                        void* stream) {
     CMT_REQUIRE(dY && X && W && M > 0 && K > 0 && N > 0 && ldx >= K, "cmt_linear_bwd_bf16x3: bad arguments");
     CMT_REQUIRE(dB == nullptr || dW != nullptr, "cmt_linear_bwd_bf16x3: dB comes with dW");
+    CMT_REQUIRE((flags & ~CMT_LINEAR_BWD_ACCUMULATE) == 0, "cmt_linear_bwd_bf16x3: unknown flags");
+    const bool acc = (flags & CMT_LINEAR_BWD_ACCUMULATE) != 0;
     hipStream_t s = (hipStream_t)stream;
     if (dX) {
         cmt_gemm_ex_args a{};
@@ -1008,18 +1011,26 @@ extern "C" int cmt_linear_bwd_bf16x3(const float* dY, const float* X, const floa
         cmt_gemm_ex_args a{};
         a.M = N; a.N = K; a.K = M; a.batch = 1; a.alpha = 1.f;
         a.ksplit = ksplit < 1 ? 1 : ksplit;
-        a.beta = a.ksplit > 1 ? 1.f : 0.f;
+        // accumulate (ABI 24): dW / dB already hold a sum to add to (a parameter's .grad): C read and
+        // rewritten (unsplit) or f32 atomics (split), the row sums atomic -- no zero fill
+        a.beta = acc || a.ksplit > 1 ? 1.f : 0.f;
         a.A = dY; a.a_sm = 1; a.a_sk = N;
         a.B = X; a.b_sn = 1; a.b_sk = ldx;
         a.C = dW; a.ldc = K;
         a.a_rowsum = dB;
-        if (a.ksplit > 1) CMT_REQUIRE(hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s) == hipSuccess,
-                                      "cmt_linear_bwd_bf16x3: memset");
-        if (dB) CMT_REQUIRE(hipMemsetAsync(dB, 0, (size_t)N * sizeof(float), s) == hipSuccess,
-                            "cmt_linear_bwd_bf16x3: memset");
+        if (!acc && a.ksplit > 1)
+            CMT_REQUIRE(hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s) == hipSuccess,
+                        "cmt_linear_bwd_bf16x3: memset");
+        if (!acc && dB) CMT_REQUIRE(hipMemsetAsync(dB, 0, (size_t)N * sizeof(float), s) == hipSuccess,
+                                    "cmt_linear_bwd_bf16x3: memset");
         return gemm_ex_launch(&a, stream, true);
     }
     return 0;
+}
+
+extern "C" int cmt_linear_bwd_bf16x3(const float* dY, const float* X, const float* W, float* dX, float* dW, float* dB,
+                                     int M, int K, int N, int64_t ldx, int ksplit, void* stream) {
+    return cmt_linear_bwd_bf16x3_ex(dY, X, W, dX, dW, dB, M, K, N, ldx, ksplit, 0, stream);
 }
 
 // shared_conv's weight gradient as the bf16x3 GEMM dW[cout][n] = sum_r dY[r][cout] im2col(X)[r][n]

@@ -87,7 +87,8 @@ def dn_mask_params(mask):
     return pad, single
 
 
-def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cross_fp16=True, seed=0, seed_dev=None):
+def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cross_fp16=True, seed=0, seed_dev=None,
+                kv=None, li=0):
     """One PETRTransformerDecoderLayer in training (petr_transformer.py:374-487,
     mmcv BaseTransformerLayer post-norm walk) on the differentiable native ops:
     rows batch-first [B, N, C]; memk = memory + key_pos.  The self-attention
@@ -96,7 +97,9 @@ def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cros
     kwarg sets both, 0.1 in every config); the cross core emulates flash-attn's
     fp16 inputs when cross_fp16.  memk / mem may be lists, one [B, Nk_a, C] pair
     per agent whose queries are the consecutive B-row blocks of tgt / qpos: the
-    query-side products run once for all agents, the cross-attention per agent."""
+    query-side products run once for all agents, the cross-attention per agent.  kv: per agent
+    the (holder, token) of train_ops.kv_all -- every layer's K / V projected up front -- and li
+    this layer's index in them (then memk / mem are not read here)."""
     from . import train_ops as ops
     sa, ca, ffn, nm = lay.attentions[0], lay.attentions[1], lay.ffns[0], lay.norms
     H = sa.num_heads
@@ -115,7 +118,11 @@ def train_layer(lay, tgt, qpos, memk, mem, *, pad=0, group=0, dropout=True, cros
     wq, wk, wv = w.in_proj_weight.chunk(3)
     bq, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
     qx = ops.linear(tgt + qpos, wq, bq)
-    if isinstance(mem, (list, tuple)):
+    if kv is not None:
+        qxs = qx.split(qx.shape[0] // len(kv), 0) if len(kv) > 1 else (qx,)
+        o = [ops.cross_attention(qxs[i], tok, hol, li, H, fp16=cross_fp16) for i, (hol, tok) in enumerate(kv)]
+        o = torch.cat(o, 0) if len(o) > 1 else o[0]
+    elif isinstance(mem, (list, tuple)):
         # split, not slicing: its backward is one cat where each slice's is a zero fill + copy + add
         qxs = qx.split(qx.shape[0] // len(mem), 0)
         o = torch.cat([ops.attention(qxs[i], ops.linear(mk, wk, bk), ops.linear(m, wv, bv), H,
@@ -474,6 +481,16 @@ class PETRTransformerDecoder(nn.Module):
         lists (one per agent, train_layer): every agent's decoder in one walk."""
         from . import train_ops as ops
         memk = [m + p for m, p in zip(mem, pos)] if isinstance(mem, (list, tuple)) else mem + pos
+        # every layer's cross-attention K / V of each agent in two Linears of width L C (train_ops.kv_all)
+        C = self.embed_dims
+        lkv = []
+        for lay in self.layers:
+            w = lay.attentions[1].attn
+            _, wk, wv = w.in_proj_weight.chunk(3)
+            _, bk, bv = w.in_proj_bias.chunk(3) if w.in_proj_bias is not None else (None, None, None)
+            lkv.append((wk, bk, wv, bv))
+        agents = list(zip(memk, mem)) if isinstance(mem, (list, tuple)) else [(memk, mem)]
+        kv = [ops.kv_all(mk, m, lkv) for mk, m in agents]
         outs = []
         if seed_dev is not None:
             seed0 = 0
@@ -481,7 +498,7 @@ class PETRTransformerDecoder(nn.Module):
             seed0 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
         for li, lay in enumerate(self.layers):
             tgt = train_layer(lay, tgt, qpos, memk, mem, pad=pad, group=group, dropout=dropout,
-                              cross_fp16=cross_fp16, seed=seed0 + li, seed_dev=seed_dev)
+                              cross_fp16=cross_fp16, seed=seed0 + li, seed_dev=seed_dev, kv=kv, li=li)
             outs.append(ops.layer_norm(tgt, self.post_norm.weight, self.post_norm.bias, self.post_norm.eps))
         return torch.nan_to_num(torch.stack(outs))
 

@@ -16,6 +16,7 @@ Reference semantics (training step of CmtHead / CmtHeadCoop):
                   gradient = the same implicit conv on the flipped weights
   nchw_rows       the memory-row layout of the feature maps (gradient back to NCHW)
 """
+import contextlib
 import math
 
 import torch
@@ -24,7 +25,59 @@ from ... import native
 from ... import native_train as T
 from ...runtime import SPLIT
 
-__all__ = ["linear", "linear_batched", "taps3", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss"]
+__all__ = ["linear", "linear_batched", "taps3", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss",
+           "direct_param_grads", "kv_all", "cross_attention"]
+
+
+# ---- parameter gradients written in place (ABI 24).  Inside direct_param_grads() the backward of
+# a Linear / LayerNorm whose weight (and bias) is a leaf parameter -- or a contiguous view of one,
+# like the chunks of nn.MultiheadAttention's packed in_proj -- adds its weight / bias gradient
+# straight into that parameter's .grad (allocated zeroed on first use, as autograd would) and
+# returns None for it: no gradient temporary, no zero fill of a split-K reduction, no
+# AccumulateGrad add per parameter and use.  Only the Trainer's backward() turns it on, and only
+# where nothing hooks the accumulation (world size 1: the bucketed all-reduce counts
+# post-accumulate-grad hooks) and no graph is being captured; .grad then holds exactly what
+# autograd would have accumulated (tests/test_gpu_train_head.py::test_direct_param_grads_match).
+# A process-wide switch, not a thread-local one: autograd runs a GPU backward on its own device
+# thread.  ``writes`` counts the gradients added in place (tests check the path ran).
+class _DirectState:
+    on = False
+    writes = 0
+
+
+_direct = _DirectState()
+
+
+@contextlib.contextmanager
+def direct_param_grads(enabled=True):
+    prev = _direct.on
+    _direct.on = bool(enabled)
+    try:
+        yield
+    finally:
+        _direct.on = prev
+
+
+def _grad_target(t):
+    """The tensor t's gradient should be added to in place (a view of its parameter's .grad), or
+    None when t's gradient must go back through autograd."""
+    if t is None or not _direct.on or not t.requires_grad:
+        return None
+    p = t if t.is_leaf else t._base
+    if p is None or not p.is_leaf or not t.is_contiguous() or getattr(p, "_post_accumulate_grad_hooks", None):
+        return None
+    if not t.is_leaf and (t._base._base is not None or t.grad_fn is None):
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    g = p.grad
+    if not g.is_contiguous() or g.dtype != t.dtype:
+        return None
+    _direct.writes += 1
+    if t is p:
+        return g
+    # t is a contiguous view of the contiguous parameter p: the same elements of its .grad
+    return g.reshape(-1)[t.storage_offset() - p.storage_offset():][:t.numel()].view(t.shape)
 
 
 class _Linear(torch.autograd.Function):
@@ -32,13 +85,25 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        ctx.wb = (w, b)
         return T.linear_fwd(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        need_db = ctx.has_b and ctx.needs_input_grad[2]
+        gw = gb = None
+        if ctx.needs_input_grad[1]:
+            gw = _grad_target(ctx.wb[0])
+            gb = _grad_target(ctx.wb[1]) if need_db else None
+            if gw is None or (need_db and gb is None):
+                gw = gb = None
+        if gw is not None:
+            dx, _, _ = T.linear_bwd(dy, x, w, need_dx=ctx.needs_input_grad[0], need_dw=True, need_db=need_db,
+                                    dw_into=gw, db_into=gb)
+            return dx, None, None
         dx, dw, db = T.linear_bwd(dy, x, w, need_dx=ctx.needs_input_grad[0], need_dw=ctx.needs_input_grad[1],
-                                  need_db=ctx.has_b and ctx.needs_input_grad[2])
+                                  need_db=need_db)
         return dx, dw, db
 
 
@@ -97,6 +162,124 @@ class _Attention(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None, None, None
 
 
+class KVAll:
+    """One agent's cross-attention keys / values of EVERY decoder layer (kv_all) and the arena
+    their gradients are written into by the layers' attention backward (cross_attention)."""
+
+    def __init__(self):
+        self.K = self.V = self.dK = self.dV = None
+        self.written = set()
+
+
+class _KVAll(torch.autograd.Function):
+    """K_l = (mem + pos) Wk_l^T + bk_l and V_l = mem Wv_l^T + bv_l of all L layers as TWO Linears of
+    width L C (FlashMHA's packed in_proj, attention.py:21-27, per layer): [B, Nk, L C] each, layer l
+    in columns [l C, (l + 1) C).  Its output is a 0-dim token the layers' cross_attention calls
+    take as input; their backward writes dK_l / dV_l straight into the holder's arena (strided,
+    no per-layer gradient tensor, no accumulation), and this backward runs the two Linears'
+    backward once: d(mem + pos) = dK Wk (reduction over L C), dW = dK^T (mem + pos) -- instead
+    of 2 L projection GEMMs each way, L per-layer weight-gradient GEMMs of a 256 x 256 output
+    split over the ~40 k key rows, and 2 L - 2 [Nk, C] gradient additions."""
+
+    @staticmethod
+    def forward(ctx, memk, mem, holder, nl, *wb):
+        B, Nk, C = memk.shape
+        wk, bk, wv, bv = wb[:nl], wb[nl:2 * nl], wb[2 * nl:3 * nl], wb[3 * nl:]
+        ctx.has_b = bk[0] is not None
+        Wk, Wv = torch.cat(wk, 0), torch.cat(wv, 0)
+        bkc = torch.cat(bk, 0) if ctx.has_b else None
+        bvc = torch.cat(bv, 0) if ctx.has_b else None
+        xk, xv = memk.reshape(B * Nk, C), mem.reshape(B * Nk, C)
+        holder.K = T.linear_fwd(xk, Wk, bkc).view(B, Nk, nl * C)
+        holder.V = T.linear_fwd(xv, Wv, bvc).view(B, Nk, nl * C)
+        holder.dK = holder.dV = None
+        holder.written = set()
+        ctx.save_for_backward(xk, xv, Wk, Wv)
+        ctx.holder, ctx.nl, ctx.shape = holder, nl, (B, Nk, C)
+        ctx.set_materialize_grads(False)
+        return memk.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _token_grad):
+        xk, xv, Wk, Wv = ctx.saved_tensors
+        h, nl, (B, Nk, C) = ctx.holder, ctx.nl, ctx.shape
+        if h.dK is None:
+            return (None,) * (4 + 4 * nl)
+        for l in set(range(nl)) - h.written:      # a layer whose attention got no gradient
+            h.dK[..., l * C:(l + 1) * C].zero_()
+            h.dV[..., l * C:(l + 1) * C].zero_()
+        gin = ctx.needs_input_grad
+        outs = []
+        for x, W, d, need_x, off in ((xk, Wk, h.dK, gin[0], 4), (xv, Wv, h.dV, gin[1], 4 + 2 * nl)):
+            need_w = any(gin[off:off + nl])
+            need_b = ctx.has_b and any(gin[off + nl:off + 2 * nl])
+            dx, dw, db = T.linear_bwd(d.view(B * Nk, nl * C), x, W, need_dx=need_x, need_dw=need_w or need_b,
+                                      need_db=need_b)
+            dws = list(dw.split(C, 0)) if need_w else [None] * nl
+            dbs = list(db.split(C, 0)) if need_b else [None] * nl
+            outs.append((None if dx is None else dx.view(B, Nk, C), dws, dbs))
+        h.K = h.V = h.dK = h.dV = None            # the step's K / V and their gradients are done
+        (dmk, dwk, dbk), (dm, dwv, dbv) = outs
+        return (dmk, dm, None, None, *dwk, *dbk, *dwv, *dbv)
+
+
+def kv_all(memk, mem, layers_kv):
+    """layers_kv: per layer (wk, bk, wv, bv) -- the K / V chunks of its packed in_proj.  Returns
+    (holder, token) for cross_attention."""
+    holder = KVAll()
+    nl = len(layers_kv)
+    wb = [t[0] for t in layers_kv] + [t[1] for t in layers_kv] + [t[2] for t in layers_kv] + \
+         [t[3] for t in layers_kv]
+    token = _KVAll.apply(memk.contiguous(), mem.contiguous(), holder, nl, *[w.contiguous() if w is not None else None
+                                                                           for w in wb])
+    return holder, token
+
+
+_ZERO_TOKEN = {}
+
+
+class _CrossAttn(torch.autograd.Function):
+    """The cross-attention core of layer l on the all-layer K / V of kv_all (columns [l C, (l+1) C),
+    strided rows: no copy); its backward writes dK_l / dV_l into the holder's arena."""
+
+    @staticmethod
+    def forward(ctx, q, token, holder, l, H, scale, fp16):
+        B, Nq, C = q.shape
+        K, V = holder.K[..., l * C:(l + 1) * C], holder.V[..., l * C:(l + 1) * C]
+        Nk, ld = K.shape[1], K.stride(1)
+        o = torch.empty_like(q)
+        lse = torch.empty((B * H * Nq,), dtype=torch.float32, device=q.device)
+        kw = dict(B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * C, 32, C), k_strides=(K.stride(0), 32, ld),
+                  v_strides=(V.stride(0), 32, V.stride(1)), o_strides=(Nq * C, 32, C), scale=scale, dn_pad=0,
+                  dn_group=0, fp16_inputs=fp16, dropout_p=0.0, seed=0, seed_dev=None)
+        T.attn_train_fwd(q, K, V, o, lse, **kw)
+        ctx.kw, ctx.holder, ctx.l = kw, holder, l
+        ctx.save_for_backward(q, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, o, lse = ctx.saved_tensors
+        h, l = ctx.holder, ctx.l
+        C = q.shape[2]
+        if h.dK is None:
+            h.dK, h.dV = torch.empty_like(h.K), torch.empty_like(h.V)
+        K, V = h.K[..., l * C:(l + 1) * C], h.V[..., l * C:(l + 1) * C]
+        dK, dV = h.dK[..., l * C:(l + 1) * C], h.dV[..., l * C:(l + 1) * C]
+        dq = torch.empty_like(q)
+        T.attn_train_bwd(q, K, V, o, lse, do.contiguous(), dq, dK, dV, **ctx.kw)
+        h.written.add(l)
+        z = _ZERO_TOKEN.get(q.device)
+        if z is None:
+            z = _ZERO_TOKEN[q.device] = torch.zeros((), dtype=torch.float32, device=q.device)
+        return dq, z, None, None, None, None, None
+
+
+def cross_attention(q, token, holder, l, num_heads, *, fp16=True):
+    return _CrossAttn.apply(q.contiguous(), token, holder, l, num_heads, 1.0 / math.sqrt(q.shape[-1] // num_heads),
+                            fp16)
+
+
 def attention(q, k, v, num_heads, *, dn_pad=0, dn_group=0, fp16=False, dropout_p=0.0, seed=0, seed_dev=None):
     """seed_dev: optional int32 device tensor [1] added to seed on the device (graph-replayed steps)"""
     return _Attention.apply(q.contiguous(), k.contiguous(), v.contiguous(), num_heads,
@@ -136,11 +319,18 @@ class _LayerNorm(torch.autograd.Function):
         y, mean, rstd = T.ln_train_fwd(x, w, b, eps=eps, rows_per_wset=rows_per_wset)
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.eps, ctx.rpw, ctx.wsets = eps, rows_per_wset, wsets
+        ctx.wb = (w, b)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, mean, rstd = ctx.saved_tensors
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            gw, gb = _grad_target(ctx.wb[0]), _grad_target(ctx.wb[1])
+            if gw is not None and gb is not None:
+                dx, _, _ = T.ln_train_bwd(dy, x, w, mean, rstd, eps=ctx.eps, rows_per_wset=ctx.rpw, wsets=ctx.wsets,
+                                          dw_into=gw, db_into=gb)
+                return dx, None, None, None, None, None
         dx, dw, db = T.ln_train_bwd(dy, x, w, mean, rstd, eps=ctx.eps, rows_per_wset=ctx.rpw, wsets=ctx.wsets)
         return dx, dw.view(w.shape), db.view(w.shape), None, None, None
 

@@ -28,8 +28,9 @@ A_ROWS, A_CONV3X3, A_CONV1D3, A_CONV3X3_NCHW = 0, 1, 2, 3
 C_ROWS, C_HEADSPLIT = 0, 1
 A2_ADD, A2_SELECT = 0, 1
 ATTN_KEEP_PARTIALS = 2048   # cmt_hip.h CMT_ATTN_KEEP_PARTIALS (ABI 19)
+LINEAR_BWD_ACCUMULATE = 1   # cmt_hip.h CMT_LINEAR_BWD_ACCUMULATE (ABI 24)
 CHAIN_XSPLITS = 8           # the split count chain B1 combines (cmt_chain_args.xsplits)
-ABI_VERSION = 23
+ABI_VERSION = 24
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -212,6 +213,7 @@ def _load():
         "cmt_gemm_f32_ex": ([P(GemmExArgs), _vp], _int),
         "cmt_gemm_bf16x3_ex": ([P(GemmExArgs), _vp], _int),
         "cmt_linear_bwd_bf16x3": ([_vp, _vp, _vp, _vp, _vp, _vp, _int, _int, _int, _i64, _int, _vp], _int),
+        "cmt_linear_bwd_bf16x3_ex": ([_vp, _vp, _vp, _vp, _vp, _vp, _int, _int, _int, _i64, _int, _int, _vp], _int),
         "cmt_attn_train_workspace_bytes": ([P(AttnTrainArgs)], _i64),
         "cmt_attn_train_fwd": ([P(AttnTrainArgs), _vp], _int),
         "cmt_attn_train_bwd": ([P(AttnTrainArgs), _vp], _int),

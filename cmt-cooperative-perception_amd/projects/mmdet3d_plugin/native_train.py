@@ -85,12 +85,37 @@ def linear_fwd(X, W, b=None):
     return Y
 
 
-def linear_bwd(dY, X, W, need_dx=True, need_dw=True, need_db=True):
-    """(dX, dW, dB) of Y = X W^T + b."""
+def linear_bwd(dY, X, W, need_dx=True, need_dw=True, need_db=True, dw_into=None, db_into=None):
+    """(dX, dW, dB) of Y = X W^T + b.  dw_into / db_into (a parameter's .grad, or a view of it):
+    the weight / bias gradient is ADDED there (ABI 24: no zero fill, no temporary) and returned
+    as None."""
     M, K = X.shape
     Nn = W.shape[0]
     dY = dY.contiguous()
     dX = dW = dB = None
+    if dw_into is not None or db_into is not None:
+        if not need_dw or dw_into is None or (need_db and db_into is None):
+            raise ValueError("linear_bwd: accumulate the weight gradient, and the bias one with it")
+        _f32(dY, X, W, dw_into, db_into)
+        if X.stride(1) != 1 or not W.is_contiguous() or not dw_into.is_contiguous() or \
+                dw_into.shape != W.shape or (db_into is not None and not db_into.is_contiguous()):
+            raise RuntimeError("linear_bwd: contiguous X rows, W and gradient targets of W's shape")
+        if need_dx:
+            dX = torch.empty((M, K), dtype=torch.float32, device=X.device)
+        if _gemm_mode == "bf16x3":
+            N._check(N.lib().cmt_linear_bwd_bf16x3_ex(dY.data_ptr(), X.data_ptr(), W.data_ptr(), _ptr(dX),
+                                                       dw_into.data_ptr(), _ptr(db_into if need_db else None), M, K,
+                                                       Nn, X.stride(0), _ksplit(M, Nn, K),
+                                                       N.LINEAR_BWD_ACCUMULATE, N._stream()),
+                     "cmt_linear_bwd_bf16x3_ex")
+        else:
+            if need_dx:
+                gemm_ex(dY, (Nn, 1), W, (1, W.stride(0)), dX, M=M, N_=K, K=Nn, ldc=K)
+            gemm_ex(dY, (1, Nn), X, (1, X.stride(0)), dw_into, M=Nn, N_=K, K=M, ldc=K, beta=1.0,
+                    ksplit=_ksplit(M, Nn, K))
+            if need_db:
+                db_into.add_(dY.sum(0))
+        return dX, None, None
     if _gemm_mode == "bf16x3" and (need_dx or need_dw):
         # one native call: both GEMMs, the split-K / bias-gradient zeroing on the stream (ABI 23)
         _f32(dY, X, W)
@@ -226,11 +251,25 @@ def ln_train_fwd(X, W, Bv, *, eps, rows_per_wset=0):
     return Y, mean, rstd
 
 
-def ln_train_bwd(dY, X, W, mean, rstd, *, eps, rows_per_wset=0, wsets=1):
+def ln_train_bwd(dY, X, W, mean, rstd, *, eps, rows_per_wset=0, wsets=1, dw_into=None, db_into=None):
+    """(dX, dW, dB); dw_into / db_into (both or neither: the parameters' .grad): the weight and
+    bias gradients are added there (the kernel's per-column sums are atomic adds) and returned
+    as None."""
     _f32(dY, X, W, mean, rstd)
     rows, C = X.shape
     dY = dY.contiguous()
     dX = torch.empty((rows, C), dtype=torch.float32, device=X.device)
+    if dw_into is not None or db_into is not None:
+        _f32(dw_into, db_into)
+        if dw_into is None or db_into is None or dw_into.numel() != wsets * C or db_into.numel() != wsets * C or \
+                not (dw_into.is_contiguous() and db_into.is_contiguous()):
+            raise ValueError("ln_train_bwd: contiguous weight and bias gradient targets")
+        a = _ln_args(X, W, W, C=C, eps=eps, rows_per_wset=rows_per_wset)
+        a.ldy, a.mean, a.rstd = C, mean.data_ptr(), rstd.data_ptr()
+        a.dY, a.dX, a.lddx, a.accumulate = dY.data_ptr(), dX.data_ptr(), C, 0
+        a.dW, a.dB = dw_into.data_ptr(), db_into.data_ptr()
+        N._check(N.lib().cmt_ln_train_bwd(ctypes.byref(a), N._stream()), "cmt_ln_train_bwd")
+        return dX, None, None
     dWB = torch.zeros((2, wsets, C), dtype=torch.float32, device=X.device)   # one fill for both sums
     dW, dB = dWB[0], dWB[1]
     a = _ln_args(X, W, W, C=C, eps=eps, rows_per_wset=rows_per_wset)

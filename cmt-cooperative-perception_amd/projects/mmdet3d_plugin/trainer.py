@@ -22,6 +22,8 @@ import torch
 import torch.distributed as dist
 
 from . import native_train as T
+from .models.utils.train_ops import direct_param_grads
+from .runtime import OPTIONS
 
 __all__ = ["FlatParams", "Trainer", "PeerBackwardError", "allreduce_buckets"]
 
@@ -271,8 +273,12 @@ class Trainer:
         if self.buckets is not None:
             self.buckets.drain()   # outstanding all-reduces write fp.grad: finish them before zeroing it
         self.fp.zero_grad()
+        # world size 1 (no accumulation hooks), no graph capture: the native backward adds each
+        # Linear / LayerNorm weight gradient straight into the flat gradient buffer (train_ops)
+        direct = self.buckets is None and not OPTIONS.train_graph
         try:
-            total.backward()
+            with direct_param_grads(direct):
+                total.backward()
         except BaseException:
             if self.buckets is not None and not self.buckets.abort():
                 # every gradient was already exchanged: the other ranks apply this step and this

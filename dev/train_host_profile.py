@@ -6,7 +6,6 @@ import os
 import pstats
 import sys
 import time
-import types
 
 import torch
 
@@ -49,13 +48,12 @@ def fake_timed(step, steps, warmup, env, sync, device):
 
 def main():
     bench.dp.timed_frames = fake_timed
-    args = types.SimpleNamespace(workload="coop", steps=10, warmup=4)
     env = bench.dp.dp_env()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     bench.native.lib()
     bench.set_precision(bench.WORKLOADS["coop"]["precision"])
-    bench.train_bench(args, env, dev)
+    bench.train_bench("coop", 10, 4, env, dev)
 
 
 if __name__ == "__main__":

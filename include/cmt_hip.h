@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 23
+#define CMT_ABI_VERSION 24
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -559,6 +559,14 @@ int cmt_gemm_bf16x3_ex(const cmt_gemm_ex_args* args, void* stream);
  * GEMM launches and the zero fill a caller of cmt_gemm_bf16x3_ex issues. */
 int cmt_linear_bwd_bf16x3(const float* dY, const float* X, const float* W, float* dX, float* dW, float* dB,
                           int M, int K, int N, int64_t ldx, int ksplit, void* stream);
+/* cmt_linear_bwd_bf16x3_ex (ABI 24): the same with flags.  CMT_LINEAR_BWD_ACCUMULATE: dW and dB
+ * already hold a sum (a parameter's gradient) and the call ADDS to it -- no zero fill, the weight
+ * gradient read-modify-written (unsplit) or f32-atomically added (split), the bias gradient added
+ * atomically: the training step writes each Linear's weight gradient straight into the
+ * parameter's .grad instead of returning it for autograd to add. */
+#define CMT_LINEAR_BWD_ACCUMULATE 1
+int cmt_linear_bwd_bf16x3_ex(const float* dY, const float* X, const float* W, float* dX, float* dW, float* dB,
+                             int M, int K, int N, int64_t ldx, int ksplit, int flags, void* stream);
 
 /* Attention forward with row statistics, and its backward (attn_train.hip),
  * exact f32, head_dim 32.  Replaces, in the training step, the fp32
