@@ -46,9 +46,47 @@ struct AP {                  // device-side copy of cmt_attn_train_args + derive
 
 __device__ __forceinline__ float r16(float x) { return (float)(_Float16)x; }
 
+// dev diagnostic bits (dev/build_exp.sh -DCMT_AT_VAR=n; the product builds 0): 2 / 4 = no dropout
+// hash / no DN mask (wrong results, for timing what each costs: dev/attn_train_probe.py)
+#ifndef CMT_AT_VAR
+#define CMT_AT_VAR 0
+#endif
+// exp2 as one v_exp_f32 (exp2f adds denormal range scaling around it): the exact-f32 kernels'
+// softmax arguments are <= 0 and a flushed denormal P is below every tolerance of the step
+// (profiles/r6_experiments.txt r6f: 70.8 -> 66.7 us forward at the coop self-attention shape)
+__device__ __forceinline__ float xexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ bool masked(const cmt_attn_train_args& a, int q, int k) {
     if (a.dn_pad <= 0 || k >= a.dn_pad) return false;
     return q >= a.dn_pad || (k / a.dn_group) != (q / a.dn_group);
+}
+
+// masked() without a per-element integer division: the DN groups tile [0, dn_pad) (dn_pad is a
+// multiple of dn_group), so for a FIXED query q the keys it sees below dn_pad are its own group
+// [lo, hi) (none when q >= dn_pad), and for a FIXED key k < dn_pad the queries that see it are
+// k's group.  One division per lane; per element two or three compares.
+struct DnRange {
+    int lo, hi;
+};
+// the lane's query q: key k is hidden iff dn_hidden_key(a, r, k)
+__device__ __forceinline__ DnRange dn_query_range(const cmt_attn_train_args& a, int q) {
+    if (a.dn_pad <= 0 || q >= a.dn_pad) return DnRange{0, 0};
+    const int lo = (q / a.dn_group) * a.dn_group;
+    return DnRange{lo, min(lo + a.dn_group, a.dn_pad)};
+}
+__device__ __forceinline__ bool dn_hidden_key(const cmt_attn_train_args& a, const DnRange& r, int k) {
+    if constexpr ((CMT_AT_VAR & 4) != 0) return false;
+    return k < a.dn_pad && (k < r.lo || k >= r.hi);
+}
+// the lane's key k: query q is hidden from it iff dn_hidden_query(r, q)
+__device__ __forceinline__ DnRange dn_key_range(const cmt_attn_train_args& a, int k) {
+    if (a.dn_pad <= 0 || k >= a.dn_pad) return DnRange{INT_MIN, INT_MAX};
+    const int lo = (k / a.dn_group) * a.dn_group;
+    return DnRange{lo, min(lo + a.dn_group, a.dn_pad)};
+}
+__device__ __forceinline__ bool dn_hidden_query(const DnRange& r, int q) {
+    if constexpr ((CMT_AT_VAR & 4) != 0) return false;
+    return q < r.lo || q >= r.hi;
 }
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -60,6 +98,7 @@ __device__ __forceinline__ void resolve_seed(AP& p) {
     if (p.a.seed_dev) p.a.seed += *p.a.seed_dev;
 }
 __device__ __forceinline__ bool keep(const AP& p, int bh, int q, int k) {
+    if constexpr ((CMT_AT_VAR & 2) != 0) return true;
     uint32_t h = mix32(p.a.seed ^ mix32((uint32_t)bh * 0x9e3779b9U + (uint32_t)q));
     h = mix32(h ^ (uint32_t)k * 0x85ebca6bU);
     return h >= p.drop_thr;
@@ -115,6 +154,7 @@ __global__ __launch_bounds__(256) void train_fwd_kernel(AP p) {
     const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
     const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
     const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const DnRange dnr = dn_query_range(a, q);
     const int qc = min(q, a.Nq - 1);
     f32x4 qf[4];
 #pragma unroll
@@ -144,7 +184,7 @@ __global__ __launch_bounds__(256) void train_fwd_kernel(AP p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = t * KT + kb * 32 + key_of(r, lh);
-                s[kb][r] = (k >= a.Nk || masked(a, q, k)) ? -__builtin_inff() : s[kb][r] * p.c;
+                s[kb][r] = (k >= a.Nk || dn_hidden_key(a, dnr, k)) ? -__builtin_inff() : s[kb][r] * p.c;
             }
         }
         float mt = -__builtin_inff();
@@ -155,13 +195,13 @@ __global__ __launch_bounds__(256) void train_fwd_kernel(AP p) {
         mt = fmaxf(mt, __shfl_xor(mt, 32));
         const float m_new = fmaxf(m_run, mt);
         const float m_use = m_new == -__builtin_inff() ? 0.f : m_new;   // fully masked so far
-        const float alpha = exp2f(m_run - m_use);
+        const float alpha = xexp2(m_run - m_use);
         float ls = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float e = exp2f(s[kb][r] - m_use);
+                const float e = xexp2(s[kb][r] - m_use);
                 ls += e;
                 float pe = f16 ? r16(e) : e;
                 if (a.dropout_p > 0.f) {
@@ -220,7 +260,7 @@ __global__ __launch_bounds__(256) void train_combine_kernel(AP p) {
     for (int s = 0; s < S; ++s) {
         const float l = ws[(int64_t)S * rows * (D + 1) + s * rows + row];
         if (!(l > 0.f)) continue;
-        const float w = exp2f(ws[(int64_t)S * rows * D + s * rows + row] - M);
+        const float w = xexp2(ws[(int64_t)S * rows * D + s * rows + row] - M);
         num += w * ws[(s * rows + row) * D + d];
         den += w * l;
     }
@@ -260,6 +300,7 @@ __global__ __launch_bounds__(256) void train_dq_kernel(AP p) {
     const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
     const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
     const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const DnRange dnr = dn_query_range(a, q);
     const int qc = min(q, a.Nq - 1);
     f32x4 qf[4], df[4];
 #pragma unroll
@@ -292,7 +333,7 @@ __global__ __launch_bounds__(256) void train_dq_kernel(AP p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = t * KT + kb * 32 + key_of(r, lh);
-                float pr = (k >= a.Nk || masked(a, q, k)) ? 0.f : exp2f(s[r] * p.c - lse);
+                float pr = (k >= a.Nk || dn_hidden_key(a, dnr, k)) ? 0.f : xexp2(s[r] * p.c - lse);
                 float g = dp[r];
                 if (a.dropout_p > 0.f) g = keep(p, bh, q, k) ? g * p.keep_scale : 0.f;
                 s[r] = pr * (g - dl);                                    // dS^T
@@ -327,6 +368,7 @@ __global__ __launch_bounds__(256) void train_dkv_kernel(AP p, int qt_per) {
     const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
     const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
     const int k = blockIdx.x * 128 + wave * 32 + lr;
+    const DnRange dnr = dn_key_range(a, k);
     const int kc = min(k, a.Nk - 1);
     f32x4 kf[4], vf[4];
 #pragma unroll
@@ -363,8 +405,8 @@ __global__ __launch_bounds__(256) void train_dkv_kernel(AP p, int qt_per) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int qi = qb * 32 + key_of(r, lh), qq = t * KT + qi;
-                const bool valid = qq < a.Nq && k < a.Nk && !masked(a, qq, k);
-                const float pr = valid ? exp2f(s[r] * p.c - Ls[qi]) : 0.f;
+                const bool valid = qq < a.Nq && k < a.Nk && !dn_hidden_query(dnr, qq);
+                const float pr = valid ? xexp2(s[r] * p.c - Ls[qi]) : 0.f;
                 float g = dp[r], pe = f16 ? r16(pr) : pr;
                 if (a.dropout_p > 0.f) {
                     const bool kp = keep(p, bh, qq, k);
@@ -485,6 +527,7 @@ __global__ __launch_bounds__(256) void train16_fwd_kernel(AP p) {
     const float* Kb = a.K + (int64_t)b * a.k_bs + (int64_t)h * a.k_hs;
     const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
     const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const DnRange dnr = dn_query_range(a, q);
     const int qc = min(q, a.Nq - 1);
     h8_t qf[2];
     own_row16(Qb + (int64_t)qc * a.q_rs, lh, qf);
@@ -510,7 +553,7 @@ __global__ __launch_bounds__(256) void train16_fwd_kernel(AP p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = t * KT + kb * 32 + key_of(r, lh);
-                const bool hide = (edge && k >= a.Nk) || (MASK && masked(a, q, k));
+                const bool hide = (edge && k >= a.Nk) || (MASK && dn_hidden_key(a, dnr, k));
                 s[kb][r] = hide ? -__builtin_inff() : s[kb][r] * p.c;
             }
         }
@@ -586,6 +629,7 @@ __global__ __launch_bounds__(256) void train16_dq_kernel(AP p) {
     const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
     const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
     const int q = blockIdx.x * 128 + wave * 32 + lr;
+    const DnRange dnr = dn_query_range(a, q);
     const int qc = min(q, a.Nq - 1);
     h8_t qf[2], df[2];
     own_row16(Qb + (int64_t)qc * a.q_rs, lh, qf);
@@ -616,7 +660,7 @@ __global__ __launch_bounds__(256) void train16_dq_kernel(AP p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = t * KT + kb * 32 + key_of(r, lh);
-                const bool hide = (edge && k >= a.Nk) || (MASK && masked(a, q, k));
+                const bool hide = (edge && k >= a.Nk) || (MASK && dn_hidden_key(a, dnr, k));
                 const float pr = hide ? 0.f : exp2f(s[r] * p.c - lse);
                 float g = dp[r];
                 if (DROP) g = keep(p, bh, q, k) ? g * p.keep_scale : 0.f;
@@ -652,6 +696,7 @@ __global__ __launch_bounds__(256) void train16_dkv_kernel(AP p) {
     const float* Vb = a.V + (int64_t)b * a.v_bs + (int64_t)h * a.v_hs;
     const float* dOb = a.dO + (int64_t)b * a.o_bs + (int64_t)h * a.o_hs;
     const int k = blockIdx.x * 128 + wave * 32 + lr;
+    const DnRange dnr = dn_key_range(a, k);
     const int kc = min(k, a.Nk - 1);
     h8_t kf[2], vf[2];
     own_row16(Kb + (int64_t)kc * a.k_rs, lh, kf);
@@ -684,7 +729,7 @@ __global__ __launch_bounds__(256) void train16_dkv_kernel(AP p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int qi = qb * 32 + key_of(r, lh), qq = t * KT + qi;
-                const bool valid = qq < a.Nq && k < a.Nk && !(MASK && masked(a, qq, k));
+                const bool valid = qq < a.Nq && k < a.Nk && !(MASK && dn_hidden_query(dnr, qq));
                 const float pr = valid ? exp2f(s[r] * p.c - Ls[qi]) : 0.f;
                 float g = dp[r], pe = pr;
                 if (DROP) {
@@ -1144,7 +1189,10 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
     const int ntiles = (ap->Nk + KT - 1) / KT;
     const int base = cdiv(ap->Nq, 128) * ap->B * ap->H;
     int qs = 1;   // key split of the dQ pass (atomics into a zeroed dQ)
-    while (base * qs < 1024 && ntiles / (2 * qs) >= 2) qs *= 2;
+    // one round at the kernel's 3 waves per SIMD (3 four-wave workgroups per CU: 768); the
+    // power-of-two split ran 1.5 rounds at the coop self-attention shape (r6f: bwd 377 -> 303 us
+    // with the dK / dV split below)
+    qs = max(1, min(ntiles / 2, 768 / base));
     AP p = make_ap(*ap, qs);
     hipStream_t s = (hipStream_t)stream;
     const int64_t rows = (int64_t)ap->B * ap->H * ap->Nq;
@@ -1213,7 +1261,8 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
         // query splits of the dK / dV pass until the grid covers ~2 workgroups per CU
         const int nqt = cdiv(ap->Nq, KT);
         int ks = 1;
-        while ((int64_t)gk.x * gk.y * ks * 2 <= 512 && nqt / (ks * 2) >= 2) ks *= 2;
+        // one round at the kernel's 2 waves per SIMD (2 four-wave workgroups per CU: 512)
+        ks = max(1, min(nqt / 2, (int)(512 / ((int64_t)gk.x * gk.y))));
         if (ks > 1) {
             const cmt_attn_train_args& a = *ap;
             for (int which = 0; which < 2; ++which) {
