@@ -384,24 +384,24 @@ class HeadTrainMixin:
     def _assign_all(self, preds, gts, cfg, code_w):
         """HungarianAssigner3D (hungarian_assigner_3d.py:68-156) for every
         (layer, task, sample): the [Nq, n_gt] cost matrices are built on the
-        device (cmt_match_cost), copied to the host in ONE transfer, solved by
-        scipy's linear_sum_assignment as the reference does, and the matched
-        (query, gt) index pairs go back in ONE transfer.  Returns
-        {(l, t, b): (rows, cols) device index tensors (None: no GT), n_pos}."""
+        device (cmt_match_cost, each sample's normalised GT built once for all
+        layers), copied to the host in ONE transfer and solved by scipy's
+        linear_sum_assignment as the reference does.  Returns {(l, t, b):
+        (rows, cols) host int64 arrays} (absent: no GT)."""
         L, B = preds[0]["center"].shape[:2]
-        dev = preds[0]["center"].device
         jobs, costs = [], []
+        gnorm = {key: (_normalize_bbox(g).contiguous(), gl.int().contiguous())
+                 for key, (g, gl) in gts.items() if g.shape[0] > 0}
         for t, d in enumerate(preds):
             pb_all = torch.cat([d[k].detach() for k in ("center", "height", "dim", "rot", "vel")], -1)  # [L, B, Nq, 10]
             pl_all = d["cls_logits"].detach()
             for l in range(L):
                 pb, pl = pb_all[l], pl_all[l]
                 for b in range(B):
-                    g_b, gl_b = gts[(t, b)]
-                    if g_b.shape[0] == 0:
+                    if (t, b) not in gnorm:
                         continue
-                    cost = T.match_cost(pl[b].contiguous(), pb[b].contiguous(),
-                                        _normalize_bbox(g_b).contiguous(), gl_b.int().contiguous(), code_w,
+                    gn, gli = gnorm[(t, b)]
+                    cost = T.match_cost(pl[b].contiguous(), pb[b].contiguous(), gn, gli, code_w,
                                         gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["match_cls_weight"],
                                         reg_weight=cfg["match_reg_weight"])
                     jobs.append(((l, t, b), cost.shape))
@@ -410,33 +410,49 @@ class HeadTrainMixin:
         if not jobs:
             return out
         host = torch.cat(costs).cpu().numpy()                     # the one device -> host copy
-        rows, cols, off = [], [], 0
+        off = 0
         for key, shape in jobs:
             n = shape[0] * shape[1]
             r, c = linear_sum_assignment(host[off:off + n].reshape(shape))
             off += n
-            rows.append(r)
-            cols.append(c)
-        lens = [len(r) for r in rows]
-        both = torch.from_numpy(np.stack([np.concatenate(rows), np.concatenate(cols)]).astype(np.int64)).to(dev)
-        start = 0
-        for (key, _), n in zip(jobs, lens):
-            out[key] = (both[0, start:start + n], both[1, start:start + n])
-            start += n
+            out[key] = (np.asarray(r, dtype=np.int64), np.asarray(c, dtype=np.int64))
         return out
 
-    def _targets(self, Nq, ncls, gtb, gtl, match, dev):
-        """_get_targets_single for one (sample, task) from its assignment."""
-        labels = torch.full((Nq,), ncls, dtype=torch.int32, device=dev)
-        tgt = torch.zeros((Nq, 9), dtype=torch.float32, device=dev)
-        bw = torch.zeros((Nq, 10), dtype=torch.float32, device=dev)
-        if match is None:
-            return labels, tgt, bw, 0, Nq
-        r, c = match
-        labels[r] = gtl[c].int()
-        tgt[r] = gtb[c].float()
-        bw[r] = 1.0
-        return labels, tgt, bw, int(r.numel()), Nq - int(r.numel())
+    def _targets_all(self, L, B, Nq, ncls, t, gts, matches, dev):
+        """_get_targets_single of every (layer, sample) of task t at once: labels [L B Nq] (ncls =
+        background), gravity-centre targets [L B Nq, 9], box weights [L B Nq, 10], and #pos per
+        layer -- three index writes from ONE host -> device copy of the matched (row, GT) pairs
+        (rows flattened over layers and samples), instead of three per (layer, sample)."""
+        R = L * B * Nq
+        labels = torch.full((R,), ncls, dtype=torch.int32, device=dev)
+        tgt = torch.zeros((R, 9), dtype=torch.float32, device=dev)
+        bw = torch.zeros((R, 10), dtype=torch.float32, device=dev)
+        npos = [0] * L
+        goff, gb_l, gl_l, g0 = {}, [], [], 0
+        for b in range(B):
+            g_b, gl_b = gts[(t, b)]
+            goff[b] = g0
+            gb_l.append(g_b)
+            gl_l.append(gl_b)
+            g0 += g_b.shape[0]
+        rows, cols = [], []
+        for l in range(L):
+            for b in range(B):
+                m = matches.get((l, t, b))
+                if m is None:
+                    continue
+                r, c = m
+                rows.append(r + (l * B + b) * Nq)
+                cols.append(c + goff[b])
+                npos[l] += len(r)
+        if rows:
+            idx = _to_dev_async(torch.from_numpy(np.stack([np.concatenate(rows), np.concatenate(cols)])), dev)
+            gb_t = gb_l[0] if B == 1 else torch.cat(gb_l)
+            gl_t = gl_l[0] if B == 1 else torch.cat(gl_l)
+            labels[idx[0]] = gl_t[idx[1]].int()
+            tgt[idx[0]] = gb_t[idx[1]].float()
+            bw[idx[0]] = 1.0
+        return labels, tgt, bw, npos
 
     def _box_terms(self, tgt, bw, code_w):
         """normalize the targets, drop non-finite rows (isnotnan), code weights."""
@@ -472,42 +488,49 @@ class HeadTrainMixin:
         num_tgt = max(num_tgt, 1.0)
         losses = {}
         # per task, once: the layers' box / logit views (one unbind each, so the backward writes every
-        # layer's gradient into one buffer instead of a zero-filled full copy per selected layer) and
-        # the layer-invariant DN terms
-        pbs, pls, dns = [], [], []
+        # layer's gradient into one buffer instead of a zero-filled full copy per selected layer), the
+        # layer-invariant DN terms and every layer's matching targets; then per layer ONE autograd
+        # node (ops.layer_loss: the matching and DN focal / L1 terms, nan_to_num, dn_weight)
+        tot = None
         for t, d in enumerate(preds):
-            pbs.append(torch.cat([d[k] for k in ("center", "height", "dim", "rot", "vel")], -1).unbind(0))
-            pls.append(d["cls_logits"].unbind(0))
+            ncls = self.num_classes[t]
+            Nq = d["cls_logits"].shape[2]
+            pbs = torch.cat([d[k] for k in ("center", "height", "dim", "rot", "vel")], -1).unbind(0)
+            pls = d["cls_logits"].unbind(0)
             md = d.get("dn_mask_dict")
-            dns.append(self._dn_prep(d, md, self.num_classes[t], code_w)
-                       if md is not None and md["pad_size"] > 0 else None)
+            dn = (self._dn_prep(d, md, ncls, code_w)
+                  if md is not None and md["pad_size"] > 0 else None)
+            labels, tgt, bw, npos = self._targets_all(L, B, Nq, ncls, t, gts, matches, dev)
+            nt, w = self._box_terms(tgt, bw, code_w)
+            lw = torch.ones(B * Nq, dtype=torch.float32, device=dev)
+            R = B * Nq
+            per_layer = []
+            for l in range(L):
+                nn_ = R - npos[l]
+                lcfg = dict(gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["cls_weight"],
+                            box_weight=cfg["box_weight"], cls_avg=max(npos[l] + 0.1 * nn_, 1.0) + eps,
+                            box_avg=float(npos[l]) + eps)
+                if dn is not None:
+                    # mmdet's loss weights times dn_weight; the box term only when the task has DN rows
+                    dcfg = dict(gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["cls_weight"] * self.dn_weight,
+                                box_weight=cfg["box_weight"] * self.dn_weight * (1.0 if dn["any_task"] else 0.0),
+                                cls_avg=dn["cls_avg"] + eps, box_avg=num_tgt + eps)
+                    v = ops.layer_loss(pls[l].reshape(-1, ncls), pbs[l].reshape(-1, 10), labels[l * R:(l + 1) * R],
+                                       lw, nt[l * R:(l + 1) * R], w[l * R:(l + 1) * R], lcfg,
+                                       dn["pls"][l], dn["pbs"][l], dn["kl"], dn["lw"], dn["ntg"], dn["w"], dcfg)
+                else:
+                    v = ops.layer_loss(pls[l].reshape(-1, ncls), pbs[l].reshape(-1, 10), labels[l * R:(l + 1) * R],
+                                       lw, nt[l * R:(l + 1) * R], w[l * R:(l + 1) * R], lcfg)
+                per_layer.append(v)
+            tot = per_layer if tot is None else [[a + b_ for a, b_ in zip(x, y)] for x, y in zip(tot, per_layer)]
         for l in range(L):
-            tot = {"loss_cls": 0.0, "loss_bbox": 0.0, "dn_loss_cls": 0.0, "dn_loss_bbox": 0.0}
-            for t, d in enumerate(preds):
-                ncls = self.num_classes[t]
-                pb, pl = pbs[t][l], pls[t][l]                                              # [B, Nq, 10 / ncls]
-                labs, tgts, bws, npos, nneg = [], [], [], 0, 0
-                for b in range(B):
-                    g_b, gl_b = gts[(t, b)]
-                    lab, tg, bw, p_, n_ = self._targets(pl.shape[1], ncls, g_b, gl_b, matches.get((l, t, b)), dev)
-                    labs.append(lab); tgts.append(tg); bws.append(bw)
-                    npos += p_; nneg += n_
-                nt, w = self._box_terms(torch.cat(tgts), torch.cat(bws), code_w)
-                lw = torch.ones(B * pl.shape[1], dtype=torch.float32, device=dev)
-                out = ops.det_loss(pl.reshape(-1, ncls), pb.reshape(-1, 10), torch.cat(labs), lw, nt, w,
-                                   gamma=cfg["gamma"], alpha=cfg["alpha"], cls_weight=cfg["cls_weight"],
-                                   box_weight=cfg["box_weight"], cls_avg=max(npos + 0.1 * nneg, 1.0) + eps,
-                                   box_avg=float(npos) + eps)
-                tot["loss_cls"] = tot["loss_cls"] + torch.nan_to_num(out[0])
-                tot["loss_bbox"] = tot["loss_bbox"] + torch.nan_to_num(out[1])
-                if dns[t] is not None:
-                    dout = self._dn_loss(dns[t], l, ncls, cfg, eps, num_tgt)
-                    tot["dn_loss_cls"] = tot["dn_loss_cls"] + dout[0]
-                    tot["dn_loss_bbox"] = tot["dn_loss_bbox"] + dout[1]
             key = "" if l == L - 1 else f"d{l}."
-            for k, v in tot.items():
-                if isinstance(v, torch.Tensor):
-                    losses[key + k] = v
+            v = tot[l]
+            losses[key + "loss_cls"] = v[0]
+            losses[key + "loss_bbox"] = v[1]
+            if len(v) > 2:
+                losses[key + "dn_loss_cls"] = v[2]
+                losses[key + "dn_loss_bbox"] = v[3]
         return losses
 
     def _dn_prep(self, d, md, ncls, code_w):
@@ -526,19 +549,4 @@ class HeadTrainMixin:
         ntg, w = self._box_terms(kb[rows].float(), torch.ones((rows.numel(), 10), device=pl.device), code_w)
         return dict(pls=pl.unbind(0), pbs=pb[:, rows].unbind(0), kl=kl.int(), ntg=ntg, w=w, any_task=any_task,
                     cls_avg=max(num_tgt * 3.14159 / 6 * self.split ** 3, 1),
-                    lw=torch.ones(pl.shape[1], dtype=torch.float32, device=pl.device),
-                    lab0=torch.full((0,), ncls, dtype=torch.int32, device=pl.device))
-
-    def _dn_loss(self, p, l, ncls, cfg, eps, nt):
-        """_dn_loss_single_task (cmt_head.py:760-806) of layer l from _dn_prep's terms; ``nt``: the
-        reduce_mean'd, clamped DN target count of the step (loss())."""
-        pl, pb, lw, ntg, w = p["pls"][l], p["pbs"][l], p["lw"], p["ntg"], p["w"]
-        # the classification term covers every DN row, the box term only the task's rows
-        out_c = ops.det_loss(pl, pb[:0], p["kl"], lw, ntg[:0], w[:0], gamma=cfg["gamma"], alpha=cfg["alpha"],
-                             cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=p["cls_avg"] + eps,
-                             box_avg=1.0)
-        out_b = ops.det_loss(pl[:0], pb, p["lab0"], lw[:0], ntg, w, gamma=cfg["gamma"], alpha=cfg["alpha"],
-                             cls_weight=cfg["cls_weight"], box_weight=cfg["box_weight"], cls_avg=1.0,
-                             box_avg=nt + eps)
-        lb = torch.nan_to_num(out_b[1]) * (1.0 if p["any_task"] else 0.0)
-        return self.dn_weight * torch.nan_to_num(out_c[0]), self.dn_weight * lb
+                    lw=torch.ones(pl.shape[1], dtype=torch.float32, device=pl.device))

@@ -26,7 +26,7 @@ from ... import native_train as T
 from ...runtime import SPLIT
 
 __all__ = ["linear", "linear_batched", "taps3", "attention", "layer_norm", "group_layer_norm", "bn_relu", "conv3x3", "nchw_rows", "det_loss",
-           "direct_param_grads", "kv_all", "cross_attention"]
+           "direct_param_grads", "kv_all", "cross_attention", "layer_loss"]
 
 
 # ---- parameter gradients written in place (ABI 24).  Inside direct_param_grads() the backward of
@@ -479,3 +479,42 @@ class _DetLoss(torch.autograd.Function):
 
 def det_loss(logits, boxes, labels, label_w, targets, box_w, **cfg):
     return _DetLoss.apply(logits, boxes, labels, label_w, targets, box_w, cfg)
+
+
+class _LayerLoss(torch.autograd.Function):
+    """The loss terms of one (decoder layer, task) in ONE autograd node (cmt_head.py:815-903):
+    the matching queries' FocalLoss + L1Loss (loss_single) and, with DN queries, the DN
+    classification term over every DN row and the box term over the task's rows
+    (dn_loss_single) -- one cmt_det_loss launch each, the DN one with dn_weight folded into the
+    loss weights -- each term through torch.nan_to_num as the reference applies it.  Returns the
+    [2] or [4] term vector; its backward scales the kernels' input gradients by the incoming
+    gradient where the raw term was finite (NanToNumBackward)."""
+
+    @staticmethod
+    def forward(ctx, pl, pb, dpl, dpb, labels, lw, nt, w, cfg, dn):
+        n = 4 if dpl is not None else 2
+        raw = torch.empty(n, dtype=torch.float32, device=pl.device)
+        _, dl, db = T.det_loss(pl.contiguous(), labels, lw, pb.contiguous(), nt, w, out=raw[0:2], **cfg)
+        grads = [dl, db]
+        if dpl is not None:
+            kl, dlw, ntg, dw, dcfg = dn
+            _, dlc, dbb = T.det_loss(dpl.contiguous(), kl, dlw, dpb.contiguous(), ntg, dw, out=raw[2:4], **dcfg)
+            grads += [dlc, dbb]
+        ctx.save_for_backward(raw, *grads)
+        ctx.n = n
+        return torch.nan_to_num(raw)
+
+    @staticmethod
+    def backward(ctx, dv):
+        raw, *grads = ctx.saved_tensors
+        g = dv * torch.isfinite(raw)
+        out = [grads[i] * g[i] for i in range(ctx.n)]
+        if ctx.n == 2:
+            out += [None, None]
+        return (*out, None, None, None, None, None, None)
+
+
+def layer_loss(pl, pb, labels, lw, nt, w, cfg, dpl=None, dpb=None, kl=None, dlw=None, ntg=None, dw=None, dcfg=None):
+    """-> tuple of the (layer, task)'s loss terms: (loss_cls, loss_bbox[, dn_loss_cls, dn_loss_bbox])."""
+    dn = (kl, dlw, ntg, dw, dcfg) if dpl is not None else None
+    return _LayerLoss.apply(pl, pb, dpl, dpb, labels, lw, nt, w, cfg, dn).unbind(0)

@@ -335,11 +335,14 @@ def conv3x3_wgrad(X, dY, nimg, H, W, Cin, ksplit):
 
 
 def det_loss(logits, labels, label_w, boxes, targets, box_w, *, gamma, alpha, cls_weight, box_weight, cls_avg,
-             box_avg, need_grad=True):
-    """(loss [2] device tensor, dlogits, dboxes) of FocalLoss + L1Loss."""
+             box_avg, need_grad=True, out=None):
+    """(loss [2] device tensor, dlogits, dboxes) of FocalLoss + L1Loss; out: a caller's [2] slot."""
     _f32(logits, boxes, targets, box_w, label_w)
     N._dev(labels)
-    out = torch.empty(2, dtype=torch.float32, device=logits.device)
+    if out is None:
+        out = torch.empty(2, dtype=torch.float32, device=logits.device)
+    elif out.dtype != torch.float32 or out.numel() != 2 or not out.is_contiguous():
+        raise RuntimeError("det_loss: out must be a contiguous fp32 [2] tensor")
     # the kernel writes every gradient element (rows x ncls, rows x 10): no fill for dense operands
     dl = (torch.empty_like if logits.is_contiguous() else torch.zeros_like)(logits) if need_grad else None
     db = (torch.empty_like if boxes.is_contiguous() else torch.zeros_like)(boxes) if need_grad else None
