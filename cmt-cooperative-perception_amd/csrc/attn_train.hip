@@ -1117,6 +1117,23 @@ void to16(const float* X, int64_t bs, int64_t hs, int64_t rs, int B, int H, int 
                                                                                         kmax);
 }
 
+// Zeroes the [N x 32] rows of every (b, h) of a strided head-split fp32 view (the accumulated
+// dQ / dK / dV of a split backward): one launch instead of a 2-D memset per (b, h)
+__global__ __launch_bounds__(256) void zero_heads_kernel(float* X, int64_t bs, int64_t hs, int64_t rs, int H, int N,
+                                                         int64_t total) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i >> 5;          // (b, h, n) row, D = 32 floats each
+        const int n = (int)(r % N);
+        const int64_t bh = r / N;
+        X[(bh / H) * bs + (bh % H) * hs + n * rs + (i & 31)] = 0.f;
+    }
+}
+
+void zero_heads(float* X, int64_t bs, int64_t hs, int64_t rs, int B, int H, int N, hipStream_t s) {
+    const int64_t total = (int64_t)B * H * N * D;
+    zero_heads_kernel<<<(unsigned)std::min<int64_t>(cdiv64(total, 256), 2048), 256, 0, s>>>(X, bs, hs, rs, H, N, total);
+}
+
 }  // namespace
 
 extern "C" int64_t cmt_attn_train_workspace_bytes(const cmt_attn_train_args* a) {
@@ -1205,10 +1222,12 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
         f16_t* k16 = (f16_t*)(base + w.k16);
         f16_t* v16 = (f16_t*)(base + w.v16);
         f16_t* d16 = (f16_t*)(base + w.d16);
-        to16(a.Q, a.q_bs, a.q_hs, a.q_rs, a.B, a.H, a.Nq, q16, nullptr, s);
         to16(a.dO, a.o_bs, a.o_hs, a.o_rs, a.B, a.H, a.Nq, d16, nullptr, s);
-        to16(a.K, a.k_bs, a.k_hs, a.k_rs, a.B, a.H, a.Nk, k16, nullptr, s);
-        to16(a.V, a.v_bs, a.v_hs, a.v_rs, a.B, a.H, a.Nk, v16, nullptr, s);
+        if (!a.ws_reuse) {   // ABI 25: else the forward's copies of Q / K / V are still in the workspace
+            to16(a.Q, a.q_bs, a.q_hs, a.q_rs, a.B, a.H, a.Nq, q16, nullptr, s);
+            to16(a.K, a.k_bs, a.k_hs, a.k_rs, a.B, a.H, a.Nk, k16, nullptr, s);
+            to16(a.V, a.v_bs, a.v_hs, a.v_rs, a.B, a.H, a.Nk, v16, nullptr, s);
+        }
         // dQ: key splits of 8-wave workgroups, about two per CU
         // (two 8-wave workgroups per CU: about 512 workgroups in one balanced round)
         const int nqb = cdiv(a.Nq, 256);
@@ -1217,12 +1236,10 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
         if (ds > 1) {
             const bool dense = a.q_hs == D && a.q_rs == (int64_t)a.H * D && a.q_bs == (int64_t)a.Nq * a.H * D;
             if (dense) {
-                hipMemsetAsync(a.dQ, 0, (size_t)a.B * a.Nq * a.H * D * sizeof(float), s);
+                CMT_REQUIRE(hipMemsetAsync(a.dQ, 0, (size_t)a.B * a.Nq * a.H * D * sizeof(float), s) == hipSuccess,
+                            "cmt_attn_train_bwd: dQ zeroing failed");
             } else {
-                for (int b = 0; b < a.B; ++b)
-                    for (int h = 0; h < a.H; ++h)
-                        hipMemset2DAsync(a.dQ + (int64_t)b * a.q_bs + (int64_t)h * a.q_hs, a.q_rs * sizeof(float), 0,
-                                         D * sizeof(float), a.Nq, s);
+                zero_heads(a.dQ, a.q_bs, a.q_hs, a.q_rs, a.B, a.H, a.Nq, s);
             }
         }
         const int nqp = cdiv(a.Nq, 64) * 64;
@@ -1235,10 +1252,7 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
     }
     if (qs > 1) {
         // dQ is accumulated: zero it (its [Nq x 32] rows per (b, h), strided)
-        for (int b = 0; b < ap->B; ++b)
-            for (int h = 0; h < ap->H; ++h)
-                hipMemset2DAsync(ap->dQ + (int64_t)b * ap->q_bs + (int64_t)h * ap->q_hs, ap->q_rs * sizeof(float), 0,
-                                 D * sizeof(float), ap->Nq, s);
+        zero_heads(ap->dQ, ap->q_bs, ap->q_hs, ap->q_rs, ap->B, ap->H, ap->Nq, s);
     }
     const dim3 gq(cdiv(ap->Nq, 128), ap->B * ap->H, qs), gk(cdiv(ap->Nk, 128), ap->B * ap->H);
     if (ap->fp16_inputs) {
@@ -1269,12 +1283,10 @@ extern "C" int cmt_attn_train_bwd(const cmt_attn_train_args* ap, void* stream) {
                 float* X = which ? a.dV : a.dK;
                 const int64_t bs = which ? a.v_bs : a.k_bs, hs = which ? a.v_hs : a.k_hs, rs = which ? a.v_rs : a.k_rs;
                 if (hs == D && rs == (int64_t)a.H * D && bs == (int64_t)a.Nk * a.H * D) {
-                    hipMemsetAsync(X, 0, (size_t)a.B * a.Nk * a.H * D * sizeof(float), s);
+                    CMT_REQUIRE(hipMemsetAsync(X, 0, (size_t)a.B * a.Nk * a.H * D * sizeof(float), s) == hipSuccess,
+                                "cmt_attn_train_bwd: dK / dV zeroing failed");
                 } else {
-                    for (int b = 0; b < a.B; ++b)
-                        for (int h = 0; h < a.H; ++h)
-                            hipMemset2DAsync(X + (int64_t)b * bs + (int64_t)h * hs, rs * sizeof(float), 0,
-                                             D * sizeof(float), a.Nk, s);
+                    zero_heads(X, bs, hs, rs, a.B, a.H, a.Nk, s);
                 }
             }
         }

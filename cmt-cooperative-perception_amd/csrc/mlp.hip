@@ -24,7 +24,10 @@
 // block (W1: K/16 x 2 KB, W2: 32 KB) are shared by the workgroup's 4 waves
 // through LDS: a two-slot ring per matrix filled by LDS-DMA one block ahead, one
 // barrier per block, and the MFMAs of fc2(hb) interleaved with those of
-// fc1(hb + 1) (independent accumulators).  One wave per SIMD: the 8 output
+// fc1(hb + 1) (independent accumulators).  Each wave issues its DMA pieces one
+// per MFMA step in the first half of a block, behind that step's MFMAs (issued
+// as a burst after the barrier they idled the matrix pipe: 95 -> 89 us for the
+// fused camera rows, profiles/r6_experiments.txt r6j).  One wave per SIMD: the 8 output
 // accumulator tiles (128 registers), the A fragments (96 at K = 192) and the
 // hidden tile need the whole 512-register file.
 #include "cmt_common.h"
@@ -104,7 +107,8 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
     const int gview = row / ghw, gpix = row - gview * ghw;      // GEO / RX: view and pixel of the row
     const int gimg = z * (a.M / ghw) + gview;
 #ifndef CMT_MLP_DIAG
-#define CMT_MLP_DIAG 0   // dev diagnostics (wrong results): 1 no C2 stores, 2 no NCHW loads, 4 no coordinates
+#define CMT_MLP_DIAG 0   // dev diagnostics (wrong results): 1 no C2 stores, 2 no NCHW loads, 4 no coordinates,
+                         // 8 no weight DMA after the prologue
 #endif
     if constexpr (GEO && (CMT_MLP_DIAG & 4)) {
 #pragma unroll
@@ -197,6 +201,21 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
     // two weight fragments (hi, lo) are read from LDS two steps ahead (a 3-slot register ring),
     // the order pinned by scheduling barriers -- left to itself the compiler read each pair right
     // before its MFMAs and waited for it (lgkmcnt(0)) 28 times per block.
+    // this wave's j-th LDS-DMA piece of block hb's successors: W2(hb + 1) pieces first (needed from
+    // the next block's first fc2 step), then W1(hb + 2)
+    constexpr int NW2 = 4 * NOT / MW, NW1 = (2 * KS + MW - 1) / MW;
+    auto dma_piece = [&](int hb, int j) {
+        if (j < NW2) {
+            if (hb + 1 >= nhb) return;
+            const int p = wave + MW * j;
+            mlp_glds16(w2g + (int64_t)(hb + 1) * W2_BLK + lane * 16 + p * FRAG_B,
+                       s2 + ((hb + 1) & 1) * W2_BLK + p * FRAG_B);
+        } else {
+            const int p = wave + MW * (j - NW2);
+            if (hb + 2 >= nhb || p >= 2 * KS) return;
+            mlp_glds16(w1g + (int64_t)(hb + 2) * W1_BLK + lane * 16 + p * FRAG_B, s1 + (hb & 1) * W1_BLK + p * FRAG_B);
+        }
+    };
     auto fc2_fc1 = [&](int hb, auto next_c) {
         constexpr bool next = decltype(next_c)::value;   // compile-time: a branch-free MFMA stream
         constexpr int NSTEP = next ? 2 * NOT + KS : 2 * NOT;
@@ -226,6 +245,10 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
             const int sl = t % (PD + 1);
             if (is_fc2(t)) oacc[i >> 1] = mma3(fh[sl], fl[sl], hh[i & 1], hl[i & 1], oacc[i >> 1]);
             else hacc = mma3(fh[sl], fl[sl], ah[i], al[i], hacc);
+            // one weight piece per step behind the step's MFMAs (NW2 + NW1 <= NSTEP for every KS):
+            // the wave issues its DMA while the matrix pipe is busy, half a block ahead of the wait
+            if constexpr (next && !(CMT_MLP_DIAG & 8))
+                if (t < NW2 + NW1) dma_piece(hb, t);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -239,13 +262,27 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
         // so the slots of W2(hb - 1) and W1(hb) take W2(hb + 1) and W1(hb + 2)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_mem();
-        issue_w2(hb + 1);
-        issue_w1(hb + 2);
         fc2_fc1(hb, std::true_type{});
         split_hidden(hb + 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_mem();
+    // RX: the row's 256 NCHW feature values are loaded here, into the registers fc1's A operand
+    // held, so their memory round trip runs under the last block's fc2 instead of the epilogue's
+    const float* const xrow = RX ? a.rx + (int64_t)gimg * NOUT * ghw + gpix : nullptr;
+    float xv[RX ? 4 : 1][2][4][4];
+    if constexpr (RX) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        xv[q][tt][g][e] = (CMT_MLP_DIAG & 2) ? 0.f
+                                                             : xrow[(int64_t)((2 * q + tt) * 32 + 8 * g + 4 * lh + e) * ghw];
+    }
     fc2_fc1(nhb - 1, std::false_type{});   // the last block: fc2 only
 
     if constexpr (RX) {
@@ -254,10 +291,10 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
         // global store is 16 contiguous bytes of a 128-byte row segment (8 lanes per row)
         __syncthreads();   // every wave is past its last weight-ring read: the rings become staging
         char* const stg = lds + wave * 16384;            // 4 slices [32 rows][64 cols] f16: C hi / lo, C2 hi / lo
-        const float* xrow = a.rx + (int64_t)gimg * NOUT * ghw + gpix;
         const int mw0 = blockIdx.x * MROWS + wave * 32;  // the wave's first row
         bool bad = false;
         typedef pair_t p4 __attribute__((ext_vector_type(4)));
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         auto sw = [](int r, int c16) { return r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4); };
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -272,7 +309,7 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         // the pair cmt_nchw_to_rows writes, and its value as the pair R row reads back
-                        const float x = (CMT_MLP_DIAG & 2) ? 0.f : xrow[(int64_t)(n + e) * ghw];
+                        const float x = xv[q][tt][g][e];
                         bad |= f16_unrepresentable(x);
                         h2[e] = (pair_t)x;
                         l2[e] = (pair_t)(x - (float)h2[e]);
@@ -292,7 +329,6 @@ __global__ __launch_bounds__(64 * MW, 1) void mlp2_x3_kernel(cmt_mlp2_args a) {
                 const int r = 8 * i + (lane >> 3), ch = lane & 7;
                 const int mr = mw0 + r;
                 const int off = sw(r, ch);
-                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
                 const u4 v0 = *(const u4*)(stg + off), v1 = *(const u4*)(stg + 4096 + off);
                 const u4 v2 = *(const u4*)(stg + 8192 + off), v3 = *(const u4*)(stg + 12288 + off);
                 if (mr < a.M && !(CMT_MLP_DIAG & 1)) {

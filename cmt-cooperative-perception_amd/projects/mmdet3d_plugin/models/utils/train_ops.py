@@ -149,7 +149,7 @@ class _Attention(torch.autograd.Function):
         kw = dict(B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * C, 32, C), k_strides=(Nk * C, 32, C),
                   v_strides=(Nk * C, 32, C), o_strides=(Nq * C, 32, C), scale=scale, dn_pad=dn_pad,
                   dn_group=dn_group, fp16_inputs=fp16, dropout_p=dropout_p, seed=seed, seed_dev=seed_dev)
-        T.attn_train_fwd(q, k, v, o, lse, **kw)
+        ctx.ws = T.attn_train_fwd(q, k, v, o, lse, **kw)
         ctx.kw = kw
         ctx.save_for_backward(q, k, v, o, lse)
         return o
@@ -158,7 +158,8 @@ class _Attention(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        T.attn_train_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, **ctx.kw)
+        T.attn_train_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, ws=ctx.ws, **ctx.kw)
+        ctx.ws = None
         return dq, dk, dv, None, None, None, None, None, None, None, None
 
 
@@ -252,7 +253,8 @@ class _CrossAttn(torch.autograd.Function):
         kw = dict(B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * C, 32, C), k_strides=(K.stride(0), 32, ld),
                   v_strides=(V.stride(0), 32, V.stride(1)), o_strides=(Nq * C, 32, C), scale=scale, dn_pad=0,
                   dn_group=0, fp16_inputs=fp16, dropout_p=0.0, seed=0, seed_dev=None)
-        T.attn_train_fwd(q, K, V, o, lse, **kw)
+        # the workspace holds the f16 copies of q / K / V the backward reuses (ABI 25)
+        ctx.ws = T.attn_train_fwd(q, K, V, o, lse, **kw)
         ctx.kw, ctx.holder, ctx.l = kw, holder, l
         ctx.save_for_backward(q, o, lse)
         return o
@@ -267,7 +269,8 @@ class _CrossAttn(torch.autograd.Function):
         K, V = h.K[..., l * C:(l + 1) * C], h.V[..., l * C:(l + 1) * C]
         dK, dV = h.dK[..., l * C:(l + 1) * C], h.dV[..., l * C:(l + 1) * C]
         dq = torch.empty_like(q)
-        T.attn_train_bwd(q, K, V, o, lse, do.contiguous(), dq, dK, dV, **ctx.kw)
+        T.attn_train_bwd(q, K, V, o, lse, do.contiguous(), dq, dK, dV, ws=ctx.ws, **ctx.kw)
+        ctx.ws = None
         h.written.add(l)
         z = _ZERO_TOKEN.get(q.device)
         if z is None:

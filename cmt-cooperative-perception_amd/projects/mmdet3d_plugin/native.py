@@ -30,7 +30,7 @@ A2_ADD, A2_SELECT = 0, 1
 ATTN_KEEP_PARTIALS = 2048   # cmt_hip.h CMT_ATTN_KEEP_PARTIALS (ABI 19)
 LINEAR_BWD_ACCUMULATE = 1   # cmt_hip.h CMT_LINEAR_BWD_ACCUMULATE (ABI 24)
 CHAIN_XSPLITS = 8           # the split count chain B1 combines (cmt_chain_args.xsplits)
-ABI_VERSION = 24
+ABI_VERSION = 25
 PLANE_MAX_ROWS = 64   # key rows per plane_max2 / kmax2 entry (cmt_hip.h)
 
 _vp = ctypes.c_void_p
@@ -102,7 +102,7 @@ class AttnTrainArgs(ctypes.Structure):
                 ("LSE", _vp), ("dO", _vp), ("dQ", _vp), ("dK", _vp), ("dV", _vp), ("delta", _vp),
                 ("scale", _flt), ("dn_pad", _int), ("dn_group", _int), ("fp16_inputs", _int),
                 ("dropout_p", _flt), ("seed", ctypes.c_uint32), ("kv_splits", _int),
-                ("workspace", _vp), ("workspace_bytes", _i64), ("seed_dev", _vp)]
+                ("workspace", _vp), ("workspace_bytes", _i64), ("seed_dev", _vp), ("ws_reuse", _int)]
 
 
 class LnTrainArgs(ctypes.Structure):

@@ -206,6 +206,8 @@ def _attn_args(Q, K, V, O, LSE, *, B, H, Nq, Nk, q_strides, k_strides, v_strides
 
 
 def attn_train_fwd(Q, K, V, O, LSE, **kw):
+    """Returns the workspace (or None): handed to attn_train_bwd(ws=...) for the same Q / K / V,
+    the backward reuses the forward's f16 copies of them (ABI 25 ws_reuse)."""
     _f32(Q, K, V, O, LSE)
     a = _attn_args(Q, K, V, O, LSE, **kw)
     need = N.lib().cmt_attn_train_workspace_bytes(ctypes.byref(a))
@@ -214,18 +216,22 @@ def attn_train_fwd(Q, K, V, O, LSE, **kw):
         ws = torch.empty(need, dtype=torch.uint8, device=O.device)
         a.workspace, a.workspace_bytes = ws.data_ptr(), need
     N._check(N.lib().cmt_attn_train_fwd(ctypes.byref(a), N._stream()), "cmt_attn_train_fwd")
+    return ws
 
 
-def attn_train_bwd(Q, K, V, O, LSE, dO, dQ, dK, dV, **kw):
+def attn_train_bwd(Q, K, V, O, LSE, dO, dQ, dK, dV, ws=None, **kw):
+    """ws: the workspace attn_train_fwd returned for these Q / K / V (unchanged since), or None"""
     _f32(Q, K, V, O, LSE, dO, dQ, dK, dV)
     a = _attn_args(Q, K, V, O, LSE, **kw)
     delta = torch.empty(kw["B"] * kw["H"] * kw["Nq"], dtype=torch.float32, device=O.device)
     a.dO, a.dQ, a.dK, a.dV, a.delta = dO.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dV.data_ptr(), delta.data_ptr()
     # the long-key fp16 path takes f16 copies of Q, dO, K, V in the workspace (cmt_hip.h)
     need = N.lib().cmt_attn_train_workspace_bytes(ctypes.byref(a))
-    ws = None
     if need > 0:
-        ws = torch.empty(need, dtype=torch.uint8, device=O.device)
+        if ws is not None and ws.numel() >= need:
+            a.ws_reuse = 1
+        else:
+            ws = torch.empty(need, dtype=torch.uint8, device=O.device)
         a.workspace, a.workspace_bytes = ws.data_ptr(), need
     N._check(N.lib().cmt_attn_train_bwd(ctypes.byref(a), N._stream()), "cmt_attn_train_bwd")
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CMT_ABI_VERSION 24
+#define CMT_ABI_VERSION 25
 
 /* CMT_F16P (ABI 12), "f16 pair": an fp32 operand split into two f16 halves,
  * x = hi + lo with hi = f16(x), lo = f16(x - hi).  Representation error:
@@ -596,6 +596,9 @@ typedef struct cmt_attn_train_args {
     void* workspace; int64_t workspace_bytes;
     const uint32_t* seed_dev;  /* ABI 22, optional: the dropout seed is seed + *seed_dev, read on the
                                 * device (a graph-replayed step draws a fresh seed without re-capture) */
+    int ws_reuse;              /* ABI 25, backward of the long-key path: nonzero = the workspace is the one
+                                * the forward ran with on the same Q / K / V, so its f16 copies of them are
+                                * reused and only dO is converted */
 } cmt_attn_train_args;
 /* Long-key fp16 path (ABI 15; fp16_inputs, no DN mask, no dropout, Nk >= 4096,
  * 128 < Nq <= 1152, heads contiguous in O (o_hs == 32), kv_splits 0 -- the

@@ -207,6 +207,40 @@ def test_attention_train_fwd_bwd(dev, B, Nq, Nk, pad, grp, fp16, p):
         assert err < (5e-3 if fp16 else 2e-5), (name, err)
 
 
+def test_attention_train_bwd_reuses_forward_copies(dev):
+    """ABI 25 ws_reuse: the long-key backward handed the forward's workspace reuses its f16 copies
+    of Q / K / V (only dO is converted) and returns the same gradients as a backward that converts
+    all four into a fresh workspace (dK / dV bit for bit, dQ up to the order of its split sums) --
+    on strided K / V views (the all-layer K / V arena of the training step), two batch elements."""
+    T = _T()
+    B, Nq, Nk, H, C = 2, 900, 4500, 8, 256
+    g = torch.Generator().manual_seed(5)
+    q = torch.randn(B, Nq, C, generator=g).to(dev)
+    kv = torch.randn(B, Nk, 3 * C, generator=g).to(dev)     # layer 1 of a 3-layer arena
+    k, v = kv[..., C:2 * C], (kv * 0.5)[..., 2 * C:]
+    do = torch.randn(B, Nq, C, generator=g).to(dev)
+    o = torch.empty_like(q)
+    lse = torch.empty(B * H * Nq, dtype=torch.float32, device=dev)
+    kw = dict(B=B, H=H, Nq=Nq, Nk=Nk, q_strides=(Nq * C, 32, C), k_strides=(k.stride(0), 32, k.stride(1)),
+              v_strides=(v.stride(0), 32, v.stride(1)), o_strides=(Nq * C, 32, C), scale=1 / math.sqrt(32),
+              fp16_inputs=True)
+    ws = T.attn_train_fwd(q, k, v, o, lse, **kw)
+    assert ws is not None
+    outs = []
+    for reuse in (False, True):
+        # dK / dV take the strides of K / V: slices of arenas shaped like kv
+        dkv = torch.empty(2, B, Nk, 3 * C, device=dev)
+        dq, dk, dv = torch.empty_like(q), dkv[0][..., C:2 * C], dkv[1][..., 2 * C:]
+        T.attn_train_bwd(q, k, v, o, lse, do, dq, dk, dv, ws=ws if reuse else None, **kw)
+        outs.append((dq, dk, dv))
+    torch.cuda.synchronize()
+    (dq0, dk0, dv0), (dq1, dk1, dv1) = outs
+    assert torch.equal(dk0, dk1) and torch.equal(dv0, dv1)
+    # dQ sums its key splits with f32 atomics: equal up to their order
+    assert (dq0 - dq1).abs().max().item() <= 1e-5 * dq0.abs().max().item()
+    assert dq0.abs().max().item() > 0
+
+
 @pytest.mark.parametrize("rows,C,G,eps", [(333, 256, 1, 1e-5), (1100, 256, 1, 1e-5), (6 * 70, 64, 6, 1e-6)])
 def test_layernorm_train(dev, rows, C, G, eps):
     from projects.mmdet3d_plugin.models.utils import train_ops as O

@@ -93,7 +93,7 @@ def test_c_abi_exports_every_declared_symbol():
     assert len(syms) >= 15
     for s in syms:
         assert hasattr(L, s), s
-    assert L.cmt_abi_version() == native.ABI_VERSION == 24
+    assert L.cmt_abi_version() == native.ABI_VERSION == 25
 
 
 def test_c_abi_argument_errors_without_device():
