@@ -299,8 +299,14 @@ class HeadTrainMixin:
         pcr = self.pc_range
         c = (out["center"] + reference[None, :, :, :2]).sigmoid()
         z = (out["height"] + reference[None, :, :, 2:3]).sigmoid()
-        out["center"] = torch.cat([c[..., 0:1] * (pcr[3] - pcr[0]) + pcr[0], c[..., 1:2] * (pcr[4] - pcr[1]) + pcr[1]],
-                                  -1)
+        # x / y scaled by their pc_range spans in one op (per-column slices would each backward as a
+        # zero fill + copy)
+        sc = self.__dict__.get("_xy_affine")
+        if sc is None or sc[0].device != c.device:
+            sc = (torch.tensor([pcr[3] - pcr[0], pcr[4] - pcr[1]], dtype=torch.float32, device=c.device),
+                  torch.tensor([pcr[0], pcr[1]], dtype=torch.float32, device=c.device))
+            self.__dict__["_xy_affine"] = sc
+        out["center"] = torch.addcmul(sc[1], c, sc[0])
         out["height"] = z * (pcr[5] - pcr[2]) + pcr[2]
         return out
 
@@ -312,6 +318,7 @@ class HeadTrainMixin:
         cmt_head.py:515-545)."""
         B = len(img_metas)
         C = self.hidden_dim
+        self._stash_gt_labels(list(gt_labels))
         ref, mask_dict = self.prepare_for_dn_train(B, gt_boxes, gt_labels, rand_prob)
         rp = inverse_sigmoid(ref.clone()).sigmoid()
         qpos = self._mlp_t(_pos2embed(rp, C), self.bev_embedding)
@@ -345,14 +352,15 @@ class HeadTrainMixin:
                 names = self.class_names[t]
                 kl, kb = mask_dict["known_lbs_bboxes"]
                 raw = mask_dict["known_labels_raw"]
-                new_kl, new_raw = torch.full_like(kl, len(names)), torch.full_like(raw, len(names))
-                for ci in range(len(names)):
-                    new_kl[kl == ci + flag] = ci
-                    new_raw[raw == ci + flag] = ci
+                n = len(names)
+                # labels of this task's classes relative to it, the others n (no boolean-mask writes:
+                # each was a device -> host sync)
+                new_kl = torch.where((kl >= flag) & (kl < flag + n), kl - flag, torch.full_like(kl, n))
+                new_raw = torch.where((raw >= flag) & (raw < flag + n), raw - flag, torch.full_like(raw, n))
                 tmd = dict(mask_dict, known_lbs_bboxes=(new_kl, kb), known_labels_raw=new_raw)
                 for key in list(outs):
-                    outs["dn_" + key] = outs[key][:, :, :pad]
-                    outs[key] = outs[key][:, :, pad:]
+                    # split, not two slices: one cat in the backward instead of two zero-filled copies + add
+                    outs["dn_" + key], outs[key] = outs[key].split([pad, outs[key].shape[2] - pad], 2)
                 outs["dn_mask_dict"] = tmd
             flag += len(self.class_names[t])
             preds.append(outs)
@@ -370,24 +378,65 @@ class HeadTrainMixin:
                     match_cls_weight=float(asg.get("cls_cost", {}).get("weight", 2.0)),
                     match_reg_weight=float(asg.get("reg_cost", {}).get("weight", 0.25)), code_weights=cw)
 
-    def _gt_split(self, gtb, gtl):
+    def _stash_gt_labels(self, gt_labels):
+        """Starts the device -> host copy of the GT labels before this step's forward kernels are
+        queued (pinned, non-blocking, with an event): loss() selects each task's GT and the DN
+        rows on the host from it, without a stream sync behind the whole forward."""
+        self.__dict__["_gt_host"] = None
+        if not gt_labels or any(l.device.type == "cpu" for l in gt_labels):
+            return
+        key = tuple((l.data_ptr(), l.numel()) for l in gt_labels)
+        cat = torch.cat([l.reshape(-1).long() for l in gt_labels])
+        host = torch.empty(cat.shape, dtype=torch.long, pin_memory=True)
+        host.copy_(cat, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.__dict__["_gt_host"] = (key, [l.numel() for l in gt_labels], host, ev)
+
+    def _gt_labels_host(self, gt_labels):
+        """Per sample the GT labels as host int64 arrays: from forward_train's stashed copy when
+        these are the tensors it saw (waits only for that copy), else copied here (a sync)."""
+        self.__dict__["_gt_host_hit"] = False
+        if all(l.device.type == "cpu" for l in gt_labels):
+            return [l.reshape(-1).long().numpy() for l in gt_labels]
+        st = self.__dict__.get("_gt_host")
+        if st is not None and st[0] == tuple((l.data_ptr(), l.numel()) for l in gt_labels):
+            st[3].synchronize()
+            flat, counts = st[2].numpy(), st[1]
+            self.__dict__["_gt_host_hit"] = True
+        else:
+            flat = torch.cat([l.reshape(-1).long() for l in gt_labels]).cpu().numpy()
+            counts = [l.numel() for l in gt_labels]
+        return list(np.split(flat, np.cumsum(counts)[:-1]))
+
+    def _gt_split(self, gtb, gtl, lab_host):
         """{(task, sample): (boxes, labels relative to the task)}: the GT of each task's classes,
-        selected once per step (each boolean selection is a device -> host sync)."""
+        selected once per step by index lists built on the host (lab_host: _gt_labels_host) --
+        a boolean-mask selection on the device is a device -> host sync each."""
         out, flag = {}, 0
         for t, ncls in enumerate(self.num_classes):
             for b in range(len(gtl)):
-                m = (gtl[b] >= flag) & (gtl[b] < flag + ncls)
-                out[(t, b)] = (gtb[b][m], gtl[b][m] - flag)
+                lh = lab_host[b]
+                idx = np.nonzero((lh >= flag) & (lh < flag + ncls))[0]
+                if len(idx) == len(lh):
+                    out[(t, b)] = (gtb[b], gtl[b] - flag)
+                elif len(idx) == 0:
+                    out[(t, b)] = (gtb[b][:0], gtl[b][:0])
+                else:
+                    it = _to_dev_async(torch.from_numpy(idx), gtb[b].device)
+                    out[(t, b)] = (gtb[b].index_select(0, it), gtl[b].index_select(0, it) - flag)
             flag += ncls
         return out
 
-    def _assign_all(self, preds, gts, cfg, code_w):
+    def _assign_all(self, preds, gts, cfg, code_w, between=None):
         """HungarianAssigner3D (hungarian_assigner_3d.py:68-156) for every
         (layer, task, sample): the [Nq, n_gt] cost matrices are built on the
         device (cmt_match_cost, each sample's normalised GT built once for all
-        layers), copied to the host in ONE transfer and solved by scipy's
-        linear_sum_assignment as the reference does.  Returns {(l, t, b):
-        (rows, cols) host int64 arrays} (absent: no GT)."""
+        layers), copied to the host in ONE non-blocking transfer and solved by
+        scipy's linear_sum_assignment as the reference does; ``between()`` (host
+        work that does not need the matches) runs while that copy waits for the
+        forward's kernels.  Returns {(l, t, b): (rows, cols) host int64 arrays}
+        (absent: no GT)."""
         L, B = preds[0]["center"].shape[:2]
         jobs, costs = [], []
         gnorm = {key: (_normalize_bbox(g).contiguous(), gl.int().contiguous())
@@ -408,8 +457,22 @@ class HeadTrainMixin:
                     costs.append(cost.reshape(-1))
         out = {}
         if not jobs:
+            if between is not None:
+                between()
             return out
-        host = torch.cat(costs).cpu().numpy()                     # the one device -> host copy
+        cat = torch.cat(costs)                                    # the one device -> host copy
+        if cat.is_cuda:
+            host_t = torch.empty(cat.shape, dtype=cat.dtype, pin_memory=True)
+            host_t.copy_(cat, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host_t, ev = cat, None
+        if between is not None:
+            between()
+        if ev is not None:
+            ev.synchronize()
+        host = host_t.numpy()
         off = 0
         for key, shape in jobs:
             n = shape[0] * shape[1]
@@ -451,7 +514,7 @@ class HeadTrainMixin:
             gl_t = gl_l[0] if B == 1 else torch.cat(gl_l)
             labels[idx[0]] = gl_t[idx[1]].int()
             tgt[idx[0]] = gb_t[idx[1]].float()
-            bw[idx[0]] = 1.0
+            bw.index_fill_(0, idx[0], 1.0)   # (an index_put of a Python scalar copies it to the device: a sync)
         return labels, tgt, bw, npos
 
     def _box_terms(self, tgt, bw, code_w):
@@ -474,8 +537,24 @@ class HeadTrainMixin:
         gtl = [l.to(dev).long() for l in gt_labels_3d]
         L, B = preds[0]["center"].shape[:2]
         eps = float(torch.finfo(torch.float32).eps)   # mmdet weight_reduce_loss avg_factor + eps
-        gts = self._gt_split(gtb, gtl)
-        matches = self._assign_all(preds, gts, cfg, code_w)
+        lab_host = self._gt_labels_host(list(gt_labels_3d))
+        gts = self._gt_split(gtb, gtl, lab_host)
+        # the per-task work that does not need the matches is issued while the cost matrices' copy
+        # to the host waits for the forward's kernels (_assign_all's between)
+        pre = {}
+
+        def between():
+            flag = 0
+            for t, d in enumerate(preds):
+                ncls = self.num_classes[t]
+                pbs = torch.cat([d[k] for k in ("center", "height", "dim", "rot", "vel")], -1).unbind(0)
+                pls = d["cls_logits"].unbind(0)
+                md = d.get("dn_mask_dict")
+                dn = (self._dn_prep(d, md, ncls, code_w, self._dn_rows_host(md, lab_host, flag, ncls))
+                      if md is not None and md["pad_size"] > 0 else None)
+                pre[t] = (pbs, pls, dn)
+                flag += ncls
+        matches = self._assign_all(preds, gts, cfg, code_w, between=between)
         # reduce_mean of the DN target count (cmt_head_coop.py:686): the same for every layer and task, so
         # one all-reduce per step -- issued on EVERY rank, also when its frames carry no GT (a rank that
         # skipped it would pair the next collective, the gradient all-reduce, with this one)
@@ -495,11 +574,7 @@ class HeadTrainMixin:
         for t, d in enumerate(preds):
             ncls = self.num_classes[t]
             Nq = d["cls_logits"].shape[2]
-            pbs = torch.cat([d[k] for k in ("center", "height", "dim", "rot", "vel")], -1).unbind(0)
-            pls = d["cls_logits"].unbind(0)
-            md = d.get("dn_mask_dict")
-            dn = (self._dn_prep(d, md, ncls, code_w)
-                  if md is not None and md["pad_size"] > 0 else None)
+            pbs, pls, dn = pre[t]
             labels, tgt, bw, npos = self._targets_all(L, B, Nq, ncls, t, gts, matches, dev)
             nt, w = self._box_terms(tgt, bw, code_w)
             lw = torch.ones(B * Nq, dtype=torch.float32, device=dev)
@@ -533,9 +608,25 @@ class HeadTrainMixin:
                 losses[key + "dn_loss_bbox"] = v[3]
         return losses
 
-    def _dn_prep(self, d, md, ncls, code_w):
+    def _dn_rows_host(self, md, lab_host, flag, ncls):
+        """The DN rows of one task (known_labels_raw of its classes, cmt_head.py:790-792) from the
+        host labels: (any row of the task, the rows to keep -- all when none), or None when
+        forward_train's stashed labels are not the ones given to loss (then _dn_prep selects on the
+        device)."""
+        if md is None or not self.__dict__.get("_gt_host_hit", False):
+            return None
+        if sum(len(x) for x in lab_host) * md["groups"] != md["known_labels_raw"].numel():
+            return None
+        rep = np.tile(np.concatenate(lab_host), md["groups"])
+        tm = (rep >= flag) & (rep < flag + ncls)
+        anyt = bool(tm.any())
+        return anyt, (np.nonzero(tm)[0] if anyt else np.arange(len(rep)))
+
+    def _dn_prep(self, d, md, ncls, code_w, rows_host=None):
         """The layer-invariant part of _dn_loss_single_task (cmt_head.py:760-806): the known
-        queries' logits / boxes of every layer (one gather), targets, weights and averages."""
+        queries' logits / boxes of every layer (one gather), targets, weights and averages.
+        rows_host: _dn_rows_host's (any_task, rows) -- without it the rows are selected on the
+        device (two syncs)."""
         kl, kb = md["known_lbs_bboxes"]
         raw = md["known_labels_raw"]
         bid = md["batch_idx"][md["known_indice"]]
@@ -543,9 +634,13 @@ class HeadTrainMixin:
         pl = d["dn_cls_logits"][:, bid, mk]                                         # [L, nk, ncls]
         pb = torch.cat([d["dn_" + k] for k in ("center", "height", "dim", "rot", "vel")], -1)[:, bid, mk]
         num_tgt = md["known_indice"].numel()
-        task_mask = raw != ncls
-        any_task = bool(task_mask.any())
-        rows = (task_mask if any_task else torch.ones_like(task_mask)).nonzero().squeeze(1)
+        if rows_host is not None:
+            any_task = rows_host[0]
+            rows = _to_dev_async(torch.from_numpy(rows_host[1].astype(np.int64)), pl.device)
+        else:
+            task_mask = raw != ncls
+            any_task = bool(task_mask.any())
+            rows = (task_mask if any_task else torch.ones_like(task_mask)).nonzero().squeeze(1)
         ntg, w = self._box_terms(kb[rows].float(), torch.ones((rows.numel(), 10), device=pl.device), code_w)
         return dict(pls=pl.unbind(0), pbs=pb[:, rows].unbind(0), kl=kl.int(), ntg=ntg, w=w, any_task=any_task,
                     cls_avg=max(num_tgt * 3.14159 / 6 * self.split ** 3, 1),

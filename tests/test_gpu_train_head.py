@@ -390,6 +390,50 @@ def test_coop_fullsize_bf16x3_grads_vs_exact_f32(dev, parity_log):
     assert per_own[w_own] < 4 * max(per_pert[w_pert], 1e-4), (per_own[w_own], per_pert[w_pert])
 
 
+def test_training_forward_and_loss_issue_without_host_sync(dev):
+    """The coop step's forward and loss queue their kernels without an implicit device -> host
+    sync (torch.cuda sync debug mode 'error'): the GT split by task and the DN rows come from the
+    labels' host copy forward_train started (a pinned non-blocking copy + event), the Hungarian
+    cost matrices go to the host by a non-blocking copy the loss waits for explicitly, after
+    queuing the DN terms -- and the losses equal those of the synchronous selection."""
+    from projects.mmdet3d_plugin import synthetic as S
+    from projects.mmdet3d_plugin.models.dense_heads.cmt_head_coop import (get_infrastructure_image_metas,
+                                                                          get_vehicle_image_metas)
+    head, _, _ = S.build_synthetic_head("cmtcoop_fusion_tumtraf", seed=0, num_query=64, num_layers=2,
+                                        grid_size=[256, 256, 40], device=dev)
+    head.train()
+    head.train_dropout = False
+    mv = S.synthetic_metas(1, yaws=S.VEHICLE_YAWS, prefix="vehicle_", pad_shape=(256, 640, 3), seed=7)
+    mi = S.synthetic_metas(1, yaws=S.INFRA_YAWS, prefix="infrastructure_", pad_shape=(256, 640, 3), seed=8)
+    metas = [dict(mv[0], **mi[0])]
+    agents = [(S.synthetic_bev(1, 32, 32, seed=1, device=dev), S.synthetic_img(1, 16, 40, seed=2, device=dev),
+               get_vehicle_image_metas(metas)),
+              (S.synthetic_bev(1, 32, 32, seed=3, device=dev), S.synthetic_img(3, 16, 40, seed=4, device=dev),
+               get_infrastructure_image_metas(metas))]
+    gtb, gtl = S.synthetic_gt(1, list(head.pc_range), head.num_classes[0], n=8, seed=5, device=dev)
+    rp = torch.rand(64, 3, generator=torch.Generator().manual_seed(6)).to(dev) * 2 - 1
+    rp = rp[:min(head.scalar, 64 // 8) * 8]
+
+    def step(check):
+        preds = head.forward_train(agents, metas, gtb, gtl, rand_prob=rp)
+        if check:   # labels the forward did not see: the synchronous selection
+            return head.loss(gtb, [l.clone() for l in gtl], [[p] for p in preds])
+        return head.loss(gtb, gtl, [[p] for p in preds])
+    step(False)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        got = step(False)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    want = step(True)
+    assert head.__dict__.get("_gt_host_hit") is False
+    torch.cuda.synchronize()
+    assert set(got) == set(want)
+    for k in got:
+        assert torch.equal(got[k], want[k]), k
+
+
 def test_direct_param_grads_match(dev, parity_log):
     """ABI 24 / train_ops.direct_param_grads (the Trainer's world-1 backward): every Linear and
     LayerNorm weight / bias gradient added straight into the parameter's .grad (the packed
