@@ -426,6 +426,7 @@ def test_training_forward_and_loss_issue_without_host_sync(dev):
         got = step(False)
     finally:
         torch.cuda.set_sync_debug_mode("default")
+    assert head.__dict__.get("_gt_host_hit") is True
     want = step(True)
     assert head.__dict__.get("_gt_host_hit") is False
     torch.cuda.synchronize()
