@@ -1623,12 +1623,47 @@ bool use_kw(const cmt_attn_args& a) {
     return (a.Nk + KT - 1) / KT <= 64;
 }
 
+// CUs of the current device (the round size of a one-workgroup-per-CU grid), read once
+int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    return cus;
+}
+
 int choose_splits(const cmt_attn_args& a) {
     if (a.kv_splits > 0) return a.kv_splits;
     if (use_kw(a)) return 1;
     const int ntiles = (a.Nk + KT - 1) / KT;
     const int nw = a.dtype == CMT_F32 ? NW : (use_long(a) ? 8 : 4);
     const int base = cdiv(a.Nq, nw * QW) * a.B * a.H;
+    if (use_long(a)) {
+        // the long-key kernel (one 8-wave workgroup per CU): the launch takes ceil(workgroups / CUs)
+        // rounds, each about as long as one split's key tiles plus a fixed ~10-tile prologue and
+        // tail; the fewest splits of the cheapest count win (the split partials cost a combine).
+        // 900 queries over 56 400 / 32 400 keys: 8 splits (one round of 256); 1 500 queries over
+        // 48 400 keys (configs[4]): 5 splits, 120 vs 142 us for the former power of two 8 -- 384
+        // workgroups in 1.5 rounds (profiles/r6_experiments.txt r6v)
+        const int cus = device_cus();
+        int best = 1;
+        int64_t best_cost = INT64_MAX;
+        for (int s = 1; s <= 16; ++s) {
+            if (s > 1 && ntiles / s < 8) break;
+            const int64_t rounds = cdiv64((int64_t)base * s, cus);
+            const int64_t cost = rounds * (cdiv(ntiles, s) + 10);
+            if (cost < best_cost) {
+                best_cost = cost;
+                best = s;
+            }
+        }
+        return best;
+    }
     int s = 1;
     // aim for >= 2048 waves (two per SIMD) while keeping >= 8 tiles per split;
     // short key ranges split down to 2 tiles per split

@@ -1,6 +1,7 @@
 """Kernel-level numerics of libcmt_hip.so against plain PyTorch (CPU, fp64 /
 fp32) references of the same op, on seeded inputs including ragged edges.
 Every call goes through the C ABI (ctypes) -- no torch compute on the device."""
+import ctypes
 import math
 
 import numpy as np
@@ -744,3 +745,14 @@ def test_rv_pe_coords_vector_path_bitexact(N, dev, odt):
     N.rv_pe_coords(i2l, b, BV=BV, h=h, w=w, D=D, pad_h=128.0, pad_w=320.0, depth_max=pcr[3], pc_range=pcr)
     torch.cuda.synchronize()
     assert torch.equal(a.cpu(), b.cpu())
+
+
+@pytest.mark.parametrize("Nq,Nk,B,want", [(900, 56400, 1, 8), (900, 32400, 1, 8), (900, 44400, 1, 8),
+                                          (1500, 48400, 1, 5), (900, 56400, 2, 4)])
+def test_attention_split_choice(N, dev, Nq, Nk, B, want):
+    """cmt_attn_splits on the long-key f16 kernel: whole rounds of the chip's 256 CUs -- the frame
+    shapes keep 8 splits (chain B1 combines exactly 8, ABI 19), configs[4]'s 1 500 queries take 5
+    (240 workgroups in one round instead of 384 in 1.5: 120 vs 142 us, r6v)."""
+    a = N.AttnArgs()
+    a.B, a.H, a.Nq, a.Nk, a.dtype = B, 8, Nq, Nk, N.F16
+    assert int(N.lib().cmt_attn_splits(ctypes.byref(a))) == want
