@@ -1222,11 +1222,13 @@ __device__ __forceinline__ void vm_wait() {
 // 16 = the halo loads as inline asm, waited for by a counted vmcnt of our own: hipcc's own wait
 // for a VGPR-destination load beside the W ring's LDS-DMA is vmcnt(0) (cdna_hip_programming.md
 // 'Three .s-level traps' (b)), which drained the W ring at the end of every chunk;
-// 4 / 8 = diagnostics only (no halo loads / no W refills: wrong results, for timing those streams)
-template <int VAR>
+// 4 / 8 = diagnostics only (no halo loads / no W refills: wrong results, for timing those streams).
+// X3 = false (round 6): one MFMA pass in the compute dtype E (f16 / bf16: the 'fp16' / 'bf16' policies'
+// shared_conv, W [N][K] in E) on the same halo / W layouts -- the lo halves are neither stored nor read
+template <int VAR, typename E = pair_t, bool X3 = true>
 __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int tiles_m, int tiles_n) {
     typedef HaloConv T;
-    typedef pair8_t frag;
+    typedef typename mfma_traits<E>::frag frag;
     constexpr bool AH = (VAR & 16) != 0;
     constexpr int BM = T::BM, S = T::S, TM = T::TM, TN = T::TN, UPT = T::UPT;
     constexpr int HLOADS = UPT * 8;                           // halo loads per thread per chunk
@@ -1319,21 +1321,23 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
             if (!u_on[i]) continue;
-            pair8_t hi, lo;
+            frag hi;
+            pair8_t lo;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const float x = AH && !u_ok[i] ? 0.f : hv[i][e];
-                hi[e] = (pair_t)x;
-                lo[e] = (pair_t)(x - (float)hi[e]);
+                hi[e] = (E)x;
+                if constexpr (X3) lo[e] = (pair_t)(x - (float)hi[e]);
             }
-            *(pair8_t*)(hb + u_lds[i]) = hi;
-            *(pair8_t*)(hb + (u_lds[i] ^ (2 << 4))) = lo;     // (2 + o) ^ sw == (o ^ sw) ^ 2
+            *(frag*)(hb + u_lds[i]) = hi;
+            if constexpr (X3) *(pair8_t*)(hb + (u_lds[i] ^ (2 << 4))) = lo;   // (2 + o) ^ sw == (o ^ sw) ^ 2
         }
     };
 
     // W slot fill: LDS byte tid * 16 of the slot = row tid / 4, physical chunk tid % 4
     const int wrow = tid >> 2, wlc = (tid & 3) ^ ((wrow >> 2) & 3);
-    const pair_t* wsrc = Wb + (int64_t)(n0 + wrow) * a.ldw + (wlc >> 1) * a.K + (wlc & 1) * 8;
+    // (one pass: the lo chunks of a slot row take the hi channels again -- never read)
+    const pair_t* wsrc = Wb + (int64_t)(n0 + wrow) * a.ldw + (X3 ? (wlc >> 1) * a.K : 0) + (wlc & 1) * 8;
     const int nchunks = Cin / T::CK, G = nchunks * 3;
     auto issue_w = [&](int g) {   // step g = (chunk g / 3, kernel row g % 3): its three taps
         const int c = g / 3, dy = g - 3 * (g / 3);
@@ -1408,33 +1412,35 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
                     const int hr = arow[tm] + tsh;
                     const int base = hr * T::ROWB, sw = hsw(hr);
                     af[tm] = *(const frag*)(Hs + base + ((lh ^ sw) << 4));
-                    al[tm] = *(const frag*)(Hs + base + (((2 + lh) ^ sw) << 4));
+                    if constexpr (X3) al[tm] = *(const frag*)(Hs + base + (((2 + lh) ^ sw) << 4));
                     if ((dx == 0 && edl[tm]) || (dx == 2 && edr[tm])) {
                         af[tm] = frag{};
-                        al[tm] = frag{};
+                        if constexpr (X3) al[tm] = frag{};
                     }
                 }
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
                     bh[tn] = *(const frag*)(Ws + dx * T::WTAP + woff[tn]);
-                    bl[tn] = *(const frag*)(Ws + dx * T::WTAP + (woff[tn] ^ (2 << 4)));
+                    if constexpr (X3) bl[tn] = *(const frag*)(Ws + dx * T::WTAP + (woff[tn] ^ (2 << 4)));
                 }
                 if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(1);
+                if constexpr (X3) {
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                        for (int tn = 0; tn < TN; ++tn)
+                            acc[tm][tn] = mfma_traits<E>::mma(bh[tn], al[tm], acc[tm][tn]);
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                        for (int tn = 0; tn < TN; ++tn)
+                            acc[tm][tn] = mfma_traits<E>::mma(bl[tn], af[tm], acc[tm][tn]);
+                }
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int tn = 0; tn < TN; ++tn)
-                        acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], al[tm], acc[tm][tn]);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < TN; ++tn)
-                        acc[tm][tn] = mfma_traits<pair_t>::mma(bl[tn], af[tm], acc[tm][tn]);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < TN; ++tn)
-                        acc[tm][tn] = mfma_traits<pair_t>::mma(bh[tn], af[tm], acc[tm][tn]);
+                        acc[tm][tn] = mfma_traits<E>::mma(bh[tn], af[tm], acc[tm][tn]);
                 if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(0);
             }
         }
@@ -1451,7 +1457,9 @@ __global__ __launch_bounds__(512) void conv_halo_x3_kernel(cmt_gemm_args a, int 
 int launch_conv_halo(const cmt_gemm_args& a, hipStream_t s) {
     const int tm = cdiv(a.conv_h * a.conv_w, HaloConv::BM), tn = a.N / HaloConv::BN;
     const unsigned nwg = (unsigned)((int64_t)tm * tn * a.batch);
-    conv_halo_x3_kernel<CMT_CONV_VAR><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
+    if (a.w_dtype == CMT_F16P) conv_halo_x3_kernel<CMT_CONV_VAR><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
+    else if (a.w_dtype == CMT_F16) conv_halo_x3_kernel<0, f16_t, false><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
+    else conv_halo_x3_kernel<0, bf16_t, false><<<nwg, HaloConv::NTX, 0, s>>>(a, tm, tn);
     return cmt_check_launch("cmt_gemm");
 }
 
@@ -1683,11 +1691,13 @@ extern "C" int cmt_gemm(const cmt_gemm_args* ap, void* stream) {
     CMT_REQUIRE(a.N % 64 == 0, "cmt_gemm: N must be a multiple of 64");
     CMT_REQUIRE(a.A && a.W && a.C, "cmt_gemm: null A/W/C");
     if (a.a_mode == CMT_A_CONV3X3_NCHW) {
-        CMT_REQUIRE(a.a_dtype == CMT_F32 && a.w_dtype == CMT_F16P &&
-                        (a.c_dtype == CMT_F16P || a.c_dtype == CMT_F32) && a.c_mode == CMT_C_ROWS &&
-                        a.k_splits <= 1 && a.plane_max2 == nullptr,
-                    "cmt_gemm: the NCHW conv3x3 takes fp32 A, CMT_F16P W, fp32 / CMT_F16P row C, no "
-                    "split-K / plane_max2");
+        CMT_REQUIRE(a.a_dtype == CMT_F32 &&
+                        ((a.w_dtype == CMT_F16P && (a.c_dtype == CMT_F16P || a.c_dtype == CMT_F32)) ||
+                         ((a.w_dtype == CMT_F16 || a.w_dtype == CMT_BF16) &&
+                          (a.c_dtype == a.w_dtype || a.c_dtype == CMT_F32))) &&
+                        a.c_mode == CMT_C_ROWS && a.k_splits <= 1 && a.plane_max2 == nullptr,
+                    "cmt_gemm: the NCHW conv3x3 takes fp32 A and CMT_F16P W (fp32 / CMT_F16P row C) or f16 / "
+                    "bf16 W (one pass; fp32 or W-dtype row C), no split-K / plane_max2");
         CMT_REQUIRE(a.A2 == nullptr || (a.lda2 % 4 == 0 && ((uintptr_t)a.A2 & 15) == 0),
                     "cmt_gemm: NCHW conv3x3 second-output rows A2: fp32, lda2 % 4 == 0, 16-byte aligned");
         CMT_REQUIRE(a.conv_c % 16 == 0 && a.K == 9 * a.conv_c && a.conv_h > 0 && a.conv_w > 0 &&

@@ -96,8 +96,9 @@ class HeadEngineMixin:
 
     def _conv_halo_ok(self, x, pk, prec):
         _, Cin, _, W = x.shape
-        return (prec.gemm == SPLIT and OPTIONS.conv_halo and Cin % 16 == 0 and W <= 180
-                and pk["conv_w"].shape[0] % 128 == 0)
+        # 'ref': three f16 passes on split pixels / weights; f16 / bf16 policies: one pass (round 6)
+        return (prec.gemm in (SPLIT, torch.float16, torch.bfloat16) and OPTIONS.conv_halo and Cin % 16 == 0
+                and W <= 180 and pk["conv_w"].shape[0] % 128 == 0 and pk["conv_w"].dtype == prec.gemm)
 
     def _range_flag(self, dev):
         """The head's f16-operand range flag: an int32 device word the kernels that read the
@@ -139,7 +140,7 @@ class HeadEngineMixin:
                         ldw=9 * Cin, ldc=Cout, bias=pk["conv_b"], relu=True, a_mode=native.A_CONV3X3_NCHW,
                         conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W, c_bstride=Nk * Cout,
                         A2=P, lda2=Cout if P is not None else 0, c2=pos if P is not None else None,
-                        range_flag=self._range_flag(x.device))
+                        range_flag=self._range_flag(x.device) if prec.gemm != torch.bfloat16 else None)
             return
         assert P is None
         xin = op_empty(B * H * W, Cin, prec.gemm, x.device)

@@ -325,6 +325,43 @@ def test_gemm_split_conv3x3_nchw(N, dev, B, Cin, H, W, Cout, cdt):
     assert torch.isnan(o.view(B, Nk, Cout)[:, H * W:]).all() and torch.isnan(o2.view(B, Nk, Cout)[:, H * W:]).all()
 
 
+@pytest.mark.parametrize("B,Cin,H,W,Cout,dt,out", [(1, 512, 180, 180, 256, torch.float16, "lowp"),   # configs[4]
+                                                   (1, 512, 180, 180, 256, torch.bfloat16, "lowp"),
+                                                   (2, 48, 37, 41, 128, torch.float16, "f32"),
+                                                   (1, 32, 9, 180, 384, torch.bfloat16, "lowp"),
+                                                   (1, 32, 300, 1, 128, torch.float16, "lowp")])
+def test_gemm_conv3x3_nchw_one_pass(N, dev, B, Cin, H, W, Cout, dt, out):
+    """The 'fp16' / 'bf16' policies' shared_conv from the NCHW fp32 map (round 6): the same halo
+    kernel in ONE MFMA pass on f16 / bf16 pixels and weights (fp32 accumulate), W-dtype or fp32 row
+    C, the second output out + P -- against float64 conv2d of the same rounded operands."""
+    g = torch.Generator().manual_seed(11 + H + W)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    b = torch.randn(Cout, generator=g)
+    wl = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).to(dt).contiguous().to(dev)
+    Nk = H * W + 37
+    cdt = dt if out == "lowp" else torch.float32
+    o = torch.full((B * Nk, Cout), float("nan"), dtype=cdt, device=dev)
+    P = torch.randn(H * W, Cout, generator=g)
+    o2 = torch.full_like(o, float("nan"))
+    N.gemm(x.to(dev), wl, o, M=H * W, N=Cout, K=9 * Cin, lda=H * W, ldw=9 * Cin, ldc=Cout, bias=b.to(dev),
+           relu=True, a_mode=N.A_CONV3X3_NCHW, conv=(H, W, Cin), batch=B, a_bstride=Cin * H * W,
+           c_bstride=Nk * Cout, A2=P.to(dev), lda2=Cout, c2=o2)
+    xr, wr = x.to(dt).double(), w.to(dt).double()
+    ref = torch.relu(torch.nn.functional.conv2d(xr, wr, b.double(), padding=1)).flatten(2).permute(0, 2, 1)
+    got = o.cpu().double().view(B, Nk, Cout)[:, :H * W]
+    eps = 2 ** -8 if dt == torch.bfloat16 else 2 ** -11
+    scale = ref.abs().max().item()
+    # fp32 accumulation order (~K 2^-24 relative) plus the output's rounding to the W dtype
+    tol = (eps if out == "lowp" else 0) * scale + 9 * Cin * 2 ** -22 * scale
+    err = (got - ref).abs().max().item()
+    assert err <= tol, (err, tol)
+    ref2 = ref + P.double()
+    err2 = (o2.cpu().double().view(B, Nk, Cout)[:, :H * W] - ref2).abs().max().item()
+    assert err2 <= tol + (eps if out == "lowp" else 0) * ref2.abs().max().item(), err2
+    assert torch.isnan(o.cpu().float().view(B, Nk, Cout)[:, H * W:]).all()
+
+
 def test_gemm_split_conv3x3_nchw_rejects(N, dev):
     x = torch.zeros(1, 16, 4, 181, device=dev)
     wp = torch.zeros(128, 2, 144, dtype=SPLIT, device=dev)
