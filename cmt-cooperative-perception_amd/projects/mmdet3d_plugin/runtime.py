@@ -121,7 +121,8 @@ class Options:
     side_stream: bool      # CMT_SIDE_STREAM=0: everything on the caller's stream
     chain: bool            # CMT_CHAIN=0: f16/bf16 decoder as separate GEMM / LayerNorm launches
     bev_pos_cache: bool    # CMT_BEV_POS_CACHE=0: rebuild the BEV position-MLP hidden rows per call
-    conv_halo: bool        # CMT_CONV_HALO=0: split shared_conv via NCHW->pair rows + per-tap gathered GEMM
+    conv_halo: bool        # CMT_CONV_HALO=0: shared_conv via an NCHW->rows pass + per-tap gathered GEMM instead
+                           # of the halo kernel reading the NCHW map (3 split passes at 'ref', 1 at f16 / bf16)
     mlp_fused: bool        # CMT_MLP_FUSED=0: split rv_embedding as two GEMMs (hidden pair rows via HBM)
     chain_combine: bool    # CMT_CHAIN_COMBINE=0: split cross-attention combined by its own launch (pair rows
                            # via HBM) instead of inside chain B1
