@@ -102,10 +102,11 @@ int64_t cmt_adamw_args_size(void);
  * ------------------------------------------------------------------------ */
 /* CMT_A_CONV3X3_NCHW (ABI 14): the 3x3 / pad 1 conv straight from an fp32 NCHW map
  * A[b * a_bstride + c * (conv_h * conv_w) + pixel] (lda unused), K = 9 * conv_c tap-major
- * as CONV3X3, M = conv_h * conv_w per batch element; split (CMT_F16P) W only (the
+ * as CONV3X3, M = conv_h * conv_w per batch element; split (CMT_F16P) W (the
  * reference-numerics shared_conv: each input pixel is split into f16 hi / lo once per
- * workgroup and serves all nine taps from LDS); conv_c % 16 == 0, conv_w <= 180,
- * N % 128 == 0, fp32 or CMT_F16P row C.  Optional second output: with A2 (fp32 rows
+ * workgroup and serves all nine taps from LDS; fp32 or CMT_F16P row C) or, since round 6,
+ * f16 / bf16 W (one MFMA pass on pixels rounded to W's dtype; fp32 or W-dtype row C);
+ * conv_c % 16 == 0, conv_w <= 180, N % 128 == 0.  Optional second output: with A2 (fp32 rows
  * A2[m * lda2 + n], the same for every batch element -- the weight-only BEV position
  * rows) it also writes out + A2 at C + c_split_stride (same layout as C): lowp(memory +
  * pos), the K-projection operand, without a separate GEMM. */
